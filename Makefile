@@ -1,0 +1,68 @@
+# Build for the MI355X-native object-storage benchmark.
+#   make            -> python extension + native tools, all in-tree
+# GPU code targets gfx950 only (CDNA4).
+PY        ?= python3
+HIPCC     ?= /opt/rocm/bin/hipcc
+CXX       ?= g++
+ARCH      ?= gfx950
+PKG       := custom_go_client_benchmark_amd
+BUILD     := build
+EXT_SUFFIX := $(shell $(PY) -c "import sysconfig;print(sysconfig.get_config_var('EXT_SUFFIX'))")
+PYBIND_INC := $(shell $(PY) -m pybind11 --includes)
+
+CXXSTD   := -std=c++17
+OPT      ?= -O3 -g1
+HOSTARCH := -march=x86-64-v2 -mtune=generic
+WARN     := -Wall -Wextra -Wno-unused-parameter -Wno-missing-field-initializers
+CPPFLAGS := -Icsrc -D__HIP_PLATFORM_AMD__ -isystem /opt/rocm/include
+CXXFLAGS := $(CXXSTD) $(OPT) $(HOSTARCH) $(WARN) -fPIC -pthread $(EXTRA_CXXFLAGS)
+HIPFLAGS := $(CXXSTD) $(OPT) --offload-arch=$(ARCH) -fPIC -pthread -Icsrc -munsafe-fp-atomics $(EXTRA_HIPFLAGS)
+LDLIBS   := -lssl -lcrypto -lpthread
+
+CORE_SRCS := csrc/core/crc32c.cc csrc/core/content.cc csrc/core/util.cc csrc/core/json.cc \
+             csrc/net/socket.cc csrc/net/buffered.cc \
+             csrc/http1/http1.cc \
+             csrc/storage/sink.cc csrc/storage/auth.cc csrc/storage/client.cc csrc/storage/http_client.cc \
+             csrc/storage/grpc_client.cc \
+             csrc/server/store.cc csrc/server/fakegcs.cc csrc/server/server_http1.cc csrc/server/server_grpc.cc \
+             csrc/gpu/crc_host.cc
+GPU_SRCS  := csrc/gpu/crc32c_kernels.hip csrc/gpu/engine.hip
+PY_SRCS   := csrc/py/bindings.cc csrc/bench/runner.cc
+
+CORE_OBJS := $(patsubst csrc/%.cc,$(BUILD)/%.o,$(CORE_SRCS))
+GPU_OBJS  := $(patsubst csrc/%.hip,$(BUILD)/%.o,$(GPU_SRCS))
+PY_OBJS   := $(patsubst csrc/%.cc,$(BUILD)/%.o,$(PY_SRCS))
+
+EXT := $(PKG)/_native$(EXT_SUFFIX)
+TOOLS := fakegcs read_operation ssd_test write_operations list_operation open_file small_poc
+TOOL_BINS := $(addprefix $(PKG)/bin/,$(TOOLS))
+
+.PHONY: all clean ext tools
+all: ext tools
+ext: $(EXT)
+tools: $(TOOL_BINS)
+
+$(BUILD)/%.o: csrc/%.cc
+	@mkdir -p $(dir $@)
+	$(CXX) $(CPPFLAGS) $(CXXFLAGS) $(PYBIND_INC) -MMD -MP -c $< -o $@
+
+$(BUILD)/%.o: csrc/%.hip
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -MMD -MP -c $< -o $@
+
+$(BUILD)/libgcsbcore.a: $(CORE_OBJS)
+	@rm -f $@
+	ar rcs $@ $^
+
+$(EXT): $(PY_OBJS) $(GPU_OBJS) $(BUILD)/libgcsbcore.a
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(PY_OBJS) $(GPU_OBJS) $(BUILD)/libgcsbcore.a \
+	  -L/opt/rocm/lib -lamdhip64 $(LDLIBS) -Wl,-rpath,/opt/rocm/lib
+
+$(PKG)/bin/%: csrc/tools/%.cc $(BUILD)/libgcsbcore.a
+	@mkdir -p $(PKG)/bin
+	$(CXX) $(CPPFLAGS) $(CXXFLAGS) -o $@ $< $(BUILD)/libgcsbcore.a $(LDLIBS)
+
+clean:
+	rm -rf $(BUILD) $(EXT) $(TOOL_BINS)
+
+-include $(CORE_OBJS:.o=.d) $(GPU_OBJS:.o=.d) $(PY_OBJS:.o=.d)

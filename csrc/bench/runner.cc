@@ -1,0 +1,216 @@
+#include "bench/runner.h"
+
+#include <unistd.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <random>
+
+#include "core/util.h"
+
+namespace gcsb {
+
+const double kOcLatencyBoundsMs[34] = {1,   2,   3,   4,   5,   6,    8,    10,   13,    16,    20,    25,
+                                       30,  40,  50,  65,  80,  100,  130,  160,  200,   250,   300,   400,
+                                       500, 650, 800, 1000, 2000, 5000, 10000, 20000, 50000, 100000};
+
+int oc_bucket_index(double v) {
+  // OpenCensus: bucket i holds bounds[i-1] <= v < bounds[i]
+  int i = 0;
+  while (i < 34 && v >= kOcLatencyBoundsMs[i]) ++i;
+  return i;
+}
+
+double percentile_floor(const std::vector<double>& sorted, int pct) {
+  if (sorted.empty()) return 0;
+  size_t idx = sorted.size() * static_cast<size_t>(pct) / 100;
+  if (idx >= sorted.size()) idx = sorted.size() - 1;
+  return sorted[idx];
+}
+
+Runner::Runner(RunnerConfig cfg) : cfg_(std::move(cfg)) {
+  if (cfg_.workers <= 0) throw StorageError("worker count not valid", false);
+  client_ = make_client(cfg_.client);
+}
+
+Runner::~Runner() {
+  stop();
+  wait();
+}
+
+std::string Runner::object_for(int worker, int64_t seq) const {
+  if (!cfg_.object_names.empty()) {
+    size_t n = cfg_.object_names.size();
+    size_t idx = (static_cast<size_t>(worker) + static_cast<size_t>(seq) * static_cast<size_t>(cfg_.workers)) % n;
+    return cfg_.object_names[idx];
+  }
+  return cfg_.object_prefix + std::to_string(cfg_.worker_id_offset + worker) + cfg_.object_suffix;
+}
+
+void Runner::start() {
+  stop_flag_ = false;
+  running_ = true;
+  gpu_stats_.assign(cfg_.workers, GpuSinkStats{});
+  for (int w = 0; w < cfg_.workers; ++w) threads_.emplace_back([this, w] { worker_main(w); });
+}
+
+void Runner::wait() {
+  for (auto& t : threads_)
+    if (t.joinable()) t.join();
+  threads_.clear();
+  running_ = false;
+}
+
+void Runner::stop() { stop_flag_ = true; }
+
+void Runner::record(ReadRecord&& r, double ms, double host_ms) {
+  std::lock_guard<std::mutex> lk(mu_);
+  ++acc_.reads;
+  if (!r.ok) {
+    ++acc_.errors;
+    if (acc_.first_error.empty()) acc_.first_error = "while reading object " + r.object + ": " + r.error;
+  } else {
+    acc_.bytes += r.bytes;
+    if (r.verified) ++acc_.verified;
+    lat_ms_.push_back(ms);
+    host_ms_.push_back(host_ms);
+    // metric semantics: integer-truncated milliseconds (reference main.go:146)
+    acc_.oc_buckets[oc_bucket_index(std::floor(ms))]++;
+  }
+  acc_.retries += r.attempts > 1 ? static_cast<uint64_t>(r.attempts - 1) : 0;
+  if (!t_first_ || r.start_ns < t_first_) t_first_ = r.start_ns;
+  if (r.end_ns > t_last_) t_last_ = r.end_ns;
+  if (cfg_.keep_records) pending_.push_back(std::move(r));
+}
+
+void Runner::worker_main(int w) {
+  std::unique_ptr<Sink> sink;
+  GpuSink* gsink = nullptr;
+  try {
+    if (cfg_.sink == "gpu") {
+      auto g = std::make_unique<GpuSink>(cfg_.gpu);
+      gsink = g.get();
+      sink = std::move(g);
+    } else {
+      sink = std::make_unique<DiscardSink>(cfg_.client.read_chunk, cfg_.host_crc);
+    }
+  } catch (const std::exception& e) {
+    ReadRecord r;
+    r.worker = w;
+    r.object = object_for(w, 0);
+    r.error = std::string("sink setup: ") + e.what();
+    r.start_ns = r.end_ns = now_ns();
+    record(std::move(r), 0, 0);
+    if (cfg_.stop_on_error) stop_flag_ = true;
+    return;
+  }
+  std::mt19937_64 rng(cfg_.seed ? cfg_.seed + static_cast<uint64_t>(w) : std::random_device{}());
+  const uint64_t sample_bound = cfg_.trace_sample_rate >= 1.0
+                                    ? ~0ull
+                                    : static_cast<uint64_t>(cfg_.trace_sample_rate * 9223372036854775808.0);
+  const int64_t t_begin = now_ns();
+  for (int64_t i = 0; i < cfg_.reads_per_worker; ++i) {
+    if (stop_flag_) break;
+    if (cfg_.duration_s > 0 && (now_ns() - t_begin) / 1e9 >= cfg_.duration_s) break;
+    ReadRecord r;
+    r.worker = cfg_.worker_id_offset + w;
+    r.seq = i;
+    r.object = object_for(w, i);
+    if (cfg_.trace_sample_rate > 0) {
+      r.trace_hi = rng();
+      r.trace_lo = rng();
+      r.span_id = rng() | 1;
+      // OTel TraceIDRatioBased: lower 8 bytes of the trace id >> 1 < rate * 2^63
+      r.sampled = cfg_.trace_sample_rate >= 1.0 || (r.trace_lo >> 1) < sample_bound;
+    }
+    r.start_wall_ns = wall_ns();
+    r.start_ns = now_ns();
+    double ms = 0, host_ms = 0;
+    try {
+      ReadResult rr = client_->read_object(cfg_.bucket, r.object, *sink, cfg_.range_offset, cfg_.range_limit,
+                                           &stop_flag_);
+      r.end_ns = now_ns();
+      r.ttfb_ns = rr.first_byte_ns;
+      r.host_done_ns = rr.host_done_ns;
+      r.bytes = rr.bytes;
+      r.attempts = rr.attempts;
+      r.verified = rr.sink.verified;
+      r.ok = !rr.sink.crc_mismatch;
+      if (!r.ok) r.error = "while reading and discarding content: " + rr.sink.detail;
+      if (r.ok && rr.info.size >= 0 && cfg_.range_limit < 0 && cfg_.range_offset == 0 &&
+          rr.bytes != static_cast<uint64_t>(rr.info.size)) {
+        r.ok = false;
+        r.error = "short read: " + std::to_string(rr.bytes) + " of " + std::to_string(rr.info.size) + " bytes";
+      }
+    } catch (const StorageError& e) {
+      r.end_ns = now_ns();
+      r.error = std::string("while creating reader object: ") + e.what();
+    } catch (const std::exception& e) {
+      r.end_ns = now_ns();
+      r.error = e.what();
+    }
+    ms = (r.end_ns - r.start_ns) / 1e6;
+    host_ms = r.host_done_ns ? (r.host_done_ns - r.start_ns) / 1e6 : ms;
+    if (r.ok && cfg_.latency_fd >= 0) {
+      char line[64];
+      int n = std::snprintf(line, sizeof(line), "%.3fms\n", ms);
+      std::lock_guard<std::mutex> lk(out_mu_);
+      ssize_t wr = ::write(cfg_.latency_fd, line, static_cast<size_t>(n));
+      (void)wr;
+    }
+    bool ok = r.ok;
+    record(std::move(r), ms, host_ms);
+    if (!ok && cfg_.stop_on_error) {
+      stop_flag_ = true;
+      break;
+    }
+  }
+  if (gsink) {
+    std::lock_guard<std::mutex> lk(mu_);
+    gpu_stats_[w] = gsink->stats();
+  }
+}
+
+std::vector<ReadRecord> Runner::drain() {
+  std::lock_guard<std::mutex> lk(mu_);
+  std::vector<ReadRecord> out;
+  out.swap(pending_);
+  return out;
+}
+
+RunSummary Runner::summary() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  RunSummary s = acc_;
+  s.elapsed_s = t_last_ > t_first_ ? (t_last_ - t_first_) / 1e9 : 0;
+  s.mb_per_s = s.elapsed_s > 0 ? s.bytes / 1048576.0 / s.elapsed_s : 0;
+  std::vector<double> v = lat_ms_;
+  std::sort(v.begin(), v.end());
+  if (!v.empty()) {
+    double sum = 0;
+    for (double x : v) sum += x;
+    s.avg_ms = sum / v.size();
+    s.p20_ms = percentile_floor(v, 20);
+    s.p50_ms = percentile_floor(v, 50);
+    s.p90_ms = percentile_floor(v, 90);
+    s.p99_ms = percentile_floor(v, 99);
+    s.min_ms = v.front();
+    s.max_ms = v.back();
+  }
+  std::vector<double> h = host_ms_;
+  std::sort(h.begin(), h.end());
+  s.host_p50_ms = percentile_floor(h, 50);
+  s.host_p99_ms = percentile_floor(h, 99);
+  for (const auto& g : gpu_stats_) {
+    s.gpu.slots_submitted += g.slots_submitted;
+    s.gpu.segments += g.segments;
+    s.gpu.chunks_verified_gpu += g.chunks_verified_gpu;
+    s.gpu.chunks_verified_host += g.chunks_verified_host;
+    s.gpu.objects_verified += g.objects_verified;
+    s.gpu.slot_waits += g.slot_waits;
+    s.gpu.slot_wait_s += g.slot_wait_s;
+  }
+  return s;
+}
+
+}  // namespace gcsb

@@ -1,0 +1,41 @@
+// CDNA4 CRC32C engine: host-side types and launchers for the kernels in
+// crc32c_kernels.hip.  [new] — the reference verifies CRC32C only inside the
+// Go storage library on the host.
+//
+// A "segment" is one contiguous device byte range [addr, addr+len) whose
+// CRC32C is wanted (one gRPC ChecksummedData message, or the part of it that
+// landed in one ring slot, or one slot's share of an HTTP body).  A batch of up
+// to kMaxSeg segments is processed by two launches on the caller's stream:
+//   K1 crc32c_tiles    : every wave CRCs one 4 KiB tile (64 lanes x 4 x 16 B,
+//                        slice-by-16 + shift tables staged in LDS, 6-level
+//                        wave tree), tiles right-aligned to the segment end so
+//                        a ragged head is just leading zeros (free for raw CRC);
+//   K2 crc32c_segments : one workgroup per segment folds its tiles (strided
+//                        Horner + 8-level tree), adds the <16-byte tail, applies
+//                        the init/xorout fixup and compares with the expected
+//                        CRC, writing {raw, crc, status} to host-mapped memory.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "gpu/crc_types.h"
+
+namespace gcsb {
+
+// Per-device, lazily uploaded tables.
+const CrcTables* device_crc_tables(int device);
+
+// Enqueue K1 + K2. tile_scratch must hold batch.total_tiles words.
+void launch_crc32c_batch(const CrcBatch& b, const CrcTables* d_tables, uint32_t* d_tile_scratch,
+                         CrcSegResult* d_results, hipStream_t stream);
+
+// Pattern kernels (K3): object bytes of the synthetic content (csrc/core/content.h).
+void launch_fill_pattern(uint8_t* dst, uint64_t n, uint64_t rot, uint64_t obj_off, hipStream_t stream);
+// Counts mismatching bytes into *d_count (uint64) and records the first index.
+void launch_verify_pattern(const uint8_t* src, uint64_t n, uint64_t rot, uint64_t obj_off,
+                           unsigned long long* d_count, unsigned long long* d_first, hipStream_t stream);
+
+void hip_check(hipError_t e, const char* what);
+
+}  // namespace gcsb

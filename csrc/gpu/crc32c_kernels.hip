@@ -1,0 +1,267 @@
+// CDNA4 (gfx950) CRC32C kernels + synthetic-pattern fill/verify kernels.
+// Design notes in crc32c_gpu.h.  Wave64 throughout: a 4 KiB tile is exactly
+// one wave-instruction of 16 B per lane x 4 rows, so the loads are perfectly
+// coalesced 1 KiB global_load_dwordx4 and need no LDS round trip (the data has
+// no reuse); the LDS instead holds the 44 KiB of lookup tables that every
+// lane hits ~20 times per 16 bytes.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+
+#include "core/content.h"
+#include "core/crc32c.h"
+#include "gpu/crc32c_gpu.h"
+
+namespace gcsb {
+
+void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string("HIP error in ") + what + ": " + hipGetErrorString(e));
+}
+
+namespace {
+
+constexpr int kK1Threads = 256;                       // 4 waves, one tile each per iteration
+constexpr int kLdsWords = 16 * 256 + 7 * 4 * 256;     // slice16 + 7 lane shift tables = 11264 words (44 KiB)
+
+__device__ __forceinline__ uint32_t shift4(const uint32_t* __restrict__ tab, uint32_t s) {
+  return tab[s & 0xff] ^ tab[256 + ((s >> 8) & 0xff)] ^ tab[512 + ((s >> 16) & 0xff)] ^ tab[768 + (s >> 24)];
+}
+
+// state advanced over 16 bytes of data (slice-by-16; T_k = byte followed by k zeros)
+__device__ __forceinline__ uint32_t update16(const uint32_t* __restrict__ sl, uint32_t state, uint4 v) {
+  const uint32_t x = state ^ v.x;
+  uint32_t c = sl[15 * 256 + (x & 0xff)] ^ sl[14 * 256 + ((x >> 8) & 0xff)] ^ sl[13 * 256 + ((x >> 16) & 0xff)] ^
+               sl[12 * 256 + (x >> 24)];
+  c ^= sl[11 * 256 + (v.y & 0xff)] ^ sl[10 * 256 + ((v.y >> 8) & 0xff)] ^ sl[9 * 256 + ((v.y >> 16) & 0xff)] ^
+       sl[8 * 256 + (v.y >> 24)];
+  c ^= sl[7 * 256 + (v.z & 0xff)] ^ sl[6 * 256 + ((v.z >> 8) & 0xff)] ^ sl[5 * 256 + ((v.z >> 16) & 0xff)] ^
+       sl[4 * 256 + (v.z >> 24)];
+  c ^= sl[3 * 256 + (v.w & 0xff)] ^ sl[2 * 256 + ((v.w >> 8) & 0xff)] ^ sl[1 * 256 + ((v.w >> 16) & 0xff)] ^
+       sl[0 * 256 + (v.w >> 24)];
+  return c;
+}
+
+__device__ __forceinline__ uint32_t mask_low_bytes(uint32_t w, int keep_from) {
+  // zero bytes [0, keep_from) of a little-endian word (keep_from in 0..4)
+  if (keep_from <= 0) return w;
+  if (keep_from >= 4) return 0;
+  return w & (0xFFFFFFFFu << (8 * keep_from));
+}
+
+// K1: raw CRC of every 4 KiB tile of every segment in the batch.
+__global__ __launch_bounds__(kK1Threads) void crc32c_tiles_kernel(const CrcBatch b, const uint32_t* __restrict__ tabs,
+                                                                   uint32_t* __restrict__ tile_out) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_tab[kLdsWords];
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(tabs);
+    uint4* dst = reinterpret_cast<uint4*>(s_tab);
+#pragma unroll
+    for (int i = threadIdx.x; i < kLdsWords / 4; i += kK1Threads) dst[i] = src[i];
+  }
+  __syncthreads();
+  const uint32_t* sl = s_tab;
+  const uint32_t* lane_shift = s_tab + 16 * 256;
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t nwaves = gridDim.x * (kK1Threads / 64);
+  for (uint32_t gt = blockIdx.x * (kK1Threads / 64) + wave; gt < b.total_tiles; gt += nwaves) {
+    uint32_t s = 0;
+    while (s + 1 < b.nseg && b.seg[s + 1].tile_base <= gt) ++s;
+    const uintptr_t addr = reinterpret_cast<uintptr_t>(b.seg[s].addr);
+    const uint32_t len = b.seg[s].len;
+    const uint32_t t = gt - b.seg[s].tile_base;
+    const uintptr_t a16 = addr & ~uintptr_t(15);
+    const uint64_t full = (addr + len - a16 + 15) / 16 - 1;
+    const intptr_t vend = static_cast<intptr_t>(a16 + 16 * full);
+    const intptr_t tstart = vend - static_cast<intptr_t>(kCrcTile) * static_cast<intptr_t>(b.seg[s].ntiles - t);
+    uint4 v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const intptr_t p = tstart + 1024 * j + 16 * lane;
+      v[j] = make_uint4(0, 0, 0, 0);
+      if (p + 16 > static_cast<intptr_t>(addr)) v[j] = *reinterpret_cast<const uint4*>(p);
+      if (p < static_cast<intptr_t>(addr) && p + 16 > static_cast<intptr_t>(addr)) {
+        const int h = static_cast<int>(static_cast<intptr_t>(addr) - p);  // 1..15 leading bytes to zero
+        v[j].x = mask_low_bytes(v[j].x, h);
+        v[j].y = mask_low_bytes(v[j].y, h - 4);
+        v[j].z = mask_low_bytes(v[j].z, h - 8);
+        v[j].w = mask_low_bytes(v[j].w, h - 12);
+      }
+    }
+    uint32_t state = update16(sl, 0u, v[0]);
+#pragma unroll
+    for (int j = 1; j < 4; ++j) state = update16(sl, shift4(lane_shift + 6 * 1024, state), v[j]);  // +1008 B gap
+    // wave tree: lane l ends at tile offset 3072 + 16(l+1); fold to the tile end
+#pragma unroll
+    for (int lv = 0; lv < 6; ++lv) {
+      const uint32_t other = __shfl_down(state, 1 << lv, 64);
+      const uint32_t shifted = shift4(lane_shift + lv * 1024, state);
+      if ((lane & ((2 << lv) - 1)) == 0) state = shifted ^ other;
+    }
+    if (lane == 0) tile_out[gt] = state;
+  }
+}
+
+// K2: fold tiles -> segment raw CRC, add the tail, fixup, compare.
+__global__ __launch_bounds__(256) void crc32c_segments_kernel(const CrcBatch b, const CrcTables* __restrict__ t,
+                                                              const uint32_t* __restrict__ tiles,
+                                                              CrcSegResult* __restrict__ out) {
+  const uint32_t s = blockIdx.x;
+  if (s >= b.nseg) return;
+  const uint32_t T = b.seg[s].ntiles;
+  const uint32_t base = b.seg[s].tile_base;
+  const int k = threadIdx.x;
+  const int lane = k & 63;
+  uint32_t acc = 0;
+  const int M = static_cast<int>((T + 255) >> 8);
+  for (int m = M - 1; m >= 0; --m) {
+    acc = shift4(&t->tile_shift[8][0][0], acc);
+    const uint32_t j = static_cast<uint32_t>(k) + 256u * static_cast<uint32_t>(m);
+    if (j < T) acc ^= tiles[base + T - 1 - j];
+  }
+#pragma unroll
+  for (int lv = 0; lv < 6; ++lv) {
+    const uint32_t other = __shfl_down(acc, 1 << lv, 64);
+    if ((lane & ((2 << lv) - 1)) == 0) acc ^= shift4(&t->tile_shift[lv][0][0], other);
+  }
+  __shared__ uint32_t part[4];
+  if (lane == 0) part[k >> 6] = acc;
+  __syncthreads();
+  if (k == 0) {
+    const uint32_t v0 = part[0] ^ shift4(&t->tile_shift[6][0][0], part[1]);
+    const uint32_t v2 = part[2] ^ shift4(&t->tile_shift[6][0][0], part[3]);
+    uint32_t raw = v0 ^ shift4(&t->tile_shift[7][0][0], v2);
+    const uint32_t len = b.seg[s].len;
+    if (len > 0) {
+      const uintptr_t addr = reinterpret_cast<uintptr_t>(b.seg[s].addr);
+      const uintptr_t a16 = addr & ~uintptr_t(15);
+      const uintptr_t e = addr + len;
+      const uintptr_t vend = a16 + 16 * ((e - a16 + 15) / 16 - 1);
+      const uint8_t* p = reinterpret_cast<const uint8_t*>(vend > addr ? vend : addr);
+      const uint8_t* pe = reinterpret_cast<const uint8_t*>(e);
+      for (; p < pe; ++p) raw = (raw >> 8) ^ t->slice16[0][(raw ^ *p) & 0xff];
+    }
+    const uint32_t crc = raw ^ b.seg[s].fixup;
+    CrcSegResult r;
+    r.raw = raw;
+    r.crc = crc;
+    r.status = (b.seg[s].flags & 1) ? (crc == b.seg[s].expected ? 1u : 2u) : 0u;
+    r.pad = 0;
+    out[s] = r;
+  }
+}
+
+__device__ __forceinline__ uint8_t obj_byte(uint64_t q) {
+  return pattern_byte(kPatternSeed, q);
+}
+
+__global__ __launch_bounds__(256) void fill_pattern_kernel(uint8_t* __restrict__ dst, uint64_t n, uint64_t rot,
+                                                           uint64_t obj_off) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  for (uint64_t g = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; g * 16 < n; g += stride) {
+    const uint64_t b0 = g * 16;
+    uint64_t q = (obj_off + b0 + rot) % kPatternLen;
+    uint8_t v[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      v[e] = obj_byte(q);
+      q = (q + 1 == kPatternLen) ? 0 : q + 1;
+    }
+    if (b0 + 16 <= n && (reinterpret_cast<uintptr_t>(dst + b0) & 15) == 0) {
+      uint4 w;
+      __builtin_memcpy(&w, v, 16);
+      *reinterpret_cast<uint4*>(dst + b0) = w;
+    } else {
+      for (int e = 0; e < 16 && b0 + e < n; ++e) dst[b0 + e] = v[e];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void verify_pattern_kernel(const uint8_t* __restrict__ src, uint64_t n, uint64_t rot,
+                                                             uint64_t obj_off, unsigned long long* count,
+                                                             unsigned long long* first) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  for (uint64_t g = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; g * 16 < n; g += stride) {
+    const uint64_t b0 = g * 16;
+    uint64_t q = (obj_off + b0 + rot) % kPatternLen;
+    unsigned bad = 0;
+    uint64_t first_bad = ~0ull;
+    for (int e = 0; e < 16 && b0 + e < n; ++e) {
+      if (src[b0 + e] != obj_byte(q)) {
+        ++bad;
+        if (first_bad == ~0ull) first_bad = b0 + e;
+      }
+      q = (q + 1 == kPatternLen) ? 0 : q + 1;
+    }
+    if (bad) {
+      atomicAdd(count, static_cast<unsigned long long>(bad));
+      atomicMin(first, static_cast<unsigned long long>(first_bad));
+    }
+  }
+}
+
+}  // namespace
+
+const CrcTables* device_crc_tables(int device) {
+  static std::mutex mu;
+  static CrcTables* per_dev[64] = {nullptr};
+  static CrcTables* host = nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  if (device < 0 || device >= 64) throw std::runtime_error("bad device index");
+  if (!per_dev[device]) {
+    if (!host) {
+      host = new CrcTables();
+      build_crc_tables(host);
+    }
+    int prev = 0;
+    hip_check(hipGetDevice(&prev), "hipGetDevice");
+    hip_check(hipSetDevice(device), "hipSetDevice");
+    CrcTables* d = nullptr;
+    hip_check(hipMalloc(reinterpret_cast<void**>(&d), sizeof(CrcTables)), "hipMalloc(tables)");
+    hip_check(hipMemcpy(d, host, sizeof(CrcTables), hipMemcpyHostToDevice), "hipMemcpy(tables)");
+    per_dev[device] = d;
+    hip_check(hipSetDevice(prev), "hipSetDevice");
+  }
+  return per_dev[device];
+}
+
+void launch_crc32c_batch(const CrcBatch& b, const CrcTables* d_tables, uint32_t* d_tile_scratch,
+                         CrcSegResult* d_results, hipStream_t stream) {
+  if (b.nseg == 0) return;
+  if (b.total_tiles > 0) {
+    uint32_t blocks = (b.total_tiles + 3) / 4;
+    if (blocks > 1024) blocks = 1024;
+    hipLaunchKernelGGL(crc32c_tiles_kernel, dim3(blocks), dim3(kK1Threads), 0, stream, b,
+                       reinterpret_cast<const uint32_t*>(d_tables), d_tile_scratch);
+    hip_check(hipGetLastError(), "crc32c_tiles_kernel");
+  }
+  hipLaunchKernelGGL(crc32c_segments_kernel, dim3(b.nseg), dim3(256), 0, stream, b, d_tables, d_tile_scratch,
+                     d_results);
+  hip_check(hipGetLastError(), "crc32c_segments_kernel");
+}
+
+void launch_fill_pattern(uint8_t* dst, uint64_t n, uint64_t rot, uint64_t obj_off, hipStream_t stream) {
+  if (n == 0) return;
+  uint64_t groups = (n + 15) / 16;
+  uint64_t blocks = (groups + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(fill_pattern_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, stream, dst, n, rot,
+                     obj_off);
+  hip_check(hipGetLastError(), "fill_pattern_kernel");
+}
+
+void launch_verify_pattern(const uint8_t* src, uint64_t n, uint64_t rot, uint64_t obj_off,
+                           unsigned long long* d_count, unsigned long long* d_first, hipStream_t stream) {
+  if (n == 0) return;
+  uint64_t groups = (n + 15) / 16;
+  uint64_t blocks = (groups + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(verify_pattern_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, stream, src, n, rot,
+                     obj_off, d_count, d_first);
+  hip_check(hipGetLastError(), "verify_pattern_kernel");
+}
+
+}  // namespace gcsb

@@ -1,0 +1,119 @@
+// Host half of the GPU CRC32C engine: table construction, batch geometry and a
+// bit-exact emulator of kernels K1/K2 (the CPU-side oracle for their math).
+#include <cstring>
+#include <vector>
+
+#include "core/crc32c.h"
+#include "gpu/crc_types.h"
+
+namespace gcsb {
+
+void build_crc_tables(CrcTables* t) {
+  crc32c_build_slice16(t->slice16);
+  for (int lv = 0; lv < 6; ++lv) crc32c_build_shift_table(16ull << lv, t->lane_shift[lv]);
+  crc32c_build_shift_table(1008, t->lane_shift[6]);
+  for (int lv = 0; lv < 9; ++lv) crc32c_build_shift_table(4096ull << lv, t->tile_shift[lv]);
+}
+
+void finalize_crc_batch(CrcBatch* b) {
+  uint32_t tiles = 0;
+  for (uint32_t i = 0; i < b->nseg; ++i) {
+    CrcSeg& s = b->seg[i];
+    s.tile_base = tiles;
+    crc_segment_geometry(reinterpret_cast<uintptr_t>(s.addr), s.len, &s.ntiles);
+    s.fixup = crc32c_fixup(s.len);
+    tiles += s.ntiles;
+  }
+  b->total_tiles = tiles;
+}
+
+namespace {
+uint32_t shift4(const uint32_t tab[4][256], uint32_t s) { return crc32c_apply_shift_table(tab, s); }
+uint32_t update16(const uint32_t sl[16][256], uint32_t state, const uint32_t v[4]) {
+  const uint32_t x = state ^ v[0];
+  uint32_t c = sl[15][x & 0xff] ^ sl[14][(x >> 8) & 0xff] ^ sl[13][(x >> 16) & 0xff] ^ sl[12][x >> 24];
+  c ^= sl[11][v[1] & 0xff] ^ sl[10][(v[1] >> 8) & 0xff] ^ sl[9][(v[1] >> 16) & 0xff] ^ sl[8][v[1] >> 24];
+  c ^= sl[7][v[2] & 0xff] ^ sl[6][(v[2] >> 8) & 0xff] ^ sl[5][(v[2] >> 16) & 0xff] ^ sl[4][v[2] >> 24];
+  c ^= sl[3][v[3] & 0xff] ^ sl[2][(v[3] >> 8) & 0xff] ^ sl[1][(v[3] >> 16) & 0xff] ^ sl[0][v[3] >> 24];
+  return c;
+}
+uint32_t mask_low_bytes(uint32_t w, int keep_from) {
+  if (keep_from <= 0) return w;
+  if (keep_from >= 4) return 0;
+  return w & (0xFFFFFFFFu << (8 * keep_from));
+}
+}  // namespace
+
+CrcSegResult emulate_crc32c_segment(const uint8_t* addr_p, uint32_t len, const CrcTables& t, uint32_t expected,
+                                    bool check) {
+  const uintptr_t addr = reinterpret_cast<uintptr_t>(addr_p);
+  uint32_t T = 0;
+  crc_segment_geometry(addr, len, &T);
+  std::vector<uint32_t> tiles(T);
+  // K1
+  for (uint32_t tt = 0; tt < T; ++tt) {
+    const uintptr_t a16 = addr & ~uintptr_t(15);
+    const uint64_t full = (addr + len - a16 + 15) / 16 - 1;
+    const intptr_t vend = static_cast<intptr_t>(a16 + 16 * full);
+    const intptr_t tstart = vend - 4096 * static_cast<intptr_t>(T - tt);
+    uint32_t lanes[64];
+    for (int lane = 0; lane < 64; ++lane) {
+      uint32_t v[4][4];
+      for (int j = 0; j < 4; ++j) {
+        const intptr_t p = tstart + 1024 * j + 16 * lane;
+        std::memset(v[j], 0, 16);
+        if (p + 16 > static_cast<intptr_t>(addr)) std::memcpy(v[j], reinterpret_cast<const void*>(p), 16);
+        if (p < static_cast<intptr_t>(addr) && p + 16 > static_cast<intptr_t>(addr)) {
+          const int h = static_cast<int>(static_cast<intptr_t>(addr) - p);
+          v[j][0] = mask_low_bytes(v[j][0], h);
+          v[j][1] = mask_low_bytes(v[j][1], h - 4);
+          v[j][2] = mask_low_bytes(v[j][2], h - 8);
+          v[j][3] = mask_low_bytes(v[j][3], h - 12);
+        }
+      }
+      uint32_t state = update16(t.slice16, 0, v[0]);
+      for (int j = 1; j < 4; ++j) state = update16(t.slice16, shift4(t.lane_shift[6], state), v[j]);
+      lanes[lane] = state;
+    }
+    for (int lv = 0; lv < 6; ++lv) {
+      uint32_t nxt[64];
+      for (int lane = 0; lane < 64; ++lane) {
+        uint32_t other = lane + (1 << lv) < 64 ? lanes[lane + (1 << lv)] : lanes[lane];
+        uint32_t shifted = shift4(t.lane_shift[lv], lanes[lane]);
+        nxt[lane] = ((lane & ((2 << lv) - 1)) == 0) ? (shifted ^ other) : lanes[lane];
+      }
+      std::memcpy(lanes, nxt, sizeof(lanes));
+    }
+    tiles[tt] = lanes[0];
+  }
+  // K2
+  uint32_t acc[256];
+  const int M = static_cast<int>((T + 255) >> 8);
+  for (int k = 0; k < 256; ++k) {
+    uint32_t a = 0;
+    for (int m = M - 1; m >= 0; --m) {
+      a = shift4(t.tile_shift[8], a);
+      uint32_t j = static_cast<uint32_t>(k) + 256u * static_cast<uint32_t>(m);
+      if (j < T) a ^= tiles[T - 1 - j];
+    }
+    acc[k] = a;
+  }
+  for (int lv = 0; lv < 8; ++lv)
+    for (int k = 0; k < 256; k += (2 << lv)) acc[k] ^= shift4(t.tile_shift[lv], acc[k + (1 << lv)]);
+  uint32_t raw = acc[0];
+  if (len > 0) {
+    const uintptr_t a16 = addr & ~uintptr_t(15);
+    const uintptr_t e = addr + len;
+    const uintptr_t vend = a16 + 16 * ((e - a16 + 15) / 16 - 1);
+    for (uintptr_t p = vend > addr ? vend : addr; p < e; ++p)
+      raw = (raw >> 8) ^ t.slice16[0][(raw ^ *reinterpret_cast<const uint8_t*>(p)) & 0xff];
+  }
+  CrcSegResult r;
+  r.raw = raw;
+  r.crc = raw ^ crc32c_fixup(len);
+  r.status = check ? (r.crc == expected ? 1u : 2u) : 0u;
+  r.pad = 0;
+  return r;
+}
+
+}  // namespace gcsb

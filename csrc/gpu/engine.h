@@ -1,0 +1,150 @@
+// GPU data plane: pinned host ring -> side HIP stream hipMemcpyAsync -> HBM,
+// with CRC32C verified by the CDNA4 kernels.  [new].
+//
+// Reference hot loop (reference main.go:133-148): NewReader, io.CopyBuffer into
+// io.Discard, stop the timer.  Here the transport recv()s each object byte
+// once, straight into a page-locked ring slot; a full slot is handed to the
+// GPU (one async H2D copy + the two CRC launches + an event on the sink's own
+// non-blocking stream) while the transport keeps filling the next slot.  The
+// read's timer stops in finish() once the last slot's event has fired: every
+// byte is in HBM and every checksum the server sent has been checked.
+//
+// Slot state machine (debuggable with GCSB_DEBUG_RING=1 asserts):
+//   FREE -> FILLING (transport writes) -> INFLIGHT (copy+kernels queued)
+//        -> harvested (event complete, results folded) -> FREE
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "gpu/crc32c_gpu.h"
+#include "storage/sink.h"
+
+namespace gcsb {
+
+enum class Landing {
+  kRing,    // HBM ring of the same geometry as the host ring (discard semantics)
+  kObject,  // whole object laid out contiguously in HBM (up to 288 GB per GPU)
+};
+
+struct GpuSinkConfig {
+  int device = 0;
+  size_t slot_bytes = 8 << 20;
+  int slots = 4;
+  bool verify = true;  // run the CRC kernels
+  Landing landing = Landing::kObject;
+  // Submit a partially filled slot when at least this many bytes are waiting
+  // and the socket has nothing more right now (0 = only full slots).
+  size_t eager_submit_bytes = 0;
+};
+
+struct GpuSinkStats {
+  uint64_t slots_submitted = 0;
+  uint64_t segments = 0;
+  uint64_t chunks_verified_gpu = 0;   // whole chunk checked by the K2 epilogue
+  uint64_t chunks_verified_host = 0;  // chunk spanning slots, folded on host
+  uint64_t objects_verified = 0;
+  uint64_t slot_waits = 0;            // transport had to wait for a free slot
+  double slot_wait_s = 0;
+};
+
+class GpuSink : public Sink {
+ public:
+  explicit GpuSink(const GpuSinkConfig& cfg);
+  ~GpuSink() override;
+  GpuSink(const GpuSink&) = delete;
+  GpuSink& operator=(const GpuSink&) = delete;
+
+  // Land objects in caller-owned HBM (e.g. a torch tensor) instead of the
+  // sink's own buffer. cap must cover the object.
+  void set_external_destination(void* dptr, size_t cap);
+  void* object_device_ptr() const { return obj_dst_; }
+  size_t object_capacity() const { return obj_cap_; }
+  hipStream_t stream() const { return stream_; }
+  const GpuSinkStats& stats() const { return stats_; }
+  const GpuSinkConfig& config() const { return cfg_; }
+
+  void begin(const ObjectInfo& info) override;
+  void update_info(const ObjectInfo& info) override;
+  Window acquire(size_t want) override;
+  void commit(size_t n) override;
+  void chunk_begin(size_t len) override;
+  void chunk_end(bool has_crc, uint32_t crc) override;
+  void resume_at(int64_t offset) override;
+  SinkResult finish() override;
+  void abort() override;
+
+ private:
+  struct SegInfo {
+    uint64_t slot_off = 0;
+    uint64_t obj_off = 0;
+    uint32_t len = 0;
+    bool closed = false;
+    bool chunk_start = false;
+    bool chunk_end = false;
+    bool has_expected = false;
+    bool broken_chunk = false;  // chunk interrupted by a resume
+    uint32_t expected = 0;
+  };
+  struct Slot {
+    uint8_t* host = nullptr;
+    uint8_t* dev_ring = nullptr;
+    size_t used = 0;
+    uint64_t obj_off = 0;
+    std::vector<SegInfo> segs;
+    hipEvent_t ev = nullptr;
+    bool inflight = false;
+    CrcSegResult* res = nullptr;  // host-mapped, kMaxSeg entries
+  };
+  void ensure_object_capacity(int64_t size);
+  Slot& take_slot();
+  void submit_current();
+  void wait_slot(Slot& s);
+  void harvest(Slot& s);
+  uint32_t shift(uint32_t v, uint64_t nbytes);
+  void set_device() const;
+
+  GpuSinkConfig cfg_;
+  hipStream_t stream_ = nullptr;
+  std::vector<Slot> slots_;
+  int cur_ = -1;         // FILLING slot index or -1
+  int next_ = 0;         // next slot to take
+  const CrcTables* d_tables_ = nullptr;
+  uint32_t* d_tiles_ = nullptr;
+  size_t tiles_cap_ = 0;
+  CrcSegResult* res_host_ = nullptr;
+  uint8_t* own_obj_ = nullptr;
+  uint8_t* obj_dst_ = nullptr;
+  size_t obj_cap_ = 0;
+  bool external_dst_ = false;
+  // per-read state
+  ObjectInfo info_;
+  uint64_t delivered_ = 0;
+  bool in_chunk_ = false;
+  bool chunk_start_pending_ = false;
+  bool chunk_broken_ = false;
+  uint32_t chunk_raw_ = 0;  // host fold of a multi-slot chunk
+  uint64_t chunk_len_ = 0;
+  uint32_t obj_raw_ = 0;    // host fold of the whole object
+  uint64_t obj_len_ = 0;
+  bool mismatch_ = false;
+  bool any_checked_ = false;
+  std::string detail_;
+  // cached x^(8n) operators for the host fold
+  uint64_t op_len_[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+  uint32_t op_val_[4] = {0, 0, 0, 0};
+  int op_rr_ = 0;
+  GpuSinkStats stats_;
+};
+
+// Device CRC32C of an arbitrary device range (test/verification utility).
+uint32_t gpu_crc32c(int device, const void* dptr, size_t n);
+// Fill / verify device memory with synthetic object bytes.
+void gpu_fill_pattern(int device, void* dptr, uint64_t n, uint64_t rot, uint64_t obj_off);
+uint64_t gpu_verify_pattern(int device, const void* dptr, uint64_t n, uint64_t rot, uint64_t obj_off,
+                            uint64_t* first_bad);
+int gpu_device_count();
+
+}  // namespace gcsb

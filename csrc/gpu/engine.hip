@@ -1,0 +1,434 @@
+// GPU sink: pinned ring -> hipMemcpyAsync -> HBM + CRC32C kernels.  See engine.h.
+#include "gpu/engine.h"
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+
+#include "core/crc32c.h"
+#include "core/util.h"
+
+namespace gcsb {
+
+namespace {
+bool debug_ring() {
+  static bool d = [] {
+    const char* e = std::getenv("GCSB_DEBUG_RING");
+    return e && *e == '1';
+  }();
+  return d;
+}
+}  // namespace
+
+int gpu_device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+void GpuSink::set_device() const { hip_check(hipSetDevice(cfg_.device), "hipSetDevice"); }
+
+GpuSink::GpuSink(const GpuSinkConfig& cfg) : cfg_(cfg) {
+  if (cfg_.slots < 2) cfg_.slots = 2;
+  cfg_.slot_bytes = (cfg_.slot_bytes + 4095) / 4096 * 4096;
+  if (cfg_.slot_bytes < 65536) cfg_.slot_bytes = 65536;
+  set_device();
+  hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
+  d_tables_ = device_crc_tables(cfg_.device);
+  tiles_cap_ = cfg_.slot_bytes / kCrcTile + 2 * kMaxSeg + 8;
+  hip_check(hipMalloc(reinterpret_cast<void**>(&d_tiles_), tiles_cap_ * sizeof(uint32_t)), "hipMalloc(tiles)");
+  hip_check(hipHostMalloc(reinterpret_cast<void**>(&res_host_), sizeof(CrcSegResult) * kMaxSeg * cfg_.slots,
+                          hipHostMallocMapped | hipHostMallocCoherent),
+            "hipHostMalloc(results)");
+  std::memset(res_host_, 0, sizeof(CrcSegResult) * kMaxSeg * cfg_.slots);
+  slots_.resize(cfg_.slots);
+  for (int i = 0; i < cfg_.slots; ++i) {
+    Slot& s = slots_[i];
+    hip_check(hipHostMalloc(reinterpret_cast<void**>(&s.host), cfg_.slot_bytes, hipHostMallocDefault),
+              "hipHostMalloc(ring slot)");
+    if (cfg_.landing == Landing::kRing)
+      hip_check(hipMalloc(reinterpret_cast<void**>(&s.dev_ring), cfg_.slot_bytes), "hipMalloc(ring slot)");
+    hip_check(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming), "hipEventCreate");
+    s.res = res_host_ + static_cast<size_t>(i) * kMaxSeg;
+  }
+}
+
+GpuSink::~GpuSink() {
+  try {
+    set_device();
+    if (stream_) (void)hipStreamSynchronize(stream_);
+  } catch (...) {
+  }
+  for (Slot& s : slots_) {
+    if (s.host) (void)hipHostFree(s.host);
+    if (s.dev_ring) (void)hipFree(s.dev_ring);
+    if (s.ev) (void)hipEventDestroy(s.ev);
+  }
+  if (res_host_) (void)hipHostFree(res_host_);
+  if (d_tiles_) (void)hipFree(d_tiles_);
+  if (own_obj_) (void)hipFree(own_obj_);
+  if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+void GpuSink::set_external_destination(void* dptr, size_t cap) {
+  set_device();
+  hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+  if (own_obj_) {
+    (void)hipFree(own_obj_);
+    own_obj_ = nullptr;
+  }
+  obj_dst_ = static_cast<uint8_t*>(dptr);
+  obj_cap_ = cap;
+  external_dst_ = dptr != nullptr;
+}
+
+void GpuSink::ensure_object_capacity(int64_t size) {
+  if (cfg_.landing != Landing::kObject || size < 0) return;
+  uint64_t need = static_cast<uint64_t>(size) - static_cast<uint64_t>(info_.start_offset);
+  if (need <= obj_cap_) return;
+  if (external_dst_)
+    throw StorageError("object (" + std::to_string(need) + " B) exceeds the external HBM destination (" +
+                           std::to_string(obj_cap_) + " B)",
+                       false);
+  set_device();
+  hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+  if (own_obj_) hip_check(hipFree(own_obj_), "hipFree");
+  size_t cap = (need + (2u << 20) - 1) / (2u << 20) * (2u << 20);
+  hip_check(hipMalloc(reinterpret_cast<void**>(&own_obj_), cap), "hipMalloc(object landing)");
+  obj_dst_ = own_obj_;
+  obj_cap_ = cap;
+}
+
+void GpuSink::begin(const ObjectInfo& info) {
+  abort();  // drain anything a previous (failed) read left behind
+  info_ = info;
+  delivered_ = 0;
+  in_chunk_ = false;
+  chunk_start_pending_ = false;
+  chunk_broken_ = false;
+  chunk_raw_ = 0;
+  chunk_len_ = 0;
+  obj_raw_ = 0;
+  obj_len_ = 0;
+  mismatch_ = false;
+  any_checked_ = false;
+  detail_.clear();
+  ensure_object_capacity(info.size);
+}
+
+void GpuSink::update_info(const ObjectInfo& info) {
+  if (info.has_crc32c) {
+    info_.has_crc32c = true;
+    info_.crc32c = info.crc32c;
+  }
+  if (!info.md5.empty()) info_.md5 = info.md5;
+  if (info.generation) info_.generation = info.generation;
+  if (info.size >= 0 && info_.size < 0) {
+    info_.size = info.size;
+    if (delivered_ == 0) ensure_object_capacity(info.size);
+  }
+}
+
+GpuSink::Slot& GpuSink::take_slot() {
+  Slot& s = slots_[next_];
+  if (s.inflight) {
+    ++stats_.slot_waits;
+    int64_t t0 = now_ns();
+    wait_slot(s);
+    stats_.slot_wait_s += (now_ns() - t0) / 1e9;
+  }
+  s.used = 0;
+  s.segs.clear();
+  s.obj_off = delivered_;
+  cur_ = next_;
+  next_ = (next_ + 1) % cfg_.slots;
+  return s;
+}
+
+Window GpuSink::acquire(size_t want) {
+  (void)want;
+  if (cur_ < 0) take_slot();
+  {
+    Slot& s = slots_[cur_];
+    bool segs_full = s.segs.size() >= static_cast<size_t>(kMaxSeg) && (s.segs.empty() || s.segs.back().closed);
+    if (s.used == cfg_.slot_bytes || segs_full) {
+      submit_current();
+      take_slot();
+    }
+  }
+  Slot& s = slots_[cur_];
+  if (s.segs.empty() || s.segs.back().closed) {
+    SegInfo g;
+    g.slot_off = s.used;
+    g.obj_off = delivered_;
+    g.chunk_start = chunk_start_pending_;
+    g.broken_chunk = chunk_broken_;
+    chunk_start_pending_ = false;
+    s.segs.push_back(g);
+  }
+  size_t cap = cfg_.slot_bytes - s.used;
+  if (cfg_.landing == Landing::kObject) {
+    if (delivered_ >= obj_cap_)
+      throw StorageError("object larger than its HBM landing buffer (" + std::to_string(obj_cap_) + " B)", false);
+    if (obj_cap_ - delivered_ < cap) cap = obj_cap_ - delivered_;
+  }
+  // keep a segment below 4 GiB (32-bit length in the kernel batch)
+  return Window{s.host + s.used, cap};
+}
+
+void GpuSink::commit(size_t n) {
+  Slot& s = slots_[cur_];
+  if (debug_ring() && (s.segs.empty() || s.segs.back().closed || s.used + n > cfg_.slot_bytes))
+    throw std::logic_error("GpuSink::commit outside an acquired window");
+  s.used += n;
+  s.segs.back().len += static_cast<uint32_t>(n);
+  delivered_ += n;
+}
+
+void GpuSink::chunk_begin(size_t len) {
+  if (cur_ >= 0) {
+    Slot& s = slots_[cur_];
+    if (!s.segs.empty()) s.segs.back().closed = true;
+    // keep a chunk inside one slot when it fits, so its CRC is checked in
+    // the K2 epilogue on the GPU instead of being folded on the host
+    if (s.used > 0 && cfg_.slot_bytes - s.used < len && len <= cfg_.slot_bytes) submit_current();
+  }
+  in_chunk_ = true;
+  chunk_start_pending_ = true;
+  chunk_broken_ = false;
+}
+
+void GpuSink::chunk_end(bool has_crc, uint32_t crc) {
+  if (!in_chunk_) return;
+  in_chunk_ = false;
+  if (chunk_start_pending_) {
+    // zero-length chunk: nothing landed
+    chunk_start_pending_ = false;
+    if (has_crc && cfg_.verify) {
+      any_checked_ = true;
+      if (crc != 0) {
+        mismatch_ = true;
+        detail_ = "empty chunk with non-zero crc32c";
+      }
+    }
+    return;
+  }
+  if (cur_ < 0 || slots_[cur_].segs.empty() || slots_[cur_].segs.back().closed) return;
+  SegInfo& g = slots_[cur_].segs.back();
+  g.closed = true;
+  g.chunk_end = true;
+  g.has_expected = has_crc;
+  g.expected = crc;
+  g.broken_chunk = chunk_broken_;
+}
+
+void GpuSink::resume_at(int64_t offset) {
+  (void)offset;
+  chunk_broken_ = true;
+  if (cur_ >= 0 && !slots_[cur_].segs.empty() && !slots_[cur_].segs.back().closed) {
+    slots_[cur_].segs.back().closed = true;
+    slots_[cur_].segs.back().broken_chunk = true;
+  }
+  in_chunk_ = false;
+  chunk_start_pending_ = false;
+}
+
+void GpuSink::submit_current() {
+  if (cur_ < 0) return;
+  Slot& s = slots_[cur_];
+  cur_ = -1;
+  if (s.used == 0) {
+    // nothing landed: hand the slot back (it is the one next_ points behind)
+    next_ = static_cast<int>((next_ + cfg_.slots - 1) % cfg_.slots);
+    return;
+  }
+  if (!s.segs.empty()) s.segs.back().closed = true;
+  set_device();
+  uint8_t* dst = cfg_.landing == Landing::kObject ? obj_dst_ + s.obj_off : s.dev_ring;
+  hip_check(hipMemcpyAsync(dst, s.host, s.used, hipMemcpyHostToDevice, stream_), "hipMemcpyAsync(H2D)");
+  if (cfg_.verify && !s.segs.empty()) {
+    CrcBatch b;
+    std::memset(&b, 0, sizeof(b));
+    b.nseg = static_cast<uint32_t>(s.segs.size());
+    for (size_t i = 0; i < s.segs.size(); ++i) {
+      const SegInfo& g = s.segs[i];
+      CrcSeg& c = b.seg[i];
+      c.addr = dst + g.slot_off;
+      c.len = g.len;
+      c.expected = g.expected;
+      c.flags = (g.chunk_start && g.chunk_end && g.has_expected && !g.broken_chunk) ? 1u : 0u;
+    }
+    finalize_crc_batch(&b);
+    if (b.total_tiles > tiles_cap_) throw std::logic_error("CRC tile scratch too small");
+    CrcSegResult* d_res = nullptr;
+    hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_res), s.res, 0), "hipHostGetDevicePointer");
+    launch_crc32c_batch(b, d_tables_, d_tiles_, d_res, stream_);
+    stats_.segments += s.segs.size();
+  }
+  hip_check(hipEventRecord(s.ev, stream_), "hipEventRecord");
+  s.inflight = true;
+  ++stats_.slots_submitted;
+}
+
+void GpuSink::wait_slot(Slot& s) {
+  if (!s.inflight) return;
+  set_device();
+  hip_check(hipEventSynchronize(s.ev), "hipEventSynchronize");
+  s.inflight = false;
+  harvest(s);
+}
+
+uint32_t GpuSink::shift(uint32_t v, uint64_t nbytes) {
+  if (v == 0 || nbytes == 0) return v;
+  for (int i = 0; i < 4; ++i)
+    if (op_len_[i] == nbytes) return gf2_multmodp(op_val_[i], v);
+  int k = op_rr_++ & 3;
+  op_len_[k] = nbytes;
+  op_val_[k] = crc32c_x8n(nbytes);
+  return gf2_multmodp(op_val_[k], v);
+}
+
+void GpuSink::harvest(Slot& s) {
+  if (!cfg_.verify) return;
+  for (size_t i = 0; i < s.segs.size(); ++i) {
+    const SegInfo& g = s.segs[i];
+    const volatile CrcSegResult* rv = s.res + i;
+    const uint32_t raw = rv->raw;
+    const uint32_t status = rv->status;
+    obj_raw_ = shift(obj_raw_, g.len) ^ raw;
+    obj_len_ += g.len;
+    if (g.chunk_start) {
+      chunk_raw_ = 0;
+      chunk_len_ = 0;
+    }
+    chunk_raw_ = shift(chunk_raw_, g.len) ^ raw;
+    chunk_len_ += g.len;
+    if (g.chunk_end && g.has_expected && !g.broken_chunk) {
+      any_checked_ = true;
+      const uint32_t crc = chunk_raw_ ^ crc32c_fixup(chunk_len_);
+      const bool whole = g.chunk_start;
+      if (whole) ++stats_.chunks_verified_gpu;
+      else ++stats_.chunks_verified_host;
+      if (crc != g.expected || (whole && status != 1)) {
+        mismatch_ = true;
+        char b[160];
+        std::snprintf(b, sizeof(b), "chunk crc32c mismatch at offset %llu: got %08x want %08x (gpu status %u)",
+                      static_cast<unsigned long long>(g.obj_off + g.len - chunk_len_), crc, g.expected, status);
+        detail_ = b;
+      }
+    }
+  }
+}
+
+SinkResult GpuSink::finish() {
+  submit_current();
+  for (int k = 0; k < cfg_.slots; ++k) wait_slot(slots_[(next_ + k) % cfg_.slots]);
+  SinkResult r;
+  r.bytes = delivered_;
+  r.landed_ns = now_ns();
+  if (cfg_.verify && info_.has_crc32c && info_.start_offset == 0 &&
+      (info_.size < 0 || static_cast<uint64_t>(info_.size) == obj_len_)) {
+    any_checked_ = true;
+    ++stats_.objects_verified;
+    const uint32_t crc = obj_raw_ ^ crc32c_fixup(obj_len_);
+    r.computed_crc32c = crc;
+    if (crc != info_.crc32c) {
+      mismatch_ = true;
+      char b[128];
+      std::snprintf(b, sizeof(b), "bad CRC on read: got %08x want %08x", crc, info_.crc32c);
+      detail_ = b;
+    }
+  } else if (cfg_.verify) {
+    r.computed_crc32c = obj_raw_ ^ crc32c_fixup(obj_len_);
+  }
+  r.verified = any_checked_ && !mismatch_;
+  r.crc_mismatch = mismatch_;
+  r.detail = detail_;
+  return r;
+}
+
+void GpuSink::abort() {
+  if (cur_ >= 0) {
+    slots_[cur_].used = 0;
+    slots_[cur_].segs.clear();
+    cur_ = -1;
+  }
+  set_device();
+  for (Slot& s : slots_)
+    if (s.inflight) {
+      hip_check(hipEventSynchronize(s.ev), "hipEventSynchronize");
+      s.inflight = false;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// utilities
+
+uint32_t gpu_crc32c(int device, const void* dptr, size_t n) {
+  hip_check(hipSetDevice(device), "hipSetDevice");
+  const CrcTables* tabs = device_crc_tables(device);
+  hipStream_t st;
+  hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+  const size_t kSeg = 1u << 30;
+  std::vector<CrcSeg> segs;
+  const uint8_t* p = static_cast<const uint8_t*>(dptr);
+  for (size_t off = 0; off < n || (n == 0 && off == 0); off += kSeg) {
+    CrcSeg s{};
+    s.addr = p + off;
+    s.len = static_cast<uint32_t>(n - off < kSeg ? n - off : kSeg);
+    segs.push_back(s);
+    if (n == 0) break;
+  }
+  uint32_t crc = 0;
+  uint64_t total = 0;
+  CrcSegResult* res = nullptr;
+  hip_check(hipHostMalloc(reinterpret_cast<void**>(&res), sizeof(CrcSegResult) * kMaxSeg,
+                          hipHostMallocMapped | hipHostMallocCoherent),
+            "hipHostMalloc");
+  uint32_t* d_tiles = nullptr;
+  for (size_t i0 = 0; i0 < segs.size(); i0 += kMaxSeg) {
+    CrcBatch b;
+    std::memset(&b, 0, sizeof(b));
+    b.nseg = static_cast<uint32_t>(std::min<size_t>(kMaxSeg, segs.size() - i0));
+    for (uint32_t i = 0; i < b.nseg; ++i) b.seg[i] = segs[i0 + i];
+    finalize_crc_batch(&b);
+    if (d_tiles) (void)hipFree(d_tiles);
+    hip_check(hipMalloc(reinterpret_cast<void**>(&d_tiles), sizeof(uint32_t) * (b.total_tiles + 1)), "hipMalloc");
+    CrcSegResult* d_res = nullptr;
+    hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_res), res, 0), "hipHostGetDevicePointer");
+    launch_crc32c_batch(b, tabs, d_tiles, d_res, st);
+    hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
+    for (uint32_t i = 0; i < b.nseg; ++i) {
+      crc = crc32c_combine(crc, res[i].crc, b.seg[i].len);
+      total += b.seg[i].len;
+    }
+  }
+  if (d_tiles) (void)hipFree(d_tiles);
+  (void)hipHostFree(res);
+  (void)hipStreamDestroy(st);
+  return crc;
+}
+
+void gpu_fill_pattern(int device, void* dptr, uint64_t n, uint64_t rot, uint64_t obj_off) {
+  hip_check(hipSetDevice(device), "hipSetDevice");
+  launch_fill_pattern(static_cast<uint8_t*>(dptr), n, rot, obj_off, nullptr);
+  hip_check(hipStreamSynchronize(nullptr), "hipStreamSynchronize");
+}
+
+uint64_t gpu_verify_pattern(int device, const void* dptr, uint64_t n, uint64_t rot, uint64_t obj_off,
+                            uint64_t* first_bad) {
+  hip_check(hipSetDevice(device), "hipSetDevice");
+  unsigned long long* d = nullptr;
+  hip_check(hipMalloc(reinterpret_cast<void**>(&d), 16), "hipMalloc");
+  unsigned long long init[2] = {0ull, ~0ull};
+  hip_check(hipMemcpy(d, init, 16, hipMemcpyHostToDevice), "hipMemcpy");
+  launch_verify_pattern(static_cast<const uint8_t*>(dptr), n, rot, obj_off, d, d + 1, nullptr);
+  unsigned long long out[2];
+  hip_check(hipMemcpy(out, d, 16, hipMemcpyDeviceToHost), "hipMemcpy");
+  (void)hipFree(d);
+  if (first_bad) *first_bad = out[1];
+  return out[0];
+}
+
+}  // namespace gcsb

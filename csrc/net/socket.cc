@@ -1,0 +1,289 @@
+#include "net/socket.h"
+
+#include <arpa/inet.h>
+#include <fcntl.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <openssl/err.h>
+#include <openssl/ssl.h>
+#include <poll.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <cstring>
+#include <mutex>
+
+#include "core/util.h"
+
+namespace gcsb {
+
+Endpoint Endpoint::parse(const std::string& url) {
+  Endpoint ep;
+  std::string rest = url;
+  size_t p = rest.find("://");
+  if (p != std::string::npos) {
+    ep.scheme = to_lower(rest.substr(0, p));
+    rest = rest.substr(p + 3);
+  }
+  ep.port = ep.scheme == "https" ? 443 : 80;
+  size_t slash = rest.find('/');
+  std::string hostport = rest.substr(0, slash);
+  if (slash != std::string::npos) {
+    ep.base_path = rest.substr(slash);
+    while (!ep.base_path.empty() && ep.base_path.back() == '/') ep.base_path.pop_back();
+  }
+  size_t colon = hostport.rfind(':');
+  if (colon != std::string::npos && hostport.find(']') == std::string::npos) {
+    ep.host = hostport.substr(0, colon);
+    ep.port = std::stoi(hostport.substr(colon + 1));
+  } else {
+    ep.host = hostport;
+  }
+  if (ep.host.empty()) ep.host = "127.0.0.1";
+  return ep;
+}
+
+std::string Endpoint::host_header() const {
+  bool dflt = (scheme == "http" && port == 80) || (scheme == "https" && port == 443);
+  return dflt ? host : host + ":" + std::to_string(port);
+}
+
+void apply_socket_options(int fd, const SocketOptions& opt) {
+  int one = 1;
+  if (opt.nodelay) setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+  if (opt.rcvbuf > 0) setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &opt.rcvbuf, sizeof(opt.rcvbuf));
+  if (opt.sndbuf > 0) setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &opt.sndbuf, sizeof(opt.sndbuf));
+  if (opt.io_timeout_ms > 0) {
+    timeval tv{opt.io_timeout_ms / 1000, (opt.io_timeout_ms % 1000) * 1000};
+    setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+    setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
+  }
+}
+
+static SSL_CTX* client_ssl_ctx(bool verify) {
+  static std::mutex mu;
+  static SSL_CTX* ctx[2] = {nullptr, nullptr};
+  std::lock_guard<std::mutex> lk(mu);
+  SSL_CTX*& c = ctx[verify ? 1 : 0];
+  if (!c) {
+    c = SSL_CTX_new(TLS_client_method());
+    if (verify) {
+      SSL_CTX_set_default_verify_paths(c);
+      SSL_CTX_set_verify(c, SSL_VERIFY_PEER, nullptr);
+    } else {
+      SSL_CTX_set_verify(c, SSL_VERIFY_NONE, nullptr);
+    }
+  }
+  return c;
+}
+
+std::unique_ptr<Conn> Conn::dial(const Endpoint& ep, const SocketOptions& opt) {
+  addrinfo hints{};
+  hints.ai_family = AF_UNSPEC;
+  hints.ai_socktype = SOCK_STREAM;
+  addrinfo* res = nullptr;
+  std::string port = std::to_string(ep.port);
+  int rc = getaddrinfo(ep.host.c_str(), port.c_str(), &hints, &res);
+  if (rc != 0) throw StorageError("resolve " + ep.host + ": " + gai_strerror(rc), true);
+  int fd = -1;
+  std::string last_err;
+  for (addrinfo* ai = res; ai; ai = ai->ai_next) {
+    fd = ::socket(ai->ai_family, ai->ai_socktype | SOCK_CLOEXEC, ai->ai_protocol);
+    if (fd < 0) continue;
+    apply_socket_options(fd, opt);
+    // non-blocking connect with timeout
+    int fl = fcntl(fd, F_GETFL, 0);
+    fcntl(fd, F_SETFL, fl | O_NONBLOCK);
+    int c = ::connect(fd, ai->ai_addr, ai->ai_addrlen);
+    if (c != 0 && errno == EINPROGRESS) {
+      pollfd pfd{fd, POLLOUT, 0};
+      int pr = ::poll(&pfd, 1, opt.connect_timeout_ms > 0 ? opt.connect_timeout_ms : -1);
+      int soerr = 0;
+      socklen_t sl = sizeof(soerr);
+      if (pr == 1) getsockopt(fd, SOL_SOCKET, SO_ERROR, &soerr, &sl);
+      c = (pr == 1 && soerr == 0) ? 0 : -1;
+      if (pr == 0) errno = ETIMEDOUT;
+      else if (soerr) errno = soerr;
+    }
+    if (c == 0) {
+      fcntl(fd, F_SETFL, fl);
+      break;
+    }
+    last_err = std::strerror(errno);
+    ::close(fd);
+    fd = -1;
+  }
+  freeaddrinfo(res);
+  if (fd < 0) throw StorageError("connect " + ep.host + ":" + port + ": " + last_err, true);
+  auto conn = std::make_unique<Conn>();
+  conn->fd_ = fd;
+  if (ep.scheme == "https") {
+    SSL* ssl = SSL_new(client_ssl_ctx(opt.tls_verify));
+    SSL_set_fd(ssl, fd);
+    SSL_set_tlsext_host_name(ssl, ep.host.c_str());
+    if (SSL_connect(ssl) != 1) {
+      SSL_free(ssl);
+      throw StorageError("TLS handshake with " + ep.host + " failed", true);
+    }
+    conn->ssl_ = ssl;
+  }
+  return conn;
+}
+
+std::unique_ptr<Conn> Conn::adopt(int fd, const SocketOptions& opt) {
+  apply_socket_options(fd, opt);
+  auto conn = std::make_unique<Conn>();
+  conn->fd_ = fd;
+  return conn;
+}
+
+Conn::~Conn() { close(); }
+
+void Conn::close() {
+  if (ssl_) {
+    SSL_shutdown(ssl_);
+    SSL_free(ssl_);
+    ssl_ = nullptr;
+  }
+  if (fd_ >= 0) {
+    ::close(fd_);
+    fd_ = -1;
+  }
+}
+
+void Conn::shutdown_write() {
+  if (fd_ >= 0) ::shutdown(fd_, SHUT_WR);
+}
+
+size_t Conn::read_some(void* buf, size_t n) {
+  if (fd_ < 0) throw StorageError("read on closed connection", true);
+  for (;;) {
+    ssize_t r;
+    if (ssl_) {
+      int k = SSL_read(ssl_, buf, static_cast<int>(n > (1u << 30) ? (1u << 30) : n));
+      if (k <= 0) {
+        int e = SSL_get_error(ssl_, k);
+        if (e == SSL_ERROR_ZERO_RETURN) return 0;
+        throw StorageError("TLS read error", true);
+      }
+      r = k;
+    } else {
+      r = ::recv(fd_, buf, n, 0);
+    }
+    if (r >= 0) {
+      bytes_read_ += static_cast<uint64_t>(r);
+      return static_cast<size_t>(r);
+    }
+    if (errno == EINTR) continue;
+    if (errno == EAGAIN || errno == EWOULDBLOCK) throw StorageError("read timeout", true);
+    throw StorageError(std::string("recv: ") + std::strerror(errno), true);
+  }
+}
+
+void Conn::read_exact(void* buf, size_t n) {
+  auto* p = static_cast<uint8_t*>(buf);
+  while (n > 0) {
+    size_t r;
+    if (!ssl_) {
+      ssize_t k = ::recv(fd_, p, n, MSG_WAITALL);
+      if (k < 0) {
+        if (errno == EINTR) continue;
+        if (errno == EAGAIN || errno == EWOULDBLOCK) throw StorageError("read timeout", true);
+        throw StorageError(std::string("recv: ") + std::strerror(errno), true);
+      }
+      r = static_cast<size_t>(k);
+      bytes_read_ += r;
+    } else {
+      r = read_some(p, n);
+    }
+    if (r == 0) throw StorageError("unexpected EOF", true);
+    p += r;
+    n -= r;
+  }
+}
+
+void Conn::write_all(const void* buf, size_t n) {
+  iovec iov{const_cast<void*>(buf), n};
+  writev_all(&iov, 1);
+}
+
+void Conn::writev_all(struct iovec* iov, int cnt) {
+  if (fd_ < 0) throw StorageError("write on closed connection", true);
+  if (ssl_) {
+    for (int i = 0; i < cnt; ++i) {
+      auto* p = static_cast<const uint8_t*>(iov[i].iov_base);
+      size_t n = iov[i].iov_len;
+      while (n > 0) {
+        int k = SSL_write(ssl_, p, static_cast<int>(n > (1u << 30) ? (1u << 30) : n));
+        if (k <= 0) throw StorageError("TLS write error", true);
+        p += k;
+        n -= static_cast<size_t>(k);
+        bytes_written_ += static_cast<uint64_t>(k);
+      }
+    }
+    return;
+  }
+  while (cnt > 0) {
+    msghdr msg{};
+    msg.msg_iov = iov;
+    msg.msg_iovlen = static_cast<size_t>(cnt > 1024 ? 1024 : cnt);
+    ssize_t w = ::sendmsg(fd_, &msg, MSG_NOSIGNAL);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      throw StorageError(std::string("send: ") + std::strerror(errno), true);
+    }
+    bytes_written_ += static_cast<uint64_t>(w);
+    size_t left = static_cast<size_t>(w);
+    while (cnt > 0 && left >= iov->iov_len) {
+      left -= iov->iov_len;
+      ++iov;
+      --cnt;
+    }
+    if (cnt > 0 && left) {
+      iov->iov_base = static_cast<uint8_t*>(iov->iov_base) + left;
+      iov->iov_len -= left;
+    }
+  }
+}
+
+Listener::Listener(const std::string& host, int port, int backlog) {
+  fd_ = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  if (fd_ < 0) throw std::runtime_error("socket failed");
+  int one = 1;
+  setsockopt(fd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+  sockaddr_in addr{};
+  addr.sin_family = AF_INET;
+  addr.sin_port = htons(static_cast<uint16_t>(port));
+  if (inet_pton(AF_INET, host.c_str(), &addr.sin_addr) != 1) addr.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  if (::bind(fd_, reinterpret_cast<sockaddr*>(&addr), sizeof(addr)) != 0)
+    throw std::runtime_error("bind " + host + ":" + std::to_string(port) + ": " + std::strerror(errno));
+  if (::listen(fd_, backlog) != 0) throw std::runtime_error("listen failed");
+  socklen_t sl = sizeof(addr);
+  getsockname(fd_, reinterpret_cast<sockaddr*>(&addr), &sl);
+  port_ = ntohs(addr.sin_port);
+}
+
+Listener::~Listener() { close(); }
+
+int Listener::accept_fd() {
+  for (;;) {
+    int fd = fd_;
+    if (fd < 0) return -1;
+    int c = ::accept4(fd, nullptr, nullptr, SOCK_CLOEXEC);
+    if (c >= 0) return c;
+    if (errno == EINTR || errno == ECONNABORTED) continue;
+    return -1;
+  }
+}
+
+void Listener::close() {
+  if (fd_ >= 0) {
+    ::shutdown(fd_, SHUT_RDWR);
+    ::close(fd_);
+    fd_ = -1;
+  }
+}
+
+}  // namespace gcsb

@@ -1,0 +1,88 @@
+// Blocking TCP connections (optionally TLS via OpenSSL) used by every
+// transport.  One connection is owned by one thread at a time, except the
+// HTTP/2 client where a reader thread owns recv and writers serialize send.
+//
+// Reference counterpart: Go net/http's Transport dials/keeps-alive TCP(+TLS)
+// connections (reference main.go:65-73); grpc-go dials one HTTP/2 connection
+// per pool entry (main.go:30,111).
+#pragma once
+#include <sys/uio.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <memory>
+#include <string>
+
+typedef struct ssl_st SSL;
+typedef struct ssl_ctx_st SSL_CTX;
+
+namespace gcsb {
+
+struct Endpoint {
+  std::string scheme = "http";  // http | https
+  std::string host = "127.0.0.1";
+  int port = 80;
+  std::string base_path;  // path prefix, e.g. "" or "/storage"
+  static Endpoint parse(const std::string& url);
+  std::string host_header() const;
+};
+
+struct SocketOptions {
+  int rcvbuf = 8 << 20;
+  int sndbuf = 8 << 20;
+  bool nodelay = true;
+  int connect_timeout_ms = 10000;
+  int io_timeout_ms = 0;  // 0 = none (reference: http.Client.Timeout=0, main.go:94)
+  bool tls_verify = false;
+};
+
+class Conn {
+ public:
+  Conn() = default;
+  ~Conn();
+  Conn(const Conn&) = delete;
+  Conn& operator=(const Conn&) = delete;
+
+  static std::unique_ptr<Conn> dial(const Endpoint& ep, const SocketOptions& opt);
+  static std::unique_ptr<Conn> adopt(int fd, const SocketOptions& opt);
+
+  // Returns bytes read (0 = orderly EOF); throws StorageError(retryable) on reset.
+  size_t read_some(void* buf, size_t n);
+  // Reads exactly n bytes or throws (EOF mid-way is a retryable error).
+  void read_exact(void* buf, size_t n);
+  void write_all(const void* buf, size_t n);
+  void writev_all(struct iovec* iov, int cnt);
+  void shutdown_write();
+  void close();
+  int fd() const { return fd_; }
+  bool is_open() const { return fd_ >= 0; }
+  bool tls() const { return ssl_ != nullptr; }
+  uint64_t bytes_read() const { return bytes_read_; }
+  uint64_t bytes_written() const { return bytes_written_; }
+
+ private:
+  int fd_ = -1;
+  SSL* ssl_ = nullptr;
+  uint64_t bytes_read_ = 0;
+  uint64_t bytes_written_ = 0;
+};
+
+// Listening socket for the synthetic server.
+class Listener {
+ public:
+  explicit Listener(const std::string& host, int port, int backlog = 1024);
+  ~Listener();
+  int port() const { return port_; }
+  int fd() const { return fd_; }
+  // Returns -1 when closed.
+  int accept_fd();
+  void close();
+
+ private:
+  int fd_ = -1;
+  int port_ = 0;
+};
+
+void apply_socket_options(int fd, const SocketOptions& opt);
+
+}  // namespace gcsb

@@ -1,0 +1,579 @@
+// Python bindings (_native): the Python layer only orchestrates (CLI flags,
+// exporters, torch.distributed barriers); every hot loop runs in this module
+// with the GIL released.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+
+#include "bench/runner.h"
+#include "core/content.h"
+#include "core/crc32c.h"
+#include "core/util.h"
+#include "gpu/crc_types.h"
+#include "gpu/engine.h"
+#include "server/fakegcs.h"
+#include "storage/auth.h"
+#include "storage/client.h"
+
+namespace py = pybind11;
+using namespace gcsb;
+
+namespace {
+
+template <typename T>
+T get_or(const py::dict& d, const char* k, T dflt) {
+  if (d.contains(k) && !d[k].is_none()) return d[k].cast<T>();
+  return dflt;
+}
+
+RetryPolicy retry_from(const py::dict& d) {
+  RetryPolicy p;
+  std::string mode = get_or<std::string>(d, "retry_mode", "always");
+  p.mode = mode == "never" ? RetryMode::kNever : mode == "idempotent" ? RetryMode::kIdempotent : RetryMode::kAlways;
+  p.initial_s = get_or<double>(d, "retry_initial_s", 1.0);
+  p.max_s = get_or<double>(d, "retry_max_s", 30.0);
+  p.multiplier = get_or<double>(d, "retry_multiplier", 2.0);
+  p.max_total_s = get_or<double>(d, "retry_max_total_s", 0.0);
+  p.max_attempts = get_or<int>(d, "retry_max_attempts", 0);
+  return p;
+}
+
+ClientConfig client_from(const py::dict& d) {
+  ClientConfig c;
+  c.protocol = get_or<std::string>(d, "protocol", "http");
+  c.endpoint = Endpoint::parse(get_or<std::string>(d, "endpoint", "http://127.0.0.1:8080"));
+  c.http_api = get_or<std::string>(d, "http_api", "xml");
+  c.user_agent = get_or<std::string>(d, "user_agent", "prince");
+  c.max_conns_per_host = get_or<int>(d, "max_conns_per_host", 100);
+  c.max_idle_conns_per_host = get_or<int>(d, "max_idle_conns_per_host", 100);
+  c.grpc_conn_pool_size = get_or<int>(d, "grpc_conn_pool_size", 1);
+  c.read_chunk = get_or<size_t>(d, "read_chunk", 2u << 20);
+  c.retry = retry_from(d);
+  c.sock.rcvbuf = get_or<int>(d, "rcvbuf", 8 << 20);
+  c.sock.sndbuf = get_or<int>(d, "sndbuf", 8 << 20);
+  c.sock.io_timeout_ms = get_or<int>(d, "io_timeout_ms", 0);
+  c.project = get_or<std::string>(d, "project", "gcs-fuse-test");
+  std::string auth = get_or<std::string>(d, "auth", "none");
+  if (auth == "static") {
+    c.token = std::make_shared<StaticTokenSource>(get_or<std::string>(d, "token", ""));
+  } else if (auth == "adc" || auth == "key_file") {
+    c.token = get_token_source(get_or<std::string>(d, "key_file", ""), kScopeFullControl,
+                               get_or<std::string>(d, "token_uri", ""));
+  }
+  return c;
+}
+
+GpuSinkConfig gpu_from(const py::dict& d) {
+  GpuSinkConfig g;
+  g.device = get_or<int>(d, "device", 0);
+  g.slot_bytes = get_or<size_t>(d, "ring_slot_bytes", 8u << 20);
+  g.slots = get_or<int>(d, "ring_slots", 4);
+  g.verify = get_or<bool>(d, "gpu_verify", true);
+  g.landing = get_or<std::string>(d, "landing", "object") == "ring" ? Landing::kRing : Landing::kObject;
+  return g;
+}
+
+py::dict sink_result_dict(const ReadResult& rr) {
+  py::dict r;
+  r["bytes"] = rr.bytes;
+  r["attempts"] = rr.attempts;
+  r["verified"] = rr.sink.verified;
+  r["crc_mismatch"] = rr.sink.crc_mismatch;
+  r["computed_crc32c"] = rr.sink.computed_crc32c;
+  r["detail"] = rr.sink.detail;
+  r["size"] = rr.info.size;
+  r["generation"] = rr.info.generation;
+  r["has_crc32c"] = rr.info.has_crc32c;
+  r["crc32c"] = rr.info.crc32c;
+  r["md5"] = py::bytes(rr.info.md5);
+  r["first_byte_ns"] = rr.first_byte_ns;
+  r["host_done_ns"] = rr.host_done_ns;
+  r["landed_ns"] = rr.sink.landed_ns;
+  return r;
+}
+
+py::dict meta_dict(const ObjectMeta& m) {
+  py::dict r;
+  r["name"] = m.name;
+  r["bucket"] = m.bucket;
+  r["size"] = m.size;
+  r["generation"] = m.generation;
+  r["metageneration"] = m.metageneration;
+  r["has_crc32c"] = m.has_crc32c;
+  r["crc32c"] = m.crc32c;
+  r["md5"] = py::bytes(m.md5);
+  r["content_type"] = m.content_type;
+  r["updated"] = m.updated;
+  return r;
+}
+
+py::dict gpu_stats_dict(const GpuSinkStats& g) {
+  py::dict r;
+  r["slots_submitted"] = g.slots_submitted;
+  r["segments"] = g.segments;
+  r["chunks_verified_gpu"] = g.chunks_verified_gpu;
+  r["chunks_verified_host"] = g.chunks_verified_host;
+  r["objects_verified"] = g.objects_verified;
+  r["slot_waits"] = g.slot_waits;
+  r["slot_wait_s"] = g.slot_wait_s;
+  return r;
+}
+
+// Owning wrapper so Python can keep a GPU sink (and its HBM) across reads.
+struct PyGpuSink {
+  std::unique_ptr<GpuSink> sink;
+};
+
+class PyClient {
+ public:
+  explicit PyClient(const py::dict& cfg) : client_(make_client(client_from(cfg))) {}
+
+  py::dict read(const std::string& bucket, const std::string& name, const std::string& sink_kind, bool host_crc,
+                int64_t offset, int64_t limit) {
+    ReadResult rr;
+    {
+      py::gil_scoped_release nogil;
+      DiscardSink s(client_->config().read_chunk, host_crc);
+      rr = client_->read_object(bucket, name, s, offset, limit);
+    }
+    (void)sink_kind;
+    return sink_result_dict(rr);
+  }
+
+  py::dict read_gpu(const std::string& bucket, const std::string& name, PyGpuSink& gs, int64_t offset, int64_t limit) {
+    ReadResult rr;
+    {
+      py::gil_scoped_release nogil;
+      rr = client_->read_object(bucket, name, *gs.sink, offset, limit);
+    }
+    py::dict d = sink_result_dict(rr);
+    d["device_ptr"] = reinterpret_cast<uintptr_t>(gs.sink->object_device_ptr());
+    return d;
+  }
+
+  py::bytes read_bytes(const std::string& bucket, const std::string& name, int64_t offset, int64_t limit) {
+    // Collecting sink for tests/small objects.
+    struct Collect : Sink {
+      std::string data;
+      size_t used = 0;
+      ObjectInfo info;
+      void begin(const ObjectInfo& i) override { info = i; data.clear(); used = 0; }
+      void update_info(const ObjectInfo&) override {}
+      Window acquire(size_t want) override {
+        if (data.size() < used + want) data.resize(used + want);
+        return Window{reinterpret_cast<uint8_t*>(&data[used]), want};
+      }
+      void commit(size_t n) override { used += n; }
+      SinkResult finish() override {
+        data.resize(used);
+        SinkResult r;
+        r.bytes = used;
+        return r;
+      }
+    } c;
+    {
+      py::gil_scoped_release nogil;
+      client_->read_object(bucket, name, c, offset, limit);
+    }
+    return py::bytes(c.data);
+  }
+
+  py::dict stat(const std::string& bucket, const std::string& name) {
+    ObjectMeta m;
+    {
+      py::gil_scoped_release nogil;
+      m = client_->stat_object(bucket, name);
+    }
+    return meta_dict(m);
+  }
+
+  py::dict list(const std::string& bucket, const std::string& prefix, int page_size, const std::string& token,
+                const std::string& delimiter) {
+    ListResult r;
+    {
+      py::gil_scoped_release nogil;
+      r = client_->list_objects(bucket, prefix, page_size, token, delimiter);
+    }
+    py::dict d;
+    py::list objs;
+    for (auto& o : r.objects) objs.append(meta_dict(o));
+    d["objects"] = objs;
+    d["prefixes"] = r.prefixes;
+    d["next_page_token"] = r.next_page_token;
+    return d;
+  }
+
+  py::list list_all(const std::string& bucket, const std::string& prefix, int page_size) {
+    std::vector<ObjectMeta> all;
+    {
+      py::gil_scoped_release nogil;
+      all = client_->list_all(bucket, prefix, page_size);
+    }
+    py::list out;
+    for (auto& o : all) out.append(meta_dict(o));
+    return out;
+  }
+
+  py::dict write_bytes(const std::string& bucket, const std::string& name, const py::bytes& data, bool resumable,
+                       size_t chunk_bytes) {
+    std::string buf = data;
+    ObjectMeta m;
+    {
+      py::gil_scoped_release nogil;
+      HostByteSource src(reinterpret_cast<const uint8_t*>(buf.data()), buf.size());
+      WriteOptions o;
+      o.resumable = resumable;
+      o.chunk_bytes = chunk_bytes;
+      m = client_->write_object(bucket, name, src, o);
+    }
+    return meta_dict(m);
+  }
+
+  py::dict stats() {
+    auto& s = client_->stats();
+    py::dict d;
+    d["requests"] = s.requests.load();
+    d["retries"] = s.retries.load();
+    d["bytes_in"] = s.bytes_in.load();
+    d["bytes_out"] = s.bytes_out.load();
+    return d;
+  }
+  StorageClient& client() { return *client_; }
+
+ private:
+  std::unique_ptr<StorageClient> client_;
+};
+
+class PyRunner {
+ public:
+  explicit PyRunner(const py::dict& d) {
+    RunnerConfig c;
+    c.client = client_from(d);
+    c.bucket = get_or<std::string>(d, "bucket", c.bucket);
+    c.object_prefix = get_or<std::string>(d, "object_prefix", c.object_prefix);
+    c.object_suffix = get_or<std::string>(d, "object_suffix", c.object_suffix);
+    if (d.contains("object_names") && !d["object_names"].is_none())
+      c.object_names = d["object_names"].cast<std::vector<std::string>>();
+    c.workers = get_or<int>(d, "workers", c.workers);
+    c.reads_per_worker = get_or<int64_t>(d, "reads_per_worker", c.reads_per_worker);
+    c.duration_s = get_or<double>(d, "duration_s", 0.0);
+    c.worker_id_offset = get_or<int>(d, "worker_id_offset", 0);
+    c.sink = get_or<std::string>(d, "sink", "discard");
+    c.host_crc = get_or<bool>(d, "host_crc", true);
+    c.gpu = gpu_from(d);
+    c.latency_fd = get_or<int>(d, "latency_fd", -1);
+    c.keep_records = get_or<bool>(d, "keep_records", true);
+    c.stop_on_error = get_or<bool>(d, "stop_on_error", true);
+    c.trace_sample_rate = get_or<double>(d, "trace_sample_rate", 0.0);
+    c.range_offset = get_or<int64_t>(d, "range_offset", 0);
+    c.range_limit = get_or<int64_t>(d, "range_limit", -1);
+    c.seed = get_or<uint64_t>(d, "seed", 0);
+    runner_ = std::make_unique<Runner>(std::move(c));
+  }
+  void start() { runner_->start(); }
+  void wait() {
+    py::gil_scoped_release nogil;
+    runner_->wait();
+  }
+  void stop() { runner_->stop(); }
+  py::list drain() {
+    std::vector<ReadRecord> recs = runner_->drain();
+    py::list out;
+    for (auto& r : recs) {
+      py::dict d;
+      d["worker"] = r.worker;
+      d["seq"] = r.seq;
+      d["object"] = r.object;
+      d["start_wall_ns"] = r.start_wall_ns;
+      d["start_ns"] = r.start_ns;
+      d["ttfb_ns"] = r.ttfb_ns;
+      d["host_done_ns"] = r.host_done_ns;
+      d["end_ns"] = r.end_ns;
+      d["bytes"] = r.bytes;
+      d["attempts"] = r.attempts;
+      d["ok"] = r.ok;
+      d["verified"] = r.verified;
+      d["sampled"] = r.sampled;
+      d["trace_hi"] = r.trace_hi;
+      d["trace_lo"] = r.trace_lo;
+      d["span_id"] = r.span_id;
+      d["error"] = r.error;
+      out.append(d);
+    }
+    return out;
+  }
+  py::dict summary() {
+    RunSummary s = runner_->summary();
+    py::dict d;
+    d["reads"] = s.reads;
+    d["errors"] = s.errors;
+    d["bytes"] = s.bytes;
+    d["retries"] = s.retries;
+    d["verified"] = s.verified;
+    d["elapsed_s"] = s.elapsed_s;
+    d["mib_per_s"] = s.mb_per_s;
+    d["avg_ms"] = s.avg_ms;
+    d["p20_ms"] = s.p20_ms;
+    d["p50_ms"] = s.p50_ms;
+    d["p90_ms"] = s.p90_ms;
+    d["p99_ms"] = s.p99_ms;
+    d["min_ms"] = s.min_ms;
+    d["max_ms"] = s.max_ms;
+    d["host_p50_ms"] = s.host_p50_ms;
+    d["host_p99_ms"] = s.host_p99_ms;
+    py::list b;
+    for (int i = 0; i < kOcBuckets; ++i) b.append(s.oc_buckets[i]);
+    d["oc_buckets"] = b;
+    d["first_error"] = s.first_error;
+    d["gpu"] = gpu_stats_dict(s.gpu);
+    return d;
+  }
+  std::string object_for(int w, int64_t seq) { return runner_->object_for(w, seq); }
+
+ private:
+  std::unique_ptr<Runner> runner_;
+};
+
+class PyServer {
+ public:
+  explicit PyServer(const py::dict& d) {
+    ServerConfig c;
+    c.host = get_or<std::string>(d, "host", "127.0.0.1");
+    c.port = get_or<int>(d, "port", 0);
+    c.require_auth = get_or<bool>(d, "require_auth", false);
+    c.jwt_public_key_pem = get_or<std::string>(d, "jwt_public_key_pem", "");
+    c.grpc_chunk = get_or<uint64_t>(d, "grpc_chunk", 2u << 20);
+    store_ = std::make_shared<ObjectStore>(get_or<bool>(d, "md5", true));
+    srv_ = std::make_unique<FakeGcsServer>(c, store_);
+  }
+  void start() { srv_->start(); }
+  void stop() {
+    py::gil_scoped_release nogil;
+    srv_->stop();
+  }
+  int port() const { return srv_->port(); }
+  std::string url() const { return srv_->url(); }
+  void add_synthetic(const std::string& bucket, const std::string& prefix, const std::string& suffix, int first,
+                     int count, uint64_t size) {
+    py::gil_scoped_release nogil;
+    store_->add_synthetic_range(bucket, prefix, suffix, first, count, size);
+  }
+  py::dict add_object(const std::string& bucket, const std::string& name, const py::bytes& data) {
+    std::string s = data;
+    auto o = store_->put(bucket, name, std::vector<uint8_t>(s.begin(), s.end()), "");
+    py::dict d;
+    d["size"] = o->size;
+    d["crc32c"] = o->crc32c;
+    d["generation"] = o->generation;
+    return d;
+  }
+  py::object object_info(const std::string& bucket, const std::string& name) {
+    auto o = store_->get(bucket, name);
+    if (!o) return py::none();
+    py::dict d;
+    d["size"] = o->size;
+    d["crc32c"] = o->crc32c;
+    d["md5"] = py::bytes(o->md5);
+    d["generation"] = o->generation;
+    d["synthetic"] = o->synthetic;
+    d["rotation"] = o->rot;
+    return d;
+  }
+  py::bytes object_bytes(const std::string& bucket, const std::string& name, uint64_t off, uint64_t n) {
+    auto o = store_->get(bucket, name);
+    if (!o) throw std::runtime_error("no such object");
+    if (off > o->size) off = o->size;
+    if (off + n > o->size) n = o->size - off;
+    std::string out;
+    out.resize(n);
+    uint64_t done = 0;
+    while (done < n) {
+      uint64_t k = std::min<uint64_t>(n - done, 8 << 20);
+      std::memcpy(&out[done], o->bytes(off + done, k), k);
+      done += k;
+    }
+    return py::bytes(out);
+  }
+  void set_faults(const py::dict& d) {
+    auto& f = srv_->faults();
+    if (d.contains("fail_next")) f.fail_next = d["fail_next"].cast<int>();
+    if (d.contains("fail_status")) f.fail_status = d["fail_status"].cast<int>();
+    if (d.contains("disconnect_at")) f.disconnect_at = d["disconnect_at"].cast<int64_t>();
+    if (d.contains("disconnect_count")) f.disconnect_count = d["disconnect_count"].cast<int>();
+    if (d.contains("corrupt_at")) f.corrupt_at = d["corrupt_at"].cast<int64_t>();
+    if (d.contains("corrupt_count")) f.corrupt_count = d["corrupt_count"].cast<int>();
+    if (d.contains("throttle_bps")) f.throttle_bps = d["throttle_bps"].cast<int64_t>();
+    if (d.contains("latency_ms")) f.latency_ms = d["latency_ms"].cast<int>();
+  }
+  py::dict stats() {
+    auto& s = srv_->stats();
+    py::dict d;
+    d["connections"] = s.connections.load();
+    d["http_requests"] = s.http_requests.load();
+    d["grpc_calls"] = s.grpc_calls.load();
+    d["bytes_sent"] = s.bytes_sent.load();
+    d["bytes_received"] = s.bytes_received.load();
+    d["faults_injected"] = s.faults_injected.load();
+    d["auth_failures"] = s.auth_failures.load();
+    return d;
+  }
+  std::string issue_token() { return srv_->issue_token(); }
+
+ private:
+  std::shared_ptr<ObjectStore> store_;
+  std::unique_ptr<FakeGcsServer> srv_;
+};
+
+const CrcTables& host_tables() {
+  static CrcTables* t = [] {
+    auto* x = new CrcTables();
+    build_crc_tables(x);
+    return x;
+  }();
+  return *t;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_native, m) {
+  m.doc() = "MI355X-native object-storage benchmark core (C++/HIP)";
+  py::register_exception<StorageError>(m, "StorageError");
+
+  m.def("crc32c", [](const py::bytes& b) {
+    std::string s = b;
+    return gcsb::crc32c(s.data(), s.size());
+  });
+  m.def("crc32c_extend", [](uint32_t crc, const py::bytes& b) {
+    std::string s = b;
+    return crc32c_extend(crc, s.data(), s.size());
+  });
+  m.def("crc32c_combine", &crc32c_combine);
+  m.def("crc32c_shift", &crc32c_shift);
+  m.def("crc32c_fixup", &crc32c_fixup);
+  m.def("crc32c_raw", [](const py::bytes& b) {
+    std::string s = b;
+    return crc32c_raw_update(0, s.data(), s.size());
+  });
+  m.def("crc32c_hw_available", &crc32c_hw_available);
+  m.def(
+      "emulate_gpu_crc32c",
+      [](const py::bytes& b, size_t misalign, uint32_t expected, bool check) {
+        std::string s = b;
+        std::vector<uint8_t> buf(s.size() + 64);
+        uint8_t* base = reinterpret_cast<uint8_t*>((reinterpret_cast<uintptr_t>(buf.data()) + 15) & ~uintptr_t(15));
+        uint8_t* p = base + (misalign % 16);
+        std::memcpy(p, s.data(), s.size());
+        CrcSegResult r = emulate_crc32c_segment(p, static_cast<uint32_t>(s.size()), host_tables(), expected, check);
+        return py::make_tuple(r.raw, r.crc, r.status);
+      },
+      py::arg("data"), py::arg("misalign") = 0, py::arg("expected") = 0, py::arg("check") = false);
+  m.def("object_rotation", &object_rotation);
+  m.def("object_bytes", [](const std::string& name, uint64_t off, uint64_t n) {
+    std::string out(n, '\0');
+    fill_object_bytes(reinterpret_cast<uint8_t*>(&out[0]), object_rotation(name), off, n);
+    return py::bytes(out);
+  });
+  m.def("object_crc32c", [](const std::string& name, uint64_t off, uint64_t n) {
+    return PatternBuffer::instance().crc32c_range(object_rotation(name), off, n);
+  });
+  m.def("pattern_len", [] { return kPatternLen; });
+  m.def("oc_latency_bounds_ms", [] {
+    return std::vector<double>(kOcLatencyBoundsMs, kOcLatencyBoundsMs + 34);
+  });
+  m.def("oc_bucket_index", &oc_bucket_index);
+  m.def("base64_encode", [](const py::bytes& b) { return base64_encode(std::string(b)); });
+  m.def("parse_goog_hash", [](const std::string& v) {
+    bool has = false;
+    uint32_t crc = 0;
+    std::string md5;
+    parse_goog_hash(v, &has, &crc, &md5);
+    return py::make_tuple(has, crc, py::bytes(md5));
+  });
+
+  m.def("rsa_generate", [] {
+    std::string a, b;
+    rsa_generate_pem(&a, &b);
+    return py::make_tuple(a, b);
+  });
+  m.def("get_access_token", [](const std::string& key_file, const std::string& token_uri) {
+    py::gil_scoped_release nogil;
+    auto ts = get_token_source(key_file, kScopeFullControl, token_uri);
+    return std::make_pair(ts->kind(), ts->token());
+  });
+  m.def("service_account_assertion", [](const std::string& key_json, const std::string& token_uri, int64_t now_s) {
+    ServiceAccountTokenSource ts(key_json, kScopeFullControl, token_uri);
+    return ts.build_assertion(now_s);
+  });
+
+  // GPU
+  m.def("gpu_device_count", &gpu_device_count);
+  m.def("gpu_crc32c", [](int dev, uintptr_t ptr, size_t n) {
+    py::gil_scoped_release nogil;
+    return gpu_crc32c(dev, reinterpret_cast<const void*>(ptr), n);
+  });
+  m.def("gpu_fill_pattern", [](int dev, uintptr_t ptr, uint64_t n, const std::string& name, uint64_t off) {
+    py::gil_scoped_release nogil;
+    gpu_fill_pattern(dev, reinterpret_cast<void*>(ptr), n, object_rotation(name), off);
+  });
+  m.def("gpu_verify_pattern", [](int dev, uintptr_t ptr, uint64_t n, const std::string& name, uint64_t off) {
+    uint64_t first = 0, bad = 0;
+    {
+      py::gil_scoped_release nogil;
+      bad = gpu_verify_pattern(dev, reinterpret_cast<const void*>(ptr), n, object_rotation(name), off, &first);
+    }
+    return py::make_tuple(bad, first);
+  });
+
+  py::class_<PyGpuSink>(m, "GpuSink")
+      .def(py::init([](const py::dict& d) {
+        auto* s = new PyGpuSink();
+        s->sink = std::make_unique<GpuSink>(gpu_from(d));
+        return s;
+      }))
+      .def("set_external_destination",
+           [](PyGpuSink& s, uintptr_t ptr, size_t cap) { s.sink->set_external_destination(reinterpret_cast<void*>(ptr), cap); })
+      .def_property_readonly("device_ptr", [](PyGpuSink& s) { return reinterpret_cast<uintptr_t>(s.sink->object_device_ptr()); })
+      .def_property_readonly("capacity", [](PyGpuSink& s) { return s.sink->object_capacity(); })
+      .def("stats", [](PyGpuSink& s) { return gpu_stats_dict(s.sink->stats()); });
+
+  py::class_<PyClient>(m, "Client")
+      .def(py::init<const py::dict&>())
+      .def("read", &PyClient::read, py::arg("bucket"), py::arg("name"), py::arg("sink") = "discard",
+           py::arg("host_crc") = true, py::arg("offset") = 0, py::arg("limit") = -1)
+      .def("read_gpu", &PyClient::read_gpu, py::arg("bucket"), py::arg("name"), py::arg("sink"), py::arg("offset") = 0,
+           py::arg("limit") = -1)
+      .def("read_bytes", &PyClient::read_bytes, py::arg("bucket"), py::arg("name"), py::arg("offset") = 0,
+           py::arg("limit") = -1)
+      .def("stat", &PyClient::stat)
+      .def("list", &PyClient::list, py::arg("bucket"), py::arg("prefix") = "", py::arg("page_size") = 1000,
+           py::arg("page_token") = "", py::arg("delimiter") = "")
+      .def("list_all", &PyClient::list_all, py::arg("bucket"), py::arg("prefix") = "", py::arg("page_size") = 1000)
+      .def("write_bytes", &PyClient::write_bytes, py::arg("bucket"), py::arg("name"), py::arg("data"),
+           py::arg("resumable") = true, py::arg("chunk_bytes") = 16u << 20)
+      .def("stats", &PyClient::stats);
+
+  py::class_<PyRunner>(m, "Runner")
+      .def(py::init<const py::dict&>())
+      .def("start", &PyRunner::start)
+      .def("wait", &PyRunner::wait)
+      .def("stop", &PyRunner::stop)
+      .def("drain", &PyRunner::drain)
+      .def("summary", &PyRunner::summary)
+      .def("object_for", &PyRunner::object_for);
+
+  py::class_<PyServer>(m, "Server")
+      .def(py::init<const py::dict&>())
+      .def("start", &PyServer::start)
+      .def("stop", &PyServer::stop)
+      .def_property_readonly("port", &PyServer::port)
+      .def_property_readonly("url", &PyServer::url)
+      .def("add_synthetic", &PyServer::add_synthetic, py::arg("bucket"), py::arg("prefix"), py::arg("suffix") = "",
+           py::arg("first") = 0, py::arg("count") = 1, py::arg("size") = 1 << 20)
+      .def("add_object", &PyServer::add_object)
+      .def("object_info", &PyServer::object_info)
+      .def("object_bytes", &PyServer::object_bytes)
+      .def("set_faults", &PyServer::set_faults)
+      .def("stats", &PyServer::stats)
+      .def("issue_token", &PyServer::issue_token);
+}

@@ -1,0 +1,99 @@
+#include "server/fakegcs.h"
+
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstring>
+
+#include "core/util.h"
+#include "net/buffered.h"
+
+namespace gcsb {
+
+FakeGcsServer::FakeGcsServer(ServerConfig cfg, std::shared_ptr<ObjectStore> store)
+    : cfg_(std::move(cfg)), store_(std::move(store)) {}
+
+FakeGcsServer::~FakeGcsServer() { stop(); }
+
+void FakeGcsServer::start() {
+  listener_ = std::make_unique<Listener>(cfg_.host, cfg_.port);
+  port_ = listener_->port();
+  stopping_ = false;
+  accept_thread_ = std::thread([this] { accept_loop(); });
+}
+
+void FakeGcsServer::stop() {
+  if (!listener_) return;
+  stopping_ = true;
+  listener_->close();
+  if (accept_thread_.joinable()) accept_thread_.join();
+  {
+    std::lock_guard<std::mutex> lk(conns_mu_);
+    for (int fd : conn_fds_) ::shutdown(fd, SHUT_RDWR);
+  }
+  // connection threads are detached; wait for them to drain
+  for (int i = 0; i < 5000 && live_threads_.load() > 0; ++i)
+    std::this_thread::sleep_for(std::chrono::milliseconds(2));
+  listener_.reset();
+}
+
+void FakeGcsServer::accept_loop() {
+  for (;;) {
+    int fd = listener_->accept_fd();
+    if (fd < 0) break;
+    if (stopping_) {
+      ::close(fd);
+      break;
+    }
+    ++stats_.connections;
+    {
+      std::lock_guard<std::mutex> lk(conns_mu_);
+      conn_fds_.insert(fd);
+    }
+    ++live_threads_;
+    std::thread([this, fd] {
+      try {
+        handle_conn(fd);
+      } catch (...) {
+      }
+      {
+        std::lock_guard<std::mutex> lk(conns_mu_);
+        conn_fds_.erase(fd);
+      }
+      --live_threads_;
+    }).detach();
+  }
+}
+
+void FakeGcsServer::handle_conn(int fd) {
+  SocketOptions so;
+  so.sndbuf = cfg_.sndbuf;
+  so.rcvbuf = 4 << 20;
+  auto bc = std::make_unique<BufferedConn>(Conn::adopt(fd, so));
+  char peek[3];
+  ssize_t k = 0;
+  for (int tries = 0; tries < 1000; ++tries) {
+    k = ::recv(fd, peek, 3, MSG_PEEK | MSG_WAITALL);
+    if (k == 3 || k <= 0) break;
+  }
+  if (k != 3) return;
+  if (std::memcmp(peek, "PRI", 3) == 0)
+    serve_h2(std::move(bc));
+  else
+    serve_http1(std::move(bc));
+}
+
+std::string FakeGcsServer::issue_token() {
+  std::lock_guard<std::mutex> lk(tok_mu_);
+  std::string t = "ya29.fake-" + std::to_string(++tok_seq_) + "-" + std::to_string(wall_ns() % 100000007);
+  tokens_.insert(t);
+  return t;
+}
+
+bool FakeGcsServer::token_valid(const std::string& tok) {
+  std::lock_guard<std::mutex> lk(tok_mu_);
+  return tokens_.count(tok) > 0;
+}
+
+}  // namespace gcsb

@@ -1,0 +1,86 @@
+// Synthetic GCS endpoint: HTTP/1.1 (XML + JSON media, JSON metadata/list,
+// resumable/simple uploads, OAuth token + metadata-server token endpoints) and
+// h2c gRPC (google.storage.v2.Storage) on ONE loopback port, sniffed by the
+// connection preface.  Fault injection covers the failure classes the
+// reference's retry policy exists for (reference main.go:179-184): 429/503
+// bursts, mid-stream disconnects, corrupted bytes (CRC failures), slow drip.
+#pragma once
+#include <atomic>
+#include <memory>
+#include <mutex>
+#include <set>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "net/socket.h"
+#include "server/store.h"
+
+namespace gcsb {
+
+struct FaultConfig {
+  std::atomic<int> fail_next{0};            // fail the next N data requests...
+  std::atomic<int> fail_status{503};        // ...with this HTTP status (gRPC: mapped code)
+  std::atomic<int64_t> disconnect_at{-1};   // cut the connection after this many body bytes...
+  std::atomic<int> disconnect_count{0};     // ...this many times
+  std::atomic<int64_t> corrupt_at{-1};      // flip one byte at this object offset...
+  std::atomic<int> corrupt_count{0};        // ...in this many responses
+  std::atomic<int64_t> throttle_bps{0};     // per-response rate cap (bytes/s), 0 = none
+  std::atomic<int> latency_ms{0};           // added time-to-first-byte
+};
+
+struct ServerConfig {
+  std::string host = "127.0.0.1";
+  int port = 0;  // 0 = ephemeral
+  bool require_auth = false;
+  std::string jwt_public_key_pem;  // verify JWT assertions at /token if set
+  uint64_t grpc_chunk = 2 << 20;   // ReadObjectResponse content bytes per message (reference main.go:123-124)
+  int sndbuf = 8 << 20;
+};
+
+struct ServerStats {
+  std::atomic<uint64_t> connections{0}, http_requests{0}, grpc_calls{0}, bytes_sent{0}, bytes_received{0},
+      faults_injected{0}, auth_failures{0};
+};
+
+class FakeGcsServer {
+ public:
+  FakeGcsServer(ServerConfig cfg, std::shared_ptr<ObjectStore> store);
+  ~FakeGcsServer();
+  void start();
+  void stop();
+  int port() const { return port_; }
+  std::string url() const { return "http://" + cfg_.host + ":" + std::to_string(port_); }
+  ObjectStore& store() { return *store_; }
+  FaultConfig& faults() { return faults_; }
+  ServerStats& stats() { return stats_; }
+  const ServerConfig& config() const { return cfg_; }
+  // Tokens issued by /token and the metadata endpoint (checked when require_auth).
+  std::string issue_token();
+  bool token_valid(const std::string& tok);
+
+  // Connection handlers (server_http1.cc / server_grpc.cc).
+  void serve_http1(std::unique_ptr<class BufferedConn> bc);
+  void serve_h2(std::unique_ptr<class BufferedConn> bc);
+
+ private:
+  void accept_loop();
+  void handle_conn(int fd);
+  ServerConfig cfg_;
+  std::shared_ptr<ObjectStore> store_;
+  FaultConfig faults_;
+  ServerStats stats_;
+  std::unique_ptr<Listener> listener_;
+  int port_ = 0;
+  std::thread accept_thread_;
+  std::atomic<bool> stopping_{false};
+  std::mutex conns_mu_;
+  std::set<int> conn_fds_;
+  std::vector<std::thread> conn_threads_;
+  std::atomic<int> live_threads_{0};
+  std::mutex tok_mu_;
+  std::set<std::string> tokens_;
+  uint64_t tok_seq_ = 0;
+};
+
+}  // namespace gcsb

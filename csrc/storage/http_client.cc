@@ -1,0 +1,285 @@
+// HTTP transport for the storage client: XML API media reads (the library's
+// default read path), JSON API reads (alt=media), JSON
+// metadata/list, and resumable / single-request uploads.
+#include <cstring>
+
+#include "core/json.h"
+#include "core/util.h"
+#include "http1/http1.h"
+#include "storage/client.h"
+
+namespace gcsb {
+namespace {
+
+bool http_retryable(int status) { return status == 408 || status == 429 || status >= 500; }
+
+ObjectMeta meta_from_json(const Json& j) {
+  ObjectMeta m;
+  m.name = j.get_string("name");
+  m.bucket = j.get_string("bucket");
+  m.size = j.get_int("size");
+  m.generation = j.get_int("generation");
+  m.metageneration = j.get_int("metageneration", 1);
+  if (const Json* c = j.get("crc32c"); c && c->is_string()) m.has_crc32c = crc32c_from_b64(c->as_string(), &m.crc32c);
+  if (const Json* h = j.get("md5Hash"); h && h->is_string()) base64_decode(h->as_string(), &m.md5);
+  m.content_type = j.get_string("contentType");
+  m.updated = j.get_string("updated");
+  return m;
+}
+
+[[noreturn]] void throw_status(int status, const std::string& what, const std::string& body) {
+  std::string msg = what + ": HTTP " + std::to_string(status);
+  if (!body.empty()) msg += ": " + body.substr(0, 512);
+  if (status == 404) msg = "storage: object doesn't exist (" + what + ")";
+  throw StorageError(msg, http_retryable(status), status);
+}
+
+class HttpStorageClient : public StorageClient {
+ public:
+  explicit HttpStorageClient(const ClientConfig& cfg)
+      : StorageClient(cfg),
+        pool_(cfg.endpoint, cfg.sock, cfg.protocol == "http2" ? 0 : cfg.max_conns_per_host,
+              cfg.protocol == "http2" ? 0 : cfg.max_idle_conns_per_host),
+        ua_(cfg.user_agent) {
+    // Decorator order mirrors the reference: oauth2.Transport wraps the base
+    // transport, the User-Agent tripper wraps that (main.go:89-101).
+    if (cfg.token) {
+      auth_ = std::make_unique<AuthDecorator>(cfg.token);
+      decorators_.push_back(auth_.get());
+    }
+    decorators_.push_back(&ua_);
+  }
+
+  std::string transport_name() const override { return "http1"; }
+
+ protected:
+  void read_attempt(const std::string& bucket, const std::string& object, Sink& sink, int64_t offset, int64_t limit,
+                    bool first_attempt, ReadResult* rr, uint64_t* delivered) override {
+    Http1Exchange ex(pool_, decorators_);
+    Headers h;
+    if (offset > 0 || limit >= 0) {
+      std::string r = "bytes=" + std::to_string(offset) + "-";
+      if (limit >= 0) r += std::to_string(offset + limit - 1);
+      h.emplace_back("Range", r);
+    }
+    h.emplace_back("x-goog-api-client", "gccl/1.33.0 gcsb-native");
+    std::string path;
+    if (cfg_.http_api == "json")
+      path = "/storage/v1/b/" + url_encode(bucket) + "/o/" + url_encode(object) + "?alt=media";
+    else
+      path = "/" + bucket + "/" + url_encode(object, true);
+    const HttpResponseHead& head = ex.send("GET", path, h);
+    if (head.status != 200 && head.status != 206) {
+      std::string body = ex.read_body_string(1 << 20);
+      throw_status(head.status, "GET " + bucket + "/" + object, body);
+    }
+    ObjectInfo info;
+    info.start_offset = offset;
+    if (const auto* g = head.get("x-goog-generation")) info.generation = std::stoll(*g);
+    for (const auto& kv : head.headers)
+      if (iequals(kv.first, "x-goog-hash")) parse_goog_hash(kv.second, &info.has_crc32c, &info.crc32c, &info.md5);
+    if (head.status == 206) {
+      if (const auto* cr = head.get("Content-Range")) {
+        size_t slash = cr->find('/');
+        if (slash != std::string::npos && (*cr)[slash + 1] != '*') info.size = std::stoll(cr->substr(slash + 1));
+      }
+    } else if (head.content_length >= 0) {
+      info.size = head.content_length;
+    }
+    if (const auto* sl = head.get("x-goog-stored-content-length"); sl && info.size < 0) info.size = std::stoll(*sl);
+    // A whole-object CRC only applies to a full read (the library skips the
+    // check for ranged reads).
+    bool full = offset == 0 && limit < 0 && head.status == 200;
+    if (first_attempt) {
+      ObjectInfo bi = info;
+      if (!full) bi.has_crc32c = false;
+      sink.begin(bi);
+      rr->sink_begun = true;
+      rr->info = info;
+    }
+    if (head.status == 200 && offset > 0) {
+      // server ignored Range: skip what we already have
+      uint8_t tmp[65536];
+      int64_t skip = offset;
+      while (skip > 0) {
+        size_t r = ex.read_body(tmp, skip < 65536 ? static_cast<size_t>(skip) : 65536);
+        if (r == 0) throw StorageError("short body while skipping", true);
+        skip -= static_cast<int64_t>(r);
+      }
+    }
+    const size_t chunk = cfg_.read_chunk;
+    for (;;) {
+      Window w = sink.acquire(chunk);
+      size_t cap = w.cap < chunk ? w.cap : chunk;
+      size_t r = ex.read_body(w.ptr, cap);
+      if (r == 0) break;
+      if (!rr->first_byte_ns) rr->first_byte_ns = now_ns();
+      sink.commit(r);
+      *delivered += r;
+    }
+    ex.close();
+  }
+
+  ObjectMeta stat_attempt(const std::string& bucket, const std::string& object) override {
+    Http1Exchange ex(pool_, decorators_);
+    ex.send("GET", "/storage/v1/b/" + url_encode(bucket) + "/o/" + url_encode(object), {});
+    std::string body = ex.read_body_string();
+    if (ex.head().status != 200) throw_status(ex.head().status, "stat " + bucket + "/" + object, body);
+    ex.close();
+    return meta_from_json(Json::parse(body));
+  }
+
+  ListResult list_attempt(const std::string& bucket, const std::string& prefix, int page_size,
+                          const std::string& page_token, const std::string& delimiter) override {
+    std::string q = "/storage/v1/b/" + url_encode(bucket) + "/o?maxResults=" + std::to_string(page_size);
+    if (!prefix.empty()) q += "&prefix=" + url_encode(prefix);
+    if (!page_token.empty()) q += "&pageToken=" + url_encode(page_token);
+    if (!delimiter.empty()) q += "&delimiter=" + url_encode(delimiter);
+    Http1Exchange ex(pool_, decorators_);
+    ex.send("GET", q, {});
+    std::string body = ex.read_body_string();
+    if (ex.head().status != 200) throw_status(ex.head().status, "list " + bucket, body);
+    ex.close();
+    Json j = Json::parse(body);
+    ListResult r;
+    if (const Json* items = j.get("items"))
+      for (const auto& it : items->items()) r.objects.push_back(meta_from_json(it));
+    if (const Json* pf = j.get("prefixes"))
+      for (const auto& p : pf->items()) r.prefixes.push_back(p.as_string());
+    r.next_page_token = j.get_string("nextPageToken");
+    return r;
+  }
+
+  ObjectMeta write_impl(const std::string& bucket, const std::string& object, ByteSource& src,
+                        const WriteOptions& opt) override {
+    const uint64_t total = src.size();
+    Json md = Json::object();
+    md.set("name", Json::str(object));
+    md.set("contentType", Json::str(opt.content_type));
+    if (src.has_crc32c()) md.set("crc32c", Json::str(crc32c_b64(src.crc32c())));
+    auto stream_body = [&](Conn& c, uint64_t n) {
+      while (n > 0) {
+        auto [p, k] = src.next(n < (8u << 20) ? static_cast<size_t>(n) : (8u << 20));
+        if (k == 0) throw StorageError("upload source ended early", false);
+        c.write_all(p, k);
+        n -= k;
+      }
+    };
+    if (!opt.resumable) {
+      return with_retry([&] {
+        src.seek(0);
+        Http1Exchange ex(pool_, decorators_);
+        std::string q = "/upload/storage/v1/b/" + url_encode(bucket) + "/o?uploadType=media&name=" + url_encode(object);
+        Headers h{{"Content-Type", opt.content_type}};
+        if (src.has_crc32c()) h.emplace_back("x-goog-hash", "crc32c=" + crc32c_b64(src.crc32c()));
+        ex.send_stream("POST", q, h, total, [&](Conn& c) { stream_body(c, total); });
+        std::string body = ex.read_body_string();
+        if (ex.head().status != 200) throw_status(ex.head().status, "upload " + object, body);
+        ex.close();
+        return meta_from_json(Json::parse(body));
+      });
+    }
+    // 1) initiate the resumable session
+    std::string session = with_retry([&] {
+      Http1Exchange ex(pool_, decorators_);
+      std::string q = "/upload/storage/v1/b/" + url_encode(bucket) + "/o?uploadType=resumable&name=" + url_encode(object);
+      std::string body = md.dump();
+      Headers h{{"Content-Type", "application/json; charset=UTF-8"},
+                {"X-Upload-Content-Type", opt.content_type},
+                {"X-Upload-Content-Length", std::to_string(total)}};
+      ex.send("POST", q, h, body.data(), body.size());
+      std::string rb = ex.read_body_string();
+      if (ex.head().status != 200) throw_status(ex.head().status, "start resumable upload", rb);
+      const std::string* loc = ex.head().get("Location");
+      if (!loc) throw StorageError("resumable upload: no Location header", false);
+      ex.close();
+      std::string l = *loc;
+      // accept absolute URLs: keep path+query
+      size_t sch = l.find("://");
+      if (sch != std::string::npos) {
+        size_t sl = l.find('/', sch + 3);
+        l = sl == std::string::npos ? "/" : l.substr(sl);
+        if (!pool_.endpoint().base_path.empty() && starts_with(l, pool_.endpoint().base_path))
+          l = l.substr(pool_.endpoint().base_path.size());
+      }
+      return l;
+    });
+    // 2) upload chunks; on failure query the persisted size and resume
+    const uint64_t chunk = std::max<uint64_t>(256 << 10, opt.chunk_bytes / (256 << 10) * (256 << 10));
+    uint64_t off = 0;
+    Backoff bo(cfg_.retry);
+    int64_t t0 = now_ns();
+    int attempt = 0;
+    for (;;) {
+      try {
+        uint64_t n = std::min<uint64_t>(chunk, total - off);
+        bool last = off + n == total;
+        std::string cr = total == 0 ? "bytes */0"
+                                    : "bytes " + std::to_string(off) + "-" + std::to_string(off + n - 1) + "/" +
+                                          (last ? std::to_string(total) : "*");
+        Http1Exchange ex(pool_, decorators_);
+        Headers h{{"Content-Range", cr}};
+        src.seek(off);
+        ex.send_stream("PUT", session, h, n, [&](Conn& c) { stream_body(c, n); });
+        std::string body = ex.read_body_string();
+        int st = ex.head().status;
+        if (st == 308) {
+          uint64_t persisted = 0;
+          if (const auto* rg = ex.head().get("Range")) {
+            size_t dash = rg->find('-');
+            if (dash != std::string::npos) persisted = std::stoull(rg->substr(dash + 1)) + 1;
+          }
+          ex.close();
+          off = persisted;
+          continue;
+        }
+        if (st == 200 || st == 201) {
+          ex.close();
+          return meta_from_json(Json::parse(body));
+        }
+        throw_status(st, "upload chunk", body);
+      } catch (const StorageError& e) {
+        ++attempt;
+        if (!e.retryable() || cfg_.retry.mode == RetryMode::kNever ||
+            (cfg_.retry.max_attempts > 0 && attempt >= cfg_.retry.max_attempts) ||
+            (cfg_.retry.max_total_s > 0 && (now_ns() - t0) / 1e9 > cfg_.retry.max_total_s))
+          throw;
+        ++stats_.retries;
+        sleep_seconds(bo.pause());
+        // query persisted size
+        try {
+          Http1Exchange ex(pool_, decorators_);
+          ex.send("PUT", session, {{"Content-Range", "bytes */" + std::to_string(total)}});
+          std::string body = ex.read_body_string();
+          if (ex.head().status == 200 || ex.head().status == 201) {
+            ex.close();
+            return meta_from_json(Json::parse(body));
+          }
+          uint64_t persisted = 0;
+          if (const auto* rg = ex.head().get("Range")) {
+            size_t dash = rg->find('-');
+            if (dash != std::string::npos) persisted = std::stoull(rg->substr(dash + 1)) + 1;
+          }
+          ex.close();
+          off = persisted;
+        } catch (const StorageError&) {
+          // keep `off`; next loop iteration retries
+        }
+      }
+    }
+  }
+
+ private:
+  Http1Pool pool_;
+  UserAgentDecorator ua_;
+  std::unique_ptr<AuthDecorator> auth_;
+  std::vector<RequestDecorator*> decorators_;
+};
+
+}  // namespace
+
+std::unique_ptr<StorageClient> make_http_client(const ClientConfig& cfg) {
+  return std::make_unique<HttpStorageClient>(cfg);
+}
+
+}  // namespace gcsb

@@ -1,0 +1,96 @@
+// Where an object's bytes go as they come off the wire.
+//
+// Reference: the timed loop copies the reader into io.Discard
+// (reference main.go:140) and relies on the storage library for CRC32C checks
+// (SURVEY.md C21).  Here the destination is pluggable:
+//   DiscardSink  — reference-equivalent CPU baseline (optional host CRC32C);
+//   GpuSink      — pinned host ring -> hipMemcpyAsync -> HBM, CRC32C verified by
+//                  the CDNA4 kernels (csrc/gpu/).
+// Transports drive the protocol below; every method runs on the thread that
+// owns the object's byte stream (worker thread for HTTP, connection reader
+// thread for multiplexed gRPC).
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <string>
+
+namespace gcsb {
+
+struct ObjectInfo {
+  int64_t size = -1;          // full object size, -1 if unknown
+  int64_t start_offset = 0;   // first byte delivered (range reads / resumes)
+  int64_t generation = 0;
+  bool has_crc32c = false;    // whole-object CRC32C (x-goog-hash / object_checksums)
+  uint32_t crc32c = 0;
+  std::string md5;            // raw 16 bytes if known
+};
+
+struct SinkResult {
+  uint64_t bytes = 0;
+  bool verified = false;      // a checksum was checked and matched
+  bool crc_mismatch = false;  // a checksum was checked and did NOT match
+  uint32_t computed_crc32c = 0;
+  std::string detail;
+  int64_t landed_ns = 0;      // steady-clock time the last byte was in its final memory
+};
+
+struct Window {
+  uint8_t* ptr = nullptr;
+  size_t cap = 0;
+};
+
+class Sink {
+ public:
+  virtual ~Sink() = default;
+  // A new object read starts (called once per read, before any byte).
+  virtual void begin(const ObjectInfo& info) = 0;
+  // Object metadata learned after begin (gRPC sends it in the first message).
+  virtual void update_info(const ObjectInfo& info) = 0;
+  // Writable memory for at least 1 byte; cap may be smaller than `want`.
+  virtual Window acquire(size_t want) = 0;
+  // `n` bytes were written at the start of the last acquired window.
+  virtual void commit(size_t n) = 0;
+  // gRPC ChecksummedData framing: a chunk of `len` content bytes follows...
+  virtual void chunk_begin(size_t len) { (void)len; }
+  // ...and ended; its crc32c if the message carried one.
+  virtual void chunk_end(bool has_crc, uint32_t crc) { (void)has_crc; (void)crc; }
+  // A retry resumes the stream at object offset `offset` (== bytes delivered).
+  virtual void resume_at(int64_t offset) { (void)offset; }
+  // All bytes delivered: wait for outstanding async work and verify.
+  virtual SinkResult finish() = 0;
+  // Abandon the current read (error path): drain async work, no verification.
+  virtual void abort() {}
+};
+
+// Reference-equivalent sink: bytes land in a reusable host buffer and are
+// dropped; CRC32C optionally computed on the host (what the Go library does
+// on full HTTP reads).
+class DiscardSink : public Sink {
+ public:
+  DiscardSink(size_t chunk_bytes, bool host_crc);
+  ~DiscardSink() override;
+  void begin(const ObjectInfo& info) override;
+  void update_info(const ObjectInfo& info) override;
+  Window acquire(size_t want) override;
+  void commit(size_t n) override;
+  void chunk_begin(size_t len) override;
+  void chunk_end(bool has_crc, uint32_t crc) override;
+  void resume_at(int64_t offset) override;
+  SinkResult finish() override;
+
+ private:
+  uint8_t* buf_;
+  size_t cap_;
+  bool host_crc_;
+  ObjectInfo info_;
+  uint64_t bytes_ = 0;
+  uint32_t obj_crc_ = 0;     // running standard crc of all delivered bytes
+  uint32_t chunk_crc_ = 0;
+  bool in_chunk_ = false;
+  bool chunk_partial_ = false;
+  bool mismatch_ = false;
+  bool any_checked_ = false;
+  std::string detail_;
+};
+
+}  // namespace gcsb

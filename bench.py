@@ -1,0 +1,174 @@
+#!/usr/bin/env python3
+"""Headline benchmark: whole-object reads from a (synthetic, loopback) GCS
+endpoint into MI355X HBM, one reader process per GPU.
+
+Metric (BASELINE.json): p50/p99 read latency (ms) + MB/s per GPU, HTTP vs gRPC
+at 1/2/4/8 MI355X.  Config: 256 MiB objects, gRPC ReadObject stream (HTTP with
+--protocol http), bytes land in HBM through the pinned ring + hipMemcpyAsync
+and every ChecksummedData CRC32C is verified by the CDNA4 kernels.
+
+One step = every rank's reader reads its own 256 MiB object (file_<rank>) once,
+so per-GPU work is fixed as N grows (weak scaling).  W untimed warmup reads,
+then K timed reads bracketed by an RCCL barrier + torch.cuda.synchronize();
+the elapsed time is the MAX over ranks and `value` is total bytes / that time.
+
+    python bench.py --gpus 1 --steps 20 --warmup 3
+    torchrun --nproc-per-node 8 bench.py --gpus 8 ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "p50/p99 read latency (ms) + MB/s per GPU; HTTP vs gRPC at 1/2/4/8 MI355X"
+
+
+def parse_size(s: str) -> int:
+    s = s.strip()
+    mult = {"k": 1 << 10, "kib": 1 << 10, "m": 1 << 20, "mib": 1 << 20, "g": 1 << 30, "gib": 1 << 30}
+    for suf in sorted(mult, key=len, reverse=True):
+        if s.lower().endswith(suf):
+            return int(float(s[: -len(suf)]) * mult[suf])
+    return int(s)
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--protocol", default="auto", help="grpc | http | auto (grpc when built)")
+    ap.add_argument("--object-size", default="256MiB")
+    ap.add_argument("--workers", type=int, default=1, help="readers per GPU (config: 1)")
+    ap.add_argument("--sink", default="gpu", help="gpu (HBM landing + GPU CRC) | discard (CPU baseline)")
+    ap.add_argument("--slot-bytes", default="8MiB")
+    ap.add_argument("--slots", type=int, default=4)
+    ap.add_argument("--grpc-pool", type=int, default=1)
+    ap.add_argument("--json-out", default="")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import custom_go_client_benchmark_amd as pkg
+    from custom_go_client_benchmark_amd.ops import hbm
+    from custom_go_client_benchmark_amd.parallel import dist as gdist
+
+    n = pkg._native
+    rank, world, local_rank = gdist.env_rank()
+    ctx = gdist.init(local_rank=local_rank, world=world, rank=rank)
+    use_gpu = args.sink == "gpu"
+    if use_gpu:
+        hbm.gpu_required()
+    protocol = args.protocol
+    if protocol == "auto":
+        protocol = "grpc" if "grpc" in hbm.available_protocols() else "http"
+    size = parse_size(args.object_size)
+
+    # Node-local synthetic GCS endpoint for this rank (no network on the box).
+    srv = n.Server({"port": 0, "md5": False})
+    srv.start()
+    bucket = "princer-working-dirs"
+    prefix = "princer_100M_files/file_"
+    first = rank * args.workers
+    srv.add_synthetic(bucket, prefix, "", first, args.workers, size)
+
+    cfg = {
+        "protocol": protocol,
+        "endpoint": srv.url,
+        "bucket": bucket,
+        "object_prefix": prefix,
+        "workers": args.workers,
+        "reads_per_worker": args.warmup,
+        "worker_id_offset": first,
+        "sink": args.sink,
+        "device": local_rank if use_gpu else 0,
+        "ring_slot_bytes": parse_size(args.slot_bytes),
+        "ring_slots": args.slots,
+        "landing": "object",
+        "grpc_conn_pool_size": args.grpc_pool,
+        "keep_records": False,
+        "retry_initial_s": 0.05,
+    }
+    run = n.Runner(cfg)
+    if args.warmup > 0:
+        run.start()
+        run.wait()
+        s = run.summary()
+        if s["errors"]:
+            print(f"[rank {rank}] warmup failed: {s['first_error']}", file=sys.stderr)
+            return 1
+    run.reset_stats()
+    run.set_reads_per_worker(args.steps)
+
+    gdist.barrier(ctx)
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run.start()
+    run.wait()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    gdist.barrier(ctx)
+    elapsed = time.perf_counter() - t0
+    s = run.summary()
+    srv.stop()
+
+    ok = 1.0 if s["errors"] == 0 and s["reads"] == args.steps * args.workers else 0.0
+    stats = gdist.reduce_stats(ctx, elapsed=elapsed, nbytes=float(s["bytes"]), ok=ok, p50=s["p50_ms"],
+                               p99=s["p99_ms"], host_p50=s["host_p50_ms"])
+    if rank == 0:
+        if stats["ok_min"] < 1.0:
+            print(f"benchmark failed: {s['first_error'] or 'incomplete reads'}", file=sys.stderr)
+            return 1
+        total = stats["nbytes_sum"]
+        tmax = stats["elapsed_max"]
+        value = total / tmax / (1 << 20)
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "MiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(tmax / args.steps * 1000.0, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "uint8",
+            "data": "synthetic",
+            "config": {
+                "model": f"{protocol} ReadObject {args.object_size} object -> HBM (CRC32C on GPU)"
+                if use_gpu else f"{protocol} read {args.object_size} -> discard (CPU baseline)",
+                "global_batch": world * args.workers,
+                "seq_len": size,
+                "parallelism": f"dp{world}",
+                "protocol": protocol,
+                "object_bytes": size,
+                "readers_per_gpu": args.workers,
+                "sink": args.sink,
+                "ring": f"{args.slots}x{args.slot_bytes}",
+            },
+            "per_gpu_mib_s": round(value / world, 2),
+            "p50_ms": round(stats["p50_max"], 3),
+            "p99_ms": round(stats["p99_max"], 3),
+            "host_landed_p50_ms": round(stats["host_p50_max"], 3),
+            "endpoint": "loopback synthetic GCS (one per rank)",
+        }
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    gdist.shutdown(ctx)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

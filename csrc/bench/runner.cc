@@ -48,10 +48,23 @@ std::string Runner::object_for(int worker, int64_t seq) const {
   return cfg_.object_prefix + std::to_string(cfg_.worker_id_offset + worker) + cfg_.object_suffix;
 }
 
+void Runner::reset_stats() {
+  std::lock_guard<std::mutex> lk(mu_);
+  acc_ = RunSummary();
+  lat_ms_.clear();
+  host_ms_.clear();
+  pending_.clear();
+  t_first_ = t_last_ = 0;
+}
+
 void Runner::start() {
   stop_flag_ = false;
   running_ = true;
-  gpu_stats_.assign(cfg_.workers, GpuSinkStats{});
+  if (sinks_.empty()) {
+    sinks_.resize(cfg_.workers);
+    gpu_sinks_.assign(cfg_.workers, nullptr);
+    gpu_stats_.assign(cfg_.workers, GpuSinkStats{});
+  }
   for (int w = 0; w < cfg_.workers; ++w) threads_.emplace_back([this, w] { worker_main(w); });
 }
 
@@ -85,15 +98,15 @@ void Runner::record(ReadRecord&& r, double ms, double host_ms) {
 }
 
 void Runner::worker_main(int w) {
-  std::unique_ptr<Sink> sink;
-  GpuSink* gsink = nullptr;
   try {
-    if (cfg_.sink == "gpu") {
-      auto g = std::make_unique<GpuSink>(cfg_.gpu);
-      gsink = g.get();
-      sink = std::move(g);
-    } else {
-      sink = std::make_unique<DiscardSink>(cfg_.client.read_chunk, cfg_.host_crc);
+    if (!sinks_[w]) {
+      if (cfg_.sink == "gpu") {
+        auto g = std::make_unique<GpuSink>(cfg_.gpu);
+        gpu_sinks_[w] = g.get();
+        sinks_[w] = std::move(g);
+      } else {
+        sinks_[w] = std::make_unique<DiscardSink>(cfg_.client.read_chunk, cfg_.host_crc);
+      }
     }
   } catch (const std::exception& e) {
     ReadRecord r;
@@ -105,6 +118,8 @@ void Runner::worker_main(int w) {
     if (cfg_.stop_on_error) stop_flag_ = true;
     return;
   }
+  Sink* sink = sinks_[w].get();
+  GpuSink* gsink = gpu_sinks_[w];
   std::mt19937_64 rng(cfg_.seed ? cfg_.seed + static_cast<uint64_t>(w) : std::random_device{}());
   const uint64_t sample_bound = cfg_.trace_sample_rate >= 1.0
                                     ? ~0ull

@@ -95,6 +95,10 @@ class Runner {
   RunSummary summary() const;
   // Per-worker object name (exposed for tests / CLI).
   std::string object_for(int worker, int64_t seq) const;
+  // Phased runs (bench warmup -> timed): sinks (pinned ring, HBM landing
+  // buffers) and connections survive between start()/wait() cycles.
+  void set_reads_per_worker(int64_t n) { cfg_.reads_per_worker = n; }
+  void reset_stats();
   StorageClient& client() { return *client_; }
 
  private:
@@ -112,6 +116,8 @@ class Runner {
   int64_t t_first_ = 0, t_last_ = 0;
   std::mutex out_mu_;
   std::vector<GpuSinkStats> gpu_stats_;
+  std::vector<std::unique_ptr<Sink>> sinks_;
+  std::vector<GpuSink*> gpu_sinks_;
 };
 
 }  // namespace gcsb

@@ -330,6 +330,8 @@ class PyRunner {
     return d;
   }
   std::string object_for(int w, int64_t seq) { return runner_->object_for(w, seq); }
+  void set_reads_per_worker(int64_t n) { runner_->set_reads_per_worker(n); }
+  void reset_stats() { runner_->reset_stats(); }
 
  private:
   std::unique_ptr<Runner> runner_;
@@ -560,7 +562,9 @@ PYBIND11_MODULE(_native, m) {
       .def("stop", &PyRunner::stop)
       .def("drain", &PyRunner::drain)
       .def("summary", &PyRunner::summary)
-      .def("object_for", &PyRunner::object_for);
+      .def("object_for", &PyRunner::object_for)
+      .def("set_reads_per_worker", &PyRunner::set_reads_per_worker)
+      .def("reset_stats", &PyRunner::reset_stats);
 
   py::class_<PyServer>(m, "Server")
       .def(py::init<const py::dict&>())

@@ -1,0 +1,59 @@
+"""CRC32C host algebra + bit-exact emulation of the GPU kernel algorithm."""
+import os
+import zlib
+
+import pytest
+
+
+def test_known_vectors(native):
+    assert native.crc32c(b"123456789") == 0xE3069283
+    assert native.crc32c(b"") == 0
+    assert native.crc32c(b"\x00" * 32) == 0x8A9136AA
+    assert native.crc32c(b"\xff" * 32) == 0x62A8AB43
+
+
+def test_extend_and_combine(native):
+    a, b = os.urandom(100001), os.urandom(777)
+    ca, cb = native.crc32c(a), native.crc32c(b)
+    assert native.crc32c_extend(ca, b) == native.crc32c(a + b)
+    assert native.crc32c_combine(ca, cb, len(b)) == native.crc32c(a + b)
+
+
+def test_raw_fixup_identity(native):
+    for n in [0, 1, 7, 4096, 123457]:
+        d = os.urandom(n)
+        assert native.crc32c_raw(d) ^ native.crc32c_fixup(n) == native.crc32c(d)
+
+
+def test_large_buffer_interleaved_path(native):
+    # > 3 * 8 KiB exercises the 3-stream interleave + shift-table recombine
+    d = os.urandom((1 << 20) + 12345)
+    c = 0
+    for i in range(0, len(d), 1000):
+        c = native.crc32c_extend(c, d[i : i + 1000])
+    assert native.crc32c(d) == c
+
+
+@pytest.mark.parametrize("misalign", [0, 1, 3, 8, 15])
+@pytest.mark.parametrize("n", [0, 1, 15, 16, 17, 4095, 4096, 4097, 65536 + 5, (1 << 20) + 3])
+def test_gpu_algorithm_emulation(native, misalign, n):
+    d = os.urandom(n)
+    want = native.crc32c(d)
+    raw, crc, status = native.emulate_gpu_crc32c(d, misalign, want, True)
+    assert crc == want and status == 1
+    assert raw == native.crc32c_raw(d)
+    _, _, bad = native.emulate_gpu_crc32c(d, misalign, want ^ 1, True)
+    assert bad == 2
+
+
+def test_emulation_multi_megabyte_tile_fold(native):
+    # > 256 tiles exercises the strided Horner (1 MiB shift) in K2
+    d = os.urandom(3 * (1 << 20) + 999)
+    raw, crc, _ = native.emulate_gpu_crc32c(d, 5, 0, False)
+    assert crc == native.crc32c(d)
+
+
+def test_goog_hash_parsing(native):
+    has, crc, md5 = native.parse_goog_hash("crc32c=4waSgw==,md5=XUFAKrxLKna5cZ2REBfFkg==")
+    assert has and crc == 0xE3069283
+    assert len(md5) == 16

@@ -1,0 +1,44 @@
+"""CDNA4 CRC32C kernels vs the host CRC32C (fp32-reference analogue: exact)."""
+import os
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("n", [0, 1, 15, 16, 17, 4095, 4096, 4097, 2 << 20, (2 << 20) + 13, 64 << 20])
+@pytest.mark.parametrize("misalign", [0, 1, 7, 15])
+def test_gpu_crc_matches_host(native, gpu_available, n, misalign):
+    import torch
+
+    data = os.urandom(n)
+    buf = torch.zeros(n + 64, dtype=torch.uint8, device="cuda:0")
+    if n:
+        buf[misalign : misalign + n] = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+    torch.cuda.synchronize()
+    got = native.gpu_crc32c(0, buf.data_ptr() + misalign, n)
+    assert got == native.crc32c(data)
+
+
+def test_gpu_crc_large_multi_segment(native, gpu_available):
+    import torch
+
+    n = (1 << 30) + 12345  # > 1 GiB: several kernel segments combined on host
+    t = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda:0")
+    host = t.cpu().numpy().tobytes()
+    assert native.gpu_crc32c(0, t.data_ptr(), n) == native.crc32c(host)
+
+
+def test_fill_and_verify_pattern(native, gpu_available):
+    import torch
+
+    name = "princer_100M_files/file_7"
+    n = (5 << 20) + 3
+    t = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+    native.gpu_fill_pattern(0, t.data_ptr(), n, name, 1000)
+    assert t.cpu().numpy().tobytes() == native.object_bytes(name, 1000, n)
+    bad, _ = native.gpu_verify_pattern(0, t.data_ptr(), n, name, 1000)
+    assert bad == 0
+    t[12345] ^= 0xFF
+    bad, first = native.gpu_verify_pattern(0, t.data_ptr(), n, name, 1000)
+    assert bad == 1 and first == 12345

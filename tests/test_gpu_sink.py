@@ -1,0 +1,81 @@
+"""Pinned ring -> hipMemcpyAsync -> HBM landing with GPU CRC32C verification."""
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+B = "princer-working-dirs"
+P = "princer_100M_files/file_"
+
+
+def _protocols(native):
+    from custom_go_client_benchmark_amd.ops import hbm
+
+    return hbm.available_protocols()
+
+
+@pytest.mark.parametrize("slot", [1 << 20, 3 << 20, 8 << 20])
+def test_read_into_tensor_byte_exact(native, server, gpu_available, slot):
+    import torch
+
+    size = (13 << 20) + 777
+    server.add_synthetic(B, P, "", 0, 1, size)
+    for proto in _protocols(native):
+        c = native.Client({"protocol": proto, "endpoint": server.url})
+        t = torch.empty(size, dtype=torch.uint8, device="cuda:0")
+        sink = native.GpuSink({"device": 0, "ring_slot_bytes": slot, "ring_slots": 3})
+        sink.set_external_destination(t.data_ptr(), t.numel())
+        for _ in range(2):  # reuse the sink across reads
+            r = c.read_gpu(B, P + "0", sink)
+            assert r["verified"] and not r["crc_mismatch"] and r["bytes"] == size, r
+            bad, first = native.gpu_verify_pattern(0, t.data_ptr(), size, P + "0", 0)
+            assert bad == 0, (proto, first)
+        assert t[:4096].cpu().numpy().tobytes() == native.object_bytes(P + "0", 0, 4096)
+
+
+def test_ring_landing_mode(native, server, gpu_available):
+    server.add_synthetic(B, P, "", 0, 1, 20 << 20)
+    c = native.Client({"protocol": "http", "endpoint": server.url})
+    sink = native.GpuSink({"device": 0, "ring_slot_bytes": 2 << 20, "ring_slots": 4, "landing": "ring"})
+    r = c.read_gpu(B, P + "0", sink)
+    assert r["verified"] and r["bytes"] == 20 << 20
+    assert sink.stats()["slots_submitted"] >= 10
+
+
+def test_gpu_detects_corruption(native, server, gpu_available):
+    server.add_synthetic(B, P, "", 0, 1, 6 << 20)
+    server.set_faults({"corrupt_at": (3 << 20) + 5, "corrupt_count": 1})
+    c = native.Client({"protocol": "http", "endpoint": server.url})
+    sink = native.GpuSink({"device": 0, "ring_slot_bytes": 1 << 20, "ring_slots": 2})
+    r = c.read_gpu(B, P + "0", sink)
+    assert r["crc_mismatch"] and not r["verified"]
+
+
+def test_gpu_resume_after_disconnect(native, server, gpu_available):
+    server.add_synthetic(B, P, "", 0, 1, 9 << 20)
+    server.set_faults({"disconnect_at": (4 << 20) + 100, "disconnect_count": 1})
+    c = native.Client({"protocol": "http", "endpoint": server.url, "retry_initial_s": 0.001})
+    sink = native.GpuSink({"device": 0, "ring_slot_bytes": 1 << 20, "ring_slots": 3})
+    r = c.read_gpu(B, P + "0", sink)
+    assert r["attempts"] == 2 and r["verified"]
+    bad, _ = native.gpu_verify_pattern(0, r["device_ptr"], 9 << 20, P + "0", 0)
+    assert bad == 0
+
+
+def test_runner_gpu_sink(native, server, gpu_available):
+    server.add_synthetic(B, P, "", 0, 4, 4 << 20)
+    run = native.Runner({"protocol": "http", "endpoint": server.url, "bucket": B, "workers": 4,
+                         "reads_per_worker": 3, "sink": "gpu", "ring_slot_bytes": 1 << 20})
+    run.start()
+    run.wait()
+    s = run.summary()
+    assert s["reads"] == 12 and s["errors"] == 0 and s["verified"] == 12, s
+    assert s["gpu"]["objects_verified"] == 12
+
+
+def test_hbm_helper_roundtrip(native, server, gpu_available):
+    from custom_go_client_benchmark_amd.ops import hbm
+
+    server.add_synthetic(B, P, "", 0, 1, 3 << 20)
+    c = native.Client({"protocol": "http", "endpoint": server.url})
+    t, r = hbm.read_object_to_tensor(c, B, P + "0")
+    assert r["verified"] and hbm.crc32c(t) == server.object_info(B, P + "0")["crc32c"]

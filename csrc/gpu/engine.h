@@ -94,11 +94,13 @@ class GpuSink : public Sink {
     size_t used = 0;
     uint64_t obj_off = 0;
     std::vector<SegInfo> segs;
-    hipEvent_t ev = nullptr;
+    hipEvent_t ev = nullptr;      // slot done: copy landed + CRC kernels finished
+    hipEvent_t copied = nullptr;  // copy landed (CRC stream waits on it)
     bool inflight = false;
     CrcSegResult* res = nullptr;  // host-mapped, kMaxSeg entries
   };
   void ensure_object_capacity(int64_t size);
+  void grow_object_buffer(uint64_t need);
   Slot& take_slot();
   void submit_current();
   void wait_slot(Slot& s);
@@ -107,7 +109,8 @@ class GpuSink : public Sink {
   void set_device() const;
 
   GpuSinkConfig cfg_;
-  hipStream_t stream_ = nullptr;
+  hipStream_t stream_ = nullptr;      // H2D copies
+  hipStream_t crc_stream_ = nullptr;  // CRC32C kernels
   std::vector<Slot> slots_;
   int cur_ = -1;         // FILLING slot index or -1
   int next_ = 0;         // next slot to take

@@ -1,6 +1,7 @@
 // GPU sink: pinned ring -> hipMemcpyAsync -> HBM + CRC32C kernels.  See engine.h.
 #include "gpu/engine.h"
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -34,7 +35,11 @@ GpuSink::GpuSink(const GpuSinkConfig& cfg) : cfg_(cfg) {
   cfg_.slot_bytes = (cfg_.slot_bytes + 4095) / 4096 * 4096;
   if (cfg_.slot_bytes < 65536) cfg_.slot_bytes = 65536;
   set_device();
+  // Two streams: back-to-back SDMA copies on one, CRC kernels on the other
+  // (each slot's kernels wait on that slot's copy event), so checksumming
+  // slot i overlaps the copy of slot i+1 instead of serializing behind it.
   hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
+  hip_check(hipStreamCreateWithFlags(&crc_stream_, hipStreamNonBlocking), "hipStreamCreate");
   d_tables_ = device_crc_tables(cfg_.device);
   tiles_cap_ = cfg_.slot_bytes / kCrcTile + 2 * kMaxSeg + 8;
   hip_check(hipMalloc(reinterpret_cast<void**>(&d_tiles_), tiles_cap_ * sizeof(uint32_t)), "hipMalloc(tiles)");
@@ -50,6 +55,7 @@ GpuSink::GpuSink(const GpuSinkConfig& cfg) : cfg_(cfg) {
     if (cfg_.landing == Landing::kRing)
       hip_check(hipMalloc(reinterpret_cast<void**>(&s.dev_ring), cfg_.slot_bytes), "hipMalloc(ring slot)");
     hip_check(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming), "hipEventCreate");
+    hip_check(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming), "hipEventCreate");
     s.res = res_host_ + static_cast<size_t>(i) * kMaxSeg;
   }
 }
@@ -58,13 +64,16 @@ GpuSink::~GpuSink() {
   try {
     set_device();
     if (stream_) (void)hipStreamSynchronize(stream_);
+    if (crc_stream_) (void)hipStreamSynchronize(crc_stream_);
   } catch (...) {
   }
   for (Slot& s : slots_) {
     if (s.host) (void)hipHostFree(s.host);
     if (s.dev_ring) (void)hipFree(s.dev_ring);
     if (s.ev) (void)hipEventDestroy(s.ev);
+    if (s.copied) (void)hipEventDestroy(s.copied);
   }
+  if (crc_stream_) (void)hipStreamDestroy(crc_stream_);
   if (res_host_) (void)hipHostFree(res_host_);
   if (d_tiles_) (void)hipFree(d_tiles_);
   if (own_obj_) (void)hipFree(own_obj_);
@@ -74,6 +83,7 @@ GpuSink::~GpuSink() {
 void GpuSink::set_external_destination(void* dptr, size_t cap) {
   set_device();
   hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+  hip_check(hipStreamSynchronize(crc_stream_), "hipStreamSynchronize");
   if (own_obj_) {
     (void)hipFree(own_obj_);
     own_obj_ = nullptr;
@@ -87,15 +97,28 @@ void GpuSink::ensure_object_capacity(int64_t size) {
   if (cfg_.landing != Landing::kObject || size < 0) return;
   uint64_t need = static_cast<uint64_t>(size) - static_cast<uint64_t>(info_.start_offset);
   if (need <= obj_cap_) return;
+  grow_object_buffer(need);
+}
+
+// Re-allocates the sink-owned HBM landing buffer, preserving the bytes that
+// already landed (gRPC learns the object size only from the first message's
+// metadata, after its content).  Happens once per sink: later reads reuse it.
+void GpuSink::grow_object_buffer(uint64_t need) {
   if (external_dst_)
-    throw StorageError("object (" + std::to_string(need) + " B) exceeds the external HBM destination (" +
-                           std::to_string(obj_cap_) + " B)",
-                       false);
+    throw StorageError("object larger than the external HBM destination (" + std::to_string(obj_cap_) + " B)", false);
   set_device();
+  for (int k = 0; k < cfg_.slots; ++k) wait_slot(slots_[(next_ + k) % cfg_.slots]);
   hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
-  if (own_obj_) hip_check(hipFree(own_obj_), "hipFree");
+  hip_check(hipStreamSynchronize(crc_stream_), "hipStreamSynchronize");
+  const uint64_t landed = cur_ >= 0 ? slots_[cur_].obj_off : delivered_;
   size_t cap = (need + (2u << 20) - 1) / (2u << 20) * (2u << 20);
-  hip_check(hipMalloc(reinterpret_cast<void**>(&own_obj_), cap), "hipMalloc(object landing)");
+  uint8_t* nb = nullptr;
+  hip_check(hipMalloc(reinterpret_cast<void**>(&nb), cap), "hipMalloc(object landing)");
+  if (own_obj_) {
+    if (landed) hip_check(hipMemcpy(nb, own_obj_, landed, hipMemcpyDeviceToDevice), "hipMemcpy(D2D grow)");
+    hip_check(hipFree(own_obj_), "hipFree");
+  }
+  own_obj_ = nb;
   obj_dst_ = own_obj_;
   obj_cap_ = cap;
 }
@@ -126,7 +149,7 @@ void GpuSink::update_info(const ObjectInfo& info) {
   if (info.generation) info_.generation = info.generation;
   if (info.size >= 0 && info_.size < 0) {
     info_.size = info.size;
-    if (delivered_ == 0) ensure_object_capacity(info.size);
+    ensure_object_capacity(info.size);
   }
 }
 
@@ -169,8 +192,10 @@ Window GpuSink::acquire(size_t want) {
   }
   size_t cap = cfg_.slot_bytes - s.used;
   if (cfg_.landing == Landing::kObject) {
-    if (delivered_ >= obj_cap_)
-      throw StorageError("object larger than its HBM landing buffer (" + std::to_string(obj_cap_) + " B)", false);
+    if (delivered_ >= obj_cap_) {
+      // size unknown so far (or larger than announced): grow, keeping landed bytes
+      grow_object_buffer(std::max<uint64_t>(2 * obj_cap_, delivered_ + cfg_.slot_bytes));
+    }
     if (obj_cap_ - delivered_ < cap) cap = obj_cap_ - delivered_;
   }
   // keep a segment below 4 GiB (32-bit length in the kernel batch)
@@ -263,10 +288,14 @@ void GpuSink::submit_current() {
     if (b.total_tiles > tiles_cap_) throw std::logic_error("CRC tile scratch too small");
     CrcSegResult* d_res = nullptr;
     hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_res), s.res, 0), "hipHostGetDevicePointer");
-    launch_crc32c_batch(b, d_tables_, d_tiles_, d_res, stream_);
+    hip_check(hipEventRecord(s.copied, stream_), "hipEventRecord");
+    hip_check(hipStreamWaitEvent(crc_stream_, s.copied, 0), "hipStreamWaitEvent");
+    launch_crc32c_batch(b, d_tables_, d_tiles_, d_res, crc_stream_);
     stats_.segments += s.segs.size();
+    hip_check(hipEventRecord(s.ev, crc_stream_), "hipEventRecord");
+  } else {
+    hip_check(hipEventRecord(s.ev, stream_), "hipEventRecord");
   }
-  hip_check(hipEventRecord(s.ev, stream_), "hipEventRecord");
   s.inflight = true;
   ++stats_.slots_submitted;
 }
@@ -337,7 +366,7 @@ SinkResult GpuSink::finish() {
       mismatch_ = true;
       char b[128];
       std::snprintf(b, sizeof(b), "bad CRC on read: got %08x want %08x", crc, info_.crc32c);
-      detail_ = b;
+      if (detail_.empty()) detail_ = b;  // keep the first (chunk-level) finding
     }
   } else if (cfg_.verify) {
     r.computed_crc32c = obj_raw_ ^ crc32c_fixup(obj_len_);

@@ -1,0 +1,184 @@
+#include "h2/h2.h"
+
+#include <sys/uio.h>
+
+#include <cstring>
+
+#include "core/util.h"
+
+namespace gcsb {
+
+const char h2::kPreface[25] = "PRI * HTTP/2.0\r\n\r\nSM\r\n\r\n";
+
+void encode_frame_header(uint8_t o[9], uint32_t len, uint8_t type, uint8_t flags, uint32_t stream) {
+  o[0] = static_cast<uint8_t>(len >> 16);
+  o[1] = static_cast<uint8_t>(len >> 8);
+  o[2] = static_cast<uint8_t>(len);
+  o[3] = type;
+  o[4] = flags;
+  o[5] = static_cast<uint8_t>((stream >> 24) & 0x7F);
+  o[6] = static_cast<uint8_t>(stream >> 16);
+  o[7] = static_cast<uint8_t>(stream >> 8);
+  o[8] = static_cast<uint8_t>(stream);
+}
+
+FrameHeader read_frame_header(BufferedConn& bc) {
+  uint8_t b[9];
+  bc.read_exact(b, 9);
+  FrameHeader h;
+  h.length = (uint32_t(b[0]) << 16) | (uint32_t(b[1]) << 8) | b[2];
+  h.type = b[3];
+  h.flags = b[4];
+  h.stream = be32(b + 5) & 0x7FFFFFFF;
+  return h;
+}
+
+std::string encode_settings(const std::vector<std::pair<uint16_t, uint32_t>>& kv) {
+  std::string s;
+  for (const auto& e : kv) {
+    s.push_back(static_cast<char>(e.first >> 8));
+    s.push_back(static_cast<char>(e.first));
+    uint8_t v[4];
+    put_be32(v, e.second);
+    s.append(reinterpret_cast<char*>(v), 4);
+  }
+  return s;
+}
+
+bool apply_settings_payload(const uint8_t* p, size_t n, H2Settings* s) {
+  if (n % 6) return false;
+  for (size_t i = 0; i < n; i += 6) {
+    uint16_t id = static_cast<uint16_t>((p[i] << 8) | p[i + 1]);
+    uint32_t v = be32(p + i + 2);
+    switch (id) {
+      case h2::kSettingsHeaderTableSize: s->header_table_size = v; break;
+      case h2::kSettingsEnablePush: s->enable_push = v; break;
+      case h2::kSettingsMaxConcurrentStreams: s->max_concurrent_streams = v; break;
+      case h2::kSettingsInitialWindowSize:
+        if (v > static_cast<uint32_t>(h2::kMaxWindow)) return false;
+        s->initial_window_size = v;
+        break;
+      case h2::kSettingsMaxFrameSize:
+        if (v < h2::kDefaultMaxFrame || v > h2::kMaxFrameLimit) return false;
+        s->max_frame_size = v;
+        break;
+      case h2::kSettingsMaxHeaderListSize: s->max_header_list_size = v; break;
+      default: break;  // unknown settings are ignored
+    }
+  }
+  return true;
+}
+
+void H2Writer::write_frame(uint8_t type, uint8_t flags, uint32_t stream, const void* p, size_t n) {
+  uint8_t hdr[9];
+  encode_frame_header(hdr, static_cast<uint32_t>(n), type, flags, stream);
+  iovec iov[2] = {{hdr, 9}, {const_cast<void*>(p), n}};
+  std::lock_guard<std::mutex> lk(wmu_);
+  conn_.writev_all(iov, n ? 2 : 1);
+}
+
+void H2Writer::write_frame_iov(uint8_t type, uint8_t flags, uint32_t stream, struct iovec* payload, int cnt,
+                               size_t total) {
+  uint8_t hdr[9];
+  encode_frame_header(hdr, static_cast<uint32_t>(total), type, flags, stream);
+  std::vector<iovec> iov(static_cast<size_t>(cnt) + 1);
+  iov[0] = {hdr, 9};
+  for (int i = 0; i < cnt; ++i) iov[static_cast<size_t>(i) + 1] = payload[i];
+  std::lock_guard<std::mutex> lk(wmu_);
+  conn_.writev_all(iov.data(), cnt + 1);
+}
+
+void H2Writer::write_headers(uint32_t stream, const std::string& block, bool end_stream) {
+  const size_t maxf = peer_max_frame_;
+  std::lock_guard<std::mutex> lk(wmu_);  // HEADERS+CONTINUATION must be contiguous
+  size_t off = 0;
+  bool first = true;
+  do {
+    size_t n = std::min(maxf, block.size() - off);
+    bool last = off + n == block.size();
+    uint8_t flags = (last ? h2::kFlagEndHeaders : 0) | (first && end_stream ? h2::kFlagEndStream : 0);
+    uint8_t hdr[9];
+    encode_frame_header(hdr, static_cast<uint32_t>(n), first ? h2::kHeaders : h2::kContinuation, flags, stream);
+    iovec iov[2] = {{hdr, 9}, {const_cast<char*>(block.data() + off), n}};
+    conn_.writev_all(iov, n ? 2 : 1);
+    off += n;
+    first = false;
+  } while (off < block.size());
+}
+
+void H2Writer::write_window_update(uint32_t stream, uint32_t inc) {
+  uint8_t v[4];
+  put_be32(v, inc & 0x7FFFFFFF);
+  write_frame(h2::kWindowUpdate, 0, stream, v, 4);
+}
+
+void H2Writer::write_rst(uint32_t stream, uint32_t code) {
+  uint8_t v[4];
+  put_be32(v, code);
+  write_frame(h2::kRstStream, 0, stream, v, 4);
+}
+
+void H2Writer::write_goaway(uint32_t last_stream, uint32_t code, const std::string& msg) {
+  std::string p(8, '\0');
+  put_be32(reinterpret_cast<uint8_t*>(&p[0]), last_stream & 0x7FFFFFFF);
+  put_be32(reinterpret_cast<uint8_t*>(&p[4]), code);
+  p += msg;
+  write_frame(h2::kGoaway, 0, 0, p.data(), p.size());
+}
+
+size_t H2Writer::reserve(uint32_t stream, size_t want) {
+  std::unique_lock<std::mutex> lk(fmu_);
+  for (;;) {
+    if (dead_) return 0;
+    auto it = stream_window_.find(stream);
+    if (it == stream_window_.end()) return 0;
+    int64_t avail = std::min(conn_window_, it->second);
+    if (avail > 0) {
+      size_t n = std::min<size_t>({want, static_cast<size_t>(avail), static_cast<size_t>(peer_max_frame_)});
+      conn_window_ -= static_cast<int64_t>(n);
+      it->second -= static_cast<int64_t>(n);
+      return n;
+    }
+    fcv_.wait(lk);
+  }
+}
+
+void H2Writer::register_stream(uint32_t stream) {
+  std::lock_guard<std::mutex> lk(fmu_);
+  stream_window_[stream] = peer_initial_window_;
+}
+
+void H2Writer::unregister_stream(uint32_t stream) {
+  std::lock_guard<std::mutex> lk(fmu_);
+  stream_window_.erase(stream);
+  fcv_.notify_all();
+}
+
+void H2Writer::on_window_update(uint32_t stream, uint32_t inc) {
+  std::lock_guard<std::mutex> lk(fmu_);
+  if (stream == 0) {
+    conn_window_ += inc;
+  } else {
+    auto it = stream_window_.find(stream);
+    if (it != stream_window_.end()) it->second += inc;
+  }
+  fcv_.notify_all();
+}
+
+void H2Writer::on_peer_settings(const H2Settings& s, uint32_t old_initial_window) {
+  std::lock_guard<std::mutex> lk(fmu_);
+  int64_t delta = static_cast<int64_t>(s.initial_window_size) - static_cast<int64_t>(old_initial_window);
+  if (delta)
+    for (auto& kv : stream_window_) kv.second += delta;
+  peer_initial_window_ = s.initial_window_size;
+  peer_max_frame_ = s.max_frame_size;
+  fcv_.notify_all();
+}
+
+void H2Writer::kill() {
+  std::lock_guard<std::mutex> lk(fmu_);
+  dead_ = true;
+  fcv_.notify_all();
+}
+
+}  // namespace gcsb

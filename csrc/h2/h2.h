@@ -1,0 +1,129 @@
+// HTTP/2 (RFC 9113) framing, flow control and connection state shared by the
+// native gRPC client (storage/grpc_client.cc) and the fake server
+// (server/server_grpc.cc).  Cleartext h2 with prior knowledge ("h2c"), which
+// is what a loopback/DirectPath-style endpoint speaks.
+//
+// Reference: grpc-go's transport (go.mod:20) multiplexes every worker's
+// ReadObject stream over ONE HTTP/2 connection when the pool size is 1
+// (reference main.go:30,111; SURVEY.md §3.3 "the key contention point").
+#pragma once
+#include <condition_variable>
+#include <cstdint>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "h2/hpack.h"
+#include "net/buffered.h"
+
+namespace gcsb {
+
+namespace h2 {
+constexpr uint8_t kData = 0x0, kHeaders = 0x1, kPriority = 0x2, kRstStream = 0x3, kSettings = 0x4,
+                  kPushPromise = 0x5, kPing = 0x6, kGoaway = 0x7, kWindowUpdate = 0x8, kContinuation = 0x9;
+constexpr uint8_t kFlagEndStream = 0x1, kFlagAck = 0x1, kFlagEndHeaders = 0x4, kFlagPadded = 0x8,
+                  kFlagPriority = 0x20;
+constexpr uint16_t kSettingsHeaderTableSize = 1, kSettingsEnablePush = 2, kSettingsMaxConcurrentStreams = 3,
+                   kSettingsInitialWindowSize = 4, kSettingsMaxFrameSize = 5, kSettingsMaxHeaderListSize = 6;
+constexpr uint32_t kErrNoError = 0, kErrProtocol = 1, kErrInternal = 2, kErrFlowControl = 3, kErrCancel = 8,
+                   kErrRefusedStream = 7;
+constexpr int64_t kMaxWindow = 0x7FFFFFFF;
+constexpr uint32_t kDefaultWindow = 65535;
+constexpr uint32_t kDefaultMaxFrame = 16384;
+constexpr uint32_t kMaxFrameLimit = (1u << 24) - 1;
+extern const char kPreface[25];  // "PRI * HTTP/2.0\r\n\r\nSM\r\n\r\n"
+}  // namespace h2
+
+struct FrameHeader {
+  uint32_t length = 0;
+  uint8_t type = 0;
+  uint8_t flags = 0;
+  uint32_t stream = 0;
+};
+
+void encode_frame_header(uint8_t out[9], uint32_t len, uint8_t type, uint8_t flags, uint32_t stream);
+FrameHeader read_frame_header(BufferedConn& bc);
+
+struct H2Settings {
+  uint32_t header_table_size = 4096;
+  uint32_t enable_push = 1;
+  uint32_t max_concurrent_streams = 0xFFFFFFFF;
+  uint32_t initial_window_size = h2::kDefaultWindow;
+  uint32_t max_frame_size = h2::kDefaultMaxFrame;
+  uint32_t max_header_list_size = 0xFFFFFFFF;
+};
+
+// Payload of a SETTINGS frame.
+std::string encode_settings(const std::vector<std::pair<uint16_t, uint32_t>>& kv);
+
+// Per-direction connection machinery common to both roles: serialized
+// writes, peer settings, send-side flow-control windows.
+class H2Writer {
+ public:
+  explicit H2Writer(Conn& c) : conn_(c) {}
+  // Writes one frame (header + payload pieces) atomically w.r.t. other writers.
+  void write_frame(uint8_t type, uint8_t flags, uint32_t stream, const void* p, size_t n);
+  void write_frame_iov(uint8_t type, uint8_t flags, uint32_t stream, struct iovec* payload, int cnt, size_t total);
+  // Header block (HEADERS + CONTINUATION as needed).
+  void write_headers(uint32_t stream, const std::string& block, bool end_stream);
+  void write_window_update(uint32_t stream, uint32_t inc);
+  void write_rst(uint32_t stream, uint32_t code);
+  void write_goaway(uint32_t last_stream, uint32_t code, const std::string& msg);
+  void write_settings(const std::string& payload) { write_frame(h2::kSettings, 0, 0, payload.data(), payload.size()); }
+  void write_settings_ack() { write_frame(h2::kSettings, h2::kFlagAck, 0, nullptr, 0); }
+  void write_ping_ack(const uint8_t opaque[8]) { write_frame(h2::kPing, h2::kFlagAck, 0, opaque, 8); }
+
+  // --- send flow control ---------------------------------------------------
+  // Blocks until the connection and stream windows allow >=1 byte; returns
+  // how many bytes (<= want, <= peer max frame) may be sent now and debits
+  // them.  Returns 0 if the connection/stream is dead.
+  size_t reserve(uint32_t stream, size_t want);
+  void register_stream(uint32_t stream);
+  void unregister_stream(uint32_t stream);
+  void on_window_update(uint32_t stream, uint32_t inc);
+  void on_peer_settings(const H2Settings& s, uint32_t old_initial_window);
+  void kill();  // wake all waiters; further reserve() returns 0
+  uint32_t peer_max_frame() const { return peer_max_frame_; }
+  uint32_t peer_initial_window() const { return peer_initial_window_; }
+  Conn& conn() { return conn_; }
+
+ private:
+  Conn& conn_;
+  std::mutex wmu_;  // frame writes
+  std::mutex fmu_;  // flow control
+  std::condition_variable fcv_;
+  int64_t conn_window_ = h2::kDefaultWindow;
+  std::map<uint32_t, int64_t> stream_window_;
+  uint32_t peer_max_frame_ = h2::kDefaultMaxFrame;
+  uint32_t peer_initial_window_ = h2::kDefaultWindow;
+  bool dead_ = false;
+};
+
+// Receive-side window replenishment: credits consumed bytes back to the peer
+// in large batches (we advertise 2^31-1 windows, so this never throttles).
+class RecvWindow {
+ public:
+  explicit RecvWindow(int64_t threshold = 64 << 20) : threshold_(threshold) {}
+  // returns increment to send now (0 = nothing yet)
+  uint32_t consume(uint32_t n) {
+    pending_ += n;
+    if (pending_ >= threshold_) {
+      uint32_t inc = static_cast<uint32_t>(pending_);
+      pending_ = 0;
+      return inc;
+    }
+    return 0;
+  }
+
+ private:
+  int64_t threshold_;
+  int64_t pending_ = 0;
+};
+
+// Parses a SETTINGS payload into s (returns false on malformed payload).
+bool apply_settings_payload(const uint8_t* p, size_t n, H2Settings* s);
+
+}  // namespace gcsb

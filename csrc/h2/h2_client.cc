@@ -1,0 +1,260 @@
+#include "h2/h2_client.h"
+
+#include <sys/socket.h>
+#include <sys/uio.h>
+
+#include <cstring>
+
+#include "core/util.h"
+
+namespace gcsb {
+
+std::shared_ptr<H2ClientConn> H2ClientConn::dial(const Endpoint& ep, const H2ClientOptions& opt) {
+  std::shared_ptr<H2ClientConn> c(new H2ClientConn(ep, opt));
+  c->bc_ = std::make_unique<BufferedConn>(Conn::dial(ep, opt.sock));
+  c->w_ = std::make_unique<H2Writer>(c->bc_->conn());
+  c->dec_ = HpackDecoder(opt.header_table_size);
+  // connection preface + our SETTINGS + open the connection window wide
+  c->bc_->conn().write_all(h2::kPreface, 24);
+  c->w_->write_settings(encode_settings({{h2::kSettingsEnablePush, 0},
+                                          {h2::kSettingsInitialWindowSize, opt.initial_window},
+                                          {h2::kSettingsMaxFrameSize, opt.max_frame_size},
+                                          {h2::kSettingsHeaderTableSize, opt.header_table_size}}));
+  c->w_->write_window_update(0, static_cast<uint32_t>(h2::kMaxWindow - h2::kDefaultWindow));
+  c->reader_ = std::thread([raw = c.get()] { raw->reader_loop(); });
+  return c;
+}
+
+H2ClientConn::~H2ClientConn() { close(); }
+
+void H2ClientConn::close() {
+  if (!dead_.exchange(true)) {
+    try {
+      w_->write_goaway(0, h2::kErrNoError, "");
+    } catch (...) {
+    }
+  }
+  if (bc_) ::shutdown(bc_->conn().fd(), SHUT_RDWR);
+  if (w_) w_->kill();
+  if (reader_.joinable()) {
+    if (reader_.get_id() == std::this_thread::get_id())
+      reader_.detach();
+    else
+      reader_.join();
+  }
+}
+
+size_t H2ClientConn::active_streams() {
+  std::lock_guard<std::mutex> lk(mu_);
+  return streams_.size();
+}
+
+std::shared_ptr<H2ClientStream> H2ClientConn::find(uint32_t id) {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto it = streams_.find(id);
+  return it == streams_.end() ? nullptr : it->second;
+}
+
+void H2ClientConn::start_stream(const std::shared_ptr<H2ClientStream>& s, const HeaderList& headers,
+                                bool end_stream) {
+  std::string block;
+  enc_.encode(headers, &block);
+  std::lock_guard<std::mutex> olk(open_mu_);  // stream ids must hit the wire in order
+  if (!usable()) throw StorageError("http2 connection unusable: " + dead_reason_, true);
+  if (next_id_ > 0x7FFFFFF0) {
+    goaway_ = true;
+    throw StorageError("http2 stream ids exhausted", true);
+  }
+  s->id_ = next_id_;
+  next_id_ += 2;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    streams_[s->id_] = s;
+  }
+  w_->register_stream(s->id_);
+  try {
+    w_->write_headers(s->id_, block, end_stream);
+  } catch (const StorageError& e) {
+    dead_ = true;
+    throw;
+  }
+}
+
+void H2ClientConn::send_data(H2ClientStream& s, const uint8_t* p, size_t n, bool end_stream) {
+  iovec iov{const_cast<uint8_t*>(p), n};
+  send_data_iov(s, &iov, 1, end_stream);
+}
+
+void H2ClientConn::send_data_iov(H2ClientStream& s, struct iovec* iov, int cnt, bool end_stream) {
+  size_t total = 0;
+  for (int i = 0; i < cnt; ++i) total += iov[i].iov_len;
+  if (total == 0) {
+    if (end_stream) w_->write_frame(h2::kData, h2::kFlagEndStream, s.id_, nullptr, 0);
+    return;
+  }
+  int idx = 0;
+  size_t off = 0;  // offset inside iov[idx]
+  size_t left = total;
+  std::vector<iovec> piece;
+  while (left > 0) {
+    size_t n = w_->reserve(s.id_, left);
+    if (n == 0) throw StorageError("http2 stream closed while sending: " + dead_reason_, true);
+    piece.clear();
+    size_t need = n;
+    while (need > 0) {
+      size_t k = std::min(need, iov[idx].iov_len - off);
+      piece.push_back({static_cast<uint8_t*>(iov[idx].iov_base) + off, k});
+      need -= k;
+      off += k;
+      if (off == iov[idx].iov_len) {
+        ++idx;
+        off = 0;
+      }
+    }
+    left -= n;
+    w_->write_frame_iov(h2::kData, (left == 0 && end_stream) ? h2::kFlagEndStream : 0, s.id_, piece.data(),
+                        static_cast<int>(piece.size()), n);
+  }
+}
+
+void H2ClientConn::end_stream(H2ClientStream& s, bool reset) {
+  if (s.id_ == 0) return;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    streams_.erase(s.id_);
+  }
+  w_->unregister_stream(s.id_);
+  if (reset && usable()) {
+    try {
+      w_->write_rst(s.id_, h2::kErrCancel);
+    } catch (...) {
+    }
+  }
+}
+
+void H2ClientConn::fail_all(const std::string& msg) {
+  dead_ = true;
+  if (dead_reason_.empty()) dead_reason_ = msg;
+  w_->kill();
+  std::map<uint32_t, std::shared_ptr<H2ClientStream>> s;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    s.swap(streams_);
+  }
+  for (auto& kv : s) kv.second->on_conn_error(msg);
+}
+
+void H2ClientConn::reader_loop() {
+  std::string hblock;
+  uint32_t hstream = 0;
+  bool hend_stream = false;
+  try {
+    for (;;) {
+      FrameHeader fh = read_frame_header(*bc_);
+      if (fh.length > opt_.max_frame_size) throw StorageError("http2: frame exceeds max_frame_size", true);
+      switch (fh.type) {
+        case h2::kData: {
+          uint32_t n = fh.length;
+          uint8_t pad = 0;
+          if (fh.flags & h2::kFlagPadded) {
+            pad = bc_->read_byte();
+            n -= 1 + pad;
+          }
+          auto s = find(fh.stream);
+          bool end = fh.flags & h2::kFlagEndStream;
+          if (s) {
+            s->on_data(*bc_, n, end);
+          } else {
+            bc_->skip(n);
+          }
+          if (pad) bc_->skip(pad);
+          // replenish flow-control credit (connection + stream)
+          if (uint32_t inc = conn_recv_.consume(fh.length)) w_->write_window_update(0, inc);
+          if (s && !end)
+            if (uint32_t inc = s->recv_window_.consume(fh.length)) w_->write_window_update(fh.stream, inc);
+          break;
+        }
+        case h2::kHeaders:
+        case h2::kContinuation: {
+          std::string frag(fh.length, '\0');
+          if (fh.length) bc_->read_exact(&frag[0], fh.length);
+          size_t b = 0, e = frag.size();
+          if (fh.type == h2::kHeaders) {
+            hstream = fh.stream;
+            hend_stream = fh.flags & h2::kFlagEndStream;
+            hblock.clear();
+            if (fh.flags & h2::kFlagPadded) {
+              uint8_t pad = static_cast<uint8_t>(frag[0]);
+              b = 1;
+              e -= pad;
+            }
+            if (fh.flags & h2::kFlagPriority) b += 5;
+          }
+          hblock.append(frag, b, e - b);
+          if (fh.flags & h2::kFlagEndHeaders) {
+            HeaderList hl;
+            dec_.decode(reinterpret_cast<const uint8_t*>(hblock.data()), hblock.size(), &hl);
+            if (auto s = find(hstream)) s->on_headers(hl, hend_stream);
+          }
+          break;
+        }
+        case h2::kRstStream: {
+          uint8_t v[4];
+          bc_->read_exact(v, 4);
+          if (auto s = find(fh.stream)) s->on_reset(be32(v));
+          break;
+        }
+        case h2::kSettings: {
+          std::string p(fh.length, '\0');
+          if (fh.length) bc_->read_exact(&p[0], fh.length);
+          if (!(fh.flags & h2::kFlagAck)) {
+            uint32_t old = peer_.initial_window_size;
+            if (!apply_settings_payload(reinterpret_cast<const uint8_t*>(p.data()), p.size(), &peer_))
+              throw StorageError("http2: bad SETTINGS", true);
+            w_->on_peer_settings(peer_, old);
+            w_->write_settings_ack();
+          }
+          break;
+        }
+        case h2::kPing: {
+          uint8_t op[8];
+          bc_->read_exact(op, 8);
+          if (!(fh.flags & h2::kFlagAck)) w_->write_ping_ack(op);
+          break;
+        }
+        case h2::kGoaway: {
+          std::string p(fh.length, '\0');
+          bc_->read_exact(&p[0], fh.length);
+          goaway_last_ = be32(reinterpret_cast<const uint8_t*>(p.data())) & 0x7FFFFFFF;
+          goaway_ = true;
+          std::vector<std::shared_ptr<H2ClientStream>> doomed;
+          {
+            std::lock_guard<std::mutex> lk(mu_);
+            for (auto it = streams_.begin(); it != streams_.end();) {
+              if (it->first > goaway_last_) {
+                doomed.push_back(it->second);
+                it = streams_.erase(it);
+              } else {
+                ++it;
+              }
+            }
+          }
+          for (auto& s : doomed) s->on_conn_error("GOAWAY");
+          break;
+        }
+        case h2::kWindowUpdate: {
+          uint8_t v[4];
+          bc_->read_exact(v, 4);
+          w_->on_window_update(fh.stream, be32(v) & 0x7FFFFFFF);
+          break;
+        }
+        default:
+          bc_->skip(fh.length);  // PRIORITY, unknown extension frames
+      }
+    }
+  } catch (const std::exception& e) {
+    fail_all(e.what());
+  }
+}
+
+}  // namespace gcsb

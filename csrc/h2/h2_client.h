@@ -1,0 +1,84 @@
+// HTTP/2 client connection: one reader thread demultiplexes frames to
+// streams; any thread may open streams and send.  DATA payloads are handed to
+// the owning stream *on the socket* (the stream recv()s them straight into its
+// destination, e.g. a pinned ring slot), so a multiplexed connection still
+// copies each object byte exactly once.
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+
+#include "h2/h2.h"
+#include "net/socket.h"
+
+namespace gcsb {
+
+class H2ClientStream {
+ public:
+  virtual ~H2ClientStream() = default;
+  // Response headers or trailers (end_stream set on trailers / trailers-only).
+  virtual void on_headers(const HeaderList& h, bool end_stream) = 0;
+  // Must consume exactly n bytes from bc (already stripped of padding).
+  virtual void on_data(BufferedConn& bc, uint32_t n, bool end_stream) = 0;
+  virtual void on_reset(uint32_t code) = 0;
+  virtual void on_conn_error(const std::string& msg) = 0;
+  uint32_t id() const { return id_; }
+
+ private:
+  friend class H2ClientConn;
+  uint32_t id_ = 0;
+  RecvWindow recv_window_{16 << 20};
+};
+
+struct H2ClientOptions {
+  SocketOptions sock;
+  uint32_t initial_window = 0x7FFFFFFF;    // per-stream receive window we advertise
+  uint32_t max_frame_size = (1u << 24) - 1;  // largest DATA frame we accept
+  uint32_t header_table_size = 4096;
+};
+
+class H2ClientConn {
+ public:
+  static std::shared_ptr<H2ClientConn> dial(const Endpoint& ep, const H2ClientOptions& opt);
+  ~H2ClientConn();
+  // Registers the stream, assigns its id and sends the request headers.
+  // Throws StorageError(retryable) if the connection is unusable.
+  void start_stream(const std::shared_ptr<H2ClientStream>& s, const HeaderList& headers, bool end_stream);
+  // Sends request body bytes honouring flow control (blocks).
+  void send_data(H2ClientStream& s, const uint8_t* p, size_t n, bool end_stream);
+  void send_data_iov(H2ClientStream& s, struct iovec* iov, int cnt, bool end_stream);
+  // Forget a stream (RST_STREAM CANCEL if it is still open on our side).
+  void end_stream(H2ClientStream& s, bool reset);
+  bool usable() const { return !dead_.load() && !goaway_.load(); }
+  size_t active_streams();
+  const Endpoint& endpoint() const { return ep_; }
+  void close();
+
+ private:
+  H2ClientConn(Endpoint ep, H2ClientOptions opt) : ep_(std::move(ep)), opt_(opt) {}
+  void reader_loop();
+  void fail_all(const std::string& msg);
+  std::shared_ptr<H2ClientStream> find(uint32_t id);
+  Endpoint ep_;
+  H2ClientOptions opt_;
+  std::unique_ptr<BufferedConn> bc_;
+  std::unique_ptr<H2Writer> w_;
+  HpackDecoder dec_;
+  HpackEncoder enc_;
+  std::thread reader_;
+  std::mutex mu_;
+  std::map<uint32_t, std::shared_ptr<H2ClientStream>> streams_;
+  uint32_t next_id_ = 1;
+  std::mutex open_mu_;  // id allocation + HEADERS ordering
+  H2Settings peer_;
+  RecvWindow conn_recv_{64 << 20};
+  std::atomic<bool> dead_{false}, goaway_{false};
+  uint32_t goaway_last_ = 0x7FFFFFFF;
+  std::string dead_reason_;
+};
+
+}  // namespace gcsb

@@ -86,6 +86,7 @@ class Http1Exchange {
   // Release the connection (reusable iff the body was fully consumed).
   void close(bool force_drop = false);
   const HttpResponseHead& head() const { return head_; }
+  bool body_done() const { return body_done_; }
 
  private:
   size_t read_chunked(void* dst, size_t n);

@@ -12,6 +12,8 @@
 #include "core/util.h"
 #include "gpu/crc_types.h"
 #include "gpu/engine.h"
+#include "h2/hpack.h"
+#include "proto/storage_v2.h"
 #include "server/fakegcs.h"
 #include "storage/auth.h"
 #include "storage/client.h"
@@ -491,6 +493,85 @@ PYBIND11_MODULE(_native, m) {
     std::string md5;
     parse_goog_hash(v, &has, &crc, &md5);
     return py::make_tuple(has, crc, py::bytes(md5));
+  });
+
+  // HTTP/2 + protobuf codecs (exposed for interop / conformance tests)
+  m.attr("HAS_GRPC") = true;
+  m.def("huffman_encode", [](const py::bytes& b) { return py::bytes(huffman_encode(std::string(b))); });
+  m.def("huffman_decode", [](const py::bytes& b) {
+    std::string s = b, out;
+    if (!huffman_decode(reinterpret_cast<const uint8_t*>(s.data()), s.size(), &out))
+      throw std::runtime_error("bad huffman string");
+    return py::bytes(out);
+  });
+  m.def(
+      "hpack_encode",
+      [](const std::vector<std::pair<std::string, std::string>>& h, bool huffman) {
+        std::string out;
+        HpackEncoder(huffman).encode(h, &out);
+        return py::bytes(out);
+      },
+      py::arg("headers"), py::arg("huffman") = false);
+  m.def("hpack_decode_blocks", [](const std::vector<py::bytes>& blocks) {
+    HpackDecoder d;
+    std::vector<std::vector<std::pair<std::string, std::string>>> out;
+    for (const auto& b : blocks) {
+      std::string s = b;
+      HeaderList hl;
+      d.decode(reinterpret_cast<const uint8_t*>(s.data()), s.size(), &hl);
+      out.push_back(hl);
+    }
+    return out;
+  });
+  m.def("pb_read_request", [](const std::string& bucket, const std::string& object, int64_t off, int64_t lim) {
+    v2::ReadObjectRequest q;
+    q.bucket = v2::bucket_resource(bucket);
+    q.object = object;
+    q.read_offset = off;
+    q.read_limit = lim;
+    return py::bytes(v2::encode_read_request(q));
+  });
+  m.def("pb_read_response", [](const py::bytes& content, uint32_t crc, uint32_t obj_crc, int64_t size,
+                               const std::string& name) {
+    std::string c = content;
+    std::string cs = v2::encode_checksums(true, obj_crc, "");
+    v2::Object o;
+    o.name = name;
+    o.size = size;
+    o.bucket = "projects/_/buckets/b";
+    std::string meta = v2::encode_object(o);
+    v2::ContentRange cr;
+    cr.end = size;
+    cr.complete_length = size;
+    std::string rg = v2::encode_content_range(cr);
+    v2::ReadResponseFrame f = v2::encode_read_response(c.size(), true, crc, &cs, &rg, &meta);
+    return py::bytes(f.head + c + f.tail);
+  });
+  m.def("pb_write_request", [](const std::string& upload_id, const std::string& bucket, const std::string& name,
+                               int64_t off, const py::bytes& content, bool finish, uint32_t obj_crc) {
+    std::string c = content;
+    v2::WriteObjectSpec spec;
+    spec.resource.name = name;
+    spec.resource.bucket = v2::bucket_resource(bucket);
+    std::string sp = v2::encode_write_spec(spec);
+    std::string cs = v2::encode_checksums(true, obj_crc, "");
+    v2::WriteRequestParts p = v2::encode_write_request(upload_id, upload_id.empty() ? &sp : nullptr, off, c.size(),
+                                                       true, crc32c(c.data(), c.size()), finish ? &cs : nullptr,
+                                                       finish);
+    return py::bytes(p.head + c + p.tail);
+  });
+  m.def("pb_decode_object", [](const py::bytes& b) {
+    v2::Object o;
+    if (!v2::decode_object(std::string(b), &o)) throw std::runtime_error("bad Object");
+    py::dict d;
+    d["name"] = o.name;
+    d["bucket"] = o.bucket;
+    d["size"] = o.size;
+    d["generation"] = o.generation;
+    d["crc32c"] = o.crc32c;
+    d["has_crc32c"] = o.has_crc32c;
+    d["content_type"] = o.content_type;
+    return d;
   });
 
   m.def("rsa_generate", [] {

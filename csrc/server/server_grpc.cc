@@ -1,8 +1,619 @@
-// h2c gRPC front end of the synthetic GCS server (placeholder until the
-// HTTP/2 stack lands).
+// h2c gRPC front end of the synthetic GCS server: google.storage.v2.Storage
+// ReadObject (server streaming, 2 MiB ChecksummedData messages with per-message
+// CRC32C; metadata + object checksums on the first message), GetObject,
+// ListObjects, WriteObject (client streaming), StartResumableWrite,
+// QueryWriteStatus.  Content is sent zero-copy from the object store (writev).
+#include <sys/socket.h>
+#include <sys/uio.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <map>
+#include <set>
+#include <thread>
+
+#include "core/crc32c.h"
+#include "core/util.h"
+#include "h2/h2.h"
 #include "net/buffered.h"
+#include "proto/storage_v2.h"
 #include "server/fakegcs.h"
 
 namespace gcsb {
-void FakeGcsServer::serve_h2(std::unique_ptr<BufferedConn> bc) { bc->conn().close(); }
+namespace {
+
+enum GrpcCode {
+  kOk = 0, kInvalidArgument = 3, kNotFound = 5, kFailedPrecondition = 9, kOutOfRange = 11, kUnimplemented = 12,
+  kInternal = 13, kUnavailable = 14, kDataLoss = 15, kUnauthenticated = 16, kResourceExhausted = 8
+};
+
+struct ServerStream {
+  uint32_t id = 0;
+  HeaderList headers;
+  std::string path, authorization;
+  std::string buf;  // unparsed request bytes
+  std::vector<std::string> messages;
+  std::atomic<bool> cancelled{false};
+  bool half_closed = false;
+  RecvWindow rw{16 << 20};
+  // WriteObject state
+  std::shared_ptr<UploadSession> session;
+  bool write_error = false;
+  int write_code = 0;
+  std::string write_msg;
+  bool write_finished = false;
+  bool write_first = true;
+};
+
+struct Cancelled {};
+
+class H2ServerConn {
+ public:
+  H2ServerConn(FakeGcsServer& srv, BufferedConn& bc) : srv_(srv), bc_(bc), w_(bc.conn()) {}
+
+  ~H2ServerConn() {
+    w_.kill();
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [&] { return active_handlers_ == 0; });
+  }
+
+  void run() {
+    char preface[24];
+    bc_.read_exact(preface, 24);
+    if (std::memcmp(preface, h2::kPreface, 24) != 0) return;
+    w_.write_settings(encode_settings({{h2::kSettingsMaxConcurrentStreams, 1000},
+                                       {h2::kSettingsInitialWindowSize, 0x7FFFFFFF},
+                                       {h2::kSettingsMaxFrameSize, h2::kMaxFrameLimit}}));
+    w_.write_window_update(0, static_cast<uint32_t>(h2::kMaxWindow - h2::kDefaultWindow));
+    std::string hblock;
+    uint32_t hstream = 0;
+    bool hend = false;
+    try {
+      for (;;) {
+        FrameHeader fh = read_frame_header(bc_);
+        if (fh.length > h2::kMaxFrameLimit) break;
+        switch (fh.type) {
+          case h2::kHeaders:
+          case h2::kContinuation: {
+            std::string frag(fh.length, '\0');
+            if (fh.length) bc_.read_exact(&frag[0], fh.length);
+            size_t b = 0, e = frag.size();
+            if (fh.type == h2::kHeaders) {
+              hstream = fh.stream;
+              hend = fh.flags & h2::kFlagEndStream;
+              hblock.clear();
+              if (fh.flags & h2::kFlagPadded) {
+                b = 1;
+                e -= static_cast<uint8_t>(frag[0]);
+              }
+              if (fh.flags & h2::kFlagPriority) b += 5;
+            }
+            hblock.append(frag, b, e - b);
+            if (fh.flags & h2::kFlagEndHeaders) on_headers(hstream, hblock, hend);
+            break;
+          }
+          case h2::kData: {
+            uint32_t n = fh.length;
+            uint8_t pad = 0;
+            if (fh.flags & h2::kFlagPadded) {
+              pad = bc_.read_byte();
+              n -= 1 + pad;
+            }
+            auto s = find(fh.stream);
+            if (s) {
+              size_t old = s->buf.size();
+              s->buf.resize(old + n);
+              if (n) bc_.read_exact(&s->buf[old], n);
+              srv_.stats().bytes_received += n;
+            } else {
+              bc_.skip(n);
+            }
+            if (pad) bc_.skip(pad);
+            if (uint32_t inc = conn_rw_.consume(fh.length)) w_.write_window_update(0, inc);
+            if (s) {
+              if (uint32_t inc = s->rw.consume(fh.length)) w_.write_window_update(fh.stream, inc);
+              split_messages(*s);
+              if (s->path == "WriteObject") process_write_messages(*s);
+              if (fh.flags & h2::kFlagEndStream) dispatch(s);
+            }
+            break;
+          }
+          case h2::kRstStream: {
+            uint8_t v[4];
+            bc_.read_exact(v, 4);
+            if (auto s = find(fh.stream)) s->cancelled = true;
+            w_.unregister_stream(fh.stream);
+            break;
+          }
+          case h2::kSettings: {
+            std::string p(fh.length, '\0');
+            if (fh.length) bc_.read_exact(&p[0], fh.length);
+            if (!(fh.flags & h2::kFlagAck)) {
+              uint32_t old = peer_.initial_window_size;
+              if (!apply_settings_payload(reinterpret_cast<const uint8_t*>(p.data()), p.size(), &peer_)) return;
+              w_.on_peer_settings(peer_, old);
+              w_.write_settings_ack();
+            }
+            break;
+          }
+          case h2::kPing: {
+            uint8_t op[8];
+            bc_.read_exact(op, 8);
+            if (!(fh.flags & h2::kFlagAck)) w_.write_ping_ack(op);
+            break;
+          }
+          case h2::kWindowUpdate: {
+            uint8_t v[4];
+            bc_.read_exact(v, 4);
+            w_.on_window_update(fh.stream, be32(v) & 0x7FFFFFFF);
+            break;
+          }
+          case h2::kGoaway:
+            bc_.skip(fh.length);
+            return;
+          default:
+            bc_.skip(fh.length);
+        }
+      }
+    } catch (const std::exception&) {
+      // connection closed or protocol error: end of connection
+    }
+  }
+
+ private:
+  std::shared_ptr<ServerStream> find(uint32_t id) {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = streams_.find(id);
+    return it == streams_.end() ? nullptr : it->second;
+  }
+
+  void on_headers(uint32_t id, const std::string& block, bool end_stream) {
+    HeaderList hl;
+    dec_.decode(reinterpret_cast<const uint8_t*>(block.data()), block.size(), &hl);
+    auto existing = find(id);
+    if (existing) {  // trailers from the client: only END_STREAM matters
+      if (end_stream) dispatch(existing);
+      return;
+    }
+    auto s = std::make_shared<ServerStream>();
+    s->id = id;
+    s->headers = hl;
+    for (const auto& kv : hl) {
+      if (kv.first == ":path") {
+        const std::string svc = v2::kService;
+        s->path = starts_with(kv.second, svc) ? kv.second.substr(svc.size()) : kv.second;
+      } else if (kv.first == "authorization") {
+        s->authorization = kv.second;
+      }
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      streams_[id] = s;
+    }
+    w_.register_stream(id);
+    ++srv_.stats().grpc_calls;
+    if (end_stream) dispatch(s);
+  }
+
+  static void split_messages_into(std::string& buf, std::vector<std::string>* out) {
+    size_t pos = 0;
+    while (buf.size() - pos >= 5) {
+      uint32_t len = be32(reinterpret_cast<const uint8_t*>(buf.data() + pos + 1));
+      if (buf.size() - pos - 5 < len) break;
+      out->emplace_back(buf, pos + 5, len);
+      pos += 5 + len;
+    }
+    if (pos) buf.erase(0, pos);
+  }
+  void split_messages(ServerStream& s) { split_messages_into(s.buf, &s.messages); }
+
+  void dispatch(const std::shared_ptr<ServerStream>& s) {
+    if (s->half_closed) return;
+    s->half_closed = true;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      ++active_handlers_;
+    }
+    std::thread([this, s] {
+      try {
+        handle(*s);
+      } catch (...) {
+      }
+      w_.unregister_stream(s->id);
+      std::lock_guard<std::mutex> lk(mu_);
+      streams_.erase(s->id);
+      if (--active_handlers_ == 0) cv_.notify_all();
+    }).detach();
+  }
+
+  // --- responses ------------------------------------------------------------
+  void send_headers(uint32_t id) {
+    std::string block;
+    enc_.encode({{":status", "200"}, {"content-type", "application/grpc"}, {"grpc-accept-encoding", "identity"}},
+                &block);
+    w_.write_headers(id, block, false);
+  }
+  void send_trailers(uint32_t id, int code, const std::string& msg, bool headers_sent) {
+    HeaderList h;
+    if (!headers_sent) {
+      h.emplace_back(":status", "200");
+      h.emplace_back("content-type", "application/grpc");
+    }
+    h.emplace_back("grpc-status", std::to_string(code));
+    if (!msg.empty()) h.emplace_back("grpc-message", url_encode(msg, true));
+    std::string block;
+    enc_.encode(h, &block);
+    w_.write_headers(id, block, true);
+  }
+  // Sends one gRPC message given as iov pieces, splitting into DATA frames as
+  // the peer's flow-control windows and max frame size allow.
+  void send_message_iov(ServerStream& s, std::vector<iovec> pieces) {
+    size_t total = 0;
+    for (auto& p : pieces) total += p.iov_len;
+    uint8_t pre[5] = {0, 0, 0, 0, 0};
+    put_be32(pre + 1, static_cast<uint32_t>(total));
+    pieces.insert(pieces.begin(), iovec{pre, 5});
+    total += 5;
+    size_t idx = 0, off = 0;
+    std::vector<iovec> frame;
+    while (total > 0) {
+      if (s.cancelled) throw Cancelled{};
+      size_t n = w_.reserve(s.id, total);
+      if (n == 0) throw Cancelled{};
+      frame.clear();
+      size_t need = n;
+      while (need > 0) {
+        size_t k = std::min(need, pieces[idx].iov_len - off);
+        frame.push_back({static_cast<uint8_t*>(pieces[idx].iov_base) + off, k});
+        need -= k;
+        off += k;
+        if (off == pieces[idx].iov_len) {
+          ++idx;
+          off = 0;
+        }
+      }
+      w_.write_frame_iov(h2::kData, 0, s.id, frame.data(), static_cast<int>(frame.size()), n);
+      total -= n;
+    }
+  }
+  void send_message(ServerStream& s, const std::string& m) {
+    send_message_iov(s, {iovec{const_cast<char*>(m.data()), m.size()}});
+  }
+
+  bool auth_ok(ServerStream& s) {
+    if (!srv_.config().require_auth) return true;
+    if (starts_with(s.authorization, "Bearer ") && srv_.token_valid(s.authorization.substr(7))) return true;
+    ++srv_.stats().auth_failures;
+    send_trailers(s.id, kUnauthenticated, "Request had invalid authentication credentials.", false);
+    return false;
+  }
+
+  bool maybe_fail(ServerStream& s) {
+    auto& f = srv_.faults();
+    int n = f.fail_next.load();
+    while (n > 0) {
+      if (f.fail_next.compare_exchange_weak(n, n - 1)) {
+        ++srv_.stats().faults_injected;
+        int code = f.fail_status.load() == 429 ? kResourceExhausted : kUnavailable;
+        send_trailers(s.id, code, "injected fault", false);
+        return true;
+      }
+    }
+    return false;
+  }
+
+  v2::Object to_v2(const StoredObject& o) {
+    v2::Object v;
+    v.name = o.name;
+    v.bucket = v2::bucket_resource(o.bucket);
+    v.generation = o.generation;
+    v.metageneration = o.metageneration;
+    v.size = static_cast<int64_t>(o.size);
+    v.content_type = o.content_type;
+    v.has_crc32c = true;
+    v.crc32c = o.crc32c;
+    v.md5 = o.md5;
+    v.create_time_s = o.created_us / 1000000;
+    v.create_time_ns = static_cast<int32_t>((o.created_us % 1000000) * 1000);
+    v.update_time_s = v.create_time_s;
+    v.update_time_ns = v.create_time_ns;
+    v.etag = "CK" + std::to_string(o.generation % 1000000) + "E=";
+    return v;
+  }
+
+  void handle(ServerStream& s) {
+    try {
+      if (!auth_ok(s)) return;
+      if (s.path == "ReadObject") return read_object(s);
+      if (s.path == "GetObject") return get_object(s);
+      if (s.path == "ListObjects") return list_objects(s);
+      if (s.path == "WriteObject") return write_object_done(s);
+      if (s.path == "StartResumableWrite") return start_resumable(s);
+      if (s.path == "QueryWriteStatus") return query_write_status(s);
+      send_trailers(s.id, kUnimplemented, "unknown method " + s.path, false);
+    } catch (const Cancelled&) {
+      if (!s.cancelled) {
+        try {
+          w_.write_rst(s.id, h2::kErrCancel);
+        } catch (...) {
+        }
+      }
+    }
+  }
+
+  void read_object(ServerStream& s) {
+    v2::ReadObjectRequest q;
+    if (s.messages.empty() || !v2::decode_read_request(s.messages[0], &q))
+      return send_trailers(s.id, kInvalidArgument, "bad ReadObjectRequest", false);
+    auto o = srv_.store().get(v2::bucket_from_resource(q.bucket), q.object);
+    if (!o || (q.generation && q.generation != o->generation))
+      return send_trailers(s.id, kNotFound, "No such object: " + v2::bucket_from_resource(q.bucket) + "/" + q.object,
+                           false);
+    if (maybe_fail(s)) return;
+    int64_t start = q.read_offset;
+    if (start < 0) start = std::max<int64_t>(0, static_cast<int64_t>(o->size) + start);
+    if (static_cast<uint64_t>(start) > o->size)
+      return send_trailers(s.id, kOutOfRange, "read_offset beyond object size", false);
+    uint64_t end = o->size;
+    if (q.read_limit > 0) end = std::min<uint64_t>(end, static_cast<uint64_t>(start + q.read_limit));
+    auto& f = srv_.faults();
+    if (int lat = f.latency_ms.load()) std::this_thread::sleep_for(std::chrono::milliseconds(lat));
+    send_headers(s.id);
+    const uint64_t chunk = srv_.config().grpc_chunk;
+    const std::string checksums = v2::encode_checksums(true, o->crc32c, o->md5);
+    v2::ContentRange cr;
+    cr.start = start;
+    cr.end = static_cast<int64_t>(end);
+    cr.complete_length = static_cast<int64_t>(o->size);
+    const std::string range = v2::encode_content_range(cr);
+    const std::string meta = v2::encode_object(to_v2(*o));
+    int64_t disc = f.disconnect_count.load() > 0 ? f.disconnect_at.load() : -1;
+    int64_t corrupt = f.corrupt_count.load() > 0 ? f.corrupt_at.load() : -1;
+    const int64_t bps = f.throttle_bps.load();
+    const int64_t t0 = now_ns();
+    uint64_t off = static_cast<uint64_t>(start);
+    bool first = true;
+    uint64_t sent = 0;
+    do {
+      uint64_t n = std::min<uint64_t>(chunk, end - off);
+      if (disc >= 0 && static_cast<int64_t>(off + n) > disc && static_cast<int64_t>(off) <= disc &&
+          f.disconnect_count.fetch_sub(1) > 0) {
+        ++srv_.stats().faults_injected;
+        ::shutdown(bc_.conn().fd(), SHUT_RDWR);
+        throw Cancelled{};
+      }
+      uint32_t crc = srv_.store().chunk_crc(*o, off, n, chunk);
+      v2::ReadResponseFrame fr = v2::encode_read_response(n, true, crc, first ? &checksums : nullptr,
+                                                          first ? &range : nullptr, first ? &meta : nullptr);
+      const uint8_t* p = n ? o->bytes(off, n) : nullptr;
+      std::vector<iovec> pieces{{fr.head.data(), fr.head.size()}};
+      uint8_t bad = 0;
+      if (corrupt >= 0 && static_cast<int64_t>(off) <= corrupt && static_cast<int64_t>(off + n) > corrupt &&
+          f.corrupt_count.fetch_sub(1) > 0) {
+        uint64_t k = static_cast<uint64_t>(corrupt) - off;
+        bad = static_cast<uint8_t>(p[k] ^ 0x5A);
+        if (k) pieces.push_back({const_cast<uint8_t*>(p), k});
+        pieces.push_back({&bad, 1});
+        if (n - k - 1) pieces.push_back({const_cast<uint8_t*>(p + k + 1), n - k - 1});
+        ++srv_.stats().faults_injected;
+        corrupt = -1;
+      } else if (n) {
+        pieces.push_back({const_cast<uint8_t*>(p), n});
+      }
+      pieces.push_back({fr.tail.data(), fr.tail.size()});
+      send_message_iov(s, pieces);
+      off += n;
+      sent += n;
+      first = false;
+      if (bps > 0) {
+        int64_t due = t0 + static_cast<int64_t>(sent * 1e9 / static_cast<double>(bps));
+        int64_t now = now_ns();
+        if (due > now) std::this_thread::sleep_for(std::chrono::nanoseconds(due - now));
+      }
+    } while (off < end);
+    srv_.stats().bytes_sent += sent;
+    send_trailers(s.id, kOk, "", true);
+  }
+
+  void get_object(ServerStream& s) {
+    v2::GetObjectRequest q;
+    if (s.messages.empty() || !v2::decode_get_request(s.messages[0], &q))
+      return send_trailers(s.id, kInvalidArgument, "bad GetObjectRequest", false);
+    auto o = srv_.store().get(v2::bucket_from_resource(q.bucket), q.object);
+    if (!o) return send_trailers(s.id, kNotFound, "No such object: " + q.object, false);
+    send_headers(s.id);
+    send_message(s, v2::encode_object(to_v2(*o)));
+    send_trailers(s.id, kOk, "", true);
+  }
+
+  void list_objects(ServerStream& s) {
+    v2::ListObjectsRequest q;
+    if (s.messages.empty() || !v2::decode_list_request(s.messages[0], &q))
+      return send_trailers(s.id, kInvalidArgument, "bad ListObjectsRequest", false);
+    const std::string bucket = v2::bucket_from_resource(q.parent);
+    size_t max = q.page_size > 0 ? std::min(1000, q.page_size) : 1000;
+    v2::ListObjectsResponse lr;
+    std::set<std::string> seen;
+    std::string cursor = q.page_token, last;
+    size_t emitted = 0;
+    bool more = false;
+    while (emitted < max && !more) {
+      auto batch = srv_.store().list(bucket, q.prefix, cursor, max - emitted + 1);
+      if (batch.empty()) break;
+      for (auto& o : batch) {
+        cursor = o->name;
+        if (emitted >= max) {
+          more = true;
+          break;
+        }
+        if (!q.delimiter.empty()) {
+          size_t d = o->name.find(q.delimiter, q.prefix.size());
+          if (d != std::string::npos) {
+            std::string pf = o->name.substr(0, d + q.delimiter.size());
+            if (seen.insert(pf).second) {
+              lr.prefixes.push_back(pf);
+              ++emitted;
+              last = o->name;
+            }
+            continue;
+          }
+        }
+        lr.objects.push_back(to_v2(*o));
+        ++emitted;
+        last = o->name;
+      }
+      if (batch.size() < max - emitted + 1) break;
+    }
+    if (!more && emitted >= max) more = !srv_.store().list(bucket, q.prefix, last, 1).empty();
+    if (more) lr.next_page_token = last;
+    send_headers(s.id);
+    send_message(s, v2::encode_list_response(lr));
+    send_trailers(s.id, kOk, "", true);
+  }
+
+  // Called on the reader thread as WriteObject messages complete.
+  void process_write_messages(ServerStream& s) {
+    for (auto& m : s.messages) {
+      if (s.write_error || s.write_finished) continue;
+      v2::WriteObjectRequestView w;
+      if (!v2::decode_write_request(m, &w)) {
+        s.write_error = true;
+        s.write_code = kInvalidArgument;
+        s.write_msg = "bad WriteObjectRequest";
+        continue;
+      }
+      if (s.write_first) {
+        s.write_first = false;
+        if (!w.upload_id.empty()) {
+          s.session = srv_.store().find_upload(w.upload_id);
+          if (!s.session) {
+            s.write_error = true;
+            s.write_code = kNotFound;
+            s.write_msg = "no such upload " + w.upload_id;
+            continue;
+          }
+        } else if (w.has_spec) {
+          s.session = srv_.store().start_upload(v2::bucket_from_resource(w.spec.resource.bucket),
+                                                w.spec.resource.name, w.spec.resource.content_type,
+                                                w.spec.object_size);
+        } else {
+          s.write_error = true;
+          s.write_code = kInvalidArgument;
+          s.write_msg = "first WriteObjectRequest needs upload_id or write_object_spec";
+          continue;
+        }
+      }
+      UploadSession& u = *s.session;
+      std::lock_guard<std::mutex> lk(u.mu);
+      if (w.write_offset != static_cast<int64_t>(u.data.size())) {
+        if (w.write_offset < static_cast<int64_t>(u.data.size()) &&
+            w.write_offset + static_cast<int64_t>(w.content.size()) <= static_cast<int64_t>(u.data.size())) {
+          // retransmission of persisted bytes: ignore
+        } else {
+          s.write_error = true;
+          s.write_code = kFailedPrecondition;
+          s.write_msg = "write_offset " + std::to_string(w.write_offset) + " != persisted size " +
+                        std::to_string(u.data.size());
+          continue;
+        }
+      } else if (w.has_data) {
+        if (w.has_content_crc && crc32c(w.content.data(), w.content.size()) != w.content_crc) {
+          s.write_error = true;
+          s.write_code = kDataLoss;
+          s.write_msg = "ChecksummedData crc32c mismatch";
+          continue;
+        }
+        u.data.insert(u.data.end(), w.content.begin(), w.content.end());
+      }
+      if (w.has_object_crc) {
+        u.has_crc = true;
+        u.crc = w.object_crc;
+      }
+      if (w.finish_write) s.write_finished = true;
+    }
+    s.messages.clear();
+  }
+
+  void write_object_done(ServerStream& s) {
+    if (s.write_error) return send_trailers(s.id, s.write_code, s.write_msg, false);
+    if (!s.session) return send_trailers(s.id, kInvalidArgument, "empty WriteObject stream", false);
+    v2::WriteStatus st;
+    if (s.write_finished) {
+      std::lock_guard<std::mutex> lk(s.session->mu);
+      std::string err;
+      auto o = srv_.store().finalize_upload(*s.session, &err);
+      if (!o) return send_trailers(s.id, kInvalidArgument, err, false);
+      st.has_resource = true;
+      st.resource = to_v2(*o);
+    } else {
+      std::lock_guard<std::mutex> lk(s.session->mu);
+      st.persisted_size = static_cast<int64_t>(s.session->data.size());
+    }
+    send_headers(s.id);
+    send_message(s, v2::encode_write_status(st));
+    send_trailers(s.id, kOk, "", true);
+  }
+
+  void start_resumable(ServerStream& s) {
+    v2::WriteObjectSpec spec;
+    bool has_crc = false;
+    uint32_t crc = 0;
+    if (s.messages.empty() || !v2::decode_start_resumable(s.messages[0], &spec, &has_crc, &crc))
+      return send_trailers(s.id, kInvalidArgument, "bad StartResumableWriteRequest", false);
+    auto u = srv_.store().start_upload(v2::bucket_from_resource(spec.resource.bucket), spec.resource.name,
+                                       spec.resource.content_type, spec.object_size);
+    if (has_crc) {
+      u->has_crc = true;
+      u->crc = crc;
+    }
+    send_headers(s.id);
+    send_message(s, v2::encode_upload_id(u->id));
+    send_trailers(s.id, kOk, "", true);
+  }
+
+  void query_write_status(ServerStream& s) {
+    std::string id;
+    if (s.messages.empty() || !v2::decode_upload_id(s.messages[0], &id))
+      return send_trailers(s.id, kInvalidArgument, "bad QueryWriteStatusRequest", false);
+    auto u = srv_.store().find_upload(id);
+    if (!u) return send_trailers(s.id, kNotFound, "no such upload", false);
+    v2::WriteStatus st;
+    {
+      std::lock_guard<std::mutex> lk(u->mu);
+      if (u->finalized) {
+        st.has_resource = true;
+        st.resource = to_v2(*u->result);
+      } else {
+        st.persisted_size = static_cast<int64_t>(u->data.size());
+      }
+    }
+    send_headers(s.id);
+    send_message(s, v2::encode_write_status(st));
+    send_trailers(s.id, kOk, "", true);
+  }
+
+  FakeGcsServer& srv_;
+  BufferedConn& bc_;
+  H2Writer w_;
+  HpackDecoder dec_;
+  HpackEncoder enc_;
+  H2Settings peer_;
+  RecvWindow conn_rw_{64 << 20};
+  std::mutex mu_;
+  std::condition_variable cv_;
+  int active_handlers_ = 0;
+  std::map<uint32_t, std::shared_ptr<ServerStream>> streams_;
+};
+
+}  // namespace
+
+void FakeGcsServer::serve_h2(std::unique_ptr<BufferedConn> bc) {
+  H2ServerConn c(*this, *bc);
+  c.run();
+  ::shutdown(bc->conn().fd(), SHUT_RDWR);
+}
+
 }  // namespace gcsb

@@ -108,7 +108,7 @@ class HttpStorageClient : public StorageClient {
       }
     }
     const size_t chunk = cfg_.read_chunk;
-    for (;;) {
+    while (!ex.body_done()) {
       Window w = sink.acquire(chunk);
       size_t cap = w.cap < chunk ? w.cap : chunk;
       size_t r = ex.read_body(w.ptr, cap);

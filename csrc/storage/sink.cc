@@ -89,7 +89,7 @@ SinkResult DiscardSink::finish() {
       mismatch_ = true;
       char b[128];
       std::snprintf(b, sizeof(b), "bad CRC on read: got %08x want %08x", obj_crc_, info_.crc32c);
-      detail_ = b;
+      if (detail_.empty()) detail_ = b;  // keep the first (chunk-level) finding
     }
   }
   r.verified = any_checked_ && !mismatch_;

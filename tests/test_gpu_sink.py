@@ -79,3 +79,37 @@ def test_hbm_helper_roundtrip(native, server, gpu_available):
     c = native.Client({"protocol": "http", "endpoint": server.url})
     t, r = hbm.read_object_to_tensor(c, B, P + "0")
     assert r["verified"] and hbm.crc32c(t) == server.object_info(B, P + "0")["crc32c"]
+
+
+def test_grpc_chunks_verified_by_gpu_epilogue(native, server, gpu_available):
+    size = (20 << 20) + 4321
+    server.add_synthetic(B, P, "", 0, 1, size)
+    c = native.Client({"protocol": "grpc", "endpoint": server.url})
+    # sink-owned landing buffer: gRPC learns the size after the first message
+    sink = native.GpuSink({"device": 0, "ring_slot_bytes": 8 << 20, "ring_slots": 3})
+    for _ in range(2):
+        r = c.read_gpu(B, P + "0", sink)
+        assert r["verified"] and r["bytes"] == size, r
+    st = sink.stats()
+    assert st["chunks_verified_gpu"] >= 2 * 10 and st["objects_verified"] == 2
+    bad, _ = native.gpu_verify_pattern(0, sink.device_ptr, size, P + "0", 0)
+    assert bad == 0
+
+
+def test_grpc_chunk_spanning_slots_folded_on_host(native, server, gpu_available):
+    # 1 MiB slots < 2 MiB messages: every chunk spans two slots
+    server.add_synthetic(B, P, "", 0, 1, 6 << 20)
+    c = native.Client({"protocol": "grpc", "endpoint": server.url})
+    sink = native.GpuSink({"device": 0, "ring_slot_bytes": 1 << 20, "ring_slots": 2})
+    r = c.read_gpu(B, P + "0", sink)
+    assert r["verified"]
+    assert sink.stats()["chunks_verified_host"] == 3
+
+
+def test_grpc_gpu_detects_corrupt_message(native, server, gpu_available):
+    server.add_synthetic(B, P, "", 0, 1, 6 << 20)
+    server.set_faults({"corrupt_at": (2 << 20) + 99, "corrupt_count": 1})
+    c = native.Client({"protocol": "grpc", "endpoint": server.url})
+    sink = native.GpuSink({"device": 0, "ring_slot_bytes": 4 << 20, "ring_slots": 2})
+    r = c.read_gpu(B, P + "0", sink)
+    assert r["crc_mismatch"] and "chunk crc32c mismatch" in r["detail"]

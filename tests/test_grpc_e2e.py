@@ -1,0 +1,96 @@
+"""Native gRPC transport against the synthetic server: reads, faults, resume."""
+import os
+
+import pytest
+
+B = "princer-working-dirs"
+P = "princer_100M_files/file_"
+
+
+def _c(native, server, **kw):
+    cfg = {"protocol": "grpc", "endpoint": server.url, "retry_initial_s": 0.001}
+    cfg.update(kw)
+    return native.Client(cfg)
+
+
+def test_read_verified_chunks(native, server):
+    server.add_synthetic(B, P, "", 0, 1, 9 * (1 << 20) + 11)
+    r = _c(native, server).read(B, P + "0")
+    assert r["bytes"] == 9 * (1 << 20) + 11 and r["verified"] and not r["crc_mismatch"]
+    assert r["size"] == 9 * (1 << 20) + 11 and r["has_crc32c"]
+
+
+def test_small_messages_many_frames(native):
+    srv = native.Server({"port": 0, "grpc_chunk": 4096 + 3})
+    srv.start()
+    try:
+        srv.add_synthetic(B, P, "", 0, 1, 100000)
+        c = native.Client({"protocol": "grpc", "endpoint": srv.url})
+        assert c.read_bytes(B, P + "0") == native.object_bytes(P + "0", 0, 100000)
+        assert c.read(B, P + "0")["verified"]
+    finally:
+        srv.stop()
+
+
+def test_unavailable_is_retried(native, server):
+    server.add_synthetic(B, P, "", 0, 1, 1 << 20)
+    server.set_faults({"fail_next": 2, "fail_status": 503})
+    r = _c(native, server).read(B, P + "0")
+    assert r["attempts"] == 3 and r["verified"]
+
+
+def test_resume_at_read_offset_after_disconnect(native, server):
+    server.add_synthetic(B, P, "", 0, 1, 10 << 20)
+    server.set_faults({"disconnect_at": (5 << 20) + 1, "disconnect_count": 1})
+    c = _c(native, server)
+    r = c.read(B, P + "0")
+    assert r["attempts"] == 2 and r["bytes"] == 10 << 20 and r["verified"]
+    assert c.read_bytes(B, P + "0") == native.object_bytes(P + "0", 0, 10 << 20)
+
+
+def test_corruption_detected_per_message(native, server):
+    server.add_synthetic(B, P, "", 0, 1, 6 << 20)
+    server.set_faults({"corrupt_at": (4 << 20) + 17, "corrupt_count": 1})
+    r = _c(native, server).read(B, P + "0")
+    assert r["crc_mismatch"] and "mismatch" in r["detail"]
+
+
+def test_not_found(native, server):
+    with pytest.raises(native.StorageError, match="doesn't exist"):
+        _c(native, server).read(B, "nope")
+
+
+def test_many_workers_one_connection(native, server):
+    server.add_synthetic(B, P, "", 0, 16, 2 << 20)
+    run = native.Runner({"protocol": "grpc", "endpoint": server.url, "bucket": B, "workers": 16,
+                         "reads_per_worker": 4, "grpc_conn_pool_size": 1})
+    run.start()
+    run.wait()
+    s = run.summary()
+    assert s["reads"] == 64 and s["errors"] == 0 and s["verified"] == 64
+    assert server.stats()["connections"] == 1
+
+
+def test_resumable_write_and_list(native, server):
+    c = _c(native, server)
+    data = os.urandom(5 * (1 << 20) + 3)
+    m = c.write_bytes(B, "w/res", data, True)
+    assert m["size"] == len(data) and m["crc32c"] == native.crc32c(data)
+    assert c.read_bytes(B, "w/res") == data
+    server.add_synthetic(B, "w/syn", "", 0, 3, 10)
+    names = [o["name"] for o in c.list_all(B, "w/", 2)]
+    assert names == ["w/res", "w/syn0", "w/syn1", "w/syn2"]
+
+
+def test_auth_required(native):
+    srv = native.Server({"port": 0, "require_auth": True})
+    srv.start()
+    try:
+        srv.add_synthetic(B, P, "", 0, 1, 4096)
+        c = native.Client({"protocol": "grpc", "endpoint": srv.url, "retry_max_attempts": 1})
+        with pytest.raises(native.StorageError, match="code = 16"):
+            c.read(B, P + "0")
+        c = native.Client({"protocol": "grpc", "endpoint": srv.url, "auth": "static", "token": srv.issue_token()})
+        assert c.read(B, P + "0")["verified"]
+    finally:
+        srv.stop()

@@ -1,7 +1,11 @@
 #include "core/content.h"
 
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <cstring>
+#include <mutex>
 #include <stdexcept>
 #include <thread>
 
@@ -53,6 +57,27 @@ PatternBuffer::PatternBuffer() {
   const uint64_t nblocks = kPatternLen / kBlock;
   block_crc_.resize(nblocks);
   for (uint64_t b = 0; b < nblocks; ++b) block_crc_[b] = crc32c(&buf_[b * kBlock], kBlock);
+}
+
+int PatternBuffer::memfd() const {
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lk(mu);
+  if (memfd_ != -2) return memfd_;
+  int fd = static_cast<int>(::syscall(SYS_memfd_create, "gcsb-pattern", 0));
+  if (fd >= 0) {
+    size_t off = 0;
+    while (off < buf_.size()) {
+      ssize_t w = ::write(fd, buf_.data() + off, buf_.size() - off);
+      if (w <= 0) {
+        ::close(fd);
+        fd = -1;
+        break;
+      }
+      off += static_cast<size_t>(w);
+    }
+  }
+  memfd_ = fd;
+  return memfd_;
 }
 
 const PatternBuffer& PatternBuffer::instance() {

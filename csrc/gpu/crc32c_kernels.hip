@@ -183,23 +183,42 @@ __global__ __launch_bounds__(256) void fill_pattern_kernel(uint8_t* __restrict__
 __global__ __launch_bounds__(256) void verify_pattern_kernel(const uint8_t* __restrict__ src, uint64_t n, uint64_t rot,
                                                              uint64_t obj_off, unsigned long long* count,
                                                              unsigned long long* first) {
+  // same generation path as fill_pattern_kernel; per-block reduction, one
+  // atomic pair per block
+  __shared__ unsigned long long s_bad[256];
+  __shared__ unsigned long long s_first[256];
+  unsigned long long bad = 0, first_bad = ~0ull;
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
   for (uint64_t g = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; g * 16 < n; g += stride) {
     const uint64_t b0 = g * 16;
     uint64_t q = (obj_off + b0 + rot) % kPatternLen;
-    unsigned bad = 0;
-    uint64_t first_bad = ~0ull;
-    for (int e = 0; e < 16 && b0 + e < n; ++e) {
-      if (src[b0 + e] != obj_byte(q)) {
-        ++bad;
-        if (first_bad == ~0ull) first_bad = b0 + e;
-      }
+    uint8_t v[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      v[e] = obj_byte(q);
       q = (q + 1 == kPatternLen) ? 0 : q + 1;
     }
-    if (bad) {
-      atomicAdd(count, static_cast<unsigned long long>(bad));
-      atomicMin(first, static_cast<unsigned long long>(first_bad));
+    const int lim = (b0 + 16 <= n) ? 16 : static_cast<int>(n - b0);
+    for (int e = 0; e < lim; ++e) {
+      if (src[b0 + e] != v[e]) {
+        ++bad;
+        if (b0 + e < first_bad) first_bad = b0 + e;
+      }
     }
+  }
+  s_bad[threadIdx.x] = bad;
+  s_first[threadIdx.x] = first_bad;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (static_cast<int>(threadIdx.x) < w) {
+      s_bad[threadIdx.x] += s_bad[threadIdx.x + w];
+      if (s_first[threadIdx.x + w] < s_first[threadIdx.x]) s_first[threadIdx.x] = s_first[threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && s_bad[0]) {
+    atomicAdd(count, s_bad[0]);
+    atomicMin(first, s_first[0]);
   }
 }
 

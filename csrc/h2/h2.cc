@@ -88,6 +88,28 @@ void H2Writer::write_frame_iov(uint8_t type, uint8_t flags, uint32_t stream, str
   conn_.writev_all(iov.data(), cnt + 1);
 }
 
+void H2Writer::write_frame_pieces(uint8_t type, uint8_t flags, uint32_t stream, const std::vector<SendPiece>& pieces,
+                                  size_t total) {
+  uint8_t hdr[9];
+  encode_frame_header(hdr, static_cast<uint32_t>(total), type, flags, stream);
+  std::vector<iovec> iov;
+  iov.push_back({hdr, 9});
+  std::lock_guard<std::mutex> lk(wmu_);
+  for (size_t i = 0; i < pieces.size(); ++i) {
+    const SendPiece& p = pieces[i];
+    if (p.fd < 0) {
+      if (p.n) iov.push_back({const_cast<uint8_t*>(p.p), p.n});
+      continue;
+    }
+    if (!iov.empty()) {
+      conn_.writev_all(iov.data(), static_cast<int>(iov.size()), /*more=*/true);
+      iov.clear();
+    }
+    conn_.sendfile_all(p.fd, p.foff, p.n, /*more=*/i + 1 < pieces.size());
+  }
+  if (!iov.empty()) conn_.writev_all(iov.data(), static_cast<int>(iov.size()));
+}
+
 void H2Writer::write_headers(uint32_t stream, const std::string& block, bool end_stream) {
   const size_t maxf = peer_max_frame_;
   std::lock_guard<std::mutex> lk(wmu_);  // HEADERS+CONTINUATION must be contiguous

@@ -59,6 +59,14 @@ struct H2Settings {
 // Payload of a SETTINGS frame.
 std::string encode_settings(const std::vector<std::pair<uint16_t, uint32_t>>& kv);
 
+// A payload piece: memory, or a file range sent with sendfile() (zero copy).
+struct SendPiece {
+  const uint8_t* p = nullptr;
+  size_t n = 0;
+  int fd = -1;
+  uint64_t foff = 0;
+};
+
 // Per-direction connection machinery common to both roles: serialized
 // writes, peer settings, send-side flow-control windows.
 class H2Writer {
@@ -67,6 +75,8 @@ class H2Writer {
   // Writes one frame (header + payload pieces) atomically w.r.t. other writers.
   void write_frame(uint8_t type, uint8_t flags, uint32_t stream, const void* p, size_t n);
   void write_frame_iov(uint8_t type, uint8_t flags, uint32_t stream, struct iovec* payload, int cnt, size_t total);
+  void write_frame_pieces(uint8_t type, uint8_t flags, uint32_t stream, const std::vector<SendPiece>& pieces,
+                          size_t total);
   // Header block (HEADERS + CONTINUATION as needed).
   void write_headers(uint32_t stream, const std::string& block, bool end_stream);
   void write_window_update(uint32_t stream, uint32_t inc);

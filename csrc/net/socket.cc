@@ -8,12 +8,15 @@
 #include <openssl/err.h>
 #include <openssl/ssl.h>
 #include <poll.h>
+#include <sys/sendfile.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
 #include <cerrno>
 #include <cstring>
+#include <algorithm>
 #include <mutex>
+#include <vector>
 
 #include "core/util.h"
 
@@ -209,7 +212,7 @@ void Conn::write_all(const void* buf, size_t n) {
   writev_all(&iov, 1);
 }
 
-void Conn::writev_all(struct iovec* iov, int cnt) {
+void Conn::writev_all(struct iovec* iov, int cnt, bool more) {
   if (fd_ < 0) throw StorageError("write on closed connection", true);
   if (ssl_) {
     for (int i = 0; i < cnt; ++i) {
@@ -229,7 +232,7 @@ void Conn::writev_all(struct iovec* iov, int cnt) {
     msghdr msg{};
     msg.msg_iov = iov;
     msg.msg_iovlen = static_cast<size_t>(cnt > 1024 ? 1024 : cnt);
-    ssize_t w = ::sendmsg(fd_, &msg, MSG_NOSIGNAL);
+    ssize_t w = ::sendmsg(fd_, &msg, MSG_NOSIGNAL | (more ? MSG_MORE : 0));
     if (w < 0) {
       if (errno == EINTR) continue;
       throw StorageError(std::string("send: ") + std::strerror(errno), true);
@@ -245,6 +248,40 @@ void Conn::writev_all(struct iovec* iov, int cnt) {
       iov->iov_base = static_cast<uint8_t*>(iov->iov_base) + left;
       iov->iov_len -= left;
     }
+  }
+}
+
+void Conn::sendfile_all(int in_fd, uint64_t off, size_t n, bool more) {
+  if (fd_ < 0) throw StorageError("write on closed connection", true);
+  if (ssl_) {  // no kernel TLS here: fall back to pread + SSL_write
+    std::vector<uint8_t> buf(std::min<size_t>(n, 1 << 20));
+    while (n > 0) {
+      ssize_t r = ::pread(in_fd, buf.data(), std::min(n, buf.size()), static_cast<off_t>(off));
+      if (r <= 0) throw StorageError("pread for TLS send failed", true);
+      write_all(buf.data(), static_cast<size_t>(r));
+      off += static_cast<uint64_t>(r);
+      n -= static_cast<size_t>(r);
+    }
+    return;
+  }
+  if (more) {
+    int one = 1;
+    setsockopt(fd_, IPPROTO_TCP, TCP_CORK, &one, sizeof(one));
+  }
+  off_t o = static_cast<off_t>(off);
+  while (n > 0) {
+    ssize_t w = ::sendfile(fd_, in_fd, &o, n);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      throw StorageError(std::string("sendfile: ") + std::strerror(errno), true);
+    }
+    if (w == 0) throw StorageError("sendfile: source ended", false);
+    bytes_written_ += static_cast<uint64_t>(w);
+    n -= static_cast<size_t>(w);
+  }
+  if (more) {
+    int zero = 0;
+    setsockopt(fd_, IPPROTO_TCP, TCP_CORK, &zero, sizeof(zero));
   }
 }
 

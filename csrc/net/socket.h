@@ -28,8 +28,8 @@ struct Endpoint {
 };
 
 struct SocketOptions {
-  int rcvbuf = 8 << 20;
-  int sndbuf = 8 << 20;
+  int rcvbuf = 0;  // 0 = kernel autotuning
+  int sndbuf = 0;
   bool nodelay = true;
   int connect_timeout_ms = 10000;
   int io_timeout_ms = 0;  // 0 = none (reference: http.Client.Timeout=0, main.go:94)
@@ -51,7 +51,9 @@ class Conn {
   // Reads exactly n bytes or throws (EOF mid-way is a retryable error).
   void read_exact(void* buf, size_t n);
   void write_all(const void* buf, size_t n);
-  void writev_all(struct iovec* iov, int cnt);
+  void writev_all(struct iovec* iov, int cnt, bool more = false);
+  // Zero-copy send of a file range (sendfile); `more` corks for a following write.
+  void sendfile_all(int in_fd, uint64_t off, size_t n, bool more = false);
   void shutdown_write();
   void close();
   int fd() const { return fd_; }

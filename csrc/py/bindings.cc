@@ -52,8 +52,10 @@ ClientConfig client_from(const py::dict& d) {
   c.grpc_conn_pool_size = get_or<int>(d, "grpc_conn_pool_size", 1);
   c.read_chunk = get_or<size_t>(d, "read_chunk", 2u << 20);
   c.retry = retry_from(d);
-  c.sock.rcvbuf = get_or<int>(d, "rcvbuf", 8 << 20);
-  c.sock.sndbuf = get_or<int>(d, "sndbuf", 8 << 20);
+  // 0 = kernel TCP autotuning (measured on the MI355X box: as fast as any
+  // fixed size, and an explicit SO_RCVBUF would cap it at rmem_max)
+  c.sock.rcvbuf = get_or<int>(d, "rcvbuf", 0);
+  c.sock.sndbuf = get_or<int>(d, "sndbuf", 0);
   c.sock.io_timeout_ms = get_or<int>(d, "io_timeout_ms", 0);
   c.project = get_or<std::string>(d, "project", "gcs-fuse-test");
   std::string auth = get_or<std::string>(d, "auth", "none");
@@ -348,6 +350,8 @@ class PyServer {
     c.require_auth = get_or<bool>(d, "require_auth", false);
     c.jwt_public_key_pem = get_or<std::string>(d, "jwt_public_key_pem", "");
     c.grpc_chunk = get_or<uint64_t>(d, "grpc_chunk", 2u << 20);
+    c.sndbuf = get_or<int>(d, "sndbuf", 0);
+    c.zero_copy = get_or<bool>(d, "zero_copy", true);
     store_ = std::make_shared<ObjectStore>(get_or<bool>(d, "md5", true));
     srv_ = std::make_unique<FakeGcsServer>(c, store_);
   }
@@ -599,7 +603,16 @@ PYBIND11_MODULE(_native, m) {
     py::gil_scoped_release nogil;
     gpu_fill_pattern(dev, reinterpret_cast<void*>(ptr), n, object_rotation(name), off);
   });
-  m.def("gpu_verify_pattern", [](int dev, uintptr_t ptr, uint64_t n, const std::string& name, uint64_t off) {
+  m.def("gpu_read_bytes", [](int dev, uintptr_t ptr, size_t n) {
+    std::string out(n, '\0');
+    {
+      py::gil_scoped_release nogil;
+      hip_check(hipSetDevice(dev), "hipSetDevice");
+      hip_check(hipMemcpy(&out[0], reinterpret_cast<const void*>(ptr), n, hipMemcpyDeviceToHost), "hipMemcpy");
+    }
+    return py::bytes(out);
+  });
+  m.def("gpu_verify_pattern",[](int dev, uintptr_t ptr, uint64_t n, const std::string& name, uint64_t off) {
     uint64_t first = 0, bad = 0;
     {
       py::gil_scoped_release nogil;

@@ -69,7 +69,7 @@ void FakeGcsServer::accept_loop() {
 void FakeGcsServer::handle_conn(int fd) {
   SocketOptions so;
   so.sndbuf = cfg_.sndbuf;
-  so.rcvbuf = 4 << 20;
+  so.rcvbuf = 0;
   auto bc = std::make_unique<BufferedConn>(Conn::adopt(fd, so));
   char peek[3];
   ssize_t k = 0;

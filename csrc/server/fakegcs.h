@@ -35,7 +35,8 @@ struct ServerConfig {
   bool require_auth = false;
   std::string jwt_public_key_pem;  // verify JWT assertions at /token if set
   uint64_t grpc_chunk = 2 << 20;   // ReadObjectResponse content bytes per message (reference main.go:123-124)
-  int sndbuf = 8 << 20;
+  int sndbuf = 0;          // 0 = kernel autotuning (an explicit size disables it)
+  bool zero_copy = true;   // sendfile() synthetic object bodies from a memfd
 };
 
 struct ServerStats {

@@ -250,15 +250,18 @@ class H2ServerConn {
   }
   // Sends one gRPC message given as iov pieces, splitting into DATA frames as
   // the peer's flow-control windows and max frame size allow.
-  void send_message_iov(ServerStream& s, std::vector<iovec> pieces) {
+  void send_message_iov(ServerStream& s, std::vector<SendPiece> pieces) {
     size_t total = 0;
-    for (auto& p : pieces) total += p.iov_len;
+    for (auto& p : pieces) total += p.n;
     uint8_t pre[5] = {0, 0, 0, 0, 0};
     put_be32(pre + 1, static_cast<uint32_t>(total));
-    pieces.insert(pieces.begin(), iovec{pre, 5});
+    SendPiece pp;
+    pp.p = pre;
+    pp.n = 5;
+    pieces.insert(pieces.begin(), pp);
     total += 5;
     size_t idx = 0, off = 0;
-    std::vector<iovec> frame;
+    std::vector<SendPiece> frame;
     while (total > 0) {
       if (s.cancelled) throw Cancelled{};
       size_t n = w_.reserve(s.id, total);
@@ -266,22 +269,31 @@ class H2ServerConn {
       frame.clear();
       size_t need = n;
       while (need > 0) {
-        size_t k = std::min(need, pieces[idx].iov_len - off);
-        frame.push_back({static_cast<uint8_t*>(pieces[idx].iov_base) + off, k});
+        const SendPiece& src = pieces[idx];
+        size_t k = std::min(need, src.n - off);
+        SendPiece part = src;
+        part.n = k;
+        if (src.fd >= 0) part.foff = src.foff + off;
+        else part.p = src.p + off;
+        frame.push_back(part);
         need -= k;
         off += k;
-        if (off == pieces[idx].iov_len) {
+        if (off == src.n) {
           ++idx;
           off = 0;
         }
       }
-      w_.write_frame_iov(h2::kData, 0, s.id, frame.data(), static_cast<int>(frame.size()), n);
+      w_.write_frame_pieces(h2::kData, 0, s.id, frame, n);
       total -= n;
     }
   }
-  void send_message(ServerStream& s, const std::string& m) {
-    send_message_iov(s, {iovec{const_cast<char*>(m.data()), m.size()}});
+  static SendPiece mem(const void* p, size_t n) {
+    SendPiece x;
+    x.p = static_cast<const uint8_t*>(p);
+    x.n = n;
+    return x;
   }
+  void send_message(ServerStream& s, const std::string& m) { send_message_iov(s, {mem(m.data(), m.size())}); }
 
   bool auth_ok(ServerStream& s) {
     if (!srv_.config().require_auth) return true;
@@ -389,21 +401,29 @@ class H2ServerConn {
       v2::ReadResponseFrame fr = v2::encode_read_response(n, true, crc, first ? &checksums : nullptr,
                                                           first ? &range : nullptr, first ? &meta : nullptr);
       const uint8_t* p = n ? o->bytes(off, n) : nullptr;
-      std::vector<iovec> pieces{{fr.head.data(), fr.head.size()}};
+      std::vector<SendPiece> pieces{mem(fr.head.data(), fr.head.size())};
       uint8_t bad = 0;
+      int ffd = -1;
+      uint64_t foff = 0;
       if (corrupt >= 0 && static_cast<int64_t>(off) <= corrupt && static_cast<int64_t>(off + n) > corrupt &&
           f.corrupt_count.fetch_sub(1) > 0) {
         uint64_t k = static_cast<uint64_t>(corrupt) - off;
         bad = static_cast<uint8_t>(p[k] ^ 0x5A);
-        if (k) pieces.push_back({const_cast<uint8_t*>(p), k});
-        pieces.push_back({&bad, 1});
-        if (n - k - 1) pieces.push_back({const_cast<uint8_t*>(p + k + 1), n - k - 1});
+        if (k) pieces.push_back(mem(p, k));
+        pieces.push_back(mem(&bad, 1));
+        if (n - k - 1) pieces.push_back(mem(p + k + 1, n - k - 1));
         ++srv_.stats().faults_injected;
         corrupt = -1;
+      } else if (n && srv_.config().zero_copy && o->file_range(off, &ffd, &foff)) {
+        SendPiece fp;
+        fp.n = n;
+        fp.fd = ffd;
+        fp.foff = foff;
+        pieces.push_back(fp);  // sendfile(): no user-space copy of the content
       } else if (n) {
-        pieces.push_back({const_cast<uint8_t*>(p), n});
+        pieces.push_back(mem(p, n));
       }
-      pieces.push_back({fr.tail.data(), fr.tail.size()});
+      pieces.push_back(mem(fr.tail.data(), fr.tail.size()));
       send_message_iov(s, pieces);
       off += n;
       sent += n;

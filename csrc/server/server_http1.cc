@@ -410,7 +410,12 @@ class Http1Handler {
         sent += k + 1;
         continue;
       }
-      c_.write_all(o.bytes(off, n), n);
+      int ffd = -1;
+      uint64_t foff = 0;
+      if (srv_.config().zero_copy && o.file_range(off, &ffd, &foff))
+        c_.sendfile_all(ffd, foff, n);  // page references, no user-space copy
+      else
+        c_.write_all(o.bytes(off, n), n);
       sent += n;
       if (bps > 0) {
         int64_t due = t0 + static_cast<int64_t>(sent * 1e9 / static_cast<double>(bps));

@@ -18,6 +18,16 @@ const uint8_t* StoredObject::bytes(uint64_t off, uint64_t n) const {
   return data->data() + off;
 }
 
+bool StoredObject::file_range(uint64_t off, int* fd, uint64_t* foff) const {
+  if (!synthetic) return false;
+  const PatternBuffer& pb = PatternBuffer::instance();
+  int f = pb.memfd();
+  if (f < 0) return false;
+  *fd = f;
+  *foff = pb.file_offset(rot, off);
+  return true;
+}
+
 uint32_t StoredObject::crc32c_range(uint64_t off, uint64_t n) const {
   if (synthetic) return PatternBuffer::instance().crc32c_range(rot, off, n);
   return gcsb::crc32c(data->data() + off, n);

@@ -33,6 +33,8 @@ struct StoredObject {
 
   // Contiguous bytes [off, off+n) with n <= kPatternExt.
   const uint8_t* bytes(uint64_t off, uint64_t n) const;
+  // Synthetic objects: (fd, file offset) of [off, off+n) for sendfile(); false otherwise.
+  bool file_range(uint64_t off, int* fd, uint64_t* foff) const;
   uint32_t crc32c_range(uint64_t off, uint64_t n) const;
 };
 

@@ -50,6 +50,8 @@ def main() -> int:
     ap.add_argument("--slot-bytes", default="8MiB")
     ap.add_argument("--slots", type=int, default=4)
     ap.add_argument("--grpc-pool", type=int, default=1)
+    ap.add_argument("--affinity", default="same",
+                    help="CPU placement of client/endpoint threads: same|split|numa|none (see parallel/affinity.py)")
     ap.add_argument("--json-out", default="")
     args = ap.parse_args()
 
@@ -72,7 +74,10 @@ def main() -> int:
     size = parse_size(args.object_size)
 
     # Node-local synthetic GCS endpoint for this rank (no network on the box).
-    srv = n.Server({"port": 0, "md5": False})
+    from custom_go_client_benchmark_amd.parallel import affinity
+
+    placement = affinity.plan(local_rank, args.affinity) if use_gpu else {"client": [], "server": []}
+    srv = n.Server({"port": 0, "md5": False, "cpus": placement["server"]})
     srv.start()
     bucket = "princer-working-dirs"
     prefix = "princer_100M_files/file_"
@@ -94,6 +99,7 @@ def main() -> int:
         "landing": "object",
         "grpc_conn_pool_size": args.grpc_pool,
         "keep_records": False,
+        "cpus": placement["client"],
         "retry_initial_s": 0.05,
     }
     run = n.Runner(cfg)
@@ -160,6 +166,7 @@ def main() -> int:
             "p99_ms": round(stats["p99_max"], 3),
             "host_landed_p50_ms": round(stats["host_p50_max"], 3),
             "endpoint": "loopback synthetic GCS (one per rank)",
+            "affinity": args.affinity,
         }
         line = json.dumps(out)
         print(line, flush=True)

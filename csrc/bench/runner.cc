@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <random>
 
+#include "core/affinity.h"
 #include "core/util.h"
 
 namespace gcsb {
@@ -98,6 +99,8 @@ void Runner::record(ReadRecord&& r, double ms, double host_ms) {
 }
 
 void Runner::worker_main(int w) {
+  // pin before the sink allocates its pinned ring: NUMA-local first touch
+  pin_current_thread(cfg_.client.cpus);
   try {
     if (!sinks_[w]) {
       if (cfg_.sink == "gpu") {

@@ -1,0 +1,23 @@
+// CPU placement for the transport threads.
+//
+// [new] MI355X nodes are 2-socket with 4 GPUs per NUMA node and 8-core L3
+// domains (measured on the GPU box: 16 L3 groups, GPUs 0a/23/5a/72 on node 0,
+// 8b/a4/d9/f1 on node 1).  Loopback throughput of one object stream swings by
+// ~1.5x with scheduler placement, so each rank pins its receive threads (and
+// its node-local endpoint's send threads) to cores of its GPU's NUMA node, and
+// allocates the pinned ring from that thread (NUMA-local first touch).
+#pragma once
+#include <string>
+#include <vector>
+
+namespace gcsb {
+
+// "0-3,8,10-11" -> {0,1,2,3,8,10,11}
+std::vector<int> parse_cpulist(const std::string& s);
+// Pins the calling thread to the given CPUs (no-op if empty). Returns success.
+bool pin_current_thread(const std::vector<int>& cpus);
+// Round-robin pick: thread k gets cpus[k % n] (single-CPU pinning) when
+// `spread` is set, else the whole set.
+std::vector<int> cpus_for(const std::vector<int>& cpus, int k, bool spread);
+
+}  // namespace gcsb

@@ -50,7 +50,9 @@ GpuSink::GpuSink(const GpuSinkConfig& cfg) : cfg_(cfg) {
   slots_.resize(cfg_.slots);
   for (int i = 0; i < cfg_.slots; ++i) {
     Slot& s = slots_[i];
-    hip_check(hipHostMalloc(reinterpret_cast<void**>(&s.host), cfg_.slot_bytes, hipHostMallocDefault),
+    // NumaUser: follow the calling (pinned) thread's NUMA policy, i.e. the
+    // GPU-local node chosen by the rank's CPU plan
+    hip_check(hipHostMalloc(reinterpret_cast<void**>(&s.host), cfg_.slot_bytes, hipHostMallocNumaUser),
               "hipHostMalloc(ring slot)");
     if (cfg_.landing == Landing::kRing)
       hip_check(hipMalloc(reinterpret_cast<void**>(&s.dev_ring), cfg_.slot_bytes), "hipMalloc(ring slot)");

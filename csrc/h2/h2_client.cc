@@ -5,6 +5,7 @@
 
 #include <cstring>
 
+#include "core/affinity.h"
 #include "core/util.h"
 
 namespace gcsb {
@@ -21,7 +22,10 @@ std::shared_ptr<H2ClientConn> H2ClientConn::dial(const Endpoint& ep, const H2Cli
                                           {h2::kSettingsMaxFrameSize, opt.max_frame_size},
                                           {h2::kSettingsHeaderTableSize, opt.header_table_size}}));
   c->w_->write_window_update(0, static_cast<uint32_t>(h2::kMaxWindow - h2::kDefaultWindow));
-  c->reader_ = std::thread([raw = c.get()] { raw->reader_loop(); });
+  c->reader_ = std::thread([raw = c.get()] {
+    pin_current_thread(raw->opt_.cpus);
+    raw->reader_loop();
+  });
   return c;
 }
 

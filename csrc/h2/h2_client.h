@@ -39,6 +39,7 @@ struct H2ClientOptions {
   uint32_t initial_window = 0x7FFFFFFF;    // per-stream receive window we advertise
   uint32_t max_frame_size = (1u << 24) - 1;  // largest DATA frame we accept
   uint32_t header_table_size = 4096;
+  std::vector<int> cpus;  // pin the connection's reader thread
 };
 
 class H2ClientConn {

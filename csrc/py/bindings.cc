@@ -7,6 +7,7 @@
 #include <cstring>
 
 #include "bench/runner.h"
+#include "core/affinity.h"
 #include "core/content.h"
 #include "core/crc32c.h"
 #include "core/util.h"
@@ -58,6 +59,7 @@ ClientConfig client_from(const py::dict& d) {
   c.sock.sndbuf = get_or<int>(d, "sndbuf", 0);
   c.sock.io_timeout_ms = get_or<int>(d, "io_timeout_ms", 0);
   c.project = get_or<std::string>(d, "project", "gcs-fuse-test");
+  if (d.contains("cpus") && !d["cpus"].is_none()) c.cpus = d["cpus"].cast<std::vector<int>>();
   std::string auth = get_or<std::string>(d, "auth", "none");
   if (auth == "static") {
     c.token = std::make_shared<StaticTokenSource>(get_or<std::string>(d, "token", ""));
@@ -352,6 +354,7 @@ class PyServer {
     c.grpc_chunk = get_or<uint64_t>(d, "grpc_chunk", 2u << 20);
     c.sndbuf = get_or<int>(d, "sndbuf", 0);
     c.zero_copy = get_or<bool>(d, "zero_copy", true);
+    if (d.contains("cpus") && !d["cpus"].is_none()) c.cpus = d["cpus"].cast<std::vector<int>>();
     store_ = std::make_shared<ObjectStore>(get_or<bool>(d, "md5", true));
     srv_ = std::make_unique<FakeGcsServer>(c, store_);
   }
@@ -595,6 +598,13 @@ PYBIND11_MODULE(_native, m) {
 
   // GPU
   m.def("gpu_device_count", &gpu_device_count);
+  m.def("gpu_pci_bus_id", [](int dev) {
+    char buf[64] = {0};
+    hip_check(hipDeviceGetPCIBusId(buf, sizeof(buf), dev), "hipDeviceGetPCIBusId");
+    return std::string(buf);
+  });
+  m.def("parse_cpulist", &parse_cpulist);
+  m.def("pin_current_thread", &pin_current_thread);
   m.def("gpu_crc32c", [](int dev, uintptr_t ptr, size_t n) {
     py::gil_scoped_release nogil;
     return gpu_crc32c(dev, reinterpret_cast<const void*>(ptr), n);

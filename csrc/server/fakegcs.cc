@@ -6,6 +6,7 @@
 #include <chrono>
 #include <cstring>
 
+#include "core/affinity.h"
 #include "core/util.h"
 #include "net/buffered.h"
 
@@ -53,6 +54,7 @@ void FakeGcsServer::accept_loop() {
     }
     ++live_threads_;
     std::thread([this, fd] {
+      pin_current_thread(cfg_.cpus);
       try {
         handle_conn(fd);
       } catch (...) {

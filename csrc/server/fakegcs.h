@@ -37,6 +37,7 @@ struct ServerConfig {
   uint64_t grpc_chunk = 2 << 20;   // ReadObjectResponse content bytes per message (reference main.go:123-124)
   int sndbuf = 0;          // 0 = kernel autotuning (an explicit size disables it)
   bool zero_copy = true;   // sendfile() synthetic object bodies from a memfd
+  std::vector<int> cpus;   // pin connection/handler threads (empty = unpinned)
 };
 
 struct ServerStats {

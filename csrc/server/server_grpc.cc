@@ -15,6 +15,7 @@
 #include <set>
 #include <thread>
 
+#include "core/affinity.h"
 #include "core/crc32c.h"
 #include "core/util.h"
 #include "h2/h2.h"
@@ -218,6 +219,7 @@ class H2ServerConn {
       ++active_handlers_;
     }
     std::thread([this, s] {
+      pin_current_thread(srv_.config().cpus);
       try {
         handle(*s);
       } catch (...) {

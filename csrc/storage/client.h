@@ -36,6 +36,7 @@ struct ClientConfig {
   SocketOptions sock;
   std::shared_ptr<TokenSource> token;  // null = no Authorization header
   std::string project = "gcs-fuse-test";
+  std::vector<int> cpus;  // transport/worker thread CPU set (empty = unpinned)
 };
 
 struct ObjectMeta {

@@ -493,6 +493,7 @@ class GrpcStorageClient : public StorageClient {
     int n = std::max(1, cfg.grpc_conn_pool_size);
     conns_.resize(static_cast<size_t>(n));
     opt_.sock = cfg.sock;
+    opt_.cpus = cfg.cpus;
   }
 
   std::string transport_name() const override { return "grpc"; }

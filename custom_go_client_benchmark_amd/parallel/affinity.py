@@ -1,0 +1,97 @@
+"""GPU-local CPU placement for the transport threads of one rank.
+
+MI355X nodes (measured on the GPU box, see csrc/core/affinity.h): 2 sockets x
+64 cores (SMT2), 16 L3 domains of 8 cores, 4 GPUs per NUMA node.  One rank
+(= one GPU) gets two of its NUMA node's L3 domains: one for the client's
+receive/worker threads (which also first-touch the pinned ring, so it is
+NUMA-local to the GPU's PCIe root), one for the node-local endpoint's send
+threads.  Nothing here is needed for correctness; it removes the ~1.5x
+run-to-run swing of a single loopback stream and keeps the 8 ranks of a node
+off each other's cores.
+"""
+from __future__ import annotations
+
+import glob
+import os
+
+from .. import _native
+
+
+def _read(path: str) -> str | None:
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def gpu_local_cpus(device: int) -> list[int]:
+    """CPUs of the GPU's NUMA node (intersected with our affinity)."""
+    allowed = sorted(os.sched_getaffinity(0))
+    try:
+        bus = _native.gpu_pci_bus_id(device).lower()
+    except Exception:
+        return allowed
+    cl = _read(f"/sys/bus/pci/devices/{bus}/local_cpulist")
+    if not cl:
+        return allowed
+    local = [c for c in _native.parse_cpulist(cl) if c in set(allowed)]
+    return local or allowed
+
+
+def gpu_numa_node(device: int) -> int:
+    try:
+        bus = _native.gpu_pci_bus_id(device).lower()
+    except Exception:
+        return -1
+    v = _read(f"/sys/bus/pci/devices/{bus}/numa_node")
+    return int(v) if v and v.lstrip("-").isdigit() else -1
+
+
+def l3_groups(cpus: list[int]) -> list[list[int]]:
+    """Partition cpus by shared L3 (in first-cpu order)."""
+    groups: dict[str, list[int]] = {}
+    for c in cpus:
+        key = _read(f"/sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list") or "all"
+        groups.setdefault(key, []).append(c)
+    return sorted(groups.values(), key=lambda g: g[0])
+
+
+def plan(device: int, mode: str = "split") -> dict:
+    """CPU sets for this rank: {"client": [...], "server": [...]}.
+
+    mode: "split" (client and endpoint on two L3 domains of the GPU's node),
+          "same" (one shared L3 domain), "numa" (whole node), "none".
+    """
+    if mode == "none":
+        return {"client": [], "server": [], "mode": mode}
+    cpus = gpu_local_cpus(device)
+    if mode == "numa":
+        return {"client": cpus, "server": cpus, "mode": mode}
+    node = gpu_numa_node(device)
+    peers = []
+    for d in range(_native.gpu_device_count()):
+        if gpu_numa_node(d) == node:
+            peers.append((_native.gpu_pci_bus_id(d).lower(), d))
+    peers.sort()
+    k = [d for _, d in peers].index(device) if any(d == device for _, d in peers) else 0
+    groups = l3_groups(cpus)
+    share = max(1, len(groups) // max(1, len(peers)))
+    base = (k * share) % max(1, len(groups))
+    client = groups[base] if groups else cpus
+    if mode == "same" or share < 2:
+        server = client
+    else:
+        server = groups[(base + 1) % len(groups)]
+    return {"client": client, "server": server, "mode": mode, "numa_node": node, "gpu_index_on_node": k}
+
+
+def visible_gpu_summary() -> list[dict]:
+    out = []
+    for d in range(_native.gpu_device_count()):
+        out.append({"device": d, "bus": _native.gpu_pci_bus_id(d), "numa": gpu_numa_node(d)})
+    return out
+
+
+def list_accelerators() -> list[str]:
+    return sorted(os.path.basename(p) for p in glob.glob("/sys/class/drm/card*"))

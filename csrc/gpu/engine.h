@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "gpu/crc32c_gpu.h"
+#include "storage/client.h"
 #include "storage/sink.h"
 
 namespace gcsb {
@@ -140,6 +141,41 @@ class GpuSink : public Sink {
   uint32_t op_val_[4] = {0, 0, 0, 0};
   int op_rr_ = 0;
   GpuSinkStats stats_;
+};
+
+// Upload source for the write path (config 5): HBM -> pinned ring via
+// hipMemcpyAsync D2H on a side stream, `slots` copies kept in flight ahead of
+// the transport; the object CRC32C is computed on the GPU from HBM.
+class GpuByteSource : public ByteSource {
+ public:
+  GpuByteSource(int device, const void* dptr, uint64_t n, size_t slot_bytes, int slots, bool gpu_crc = true);
+  ~GpuByteSource() override;
+  uint64_t size() const override { return n_; }
+  std::pair<const uint8_t*, size_t> next(size_t max) override;
+  void seek(uint64_t off) override;
+  bool has_crc32c() const override { return has_crc_; }
+  uint32_t crc32c() const override { return crc_; }
+  uint64_t copies() const { return copies_; }
+
+ private:
+  void restart(uint64_t off);
+  void issue(int slot, uint64_t off);
+  int device_;
+  const uint8_t* src_;
+  uint64_t n_;
+  size_t slot_bytes_;
+  int nslots_;
+  hipStream_t stream_ = nullptr;
+  std::vector<uint8_t*> host_;
+  std::vector<hipEvent_t> ev_;
+  std::vector<uint64_t> slot_off_;  // object offset held by each slot (~0 = idle)
+  std::vector<size_t> slot_len_;
+  uint64_t pos_ = 0;        // next byte the consumer gets
+  uint64_t next_issue_ = 0; // next object offset to prefetch
+  int cur_ = 0;
+  bool has_crc_ = false;
+  uint32_t crc_ = 0;
+  uint64_t copies_ = 0;
 };
 
 // Device CRC32C of an arbitrary device range (test/verification utility).

@@ -394,6 +394,92 @@ void GpuSink::abort() {
 }
 
 // ---------------------------------------------------------------------------
+// write path: HBM -> pinned ring (D2H) -> transport
+
+GpuByteSource::GpuByteSource(int device, const void* dptr, uint64_t n, size_t slot_bytes, int slots, bool gpu_crc)
+    : device_(device),
+      src_(static_cast<const uint8_t*>(dptr)),
+      n_(n),
+      slot_bytes_(std::max<size_t>(slot_bytes, 65536)),
+      nslots_(std::max(2, slots)) {
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
+  host_.resize(nslots_);
+  ev_.resize(nslots_);
+  slot_off_.assign(nslots_, ~0ull);
+  slot_len_.assign(nslots_, 0);
+  for (int i = 0; i < nslots_; ++i) {
+    hip_check(hipHostMalloc(reinterpret_cast<void**>(&host_[i]), slot_bytes_, hipHostMallocNumaUser),
+              "hipHostMalloc(upload slot)");
+    hip_check(hipEventCreateWithFlags(&ev_[i], hipEventDisableTiming), "hipEventCreate");
+  }
+  if (gpu_crc) {
+    crc_ = gpu_crc32c(device_, src_, n_);
+    has_crc_ = true;
+  }
+  restart(0);
+}
+
+GpuByteSource::~GpuByteSource() {
+  if (stream_) (void)hipStreamSynchronize(stream_);
+  for (int i = 0; i < nslots_; ++i) {
+    if (host_[i]) (void)hipHostFree(host_[i]);
+    if (ev_[i]) (void)hipEventDestroy(ev_[i]);
+  }
+  if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+void GpuByteSource::issue(int slot, uint64_t off) {
+  size_t len = static_cast<size_t>(std::min<uint64_t>(slot_bytes_, n_ - off));
+  slot_off_[slot] = off;
+  slot_len_[slot] = len;
+  hip_check(hipMemcpyAsync(host_[slot], src_ + off, len, hipMemcpyDeviceToHost, stream_), "hipMemcpyAsync(D2H)");
+  hip_check(hipEventRecord(ev_[slot], stream_), "hipEventRecord");
+  ++copies_;
+}
+
+void GpuByteSource::restart(uint64_t off) {
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+  pos_ = off;
+  uint64_t base = off / slot_bytes_ * slot_bytes_;
+  next_issue_ = base;
+  cur_ = 0;
+  slot_off_.assign(nslots_, ~0ull);
+  for (int i = 0; i < nslots_ && next_issue_ < n_; ++i) {
+    issue(i, next_issue_);
+    next_issue_ += slot_bytes_;
+  }
+}
+
+void GpuByteSource::seek(uint64_t off) {
+  if (off == pos_) return;
+  restart(off);
+}
+
+std::pair<const uint8_t*, size_t> GpuByteSource::next(size_t max) {
+  if (pos_ >= n_ || max == 0) return {nullptr, 0};
+  // slot cur_ holds [slot_off_, slot_off_ + len) and pos_ lies inside it
+  if (slot_off_[cur_] == ~0ull || pos_ >= slot_off_[cur_] + slot_len_[cur_]) {
+    // the consumer moved past this slot: refill it far ahead, advance
+    if (slot_off_[cur_] != ~0ull && next_issue_ < n_) {
+      issue(cur_, next_issue_);
+      next_issue_ += slot_bytes_;
+    }
+    cur_ = (cur_ + 1) % nslots_;
+  }
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  hip_check(hipEventSynchronize(ev_[cur_]), "hipEventSynchronize");
+  const uint64_t so = slot_off_[cur_];
+  if (so == ~0ull || pos_ < so || pos_ >= so + slot_len_[cur_])
+    throw std::logic_error("GpuByteSource: staging ring out of step");
+  size_t k = static_cast<size_t>(std::min<uint64_t>(max, so + slot_len_[cur_] - pos_));
+  const uint8_t* p = host_[cur_] + (pos_ - so);
+  pos_ += k;
+  return {p, k};
+}
+
+// ---------------------------------------------------------------------------
 // utilities
 
 uint32_t gpu_crc32c(int device, const void* dptr, size_t n) {

@@ -236,6 +236,36 @@ class PyClient {
     return meta_dict(m);
   }
 
+  // Write path (config 5): object bytes in HBM -> pinned ring (D2H) -> upload.
+  py::dict write_from_device(const std::string& bucket, const std::string& name, uintptr_t dptr, uint64_t n,
+                             int device, bool resumable, size_t chunk_bytes, size_t slot_bytes, int slots) {
+    ObjectMeta m;
+    double crc_ms = 0, upload_ms = 0;
+    uint64_t copies = 0;
+    uint32_t crc = 0;
+    {
+      py::gil_scoped_release nogil;
+      int64_t t0 = now_ns();
+      GpuByteSource src(device, reinterpret_cast<const void*>(dptr), n, slot_bytes, slots, true);
+      int64_t t1 = now_ns();
+      WriteOptions o;
+      o.resumable = resumable;
+      o.chunk_bytes = chunk_bytes;
+      m = client_->write_object(bucket, name, src, o);
+      int64_t t2 = now_ns();
+      crc_ms = (t1 - t0) / 1e6;
+      upload_ms = (t2 - t1) / 1e6;
+      copies = src.copies();
+      crc = src.crc32c();
+    }
+    py::dict d = meta_dict(m);
+    d["gpu_crc32c"] = crc;
+    d["gpu_crc_ms"] = crc_ms;
+    d["upload_ms"] = upload_ms;
+    d["d2h_copies"] = copies;
+    return d;
+  }
+
   py::dict stats() {
     auto& s = client_->stats();
     py::dict d;
@@ -657,6 +687,9 @@ PYBIND11_MODULE(_native, m) {
       .def("list_all", &PyClient::list_all, py::arg("bucket"), py::arg("prefix") = "", py::arg("page_size") = 1000)
       .def("write_bytes", &PyClient::write_bytes, py::arg("bucket"), py::arg("name"), py::arg("data"),
            py::arg("resumable") = true, py::arg("chunk_bytes") = 16u << 20)
+      .def("write_from_device", &PyClient::write_from_device, py::arg("bucket"), py::arg("name"), py::arg("dptr"),
+           py::arg("n"), py::arg("device") = 0, py::arg("resumable") = true, py::arg("chunk_bytes") = 16u << 20,
+           py::arg("slot_bytes") = 8u << 20, py::arg("slots") = 4)
       .def("stats", &PyClient::stats);
 
   py::class_<PyRunner>(m, "Runner")

@@ -7,6 +7,7 @@
 #include <cstring>
 
 #include "core/affinity.h"
+#include "core/content.h"
 #include "core/util.h"
 #include "net/buffered.h"
 
@@ -18,6 +19,9 @@ FakeGcsServer::FakeGcsServer(ServerConfig cfg, std::shared_ptr<ObjectStore> stor
 FakeGcsServer::~FakeGcsServer() { stop(); }
 
 void FakeGcsServer::start() {
+  // build the pattern buffer (+ its memfd for sendfile) before the first
+  // request, so no read pays for it
+  if (cfg_.zero_copy) PatternBuffer::instance().memfd();
   listener_ = std::make_unique<Listener>(cfg_.host, cfg_.port);
   port_ = listener_->port();
   stopping_ = false;

@@ -1,0 +1,272 @@
+"""`gcsbench` — the benchmark CLI (reference main.go:158-220).
+
+Keeps the reference's flags, defaults and usage strings (main.go:36-57):
+
+    -worker 48  -read-call-per-worker 1000000  -bucket princer-working-dirs
+    -project gcs-fuse-test  -client-protocol http  -enable-tracing=false
+    -trace-sample-rate 1.0
+
+and its output contract as the reference's drivers expect it: one latency
+line per read on stdout ("12.345ms", so execute_pb.sh's `tr 'ms' ' '` turns
+it into a float the README histogram script can read), all
+status text on stderr.  Everything else is additive (endpoint, object naming,
+GPU sink, exporters, auth, retry knobs, multi-GPU).
+
+Fixed reference quirks: Q1 client-creation errors exit 1;
+Q2 the metric exporter flushes on exit; Q3 no shared error variable; Q9
+-client-protocol must be http|http2|grpc; Q11 first error cancels the other
+workers; Q12 optional -duration bound.
+
+Multi-GPU: launch with torchrun, one rank per GPU; rank r's workers read
+file_<r*W + w>; RCCL barriers bracket the timed region and a stats
+all-reduce produces the node view (parallel/dist.py).
+"""
+from __future__ import annotations
+
+import os
+import sys
+import time
+
+from . import _native
+from .models import workloads
+from .utils import metrics_exporter, trace_exporter
+from .utils.goflags import FlagSet
+
+
+def build_flags() -> FlagSet:
+    fs = FlagSet("gcsbench")
+    # --- reference flags (main.go:36-57), same names/defaults/usage -------------
+    fs.int("worker", 48, "Number of concurrent worker to read")
+    fs.int("read-call-per-worker", 1000000, "Number of read call per worker")
+    fs.string("bucket", "princer-working-dirs", "GCS bucket name.")
+    fs.string("project", "gcs-fuse-test", "GCP project name.")
+    fs.string("client-protocol", "http", "Network protocol.")
+    fs.bool("enable-tracing", False, "Enable tracing with Cloud Trace export")
+    fs.float("trace-sample-rate", 1.0, "Sampling rate for Cloud Trace")
+    # --- additive ---------------------------------------------------------------
+    fs.string("endpoint", "", "Storage endpoint URL (default $GCSB_ENDPOINT or $STORAGE_EMULATOR_HOST)")
+    fs.string("object-prefix", "princer_100M_files/file_", "Object name = prefix + worker id + suffix")
+    fs.string("object-suffix", "", "Object name suffix")
+    fs.string("workload", "read", "read | list-read | write")
+    fs.string("list-prefix", "", "list-read: prefix to list (default: -object-prefix)")
+    fs.int("write-objects", 1, "write: objects per rank")
+    fs.int("write-size", 64 << 20, "write: object size in bytes")
+    fs.bool("resumable", True, "write: resumable session (HTTP) / StartResumableWrite (gRPC)")
+    fs.string("http-api", "xml", "HTTP media API: xml (library default) | json (alt=media)")
+    fs.int("read-chunk", 2 << 20, "Bytes per receive into the sink (reference intent: 2 MiB buffer)")
+    fs.int("grpc-conn-pool-size", 1, "gRPC connections (reference GrpcConnPoolSize = 1)")
+    fs.int("max-conns-per-host", 100, "HTTP connection cap (reference MaxConnsPerHost = 100)")
+    fs.string("sink", "discard", "discard (reference io.Discard) | gpu (pinned ring -> HBM, CRC32C on GPU)")
+    fs.int("gpu-device", -1, "HIP device (default: LOCAL_RANK)")
+    fs.int("ring-slot-bytes", 8 << 20, "Pinned ring slot size")
+    fs.int("ring-slots", 4, "Pinned ring slots")
+    fs.string("landing", "object", "object (whole object in HBM) | ring (HBM ring, discard semantics)")
+    fs.bool("gpu-verify", True, "Verify CRC32C with the GPU kernels")
+    fs.bool("host-crc", True, "discard sink: verify CRC32C on the host (what the Go library does)")
+    fs.duration("duration", 0.0, "Stop after this long (0 = only -read-call-per-worker)")
+    fs.string("latency-file", "", "Write per-read latency lines here instead of stdout")
+    fs.string("metrics-file", "", "Prometheus text file for the read-latency view")
+    fs.string("metrics-jsonl", "", "Cloud-Monitoring-shaped JSONL time series file")
+    fs.int("metrics-port", 0, "Serve the view on 127.0.0.1:<port>/metrics")
+    fs.duration("metrics-interval", metrics_exporter.REPORTING_INTERVAL_S, "Export interval (reference: 30s)")
+    fs.string("trace-file", "traces.jsonl", "OTLP/JSON span batches (with -enable-tracing)")
+    fs.string("auth", "none", "none | static | adc | key_file")
+    fs.string("token", "", "Bearer token for -auth static")
+    fs.string("key-file", "", "Service-account JSON key (-auth key_file)")
+    fs.string("token-uri", "", "Override the key file's token_uri")
+    fs.string("user-agent", "prince", "User-Agent (reference userAgentRoundTripper)")
+    fs.duration("retry-initial", 1.0, "Initial backoff (gax default 1s)")
+    fs.duration("retry-max", 30.0, "Max backoff (reference MaxRetryDuration 30s)")
+    fs.float("retry-multiplier", 2.0, "Backoff multiplier (reference RetryMultiplier 2)")
+    fs.duration("retry-max-total", 0.0, "Give up retrying after this long (0 = never, as the reference)")
+    fs.int("retry-max-attempts", 0, "Give up after this many attempts (0 = unlimited)")
+    fs.string("affinity", "auto", "CPU placement: auto | same | split | numa | none")
+    fs.bool("start-fake-server", False, "Start a node-local synthetic GCS endpoint (no network)")
+    fs.int("fake-object-size", 100 << 20, "Synthetic object size (reference objects are ~100 MB)")
+    fs.int("fake-objects", -1, "Synthetic objects per rank (default: -worker)")
+    return fs
+
+
+def _err(msg: str):
+    sys.stderr.write(msg.rstrip("\n") + "\n")
+    sys.stderr.flush()
+
+
+def main(argv: list[str] | None = None) -> int:
+    fs = build_flags().parse(sys.argv[1:] if argv is None else argv)
+    proto = fs.get("client-protocol")
+    if proto not in ("http", "http2", "grpc"):  # Q9
+        _err(f'invalid -client-protocol "{proto}": want http, http2 or grpc')
+        return 2
+    if fs.get("worker") <= 0:
+        _err("worker count not valid")
+        return 2
+
+    from .parallel import dist
+
+    rank, world, local_rank = dist.env_rank()
+    ctx = None
+    sink = fs.get("sink")
+    device = fs.get("gpu-device") if fs.get("gpu-device") >= 0 else local_rank
+    if world > 1 or sink == "gpu":
+        ctx = dist.init(local_rank=local_rank, world=world, rank=rank)
+    workers = fs.get("worker")
+    first = rank * workers
+
+    placement = {"client": [], "server": []}
+    aff = fs.get("affinity")
+    if aff == "auto":
+        aff = "same" if sink == "gpu" else "none"
+    if aff != "none" and sink == "gpu":
+        from .parallel import affinity
+
+        placement = affinity.plan(device, aff)
+
+    endpoint = fs.get("endpoint") or os.environ.get("GCSB_ENDPOINT", "") or os.environ.get("STORAGE_EMULATOR_HOST", "")
+    ep_handle = None
+    if fs.get("start-fake-server"):
+        from . import server
+
+        n_obj = fs.get("fake-objects") if fs.get("fake-objects") >= 0 else workers
+        ep_handle = server.start_inprocess(fs.get("bucket"), fs.get("object-prefix"), fs.get("object-suffix"), first,
+                                           n_obj, fs.get("fake-object-size"), md5=True, cpus=placement["server"])
+        endpoint = ep_handle.url
+        _err(f"synthetic GCS endpoint {endpoint}: {n_obj} objects of {fs.get('fake-object-size')} bytes")
+    if not endpoint:
+        _err("while creating the client: no endpoint (set -endpoint, $GCSB_ENDPOINT or -start-fake-server; "
+             "this environment has no network)")
+        return 1
+    if endpoint and "://" not in endpoint:
+        endpoint = "http://" + endpoint
+
+    latency_fd = 1
+    lat_file = None
+    if fs.get("latency-file"):
+        lat_file = open(fs.get("latency-file"), "w")
+        latency_fd = lat_file.fileno()
+    sys.stdout.flush()
+
+    opts = workloads.RunOptions(
+        protocol=proto, endpoint=endpoint, bucket=fs.get("bucket"), object_prefix=fs.get("object-prefix"),
+        object_suffix=fs.get("object-suffix"), workers=workers, reads_per_worker=fs.get("read-call-per-worker"),
+        duration_s=fs.get("duration"), worker_id_offset=first, http_api=fs.get("http-api"),
+        read_chunk=fs.get("read-chunk"), max_conns_per_host=fs.get("max-conns-per-host"),
+        grpc_conn_pool_size=fs.get("grpc-conn-pool-size"), sink=sink, host_crc=fs.get("host-crc"), device=device,
+        ring_slot_bytes=fs.get("ring-slot-bytes"), ring_slots=fs.get("ring-slots"), landing=fs.get("landing"),
+        gpu_verify=fs.get("gpu-verify"), latency_fd=latency_fd,
+        trace_sample_rate=fs.get("trace-sample-rate") if fs.get("enable-tracing") else 0.0,
+        cpus=placement["client"], auth=fs.get("auth"), token=fs.get("token"), key_file=fs.get("key-file"),
+        token_uri=fs.get("token-uri"), user_agent=fs.get("user-agent"), retry_initial_s=fs.get("retry-initial"),
+        retry_max_s=fs.get("retry-max"), retry_multiplier=fs.get("retry-multiplier"),
+        retry_max_total_s=fs.get("retry-max-total"), retry_max_attempts=fs.get("retry-max-attempts"))
+
+    # tracing (reference main.go:162-165)
+    tracer, trace_cleanup = None, None
+    if fs.get("enable-tracing"):
+        path = fs.get("trace-file")
+        if world > 1:
+            root, ext = os.path.splitext(path)
+            path = f"{root}.rank{rank}{ext or '.jsonl'}"
+        tracer, trace_cleanup = trace_exporter.enable_trace_export(path, proto, fs.get("bucket"), gpu=sink == "gpu")
+        _err(f"trace export enabled -> {path} (sample rate {fs.get('trace-sample-rate')})")
+
+    # metrics view + exporter (reference main.go:190-197)
+    metrics_exporter.register_latency_view()
+    live = {"summary": None, "runner": None}
+
+    def source():
+        s = live["summary"]
+        return metrics_exporter.distribution_from_summary(s) if s else metrics_exporter.Distribution()
+
+    exporter = None
+    if fs.get("metrics-file") or fs.get("metrics-jsonl") or fs.get("metrics-port"):
+        sfx = f".rank{rank}" if world > 1 else ""
+        exporter = metrics_exporter.MetricsExporter(
+            source, fs.get("project"),
+            prom_file=(fs.get("metrics-file") + sfx) if fs.get("metrics-file") else "",
+            jsonl_file=(fs.get("metrics-jsonl") + sfx) if fs.get("metrics-jsonl") else "",
+            http_port=fs.get("metrics-port") + (local_rank if fs.get("metrics-port") else 0),
+            interval_s=fs.get("metrics-interval"), labels={"rank": str(rank)} if world > 1 else None).start()
+        _err("metrics exporter started successfully")
+
+    def before_start():
+        if ctx is not None:
+            dist.barrier(ctx)  # R1: synchronized start
+
+    def on_records(recs):
+        if tracer:
+            tracer.on_records(recs)
+
+    t0 = time.perf_counter()
+    rc = 0
+    try:
+        wl = fs.get("workload")
+        if wl == "read":
+            res = _run_with_live(opts, on_records, before_start, live)
+        elif wl == "list-read":
+            res = workloads.run_list_read(opts, fs.get("list-prefix") or fs.get("object-prefix"), on_records,
+                                          before_start)
+        elif wl == "write":
+            before_start()
+            res = workloads.run_write(opts, fs.get("write-objects"), fs.get("write-size"),
+                                      resumable=fs.get("resumable"))
+        else:
+            _err(f"unknown -workload {wl}")
+            return 2
+        live["summary"] = res.summary
+    except _native.StorageError as e:
+        _err(f"while creating the client: {e}")
+        return 1
+    finally:
+        if ctx is not None:
+            try:
+                dist.barrier(ctx)  # R2: synchronized stop
+            except Exception:
+                pass
+    wall = time.perf_counter() - t0
+    s = res.summary
+    if exporter:
+        exporter.close()  # flushes (reference Q2)
+    if trace_cleanup:
+        trace_cleanup()
+    if lat_file:
+        lat_file.close()
+
+    # node view (R3/R4)
+    if ctx is not None and ctx.world > 1:
+        st = dist.reduce_stats(ctx, nbytes=float(s["bytes"]), reads=float(s.get("reads", 0) + s.get("writes", 0)),
+                               errors=float(s["errors"]), wall=wall, p50=s["p50_ms"], p99=s["p99_ms"])
+        if rank == 0:
+            _err(f"node: {int(st['reads_sum'])} ops, {st['nbytes_sum'] / 2**20 / st['wall_max']:.1f} MiB/s over "
+                 f"{ctx.world} ranks; per-rank p50 {['%.2f' % x for x in st['p50_per_rank']]} ms, "
+                 f"p99 {['%.2f' % x for x in st['p99_per_rank']]} ms")
+    ops = s.get("reads", 0) or s.get("writes", 0)
+    _err(f"[rank {rank}] {ops} ops, {s['errors']} errors, {s['bytes'] / 2**20:.1f} MiB, "
+         f"p50 {s['p50_ms']:.3f} ms, p99 {s['p99_ms']:.3f} ms, {s.get('mib_per_s', 0):.1f} MiB/s")
+    if s["errors"]:
+        _err(f"Error while running benchmark: {s.get('first_error', '')}")
+        rc = 1
+    else:
+        _err("Read benchmark completed successfully!" if fs.get("workload") != "write"
+             else "Write benchmark completed successfully!")
+    if ep_handle:
+        ep_handle.stop()
+    if ctx is not None:
+        dist.shutdown(ctx)
+    return rc
+
+
+def _run_with_live(opts, on_records, before_start, live):
+    runner = _native.Runner(opts.runner_dict())
+    live["runner"] = runner
+
+    def recs(r):
+        live["summary"] = runner.summary()
+        on_records(r)
+
+    seen = workloads._drive(runner, recs, before_start=before_start)
+    return workloads.WorkloadResult(runner.summary(), seen)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

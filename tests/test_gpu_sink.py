@@ -113,3 +113,34 @@ def test_grpc_gpu_detects_corrupt_message(native, server, gpu_available):
     sink = native.GpuSink({"device": 0, "ring_slot_bytes": 4 << 20, "ring_slots": 2})
     r = c.read_gpu(B, P + "0", sink)
     assert r["crc_mismatch"] and "chunk crc32c mismatch" in r["detail"]
+
+
+@pytest.mark.parametrize("proto", ["http", "grpc"])
+@pytest.mark.parametrize("resumable", [True, False])
+def test_write_path_hbm_to_server(native, server, gpu_available, proto, resumable):
+    """Config 5: object generated in HBM (K3), D2H-staged through the pinned
+    ring, uploaded; the server verifies the GPU-computed CRC32C."""
+    import torch
+
+    size = (9 << 20) + 77
+    name = "upload/obj_3"
+    t = torch.empty(size, dtype=torch.uint8, device="cuda:0")
+    native.gpu_fill_pattern(0, t.data_ptr(), size, name, 0)
+    c = native.Client({"protocol": proto, "endpoint": server.url})
+    m = c.write_from_device(B, name, t.data_ptr(), size, 0, resumable, 4 << 20, 1 << 20, 3)
+    assert m["size"] == size and m["crc32c"] == m["gpu_crc32c"] == native.crc32c(native.object_bytes(name, 0, size))
+    assert m["d2h_copies"] >= 10
+    assert server.object_bytes(B, name, 0, size) == native.object_bytes(name, 0, size)
+
+
+def test_cli_gpu_sink(native, gpu_available):
+    import subprocess
+    import sys as _sys
+    import os as _os
+
+    root = _os.path.dirname(_os.path.dirname(_os.path.abspath(__file__)))
+    r = subprocess.run([_os.path.join(root, "gcsbench"), "-worker", "2", "-read-call-per-worker", "3",
+                        "-start-fake-server", "-fake-object-size", str(3 << 20), "-sink", "gpu",
+                        "-client-protocol", "grpc"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert len(r.stdout.strip().splitlines()) == 6

@@ -527,6 +527,51 @@ uint32_t gpu_crc32c(int device, const void* dptr, size_t n) {
   return crc;
 }
 
+double gpu_crc32c_throughput(int device, const void* dptr, size_t n, int iters, size_t seg_bytes, uint32_t* raw0) {
+  hip_check(hipSetDevice(device), "hipSetDevice");
+  const CrcTables* tabs = device_crc_tables(device);
+  hipStream_t st;
+  hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+  // one batch of up to kMaxSeg segments covering [dptr, dptr+n)
+  CrcBatch b;
+  std::memset(&b, 0, sizeof(b));
+  const uint8_t* p = static_cast<const uint8_t*>(dptr);
+  size_t off = 0;
+  while (off < n && b.nseg < static_cast<uint32_t>(kMaxSeg)) {
+    size_t len = std::min(seg_bytes, n - off);
+    b.seg[b.nseg].addr = p + off;
+    b.seg[b.nseg].len = static_cast<uint32_t>(len);
+    ++b.nseg;
+    off += len;
+  }
+  finalize_crc_batch(&b);
+  uint32_t* d_tiles = nullptr;
+  hip_check(hipMalloc(reinterpret_cast<void**>(&d_tiles), sizeof(uint32_t) * (b.total_tiles + 1)), "hipMalloc");
+  CrcSegResult* res = nullptr;
+  hip_check(hipHostMalloc(reinterpret_cast<void**>(&res), sizeof(CrcSegResult) * kMaxSeg,
+                          hipHostMallocMapped | hipHostMallocCoherent),
+            "hipHostMalloc");
+  CrcSegResult* d_res = nullptr;
+  hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_res), res, 0), "hipHostGetDevicePointer");
+  hipEvent_t e0, e1;
+  hip_check(hipEventCreate(&e0), "hipEventCreate");
+  hip_check(hipEventCreate(&e1), "hipEventCreate");
+  launch_crc32c_batch(b, tabs, d_tiles, d_res, st);  // warm-up
+  hip_check(hipEventRecord(e0, st), "hipEventRecord");
+  for (int i = 0; i < iters; ++i) launch_crc32c_batch(b, tabs, d_tiles, d_res, st);
+  hip_check(hipEventRecord(e1, st), "hipEventRecord");
+  hip_check(hipEventSynchronize(e1), "hipEventSynchronize");
+  float ms = 0;
+  hip_check(hipEventElapsedTime(&ms, e0, e1), "hipEventElapsedTime");
+  if (raw0) *raw0 = res[0].crc;
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipFree(d_tiles);
+  (void)hipHostFree(res);
+  (void)hipStreamDestroy(st);
+  return static_cast<double>(off) * iters / (ms / 1e3) / 1e9;  // GB/s over the covered bytes
+}
+
 void gpu_fill_pattern(int device, void* dptr, uint64_t n, uint64_t rot, uint64_t obj_off) {
   hip_check(hipSetDevice(device), "hipSetDevice");
   launch_fill_pattern(static_cast<uint8_t*>(dptr), n, rot, obj_off, nullptr);

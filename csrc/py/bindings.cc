@@ -643,7 +643,19 @@ PYBIND11_MODULE(_native, m) {
     py::gil_scoped_release nogil;
     gpu_fill_pattern(dev, reinterpret_cast<void*>(ptr), n, object_rotation(name), off);
   });
-  m.def("gpu_read_bytes", [](int dev, uintptr_t ptr, size_t n) {
+  m.def(
+      "gpu_crc32c_throughput",
+      [](int dev, uintptr_t ptr, size_t n, int iters, size_t seg_bytes) {
+        uint32_t c0 = 0;
+        double gbs;
+        {
+          py::gil_scoped_release nogil;
+          gbs = gpu_crc32c_throughput(dev, reinterpret_cast<const void*>(ptr), n, iters, seg_bytes, &c0);
+        }
+        return py::make_tuple(gbs, c0);
+      },
+      py::arg("device"), py::arg("ptr"), py::arg("n"), py::arg("iters") = 20, py::arg("seg_bytes") = 64u << 20);
+  m.def("gpu_read_bytes",[](int dev, uintptr_t ptr, size_t n) {
     std::string out(n, '\0');
     {
       py::gil_scoped_release nogil;

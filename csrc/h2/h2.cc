@@ -105,7 +105,7 @@ void H2Writer::write_frame_pieces(uint8_t type, uint8_t flags, uint32_t stream, 
       conn_.writev_all(iov.data(), static_cast<int>(iov.size()), /*more=*/true);
       iov.clear();
     }
-    conn_.sendfile_all(p.fd, p.foff, p.n, /*more=*/i + 1 < pieces.size());
+    conn_.sendfile_all(p.fd, p.foff, p.n, /*more=*/false);
   }
   if (!iov.empty()) conn_.writev_all(iov.data(), static_cast<int>(iov.size()));
 }
@@ -126,6 +126,25 @@ void H2Writer::write_headers(uint32_t stream, const std::string& block, bool end
     off += n;
     first = false;
   } while (off < block.size());
+}
+
+bool H2Writer::write_headers_and_data(uint32_t stream, const std::string& block, const uint8_t* p, size_t n) {
+  {
+    std::lock_guard<std::mutex> lk(fmu_);
+    auto it = stream_window_.find(stream);
+    if (dead_ || it == stream_window_.end() || block.size() > peer_max_frame_ || n > peer_max_frame_ ||
+        static_cast<int64_t>(n) > std::min(conn_window_, it->second))
+      return false;
+    conn_window_ -= static_cast<int64_t>(n);
+    it->second -= static_cast<int64_t>(n);
+  }
+  uint8_t hh[9], dh[9];
+  encode_frame_header(hh, static_cast<uint32_t>(block.size()), h2::kHeaders, h2::kFlagEndHeaders, stream);
+  encode_frame_header(dh, static_cast<uint32_t>(n), h2::kData, h2::kFlagEndStream, stream);
+  iovec iov[4] = {{hh, 9}, {const_cast<char*>(block.data()), block.size()}, {dh, 9}, {const_cast<uint8_t*>(p), n}};
+  std::lock_guard<std::mutex> lk(wmu_);
+  conn_.writev_all(iov, 4);
+  return true;
 }
 
 void H2Writer::write_window_update(uint32_t stream, uint32_t inc) {

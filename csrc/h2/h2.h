@@ -79,6 +79,11 @@ class H2Writer {
                           size_t total);
   // Header block (HEADERS + CONTINUATION as needed).
   void write_headers(uint32_t stream, const std::string& block, bool end_stream);
+  // HEADERS + one DATA frame (END_STREAM) in a single writev: a unary or
+  // server-streaming request reaches the peer in one segment.  Returns false
+  // (nothing written) if the block or the body does not fit one frame / the
+  // current send windows; the caller then sends them separately.
+  bool write_headers_and_data(uint32_t stream, const std::string& block, const uint8_t* p, size_t n);
   void write_window_update(uint32_t stream, uint32_t inc);
   void write_rst(uint32_t stream, uint32_t code);
   void write_goaway(uint32_t last_stream, uint32_t code, const std::string& msg);

@@ -84,6 +84,36 @@ void H2ClientConn::start_stream(const std::shared_ptr<H2ClientStream>& s, const 
   }
 }
 
+void H2ClientConn::start_stream_with_body(const std::shared_ptr<H2ClientStream>& s, const HeaderList& headers,
+                                          const std::string& body) {
+  std::string block;
+  enc_.encode(headers, &block);
+  {
+    std::lock_guard<std::mutex> olk(open_mu_);
+    if (!usable()) throw StorageError("http2 connection unusable: " + dead_reason_, true);
+    if (next_id_ > 0x7FFFFFF0) {
+      goaway_ = true;
+      throw StorageError("http2 stream ids exhausted", true);
+    }
+    s->id_ = next_id_;
+    next_id_ += 2;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      streams_[s->id_] = s;
+    }
+    w_->register_stream(s->id_);
+    try {
+      if (w_->write_headers_and_data(s->id_, block, reinterpret_cast<const uint8_t*>(body.data()), body.size()))
+        return;
+      w_->write_headers(s->id_, block, false);
+    } catch (const StorageError& e) {
+      dead_ = true;
+      throw;
+    }
+  }
+  send_data(*s, reinterpret_cast<const uint8_t*>(body.data()), body.size(), true);
+}
+
 void H2ClientConn::send_data(H2ClientStream& s, const uint8_t* p, size_t n, bool end_stream) {
   iovec iov{const_cast<uint8_t*>(p), n};
   send_data_iov(s, &iov, 1, end_stream);

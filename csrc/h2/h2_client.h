@@ -49,6 +49,10 @@ class H2ClientConn {
   // Registers the stream, assigns its id and sends the request headers.
   // Throws StorageError(retryable) if the connection is unusable.
   void start_stream(const std::shared_ptr<H2ClientStream>& s, const HeaderList& headers, bool end_stream);
+  // Opens a stream whose whole request body is `body` (END_STREAM on it):
+  // HEADERS and DATA leave in one write when they fit one frame each.
+  void start_stream_with_body(const std::shared_ptr<H2ClientStream>& s, const HeaderList& headers,
+                              const std::string& body);
   // Sends request body bytes honouring flow control (blocks).
   void send_data(H2ClientStream& s, const uint8_t* p, size_t n, bool end_stream);
   void send_data_iov(H2ClientStream& s, struct iovec* iov, int cnt, bool end_stream);

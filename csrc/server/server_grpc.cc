@@ -11,6 +11,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <set>
 #include <thread>
@@ -57,8 +58,13 @@ class H2ServerConn {
 
   ~H2ServerConn() {
     w_.kill();
-    std::unique_lock<std::mutex> lk(mu_);
-    cv_.wait(lk, [&] { return active_handlers_ == 0; });
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] { return active_handlers_ == 0; });
+      pool_stop_ = true;
+    }
+    pool_cv_.notify_all();
+    for (auto& t : pool_) t.join();
   }
 
   void run() {
@@ -218,17 +224,36 @@ class H2ServerConn {
       std::lock_guard<std::mutex> lk(mu_);
       ++active_handlers_;
     }
-    std::thread([this, s] {
-      pin_current_thread(srv_.config().cpus);
+    // handler threads are pooled per connection: a stream costs one futex
+    // wake, not a thread creation (the per-read fixed cost of small objects)
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      queue_.push_back(s);
+      if (idle_ == 0) pool_.emplace_back([this] { pool_loop(); });
+    }
+    pool_cv_.notify_one();
+  }
+
+  void pool_loop() {
+    pin_current_thread(srv_.config().cpus);
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      ++idle_;
+      pool_cv_.wait(lk, [&] { return pool_stop_ || !queue_.empty(); });
+      --idle_;
+      if (queue_.empty()) return;  // stopping
+      auto s = std::move(queue_.front());
+      queue_.pop_front();
+      lk.unlock();
       try {
         handle(*s);
       } catch (...) {
       }
       w_.unregister_stream(s->id);
-      std::lock_guard<std::mutex> lk(mu_);
+      lk.lock();
       streams_.erase(s->id);
       if (--active_handlers_ == 0) cv_.notify_all();
-    }).detach();
+    }
   }
 
   // --- responses ------------------------------------------------------------
@@ -627,6 +652,11 @@ class H2ServerConn {
   std::mutex mu_;
   std::condition_variable cv_;
   int active_handlers_ = 0;
+  std::vector<std::thread> pool_;
+  std::deque<std::shared_ptr<ServerStream>> queue_;
+  std::condition_variable pool_cv_;
+  int idle_ = 0;
+  bool pool_stop_ = false;
   std::map<uint32_t, std::shared_ptr<ServerStream>> streams_;
 };
 

@@ -267,8 +267,10 @@ class ReadObjectHandler : public MessageHandler {
             k = 0;
             break;
           }
-          size_t m = std::min<uint64_t>(k, w.cap);
-          bc.read_exact(w.ptr, m);
+          // commit whatever the socket has now (not the whole frame), so the
+          // sink's CRC / slot hand-off overlaps the rest of the frame arriving
+          size_t m = bc.read_some(w.ptr, std::min<uint64_t>(k, w.cap));
+          if (m == 0) throw StorageError("connection closed inside a DATA frame", true);
           if (!rr_->first_byte_ns) rr_->first_byte_ns = now_ns();
           try {
             sink_.commit(m);
@@ -537,10 +539,9 @@ class GrpcStorageClient : public StorageClient {
     BufferingHandler h;
     auto call = std::make_shared<GrpcCall>(&h);
     auto c = conn();
-    c->start_stream(call, headers(method, bucket_res), false);
     std::string f = frame(req);
     try {
-      c->send_data(*call, reinterpret_cast<const uint8_t*>(f.data()), f.size(), true);
+      c->start_stream_with_body(call, headers(method, bucket_res), f);
       call->wait_ok();
     } catch (...) {
       c->end_stream(*call, true);
@@ -571,10 +572,9 @@ class GrpcStorageClient : public StorageClient {
     auto call = std::make_shared<GrpcCall>(&h);
     raw = call.get();
     auto c = conn();
-    c->start_stream(call, headers("ReadObject", q.bucket), false);
     std::string f = frame(v2::encode_read_request(q));
     try {
-      c->send_data(*call, reinterpret_cast<const uint8_t*>(f.data()), f.size(), true);
+      c->start_stream_with_body(call, headers("ReadObject", q.bucket), f);
       call->wait_ok();
     } catch (...) {
       c->end_stream(*call, true);

@@ -20,6 +20,7 @@ void DiscardSink::begin(const ObjectInfo& info) {
   bytes_ = 0;
   obj_crc_ = 0;
   chunk_crc_ = 0;
+  chunk_len_ = 0;
   in_chunk_ = false;
   chunk_partial_ = false;
   mismatch_ = false;
@@ -43,16 +44,28 @@ Window DiscardSink::acquire(size_t want) {
 }
 
 void DiscardSink::commit(size_t n) {
+  // each byte is CRC'd once: inside a chunk into the chunk CRC (combined
+  // into the object CRC at chunk end), outside directly into the object CRC
   if (host_crc_) {
-    obj_crc_ = crc32c_extend(obj_crc_, buf_, n);
-    if (in_chunk_) chunk_crc_ = crc32c_extend(chunk_crc_, buf_, n);
+    if (in_chunk_) {
+      chunk_crc_ = crc32c_extend(chunk_crc_, buf_, n);
+      chunk_len_ += n;
+    } else {
+      obj_crc_ = crc32c_extend(obj_crc_, buf_, n);
+    }
   }
   bytes_ += n;
 }
 
-void DiscardSink::chunk_begin(size_t) {
-  in_chunk_ = true;
+void DiscardSink::fold_chunk() {
+  if (in_chunk_ && chunk_len_) obj_crc_ = crc32c_combine(obj_crc_, chunk_crc_, chunk_len_);
   chunk_crc_ = 0;
+  chunk_len_ = 0;
+}
+
+void DiscardSink::chunk_begin(size_t) {
+  fold_chunk();
+  in_chunk_ = true;
 }
 
 void DiscardSink::chunk_end(bool has_crc, uint32_t crc) {
@@ -65,6 +78,7 @@ void DiscardSink::chunk_end(bool has_crc, uint32_t crc) {
       detail_ = b;
     }
   }
+  fold_chunk();
   in_chunk_ = false;
   chunk_partial_ = false;
 }
@@ -74,11 +88,14 @@ void DiscardSink::resume_at(int64_t offset) {
   // itself can no longer be checked on its own.
   (void)offset;
   if (in_chunk_) chunk_partial_ = true;
+  fold_chunk();
   in_chunk_ = false;
 }
 
 SinkResult DiscardSink::finish() {
   SinkResult r;
+  fold_chunk();
+  in_chunk_ = false;
   r.bytes = bytes_;
   r.landed_ns = now_ns();
   r.computed_crc32c = obj_crc_;

@@ -85,8 +85,10 @@ class DiscardSink : public Sink {
   ObjectInfo info_;
   uint64_t bytes_ = 0;
   uint32_t obj_crc_ = 0;     // running standard crc of all delivered bytes
-  uint32_t chunk_crc_ = 0;
+  uint32_t chunk_crc_ = 0;    // crc of the open chunk's bytes, folded into obj_crc_ at its end
+  uint64_t chunk_len_ = 0;
   bool in_chunk_ = false;
+  void fold_chunk();
   bool chunk_partial_ = false;
   bool mismatch_ = false;
   bool any_checked_ = false;

@@ -23,6 +23,7 @@ all-reduce produces the node view (parallel/dist.py).
 """
 from __future__ import annotations
 
+import json
 import os
 import sys
 import time
@@ -84,6 +85,7 @@ def build_flags() -> FlagSet:
     fs.bool("start-fake-server", False, "Start a node-local synthetic GCS endpoint (no network)")
     fs.int("fake-object-size", 100 << 20, "Synthetic object size (reference objects are ~100 MB)")
     fs.int("fake-objects", -1, "Synthetic objects per rank (default: -worker)")
+    fs.string("summary-json", "", "Write the run summary (p50/p99/MiB/s, node view) as JSON here")
     return fs
 
 
@@ -240,6 +242,14 @@ def main(argv: list[str] | None = None) -> int:
             _err(f"node: {int(st['reads_sum'])} ops, {st['nbytes_sum'] / 2**20 / st['wall_max']:.1f} MiB/s over "
                  f"{ctx.world} ranks; per-rank p50 {['%.2f' % x for x in st['p50_per_rank']]} ms, "
                  f"p99 {['%.2f' % x for x in st['p99_per_rank']]} ms")
+    if fs.get("summary-json") and rank == 0:
+        out = {k: v for k, v in s.items() if isinstance(v, (int, float, str, bool))}
+        out.update({"workload": fs.get("workload"), "protocol": proto, "sink": sink, "workers": workers,
+                    "world": world, "wall_s": wall, "extra": res.extra})
+        if ctx is not None and ctx.world > 1:
+            out["node"] = st
+        with open(fs.get("summary-json"), "w") as f:
+            json.dump(out, f, indent=1, default=str)
     ops = s.get("reads", 0) or s.get("writes", 0)
     _err(f"[rank {rank}] {ops} ops, {s['errors']} errors, {s['bytes'] / 2**20:.1f} MiB, "
          f"p50 {s['p50_ms']:.3f} ms, p99 {s['p99_ms']:.3f} ms, {s.get('mib_per_s', 0):.1f} MiB/s")

@@ -5,6 +5,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <stdexcept>
 
 #include "core/crc32c.h"
@@ -20,6 +22,83 @@ bool debug_ring() {
   }();
   return d;
 }
+
+// Per-device resources reused across calls: a stream for one-off CRC jobs,
+// host-mapped result slots and a tile scratch buffer.  Creating these per
+// call (streams, hipHostMalloc, hipMalloc) cost milliseconds per upload.
+struct DeviceCtx {
+  std::mutex mu;  // one gpu_crc32c job at a time per device
+  hipStream_t st = nullptr;
+  CrcSegResult* res = nullptr;
+  CrcSegResult* d_res = nullptr;
+  uint32_t* d_tiles = nullptr;
+  size_t tiles_cap = 0;
+};
+
+DeviceCtx& device_ctx(int dev) {
+  static std::mutex mu;
+  static std::map<int, std::unique_ptr<DeviceCtx>> ctx;
+  std::lock_guard<std::mutex> lk(mu);
+  auto& c = ctx[dev];
+  if (!c) {
+    auto n = std::make_unique<DeviceCtx>();
+    hip_check(hipStreamCreateWithFlags(&n->st, hipStreamNonBlocking), "hipStreamCreate");
+    hip_check(hipHostMalloc(reinterpret_cast<void**>(&n->res), sizeof(CrcSegResult) * kMaxSeg,
+                            hipHostMallocMapped | hipHostMallocCoherent),
+              "hipHostMalloc(results)");
+    hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&n->d_res), n->res, 0), "hipHostGetDevicePointer");
+    c = std::move(n);
+  }
+  return *c;
+}
+
+// Page-locked staging buffers recycled by size (upload rings, per-call
+// sinks): hipHostMalloc of tens of MiB is far slower than the D2H it feeds.
+class PinnedPool {
+ public:
+  static void* get(size_t n) {
+    {
+      std::lock_guard<std::mutex> lk(mu());
+      auto it = free_list().find(n);
+      if (it != free_list().end()) {
+        void* p = it->second;
+        free_list().erase(it);
+        held() -= n;
+        return p;
+      }
+    }
+    void* p = nullptr;
+    hip_check(hipHostMalloc(&p, n, hipHostMallocNumaUser), "hipHostMalloc(staging)");
+    return p;
+  }
+  static void put(void* p, size_t n) {
+    if (!p) return;
+    {
+      std::lock_guard<std::mutex> lk(mu());
+      if (held() + n <= kMaxHeld) {
+        free_list().emplace(n, p);
+        held() += n;
+        return;
+      }
+    }
+    (void)hipHostFree(p);
+  }
+
+ private:
+  static constexpr size_t kMaxHeld = size_t(1) << 30;
+  static std::mutex& mu() {
+    static std::mutex m;
+    return m;
+  }
+  static std::multimap<size_t, void*>& free_list() {
+    static std::multimap<size_t, void*> f;
+    return f;
+  }
+  static size_t& held() {
+    static size_t h = 0;
+    return h;
+  }
+};
 }  // namespace
 
 int gpu_device_count() {
@@ -52,8 +131,7 @@ GpuSink::GpuSink(const GpuSinkConfig& cfg) : cfg_(cfg) {
     Slot& s = slots_[i];
     // NumaUser: follow the calling (pinned) thread's NUMA policy, i.e. the
     // GPU-local node chosen by the rank's CPU plan
-    hip_check(hipHostMalloc(reinterpret_cast<void**>(&s.host), cfg_.slot_bytes, hipHostMallocNumaUser),
-              "hipHostMalloc(ring slot)");
+    s.host = static_cast<uint8_t*>(PinnedPool::get(cfg_.slot_bytes));
     if (cfg_.landing == Landing::kRing)
       hip_check(hipMalloc(reinterpret_cast<void**>(&s.dev_ring), cfg_.slot_bytes), "hipMalloc(ring slot)");
     hip_check(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming), "hipEventCreate");
@@ -70,7 +148,7 @@ GpuSink::~GpuSink() {
   } catch (...) {
   }
   for (Slot& s : slots_) {
-    if (s.host) (void)hipHostFree(s.host);
+    PinnedPool::put(s.host, cfg_.slot_bytes);
     if (s.dev_ring) (void)hipFree(s.dev_ring);
     if (s.ev) (void)hipEventDestroy(s.ev);
     if (s.copied) (void)hipEventDestroy(s.copied);
@@ -409,8 +487,7 @@ GpuByteSource::GpuByteSource(int device, const void* dptr, uint64_t n, size_t sl
   slot_off_.assign(nslots_, ~0ull);
   slot_len_.assign(nslots_, 0);
   for (int i = 0; i < nslots_; ++i) {
-    hip_check(hipHostMalloc(reinterpret_cast<void**>(&host_[i]), slot_bytes_, hipHostMallocNumaUser),
-              "hipHostMalloc(upload slot)");
+    host_[i] = static_cast<uint8_t*>(PinnedPool::get(slot_bytes_));
     hip_check(hipEventCreateWithFlags(&ev_[i], hipEventDisableTiming), "hipEventCreate");
   }
   if (gpu_crc) {
@@ -423,7 +500,7 @@ GpuByteSource::GpuByteSource(int device, const void* dptr, uint64_t n, size_t sl
 GpuByteSource::~GpuByteSource() {
   if (stream_) (void)hipStreamSynchronize(stream_);
   for (int i = 0; i < nslots_; ++i) {
-    if (host_[i]) (void)hipHostFree(host_[i]);
+    PinnedPool::put(host_[i], slot_bytes_);
     if (ev_[i]) (void)hipEventDestroy(ev_[i]);
   }
   if (stream_) (void)hipStreamDestroy(stream_);
@@ -483,47 +560,38 @@ std::pair<const uint8_t*, size_t> GpuByteSource::next(size_t max) {
 // utilities
 
 uint32_t gpu_crc32c(int device, const void* dptr, size_t n) {
+  if (n == 0) return 0;
   hip_check(hipSetDevice(device), "hipSetDevice");
   const CrcTables* tabs = device_crc_tables(device);
-  hipStream_t st;
-  hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
-  const size_t kSeg = 1u << 30;
-  std::vector<CrcSeg> segs;
+  DeviceCtx& c = device_ctx(device);
+  std::lock_guard<std::mutex> lk(c.mu);
+  // kMaxSeg segments per batch (>= 1 MiB, 4 KiB multiples): K1 covers every
+  // tile in parallel and K2 folds with kMaxSeg workgroups, not one.
+  size_t seg = (n + kMaxSeg - 1) / kMaxSeg;
+  seg = std::min<size_t>(std::max<size_t>((seg + kCrcTile - 1) / kCrcTile * kCrcTile, 1u << 20), 1u << 30);
   const uint8_t* p = static_cast<const uint8_t*>(dptr);
-  for (size_t off = 0; off < n || (n == 0 && off == 0); off += kSeg) {
-    CrcSeg s{};
-    s.addr = p + off;
-    s.len = static_cast<uint32_t>(n - off < kSeg ? n - off : kSeg);
-    segs.push_back(s);
-    if (n == 0) break;
-  }
   uint32_t crc = 0;
-  uint64_t total = 0;
-  CrcSegResult* res = nullptr;
-  hip_check(hipHostMalloc(reinterpret_cast<void**>(&res), sizeof(CrcSegResult) * kMaxSeg,
-                          hipHostMallocMapped | hipHostMallocCoherent),
-            "hipHostMalloc");
-  uint32_t* d_tiles = nullptr;
-  for (size_t i0 = 0; i0 < segs.size(); i0 += kMaxSeg) {
+  size_t off = 0;
+  while (off < n) {
     CrcBatch b;
     std::memset(&b, 0, sizeof(b));
-    b.nseg = static_cast<uint32_t>(std::min<size_t>(kMaxSeg, segs.size() - i0));
-    for (uint32_t i = 0; i < b.nseg; ++i) b.seg[i] = segs[i0 + i];
-    finalize_crc_batch(&b);
-    if (d_tiles) (void)hipFree(d_tiles);
-    hip_check(hipMalloc(reinterpret_cast<void**>(&d_tiles), sizeof(uint32_t) * (b.total_tiles + 1)), "hipMalloc");
-    CrcSegResult* d_res = nullptr;
-    hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_res), res, 0), "hipHostGetDevicePointer");
-    launch_crc32c_batch(b, tabs, d_tiles, d_res, st);
-    hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
-    for (uint32_t i = 0; i < b.nseg; ++i) {
-      crc = crc32c_combine(crc, res[i].crc, b.seg[i].len);
-      total += b.seg[i].len;
+    while (off < n && b.nseg < static_cast<uint32_t>(kMaxSeg)) {
+      size_t len = std::min(seg, n - off);
+      b.seg[b.nseg].addr = p + off;
+      b.seg[b.nseg].len = static_cast<uint32_t>(len);
+      ++b.nseg;
+      off += len;
     }
+    finalize_crc_batch(&b);
+    if (b.total_tiles + 1 > c.tiles_cap) {
+      if (c.d_tiles) (void)hipFree(c.d_tiles);
+      c.tiles_cap = b.total_tiles + 1;
+      hip_check(hipMalloc(reinterpret_cast<void**>(&c.d_tiles), sizeof(uint32_t) * c.tiles_cap), "hipMalloc(tiles)");
+    }
+    launch_crc32c_batch(b, tabs, c.d_tiles, c.d_res, c.st);
+    hip_check(hipStreamSynchronize(c.st), "hipStreamSynchronize");
+    for (uint32_t i = 0; i < b.nseg; ++i) crc = crc32c_combine(crc, c.res[i].crc, b.seg[i].len);
   }
-  if (d_tiles) (void)hipFree(d_tiles);
-  (void)hipHostFree(res);
-  (void)hipStreamDestroy(st);
   return crc;
 }
 

@@ -223,11 +223,15 @@ class PyClient {
 
   py::dict write_bytes(const std::string& bucket, const std::string& name, const py::bytes& data, bool resumable,
                        size_t chunk_bytes) {
-    std::string buf = data;
+    // bytes are immutable and `data` holds a reference: upload straight from
+    // the Python buffer, without a copy
+    char* ptr = nullptr;
+    Py_ssize_t len = 0;
+    if (PyBytes_AsStringAndSize(data.ptr(), &ptr, &len) != 0) throw py::error_already_set();
     ObjectMeta m;
     {
       py::gil_scoped_release nogil;
-      HostByteSource src(reinterpret_cast<const uint8_t*>(buf.data()), buf.size());
+      HostByteSource src(reinterpret_cast<const uint8_t*>(ptr), static_cast<size_t>(len));
       WriteOptions o;
       o.resumable = resumable;
       o.chunk_bytes = chunk_bytes;
@@ -386,6 +390,7 @@ class PyServer {
     c.zero_copy = get_or<bool>(d, "zero_copy", true);
     if (d.contains("cpus") && !d["cpus"].is_none()) c.cpus = d["cpus"].cast<std::vector<int>>();
     store_ = std::make_shared<ObjectStore>(get_or<bool>(d, "md5", true));
+    store_->set_retain_uploads(get_or<bool>(d, "retain_uploads", true));
     srv_ = std::make_unique<FakeGcsServer>(c, store_);
   }
   void start() { srv_->start(); }
@@ -402,7 +407,9 @@ class PyServer {
   }
   py::dict add_object(const std::string& bucket, const std::string& name, const py::bytes& data) {
     std::string s = data;
-    auto o = store_->put(bucket, name, std::vector<uint8_t>(s.begin(), s.end()), "");
+    Blob b;
+    b.append(s.data(), s.size());
+    auto o = store_->put(bucket, name, std::move(b), "");
     py::dict d;
     d["size"] = o->size;
     d["crc32c"] = o->crc32c;
@@ -415,7 +422,7 @@ class PyServer {
     py::dict d;
     d["size"] = o->size;
     d["crc32c"] = o->crc32c;
-    d["md5"] = py::bytes(o->md5);
+    d["md5"] = py::bytes(o->md5());
     d["generation"] = o->generation;
     d["synthetic"] = o->synthetic;
     d["rotation"] = o->rot;

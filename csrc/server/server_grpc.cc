@@ -32,11 +32,36 @@ enum GrpcCode {
   kInternal = 13, kUnavailable = 14, kDataLoss = 15, kUnauthenticated = 16, kResourceExhausted = 8
 };
 
+// Unparsed request bytes of a stream; grows without zero-filling (upload
+// DATA frames are MiBs each) and keeps its capacity across messages.
+struct RecvBuf {
+  std::unique_ptr<char[]> p;
+  size_t n = 0, cap = 0;
+  char* grow(size_t k) {
+    if (n + k > cap) {
+      size_t c = std::max(n + k, cap * 2);
+      std::unique_ptr<char[]> q(new char[c]);
+      if (n) std::memcpy(q.get(), p.get(), n);
+      p = std::move(q);
+      cap = c;
+    }
+    char* d = p.get() + n;
+    n += k;
+    return d;
+  }
+  void consume(size_t k) {
+    if (k < n) std::memmove(p.get(), p.get() + k, n - k);
+    n -= k;
+  }
+  const char* data() const { return p.get(); }
+  size_t size() const { return n; }
+};
+
 struct ServerStream {
   uint32_t id = 0;
   HeaderList headers;
   std::string path, authorization;
-  std::string buf;  // unparsed request bytes
+  RecvBuf buf;  // unparsed request bytes
   std::vector<std::string> messages;
   std::atomic<bool> cancelled{false};
   bool half_closed = false;
@@ -111,9 +136,7 @@ class H2ServerConn {
             }
             auto s = find(fh.stream);
             if (s) {
-              size_t old = s->buf.size();
-              s->buf.resize(old + n);
-              if (n) bc_.read_exact(&s->buf[old], n);
+              if (n) bc_.read_exact(s->buf.grow(n), n);
               srv_.stats().bytes_received += n;
             } else {
               bc_.skip(n);
@@ -122,8 +145,10 @@ class H2ServerConn {
             if (uint32_t inc = conn_rw_.consume(fh.length)) w_.write_window_update(0, inc);
             if (s) {
               if (uint32_t inc = s->rw.consume(fh.length)) w_.write_window_update(fh.stream, inc);
-              split_messages(*s);
-              if (s->path == "WriteObject") process_write_messages(*s);
+              if (s->path == "WriteObject")
+                process_write_buffer(*s);  // in place: no per-message copies
+              else
+                split_messages(*s);
               if (fh.flags & h2::kFlagEndStream) dispatch(s);
             }
             break;
@@ -205,15 +230,24 @@ class H2ServerConn {
     if (end_stream) dispatch(s);
   }
 
-  static void split_messages_into(std::string& buf, std::vector<std::string>* out) {
+  // Calls f(message) for every complete length-prefixed message in buf,
+  // then drops them from buf.
+  template <typename F>
+  static void for_each_message(RecvBuf& buf, F&& f) {
     size_t pos = 0;
     while (buf.size() - pos >= 5) {
       uint32_t len = be32(reinterpret_cast<const uint8_t*>(buf.data() + pos + 1));
       if (buf.size() - pos - 5 < len) break;
-      out->emplace_back(buf, pos + 5, len);
+      f(std::string_view(buf.data() + pos + 5, len));
       pos += 5 + len;
     }
-    if (pos) buf.erase(0, pos);
+    if (pos) buf.consume(pos);
+  }
+  static void split_messages_into(RecvBuf& buf, std::vector<std::string>* out) {
+    for_each_message(buf, [&](std::string_view m) { out->emplace_back(m); });
+  }
+  void process_write_buffer(ServerStream& s) {
+    for_each_message(s.buf, [&](std::string_view m) { process_write_message(s, m); });
   }
   void split_messages(ServerStream& s) { split_messages_into(s.buf, &s.messages); }
 
@@ -344,7 +378,7 @@ class H2ServerConn {
     return false;
   }
 
-  v2::Object to_v2(const StoredObject& o) {
+  v2::Object to_v2(const StoredObject& o, bool force_md5 = true) {
     v2::Object v;
     v.name = o.name;
     v.bucket = v2::bucket_resource(o.bucket);
@@ -354,7 +388,7 @@ class H2ServerConn {
     v.content_type = o.content_type;
     v.has_crc32c = true;
     v.crc32c = o.crc32c;
-    v.md5 = o.md5;
+    if (force_md5 || o.md5_ready()) v.md5 = o.md5();
     v.create_time_s = o.created_us / 1000000;
     v.create_time_ns = static_cast<int32_t>((o.created_us % 1000000) * 1000);
     v.update_time_s = v.create_time_s;
@@ -392,6 +426,9 @@ class H2ServerConn {
       return send_trailers(s.id, kNotFound, "No such object: " + v2::bucket_from_resource(q.bucket) + "/" + q.object,
                            false);
     if (maybe_fail(s)) return;
+    if (o->hollow)
+      return send_trailers(s.id, kFailedPrecondition,
+                           "object content was not retained (server retain_uploads=false)", false);
     int64_t start = q.read_offset;
     if (start < 0) start = std::max<int64_t>(0, static_cast<int64_t>(o->size) + start);
     if (static_cast<uint64_t>(start) > o->size)
@@ -402,7 +439,7 @@ class H2ServerConn {
     if (int lat = f.latency_ms.load()) std::this_thread::sleep_for(std::chrono::milliseconds(lat));
     send_headers(s.id);
     const uint64_t chunk = srv_.config().grpc_chunk;
-    const std::string checksums = v2::encode_checksums(true, o->crc32c, o->md5);
+    const std::string checksums = v2::encode_checksums(true, o->crc32c, o->md5());
     v2::ContentRange cr;
     cr.start = start;
     cr.end = static_cast<int64_t>(end);
@@ -523,65 +560,50 @@ class H2ServerConn {
 
   // Called on the reader thread as WriteObject messages complete.
   void process_write_messages(ServerStream& s) {
-    for (auto& m : s.messages) {
-      if (s.write_error || s.write_finished) continue;
-      v2::WriteObjectRequestView w;
-      if (!v2::decode_write_request(m, &w)) {
-        s.write_error = true;
-        s.write_code = kInvalidArgument;
-        s.write_msg = "bad WriteObjectRequest";
-        continue;
-      }
-      if (s.write_first) {
-        s.write_first = false;
-        if (!w.upload_id.empty()) {
-          s.session = srv_.store().find_upload(w.upload_id);
-          if (!s.session) {
-            s.write_error = true;
-            s.write_code = kNotFound;
-            s.write_msg = "no such upload " + w.upload_id;
-            continue;
-          }
-        } else if (w.has_spec) {
-          s.session = srv_.store().start_upload(v2::bucket_from_resource(w.spec.resource.bucket),
-                                                w.spec.resource.name, w.spec.resource.content_type,
-                                                w.spec.object_size);
-        } else {
-          s.write_error = true;
-          s.write_code = kInvalidArgument;
-          s.write_msg = "first WriteObjectRequest needs upload_id or write_object_spec";
-          continue;
-        }
-      }
-      UploadSession& u = *s.session;
-      std::lock_guard<std::mutex> lk(u.mu);
-      if (w.write_offset != static_cast<int64_t>(u.data.size())) {
-        if (w.write_offset < static_cast<int64_t>(u.data.size()) &&
-            w.write_offset + static_cast<int64_t>(w.content.size()) <= static_cast<int64_t>(u.data.size())) {
-          // retransmission of persisted bytes: ignore
-        } else {
-          s.write_error = true;
-          s.write_code = kFailedPrecondition;
-          s.write_msg = "write_offset " + std::to_string(w.write_offset) + " != persisted size " +
-                        std::to_string(u.data.size());
-          continue;
-        }
-      } else if (w.has_data) {
-        if (w.has_content_crc && crc32c(w.content.data(), w.content.size()) != w.content_crc) {
-          s.write_error = true;
-          s.write_code = kDataLoss;
-          s.write_msg = "ChecksummedData crc32c mismatch";
-          continue;
-        }
-        u.data.insert(u.data.end(), w.content.begin(), w.content.end());
-      }
-      if (w.has_object_crc) {
-        u.has_crc = true;
-        u.crc = w.object_crc;
-      }
-      if (w.finish_write) s.write_finished = true;
-    }
+    for (auto& m : s.messages) process_write_message(s, m);
     s.messages.clear();
+  }
+
+  void process_write_message(ServerStream& s, std::string_view m) {
+    if (s.write_error || s.write_finished) return;
+    auto fail = [&](int code, std::string msg) {
+      s.write_error = true;
+      s.write_code = code;
+      s.write_msg = std::move(msg);
+    };
+    v2::WriteObjectRequestView w;
+    if (!v2::decode_write_request(m, &w)) return fail(kInvalidArgument, "bad WriteObjectRequest");
+    if (s.write_first) {
+      s.write_first = false;
+      if (!w.upload_id.empty()) {
+        s.session = srv_.store().find_upload(w.upload_id);
+        if (!s.session) return fail(kNotFound, "no such upload " + w.upload_id);
+      } else if (w.has_spec) {
+        s.session = srv_.store().start_upload(v2::bucket_from_resource(w.spec.resource.bucket), w.spec.resource.name,
+                                              w.spec.resource.content_type, w.spec.object_size);
+      } else {
+        return fail(kInvalidArgument, "first WriteObjectRequest needs upload_id or write_object_spec");
+      }
+    }
+    UploadSession& u = *s.session;
+    std::lock_guard<std::mutex> lk(u.mu);
+    const int64_t persisted = static_cast<int64_t>(u.received);
+    if (w.write_offset != persisted) {
+      // a retransmission of persisted bytes is ignored; a gap is an error
+      if (!(w.write_offset < persisted && w.write_offset + static_cast<int64_t>(w.content.size()) <= persisted))
+        return fail(kFailedPrecondition, "write_offset " + std::to_string(w.write_offset) + " != persisted size " +
+                                             std::to_string(persisted));
+    } else if (w.has_data) {
+      // one CRC pass: checks the message and extends the object CRC
+      const uint32_t c = crc32c(w.content.data(), w.content.size());
+      if (w.has_content_crc && c != w.content_crc) return fail(kDataLoss, "ChecksummedData crc32c mismatch");
+      u.append_with_crc(w.content.data(), w.content.size(), c);
+    }
+    if (w.has_object_crc) {
+      u.has_crc = true;
+      u.crc = w.object_crc;
+    }
+    if (w.finish_write) s.write_finished = true;
   }
 
   void write_object_done(ServerStream& s) {
@@ -594,10 +616,10 @@ class H2ServerConn {
       auto o = srv_.store().finalize_upload(*s.session, &err);
       if (!o) return send_trailers(s.id, kInvalidArgument, err, false);
       st.has_resource = true;
-      st.resource = to_v2(*o);
+      st.resource = to_v2(*o, false);
     } else {
       std::lock_guard<std::mutex> lk(s.session->mu);
-      st.persisted_size = static_cast<int64_t>(s.session->data.size());
+      st.persisted_size = static_cast<int64_t>(s.session->received);
     }
     send_headers(s.id);
     send_message(s, v2::encode_write_status(st));
@@ -632,9 +654,9 @@ class H2ServerConn {
       std::lock_guard<std::mutex> lk(u->mu);
       if (u->finalized) {
         st.has_resource = true;
-        st.resource = to_v2(*u->result);
+        st.resource = to_v2(*u->result, false);
       } else {
-        st.persisted_size = static_cast<int64_t>(u->data.size());
+        st.persisted_size = static_cast<int64_t>(u->received);
       }
     }
     send_headers(s.id);

@@ -25,6 +25,10 @@ struct Request {
   std::vector<std::pair<std::string, std::string>> query;
   Headers headers;
   std::string body;
+  // Resumable-upload chunk bodies are not buffered: the handler streams them
+  // from the socket (CRC + store while the client is still sending).  Bytes
+  // of a deferred body not consumed by the handler are drained after it.
+  uint64_t deferred = 0;
   const std::string* header(std::string_view n) const { return find_header(headers, n); }
   std::string q(const std::string& k, const std::string& dflt = "") const {
     for (const auto& kv : query)
@@ -113,7 +117,7 @@ std::string json_error(int code, const std::string& msg, const std::string& reas
   return e.dump();
 }
 
-Json object_json(const StoredObject& o) {
+Json object_json(const StoredObject& o, bool force_md5 = true) {
   Json j = Json::object();
   j.set("kind", Json::str("storage#object"));
   j.set("id", Json::str(o.bucket + "/" + o.name + "/" + std::to_string(o.generation)));
@@ -127,7 +131,7 @@ Json object_json(const StoredObject& o) {
   j.set("contentType", Json::str(o.content_type));
   j.set("storageClass", Json::str("STANDARD"));
   j.set("size", Json::str(std::to_string(o.size)));
-  if (!o.md5.empty()) j.set("md5Hash", Json::str(base64_encode(o.md5)));
+  if ((force_md5 || o.md5_ready()) && !o.md5().empty()) j.set("md5Hash", Json::str(base64_encode(o.md5())));
   j.set("crc32c", Json::str(crc32c_b64(o.crc32c)));
   j.set("etag", Json::str("CK" + std::to_string(o.generation % 1000000) + "E="));
   j.set("timeCreated", Json::str(rfc3339(o.created_us)));
@@ -142,6 +146,10 @@ class Http1Handler {
   void run() {
     for (;;) {
       Request r;
+      // request bodies (upload chunks) land in a buffer reused across the
+      // connection's requests: warm pages instead of fresh faults per chunk
+      r.body.swap(body_buf_);
+      r.body.clear();
       try {
         if (!read_request(&r)) return;
       } catch (const StorageError&) {
@@ -152,6 +160,7 @@ class Http1Handler {
       if (const auto* cn = r.header("Connection"); cn && iequals(*cn, "close")) keep = false;
       try {
         dispatch(r);
+        if (r.deferred) bc_.skip(r.deferred);
       } catch (const CloseConnection&) {
         return;
       } catch (const StorageError&) {
@@ -164,6 +173,7 @@ class Http1Handler {
         }
       }
       if (!keep) return;
+      if (r.body.capacity() <= (64u << 20)) body_buf_.swap(r.body);
     }
   }
 
@@ -201,6 +211,11 @@ class Http1Handler {
       }
     } else if (const auto* cl = r->header("Content-Length")) {
       size_t n = std::stoull(*cl);
+      if (r->method == "PUT" && starts_with(r->path, "/upload/storage/v1/b/") && r->has_q("upload_id")) {
+        r->deferred = n;
+        srv_.stats().bytes_received += n;
+        return true;
+      }
       r->body.resize(n);
       if (n) bc_.read_exact(&r->body[0], n);
     }
@@ -342,6 +357,9 @@ class Http1Handler {
 
   void send_media(const Request& r, const StoredObject& o, bool xml) {
     if (maybe_fail(xml)) return;
+    if (o.hollow)
+      return respond(c_, 412, {}, json_error(412, "object content was not retained (server retain_uploads=false)",
+                                             "conditionNotMet"));
     uint64_t a = 0, b = o.size ? o.size - 1 : 0;
     bool partial = false;
     if (const auto* rg = r.header("Range"); rg && o.size > 0) {
@@ -365,7 +383,7 @@ class Http1Handler {
               {"ETag", "\"" + std::to_string(o.generation) + "\""},
               {"Last-Modified", http_date(o.created_us)},
               {"Server", "gcsb-fakegcs"}};
-    if (!o.md5.empty()) h.emplace_back("x-goog-hash", "md5=" + base64_encode(o.md5));
+    if (!o.md5().empty()) h.emplace_back("x-goog-hash", "md5=" + base64_encode(o.md5()));
     if (partial)
       h.emplace_back("Content-Range",
                      "bytes " + std::to_string(a) + "-" + std::to_string(b) + "/" + std::to_string(o.size));
@@ -445,7 +463,8 @@ class Http1Handler {
       return send_media(r, *o, true);
     }
     if (r.method == "PUT") {
-      std::vector<uint8_t> data(r.body.begin(), r.body.end());
+      Blob data;
+      data.append(r.body.data(), r.body.size());
       const auto* ct = r.header("Content-Type");
       auto o = srv_.store().put(bucket, name, std::move(data), ct ? *ct : "");
       return respond(c_, 200, {{"ETag", "\"" + std::to_string(o->generation) + "\""},
@@ -537,18 +556,20 @@ class Http1Handler {
     if (r.method == "POST" && type == "media") {
       std::string name = r.q("name");
       if (name.empty()) return respond(c_, 400, {}, json_error(400, "Required parameter: name", "required"));
-      std::vector<uint8_t> data(r.body.begin(), r.body.end());
+      Blob data;
+      data.append(r.body.data(), r.body.size());
+      const uint32_t data_crc = gcsb::crc32c(data.data(), data.size());
       if (const auto* gh = r.header("x-goog-hash")) {
         bool has = false;
         uint32_t crc = 0;
         std::string md5;
         parse_goog_hash(*gh, &has, &crc, &md5);
-        if (has && crc != gcsb::crc32c(data.data(), data.size()))
+        if (has && crc != data_crc)
           return respond(c_, 400, {}, json_error(400, "Provided CRC32C doesn't match calculated CRC32C", "invalid"));
       }
       const auto* ct = r.header("Content-Type");
-      auto o = srv_.store().put(bucket, name, std::move(data), ct ? *ct : "");
-      return respond(c_, 200, {}, object_json(*o).dump());
+      auto o = srv_.store().put(bucket, name, std::move(data), ct ? *ct : "", &data_crc);
+      return respond(c_, 200, {}, object_json(*o, false).dump());
     }
     if (r.method == "POST" && type == "resumable") {
       std::string name = r.q("name");
@@ -580,7 +601,7 @@ class Http1Handler {
       auto s = srv_.store().find_upload(r.q("upload_id"));
       if (!s) return respond(c_, 404, {}, json_error(404, "No such upload", "notFound"));
       std::lock_guard<std::mutex> lk(s->mu);
-      if (s->finalized) return respond(c_, 200, {}, object_json(*s->result).dump());
+      if (s->finalized) return respond(c_, 200, {}, object_json(*s->result, false).dump());
       std::string cr;
       if (const auto* h = r.header("Content-Range")) cr = *h;
       // "bytes a-b/total" | "bytes a-b/*" | "bytes */total" | "bytes */*"
@@ -596,21 +617,37 @@ class Http1Handler {
           b = std::stoll(range.substr(dash + 1));
         }
       }
-      int64_t persisted = static_cast<int64_t>(s->data.size());
+      int64_t persisted = static_cast<int64_t>(s->received);
       if (a >= 0) {
         if (a > persisted)
           return respond(c_, 400, {}, json_error(400, "Invalid request: missing bytes before offset", "invalid"));
-        int64_t skip = persisted - a;
-        if (skip < static_cast<int64_t>(r.body.size()))
-          s->data.insert(s->data.end(), r.body.begin() + skip, r.body.end());
+        uint64_t skip = static_cast<uint64_t>(persisted - a);
+        if (r.deferred) {
+          // stream the chunk: 1 MiB socket reads, CRC'd (and kept) while the
+          // client is still sending the rest
+          if (piece_.empty()) piece_.resize(1u << 20);
+          while (r.deferred) {
+            size_t k = static_cast<size_t>(std::min<uint64_t>(r.deferred, piece_.size()));
+            bc_.read_exact(piece_.data(), k);
+            r.deferred -= k;
+            if (skip >= k) {
+              skip -= k;
+              continue;
+            }
+            s->append(piece_.data() + skip, k - skip);
+            skip = 0;
+          }
+        } else if (skip < r.body.size()) {
+          s->append(r.body.data() + skip, r.body.size() - skip);
+        }
         (void)b;
-        persisted = static_cast<int64_t>(s->data.size());
+        persisted = static_cast<int64_t>(s->received);
       }
       if (total >= 0 && persisted == total) {
         std::string err;
         auto o = srv_.store().finalize_upload(*s, &err);
         if (!o) return respond(c_, 400, {}, json_error(400, err, "invalid"));
-        return respond(c_, 200, {}, object_json(*o).dump());
+        return respond(c_, 200, {}, object_json(*o, false).dump());
       }
       Headers h;
       if (persisted > 0) h.emplace_back("Range", "bytes=0-" + std::to_string(persisted - 1));
@@ -621,6 +658,8 @@ class Http1Handler {
 
   FakeGcsServer& srv_;
   BufferedConn& bc_;
+  std::string body_buf_;
+  std::vector<uint8_t> piece_;
   Conn& c_;
 };
 

@@ -1,6 +1,7 @@
 #include "server/store.h"
 
 #include <openssl/evp.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <atomic>
@@ -13,7 +14,35 @@
 
 namespace gcsb {
 
+Blob::~Blob() {
+  if (p_) ::munmap(p_, cap_);
+}
+
+void Blob::reserve(size_t n) {
+  if (n <= cap_) return;
+  const size_t huge = 2u << 20;
+  size_t cap = std::max<size_t>(huge, (n + huge - 1) / huge * huge);
+  void* q = p_ ? ::mremap(p_, cap_, cap, MREMAP_MAYMOVE)
+               : ::mmap(nullptr, cap, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (q == MAP_FAILED) throw std::bad_alloc();
+  ::madvise(q, cap, MADV_HUGEPAGE);
+  p_ = static_cast<uint8_t*>(q);
+  cap_ = cap;
+}
+
+uint8_t* Blob::extend(size_t n) {
+  if (size_ + n > cap_) reserve(std::max(size_ + n, cap_ * 2));
+  uint8_t* q = p_ + size_;
+  size_ += n;
+  return q;
+}
+
+void Blob::append(const void* p, size_t n) {
+  if (n) std::memcpy(extend(n), p, n);
+}
+
 const uint8_t* StoredObject::bytes(uint64_t off, uint64_t n) const {
+  if (hollow) throw std::runtime_error("object content was not retained by the server (retain_uploads=false)");
   if (synthetic) return PatternBuffer::instance().slice(rot, off, n);
   return data->data() + off;
 }
@@ -29,6 +58,7 @@ bool StoredObject::file_range(uint64_t off, int* fd, uint64_t* foff) const {
 }
 
 uint32_t StoredObject::crc32c_range(uint64_t off, uint64_t n) const {
+  if (hollow) throw std::runtime_error("object content was not retained by the server (retain_uploads=false)");
   if (synthetic) return PatternBuffer::instance().crc32c_range(rot, off, n);
   return gcsb::crc32c(data->data() + off, n);
 }
@@ -39,6 +69,17 @@ int64_t ObjectStore::next_generation() {
   if (g <= last_gen_) g = last_gen_ + 1;
   last_gen_ = g;
   return g;
+}
+
+static std::string md5_of_object(const StoredObject& o);
+
+const std::string& StoredObject::md5() const {
+  if (md5_lazy_)
+    std::call_once(md5_once_, [this] {
+      md5_ = md5_of_object(*this);
+      md5_done_.store(true, std::memory_order_release);
+    });
+  return md5_;
 }
 
 static std::string md5_of_object(const StoredObject& o) {
@@ -74,7 +115,7 @@ std::shared_ptr<const StoredObject> ObjectStore::add_synthetic(const std::string
   o->generation = next_generation();
   o->created_us = wall_ns() / 1000;
   o->crc32c = PatternBuffer::instance().crc32c_range(o->rot, 0, size);
-  if (compute_md5_) o->md5 = md5_of_object(*o);
+  if (compute_md5_) o->set_md5(md5_of_object(*o));
   std::unique_lock<std::shared_mutex> lk(mu_);
   objects_[{bucket, name}] = o;
   return o;
@@ -95,7 +136,8 @@ void ObjectStore::add_synthetic_range(const std::string& bucket, const std::stri
 }
 
 std::shared_ptr<const StoredObject> ObjectStore::put(const std::string& bucket, const std::string& name,
-                                                     std::vector<uint8_t> data, const std::string& content_type) {
+                                                     Blob data, const std::string& content_type,
+                                                     const uint32_t* known_crc) {
   auto o = std::make_shared<StoredObject>();
   o->bucket = bucket;
   o->name = name;
@@ -103,9 +145,9 @@ std::shared_ptr<const StoredObject> ObjectStore::put(const std::string& bucket, 
   o->content_type = content_type.empty() ? "application/octet-stream" : content_type;
   o->generation = next_generation();
   o->created_us = wall_ns() / 1000;
-  o->crc32c = gcsb::crc32c(data.data(), data.size());
-  o->md5 = md5_digest(data.data(), data.size());
-  o->data = std::make_shared<const std::vector<uint8_t>>(std::move(data));
+  o->crc32c = known_crc ? *known_crc : gcsb::crc32c(data.data(), data.size());
+  o->data = std::make_shared<const Blob>(std::move(data));
+  if (compute_md5_) o->set_md5_lazy();
   std::unique_lock<std::shared_mutex> lk(mu_);
   objects_[{bucket, name}] = o;
   return o;
@@ -148,7 +190,8 @@ std::shared_ptr<UploadSession> ObjectStore::start_upload(const std::string& buck
   s->name = name;
   s->content_type = content_type;
   s->expected_size = expected_size;
-  if (expected_size > 0) s->data.reserve(static_cast<size_t>(expected_size));
+  s->retain = retain_uploads_;
+  if (expected_size > 0 && s->retain) s->data.reserve(static_cast<size_t>(expected_size));
   uploads_[s->id] = s;
   return s;
 }
@@ -161,8 +204,8 @@ std::shared_ptr<UploadSession> ObjectStore::find_upload(const std::string& id) c
 
 std::shared_ptr<const StoredObject> ObjectStore::finalize_upload(UploadSession& s, std::string* err) {
   if (s.finalized) return s.result;
+  const uint32_t got = s.data_crc;
   if (s.has_crc) {
-    uint32_t got = gcsb::crc32c(s.data.data(), s.data.size());
     if (got != s.crc) {
       char b[128];
       std::snprintf(b, sizeof(b), "Provided CRC32C \"%08x\" doesn't match calculated CRC32C \"%08x\"", s.crc, got);
@@ -170,7 +213,22 @@ std::shared_ptr<const StoredObject> ObjectStore::finalize_upload(UploadSession& 
       return nullptr;
     }
   }
-  s.result = put(s.bucket, s.name, std::move(s.data), s.content_type);
+  if (s.retain) {
+    s.result = put(s.bucket, s.name, std::move(s.data), s.content_type, &got);
+  } else {
+    auto o = std::make_shared<StoredObject>();
+    o->bucket = s.bucket;
+    o->name = s.name;
+    o->size = s.received;
+    o->hollow = true;
+    o->content_type = s.content_type.empty() ? "application/octet-stream" : s.content_type;
+    o->generation = next_generation();
+    o->created_us = wall_ns() / 1000;
+    o->crc32c = got;
+    std::unique_lock<std::shared_mutex> lk(mu_);
+    objects_[{s.bucket, s.name}] = o;
+    s.result = o;
+  }
   s.data.clear();
   s.finalized = true;
   return s.result;

@@ -25,6 +25,7 @@ int main(int argc, char** argv) {
   auto count = f.Int("objects", 48, "Number of synthetic objects prefix<i>suffix");
   auto size = f.Int("object-size", 100 << 20, "Synthetic object size in bytes");
   auto md5 = f.Bool("md5", true, "Compute MD5 for synthetic objects (x-goog-hash md5=)");
+  auto retain = f.Bool("retain-uploads", true, "Keep uploaded bytes (false: verify size + CRC32C, keep metadata only)");
   auto require_auth = f.Bool("require-auth", false, "Require a bearer token issued by /token");
   auto jwt_key = f.String("jwt-public-key", "", "PEM public key used to verify JWT assertions at /token");
   auto grpc_chunk = f.Int("grpc-chunk", 2 << 20, "ReadObjectResponse content bytes per message");
@@ -52,6 +53,7 @@ int main(int argc, char** argv) {
     cfg.jwt_public_key_pem = ss.str();
   }
   auto store = std::make_shared<ObjectStore>(*md5);
+  store->set_retain_uploads(*retain);
   int64_t t0 = now_ns();
   if (*count > 0)
     store->add_synthetic_range(*bucket, *prefix, *suffix, static_cast<int>(*first), static_cast<int>(*count),

@@ -85,6 +85,8 @@ def build_flags() -> FlagSet:
     fs.bool("start-fake-server", False, "Start a node-local synthetic GCS endpoint (no network)")
     fs.int("fake-object-size", 100 << 20, "Synthetic object size (reference objects are ~100 MB)")
     fs.int("fake-objects", -1, "Synthetic objects per rank (default: -worker)")
+    fs.bool("fake-retain-uploads", True, "Synthetic endpoint keeps uploaded bytes (false: verifies size + CRC32C "
+            "and keeps metadata only, the server-side io.Discard for write benchmarks)")
     fs.string("summary-json", "", "Write the run summary (p50/p99/MiB/s, node view) as JSON here")
     return fs
 
@@ -131,7 +133,8 @@ def main(argv: list[str] | None = None) -> int:
 
         n_obj = fs.get("fake-objects") if fs.get("fake-objects") >= 0 else workers
         ep_handle = server.start_inprocess(fs.get("bucket"), fs.get("object-prefix"), fs.get("object-suffix"), first,
-                                           n_obj, fs.get("fake-object-size"), md5=True, cpus=placement["server"])
+                                           n_obj, fs.get("fake-object-size"), md5=True, cpus=placement["server"],
+                                           retain_uploads=fs.get("fake-retain-uploads"))
         endpoint = ep_handle.url
         _err(f"synthetic GCS endpoint {endpoint}: {n_obj} objects of {fs.get('fake-object-size')} bytes")
     if not endpoint:

@@ -161,6 +161,7 @@ def run_write(opts: RunOptions, nobjects: int, size: int, name_prefix: str = "up
     dev = opts.device
     buf = torch.empty(size, dtype=torch.uint8, device=f"cuda:{dev}")
     lat = []
+    setup = []
     total = 0
     t_all = time.perf_counter()
     for i in range(nobjects):
@@ -171,6 +172,7 @@ def run_write(opts: RunOptions, nobjects: int, size: int, name_prefix: str = "up
         m = client.write_from_device(opts.bucket, name, buf.data_ptr(), size, dev, resumable, chunk_bytes,
                                      opts.ring_slot_bytes, opts.ring_slots)
         lat.append((time.perf_counter() - t0) * 1e3)
+        setup.append(m["gpu_crc_ms"])
         if m["size"] != size or m["crc32c"] != m["gpu_crc32c"]:
             raise RuntimeError(f"upload of {name} not confirmed: {m}")
         total += size
@@ -187,4 +189,5 @@ def run_write(opts: RunOptions, nobjects: int, size: int, name_prefix: str = "up
     summary = {"reads": 0, "writes": nobjects, "errors": 0, "bytes": total, "elapsed_s": elapsed,
                "mib_per_s": total / elapsed / 2**20 if elapsed else 0.0, "p50_ms": pct(50), "p99_ms": pct(99),
                "min_ms": s[0] if s else 0.0, "max_ms": s[-1] if s else 0.0, "avg_ms": sum(s) / len(s) if s else 0.0}
+    summary["gpu_setup_p50_ms"] = sorted(setup)[len(setup) // 2] if setup else 0.0  # staging ring + GPU CRC32C
     return WorkloadResult(summary, 0, {"latencies_ms": lat})

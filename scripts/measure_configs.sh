@@ -47,9 +47,14 @@ for p in http grpc; do
     -read-call-per-worker 3 -fake-objects 1000 -fake-object-size $MIB
 done
 
-# config 5 (1-GPU part): 64 MiB uploads HBM -> pinned -> resumable / WriteObject
+# config 5 (1-GPU part): 64 MiB uploads HBM -> pinned -> resumable / WriteObject.
+# The synthetic server verifies size + CRC32C of every upload; the first run
+# discards the bytes after that (server-side io.Discard), the second keeps them.
 for p in grpc http; do
   run c5_${p}_write64m 300 -workload write -client-protocol $p -sink gpu -worker 1 -write-objects 20 \
+    -fake-retain-uploads=false \
+    -write-size $((64 * MIB)) -fake-objects 1 -fake-object-size $MIB
+  run c5_${p}_write64m_retain 300 -workload write -client-protocol $p -sink gpu -worker 1 -write-objects 20 \
     -write-size $((64 * MIB)) -fake-objects 1 -fake-object-size $MIB
 done
 echo "done"

@@ -22,7 +22,7 @@ LDLIBS   := -lssl -lcrypto -lpthread
 CORE_SRCS := csrc/core/crc32c.cc csrc/core/affinity.cc csrc/core/content.cc csrc/core/util.cc csrc/core/json.cc \
              csrc/net/socket.cc csrc/net/buffered.cc \
              csrc/http1/http1.cc csrc/h2/hpack.cc csrc/h2/h2.cc csrc/h2/h2_client.cc csrc/proto/storage_v2.cc \
-             csrc/storage/sink.cc csrc/storage/auth.cc csrc/storage/client.cc csrc/storage/http_client.cc \
+             csrc/storage/sink.cc csrc/storage/sliced.cc csrc/storage/auth.cc csrc/storage/client.cc csrc/storage/http_client.cc \
              csrc/storage/grpc_client.cc \
              csrc/server/store.cc csrc/server/fakegcs.cc csrc/server/server_http1.cc csrc/server/server_grpc.cc \
              csrc/gpu/crc_host.cc

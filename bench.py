@@ -50,6 +50,8 @@ def main() -> int:
     ap.add_argument("--slot-bytes", default="8MiB")
     ap.add_argument("--slots", type=int, default=4)
     ap.add_argument("--grpc-pool", type=int, default=1)
+    ap.add_argument("--slices", type=int, default=1,
+                    help="concurrent ranged streams per object read, each on its own connection (1 = one stream)")
     ap.add_argument("--affinity", default="same",
                     help="CPU placement of client/endpoint threads: same|split|numa|none (see parallel/affinity.py)")
     ap.add_argument("--json-out", default="")
@@ -101,6 +103,7 @@ def main() -> int:
         "keep_records": False,
         "cpus": placement["client"],
         "retry_initial_s": 0.05,
+        "slices": args.slices,
     }
     run = n.Runner(cfg)
     if args.warmup > 0:
@@ -160,6 +163,7 @@ def main() -> int:
                 "readers_per_gpu": args.workers,
                 "sink": args.sink,
                 "ring": f"{args.slots}x{args.slot_bytes}",
+                "streams_per_read": args.slices,
             },
             "per_gpu_mib_s": round(value / world, 2),
             "p50_ms": round(stats["p50_max"], 3),

@@ -49,6 +49,13 @@ std::string Runner::object_for(int worker, int64_t seq) const {
   return cfg_.object_prefix + std::to_string(cfg_.worker_id_offset + worker) + cfg_.object_suffix;
 }
 
+uintptr_t Runner::landing_ptr(int w) const {
+  if (w < 0 || w >= static_cast<int>(sinks_.size())) return 0;
+  if (landing_[w]) return reinterpret_cast<uintptr_t>(landing_[w]->data());
+  if (gpu_sinks_[w]) return reinterpret_cast<uintptr_t>(gpu_sinks_[w]->object_device_ptr());
+  return 0;
+}
+
 void Runner::reset_stats() {
   std::lock_guard<std::mutex> lk(mu_);
   acc_ = RunSummary();
@@ -65,6 +72,8 @@ void Runner::start() {
     sinks_.resize(cfg_.workers);
     gpu_sinks_.assign(cfg_.workers, nullptr);
     gpu_stats_.assign(cfg_.workers, GpuSinkStats{});
+    sliced_.resize(cfg_.workers);
+    landing_.resize(cfg_.workers);
   }
   for (int w = 0; w < cfg_.workers; ++w) threads_.emplace_back([this, w] { worker_main(w); });
 }
@@ -102,7 +111,39 @@ void Runner::worker_main(int w) {
   // pin before the sink allocates its pinned ring: NUMA-local first touch
   pin_current_thread(cfg_.client.cpus);
   try {
-    if (!sinks_[w]) {
+    if (cfg_.slices > 1 && !sliced_[w]) {
+      SlicedReadConfig sc;
+      sc.slices = cfg_.slices;
+      sc.min_slice_bytes = cfg_.slice_min_bytes;
+      sc.cpus = cfg_.client.cpus;
+      const bool gpu = cfg_.sink == "gpu";
+      sc.verify = gpu ? cfg_.gpu.verify : cfg_.host_crc;
+      DeviceBuffer* land = nullptr;
+      if (gpu) {
+        landing_[w] = std::make_unique<DeviceBuffer>(cfg_.gpu.device);
+        land = landing_[w].get();
+      }
+      const RunnerConfig& rc = cfg_;
+      sliced_[w] = std::make_unique<SlicedReader>(
+          cfg_.client, sc,
+          [&rc, gpu](int) -> std::unique_ptr<Sink> {
+            if (gpu) {
+              GpuSinkConfig g = rc.gpu;
+              g.landing = Landing::kObject;
+              return std::make_unique<GpuSink>(g);
+            }
+            return std::make_unique<DiscardSink>(rc.client.read_chunk, rc.host_crc);
+          },
+          [land](uint64_t total) {
+            if (land) land->ensure(total);
+          },
+          [land](int, Sink& sk, uint64_t off, uint64_t) {
+            // each slice lands at its offset; the capacity is the rest of
+            // the buffer (a ranged read learns the whole object's size)
+            if (land) static_cast<GpuSink&>(sk).set_external_destination(land->data() + off, land->capacity() - off);
+          });
+    }
+    if (!sinks_[w] && cfg_.slices <= 1) {
       if (cfg_.sink == "gpu") {
         auto g = std::make_unique<GpuSink>(cfg_.gpu);
         gpu_sinks_[w] = g.get();
@@ -123,6 +164,7 @@ void Runner::worker_main(int w) {
   }
   Sink* sink = sinks_[w].get();
   GpuSink* gsink = gpu_sinks_[w];
+  SlicedReader* sliced = sliced_[w].get();
   std::mt19937_64 rng(cfg_.seed ? cfg_.seed + static_cast<uint64_t>(w) : std::random_device{}());
   const uint64_t sample_bound = cfg_.trace_sample_rate >= 1.0
                                     ? ~0ull
@@ -146,8 +188,9 @@ void Runner::worker_main(int w) {
     r.start_ns = now_ns();
     double ms = 0, host_ms = 0;
     try {
-      ReadResult rr = client_->read_object(cfg_.bucket, r.object, *sink, cfg_.range_offset, cfg_.range_limit,
-                                           &stop_flag_);
+      ReadResult rr = sliced ? sliced->read(cfg_.bucket, r.object, &stop_flag_)
+                             : client_->read_object(cfg_.bucket, r.object, *sink, cfg_.range_offset,
+                                                    cfg_.range_limit, &stop_flag_);
       r.end_ns = now_ns();
       r.ttfb_ns = rr.first_byte_ns;
       r.host_done_ns = rr.host_done_ns;
@@ -187,6 +230,20 @@ void Runner::worker_main(int w) {
   if (gsink) {
     std::lock_guard<std::mutex> lk(mu_);
     gpu_stats_[w] = gsink->stats();
+  } else if (sliced && cfg_.sink == "gpu") {
+    GpuSinkStats t;
+    for (int i = 0; i < sliced->slices(); ++i) {
+      const GpuSinkStats& g = static_cast<GpuSink&>(sliced->sink(i)).stats();
+      t.slots_submitted += g.slots_submitted;
+      t.segments += g.segments;
+      t.chunks_verified_gpu += g.chunks_verified_gpu;
+      t.chunks_verified_host += g.chunks_verified_host;
+      t.objects_verified += g.objects_verified;
+      t.slot_waits += g.slot_waits;
+      t.slot_wait_s += g.slot_wait_s;
+    }
+    std::lock_guard<std::mutex> lk(mu_);
+    gpu_stats_[w] = t;
   }
 }
 

@@ -25,6 +25,7 @@
 
 #include "gpu/engine.h"
 #include "storage/client.h"
+#include "storage/sliced.h"
 
 namespace gcsb {
 
@@ -52,6 +53,11 @@ struct RunnerConfig {
   double trace_sample_rate = 0.0;                       // 0 disables span records
   int64_t range_offset = 0;
   int64_t range_limit = -1;
+  // >1: each read is a sliced read (storage/sliced.h): stat, then `slices`
+  // concurrent ranged streams on their own connections, one sink each,
+  // landing at their offsets of one HBM buffer; object CRC32C combined.
+  int slices = 1;
+  uint64_t slice_min_bytes = 8u << 20;
   uint64_t seed = 0;
 };
 
@@ -100,6 +106,9 @@ class Runner {
   void set_reads_per_worker(int64_t n) { cfg_.reads_per_worker = n; }
   void reset_stats();
   StorageClient& client() { return *client_; }
+  // HBM address worker w's last object landed at (GPU sink, object landing;
+  // sliced reads: the shared landing buffer), 0 if none.
+  uintptr_t landing_ptr(int w) const;
 
  private:
   void worker_main(int w);
@@ -118,6 +127,8 @@ class Runner {
   std::vector<GpuSinkStats> gpu_stats_;
   std::vector<std::unique_ptr<Sink>> sinks_;
   std::vector<GpuSink*> gpu_sinks_;
+  std::vector<std::unique_ptr<SlicedReader>> sliced_;   // per worker (slices > 1)
+  std::vector<std::unique_ptr<DeviceBuffer>> landing_;  // per worker (sliced GPU reads)
 };
 
 }  // namespace gcsb

@@ -178,6 +178,24 @@ class GpuByteSource : public ByteSource {
   uint64_t copies_ = 0;
 };
 
+// Grow-only HBM buffer (e.g. the landing zone a sliced read's slice sinks
+// share: each GpuSink is pointed at base + slice offset).
+class DeviceBuffer {
+ public:
+  explicit DeviceBuffer(int device) : device_(device) {}
+  ~DeviceBuffer();
+  DeviceBuffer(const DeviceBuffer&) = delete;
+  DeviceBuffer& operator=(const DeviceBuffer&) = delete;
+  uint8_t* ensure(size_t n);  // contents are not preserved on growth
+  uint8_t* data() const { return p_; }
+  size_t capacity() const { return cap_; }
+
+ private:
+  int device_;
+  uint8_t* p_ = nullptr;
+  size_t cap_ = 0;
+};
+
 // Device CRC32C of an arbitrary device range (test/verification utility).
 uint32_t gpu_crc32c(int device, const void* dptr, size_t n);
 // Kernel throughput probe: K1+K2 over [dptr, dptr+n) in segments of

@@ -559,6 +559,25 @@ std::pair<const uint8_t*, size_t> GpuByteSource::next(size_t max) {
 // ---------------------------------------------------------------------------
 // utilities
 
+DeviceBuffer::~DeviceBuffer() {
+  if (p_) {
+    (void)hipSetDevice(device_);
+    (void)hipFree(p_);
+  }
+}
+
+uint8_t* DeviceBuffer::ensure(size_t n) {
+  if (n <= cap_ && p_) return p_;
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  if (p_) hip_check(hipFree(p_), "hipFree");
+  p_ = nullptr;
+  size_t cap = std::max<size_t>((n + (2u << 20) - 1) / (2u << 20) * (2u << 20), 2u << 20);
+  hip_check(hipMalloc(reinterpret_cast<void**>(&p_), cap), "hipMalloc(landing)");
+  cap_ = cap;
+  return p_;
+}
+
 uint32_t gpu_crc32c(int device, const void* dptr, size_t n) {
   if (n == 0) return 0;
   hip_check(hipSetDevice(device), "hipSetDevice");

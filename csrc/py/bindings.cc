@@ -308,6 +308,8 @@ class PyRunner {
     c.trace_sample_rate = get_or<double>(d, "trace_sample_rate", 0.0);
     c.range_offset = get_or<int64_t>(d, "range_offset", 0);
     c.range_limit = get_or<int64_t>(d, "range_limit", -1);
+    c.slices = get_or<int>(d, "slices", 1);
+    c.slice_min_bytes = get_or<uint64_t>(d, "slice_min_bytes", 8u << 20);
     c.seed = get_or<uint64_t>(d, "seed", 0);
     runner_ = std::make_unique<Runner>(std::move(c));
   }
@@ -370,6 +372,7 @@ class PyRunner {
     return d;
   }
   std::string object_for(int w, int64_t seq) { return runner_->object_for(w, seq); }
+  uintptr_t landing_ptr(int w) { return runner_->landing_ptr(w); }
   void set_reads_per_worker(int64_t n) { runner_->set_reads_per_worker(n); }
   void reset_stats() { runner_->reset_stats(); }
 
@@ -719,6 +722,7 @@ PYBIND11_MODULE(_native, m) {
       .def("drain", &PyRunner::drain)
       .def("summary", &PyRunner::summary)
       .def("object_for", &PyRunner::object_for)
+      .def("landing_ptr", &PyRunner::landing_ptr)
       .def("set_reads_per_worker", &PyRunner::set_reads_per_worker)
       .def("reset_stats", &PyRunner::reset_stats);
 

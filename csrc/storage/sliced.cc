@@ -1,0 +1,156 @@
+#include "storage/sliced.h"
+
+#include <algorithm>
+#include <cstdio>
+
+#include "core/affinity.h"
+#include "core/crc32c.h"
+#include "core/util.h"
+
+namespace gcsb {
+
+SlicedReader::SlicedReader(const ClientConfig& client_cfg, SlicedReadConfig cfg, MakeSink make_sink, Prepare prepare,
+                           Place place)
+    : cfg_(std::move(cfg)), prepare_(std::move(prepare)), place_(std::move(place)) {
+  if (cfg_.slices < 1) cfg_.slices = 1;
+  ClientConfig cc = client_cfg;
+  cc.grpc_conn_pool_size = 1;  // one connection per slice client
+  for (int i = 0; i < cfg_.slices; ++i) {
+    clients_.push_back(make_client(cc));
+    sinks_.push_back(make_sink(i));
+  }
+  jobs_.resize(cfg_.slices);
+  for (int i = 1; i < cfg_.slices; ++i) threads_.emplace_back([this, i] { thread_main(i); });
+}
+
+SlicedReader::~SlicedReader() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  for (auto& t : threads_) t.join();
+}
+
+void SlicedReader::run_slice(int i) {
+  Job& j = jobs_[i];
+  try {
+    j.rr = clients_[i]->read_object(j.bucket, j.object, *sinks_[i], static_cast<int64_t>(j.off),
+                                    static_cast<int64_t>(j.len), j.cancel);
+  } catch (const StorageError& e) {
+    j.error = e.what();
+    j.retryable = e.retryable();
+  } catch (const std::exception& e) {
+    j.error = e.what();
+  }
+}
+
+void SlicedReader::thread_main(int i) {
+  pin_current_thread(cfg_.cpus);
+  std::unique_lock<std::mutex> lk(mu_);
+  for (;;) {
+    cv_.wait(lk, [&] { return stop_ || jobs_[i].pending; });
+    if (stop_) return;
+    jobs_[i].pending = false;
+    lk.unlock();
+    run_slice(i);
+    lk.lock();
+    jobs_[i].done = true;
+    done_cv_.notify_all();
+  }
+}
+
+ReadResult SlicedReader::read(const std::string& bucket, const std::string& object, const volatile bool* cancel) {
+  ObjectMeta m = clients_[0]->stat_object(bucket, object);
+  const uint64_t total = static_cast<uint64_t>(m.size);
+  prepare_(total);
+  // slice boundaries on 2 MiB multiples (whole gRPC messages / ring chunks)
+  int n = cfg_.slices;
+  if (cfg_.min_slice_bytes) n = static_cast<int>(std::min<uint64_t>(n, std::max<uint64_t>(1, total / cfg_.min_slice_bytes)));
+  const uint64_t align = 2u << 20;
+  uint64_t per = (total + n - 1) / std::max(1, n);
+  per = (per + align - 1) / align * align;
+  std::vector<std::pair<uint64_t, uint64_t>> ranges;
+  for (uint64_t off = 0; off < total || ranges.empty(); off += per) {
+    ranges.emplace_back(off, std::min(per, total - off));
+    if (total == 0) break;
+  }
+  n = static_cast<int>(ranges.size());
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (int i = 0; i < n; ++i) {
+      Job& j = jobs_[i];
+      j.bucket = bucket;
+      j.object = object;
+      j.off = ranges[i].first;
+      j.len = ranges[i].second;
+      j.cancel = cancel;
+      j.rr = ReadResult();
+      j.error.clear();
+      j.retryable = false;
+      j.done = false;
+      place_(i, *sinks_[i], j.off, j.len);
+      j.pending = i > 0;
+    }
+  }
+  cv_.notify_all();
+  run_slice(0);
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] {
+      for (int i = 1; i < n; ++i)
+        if (!jobs_[i].done) return false;
+      return true;
+    });
+  }
+  // merge: first error wins; otherwise combine the slice CRCs in order
+  ReadResult out;
+  out.info.size = m.size;
+  out.info.generation = m.generation;
+  out.info.has_crc32c = m.has_crc32c;
+  out.info.crc32c = m.crc32c;
+  out.info.md5 = m.md5;
+  out.sink_begun = true;
+  uint32_t crc = 0;
+  bool all_verified = true;
+  for (int i = 0; i < n; ++i) {
+    const Job& j = jobs_[i];
+    if (!j.error.empty())
+      throw StorageError("slice " + std::to_string(i) + " [" + std::to_string(j.off) + ", +" + std::to_string(j.len) +
+                             "): " + j.error,
+                         j.retryable);
+    out.bytes += j.rr.bytes;
+    out.attempts = std::max(out.attempts, j.rr.attempts);
+    if (j.rr.first_byte_ns && (!out.first_byte_ns || j.rr.first_byte_ns < out.first_byte_ns))
+      out.first_byte_ns = j.rr.first_byte_ns;
+    out.host_done_ns = std::max(out.host_done_ns, j.rr.host_done_ns);
+    out.sink.landed_ns = std::max(out.sink.landed_ns, j.rr.sink.landed_ns);
+    if (j.rr.sink.crc_mismatch && !out.sink.crc_mismatch) {
+      out.sink.crc_mismatch = true;
+      out.sink.detail = "slice " + std::to_string(i) + ": " + j.rr.sink.detail;
+    }
+    all_verified = all_verified && j.rr.sink.verified;
+    crc = crc32c_combine(crc, j.rr.sink.computed_crc32c, j.rr.bytes);
+  }
+  out.sink.bytes = out.bytes;
+  out.sink.computed_crc32c = crc;
+  if (out.bytes != total) {
+    throw StorageError("sliced read: " + std::to_string(out.bytes) + " of " + std::to_string(total) + " bytes", true);
+  }
+  if (!cfg_.verify) {
+    out.sink.verified = false;
+  } else if (m.has_crc32c) {
+    if (crc != m.crc32c) {
+      out.sink.crc_mismatch = true;
+      char b[128];
+      std::snprintf(b, sizeof(b), "bad CRC on read: combined slices %08x want %08x", crc, m.crc32c);
+      if (out.sink.detail.empty()) out.sink.detail = b;
+    }
+    out.sink.verified = !out.sink.crc_mismatch;
+  } else {
+    out.sink.verified = all_verified && !out.sink.crc_mismatch;
+  }
+  return out;
+}
+
+}  // namespace gcsb

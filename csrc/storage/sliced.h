@@ -1,0 +1,81 @@
+// Sliced (parallel ranged) read of one object.  [new] — SURVEY.md §2.5
+// "Ranged split of a single object across workers: optional extension".
+//
+// The reference reads every object as ONE stream (reference main.go:134-140:
+// NewReader + io.CopyBuffer), so a single object is bound by one TCP stream,
+// i.e. one receiving core (~9-16 GB/s on the MI355X hosts' loopback).  A
+// sliced read stats the object, then fetches `slices` disjoint byte ranges
+// concurrently, each on its own connection (own StorageClient, so gRPC slices
+// never share an HTTP/2 connection) and its own sink, each slice landing at
+// its offset of the destination.  The object CRC32C is the GF(2) combine of
+// the slices' CRCs, checked against the object's stored CRC32C: the read is
+// verified end to end exactly like a single-stream read.  The timed region is
+// unchanged (request -> every byte landed + verified).
+#pragma once
+#include <condition_variable>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "storage/client.h"
+#include "storage/sink.h"
+
+namespace gcsb {
+
+struct SlicedReadConfig {
+  int slices = 4;
+  uint64_t min_slice_bytes = 8u << 20;  // smaller objects use fewer slices (1 = plain read)
+  std::vector<int> cpus;                // pin the slice threads
+  bool verify = true;                   // sinks compute CRCs: check the combined object CRC32C
+};
+
+class SlicedReader {
+ public:
+  // make_sink(i): the sink slice i reads into (created once, reused).
+  // prepare(total): called once per read, before any slice starts.
+  // place(i, sink, offset, len): called for each slice before it starts, on
+  // the caller's thread (e.g. point a GpuSink at dst + offset).
+  using MakeSink = std::function<std::unique_ptr<Sink>(int)>;
+  using Prepare = std::function<void(uint64_t total)>;
+  using Place = std::function<void(int, Sink&, uint64_t, uint64_t)>;
+
+  SlicedReader(const ClientConfig& client_cfg, SlicedReadConfig cfg, MakeSink make_sink, Prepare prepare,
+               Place place);
+  ~SlicedReader();
+  SlicedReader(const SlicedReader&) = delete;
+  SlicedReader& operator=(const SlicedReader&) = delete;
+
+  ReadResult read(const std::string& bucket, const std::string& object, const volatile bool* cancel = nullptr);
+  int slices() const { return cfg_.slices; }
+  Sink& sink(int i) { return *sinks_[i]; }
+  StorageClient& client(int i) { return *clients_[i]; }
+
+ private:
+  struct Job {
+    std::string bucket, object;
+    uint64_t off = 0, len = 0;
+    const volatile bool* cancel = nullptr;
+    bool pending = false, done = false;
+    ReadResult rr;
+    std::string error;
+    bool retryable = false;
+  };
+  void thread_main(int i);
+  void run_slice(int i);
+
+  SlicedReadConfig cfg_;
+  Prepare prepare_;
+  Place place_;
+  std::vector<std::unique_ptr<StorageClient>> clients_;
+  std::vector<std::unique_ptr<Sink>> sinks_;
+  std::vector<Job> jobs_;
+  std::vector<std::thread> threads_;  // slices 1..n-1 (slice 0 runs on the caller)
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  bool stop_ = false;
+};
+
+}  // namespace gcsb

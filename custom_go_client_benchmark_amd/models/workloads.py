@@ -52,6 +52,8 @@ class RunOptions:
     retry_max_attempts: int = 0
     object_names: list | None = None
     keep_records: bool = True
+    slices: int = 1                        # >1: sliced (parallel ranged) reads, see csrc/storage/sliced.h
+    slice_min_bytes: int = 8 << 20
 
     def client_dict(self) -> dict:
         return {
@@ -73,7 +75,7 @@ class RunOptions:
             "device": self.device, "ring_slot_bytes": self.ring_slot_bytes, "ring_slots": self.ring_slots,
             "landing": self.landing, "gpu_verify": self.gpu_verify, "latency_fd": self.latency_fd,
             "trace_sample_rate": self.trace_sample_rate, "stop_on_error": self.stop_on_error,
-            "keep_records": self.keep_records,
+            "keep_records": self.keep_records, "slices": self.slices, "slice_min_bytes": self.slice_min_bytes,
         })
         if self.object_names:
             d["object_names"] = list(self.object_names)

@@ -144,3 +144,33 @@ def test_cli_gpu_sink(native, gpu_available):
                         "-client-protocol", "grpc"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     assert len(r.stdout.strip().splitlines()) == 6
+
+
+@pytest.mark.parametrize("proto", ["http", "grpc"])
+@pytest.mark.parametrize("slices", [2, 4])
+def test_sliced_read_lands_byte_exact_in_hbm(native, server, gpu_available, proto, slices):
+    size = (40 << 20) + 4097
+    server.add_synthetic(B, P, "", 0, 1, size)
+    r = native.Runner({"protocol": proto, "endpoint": server.url, "bucket": B, "object_prefix": P, "workers": 1,
+                       "reads_per_worker": 2, "sink": "gpu", "slices": slices, "ring_slot_bytes": 4 << 20,
+                       "ring_slots": 4, "keep_records": False})
+    r.start()
+    r.wait()
+    s = r.summary()
+    assert s["errors"] == 0, s["first_error"]
+    assert s["verified"] == 2 and s["bytes"] == 2 * size
+    assert s["gpu"]["chunks_verified_gpu"] + s["gpu"]["chunks_verified_host"] > 0 or proto == "http"
+    bad, first = native.gpu_verify_pattern(0, r.landing_ptr(0), size, P + "0", 0)
+    assert bad == 0, first
+
+
+def test_sliced_gpu_read_detects_corruption(native, server, gpu_available):
+    size = 32 << 20
+    server.add_synthetic(B, P, "", 0, 1, size)
+    server.set_faults({"corrupt_at": (27 << 20) + 3, "corrupt_count": 1})
+    r = native.Runner({"protocol": "http", "endpoint": server.url, "bucket": B, "object_prefix": P, "workers": 1,
+                       "reads_per_worker": 1, "sink": "gpu", "slices": 4, "keep_records": False})
+    r.start()
+    r.wait()
+    s = r.summary()
+    assert s["errors"] == 1 and "bad CRC" in s["first_error"]

@@ -8,7 +8,12 @@ at 1/2/4/8 MI355X.  Config: 256 MiB objects, gRPC ReadObject stream (HTTP with
 and every ChecksummedData CRC32C is verified by the CDNA4 kernels.
 
 One step = every rank's reader reads its own 256 MiB object (file_<rank>) once,
-so per-GPU work is fixed as N grows (weak scaling).  W untimed warmup reads,
+so per-GPU work is fixed as N grows (weak scaling).  Each read is a sliced read
+by default (--slices 4: stat, then 4 concurrent ranged streams on their own
+connections landing at their offsets in HBM, object CRC32C = combine of the
+slice CRCs, checked against the stored CRC32C); a single-stream read (the
+reference's one NewReader per object) is measured right after on the same
+endpoint and reported as `single_stream_*`.  W untimed warmup reads,
 then K timed reads bracketed by an RCCL barrier + torch.cuda.synchronize();
 the elapsed time is the MAX over ranks and `value` is total bytes / that time.
 
@@ -50,10 +55,12 @@ def main() -> int:
     ap.add_argument("--slot-bytes", default="8MiB")
     ap.add_argument("--slots", type=int, default=4)
     ap.add_argument("--grpc-pool", type=int, default=1)
-    ap.add_argument("--slices", type=int, default=1,
+    ap.add_argument("--slices", type=int, default=4,
                     help="concurrent ranged streams per object read, each on its own connection (1 = one stream)")
-    ap.add_argument("--affinity", default="same",
+    ap.add_argument("--affinity", default="split",
                     help="CPU placement of client/endpoint threads: same|split|numa|none (see parallel/affinity.py)")
+    ap.add_argument("--single-stream-steps", type=int, default=-1,
+                    help="timed single-stream reads measured after the main run for comparison (-1: = --steps, 0: skip)")
     ap.add_argument("--json-out", default="")
     args = ap.parse_args()
 
@@ -127,11 +134,35 @@ def main() -> int:
     gdist.barrier(ctx)
     elapsed = time.perf_counter() - t0
     s = run.summary()
+
+    # single-stream comparison (slices=1: the reference's one stream per read)
+    ss_steps = args.steps if args.single_stream_steps < 0 else args.single_stream_steps
+    ss = None
+    if args.slices > 1 and ss_steps > 0:
+        run1 = n.Runner({**cfg, "slices": 1, "reads_per_worker": 1})
+        run1.start()
+        run1.wait()
+        run1.reset_stats()
+        run1.set_reads_per_worker(ss_steps)
+        gdist.barrier(ctx)
+        t1 = time.perf_counter()
+        run1.start()
+        run1.wait()
+        gdist.barrier(ctx)
+        ss_elapsed = time.perf_counter() - t1
+        s1 = run1.summary()
+        ss = {"elapsed": ss_elapsed, "bytes": float(s1["bytes"]), "p50": s1["p50_ms"], "p99": s1["p99_ms"],
+              "ok": 1.0 if s1["errors"] == 0 else 0.0}
+        del run1
     srv.stop()
 
     ok = 1.0 if s["errors"] == 0 and s["reads"] == args.steps * args.workers else 0.0
     stats = gdist.reduce_stats(ctx, elapsed=elapsed, nbytes=float(s["bytes"]), ok=ok, p50=s["p50_ms"],
                                p99=s["p99_ms"], host_p50=s["host_p50_ms"])
+    ss_stats = None
+    if ss is not None:
+        ss_stats = gdist.reduce_stats(ctx, elapsed=ss["elapsed"], nbytes=ss["bytes"], p50=ss["p50"], p99=ss["p99"],
+                                      ok=ss["ok"])
     if rank == 0:
         if stats["ok_min"] < 1.0:
             print(f"benchmark failed: {s['first_error'] or 'incomplete reads'}", file=sys.stderr)
@@ -172,6 +203,10 @@ def main() -> int:
             "endpoint": "loopback synthetic GCS (one per rank)",
             "affinity": args.affinity,
         }
+        if ss_stats is not None:
+            out["single_stream_mib_s"] = round(ss_stats["nbytes_sum"] / ss_stats["elapsed_max"] / (1 << 20), 2)
+            out["single_stream_p50_ms"] = round(ss_stats["p50_max"], 3)
+            out["single_stream_p99_ms"] = round(ss_stats["p99_max"], 3)
         line = json.dumps(out)
         print(line, flush=True)
         if args.json_out:

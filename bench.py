@@ -9,7 +9,7 @@ and every ChecksummedData CRC32C is verified by the CDNA4 kernels.
 
 One step = every rank's reader reads its own 256 MiB object (file_<rank>) once,
 so per-GPU work is fixed as N grows (weak scaling).  Each read is a sliced read
-by default (--slices 4: stat, then 4 concurrent ranged streams on their own
+by default (--slices 8: stat, then 8 concurrent ranged streams on their own
 connections landing at their offsets in HBM, object CRC32C = combine of the
 slice CRCs, checked against the stored CRC32C); a single-stream read (the
 reference's one NewReader per object) is measured right after on the same
@@ -52,13 +52,13 @@ def main() -> int:
     ap.add_argument("--object-size", default="256MiB")
     ap.add_argument("--workers", type=int, default=1, help="readers per GPU (config: 1)")
     ap.add_argument("--sink", default="gpu", help="gpu (HBM landing + GPU CRC) | discard (CPU baseline)")
-    ap.add_argument("--slot-bytes", default="8MiB")
+    ap.add_argument("--slot-bytes", default="4MiB")
     ap.add_argument("--slots", type=int, default=4)
     ap.add_argument("--grpc-pool", type=int, default=1)
-    ap.add_argument("--slices", type=int, default=4,
+    ap.add_argument("--slices", type=int, default=8,
                     help="concurrent ranged streams per object read, each on its own connection (1 = one stream)")
-    ap.add_argument("--affinity", default="split",
-                    help="CPU placement of client/endpoint threads: same|split|numa|none (see parallel/affinity.py)")
+    ap.add_argument("--affinity", default="share",
+                    help="CPU placement of client/endpoint threads: share|same|split|numa|none (see parallel/affinity.py)")
     ap.add_argument("--single-stream-steps", type=int, default=-1,
                     help="timed single-stream reads measured after the main run for comparison (-1: = --steps, 0: skip)")
     ap.add_argument("--json-out", default="")

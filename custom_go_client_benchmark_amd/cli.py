@@ -84,7 +84,7 @@ def build_flags() -> FlagSet:
     fs.float("retry-multiplier", 2.0, "Backoff multiplier (reference RetryMultiplier 2)")
     fs.duration("retry-max-total", 0.0, "Give up retrying after this long (0 = never, as the reference)")
     fs.int("retry-max-attempts", 0, "Give up after this many attempts (0 = unlimited)")
-    fs.string("affinity", "auto", "CPU placement: auto | same | split | numa | none")
+    fs.string("affinity", "auto", "CPU placement: auto | share | same | split | numa | none")
     fs.bool("start-fake-server", False, "Start a node-local synthetic GCS endpoint (no network)")
     fs.int("fake-object-size", 100 << 20, "Synthetic object size (reference objects are ~100 MB)")
     fs.int("fake-objects", -1, "Synthetic objects per rank (default: -worker)")
@@ -123,7 +123,7 @@ def main(argv: list[str] | None = None) -> int:
     placement = {"client": [], "server": []}
     aff = fs.get("affinity")
     if aff == "auto":
-        aff = "same" if sink == "gpu" else "none"
+        aff = ("share" if fs.get("slices") > 1 else "same") if sink == "gpu" else "none"
     if aff != "none" and sink == "gpu":
         from .parallel import affinity
 

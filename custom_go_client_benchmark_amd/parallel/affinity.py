@@ -60,7 +60,11 @@ def l3_groups(cpus: list[int]) -> list[list[int]]:
 def plan(device: int, mode: str = "split") -> dict:
     """CPU sets for this rank: {"client": [...], "server": [...]}.
 
-    mode: "split" (client and endpoint on two L3 domains of the GPU's node),
+    mode: "share" (this rank's fair share of its NUMA node's L3 domains --
+                   node L3 domains / GPUs on the node -- shared by client and
+                   endpoint threads: all 8 domains on a 1-GPU box, 2 per rank
+                   on a full 8-GPU node; best for sliced reads),
+          "split" (client and endpoint on two L3 domains of the GPU's node),
           "same" (one shared L3 domain), "numa" (whole node), "none".
     """
     if mode == "none":
@@ -78,6 +82,10 @@ def plan(device: int, mode: str = "split") -> dict:
     groups = l3_groups(cpus)
     share = max(1, len(groups) // max(1, len(peers)))
     base = (k * share) % max(1, len(groups))
+    if mode == "share":
+        mine = [c for g in groups[base:base + share] for c in g] or cpus
+        return {"client": mine, "server": mine, "mode": mode, "numa_node": node, "gpu_index_on_node": k,
+                "l3_domains": share}
     client = groups[base] if groups else cpus
     if mode == "same" or share < 2:
         server = client

@@ -37,7 +37,7 @@ EXT := $(PKG)/_native$(EXT_SUFFIX)
 TOOLS := fakegcs read_operation ssd_test write_operations list_operation open_file small_poc
 TOOL_BINS := $(addprefix $(PKG)/bin/,$(TOOLS))
 
-.PHONY: all clean ext tools
+.PHONY: all clean ext tools asan tsan stress
 all: ext tools
 ext: $(EXT)
 tools: $(TOOL_BINS)
@@ -61,6 +61,36 @@ $(EXT): $(PY_OBJS) $(GPU_OBJS) $(BUILD)/libgcsbcore.a
 $(PKG)/bin/%: csrc/tools/%.cc $(BUILD)/libgcsbcore.a
 	@mkdir -p $(PKG)/bin
 	$(CXX) $(CPPFLAGS) $(CXXFLAGS) -o $@ $< $(BUILD)/libgcsbcore.a $(LDLIBS)
+
+# Host-side sanitizer builds of the C++ core + a concurrency stress driver
+# (csrc/tests/stress.cc).  GPU code is not sanitized (no GPU ASan on this pool).
+SAN_SRCS := $(CORE_SRCS) csrc/tests/stress.cc
+SAN_OPT  := -O1 -g -fno-omit-frame-pointer
+ASAN_FL  := -fsanitize=address,undefined -fno-sanitize-recover=undefined
+TSAN_FL  := -fsanitize=thread
+$(BUILD)/asan/%.o: csrc/%.cc
+	@mkdir -p $(dir $@)
+	$(CXX) $(CPPFLAGS) $(CXXSTD) $(SAN_OPT) $(HOSTARCH) -pthread $(ASAN_FL) -MMD -MP -c $< -o $@
+$(BUILD)/tsan/%.o: csrc/%.cc
+	@mkdir -p $(dir $@)
+	$(CXX) $(CPPFLAGS) $(CXXSTD) $(SAN_OPT) $(HOSTARCH) -pthread $(TSAN_FL) -MMD -MP -c $< -o $@
+$(BUILD)/plain/%.o: csrc/%.cc
+	@mkdir -p $(dir $@)
+	$(CXX) $(CPPFLAGS) $(CXXSTD) -O2 -g $(HOSTARCH) -pthread -MMD -MP -c $< -o $@
+$(BUILD)/asan/stress: $(patsubst csrc/%.cc,$(BUILD)/asan/%.o,$(SAN_SRCS))
+	$(CXX) -pthread $(ASAN_FL) -o $@ $^ $(LDLIBS)
+$(BUILD)/tsan/stress: $(patsubst csrc/%.cc,$(BUILD)/tsan/%.o,$(SAN_SRCS))
+	$(CXX) -pthread $(TSAN_FL) -o $@ $^ $(LDLIBS)
+$(BUILD)/plain/stress: $(patsubst csrc/%.cc,$(BUILD)/plain/%.o,$(SAN_SRCS))
+	$(CXX) -pthread -o $@ $^ $(LDLIBS)
+asan: $(BUILD)/asan/stress
+	ASAN_OPTIONS=detect_leaks=1 $(BUILD)/asan/stress
+tsan: $(BUILD)/tsan/stress
+	TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1" $(BUILD)/tsan/stress
+stress: $(BUILD)/plain/stress
+	$(BUILD)/plain/stress 3
+
+-include $(patsubst csrc/%.cc,$(BUILD)/asan/%.d,$(SAN_SRCS)) $(patsubst csrc/%.cc,$(BUILD)/tsan/%.d,$(SAN_SRCS))
 
 clean:
 	rm -rf $(BUILD) $(EXT) $(TOOL_BINS)

@@ -286,40 +286,58 @@ void Conn::sendfile_all(int in_fd, uint64_t off, size_t n, bool more) {
 }
 
 Listener::Listener(const std::string& host, int port, int backlog) {
-  fd_ = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
-  if (fd_ < 0) throw std::runtime_error("socket failed");
+  int fd = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  if (fd < 0) throw std::runtime_error("socket failed");
   int one = 1;
-  setsockopt(fd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+  setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
   sockaddr_in addr{};
   addr.sin_family = AF_INET;
   addr.sin_port = htons(static_cast<uint16_t>(port));
   if (inet_pton(AF_INET, host.c_str(), &addr.sin_addr) != 1) addr.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
-  if (::bind(fd_, reinterpret_cast<sockaddr*>(&addr), sizeof(addr)) != 0)
-    throw std::runtime_error("bind " + host + ":" + std::to_string(port) + ": " + std::strerror(errno));
-  if (::listen(fd_, backlog) != 0) throw std::runtime_error("listen failed");
+  if (::bind(fd, reinterpret_cast<sockaddr*>(&addr), sizeof(addr)) != 0) {
+    std::string err = std::strerror(errno);
+    ::close(fd);
+    throw std::runtime_error("bind " + host + ":" + std::to_string(port) + ": " + err);
+  }
+  if (::listen(fd, backlog) != 0) {
+    ::close(fd);
+    throw std::runtime_error("listen failed");
+  }
   socklen_t sl = sizeof(addr);
-  getsockname(fd_, reinterpret_cast<sockaddr*>(&addr), &sl);
+  getsockname(fd, reinterpret_cast<sockaddr*>(&addr), &sl);
   port_ = ntohs(addr.sin_port);
+  fd_ = fd;
 }
 
-Listener::~Listener() { close(); }
+Listener::~Listener() {
+  close();
+  int fd = fd_.exchange(-1);
+  if (fd >= 0) ::close(fd);
+}
 
 int Listener::accept_fd() {
   for (;;) {
-    int fd = fd_;
-    if (fd < 0) return -1;
-    int c = ::accept4(fd, nullptr, nullptr, SOCK_CLOEXEC);
-    if (c >= 0) return c;
+    if (closed_.load(std::memory_order_acquire)) return -1;
+    int c = ::accept4(fd_.load(std::memory_order_relaxed), nullptr, nullptr, SOCK_CLOEXEC);
+    if (c >= 0) {
+      if (closed_.load(std::memory_order_acquire)) {
+        ::close(c);
+        return -1;
+      }
+      return c;
+    }
     if (errno == EINTR || errno == ECONNABORTED) continue;
     return -1;
   }
 }
 
+// Wakes a blocked accept_fd() (shutdown) without releasing the descriptor:
+// the fd number cannot be reused under a concurrent accept4; the destructor
+// closes it once the accepting thread is gone.
 void Listener::close() {
-  if (fd_ >= 0) {
-    ::shutdown(fd_, SHUT_RDWR);
-    ::close(fd_);
-    fd_ = -1;
+  if (!closed_.exchange(true, std::memory_order_acq_rel)) {
+    int fd = fd_.load(std::memory_order_relaxed);
+    if (fd >= 0) ::shutdown(fd, SHUT_RDWR);
   }
 }
 

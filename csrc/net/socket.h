@@ -6,6 +6,7 @@
 // connections (reference main.go:65-73); grpc-go dials one HTTP/2 connection
 // per pool entry (main.go:30,111).
 #pragma once
+#include <atomic>
 #include <sys/uio.h>
 
 #include <cstddef>
@@ -75,13 +76,14 @@ class Listener {
   explicit Listener(const std::string& host, int port, int backlog = 1024);
   ~Listener();
   int port() const { return port_; }
-  int fd() const { return fd_; }
+  int fd() const { return fd_.load(std::memory_order_relaxed); }
   // Returns -1 when closed.
   int accept_fd();
   void close();
 
  private:
-  int fd_ = -1;
+  std::atomic<int> fd_{-1};
+  std::atomic<bool> closed_{false};
   int port_ = 0;
 };
 

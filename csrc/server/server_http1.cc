@@ -397,6 +397,7 @@ class Http1Handler {
   void stream_bytes(const StoredObject& o, uint64_t start, uint64_t len) {
     auto& f = srv_.faults();
     int64_t disc = f.disconnect_count.load() > 0 ? f.disconnect_at.load() : -1;
+    const int64_t disc_at = disc;
     int64_t corrupt = f.corrupt_count.load() > 0 ? f.corrupt_at.load() : -1;
     int64_t bps = f.throttle_bps.load();
     int64_t t0 = now_ns();
@@ -407,25 +408,28 @@ class Http1Handler {
       uint64_t n = std::min<uint64_t>(piece_max, len - sent);
       if (bps > 0) n = std::min<uint64_t>(n, std::max<int64_t>(4096, bps / 100));
       if (disc >= 0 && static_cast<int64_t>(off + n) > disc && static_cast<int64_t>(off) <= disc) {
-        uint64_t k = static_cast<uint64_t>(disc) - off;
-        if (k) c_.write_all(o.bytes(off, k), k);
+        disc = -1;  // at most once per response
+        // claim one of the remaining faults (concurrent responses race for it)
         if (f.disconnect_count.fetch_sub(1) > 0) {
+          uint64_t k = static_cast<uint64_t>(disc_at) - off;
+          if (k) c_.write_all(o.bytes(off, k), k);
           ++srv_.stats().faults_injected;
           srv_.stats().bytes_sent += sent + k;
           ::shutdown(c_.fd(), SHUT_RDWR);
           throw CloseConnection{};
         }
-        sent += k;
         continue;
       }
       if (corrupt >= 0 && static_cast<int64_t>(off) <= corrupt && static_cast<int64_t>(off + n) > corrupt) {
-        uint64_t k = static_cast<uint64_t>(corrupt) - off;
-        if (k) c_.write_all(o.bytes(off, k), k);
-        uint8_t bad = static_cast<uint8_t>(o.bytes(off + k, 1)[0] ^ 0x5A);
-        c_.write_all(&bad, 1);
-        if (f.corrupt_count.fetch_sub(1) > 0) ++srv_.stats().faults_injected;
+        const uint64_t k = static_cast<uint64_t>(corrupt) - off;
         corrupt = -1;
-        sent += k + 1;
+        if (f.corrupt_count.fetch_sub(1) > 0) {
+          ++srv_.stats().faults_injected;
+          if (k) c_.write_all(o.bytes(off, k), k);
+          uint8_t bad = static_cast<uint8_t>(o.bytes(off + k, 1)[0] ^ 0x5A);
+          c_.write_all(&bad, 1);
+          sent += k + 1;
+        }
         continue;
       }
       int ffd = -1;

@@ -64,7 +64,7 @@ void H2ClientConn::start_stream(const std::shared_ptr<H2ClientStream>& s, const 
   std::string block;
   enc_.encode(headers, &block);
   std::lock_guard<std::mutex> olk(open_mu_);  // stream ids must hit the wire in order
-  if (!usable()) throw StorageError("http2 connection unusable: " + dead_reason_, true);
+  if (!usable()) throw StorageError("http2 connection unusable: " + dead_reason(), true);
   if (next_id_ > 0x7FFFFFF0) {
     goaway_ = true;
     throw StorageError("http2 stream ids exhausted", true);
@@ -90,7 +90,7 @@ void H2ClientConn::start_stream_with_body(const std::shared_ptr<H2ClientStream>&
   enc_.encode(headers, &block);
   {
     std::lock_guard<std::mutex> olk(open_mu_);
-    if (!usable()) throw StorageError("http2 connection unusable: " + dead_reason_, true);
+    if (!usable()) throw StorageError("http2 connection unusable: " + dead_reason(), true);
     if (next_id_ > 0x7FFFFFF0) {
       goaway_ = true;
       throw StorageError("http2 stream ids exhausted", true);
@@ -132,7 +132,7 @@ void H2ClientConn::send_data_iov(H2ClientStream& s, struct iovec* iov, int cnt, 
   std::vector<iovec> piece;
   while (left > 0) {
     size_t n = w_->reserve(s.id_, left);
-    if (n == 0) throw StorageError("http2 stream closed while sending: " + dead_reason_, true);
+    if (n == 0) throw StorageError("http2 stream closed while sending: " + dead_reason(), true);
     piece.clear();
     size_t need = n;
     while (need > 0) {
@@ -167,8 +167,11 @@ void H2ClientConn::end_stream(H2ClientStream& s, bool reset) {
 }
 
 void H2ClientConn::fail_all(const std::string& msg) {
+  {
+    std::lock_guard<std::mutex> lk(reason_mu_);
+    if (dead_reason_.empty()) dead_reason_ = msg;
+  }
   dead_ = true;
-  if (dead_reason_.empty()) dead_reason_ = msg;
   w_->kill();
   std::map<uint32_t, std::shared_ptr<H2ClientStream>> s;
   {

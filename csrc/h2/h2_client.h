@@ -83,7 +83,12 @@ class H2ClientConn {
   RecvWindow conn_recv_{64 << 20};
   std::atomic<bool> dead_{false}, goaway_{false};
   uint32_t goaway_last_ = 0x7FFFFFFF;
-  std::string dead_reason_;
+  mutable std::mutex reason_mu_;
+  std::string dead_reason_;  // guarded by reason_mu_ (written by the reader thread)
+  std::string dead_reason() const {
+    std::lock_guard<std::mutex> lk(reason_mu_);
+    return dead_reason_;
+  }
 };
 
 }  // namespace gcsb

@@ -56,7 +56,7 @@ $(BUILD)/libgcsbcore.a: $(CORE_OBJS)
 
 $(EXT): $(PY_OBJS) $(GPU_OBJS) $(BUILD)/libgcsbcore.a
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(PY_OBJS) $(GPU_OBJS) $(BUILD)/libgcsbcore.a \
-	  -L/opt/rocm/lib -lamdhip64 $(LDLIBS) -Wl,-rpath,/opt/rocm/lib
+	  -L/opt/rocm/lib -lamdhip64 -lrocprofiler-sdk-roctx $(LDLIBS) -Wl,-rpath,/opt/rocm/lib
 
 $(PKG)/bin/%: csrc/tools/%.cc $(BUILD)/libgcsbcore.a
 	@mkdir -p $(PKG)/bin

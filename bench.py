@@ -85,7 +85,8 @@ def main() -> int:
     # Node-local synthetic GCS endpoint for this rank (no network on the box).
     from custom_go_client_benchmark_amd.parallel import affinity
 
-    placement = affinity.plan(local_rank, args.affinity) if use_gpu else {"client": [], "server": []}
+    gpu = ctx.gpu if ctx.gpu >= 0 else 0
+    placement = affinity.plan(gpu, args.affinity) if use_gpu else {"client": [], "server": []}
     srv = n.Server({"port": 0, "md5": False, "cpus": placement["server"]})
     srv.start()
     bucket = "princer-working-dirs"
@@ -102,7 +103,7 @@ def main() -> int:
         "reads_per_worker": args.warmup,
         "worker_id_offset": first,
         "sink": args.sink,
-        "device": local_rank if use_gpu else 0,
+        "device": gpu if use_gpu else 0,
         "ring_slot_bytes": parse_size(args.slot_bytes),
         "ring_slots": args.slots,
         "landing": "object",

@@ -1,5 +1,7 @@
 #include "bench/runner.h"
 
+#include "gpu/markers.h"
+
 #include <unistd.h>
 
 #include <algorithm>
@@ -184,6 +186,7 @@ void Runner::worker_main(int w) {
       // OTel TraceIDRatioBased: lower 8 bytes of the trace id >> 1 < rate * 2^63
       r.sampled = cfg_.trace_sample_rate >= 1.0 || (r.trace_lo >> 1) < sample_bound;
     }
+    RoctxRange rg(sliced ? "gcsb.read_object(sliced)" : "gcsb.read_object");
     r.start_wall_ns = wall_ns();
     r.start_ns = now_ns();
     double ms = 0, host_ms = 0;

@@ -11,6 +11,7 @@
 
 #include "core/crc32c.h"
 #include "core/util.h"
+#include "gpu/markers.h"
 
 namespace gcsb {
 
@@ -341,6 +342,7 @@ void GpuSink::resume_at(int64_t offset) {
 
 void GpuSink::submit_current() {
   if (cur_ < 0) return;
+  RoctxRange rg("gcsb.slot_submit");
   Slot& s = slots_[cur_];
   cur_ = -1;
   if (s.used == 0) {
@@ -382,6 +384,7 @@ void GpuSink::submit_current() {
 
 void GpuSink::wait_slot(Slot& s) {
   if (!s.inflight) return;
+  RoctxRange rg("gcsb.wait_slot");
   set_device();
   hip_check(hipEventSynchronize(s.ev), "hipEventSynchronize");
   s.inflight = false;
@@ -432,6 +435,7 @@ void GpuSink::harvest(Slot& s) {
 
 SinkResult GpuSink::finish() {
   submit_current();
+  RoctxRange rg("gcsb.wait_landed");
   for (int k = 0; k < cfg_.slots; ++k) wait_slot(slots_[(next_ + k) % cfg_.slots]);
   SinkResult r;
   r.bytes = delivered_;

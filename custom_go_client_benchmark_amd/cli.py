@@ -117,6 +117,8 @@ def main(argv: list[str] | None = None) -> int:
     device = fs.get("gpu-device") if fs.get("gpu-device") >= 0 else local_rank
     if world > 1 or sink == "gpu":
         ctx = dist.init(local_rank=local_rank, world=world, rank=rank)
+        if fs.get("gpu-device") < 0 and ctx.gpu >= 0:
+            device = ctx.gpu
     workers = fs.get("worker")
     first = rank * workers
 

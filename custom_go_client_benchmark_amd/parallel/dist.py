@@ -25,7 +25,8 @@ class DistContext:
     rank: int = 0
     world: int = 1
     local_rank: int = 0
-    device: object = None
+    device: object = None       # where control-plane tensors live (cuda:<gpu> for RCCL, cpu for gloo)
+    gpu: int = -1               # this rank's HIP device, -1 without a GPU
     backend: str = "none"
     initialized_here: bool = False
 
@@ -37,8 +38,21 @@ def env_rank() -> tuple[int, int, int]:
     return rank, world, local
 
 
+def local_device(local_rank: int) -> int:
+    """HIP device of a local rank: LOCAL_RANK on a full node (one rank per
+    GPU).  More ranks than visible GPUs only happens in rehearsals
+    (GCSB_DIST_BACKEND=gloo on a 1-GPU box) and wraps around."""
+    import torch
+
+    n = torch.cuda.device_count()
+    return local_rank % n if n > 0 else -1
+
+
 def init(local_rank: int | None = None, world: int | None = None, rank: int | None = None,
          backend: str | None = None, timeout_s: float = 600.0) -> DistContext:
+    """backend None: "nccl" (RCCL) with a GPU, "gloo" without.  The
+    GCSB_DIST_BACKEND env var overrides it (gloo rehearsals of N ranks on a
+    box with fewer GPUs: RCCL rejects two ranks on one GPU)."""
     import torch
     import torch.distributed as dist
 
@@ -48,9 +62,11 @@ def init(local_rank: int | None = None, world: int | None = None, rank: int | No
     local_rank = lr if local_rank is None else local_rank
     ctx = DistContext(rank=rank, world=world, local_rank=local_rank)
     use_cuda = torch.cuda.is_available()
+    backend = backend or os.environ.get("GCSB_DIST_BACKEND") or None
     if use_cuda:
-        torch.cuda.set_device(local_rank)
-        ctx.device = torch.device("cuda", local_rank)
+        ctx.gpu = local_device(local_rank)
+        torch.cuda.set_device(ctx.gpu)
+        ctx.device = torch.device("cuda", ctx.gpu) if backend in (None, "nccl") else torch.device("cpu")
     else:
         ctx.device = torch.device("cpu")
     if world > 1:
@@ -78,8 +94,8 @@ def barrier(ctx: DistContext) -> None:
 
     t = torch.ones(1, dtype=torch.int32, device=ctx.device)
     dist.all_reduce(t)
-    if ctx.device.type == "cuda":
-        torch.cuda.synchronize(ctx.device)
+    if ctx.gpu >= 0:
+        torch.cuda.synchronize(ctx.gpu)
     if int(t.item()) != ctx.world:
         raise RuntimeError(f"barrier mismatch: {int(t.item())} != {ctx.world}")
 

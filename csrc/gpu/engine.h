@@ -15,7 +15,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <condition_variable>
 #include <cstdint>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -39,6 +41,15 @@ struct GpuSinkConfig {
   // Submit a partially filled slot when at least this many bytes are waiting
   // and the socket has nothing more right now (0 = only full slots).
   size_t eager_submit_bytes = 0;
+  // Slot hand-off (H2D copy + CRC launches + events) runs on one per-device
+  // submitter thread instead of the transport thread: transport threads never
+  // contend for the HIP runtime's locks (8 sliced streams calling HIP at once
+  // spent ~170 us per slot there, profiles/r1_markers).  Env GCSB_ASYNC_SUBMIT.
+  bool async_submit = true;
+  // Wait on slot events by blocking (interrupt) instead of spinning: under the
+  // GPU box's CPU quota (16 CPUs) spinning waiters steal cycles from the
+  // receiving threads.  Env GCSB_EVENT_SPIN=1 selects spinning.
+  bool blocking_sync = true;
 };
 
 struct GpuSinkStats {
@@ -98,8 +109,11 @@ class GpuSink : public Sink {
     hipEvent_t ev = nullptr;      // slot done: copy landed + CRC kernels finished
     hipEvent_t copied = nullptr;  // copy landed (CRC stream waits on it)
     bool inflight = false;
+    bool submitted = false;       // async: the submitter has recorded `ev` (guarded by sub_mu_)
     CrcSegResult* res = nullptr;  // host-mapped, kMaxSeg entries
+    CrcSegResult* d_res = nullptr;  // device alias of res
   };
+  void enqueue_slot(Slot& s, uint8_t* dst, const CrcBatch* batch);
   void ensure_object_capacity(int64_t size);
   void grow_object_buffer(uint64_t need);
   Slot& take_slot();
@@ -141,6 +155,8 @@ class GpuSink : public Sink {
   uint32_t op_val_[4] = {0, 0, 0, 0};
   int op_rr_ = 0;
   GpuSinkStats stats_;
+  std::mutex sub_mu_;
+  std::condition_variable sub_cv_;
 };
 
 // Upload source for the write path (config 5): HBM -> pinned ring via

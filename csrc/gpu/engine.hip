@@ -5,8 +5,11 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <functional>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <stdexcept>
 
 #include "core/crc32c.h"
@@ -108,9 +111,71 @@ int gpu_device_count() {
   return n;
 }
 
-void GpuSink::set_device() const { hip_check(hipSetDevice(cfg_.device), "hipSetDevice"); }
+namespace {
+// hipSetDevice only when this thread's current device differs.
+void ensure_device(int dev) {
+  thread_local int cur = -1;
+  if (cur != dev) {
+    hip_check(hipSetDevice(dev), "hipSetDevice");
+    cur = dev;
+  }
+}
+
+bool env_flag(const char* name, bool dflt) {
+  const char* e = std::getenv(name);
+  if (!e || !*e) return dflt;
+  return *e == '1' || *e == 't' || *e == 'T' || *e == 'y' || *e == 'Y';
+}
+
+// One thread per device that issues every queued ring-slot hand-off, so HIP
+// API calls are made by one thread instead of contending from many transport
+// threads.  Jobs run in FIFO order; each job is a few async HIP calls.
+class DeviceSubmitter {
+ public:
+  static DeviceSubmitter& get(int dev) {
+    static std::mutex mu;
+    static std::map<int, DeviceSubmitter*> all;  // process lifetime (never joined at exit)
+    std::lock_guard<std::mutex> lk(mu);
+    auto& p = all[dev];
+    if (!p) p = new DeviceSubmitter(dev);
+    return *p;
+  }
+  void post(std::function<void()> f) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      q_.push_back(std::move(f));
+    }
+    cv_.notify_one();
+  }
+
+ private:
+  explicit DeviceSubmitter(int dev) : dev_(dev) {
+    std::thread([this] { loop(); }).detach();
+  }
+  void loop() {
+    ensure_device(dev_);
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [&] { return !q_.empty(); });
+      auto f = std::move(q_.front());
+      q_.pop_front();
+      lk.unlock();
+      f();
+      lk.lock();
+    }
+  }
+  int dev_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+};
+}  // namespace
+
+void GpuSink::set_device() const { ensure_device(cfg_.device); }
 
 GpuSink::GpuSink(const GpuSinkConfig& cfg) : cfg_(cfg) {
+  cfg_.async_submit = env_flag("GCSB_ASYNC_SUBMIT", cfg_.async_submit);
+  if (env_flag("GCSB_EVENT_SPIN", false)) cfg_.blocking_sync = false;
   if (cfg_.slots < 2) cfg_.slots = 2;
   cfg_.slot_bytes = (cfg_.slot_bytes + 4095) / 4096 * 4096;
   if (cfg_.slot_bytes < 65536) cfg_.slot_bytes = 65536;
@@ -135,14 +200,17 @@ GpuSink::GpuSink(const GpuSinkConfig& cfg) : cfg_(cfg) {
     s.host = static_cast<uint8_t*>(PinnedPool::get(cfg_.slot_bytes));
     if (cfg_.landing == Landing::kRing)
       hip_check(hipMalloc(reinterpret_cast<void**>(&s.dev_ring), cfg_.slot_bytes), "hipMalloc(ring slot)");
-    hip_check(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming), "hipEventCreate");
+    const unsigned evf = hipEventDisableTiming | (cfg_.blocking_sync ? hipEventBlockingSync : 0u);
+    hip_check(hipEventCreateWithFlags(&s.ev, evf), "hipEventCreate");
     hip_check(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming), "hipEventCreate");
     s.res = res_host_ + static_cast<size_t>(i) * kMaxSeg;
+    hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&s.d_res), s.res, 0), "hipHostGetDevicePointer");
   }
 }
 
 GpuSink::~GpuSink() {
   try {
+    for (Slot& sl : slots_) wait_slot(sl);  // no queued hand-off may outlive the sink
     set_device();
     if (stream_) (void)hipStreamSynchronize(stream_);
     if (crc_stream_) (void)hipStreamSynchronize(crc_stream_);
@@ -351,11 +419,10 @@ void GpuSink::submit_current() {
     return;
   }
   if (!s.segs.empty()) s.segs.back().closed = true;
-  set_device();
   uint8_t* dst = cfg_.landing == Landing::kObject ? obj_dst_ + s.obj_off : s.dev_ring;
-  hip_check(hipMemcpyAsync(dst, s.host, s.used, hipMemcpyHostToDevice, stream_), "hipMemcpyAsync(H2D)");
-  if (cfg_.verify && !s.segs.empty()) {
-    CrcBatch b;
+  CrcBatch b;
+  const bool crc = cfg_.verify && !s.segs.empty();
+  if (crc) {
     std::memset(&b, 0, sizeof(b));
     b.nseg = static_cast<uint32_t>(s.segs.size());
     for (size_t i = 0; i < s.segs.size(); ++i) {
@@ -368,23 +435,66 @@ void GpuSink::submit_current() {
     }
     finalize_crc_batch(&b);
     if (b.total_tiles > tiles_cap_) throw std::logic_error("CRC tile scratch too small");
-    CrcSegResult* d_res = nullptr;
-    hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_res), s.res, 0), "hipHostGetDevicePointer");
-    hip_check(hipEventRecord(s.copied, stream_), "hipEventRecord");
-    hip_check(hipStreamWaitEvent(crc_stream_, s.copied, 0), "hipStreamWaitEvent");
-    launch_crc32c_batch(b, d_tables_, d_tiles_, d_res, crc_stream_);
     stats_.segments += s.segs.size();
-    hip_check(hipEventRecord(s.ev, crc_stream_), "hipEventRecord");
-  } else {
-    hip_check(hipEventRecord(s.ev, stream_), "hipEventRecord");
   }
   s.inflight = true;
   ++stats_.slots_submitted;
+  enqueue_slot(s, dst, crc ? &b : nullptr);
+}
+
+// The slot's H2D copy, CRC launches and completion event.  Runs on the
+// device submitter thread (async_submit) or inline.
+void GpuSink::enqueue_slot(Slot& s, uint8_t* dst, const CrcBatch* batch) {
+  auto issue = [this, &s, dst](const CrcBatch* b) {
+    ensure_device(cfg_.device);
+    hip_check(hipMemcpyAsync(dst, s.host, s.used, hipMemcpyHostToDevice, stream_), "hipMemcpyAsync(H2D)");
+    if (b) {
+      hip_check(hipEventRecord(s.copied, stream_), "hipEventRecord");
+      hip_check(hipStreamWaitEvent(crc_stream_, s.copied, 0), "hipStreamWaitEvent");
+      launch_crc32c_batch(*b, d_tables_, d_tiles_, s.d_res, crc_stream_);
+      hip_check(hipEventRecord(s.ev, crc_stream_), "hipEventRecord");
+    } else {
+      hip_check(hipEventRecord(s.ev, stream_), "hipEventRecord");
+    }
+  };
+  if (!cfg_.async_submit) {
+    s.submitted = true;
+    issue(batch);
+    return;
+  }
+  {
+    std::lock_guard<std::mutex> lk(sub_mu_);
+    s.submitted = false;
+  }
+  const bool has = batch != nullptr;
+  CrcBatch copy;
+  if (has) copy = *batch;
+  DeviceSubmitter::get(cfg_.device).post([this, &s, issue, has, copy]() {
+    std::string err;
+    try {
+      issue(has ? &copy : nullptr);
+    } catch (const std::exception& e) {
+      err = e.what();
+    }
+    {
+      std::lock_guard<std::mutex> lk(sub_mu_);
+      s.submitted = true;
+      if (!err.empty() && detail_.empty()) {
+        mismatch_ = true;
+        detail_ = "GPU submit failed: " + err;
+      }
+    }
+    sub_cv_.notify_all();
+  });
 }
 
 void GpuSink::wait_slot(Slot& s) {
   if (!s.inflight) return;
   RoctxRange rg("gcsb.wait_slot");
+  if (cfg_.async_submit) {
+    std::unique_lock<std::mutex> lk(sub_mu_);
+    sub_cv_.wait(lk, [&] { return s.submitted; });
+  }
   set_device();
   hip_check(hipEventSynchronize(s.ev), "hipEventSynchronize");
   s.inflight = false;
@@ -470,6 +580,10 @@ void GpuSink::abort() {
   set_device();
   for (Slot& s : slots_)
     if (s.inflight) {
+      if (cfg_.async_submit) {  // the hand-off may still be queued on the submitter
+        std::unique_lock<std::mutex> lk(sub_mu_);
+        sub_cv_.wait(lk, [&] { return s.submitted; });
+      }
       hip_check(hipEventSynchronize(s.ev), "hipEventSynchronize");
       s.inflight = false;
     }

@@ -41,11 +41,14 @@ struct GpuSinkConfig {
   // Submit a partially filled slot when at least this many bytes are waiting
   // and the socket has nothing more right now (0 = only full slots).
   size_t eager_submit_bytes = 0;
-  // Slot hand-off (H2D copy + CRC launches + events) runs on one per-device
-  // submitter thread instead of the transport thread: transport threads never
-  // contend for the HIP runtime's locks (8 sliced streams calling HIP at once
-  // spent ~170 us per slot there, profiles/r1_markers).  Env GCSB_ASYNC_SUBMIT.
-  bool async_submit = true;
+  // Slot hand-off (H2D copy + CRC launches + events) on one per-device
+  // submitter thread instead of the transport thread.  Cuts the transport
+  // thread's hand-off from ~170 us to ~3 us per slot with 8 sliced streams
+  // (HIP runtime lock contention, profiles/r1_markers), but the A/B on the
+  // headline bench (profiles/r1_submit_ab) shows equal throughput and ~2 ms
+  // worse p99 under the box's 16-CPU quota (one more thread to throttle), so
+  // it is opt-in.  Env GCSB_ASYNC_SUBMIT=1.
+  bool async_submit = false;
   // Wait on slot events by blocking (interrupt) instead of spinning: under the
   // GPU box's CPU quota (16 CPUs) spinning waiters steal cycles from the
   // receiving threads.  Env GCSB_EVENT_SPIN=1 selects spinning.

@@ -77,6 +77,8 @@ GpuSinkConfig gpu_from(const py::dict& d) {
   g.slots = get_or<int>(d, "ring_slots", 4);
   g.verify = get_or<bool>(d, "gpu_verify", true);
   g.landing = get_or<std::string>(d, "landing", "object") == "ring" ? Landing::kRing : Landing::kObject;
+  g.async_submit = get_or<bool>(d, "async_submit", g.async_submit);
+  g.blocking_sync = get_or<bool>(d, "blocking_sync", g.blocking_sync);
   return g;
 }
 

@@ -174,3 +174,31 @@ def test_sliced_gpu_read_detects_corruption(native, server, gpu_available):
     r.wait()
     s = r.summary()
     assert s["errors"] == 1 and "bad CRC" in s["first_error"]
+
+
+@pytest.mark.parametrize("async_submit,blocking", [(True, True), (True, False), (False, False)])
+def test_submit_modes_byte_exact(native, server, gpu_available, async_submit, blocking):
+    """Every hand-off mode (submitter thread / inline, blocking / spinning
+    event waits) lands the same bytes and verifies every chunk."""
+    size = (21 << 20) + 99
+    server.add_synthetic(B, P, "", 0, 1, size)
+    for proto in ("http", "grpc"):
+        r = native.Runner({"protocol": proto, "endpoint": server.url, "bucket": B, "object_prefix": P, "workers": 1,
+                           "reads_per_worker": 3, "sink": "gpu", "slices": 3, "ring_slot_bytes": 2 << 20,
+                           "ring_slots": 3, "keep_records": False, "async_submit": async_submit,
+                           "blocking_sync": blocking})
+        r.start()
+        r.wait()
+        s = r.summary()
+        assert s["errors"] == 0 and s["verified"] == 3, s["first_error"]
+        bad, first = native.gpu_verify_pattern(0, r.landing_ptr(0), size, P + "0", 0)
+        assert bad == 0, (proto, first)
+
+
+def test_async_submit_detects_corruption(native, server, gpu_available):
+    server.add_synthetic(B, P, "", 0, 1, 6 << 20)
+    server.set_faults({"corrupt_at": (3 << 20) + 5, "corrupt_count": 1})
+    c = native.Client({"protocol": "grpc", "endpoint": server.url})
+    sink = native.GpuSink({"device": 0, "ring_slot_bytes": 1 << 20, "ring_slots": 2, "async_submit": True})
+    r = c.read_gpu(B, P + "0", sink)
+    assert r["crc_mismatch"] and not r["verified"]

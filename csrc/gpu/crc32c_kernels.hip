@@ -1,9 +1,13 @@
 // CDNA4 (gfx950) CRC32C kernels + synthetic-pattern fill/verify kernels.
-// Design notes in crc32c_gpu.h.  Wave64 throughout: a 4 KiB tile is exactly
-// one wave-instruction of 16 B per lane x 4 rows, so the loads are perfectly
-// coalesced 1 KiB global_load_dwordx4 and need no LDS round trip (the data has
-// no reuse); the LDS instead holds the 44 KiB of lookup tables that every
-// lane hits ~20 times per 16 bytes.
+// Design notes in crc32c_gpu.h.  Wave64 throughout: a wave owns a 16 KiB tile
+// and lane l CRCs its own contiguous 256-byte run (16 global_load_dwordx4 in
+// flight per lane; the data has no reuse so it never touches LDS).  The LDS
+// holds the 40 KiB of lookup tables: slice-by-16 (16 lookups per 16 B) plus
+// the 6 wave-tree shift tables (24 lookups per lane per tile, i.e. 1.5 per
+// 16 B).  Table lookups are random ds_read_b32 and set the kernel's pace
+// (profiles/r1_crc_pmc_summary.json), so the design minimises lookups per
+// byte: contiguous runs need no gap shifts (the round-0 kernel's 4 KiB tiles
+// with 16 B-strided lanes spent 36 % of its lookups on shifts).
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -23,8 +27,8 @@ void hip_check(hipError_t e, const char* what) {
 
 namespace {
 
-constexpr int kK1Threads = 256;                       // 4 waves, one tile each per iteration
-constexpr int kLdsWords = 16 * 256 + 7 * 4 * 256;     // slice16 + 7 lane shift tables = 11264 words (44 KiB)
+constexpr int kK1Threads = 512;                       // 8 waves (tiles) per workgroup: amortise the table fill
+constexpr int kLdsWords = 16 * 256 + 6 * 4 * 256;     // slice16 + 6 wave-tree shift tables = 10240 words (40 KiB)
 
 __device__ __forceinline__ uint32_t shift4(const uint32_t* __restrict__ tab, uint32_t s) {
   return tab[s & 0xff] ^ tab[256 + ((s >> 8) & 0xff)] ^ tab[512 + ((s >> 16) & 0xff)] ^ tab[768 + (s >> 24)];
@@ -77,12 +81,17 @@ __global__ __launch_bounds__(kK1Threads) void crc32c_tiles_kernel(const CrcBatch
     const uint64_t full = (addr + len - a16 + 15) / 16 - 1;
     const intptr_t vend = static_cast<intptr_t>(a16 + 16 * full);
     const intptr_t tstart = vend - static_cast<intptr_t>(kCrcTile) * static_cast<intptr_t>(b.seg[s].ntiles - t);
-    uint4 v[4];
+    const intptr_t run = tstart + static_cast<intptr_t>(kCrcRunBytes) * lane;
+    uint4 v[kCrcLaneRun];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const intptr_t p = tstart + 1024 * j + 16 * lane;
+    for (int j = 0; j < kCrcLaneRun; ++j) {
+      const intptr_t p = run + 16 * j;
       v[j] = make_uint4(0, 0, 0, 0);
       if (p + 16 > static_cast<intptr_t>(addr)) v[j] = *reinterpret_cast<const uint4*>(p);
+    }
+#pragma unroll
+    for (int j = 0; j < kCrcLaneRun; ++j) {
+      const intptr_t p = run + 16 * j;
       if (p < static_cast<intptr_t>(addr) && p + 16 > static_cast<intptr_t>(addr)) {
         const int h = static_cast<int>(static_cast<intptr_t>(addr) - p);  // 1..15 leading bytes to zero
         v[j].x = mask_low_bytes(v[j].x, h);
@@ -91,10 +100,10 @@ __global__ __launch_bounds__(kK1Threads) void crc32c_tiles_kernel(const CrcBatch
         v[j].w = mask_low_bytes(v[j].w, h - 12);
       }
     }
-    uint32_t state = update16(sl, 0u, v[0]);
+    uint32_t state = 0;
 #pragma unroll
-    for (int j = 1; j < 4; ++j) state = update16(sl, shift4(lane_shift + 6 * 1024, state), v[j]);  // +1008 B gap
-    // wave tree: lane l ends at tile offset 3072 + 16(l+1); fold to the tile end
+    for (int j = 0; j < kCrcLaneRun; ++j) state = update16(sl, state, v[j]);
+    // wave tree: lane l's run ends kCrcRunBytes * (63 - l) before the tile end
 #pragma unroll
     for (int lv = 0; lv < 6; ++lv) {
       const uint32_t other = __shfl_down(state, 1 << lv, 64);
@@ -251,7 +260,8 @@ void launch_crc32c_batch(const CrcBatch& b, const CrcTables* d_tables, uint32_t*
                          CrcSegResult* d_results, hipStream_t stream) {
   if (b.nseg == 0) return;
   if (b.total_tiles > 0) {
-    uint32_t blocks = (b.total_tiles + 3) / 4;
+    constexpr uint32_t tiles_per_block = kK1Threads / 64;
+    uint32_t blocks = (b.total_tiles + tiles_per_block - 1) / tiles_per_block;
     if (blocks > 1024) blocks = 1024;
     hipLaunchKernelGGL(crc32c_tiles_kernel, dim3(blocks), dim3(kK1Threads), 0, stream, b,
                        reinterpret_cast<const uint32_t*>(d_tables), d_tile_scratch);

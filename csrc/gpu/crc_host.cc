@@ -10,9 +10,8 @@ namespace gcsb {
 
 void build_crc_tables(CrcTables* t) {
   crc32c_build_slice16(t->slice16);
-  for (int lv = 0; lv < 6; ++lv) crc32c_build_shift_table(16ull << lv, t->lane_shift[lv]);
-  crc32c_build_shift_table(1008, t->lane_shift[6]);
-  for (int lv = 0; lv < 9; ++lv) crc32c_build_shift_table(4096ull << lv, t->tile_shift[lv]);
+  for (int lv = 0; lv < 6; ++lv) crc32c_build_shift_table(static_cast<uint64_t>(kCrcRunBytes) << lv, t->lane_shift[lv]);
+  for (int lv = 0; lv < 9; ++lv) crc32c_build_shift_table(static_cast<uint64_t>(kCrcTile) << lv, t->tile_shift[lv]);
 }
 
 void finalize_crc_batch(CrcBatch* b) {
@@ -55,24 +54,23 @@ CrcSegResult emulate_crc32c_segment(const uint8_t* addr_p, uint32_t len, const C
     const uintptr_t a16 = addr & ~uintptr_t(15);
     const uint64_t full = (addr + len - a16 + 15) / 16 - 1;
     const intptr_t vend = static_cast<intptr_t>(a16 + 16 * full);
-    const intptr_t tstart = vend - 4096 * static_cast<intptr_t>(T - tt);
+    const intptr_t tstart = vend - static_cast<intptr_t>(kCrcTile) * static_cast<intptr_t>(T - tt);
     uint32_t lanes[64];
     for (int lane = 0; lane < 64; ++lane) {
-      uint32_t v[4][4];
-      for (int j = 0; j < 4; ++j) {
-        const intptr_t p = tstart + 1024 * j + 16 * lane;
-        std::memset(v[j], 0, 16);
-        if (p + 16 > static_cast<intptr_t>(addr)) std::memcpy(v[j], reinterpret_cast<const void*>(p), 16);
+      uint32_t state = 0;
+      for (int j = 0; j < kCrcLaneRun; ++j) {
+        const intptr_t p = tstart + static_cast<intptr_t>(kCrcRunBytes) * lane + 16 * j;
+        uint32_t v[4] = {0, 0, 0, 0};
+        if (p + 16 > static_cast<intptr_t>(addr)) std::memcpy(v, reinterpret_cast<const void*>(p), 16);
         if (p < static_cast<intptr_t>(addr) && p + 16 > static_cast<intptr_t>(addr)) {
           const int h = static_cast<int>(static_cast<intptr_t>(addr) - p);
-          v[j][0] = mask_low_bytes(v[j][0], h);
-          v[j][1] = mask_low_bytes(v[j][1], h - 4);
-          v[j][2] = mask_low_bytes(v[j][2], h - 8);
-          v[j][3] = mask_low_bytes(v[j][3], h - 12);
+          v[0] = mask_low_bytes(v[0], h);
+          v[1] = mask_low_bytes(v[1], h - 4);
+          v[2] = mask_low_bytes(v[2], h - 8);
+          v[3] = mask_low_bytes(v[3], h - 12);
         }
+        state = update16(t.slice16, state, v);
       }
-      uint32_t state = update16(t.slice16, 0, v[0]);
-      for (int j = 1; j < 4; ++j) state = update16(t.slice16, shift4(t.lane_shift[6], state), v[j]);
       lanes[lane] = state;
     }
     for (int lv = 0; lv < 6; ++lv) {

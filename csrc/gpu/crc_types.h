@@ -5,7 +5,13 @@
 
 namespace gcsb {
 
-constexpr int kCrcTile = 4096;
+// K1 geometry: a wave64 owns one tile; lane l CRCs kCrcLaneRun consecutive
+// 16-byte pieces (a contiguous run), then the 64 runs fold in a 6-level wave
+// tree.  Contiguous runs need no per-piece gap shifts, so LDS lookups per 16 B
+// are 16 (slice-by-16) + 24 / kCrcLaneRun (tree).
+constexpr int kCrcLaneRun = 16;
+constexpr int kCrcRunBytes = 16 * kCrcLaneRun;  // 256 B per lane
+constexpr int kCrcTile = 64 * kCrcRunBytes;     // 16 KiB per wave
 constexpr int kMaxSeg = 32;
 
 struct CrcSeg {
@@ -33,11 +39,11 @@ struct CrcSegResult {
 
 struct CrcTables {
   uint32_t slice16[16][256];
-  uint32_t lane_shift[7][4][256];  // shift by 16,32,64,128,256,512 and 1008 bytes
-  uint32_t tile_shift[9][4][256];  // shift by 4096 * 2^s, s = 0..8 (last = 1 MiB)
+  uint32_t lane_shift[6][4][256];  // shift by kCrcRunBytes * 2^lv (wave tree levels)
+  uint32_t tile_shift[9][4][256];  // shift by kCrcTile * 2^s, s = 0..8 (last = 256 tiles)
 };
 
-// Number of full 16-byte pieces and 4 KiB tiles of a segment (host helper).
+// Number of kCrcTile tiles covering a segment's full 16-byte pieces (host helper).
 inline void crc_segment_geometry(uintptr_t addr, uint32_t len, uint32_t* ntiles) {
   if (len == 0) {
     *ntiles = 0;
@@ -46,7 +52,8 @@ inline void crc_segment_geometry(uintptr_t addr, uint32_t len, uint32_t* ntiles)
   uintptr_t a16 = addr & ~uintptr_t(15);
   uint64_t pieces = (addr + len - a16 + 15) / 16;
   uint64_t full = pieces - 1;
-  *ntiles = static_cast<uint32_t>((full + 255) / 256);
+  constexpr uint64_t per_tile = kCrcTile / 16;
+  *ntiles = static_cast<uint32_t>((full + per_tile - 1) / per_tile);
 }
 
 // Host emulation of K1+K2 (same tables, same tile/lane decomposition) — the

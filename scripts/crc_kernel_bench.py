@@ -23,7 +23,7 @@ def main():
     torch.cuda.synchronize()
     for seg in [2 << 20, 8 << 20, 32 << 20]:
         cover = min(total, seg * 32)
-        gbs, c0 = n.gpu_crc32c_throughput(0, t.data_ptr(), cover, 20, seg)
+        gbs, c0 = n.gpu_crc32c_throughput(0, t.data_ptr(), cover, int(os.environ.get("CRC_ITERS", 20)), seg)
         want = n.crc32c(t[:seg].cpu().numpy().tobytes())
         print(json.dumps({"kernel": "crc32c_tiles+segments", "seg_bytes": seg, "bytes": cover,
                           "GB/s": round(gbs, 1), "crc_ok": c0 == want}), flush=True)

@@ -35,7 +35,8 @@ def test_large_buffer_interleaved_path(native):
 
 
 @pytest.mark.parametrize("misalign", [0, 1, 3, 8, 15])
-@pytest.mark.parametrize("n", [0, 1, 15, 16, 17, 4095, 4096, 4097, 65536 + 5, (1 << 20) + 3])
+@pytest.mark.parametrize("n", [0, 1, 15, 16, 17, 255, 256, 257, 4095, 4096, 4097, 16383, 16384, 16385, 16400,
+                               65536 + 5, (1 << 20) + 3])
 def test_gpu_algorithm_emulation(native, misalign, n):
     d = os.urandom(n)
     want = native.crc32c(d)
@@ -47,8 +48,8 @@ def test_gpu_algorithm_emulation(native, misalign, n):
 
 
 def test_emulation_multi_megabyte_tile_fold(native):
-    # > 256 tiles exercises the strided Horner (1 MiB shift) in K2
-    d = os.urandom(3 * (1 << 20) + 999)
+    # > 256 tiles exercises the strided Horner (256-tile shift) in K2
+    d = os.urandom(9 * (1 << 20) + 999)
     raw, crc, _ = native.emulate_gpu_crc32c(d, 5, 0, False)
     assert crc == native.crc32c(d)
 

@@ -6,7 +6,8 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("n", [0, 1, 15, 16, 17, 4095, 4096, 4097, 2 << 20, (2 << 20) + 13, 64 << 20])
+@pytest.mark.parametrize("n", [0, 1, 15, 16, 17, 4095, 4096, 4097, 16383, 16384, 16385, 2 << 20, (2 << 20) + 13,
+                               (4 << 20) + 16384 + 7, 64 << 20])
 @pytest.mark.parametrize("misalign", [0, 1, 7, 15])
 def test_gpu_crc_matches_host(native, gpu_available, n, misalign):
     import torch

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -104,6 +105,88 @@ __global__ __launch_bounds__(kK1Threads) void crc32c_tiles_kernel(const CrcBatch
 #pragma unroll
     for (int j = 0; j < kCrcLaneRun; ++j) state = update16(sl, state, v[j]);
     // wave tree: lane l's run ends kCrcRunBytes * (63 - l) before the tile end
+#pragma unroll
+    for (int lv = 0; lv < 6; ++lv) {
+      const uint32_t other = __shfl_down(state, 1 << lv, 64);
+      const uint32_t shifted = shift4(lane_shift + lv * 1024, state);
+      if ((lane & ((2 << lv) - 1)) == 0) state = shifted ^ other;
+    }
+    if (lane == 0) tile_out[gt] = state;
+  }
+}
+
+// K1, conflict-free variant ("nib"): the slice-by-16 lookups are split into
+// 32 nibble tables (16 entries each) and the whole 2 KiB nibble set is
+// replicated 32x in LDS so that lane l of each 32-lane LDS group reads only
+// bank l: every lookup is one LDS cycle per group (random byte tables cost
+// 2 + ~4 conflict cycles per wave instruction, profiles/r1_crc_pmc_*).  Twice
+// the lookups (32 per 16 B) at a third of the cycles each; 88 KiB of LDS, so
+// one 16-wave workgroup per CU.
+constexpr int kK1NibThreads = 1024;
+constexpr int kNibWords = 32 * 16 * 32;                  // 64 KiB replicated nibble tables
+constexpr int kLdsNibWords = kNibWords + 6 * 4 * 256;    // + wave-tree shift tables = 88 KiB
+
+__device__ __forceinline__ uint32_t nib_word(const uint32_t* __restrict__ lbase, uint32_t w, int t0) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) c ^= lbase[((t0 + j) * 16 + ((w >> (4 * j)) & 15)) * 32];
+  return c;
+}
+
+__device__ __forceinline__ uint32_t update16_nib(const uint32_t* __restrict__ lbase, uint32_t state, uint4 v) {
+  return nib_word(lbase, state ^ v.x, 0) ^ nib_word(lbase, v.y, 8) ^ nib_word(lbase, v.z, 16) ^
+         nib_word(lbase, v.w, 24);
+}
+
+__global__ __launch_bounds__(kK1NibThreads) void crc32c_tiles_nib_kernel(const CrcBatch b,
+                                                                         const CrcTables* __restrict__ tabs,
+                                                                         uint32_t* __restrict__ tile_out) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_tab[kLdsNibWords];
+  {
+    const uint32_t* nib = &tabs->nib[0][0];
+    for (int i = threadIdx.x; i < kNibWords; i += kK1NibThreads) s_tab[i] = nib[i >> 5];
+    const uint4* src = reinterpret_cast<const uint4*>(&tabs->lane_shift[0][0][0]);
+    uint4* dst = reinterpret_cast<uint4*>(s_tab + kNibWords);
+    for (int i = threadIdx.x; i < 6 * 256; i += kK1NibThreads) dst[i] = src[i];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const uint32_t* lbase = s_tab + (lane & 31);
+  const uint32_t* lane_shift = s_tab + kNibWords;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t nwaves = gridDim.x * (kK1NibThreads / 64);
+  for (uint32_t gt = blockIdx.x * (kK1NibThreads / 64) + wave; gt < b.total_tiles; gt += nwaves) {
+    uint32_t s = 0;
+    while (s + 1 < b.nseg && b.seg[s + 1].tile_base <= gt) ++s;
+    const uintptr_t addr = reinterpret_cast<uintptr_t>(b.seg[s].addr);
+    const uint32_t len = b.seg[s].len;
+    const uint32_t t = gt - b.seg[s].tile_base;
+    const uintptr_t a16 = addr & ~uintptr_t(15);
+    const uint64_t full = (addr + len - a16 + 15) / 16 - 1;
+    const intptr_t vend = static_cast<intptr_t>(a16 + 16 * full);
+    const intptr_t tstart = vend - static_cast<intptr_t>(kCrcTile) * static_cast<intptr_t>(b.seg[s].ntiles - t);
+    const intptr_t run = tstart + static_cast<intptr_t>(kCrcRunBytes) * lane;
+    uint4 v[kCrcLaneRun];
+#pragma unroll
+    for (int j = 0; j < kCrcLaneRun; ++j) {
+      const intptr_t p = run + 16 * j;
+      v[j] = make_uint4(0, 0, 0, 0);
+      if (p + 16 > static_cast<intptr_t>(addr)) v[j] = *reinterpret_cast<const uint4*>(p);
+    }
+#pragma unroll
+    for (int j = 0; j < kCrcLaneRun; ++j) {
+      const intptr_t p = run + 16 * j;
+      if (p < static_cast<intptr_t>(addr) && p + 16 > static_cast<intptr_t>(addr)) {
+        const int h = static_cast<int>(static_cast<intptr_t>(addr) - p);
+        v[j].x = mask_low_bytes(v[j].x, h);
+        v[j].y = mask_low_bytes(v[j].y, h - 4);
+        v[j].z = mask_low_bytes(v[j].z, h - 8);
+        v[j].w = mask_low_bytes(v[j].w, h - 12);
+      }
+    }
+    uint32_t state = 0;
+#pragma unroll
+    for (int j = 0; j < kCrcLaneRun; ++j) state = update16_nib(lbase, state, v[j]);
 #pragma unroll
     for (int lv = 0; lv < 6; ++lv) {
       const uint32_t other = __shfl_down(state, 1 << lv, 64);
@@ -231,6 +314,19 @@ __global__ __launch_bounds__(256) void verify_pattern_kernel(const uint8_t* __re
   }
 }
 
+enum class K1Variant { kSlice16, kNib };
+
+// GCSB_CRC_K1=slice16|nib selects the tile kernel (A/B switch; default below).
+K1Variant k1_variant() {
+  static K1Variant v = [] {
+    const char* e = std::getenv("GCSB_CRC_K1");
+    if (e && std::string(e) == "slice16") return K1Variant::kSlice16;
+    if (e && std::string(e) == "nib") return K1Variant::kNib;
+    return K1Variant::kSlice16;
+  }();
+  return v;
+}
+
 }  // namespace
 
 const CrcTables* device_crc_tables(int device) {
@@ -260,12 +356,21 @@ void launch_crc32c_batch(const CrcBatch& b, const CrcTables* d_tables, uint32_t*
                          CrcSegResult* d_results, hipStream_t stream) {
   if (b.nseg == 0) return;
   if (b.total_tiles > 0) {
-    constexpr uint32_t tiles_per_block = kK1Threads / 64;
-    uint32_t blocks = (b.total_tiles + tiles_per_block - 1) / tiles_per_block;
-    if (blocks > 1024) blocks = 1024;
-    hipLaunchKernelGGL(crc32c_tiles_kernel, dim3(blocks), dim3(kK1Threads), 0, stream, b,
-                       reinterpret_cast<const uint32_t*>(d_tables), d_tile_scratch);
-    hip_check(hipGetLastError(), "crc32c_tiles_kernel");
+    if (k1_variant() == K1Variant::kNib) {
+      constexpr uint32_t tiles_per_block = kK1NibThreads / 64;
+      uint32_t blocks = (b.total_tiles + tiles_per_block - 1) / tiles_per_block;
+      if (blocks > 256) blocks = 256;  // one 88 KiB workgroup per CU, grid-stride over tiles
+      hipLaunchKernelGGL(crc32c_tiles_nib_kernel, dim3(blocks), dim3(kK1NibThreads), 0, stream, b, d_tables,
+                         d_tile_scratch);
+      hip_check(hipGetLastError(), "crc32c_tiles_nib_kernel");
+    } else {
+      constexpr uint32_t tiles_per_block = kK1Threads / 64;
+      uint32_t blocks = (b.total_tiles + tiles_per_block - 1) / tiles_per_block;
+      if (blocks > 1024) blocks = 1024;
+      hipLaunchKernelGGL(crc32c_tiles_kernel, dim3(blocks), dim3(kK1Threads), 0, stream, b,
+                         reinterpret_cast<const uint32_t*>(d_tables), d_tile_scratch);
+      hip_check(hipGetLastError(), "crc32c_tiles_kernel");
+    }
   }
   hipLaunchKernelGGL(crc32c_segments_kernel, dim3(b.nseg), dim3(256), 0, stream, b, d_tables, d_tile_scratch,
                      d_results);

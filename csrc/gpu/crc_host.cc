@@ -12,6 +12,11 @@ void build_crc_tables(CrcTables* t) {
   crc32c_build_slice16(t->slice16);
   for (int lv = 0; lv < 6; ++lv) crc32c_build_shift_table(static_cast<uint64_t>(kCrcRunBytes) << lv, t->lane_shift[lv]);
   for (int lv = 0; lv < 9; ++lv) crc32c_build_shift_table(static_cast<uint64_t>(kCrcTile) << lv, t->tile_shift[lv]);
+  for (int p = 0; p < 16; ++p)
+    for (int n = 0; n < 16; ++n) {
+      t->nib[2 * p][n] = t->slice16[15 - p][n];
+      t->nib[2 * p + 1][n] = t->slice16[15 - p][n << 4];
+    }
 }
 
 void finalize_crc_batch(CrcBatch* b) {

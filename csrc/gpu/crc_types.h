@@ -41,6 +41,9 @@ struct CrcTables {
   uint32_t slice16[16][256];
   uint32_t lane_shift[6][4][256];  // shift by kCrcRunBytes * 2^lv (wave tree levels)
   uint32_t tile_shift[9][4][256];  // shift by kCrcTile * 2^s, s = 0..8 (last = 256 tiles)
+  // slice-by-16 split into nibble tables: byte p of a 16-byte block (table
+  // slice16[15-p]) = nib[2p][lo nibble] ^ nib[2p+1][hi nibble] (GF(2)-linear)
+  uint32_t nib[32][16];
 };
 
 // Number of kCrcTile tiles covering a segment's full 16-byte pieces (host helper).

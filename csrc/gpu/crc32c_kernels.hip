@@ -72,8 +72,10 @@ __global__ __launch_bounds__(kK1Threads) void crc32c_tiles_kernel(const CrcBatch
   const int lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t nwaves = gridDim.x * (kK1Threads / 64);
+  // gt only grows, so the segment search resumes where the last tile left it
+  // (restarting from 0 cost up to kMaxSeg dependent scalar loads per tile)
+  uint32_t s = 0;
   for (uint32_t gt = blockIdx.x * (kK1Threads / 64) + wave; gt < b.total_tiles; gt += nwaves) {
-    uint32_t s = 0;
     while (s + 1 < b.nseg && b.seg[s + 1].tile_base <= gt) ++s;
     const uintptr_t addr = reinterpret_cast<uintptr_t>(b.seg[s].addr);
     const uint32_t len = b.seg[s].len;
@@ -155,8 +157,8 @@ __global__ __launch_bounds__(kK1NibThreads) void crc32c_tiles_nib_kernel(const C
   const uint32_t* lane_shift = s_tab + kNibWords;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t nwaves = gridDim.x * (kK1NibThreads / 64);
+  uint32_t s = 0;
   for (uint32_t gt = blockIdx.x * (kK1NibThreads / 64) + wave; gt < b.total_tiles; gt += nwaves) {
-    uint32_t s = 0;
     while (s + 1 < b.nseg && b.seg[s + 1].tile_base <= gt) ++s;
     const uintptr_t addr = reinterpret_cast<uintptr_t>(b.seg[s].addr);
     const uint32_t len = b.seg[s].len;

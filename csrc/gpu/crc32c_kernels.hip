@@ -29,7 +29,7 @@ void hip_check(hipError_t e, const char* what) {
 namespace {
 
 constexpr int kK1Threads = 512;                       // 8 waves (tiles) per workgroup: amortise the table fill
-constexpr int kLdsWords = 16 * 256 + 6 * 4 * 256;     // slice16 + 6 wave-tree shift tables = 10240 words (40 KiB)
+constexpr int kLdsWords = 16 * 256 + 7 * 4 * 256;     // slice16 + 6 tree + 1 gap shift tables = 11264 words (44 KiB)
 
 __device__ __forceinline__ uint32_t shift4(const uint32_t* __restrict__ tab, uint32_t s) {
   return tab[s & 0xff] ^ tab[256 + ((s >> 8) & 0xff)] ^ tab[512 + ((s >> 16) & 0xff)] ^ tab[768 + (s >> 24)];
@@ -54,6 +54,31 @@ __device__ __forceinline__ uint32_t mask_low_bytes(uint32_t w, int keep_from) {
   if (keep_from <= 0) return w;
   if (keep_from >= 4) return 0;
   return w & (0xFFFFFFFFu << (8 * keep_from));
+}
+
+// Lane `lane`'s 16 pieces of the tile starting at tstart, in CRC order:
+// piece (k, j) = round k, chunk piece j at tstart + 4096 k + 64 lane + 16 j.
+// Pieces before the segment start read as zeros (free for a raw CRC); the
+// piece straddling it is masked.  Tiles are right-aligned to the segment end,
+// so only the first tile of a segment has such a head.
+__device__ __forceinline__ void load_lane_pieces(uint4 (&v)[kCrcRounds * kCrcChunkPieces], intptr_t tstart, int lane,
+                                                 uintptr_t addr) {
+#pragma unroll
+  for (int k = 0; k < kCrcRounds; ++k)
+#pragma unroll
+    for (int j = 0; j < kCrcChunkPieces; ++j) {
+      const intptr_t p = tstart + kCrcRoundBytes * k + kCrcChunkBytes * lane + 16 * j;
+      uint4 x = make_uint4(0, 0, 0, 0);
+      if (p + 16 > static_cast<intptr_t>(addr)) x = *reinterpret_cast<const uint4*>(p);
+      if (p < static_cast<intptr_t>(addr) && p + 16 > static_cast<intptr_t>(addr)) {
+        const int h = static_cast<int>(static_cast<intptr_t>(addr) - p);  // 1..15 leading bytes to zero
+        x.x = mask_low_bytes(x.x, h);
+        x.y = mask_low_bytes(x.y, h - 4);
+        x.z = mask_low_bytes(x.z, h - 8);
+        x.w = mask_low_bytes(x.w, h - 12);
+      }
+      v[k * kCrcChunkPieces + j] = x;
+    }
 }
 
 // K1: raw CRC of every 4 KiB tile of every segment in the batch.
@@ -84,29 +109,16 @@ __global__ __launch_bounds__(kK1Threads) void crc32c_tiles_kernel(const CrcBatch
     const uint64_t full = (addr + len - a16 + 15) / 16 - 1;
     const intptr_t vend = static_cast<intptr_t>(a16 + 16 * full);
     const intptr_t tstart = vend - static_cast<intptr_t>(kCrcTile) * static_cast<intptr_t>(b.seg[s].ntiles - t);
-    const intptr_t run = tstart + static_cast<intptr_t>(kCrcRunBytes) * lane;
-    uint4 v[kCrcLaneRun];
-#pragma unroll
-    for (int j = 0; j < kCrcLaneRun; ++j) {
-      const intptr_t p = run + 16 * j;
-      v[j] = make_uint4(0, 0, 0, 0);
-      if (p + 16 > static_cast<intptr_t>(addr)) v[j] = *reinterpret_cast<const uint4*>(p);
-    }
-#pragma unroll
-    for (int j = 0; j < kCrcLaneRun; ++j) {
-      const intptr_t p = run + 16 * j;
-      if (p < static_cast<intptr_t>(addr) && p + 16 > static_cast<intptr_t>(addr)) {
-        const int h = static_cast<int>(static_cast<intptr_t>(addr) - p);  // 1..15 leading bytes to zero
-        v[j].x = mask_low_bytes(v[j].x, h);
-        v[j].y = mask_low_bytes(v[j].y, h - 4);
-        v[j].z = mask_low_bytes(v[j].z, h - 8);
-        v[j].w = mask_low_bytes(v[j].w, h - 12);
-      }
-    }
+    uint4 v[kCrcRounds * kCrcChunkPieces];
+    load_lane_pieces(v, tstart, lane, addr);
     uint32_t state = 0;
 #pragma unroll
-    for (int j = 0; j < kCrcLaneRun; ++j) state = update16(sl, state, v[j]);
-    // wave tree: lane l's run ends kCrcRunBytes * (63 - l) before the tile end
+    for (int k = 0; k < kCrcRounds; ++k) {
+      if (k) state = shift4(lane_shift + 6 * 1024, state);  // over the 4032-byte gap to this lane's next chunk
+#pragma unroll
+      for (int j = 0; j < kCrcChunkPieces; ++j) state = update16(sl, state, v[k * kCrcChunkPieces + j]);
+    }
+    // wave tree: lane l's last chunk ends 64 (63 - l) bytes before the tile end
 #pragma unroll
     for (int lv = 0; lv < 6; ++lv) {
       const uint32_t other = __shfl_down(state, 1 << lv, 64);
@@ -126,7 +138,7 @@ __global__ __launch_bounds__(kK1Threads) void crc32c_tiles_kernel(const CrcBatch
 // one 16-wave workgroup per CU.
 constexpr int kK1NibThreads = 1024;
 constexpr int kNibWords = 32 * 16 * 32;                  // 64 KiB replicated nibble tables
-constexpr int kLdsNibWords = kNibWords + 6 * 4 * 256;    // + wave-tree shift tables = 88 KiB
+constexpr int kLdsNibWords = kNibWords + 7 * 4 * 256;    // + tree/gap shift tables = 92 KiB
 
 __device__ __forceinline__ uint32_t nib_word(const uint32_t* __restrict__ lbase, uint32_t w, int t0) {
   uint32_t c = 0;
@@ -149,7 +161,7 @@ __global__ __launch_bounds__(kK1NibThreads) void crc32c_tiles_nib_kernel(const C
     for (int i = threadIdx.x; i < kNibWords; i += kK1NibThreads) s_tab[i] = nib[i >> 5];
     const uint4* src = reinterpret_cast<const uint4*>(&tabs->lane_shift[0][0][0]);
     uint4* dst = reinterpret_cast<uint4*>(s_tab + kNibWords);
-    for (int i = threadIdx.x; i < 6 * 256; i += kK1NibThreads) dst[i] = src[i];
+    for (int i = threadIdx.x; i < 7 * 256; i += kK1NibThreads) dst[i] = src[i];
   }
   __syncthreads();
   const int lane = threadIdx.x & 63;
@@ -167,28 +179,15 @@ __global__ __launch_bounds__(kK1NibThreads) void crc32c_tiles_nib_kernel(const C
     const uint64_t full = (addr + len - a16 + 15) / 16 - 1;
     const intptr_t vend = static_cast<intptr_t>(a16 + 16 * full);
     const intptr_t tstart = vend - static_cast<intptr_t>(kCrcTile) * static_cast<intptr_t>(b.seg[s].ntiles - t);
-    const intptr_t run = tstart + static_cast<intptr_t>(kCrcRunBytes) * lane;
-    uint4 v[kCrcLaneRun];
-#pragma unroll
-    for (int j = 0; j < kCrcLaneRun; ++j) {
-      const intptr_t p = run + 16 * j;
-      v[j] = make_uint4(0, 0, 0, 0);
-      if (p + 16 > static_cast<intptr_t>(addr)) v[j] = *reinterpret_cast<const uint4*>(p);
-    }
-#pragma unroll
-    for (int j = 0; j < kCrcLaneRun; ++j) {
-      const intptr_t p = run + 16 * j;
-      if (p < static_cast<intptr_t>(addr) && p + 16 > static_cast<intptr_t>(addr)) {
-        const int h = static_cast<int>(static_cast<intptr_t>(addr) - p);
-        v[j].x = mask_low_bytes(v[j].x, h);
-        v[j].y = mask_low_bytes(v[j].y, h - 4);
-        v[j].z = mask_low_bytes(v[j].z, h - 8);
-        v[j].w = mask_low_bytes(v[j].w, h - 12);
-      }
-    }
+    uint4 v[kCrcRounds * kCrcChunkPieces];
+    load_lane_pieces(v, tstart, lane, addr);
     uint32_t state = 0;
 #pragma unroll
-    for (int j = 0; j < kCrcLaneRun; ++j) state = update16_nib(lbase, state, v[j]);
+    for (int k = 0; k < kCrcRounds; ++k) {
+      if (k) state = shift4(lane_shift + 6 * 1024, state);
+#pragma unroll
+      for (int j = 0; j < kCrcChunkPieces; ++j) state = update16_nib(lbase, state, v[k * kCrcChunkPieces + j]);
+    }
 #pragma unroll
     for (int lv = 0; lv < 6; ++lv) {
       const uint32_t other = __shfl_down(state, 1 << lv, 64);

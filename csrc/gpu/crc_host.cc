@@ -10,7 +10,8 @@ namespace gcsb {
 
 void build_crc_tables(CrcTables* t) {
   crc32c_build_slice16(t->slice16);
-  for (int lv = 0; lv < 6; ++lv) crc32c_build_shift_table(static_cast<uint64_t>(kCrcRunBytes) << lv, t->lane_shift[lv]);
+  for (int lv = 0; lv < 6; ++lv) crc32c_build_shift_table(static_cast<uint64_t>(kCrcChunkBytes) << lv, t->lane_shift[lv]);
+  crc32c_build_shift_table(kCrcLaneGap, t->lane_shift[6]);
   for (int lv = 0; lv < 9; ++lv) crc32c_build_shift_table(static_cast<uint64_t>(kCrcTile) << lv, t->tile_shift[lv]);
   for (int p = 0; p < 16; ++p)
     for (int n = 0; n < 16; ++n) {
@@ -63,18 +64,22 @@ CrcSegResult emulate_crc32c_segment(const uint8_t* addr_p, uint32_t len, const C
     uint32_t lanes[64];
     for (int lane = 0; lane < 64; ++lane) {
       uint32_t state = 0;
-      for (int j = 0; j < kCrcLaneRun; ++j) {
-        const intptr_t p = tstart + static_cast<intptr_t>(kCrcRunBytes) * lane + 16 * j;
-        uint32_t v[4] = {0, 0, 0, 0};
-        if (p + 16 > static_cast<intptr_t>(addr)) std::memcpy(v, reinterpret_cast<const void*>(p), 16);
-        if (p < static_cast<intptr_t>(addr) && p + 16 > static_cast<intptr_t>(addr)) {
-          const int h = static_cast<int>(static_cast<intptr_t>(addr) - p);
-          v[0] = mask_low_bytes(v[0], h);
-          v[1] = mask_low_bytes(v[1], h - 4);
-          v[2] = mask_low_bytes(v[2], h - 8);
-          v[3] = mask_low_bytes(v[3], h - 12);
+      for (int k = 0; k < kCrcRounds; ++k) {
+        if (k) state = shift4(t.lane_shift[6], state);
+        for (int j = 0; j < kCrcChunkPieces; ++j) {
+          const intptr_t p = tstart + static_cast<intptr_t>(kCrcRoundBytes) * k +
+                             static_cast<intptr_t>(kCrcChunkBytes) * lane + 16 * j;
+          uint32_t v[4] = {0, 0, 0, 0};
+          if (p + 16 > static_cast<intptr_t>(addr)) std::memcpy(v, reinterpret_cast<const void*>(p), 16);
+          if (p < static_cast<intptr_t>(addr) && p + 16 > static_cast<intptr_t>(addr)) {
+            const int h = static_cast<int>(static_cast<intptr_t>(addr) - p);
+            v[0] = mask_low_bytes(v[0], h);
+            v[1] = mask_low_bytes(v[1], h - 4);
+            v[2] = mask_low_bytes(v[2], h - 8);
+            v[3] = mask_low_bytes(v[3], h - 12);
+          }
+          state = update16(t.slice16, state, v);
         }
-        state = update16(t.slice16, state, v);
       }
       lanes[lane] = state;
     }

@@ -5,13 +5,20 @@
 
 namespace gcsb {
 
-// K1 geometry: a wave64 owns one tile; lane l CRCs kCrcLaneRun consecutive
-// 16-byte pieces (a contiguous run), then the 64 runs fold in a 6-level wave
-// tree.  Contiguous runs need no per-piece gap shifts, so LDS lookups per 16 B
-// are 16 (slice-by-16) + 24 / kCrcLaneRun (tree).
-constexpr int kCrcLaneRun = 16;
-constexpr int kCrcRunBytes = 16 * kCrcLaneRun;  // 256 B per lane
-constexpr int kCrcTile = 64 * kCrcRunBytes;     // 16 KiB per wave
+// K1 geometry: a wave64 owns one 16 KiB tile, read in kCrcRounds rounds of
+// 4 KiB; in each round lane l reads its own contiguous 64-byte chunk
+// (kCrcChunkPieces x 16 B) at round_base + 64 l, so every 128-byte line is
+// consumed by 2 lanes within 4 consecutive load instructions (L1-friendly),
+// and a lane's CRC chain is contiguous inside a chunk.  Between its chunks a
+// lane's state is shifted over the 4032-byte gap (one 4-lookup shift), and the
+// 64 lane states fold in a 6-level wave tree (shifts of 64 B * 2^lv).  LDS
+// lookups per 16 B: 16 (slice-by-16) + 0.75 (gaps) + 1.5 (tree).
+constexpr int kCrcChunkPieces = 4;
+constexpr int kCrcChunkBytes = 16 * kCrcChunkPieces;  // 64 B per lane per round
+constexpr int kCrcRoundBytes = 64 * kCrcChunkBytes;   // 4 KiB per round
+constexpr int kCrcRounds = 4;
+constexpr int kCrcTile = kCrcRounds * kCrcRoundBytes;  // 16 KiB per wave
+constexpr int kCrcLaneGap = kCrcRoundBytes - kCrcChunkBytes;  // 4032 B between a lane's chunks
 constexpr int kMaxSeg = 32;
 
 struct CrcSeg {
@@ -39,7 +46,7 @@ struct CrcSegResult {
 
 struct CrcTables {
   uint32_t slice16[16][256];
-  uint32_t lane_shift[6][4][256];  // shift by kCrcRunBytes * 2^lv (wave tree levels)
+  uint32_t lane_shift[7][4][256];  // [0..5]: shift by kCrcChunkBytes * 2^lv (wave tree); [6]: kCrcLaneGap
   uint32_t tile_shift[9][4][256];  // shift by kCrcTile * 2^s, s = 0..8 (last = 256 tiles)
   // slice-by-16 split into nibble tables: byte p of a 16-byte block (table
   // slice16[15-p]) = nib[2p][lo nibble] ^ nib[2p+1][hi nibble] (GF(2)-linear)

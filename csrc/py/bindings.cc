@@ -279,6 +279,7 @@ class PyClient {
     d["retries"] = s.retries.load();
     d["bytes_in"] = s.bytes_in.load();
     d["bytes_out"] = s.bytes_out.load();
+    d["path"] = client_->transport_path();
     return d;
   }
   StorageClient& client() { return *client_; }
@@ -375,6 +376,7 @@ class PyRunner {
   }
   std::string object_for(int w, int64_t seq) { return runner_->object_for(w, seq); }
   uintptr_t landing_ptr(int w) { return runner_->landing_ptr(w); }
+  std::string transport_path() { return runner_->client().transport_path(); }
   void set_reads_per_worker(int64_t n) { runner_->set_reads_per_worker(n); }
   void reset_stats() { runner_->reset_stats(); }
 
@@ -725,6 +727,7 @@ PYBIND11_MODULE(_native, m) {
       .def("summary", &PyRunner::summary)
       .def("object_for", &PyRunner::object_for)
       .def("landing_ptr", &PyRunner::landing_ptr)
+      .def("transport_path", &PyRunner::transport_path)
       .def("set_reads_per_worker", &PyRunner::set_reads_per_worker)
       .def("reset_stats", &PyRunner::reset_stats);
 

@@ -122,6 +122,8 @@ class StorageClient {
   const ClientConfig& config() const { return cfg_; }
   CallStats& stats() { return stats_; }
   virtual std::string transport_name() const = 0;
+  // Network path actually used (gRPC: DirectPath vs CloudPath, see grpc_client.cc).
+  virtual std::string transport_path() const { return "cloudpath"; }
 
  protected:
   explicit StorageClient(ClientConfig cfg) : cfg_(std::move(cfg)) {}

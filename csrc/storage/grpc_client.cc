@@ -10,6 +10,7 @@
 #include <sys/uio.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <atomic>
 #include <condition_variable>
 #include <cstring>
@@ -490,15 +491,30 @@ class ReadObjectHandler : public MessageHandler {
 };
 
 class GrpcStorageClient : public StorageClient {
+  std::string path_ = "cloudpath";
+
  public:
   explicit GrpcStorageClient(const ClientConfig& cfg) : StorageClient(cfg) {
     int n = std::max(1, cfg.grpc_conn_pool_size);
     conns_.resize(static_cast<size_t>(n));
     opt_.sock = cfg.sock;
     opt_.cpus = cfg.cpus;
+    // DirectPath (reference main.go:106-117: GOOGLE_CLOUD_ENABLE_DIRECT_PATH_XDS
+    // is set only around NewGRPCClient, with the google-c2p xDS resolver and
+    // the RLS balancer linked in).  DirectPath needs the GCE metadata server,
+    // an xDS bootstrap and ALTS; without them the library falls back to
+    // CloudPath, and so does this client: the request is recorded, the
+    // configured endpoint is used.
+    const char* dp = std::getenv("GOOGLE_CLOUD_ENABLE_DIRECT_PATH_XDS");
+    if (dp && std::string(dp) == "true") {
+      const bool prod = cfg.endpoint.host == "storage.googleapis.com";
+      path_ = prod ? "cloudpath (DirectPath requested: no xDS bootstrap / ALTS on this host)"
+                   : "cloudpath (DirectPath requested: custom endpoint " + cfg.endpoint.host + ")";
+    }
   }
 
   std::string transport_name() const override { return "grpc"; }
+  std::string transport_path() const override { return path_; }
 
  protected:
   std::shared_ptr<H2ClientConn> conn() {

@@ -56,6 +56,8 @@ def build_flags() -> FlagSet:
     fs.string("http-api", "xml", "HTTP media API: xml (library default) | json (alt=media)")
     fs.int("read-chunk", 2 << 20, "Bytes per receive into the sink (reference intent: 2 MiB buffer)")
     fs.int("grpc-conn-pool-size", 1, "gRPC connections (reference GrpcConnPoolSize = 1)")
+    fs.bool("grpc-directpath", True, "Request DirectPath while creating the gRPC client (reference sets "
+            "GOOGLE_CLOUD_ENABLE_DIRECT_PATH_XDS=true around NewGRPCClient; falls back to CloudPath)")
     fs.int("max-conns-per-host", 100, "HTTP connection cap (reference MaxConnsPerHost = 100)")
     fs.string("sink", "discard", "discard (reference io.Discard) | gpu (pinned ring -> HBM, CRC32C on GPU)")
     fs.int("gpu-device", -1, "HIP device (default: LOCAL_RANK)")
@@ -213,7 +215,7 @@ def main(argv: list[str] | None = None) -> int:
     try:
         wl = fs.get("workload")
         if wl == "read":
-            res = _run_with_live(opts, on_records, before_start, live)
+            res = _run_with_live(opts, on_records, before_start, live, fs.get("grpc-directpath"))
         elif wl == "list-read":
             res = workloads.run_list_read(opts, fs.get("list-prefix") or fs.get("object-prefix"), on_records,
                                           before_start)
@@ -275,8 +277,28 @@ def main(argv: list[str] | None = None) -> int:
     return rc
 
 
-def _run_with_live(opts, on_records, before_start, live):
-    runner = _native.Runner(opts.runner_dict())
+def _make_runner(opts, directpath: bool):
+    """Creates the native runner (and its storage client).  For gRPC the
+    reference sets GOOGLE_CLOUD_ENABLE_DIRECT_PATH_XDS=true only while the
+    client is constructed and unsets it afterwards (main.go:106-117)."""
+    if opts.protocol != "grpc" or not directpath:
+        return _native.Runner(opts.runner_dict())
+    key = "GOOGLE_CLOUD_ENABLE_DIRECT_PATH_XDS"
+    old = os.environ.get(key)
+    os.environ[key] = "true"
+    try:
+        runner = _native.Runner(opts.runner_dict())
+    finally:
+        if old is None:
+            os.environ.pop(key, None)
+        else:
+            os.environ[key] = old
+    _err(f"gRPC transport: {runner.transport_path()}")
+    return runner
+
+
+def _run_with_live(opts, on_records, before_start, live, directpath: bool = True):
+    runner = _make_runner(opts, directpath)
     live["runner"] = runner
 
     def recs(r):

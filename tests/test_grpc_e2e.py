@@ -94,3 +94,29 @@ def test_auth_required(native):
         assert c.read(B, P + "0")["verified"]
     finally:
         srv.stop()
+
+
+def test_directpath_request_falls_back_to_cloudpath(native, server, monkeypatch):
+    """Reference CreateGrpcClient (main.go:106-117) sets
+    GOOGLE_CLOUD_ENABLE_DIRECT_PATH_XDS=true around client creation; without
+    xDS/ALTS the library uses CloudPath.  The native client records the
+    request and uses the configured endpoint."""
+    monkeypatch.setenv("GOOGLE_CLOUD_ENABLE_DIRECT_PATH_XDS", "true")
+    c = native.Client({"protocol": "grpc", "endpoint": server.url})
+    assert c.stats()["path"].startswith("cloudpath (DirectPath requested")
+    monkeypatch.delenv("GOOGLE_CLOUD_ENABLE_DIRECT_PATH_XDS")
+    assert native.Client({"protocol": "grpc", "endpoint": server.url}).stats()["path"] == "cloudpath"
+
+
+def test_cli_sets_directpath_env_only_during_client_creation(native):
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-m", "custom_go_client_benchmark_amd", "-start-fake-server",
+                        "-client-protocol", "grpc", "-worker", "1", "-read-call-per-worker", "1",
+                        "-fake-object-size", "4096"], capture_output=True, text=True, timeout=120, cwd=root)
+    assert r.returncode == 0, r.stderr
+    assert "gRPC transport: cloudpath (DirectPath requested" in r.stderr
+    assert os.environ.get("GOOGLE_CLOUD_ENABLE_DIRECT_PATH_XDS") is None

@@ -82,6 +82,7 @@ __device__ __forceinline__ void load_lane_pieces(uint4 (&v)[kCrcRounds * kCrcChu
 }
 
 // K1: raw CRC of every 4 KiB tile of every segment in the batch.
+template <bool kK1LoadsFirst>
 __global__ __launch_bounds__(kK1Threads) void crc32c_tiles_kernel(const CrcBatch b, const uint32_t* __restrict__ tabs,
                                                                    uint32_t* __restrict__ tile_out) {
   __shared__ __attribute__((aligned(16))) uint32_t s_tab[kLdsWords];
@@ -111,6 +112,10 @@ __global__ __launch_bounds__(kK1Threads) void crc32c_tiles_kernel(const CrcBatch
     const intptr_t tstart = vend - static_cast<intptr_t>(kCrcTile) * static_cast<intptr_t>(b.seg[s].ntiles - t);
     uint4 v[kCrcRounds * kCrcChunkPieces];
     load_lane_pieces(v, tstart, lane, addr);
+    // keep all 16 loads of the tile in flight before the first lookup (the
+    // scheduler otherwise sinks them into the lookup chain: fewer bytes in
+    // flight per wave)
+    if (kK1LoadsFirst) __builtin_amdgcn_sched_barrier(0);
     uint32_t state = 0;
 #pragma unroll
     for (int k = 0; k < kCrcRounds; ++k) {
@@ -328,6 +333,16 @@ K1Variant k1_variant() {
   return v;
 }
 
+// GCSB_K1_LOADS_FIRST=0 lets the scheduler interleave the tile loads with the
+// lookups (A/B switch; default: all 16 loads issued first).
+bool k1_loads_first() {
+  static bool v = [] {
+    const char* e = std::getenv("GCSB_K1_LOADS_FIRST");
+    return !(e && *e == '0');
+  }();
+  return v;
+}
+
 }  // namespace
 
 const CrcTables* device_crc_tables(int device) {
@@ -368,8 +383,12 @@ void launch_crc32c_batch(const CrcBatch& b, const CrcTables* d_tables, uint32_t*
       constexpr uint32_t tiles_per_block = kK1Threads / 64;
       uint32_t blocks = (b.total_tiles + tiles_per_block - 1) / tiles_per_block;
       if (blocks > 1024) blocks = 1024;
-      hipLaunchKernelGGL(crc32c_tiles_kernel, dim3(blocks), dim3(kK1Threads), 0, stream, b,
-                         reinterpret_cast<const uint32_t*>(d_tables), d_tile_scratch);
+      if (k1_loads_first())
+        hipLaunchKernelGGL(crc32c_tiles_kernel<true>, dim3(blocks), dim3(kK1Threads), 0, stream, b,
+                           reinterpret_cast<const uint32_t*>(d_tables), d_tile_scratch);
+      else
+        hipLaunchKernelGGL(crc32c_tiles_kernel<false>, dim3(blocks), dim3(kK1Threads), 0, stream, b,
+                           reinterpret_cast<const uint32_t*>(d_tables), d_tile_scratch);
       hip_check(hipGetLastError(), "crc32c_tiles_kernel");
     }
   }

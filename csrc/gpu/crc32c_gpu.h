@@ -6,10 +6,11 @@
 // CRC32C is wanted (one gRPC ChecksummedData message, or the part of it that
 // landed in one ring slot, or one slot's share of an HTTP body).  A batch of up
 // to kMaxSeg segments is processed by two launches on the caller's stream:
-//   K1 crc32c_tiles    : every wave CRCs one 4 KiB tile (64 lanes x 4 x 16 B,
-//                        slice-by-16 + shift tables staged in LDS, 6-level
-//                        wave tree), tiles right-aligned to the segment end so
-//                        a ragged head is just leading zeros (free for raw CRC);
+//   K1 crc32c_tiles    : every wave CRCs one 16 KiB tile (4 rounds x 64 lanes x
+//                        64-byte chunks, slice-by-16 + gap/tree shift tables
+//                        staged in LDS, 6-level wave tree), tiles
+//                        right-aligned to the segment end so a ragged head is
+//                        just leading zeros (free for a raw CRC);
 //   K2 crc32c_segments : one workgroup per segment folds its tiles (strided
 //                        Horner + 8-level tree), adds the <16-byte tail, applies
 //                        the init/xorout fixup and compares with the expected

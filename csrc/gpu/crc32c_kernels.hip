@@ -1,13 +1,21 @@
 // CDNA4 (gfx950) CRC32C kernels + synthetic-pattern fill/verify kernels.
-// Design notes in crc32c_gpu.h.  Wave64 throughout: a wave owns a 16 KiB tile
-// and lane l CRCs its own contiguous 256-byte run (16 global_load_dwordx4 in
-// flight per lane; the data has no reuse so it never touches LDS).  The LDS
-// holds the 40 KiB of lookup tables: slice-by-16 (16 lookups per 16 B) plus
-// the 6 wave-tree shift tables (24 lookups per lane per tile, i.e. 1.5 per
-// 16 B).  Table lookups are random ds_read_b32 and set the kernel's pace
-// (profiles/r1_crc_pmc_summary.json), so the design minimises lookups per
-// byte: contiguous runs need no gap shifts (the round-0 kernel's 4 KiB tiles
-// with 16 B-strided lanes spent 36 % of its lookups on shifts).
+// Design notes in crc32c_gpu.h and crc_types.h (tile geometry).  Wave64
+// throughout: a wave owns a 16 KiB tile, read in 4 rounds of 4 KiB where lane
+// l takes its own contiguous 64-byte chunk (4 x global_load_dwordx4; each
+// 128-byte line is consumed by two lanes within 4 consecutive loads, so L1
+// absorbs the 16 B-per-lane pattern).  The data has no reuse and never touches
+// LDS; the LDS holds the 44 KiB of lookup tables: slice-by-16 (16 lookups per
+// 16 B), one gap-shift table (a lane's state jumps 4032 B to its next chunk:
+// 0.75 lookups per 16 B) and 6 wave-tree shift tables (1.5 per 16 B).
+//
+// Measured (profiles/r1_k1, scripts/crc_kernel_bench.py, 1 GiB in 32 MiB
+// segments): round-0 kernel (4 KiB tiles, 16 B-strided lanes, 36 % of lookups
+// spent on gap shifts) 2.4 TB/s -> lane-contiguous 256 B runs 3.0-3.1 TB/s
+// (fewer lookups but L1-hostile 256 B lane strides) -> 64 B chunks in 4 KiB
+// rounds 3.5-3.7 TB/s.  Random ds_read_b32 table lookups still cost ~4
+// bank-conflict cycles per instruction; the conflict-free "nib" variant
+// (nibble tables replicated per LDS bank, GCSB_CRC_K1=nib) removes them
+// (0.16/instr) but doubles lookups and VALU and runs at 3.2 TB/s.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>

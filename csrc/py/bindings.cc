@@ -18,6 +18,7 @@
 #include "server/fakegcs.h"
 #include "storage/auth.h"
 #include "storage/client.h"
+#include "storage/sliced.h"
 
 namespace py = pybind11;
 using namespace gcsb;
@@ -131,6 +132,48 @@ py::dict gpu_stats_dict(const GpuSinkStats& g) {
 // Owning wrapper so Python can keep a GPU sink (and its HBM) across reads.
 struct PyGpuSink {
   std::unique_ptr<GpuSink> sink;
+};
+
+// Sliced reads into caller-owned HBM (e.g. a torch tensor): stat, then N
+// concurrent ranged streams, each on its own connection and GpuSink, landing
+// at their offsets of [dptr, dptr + cap); object CRC32C combined and checked.
+struct PySlicedGpuReader {
+  std::unique_ptr<SlicedReader> reader;
+  uint8_t* dst = nullptr;
+  size_t cap = 0;
+  uint64_t need = 0;
+  PySlicedGpuReader(const py::dict& d) {
+    ClientConfig cc = client_from(d);
+    GpuSinkConfig g = gpu_from(d);
+    g.landing = Landing::kObject;
+    SlicedReadConfig sc;
+    sc.slices = get_or<int>(d, "slices", 8);
+    sc.min_slice_bytes = get_or<uint64_t>(d, "slice_min_bytes", 8u << 20);
+    sc.cpus = cc.cpus;
+    sc.verify = g.verify;
+    reader = std::make_unique<SlicedReader>(
+        cc, sc, [g](int) -> std::unique_ptr<Sink> { return std::make_unique<GpuSink>(g); },
+        [this](uint64_t total) {
+          need = total;
+          if (total > cap)
+            throw StorageError("object (" + std::to_string(total) + " B) larger than the destination (" +
+                                   std::to_string(cap) + " B)",
+                               false);
+        },
+        [this](int, Sink& sk, uint64_t off, uint64_t) {
+          static_cast<GpuSink&>(sk).set_external_destination(dst + off, cap - off);
+        });
+  }
+  py::dict read_into(const std::string& bucket, const std::string& name, uintptr_t dptr, size_t n) {
+    ReadResult rr;
+    {
+      py::gil_scoped_release nogil;
+      dst = reinterpret_cast<uint8_t*>(dptr);
+      cap = n;
+      rr = reader->read(bucket, name);
+    }
+    return sink_result_dict(rr);
+  }
 };
 
 class PyClient {
@@ -686,6 +729,11 @@ PYBIND11_MODULE(_native, m) {
     }
     return py::make_tuple(bad, first);
   });
+
+  py::class_<PySlicedGpuReader>(m, "SlicedGpuReader")
+      .def(py::init<const py::dict&>())
+      .def("read_into", &PySlicedGpuReader::read_into, py::arg("bucket"), py::arg("name"), py::arg("dptr"),
+           py::arg("n"));
 
   py::class_<PyGpuSink>(m, "GpuSink")
       .def(py::init([](const py::dict& d) {

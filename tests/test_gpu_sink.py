@@ -202,3 +202,33 @@ def test_async_submit_detects_corruption(native, server, gpu_available):
     sink = native.GpuSink({"device": 0, "ring_slot_bytes": 1 << 20, "ring_slots": 2, "async_submit": True})
     r = c.read_gpu(B, P + "0", sink)
     assert r["crc_mismatch"] and not r["verified"]
+
+
+@pytest.mark.parametrize("slices", [1, 4])
+@pytest.mark.parametrize("proto", ["http", "grpc"])
+def test_hbm_reader_api(native, server, gpu_available, slices, proto):
+    from custom_go_client_benchmark_amd.ops import hbm
+
+    size = (19 << 20) + 321
+    server.add_synthetic(B, P, "", 0, 2, size)
+    r = hbm.HbmReader(proto, server.url, device=0, slices=slices, slot_bytes=2 << 20, slots=3,
+                      slice_min_bytes=2 << 20)
+    t, res = r.read(B, P + "0")
+    assert res["verified"] and res["bytes"] == size and t.numel() == size
+    bad, first = native.gpu_verify_pattern(0, t.data_ptr(), size, P + "0", 0)
+    assert bad == 0, first
+    t2, res2 = r.read(B, P + "1", out=t)  # reuse the destination
+    assert t2.data_ptr() == t.data_ptr() and res2["verified"]
+    bad, first = native.gpu_verify_pattern(0, t.data_ptr(), size, P + "1", 0)
+    assert bad == 0, first
+    assert hbm.crc32c(t) == server.object_info(B, P + "1")["crc32c"]
+
+
+def test_hbm_reader_destination_too_small(native, server, gpu_available):
+    import torch
+    from custom_go_client_benchmark_amd.ops import hbm
+
+    server.add_synthetic(B, P, "", 0, 1, 8 << 20)
+    r = hbm.HbmReader("http", server.url, slices=4, slice_min_bytes=1 << 20)
+    with pytest.raises(native.StorageError, match="larger than the destination"):
+        r.read(B, P + "0", out=torch.empty(1 << 20, dtype=torch.uint8, device="cuda:0"))

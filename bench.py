@@ -124,7 +124,7 @@ def main() -> int:
     run.reset_stats()
     run.set_reads_per_worker(args.steps)
 
-    gdist.barrier(ctx)
+    gdist.barrier(ctx, "R1/R2 bench barrier")
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -132,7 +132,7 @@ def main() -> int:
     run.wait()
     if torch.cuda.is_available():
         torch.cuda.synchronize()
-    gdist.barrier(ctx)
+    gdist.barrier(ctx, "R1/R2 bench barrier")
     elapsed = time.perf_counter() - t0
     s = run.summary()
 
@@ -145,11 +145,11 @@ def main() -> int:
         run1.wait()
         run1.reset_stats()
         run1.set_reads_per_worker(ss_steps)
-        gdist.barrier(ctx)
+        gdist.barrier(ctx, "R1/R2 single-stream barrier")
         t1 = time.perf_counter()
         run1.start()
         run1.wait()
-        gdist.barrier(ctx)
+        gdist.barrier(ctx, "R1/R2 single-stream barrier")
         ss_elapsed = time.perf_counter() - t1
         s1 = run1.summary()
         ss = {"elapsed": ss_elapsed, "bytes": float(s1["bytes"]), "p50": s1["p50_ms"], "p99": s1["p99_ms"],

@@ -204,7 +204,7 @@ def main(argv: list[str] | None = None) -> int:
 
     def before_start():
         if ctx is not None:
-            dist.barrier(ctx)  # R1: synchronized start
+            dist.barrier(ctx, "R1 start barrier")  # synchronized start
 
     def on_records(recs):
         if tracer:
@@ -233,7 +233,7 @@ def main(argv: list[str] | None = None) -> int:
     finally:
         if ctx is not None:
             try:
-                dist.barrier(ctx)  # R2: synchronized stop
+                dist.barrier(ctx, "R2 stop barrier")  # synchronized stop
             except Exception:
                 pass
     wall = time.perf_counter() - t0

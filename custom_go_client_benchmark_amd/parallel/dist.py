@@ -17,6 +17,8 @@ from __future__ import annotations
 
 import datetime
 import os
+import sys
+import threading
 from dataclasses import dataclass
 
 
@@ -85,17 +87,56 @@ def init(local_rank: int | None = None, world: int | None = None, rank: int | No
     return ctx
 
 
-def barrier(ctx: DistContext) -> None:
-    """R1/R2: RCCL all_reduce of one int32 + device sync (gloo on CPU)."""
+class BarrierTimeout(RuntimeError):
+    """A peer rank did not reach a barrier in time (dead or stuck)."""
+
+
+def _watchdog(ctx: DistContext, what: str, timeout_s: float, done: threading.Event) -> None:
+    """SURVEY.md §5 failure detection: a rank whose peer died would otherwise
+    sit in the collective until the process-group timeout (10 min).  After
+    `timeout_s` the watchdog names the barrier, aborts the communicator
+    (ncclCommAbort through torch's _abort_process_group) so the blocked
+    collective raises, and if it still has not returned shortly after,
+    ends the process with exit status 3."""
+    if done.wait(timeout_s):
+        return
+    sys.stderr.write(f"[rank {ctx.rank}] {what}: peer ranks did not arrive within {timeout_s:.0f} s "
+                     f"(dead or stuck rank); aborting the {ctx.backend} communicator\n")
+    sys.stderr.flush()
+    try:
+        from torch.distributed import distributed_c10d as c10d
+
+        c10d._abort_process_group()
+    except Exception as e:  # gloo has no abort; fall through to the hard exit
+        sys.stderr.write(f"[rank {ctx.rank}] communicator abort unavailable: {e}\n")
+    if not done.wait(5.0):
+        sys.stderr.flush()
+        os._exit(3)
+
+
+def barrier(ctx: DistContext, what: str = "barrier", timeout_s: float | None = None) -> None:
+    """R1/R2: RCCL all_reduce of one int32 + device sync (gloo on CPU), under a
+    watchdog (GCSB_BARRIER_TIMEOUT_S, default 300 s)."""
     if ctx.world <= 1:
         return
     import torch
     import torch.distributed as dist
 
-    t = torch.ones(1, dtype=torch.int32, device=ctx.device)
-    dist.all_reduce(t)
-    if ctx.gpu >= 0:
-        torch.cuda.synchronize(ctx.gpu)
+    if timeout_s is None:
+        timeout_s = float(os.environ.get("GCSB_BARRIER_TIMEOUT_S", "300"))
+    done = threading.Event()
+    wd = threading.Thread(target=_watchdog, args=(ctx, what, timeout_s, done), name="gcsb-barrier-watchdog",
+                          daemon=True)
+    wd.start()
+    try:
+        t = torch.ones(1, dtype=torch.int32, device=ctx.device)
+        dist.all_reduce(t)
+        if ctx.gpu >= 0:
+            torch.cuda.synchronize(ctx.gpu)
+    except Exception as e:
+        raise BarrierTimeout(f"{what} failed on rank {ctx.rank}: {e}") from e
+    finally:
+        done.set()
     if int(t.item()) != ctx.world:
         raise RuntimeError(f"barrier mismatch: {int(t.item())} != {ctx.world}")
 

@@ -84,3 +84,54 @@ def test_reduce_stats_gloo():
         assert st["x_sum"] == 3.0 and st["x_max"] == 2.0 and st["x_min"] == 1.0
         assert st["y_per_rank"] == [0.0, 10.0]
         assert h == [1, 2, 4]
+
+
+def _stuck_worker(rank, world, port, q):
+    import time
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path.insert(0, ROOT)
+    from custom_go_client_benchmark_amd.parallel import dist
+
+    ctx = dist.init()
+    dist.barrier(ctx, "warm barrier")
+    if rank == 1:
+        time.sleep(30)  # a stuck rank: never reaches the next barrier
+        os._exit(0)
+    t0 = time.time()
+    try:
+        dist.barrier(ctx, "R2 stop barrier", timeout_s=2.0)
+        q.put(("returned", time.time() - t0))
+    except dist.BarrierTimeout as e:
+        q.put(("raised", time.time() - t0, str(e)))
+    os._exit(0)
+
+
+def test_barrier_watchdog_surfaces_a_stuck_rank():
+    """a dead/stuck peer is reported by the barrier watchdog
+    within its timeout (communicator aborted, or exit status 3 when the
+    backend cannot abort), instead of hanging until the process-group
+    timeout."""
+    import time
+
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    ps = [ctx.Process(target=_stuck_worker, args=(r, 2, port, q)) for r in range(2)]
+    t0 = time.time()
+    [p.start() for p in ps]
+    ps[0].join(60)
+    elapsed = time.time() - t0
+    assert not ps[0].is_alive()
+    if ps[0].exitcode == 3:
+        outcome = None  # watchdog hard exit (gloo has no abort)
+    else:
+        outcome = q.get(timeout=5)
+        assert outcome[0] == "raised", outcome
+        assert outcome[1] < 20
+    assert elapsed < 45
+    ps[1].kill()
+    ps[1].join(10)

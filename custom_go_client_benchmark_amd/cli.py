@@ -153,8 +153,12 @@ def main(argv: list[str] | None = None) -> int:
 
     latency_fd = 1
     lat_file = None
-    if fs.get("latency-file"):
-        lat_file = open(fs.get("latency-file"), "w")
+    lat_path = fs.get("latency-file")
+    if lat_path:
+        if world > 1:  # one file per rank; scripts/merge_latency.py gives exact node percentiles
+            root, ext = os.path.splitext(lat_path)
+            lat_path = f"{root}.rank{rank}{ext}"
+        lat_file = open(lat_path, "w")
         latency_fd = lat_file.fileno()
     sys.stdout.flush()
 

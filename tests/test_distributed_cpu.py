@@ -135,3 +135,19 @@ def test_barrier_watchdog_surfaces_a_stuck_rank():
     assert elapsed < 45
     ps[1].kill()
     ps[1].join(10)
+
+
+def test_cli_two_ranks_latency_files_merge(tmp_path):
+    lat = tmp_path / "lat.txt"
+    r = torchrun(["-m", "custom_go_client_benchmark_amd", "-worker", "2", "-read-call-per-worker", "4",
+                  "-start-fake-server", "-fake-object-size", "65536", "-latency-file", str(lat)])
+    assert r.returncode == 0, r.stderr[-3000:]
+    files = sorted(str(p) for p in tmp_path.glob("lat.rank*.txt"))
+    assert len(files) == 2  # one file per rank, no clobbering
+    for f in files:
+        assert len(open(f).read().splitlines()) == 8
+    m = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "merge_latency.py"), "--json"] + files,
+                       capture_output=True, text=True, timeout=60)
+    out = json.loads(m.stdout)
+    assert out["node"]["count"] == 16
+    assert out["node"]["min_ms"] <= out["node"]["p50_ms"] <= out["node"]["p99_ms"] <= out["node"]["max_ms"]

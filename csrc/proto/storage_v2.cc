@@ -190,6 +190,63 @@ bool decode_get_request(std::string_view b, GetObjectRequest* q) {
   return r.ok();
 }
 
+std::string encode_delete_request(const GetObjectRequest& q) {
+  std::string s;
+  pb::put_string(&s, 1, q.bucket);
+  pb::put_string(&s, 2, q.object);
+  pb::put_int64(&s, 4, q.generation);
+  return s;
+}
+
+bool decode_delete_request(std::string_view b, GetObjectRequest* q) {
+  Reader r(b);
+  uint32_t f;
+  WireType wt;
+  while (r.next(&f, &wt)) {
+    if (f == 1) q->bucket = std::string(r.bytes());
+    else if (f == 2) q->object = std::string(r.bytes());
+    else if (f == 4) q->generation = static_cast<int64_t>(r.varint());
+    else r.skip(wt);
+  }
+  return r.ok();
+}
+
+std::string encode_compose_request(const ComposeObjectRequest& q) {
+  std::string s;
+  pb::put_message(&s, 1, encode_object(q.destination));
+  for (const auto& n : q.sources) {
+    std::string so;
+    pb::put_string(&so, 1, n);
+    pb::put_message(&s, 2, so);
+  }
+  return s;
+}
+
+bool decode_compose_request(std::string_view b, ComposeObjectRequest* q) {
+  Reader r(b);
+  uint32_t f;
+  WireType wt;
+  while (r.next(&f, &wt)) {
+    if (f == 1) {
+      if (!decode_object(r.bytes(), &q->destination)) return false;
+    } else if (f == 2) {
+      Reader so(r.bytes());
+      uint32_t g;
+      WireType w2;
+      std::string name;
+      while (so.next(&g, &w2)) {
+        if (g == 1) name = std::string(so.bytes());
+        else so.skip(w2);
+      }
+      if (!so.ok()) return false;
+      q->sources.push_back(name);
+    } else {
+      r.skip(wt);
+    }
+  }
+  return r.ok();
+}
+
 std::string encode_list_request(const ListObjectsRequest& q) {
   std::string s;
   pb::put_string(&s, 1, q.parent);

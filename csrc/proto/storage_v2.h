@@ -78,6 +78,19 @@ struct GetObjectRequest {
 std::string encode_get_request(const GetObjectRequest& r);
 bool decode_get_request(std::string_view b, GetObjectRequest* r);
 
+// DeleteObjectRequest {bucket=1, object=2, generation=4} (same fields as Get)
+std::string encode_delete_request(const GetObjectRequest& r);
+bool decode_delete_request(std::string_view b, GetObjectRequest* r);
+
+// ComposeObjectRequest {destination=1 (Object), source_objects=2 (repeated
+// SourceObject {name=1, generation=2})} -> Object
+struct ComposeObjectRequest {
+  Object destination;  // bucket (resource form) + name + content_type
+  std::vector<std::string> sources;
+};
+std::string encode_compose_request(const ComposeObjectRequest& r);
+bool decode_compose_request(std::string_view b, ComposeObjectRequest* r);
+
 struct ListObjectsRequest {
   std::string parent, page_token, delimiter, prefix;
   int32_t page_size = 0;

@@ -130,6 +130,63 @@ py::dict gpu_stats_dict(const GpuSinkStats& g) {
 }
 
 // Owning wrapper so Python can keep a GPU sink (and its HBM) across reads.
+// Parallel composite uploads (storage/sliced.h SlicedWriter) from host bytes
+// or from HBM (per-part GpuByteSource: D2H staging ring + GPU CRC32C).
+struct PySlicedWriter {
+  std::unique_ptr<SlicedWriter> writer;
+  explicit PySlicedWriter(const py::dict& d) {
+    ClientConfig cc = client_from(d);
+    SlicedWriteConfig sc;
+    sc.slices = get_or<int>(d, "slices", 8);
+    sc.min_slice_bytes = get_or<uint64_t>(d, "slice_min_bytes", 8u << 20);
+    sc.cpus = cc.cpus;
+    writer = std::make_unique<SlicedWriter>(cc, sc);
+  }
+  py::dict write_bytes(const std::string& bucket, const std::string& name, const py::bytes& data, bool resumable,
+                       size_t chunk_bytes) {
+    char* ptr = nullptr;
+    Py_ssize_t len = 0;
+    if (PyBytes_AsStringAndSize(data.ptr(), &ptr, &len) != 0) throw py::error_already_set();
+    ObjectMeta m;
+    {
+      py::gil_scoped_release nogil;
+      WriteOptions o;
+      o.resumable = resumable;
+      o.chunk_bytes = chunk_bytes;
+      const auto* base = reinterpret_cast<const uint8_t*>(ptr);
+      m = writer->write(bucket, name, static_cast<uint64_t>(len),
+                        [base](int, uint64_t off, uint64_t n) -> std::unique_ptr<ByteSource> {
+                          return std::make_unique<HostByteSource>(base + off, n);
+                        },
+                        o);
+    }
+    return meta_dict(m);
+  }
+  py::dict write_from_device(const std::string& bucket, const std::string& name, uintptr_t dptr, uint64_t n,
+                             int device, bool resumable, size_t chunk_bytes, size_t slot_bytes, int slots) {
+    ObjectMeta m;
+    double ms = 0;
+    {
+      py::gil_scoped_release nogil;
+      WriteOptions o;
+      o.resumable = resumable;
+      o.chunk_bytes = chunk_bytes;
+      const auto* base = reinterpret_cast<const uint8_t*>(dptr);
+      const int64_t t0 = now_ns();
+      m = writer->write(bucket, name, n,
+                        [=](int, uint64_t off, uint64_t len) -> std::unique_ptr<ByteSource> {
+                          return std::make_unique<GpuByteSource>(device, base + off, len, slot_bytes, slots, true);
+                        },
+                        o);
+      ms = (now_ns() - t0) / 1e6;
+    }
+    py::dict d = meta_dict(m);
+    d["upload_ms"] = ms;
+    d["parts"] = writer->slices();
+    return d;
+  }
+};
+
 struct PyGpuSink {
   std::unique_ptr<GpuSink> sink;
 };
@@ -313,6 +370,20 @@ class PyClient {
     d["upload_ms"] = upload_ms;
     d["d2h_copies"] = copies;
     return d;
+  }
+
+  py::dict compose(const std::string& bucket, const std::string& dest, const std::vector<std::string>& sources,
+                   const std::string& content_type) {
+    ObjectMeta m;
+    {
+      py::gil_scoped_release nogil;
+      m = client_->compose_object(bucket, dest, sources, content_type);
+    }
+    return meta_dict(m);
+  }
+  void remove(const std::string& bucket, const std::string& name) {
+    py::gil_scoped_release nogil;
+    client_->delete_object(bucket, name);
   }
 
   py::dict stats() {
@@ -730,6 +801,14 @@ PYBIND11_MODULE(_native, m) {
     return py::make_tuple(bad, first);
   });
 
+  py::class_<PySlicedWriter>(m, "SlicedWriter")
+      .def(py::init<const py::dict&>())
+      .def("write_bytes", &PySlicedWriter::write_bytes, py::arg("bucket"), py::arg("name"), py::arg("data"),
+           py::arg("resumable") = true, py::arg("chunk_bytes") = 16u << 20)
+      .def("write_from_device", &PySlicedWriter::write_from_device, py::arg("bucket"), py::arg("name"),
+           py::arg("dptr"), py::arg("n"), py::arg("device") = 0, py::arg("resumable") = true,
+           py::arg("chunk_bytes") = 16u << 20, py::arg("slot_bytes") = 8u << 20, py::arg("slots") = 4);
+
   py::class_<PySlicedGpuReader>(m, "SlicedGpuReader")
       .def(py::init<const py::dict&>())
       .def("read_into", &PySlicedGpuReader::read_into, py::arg("bucket"), py::arg("name"), py::arg("dptr"),
@@ -764,6 +843,9 @@ PYBIND11_MODULE(_native, m) {
       .def("write_from_device", &PyClient::write_from_device, py::arg("bucket"), py::arg("name"), py::arg("dptr"),
            py::arg("n"), py::arg("device") = 0, py::arg("resumable") = true, py::arg("chunk_bytes") = 16u << 20,
            py::arg("slot_bytes") = 8u << 20, py::arg("slots") = 4)
+      .def("compose", &PyClient::compose, py::arg("bucket"), py::arg("dest"), py::arg("sources"),
+           py::arg("content_type") = "")
+      .def("delete", &PyClient::remove)
       .def("stats", &PyClient::stats);
 
   py::class_<PyRunner>(m, "Runner")

@@ -402,6 +402,8 @@ class H2ServerConn {
       if (!auth_ok(s)) return;
       if (s.path == "ReadObject") return read_object(s);
       if (s.path == "GetObject") return get_object(s);
+      if (s.path == "DeleteObject") return delete_object(s);
+      if (s.path == "ComposeObject") return compose_object(s);
       if (s.path == "ListObjects") return list_objects(s);
       if (s.path == "WriteObject") return write_object_done(s);
       if (s.path == "StartResumableWrite") return start_resumable(s);
@@ -510,6 +512,32 @@ class H2ServerConn {
     if (!o) return send_trailers(s.id, kNotFound, "No such object: " + q.object, false);
     send_headers(s.id);
     send_message(s, v2::encode_object(to_v2(*o)));
+    send_trailers(s.id, kOk, "", true);
+  }
+
+  void delete_object(ServerStream& s) {
+    v2::GetObjectRequest q;
+    if (s.messages.empty() || !v2::decode_delete_request(s.messages[0], &q))
+      return send_trailers(s.id, kInvalidArgument, "bad DeleteObjectRequest", false);
+    if (!srv_.store().remove(v2::bucket_from_resource(q.bucket), q.object))
+      return send_trailers(s.id, kNotFound, "No such object: " + q.object, false);
+    send_headers(s.id);
+    send_message(s, std::string());  // google.protobuf.Empty
+    send_trailers(s.id, kOk, "", true);
+  }
+
+  void compose_object(ServerStream& s) {
+    v2::ComposeObjectRequest q;
+    if (s.messages.empty() || !v2::decode_compose_request(s.messages[0], &q))
+      return send_trailers(s.id, kInvalidArgument, "bad ComposeObjectRequest", false);
+    std::string err;
+    auto o = srv_.store().compose(v2::bucket_from_resource(q.destination.bucket), q.destination.name, q.sources,
+                                  q.destination.content_type, &err);
+    if (!o)
+      return send_trailers(s.id, err.find("not found") != std::string::npos ? kNotFound : kInvalidArgument, err,
+                           false);
+    send_headers(s.id);
+    send_message(s, v2::encode_object(to_v2(*o, false)));
     send_trailers(s.id, kOk, "", true);
   }
 

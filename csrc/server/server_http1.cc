@@ -493,6 +493,11 @@ class Http1Handler {
       return list(r, bucket);
     }
     if (!starts_with(tail, "/o/")) return respond(c_, 404, {}, json_error(404, "Not Found", "notFound"));
+    static const std::string kCompose = "/compose";
+    if (r.method == "POST" && tail.size() > 3 + kCompose.size() &&
+        tail.compare(tail.size() - kCompose.size(), kCompose.size(), kCompose) == 0) {
+      return compose(r, bucket, url_decode(tail.substr(3, tail.size() - 3 - kCompose.size())));
+    }
     std::string name = url_decode(tail.substr(3));
     if (r.method == "DELETE") {
       if (!srv_.store().remove(bucket, name))
@@ -503,6 +508,28 @@ class Http1Handler {
     if (!o) return respond(c_, 404, {}, json_error(404, "No such object: " + bucket + "/" + name, "notFound"));
     if (r.q("alt") == "media") return send_media(r, *o, false);
     respond(c_, 200, {}, object_json(*o).dump());
+  }
+
+  // POST /storage/v1/b/<b>/o/<dest>/compose
+  //   {"sourceObjects": [{"name": ...}, ...], "destination": {"contentType": ...}}
+  void compose(const Request& r, const std::string& bucket, const std::string& dest) {
+    Json j;
+    try {
+      j = Json::parse(r.body);
+    } catch (const std::exception&) {
+      return respond(c_, 400, {}, json_error(400, "Parse Error", "parseError"));
+    }
+    std::vector<std::string> names;
+    if (const Json* so = j.get("sourceObjects"); so && so->is_array())
+      for (const auto& e : so->items())
+        if (const Json* n = e.get("name"); n && n->is_string()) names.push_back(n->as_string());
+    std::string ct;
+    if (const Json* d = j.get("destination"))
+      if (const Json* c = d->get("contentType"); c && c->is_string()) ct = c->as_string();
+    std::string err;
+    auto o = srv_.store().compose(bucket, dest, names, ct, &err);
+    if (!o) return respond(c_, err.find("not found") != std::string::npos ? 404 : 400, {}, json_error(400, err, "invalid"));
+    respond(c_, 200, {}, object_json(*o, false).dump());
   }
 
   void list(const Request& r, const std::string& bucket) {

@@ -153,6 +153,55 @@ std::shared_ptr<const StoredObject> ObjectStore::put(const std::string& bucket, 
   return o;
 }
 
+std::shared_ptr<const StoredObject> ObjectStore::compose(const std::string& bucket, const std::string& dest,
+                                                         const std::vector<std::string>& sources,
+                                                         const std::string& content_type, std::string* err) {
+  if (sources.empty() || sources.size() > 32) {
+    *err = "The number of source components provided (" + std::to_string(sources.size()) +
+           ") must be between 1 and 32";
+    return nullptr;
+  }
+  std::vector<std::shared_ptr<const StoredObject>> src;
+  uint64_t total = 0;
+  uint32_t crc = 0;
+  bool hollow = !retain_uploads_;
+  for (const auto& n : sources) {
+    auto o = get(bucket, n);
+    if (!o) {
+      *err = "Object " + n + " (in compose source list) not found";
+      return nullptr;
+    }
+    crc = crc32c_combine(crc, o->crc32c, o->size);
+    total += o->size;
+    hollow = hollow || o->hollow;
+    src.push_back(std::move(o));
+  }
+  auto out = std::make_shared<StoredObject>();
+  out->bucket = bucket;
+  out->name = dest;
+  out->size = total;
+  out->content_type = content_type.empty() ? src[0]->content_type : content_type;
+  out->generation = next_generation();
+  out->created_us = wall_ns() / 1000;
+  out->crc32c = crc;
+  out->hollow = hollow;
+  if (!hollow) {
+    Blob data;
+    data.reserve(total);
+    for (const auto& o : src)
+      for (uint64_t off = 0; off < o->size;) {
+        uint64_t n = std::min<uint64_t>(o->size - off, 8u << 20);
+        data.append(o->bytes(off, n), n);
+        off += n;
+      }
+    out->data = std::make_shared<const Blob>(std::move(data));
+    if (compute_md5_) out->set_md5_lazy();
+  }
+  std::unique_lock<std::shared_mutex> lk(mu_);
+  objects_[{bucket, dest}] = out;
+  return out;
+}
+
 bool ObjectStore::remove(const std::string& bucket, const std::string& name) {
   std::unique_lock<std::shared_mutex> lk(mu_);
   return objects_.erase({bucket, name}) > 0;

@@ -130,6 +130,13 @@ class ObjectStore {
                                           Blob data, const std::string& content_type,
                                           const uint32_t* known_crc = nullptr);
   bool remove(const std::string& bucket, const std::string& name);
+  // objects.compose / ComposeObject: dest = concatenation of 1..32 sources.
+  // CRC32C is the GF(2) combine of the sources' CRCs, so metadata-only
+  // (non-retained) sources compose without bytes; the result keeps bytes
+  // only if every source has them and uploads are retained.
+  std::shared_ptr<const StoredObject> compose(const std::string& bucket, const std::string& dest,
+                                              const std::vector<std::string>& sources,
+                                              const std::string& content_type, std::string* err);
   // Objects with the prefix, sorted by name, names > start_after, at most max.
   std::vector<std::shared_ptr<const StoredObject>> list(const std::string& bucket, const std::string& prefix,
                                                         const std::string& start_after, size_t max) const;

@@ -66,6 +66,20 @@ ObjectMeta StorageClient::stat_object(const std::string& bucket, const std::stri
   return with_retry([&] { return stat_attempt(bucket, object); });
 }
 
+ObjectMeta StorageClient::compose_object(const std::string& bucket, const std::string& dest,
+                                        const std::vector<std::string>& sources, const std::string& content_type) {
+  ++stats_.requests;
+  return with_retry([&] { return compose_attempt(bucket, dest, sources, content_type); });
+}
+
+void StorageClient::delete_object(const std::string& bucket, const std::string& object) {
+  ++stats_.requests;
+  with_retry([&] {
+    delete_attempt(bucket, object);
+    return 0;
+  });
+}
+
 ListResult StorageClient::list_objects(const std::string& bucket, const std::string& prefix, int page_size,
                                        const std::string& page_token, const std::string& delimiter) {
   return with_retry([&] { return list_attempt(bucket, prefix, page_size, page_token, delimiter); });

@@ -113,6 +113,10 @@ class StorageClient {
   ReadResult read_object(const std::string& bucket, const std::string& object, Sink& sink, int64_t offset = 0,
                          int64_t limit = -1, const volatile bool* cancel = nullptr);
   ObjectMeta stat_object(const std::string& bucket, const std::string& object);
+  // objects.compose / ComposeObject (1..32 sources, same bucket).
+  ObjectMeta compose_object(const std::string& bucket, const std::string& dest, const std::vector<std::string>& sources,
+                            const std::string& content_type = "");
+  void delete_object(const std::string& bucket, const std::string& object);
   ListResult list_objects(const std::string& bucket, const std::string& prefix, int page_size = 1000,
                           const std::string& page_token = "", const std::string& delimiter = "");
   // Lists every page.
@@ -132,6 +136,9 @@ class StorageClient {
   virtual void read_attempt(const std::string& bucket, const std::string& object, Sink& sink, int64_t offset,
                             int64_t limit, bool first_attempt, ReadResult* rr, uint64_t* delivered) = 0;
   virtual ObjectMeta stat_attempt(const std::string& bucket, const std::string& object) = 0;
+  virtual ObjectMeta compose_attempt(const std::string& bucket, const std::string& dest,
+                                     const std::vector<std::string>& sources, const std::string& content_type) = 0;
+  virtual void delete_attempt(const std::string& bucket, const std::string& object) = 0;
   virtual ListResult list_attempt(const std::string& bucket, const std::string& prefix, int page_size,
                                   const std::string& page_token, const std::string& delimiter) = 0;
   virtual ObjectMeta write_impl(const std::string& bucket, const std::string& object, ByteSource& src,

@@ -624,6 +624,26 @@ class GrpcStorageClient : public StorageClient {
     return from_v2(o);
   }
 
+  ObjectMeta compose_attempt(const std::string& bucket, const std::string& dest,
+                             const std::vector<std::string>& sources, const std::string& content_type) override {
+    v2::ComposeObjectRequest q;
+    q.destination.bucket = v2::bucket_resource(bucket);
+    q.destination.name = dest;
+    q.destination.content_type = content_type;
+    q.sources = sources;
+    std::string resp = unary("ComposeObject", q.destination.bucket, v2::encode_compose_request(q));
+    v2::Object o;
+    if (!v2::decode_object(resp, &o)) throw StorageError("ComposeObject: bad response", false);
+    return from_v2(o);
+  }
+
+  void delete_attempt(const std::string& bucket, const std::string& object) override {
+    v2::GetObjectRequest q;
+    q.bucket = v2::bucket_resource(bucket);
+    q.object = object;
+    unary("DeleteObject", q.bucket, v2::encode_delete_request(q));
+  }
+
   ListResult list_attempt(const std::string& bucket, const std::string& prefix, int page_size,
                           const std::string& page_token, const std::string& delimiter) override {
     v2::ListObjectsRequest q;

@@ -129,6 +129,38 @@ class HttpStorageClient : public StorageClient {
     return meta_from_json(Json::parse(body));
   }
 
+  ObjectMeta compose_attempt(const std::string& bucket, const std::string& dest,
+                             const std::vector<std::string>& sources, const std::string& content_type) override {
+    Json body = Json::object();
+    Json arr = Json::array();
+    for (const auto& n : sources) {
+      Json e = Json::object();
+      e.set("name", Json::str(n));
+      arr.push(e);
+    }
+    body.set("sourceObjects", arr);
+    Json d = Json::object();
+    if (!content_type.empty()) d.set("contentType", Json::str(content_type));
+    body.set("destination", d);
+    const std::string b = body.dump();
+    Http1Exchange ex(pool_, decorators_);
+    ex.send("POST", "/storage/v1/b/" + url_encode(bucket) + "/o/" + url_encode(dest) + "/compose",
+            {{"Content-Type", "application/json; charset=UTF-8"}}, b.data(), b.size());
+    std::string rb = ex.read_body_string();
+    if (ex.head().status != 200) throw_status(ex.head().status, "compose " + bucket + "/" + dest, rb);
+    ex.close();
+    return meta_from_json(Json::parse(rb));
+  }
+
+  void delete_attempt(const std::string& bucket, const std::string& object) override {
+    Http1Exchange ex(pool_, decorators_);
+    ex.send("DELETE", "/storage/v1/b/" + url_encode(bucket) + "/o/" + url_encode(object), {});
+    std::string rb = ex.read_body_string();
+    if (ex.head().status != 204 && ex.head().status != 200)
+      throw_status(ex.head().status, "delete " + bucket + "/" + object, rb);
+    ex.close();
+  }
+
   ListResult list_attempt(const std::string& bucket, const std::string& prefix, int page_size,
                           const std::string& page_token, const std::string& delimiter) override {
     std::string q = "/storage/v1/b/" + url_encode(bucket) + "/o?maxResults=" + std::to_string(page_size);

@@ -154,3 +154,147 @@ ReadResult SlicedReader::read(const std::string& bucket, const std::string& obje
 }
 
 }  // namespace gcsb
+
+namespace gcsb {
+
+SlicedWriter::SlicedWriter(const ClientConfig& client_cfg, SlicedWriteConfig cfg) : cfg_(std::move(cfg)) {
+  cfg_.slices = std::max(1, std::min(32, cfg_.slices));
+  ClientConfig cc = client_cfg;
+  cc.grpc_conn_pool_size = 1;
+  for (int i = 0; i < cfg_.slices; ++i) clients_.push_back(make_client(cc));
+  jobs_.resize(cfg_.slices);
+  for (int i = 1; i < cfg_.slices; ++i) threads_.emplace_back([this, i] { thread_main(i); });
+}
+
+SlicedWriter::~SlicedWriter() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  for (auto& t : threads_) t.join();
+}
+
+void SlicedWriter::thread_main(int i) {
+  pin_current_thread(cfg_.cpus);
+  std::unique_lock<std::mutex> lk(mu_);
+  for (;;) {
+    cv_.wait(lk, [&] { return stop_ || jobs_[i].pending; });
+    if (stop_) return;
+    jobs_[i].pending = false;
+    lk.unlock();
+    try {
+      jobs_[i].fn();
+    } catch (const StorageError& e) {
+      jobs_[i].error = e.what();
+      jobs_[i].retryable = e.retryable();
+    } catch (const std::exception& e) {
+      jobs_[i].error = e.what();
+    }
+    lk.lock();
+    jobs_[i].done = true;
+    done_cv_.notify_all();
+  }
+}
+
+// Runs jobs_[0..n) (job 0 on the caller) and waits for all of them.
+void SlicedWriter::run_all(int n) {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (int i = 0; i < n; ++i) {
+      jobs_[i].done = false;
+      jobs_[i].error.clear();
+      jobs_[i].retryable = false;
+      jobs_[i].pending = i > 0;
+    }
+  }
+  cv_.notify_all();
+  try {
+    jobs_[0].fn();
+  } catch (const StorageError& e) {
+    jobs_[0].error = e.what();
+    jobs_[0].retryable = e.retryable();
+  } catch (const std::exception& e) {
+    jobs_[0].error = e.what();
+  }
+  std::unique_lock<std::mutex> lk(mu_);
+  done_cv_.wait(lk, [&] {
+    for (int i = 1; i < n; ++i)
+      if (!jobs_[i].done) return false;
+    return true;
+  });
+}
+
+ObjectMeta SlicedWriter::write(const std::string& bucket, const std::string& object, uint64_t total,
+                               const MakeSource& make_source, const WriteOptions& opt) {
+  int n = cfg_.slices;
+  if (cfg_.min_slice_bytes) n = static_cast<int>(std::min<uint64_t>(n, std::max<uint64_t>(1, total / cfg_.min_slice_bytes)));
+  const uint64_t align = 256u << 10;  // resumable chunk granularity
+  uint64_t per = (total + n - 1) / std::max(1, n);
+  per = std::max<uint64_t>(align, (per + align - 1) / align * align);
+  std::vector<std::pair<uint64_t, uint64_t>> parts;
+  for (uint64_t off = 0; off < total || parts.empty(); off += per) {
+    parts.emplace_back(off, std::min(per, total - off));
+    if (total == 0) break;
+  }
+  n = static_cast<int>(parts.size());
+  if (n == 1) {  // nothing to compose: a plain upload
+    auto src = make_source(0, 0, total);
+    return clients_[0]->write_object(bucket, object, *src, opt);
+  }
+  const std::string tag = std::to_string(wall_ns() % 1000000007) + "-" + std::to_string(++seq_);
+  std::vector<std::string> names(n);
+  std::vector<ObjectMeta> metas(n);
+  std::vector<uint32_t> crcs(n, 0);
+  std::vector<bool> has_crc(n, false);
+  for (int i = 0; i < n; ++i) {
+    names[i] = object + ".gcsb-part-" + tag + "-" + std::to_string(i);
+    jobs_[i].fn = [&, i] {
+      auto src = make_source(i, parts[i].first, parts[i].second);
+      has_crc[i] = src->has_crc32c();
+      crcs[i] = src->crc32c();
+      metas[i] = clients_[i]->write_object(bucket, names[i], *src, opt);
+    };
+  }
+  run_all(n);
+  std::string err;
+  bool retryable = true;
+  for (int i = 0; i < n; ++i)
+    if (!jobs_[i].error.empty() && err.empty()) {
+      err = "part " + std::to_string(i) + ": " + jobs_[i].error;
+      retryable = jobs_[i].retryable;
+    }
+  auto cleanup = [&] {
+    for (int i = 0; i < n; ++i)
+      jobs_[i].fn = [&, i] {
+        try {
+          clients_[i]->delete_object(bucket, names[i]);
+        } catch (const StorageError&) {
+        }
+      };
+    run_all(n);
+  };
+  if (!err.empty()) {
+    cleanup();
+    throw StorageError("parallel composite upload of " + object + ": " + err, retryable);
+  }
+  ObjectMeta m = clients_[0]->compose_object(bucket, object, names, opt.content_type);
+  cleanup();
+  uint32_t want = 0;
+  bool known = true;
+  for (int i = 0; i < n; ++i) {
+    known = known && has_crc[i];
+    want = crc32c_combine(want, crcs[i], parts[i].second);
+  }
+  if (known && m.has_crc32c && m.crc32c != want) {
+    char b[160];
+    std::snprintf(b, sizeof(b), "composed object CRC32C %08x != combined part CRC32C %08x", m.crc32c, want);
+    throw StorageError(b, false);
+  }
+  if (m.size != static_cast<int64_t>(total))
+    throw StorageError("composed object has " + std::to_string(m.size) + " of " + std::to_string(total) + " bytes",
+                       false);
+  return m;
+}
+
+}  // namespace gcsb

@@ -79,3 +79,54 @@ class SlicedReader {
 };
 
 }  // namespace gcsb
+
+namespace gcsb {
+
+// Parallel composite upload (the gcloud / gsutil "parallel composite upload"
+// technique) [new]: the object is cut into `slices` parts that upload
+// concurrently, each on its own connection (own StorageClient) as a temporary
+// object, then one compose call assembles the destination and the parts are
+// deleted.  Each part's CRC32C is sent with it and checked by the server; the
+// composed object's CRC32C must equal the GF(2) combine of the parts' CRCs.
+struct SlicedWriteConfig {
+  int slices = 8;                       // <= 32 (compose limit)
+  uint64_t min_slice_bytes = 8u << 20;
+  std::vector<int> cpus;
+};
+
+class SlicedWriter {
+ public:
+  // make_source(i, offset, len): the ByteSource for part i (e.g. a
+  // GpuByteSource over HBM [dptr + offset, +len)).
+  using MakeSource = std::function<std::unique_ptr<ByteSource>(int, uint64_t, uint64_t)>;
+
+  SlicedWriter(const ClientConfig& client_cfg, SlicedWriteConfig cfg);
+  ~SlicedWriter();
+  SlicedWriter(const SlicedWriter&) = delete;
+  SlicedWriter& operator=(const SlicedWriter&) = delete;
+
+  ObjectMeta write(const std::string& bucket, const std::string& object, uint64_t total, const MakeSource& make_source,
+                   const WriteOptions& opt);
+  int slices() const { return cfg_.slices; }
+
+ private:
+  struct Job {
+    std::function<void()> fn;
+    bool pending = false, done = false;
+    std::string error;
+    bool retryable = false;
+  };
+  void thread_main(int i);
+  void run_all(int n);
+
+  SlicedWriteConfig cfg_;
+  std::vector<std::unique_ptr<StorageClient>> clients_;
+  std::vector<Job> jobs_;
+  std::vector<std::thread> threads_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  bool stop_ = false;
+  uint64_t seq_ = 0;
+};
+
+}  // namespace gcsb

@@ -160,6 +160,10 @@ def run_write(opts: RunOptions, nobjects: int, size: int, name_prefix: str = "up
     import torch
 
     client = _native.Client(opts.client_dict())
+    # slices > 1: parallel composite upload (parts on their own connections,
+    # composed server-side; csrc/storage/sliced.h SlicedWriter)
+    writer = _native.SlicedWriter({**opts.client_dict(), "slices": opts.slices,
+                                   "slice_min_bytes": opts.slice_min_bytes}) if opts.slices > 1 else None
     dev = opts.device
     buf = torch.empty(size, dtype=torch.uint8, device=f"cuda:{dev}")
     lat = []
@@ -171,12 +175,21 @@ def run_write(opts: RunOptions, nobjects: int, size: int, name_prefix: str = "up
         name = f"{name_prefix}{gid}"
         _native.gpu_fill_pattern(dev, buf.data_ptr(), size, name, 0)
         t0 = time.perf_counter()
-        m = client.write_from_device(opts.bucket, name, buf.data_ptr(), size, dev, resumable, chunk_bytes,
-                                     opts.ring_slot_bytes, opts.ring_slots)
-        lat.append((time.perf_counter() - t0) * 1e3)
-        setup.append(m["gpu_crc_ms"])
-        if m["size"] != size or m["crc32c"] != m["gpu_crc32c"]:
-            raise RuntimeError(f"upload of {name} not confirmed: {m}")
+        if writer is not None:
+            m = writer.write_from_device(opts.bucket, name, buf.data_ptr(), size, dev, resumable, chunk_bytes,
+                                         opts.ring_slot_bytes, opts.ring_slots)
+            lat.append((time.perf_counter() - t0) * 1e3)
+            # SlicedWriter already checked the composed CRC32C against the
+            # combine of the parts' GPU CRCs
+            if m["size"] != size:
+                raise RuntimeError(f"upload of {name} not confirmed: {m}")
+        else:
+            m = client.write_from_device(opts.bucket, name, buf.data_ptr(), size, dev, resumable, chunk_bytes,
+                                         opts.ring_slot_bytes, opts.ring_slots)
+            lat.append((time.perf_counter() - t0) * 1e3)
+            setup.append(m["gpu_crc_ms"])
+            if m["size"] != size or m["crc32c"] != m["gpu_crc32c"]:
+                raise RuntimeError(f"upload of {name} not confirmed: {m}")
         total += size
         if verify_readback:
             got = client.read(opts.bucket, name)

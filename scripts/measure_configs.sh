@@ -54,6 +54,8 @@ for p in grpc http; do
   run c5_${p}_write64m 300 -workload write -client-protocol $p -sink gpu -worker 1 -write-objects 20 \
     -fake-retain-uploads=false \
     -write-size $((64 * MIB)) -fake-objects 1 -fake-object-size $MIB
+  run c5_${p}_write64m_pcu8 300 -workload write -client-protocol $p -sink gpu -worker 1 -write-objects 20 \
+    -fake-retain-uploads=false -slices 8 -write-size $((64 * MIB)) -fake-objects 1 -fake-object-size $MIB
   run c5_${p}_write64m_retain 300 -workload write -client-protocol $p -sink gpu -worker 1 -write-objects 20 \
     -write-size $((64 * MIB)) -fake-objects 1 -fake-object-size $MIB
 done

@@ -232,3 +232,19 @@ def test_hbm_reader_destination_too_small(native, server, gpu_available):
     r = hbm.HbmReader("http", server.url, slices=4, slice_min_bytes=1 << 20)
     with pytest.raises(native.StorageError, match="larger than the destination"):
         r.read(B, P + "0", out=torch.empty(1 << 20, dtype=torch.uint8, device="cuda:0"))
+
+
+@pytest.mark.parametrize("proto", ["http", "grpc"])
+def test_parallel_composite_upload_from_hbm(native, server, gpu_available, proto):
+    import torch
+
+    size = (24 << 20) + 4097
+    name = "upload/pcu"
+    t = torch.empty(size, dtype=torch.uint8, device="cuda:0")
+    native.gpu_fill_pattern(0, t.data_ptr(), size, name, 0)
+    w = native.SlicedWriter({"protocol": proto, "endpoint": server.url, "slices": 6, "slice_min_bytes": 1 << 20})
+    m = w.write_from_device(B, name, t.data_ptr(), size, 0, True, 4 << 20, 2 << 20, 3)
+    assert m["size"] == size and m["crc32c"] == native.gpu_crc32c(0, t.data_ptr(), size)
+    c = native.Client({"protocol": proto, "endpoint": server.url})
+    assert c.read_bytes(B, name) == native.object_bytes(name, 0, size)
+    assert [o["name"] for o in c.list_all(B, "upload/")] == [name]

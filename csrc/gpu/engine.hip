@@ -596,7 +596,8 @@ GpuByteSource::GpuByteSource(int device, const void* dptr, uint64_t n, size_t sl
     : device_(device),
       src_(static_cast<const uint8_t*>(dptr)),
       n_(n),
-      slot_bytes_(std::max<size_t>(slot_bytes, 65536)),
+      // a ring slot never larger than the (part of the) object it stages
+      slot_bytes_(std::max<size_t>(std::min<uint64_t>(slot_bytes, (n + 65535) / 65536 * 65536), 65536)),
       nslots_(std::max(2, slots)) {
   hip_check(hipSetDevice(device_), "hipSetDevice");
   hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");

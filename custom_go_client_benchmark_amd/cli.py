@@ -53,6 +53,7 @@ def build_flags() -> FlagSet:
     fs.int("write-objects", 1, "write: objects per rank")
     fs.int("write-size", 64 << 20, "write: object size in bytes")
     fs.bool("resumable", True, "write: resumable session (HTTP) / StartResumableWrite (gRPC)")
+    fs.int("write-warmup", 1, "write: untimed warm-up uploads first (connections, pinned staging rings)")
     fs.string("http-api", "xml", "HTTP media API: xml (library default) | json (alt=media)")
     fs.int("read-chunk", 2 << 20, "Bytes per receive into the sink (reference intent: 2 MiB buffer)")
     fs.int("grpc-conn-pool-size", 1, "gRPC connections (reference GrpcConnPoolSize = 1)")
@@ -226,7 +227,7 @@ def main(argv: list[str] | None = None) -> int:
         elif wl == "write":
             before_start()
             res = workloads.run_write(opts, fs.get("write-objects"), fs.get("write-size"),
-                                      resumable=fs.get("resumable"))
+                                      resumable=fs.get("resumable"), warmup=fs.get("write-warmup"))
         else:
             _err(f"unknown -workload {wl}")
             return 2

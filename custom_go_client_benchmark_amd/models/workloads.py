@@ -153,7 +153,8 @@ def run_list_read(opts: RunOptions, prefix: str, on_records=None, before_start=N
 
 
 def run_write(opts: RunOptions, nobjects: int, size: int, name_prefix: str = "upload/obj_",
-              resumable: bool = True, chunk_bytes: int = 16 << 20, verify_readback: bool = False) -> WorkloadResult:
+              resumable: bool = True, chunk_bytes: int = 16 << 20, verify_readback: bool = False,
+              warmup: int = 1) -> WorkloadResult:
     """Config 5: objects generated in HBM (K3 fill kernel), staged HBM ->
     pinned (D2H on a side stream), uploaded via a resumable session (HTTP) or
     StartResumableWrite + WriteObject (gRPC); the server checks CRC32C."""
@@ -166,6 +167,16 @@ def run_write(opts: RunOptions, nobjects: int, size: int, name_prefix: str = "up
                                    "slice_min_bytes": opts.slice_min_bytes}) if opts.slices > 1 else None
     dev = opts.device
     buf = torch.empty(size, dtype=torch.uint8, device=f"cuda:{dev}")
+    # untimed warm-up uploads: connections, pinned staging rings (PinnedPool)
+    for i in range(warmup):
+        wname = f"{name_prefix}warmup_{opts.worker_id_offset}_{i}"
+        _native.gpu_fill_pattern(dev, buf.data_ptr(), size, wname, 0)
+        if writer is not None:
+            writer.write_from_device(opts.bucket, wname, buf.data_ptr(), size, dev, resumable, chunk_bytes,
+                                     opts.ring_slot_bytes, opts.ring_slots)
+        else:
+            client.write_from_device(opts.bucket, wname, buf.data_ptr(), size, dev, resumable, chunk_bytes,
+                                     opts.ring_slot_bytes, opts.ring_slots)
     lat = []
     setup = []
     total = 0
@@ -201,7 +212,8 @@ def run_write(opts: RunOptions, nobjects: int, size: int, name_prefix: str = "up
     def pct(p):
         return s[min(len(s) - 1, len(s) * p // 100)] if s else 0.0
 
-    summary = {"reads": 0, "writes": nobjects, "errors": 0, "bytes": total, "elapsed_s": elapsed,
+    summary = {"reads": 0, "writes": nobjects, "warmup_writes": warmup, "errors": 0, "bytes": total,
+               "elapsed_s": elapsed,
                "mib_per_s": total / elapsed / 2**20 if elapsed else 0.0, "p50_ms": pct(50), "p99_ms": pct(99),
                "min_ms": s[0] if s else 0.0, "max_ms": s[-1] if s else 0.0, "avg_ms": sum(s) / len(s) if s else 0.0}
     summary["gpu_setup_p50_ms"] = sorted(setup)[len(setup) // 2] if setup else 0.0  # staging ring + GPU CRC32C

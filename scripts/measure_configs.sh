@@ -36,6 +36,10 @@ run c1_grpc_1m_cpu_w48 300 -client-protocol grpc -worker 48 -read-call-per-worke
 S256=$((256 * MIB))
 run c2_grpc_256m_hbm 300 -client-protocol grpc -sink gpu -worker 1 -read-call-per-worker 40 -fake-object-size $S256
 run c2_http_256m_hbm 300 -client-protocol http -sink gpu -worker 1 -read-call-per-worker 40 -fake-object-size $S256
+run c2_grpc_256m_hbm_s8 300 -client-protocol grpc -sink gpu -worker 1 -read-call-per-worker 40 -fake-object-size $S256 \
+  -slices 8 -ring-slot-bytes 4194304
+run c2_http_256m_hbm_s8 300 -client-protocol http -sink gpu -worker 1 -read-call-per-worker 40 -fake-object-size $S256 \
+  -slices 8 -ring-slot-bytes 4194304
 run c2_grpc_256m_cpu 300 -client-protocol grpc -worker 1 -read-call-per-worker 40 -fake-object-size $S256
 run c2_http_256m_cpu 300 -client-protocol http -worker 1 -read-call-per-worker 40 -fake-object-size $S256
 

@@ -198,3 +198,24 @@ def test_fakegcs_binary_serves_both_protocols():
             assert r["verified"] and r["bytes"] == 1 << 20
     finally:
         ep.stop()
+
+
+def test_fs_suite_drivers(tmp_path):
+    """scripts/fs_suite.py: the reference's benchmark-script drivers over the
+    native tools (read matrix, write, list with/without cache, open files,
+    ssd_test seq + random) on a prepared directory tree."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / "fs.json"
+    r = subprocess.run([sys.executable, os.path.join(root, "scripts", "fs_suite.py"), "--root", str(tmp_path / "fs"),
+                        "--prepare", "--threads", "2", "--scale", "0.002", "--hold", "0", "--list-files", "20",
+                        "--open-files", "8", "--out", str(out)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    d = json.loads(out.read_text())
+    phases = [p["phase"] for p in d["phases"]]
+    assert len(phases) == 11 and all(p["rc"] == 0 for p in d["phases"])
+    ssd = [p for p in d["phases"] if p["phase"].startswith("ssd_test")]
+    assert all("P50" in p["stdout"] or "p99" in p["stdout"] for p in ssd)

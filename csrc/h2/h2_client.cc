@@ -12,7 +12,10 @@ namespace gcsb {
 
 std::shared_ptr<H2ClientConn> H2ClientConn::dial(const Endpoint& ep, const H2ClientOptions& opt) {
   std::shared_ptr<H2ClientConn> c(new H2ClientConn(ep, opt));
-  c->bc_ = std::make_unique<BufferedConn>(Conn::dial(ep, opt.sock));
+  auto conn = Conn::dial(ep, opt.sock);
+  if (conn->tls() && conn->alpn() != "h2")
+    throw StorageError("TLS peer " + ep.host + " did not negotiate h2 (ALPN '" + conn->alpn() + "')", false);
+  c->bc_ = std::make_unique<BufferedConn>(std::move(conn));
   c->w_ = std::make_unique<H2Writer>(c->bc_->conn());
   c->dec_ = HpackDecoder(opt.header_table_size);
   // connection preface + our SETTINGS + open the connection window wide
@@ -32,7 +35,7 @@ std::shared_ptr<H2ClientConn> H2ClientConn::dial(const Endpoint& ep, const H2Cli
 H2ClientConn::~H2ClientConn() { close(); }
 
 void H2ClientConn::close() {
-  if (!dead_.exchange(true)) {
+  if (!dead_.exchange(true) && w_) {  // w_ is null if dial() failed before the preface
     try {
       w_->write_goaway(0, h2::kErrNoError, "");
     } catch (...) {

@@ -14,6 +14,7 @@
 
 #include <cerrno>
 #include <cstring>
+#include <map>
 #include <algorithm>
 #include <mutex>
 #include <vector>
@@ -65,21 +66,85 @@ void apply_socket_options(int fd, const SocketOptions& opt) {
   }
 }
 
-static SSL_CTX* client_ssl_ctx(bool verify) {
+static SSL_CTX* client_ssl_ctx(bool verify, const std::string& ca_file) {
   static std::mutex mu;
-  static SSL_CTX* ctx[2] = {nullptr, nullptr};
+  static std::map<std::pair<bool, std::string>, SSL_CTX*> ctx;
   std::lock_guard<std::mutex> lk(mu);
-  SSL_CTX*& c = ctx[verify ? 1 : 0];
+  SSL_CTX*& c = ctx[{verify, ca_file}];
   if (!c) {
     c = SSL_CTX_new(TLS_client_method());
+    SSL_CTX_set_min_proto_version(c, TLS1_2_VERSION);
     if (verify) {
-      SSL_CTX_set_default_verify_paths(c);
+      if (!ca_file.empty()) {
+        if (SSL_CTX_load_verify_locations(c, ca_file.c_str(), nullptr) != 1)
+          throw StorageError("TLS: cannot load CA file " + ca_file, false);
+      } else {
+        SSL_CTX_set_default_verify_paths(c);
+      }
       SSL_CTX_set_verify(c, SSL_VERIFY_PEER, nullptr);
     } else {
       SSL_CTX_set_verify(c, SSL_VERIFY_NONE, nullptr);
     }
   }
   return c;
+}
+
+static std::string alpn_wire(const std::string& protos) {  // "h2,http/1.1" -> length-prefixed list
+  std::string w;
+  size_t b = 0;
+  while (b <= protos.size()) {
+    size_t e = protos.find(',', b);
+    if (e == std::string::npos) e = protos.size();
+    if (e > b) {
+      w.push_back(static_cast<char>(e - b));
+      w.append(protos, b, e - b);
+    }
+    b = e + 1;
+  }
+  return w;
+}
+
+void* make_server_tls_ctx(const TlsServer& t) {
+  SSL_CTX* c = SSL_CTX_new(TLS_server_method());
+  if (!c) throw std::runtime_error("SSL_CTX_new failed");
+  if (SSL_CTX_use_certificate_chain_file(c, t.cert_file.c_str()) != 1 ||
+      SSL_CTX_use_PrivateKey_file(c, t.key_file.c_str(), SSL_FILETYPE_PEM) != 1) {
+    SSL_CTX_free(c);
+    throw std::runtime_error("TLS: cannot load server certificate/key " + t.cert_file + " / " + t.key_file);
+  }
+  SSL_CTX_set_alpn_select_cb(
+      c,
+      [](SSL*, const unsigned char** out, unsigned char* outlen, const unsigned char* in, unsigned int inlen,
+         void*) -> int {
+        // prefer h2, then http/1.1
+        for (const char* want : {"h2", "http/1.1"}) {
+          const size_t wl = std::strlen(want);
+          for (unsigned int i = 0; i < inlen;) {
+            unsigned int l = in[i];
+            if (l == wl && i + 1 + l <= inlen && std::memcmp(in + i + 1, want, l) == 0) {
+              *out = in + i + 1;
+              *outlen = static_cast<unsigned char>(l);
+              return SSL_TLSEXT_ERR_OK;
+            }
+            i += 1 + l;
+          }
+        }
+        return SSL_TLSEXT_ERR_NOACK;
+      },
+      nullptr);
+  return c;
+}
+
+void free_server_tls_ctx(void* ctx) {
+  if (ctx) SSL_CTX_free(static_cast<SSL_CTX*>(ctx));
+}
+
+std::string Conn::alpn() const {
+  if (!ssl_) return "";
+  const unsigned char* p = nullptr;
+  unsigned int n = 0;
+  SSL_get0_alpn_selected(ssl_, &p, &n);
+  return p ? std::string(reinterpret_cast<const char*>(p), n) : "";
 }
 
 std::unique_ptr<Conn> Conn::dial(const Endpoint& ep, const SocketOptions& opt) {
@@ -123,15 +188,37 @@ std::unique_ptr<Conn> Conn::dial(const Endpoint& ep, const SocketOptions& opt) {
   auto conn = std::make_unique<Conn>();
   conn->fd_ = fd;
   if (ep.scheme == "https") {
-    SSL* ssl = SSL_new(client_ssl_ctx(opt.tls_verify));
+    SSL* ssl = SSL_new(client_ssl_ctx(opt.tls_verify, opt.tls_ca_file));
     SSL_set_fd(ssl, fd);
     SSL_set_tlsext_host_name(ssl, ep.host.c_str());
+    if (opt.tls_verify) SSL_set1_host(ssl, ep.host.c_str());  // host-name check of the leaf certificate
+    if (!opt.alpn.empty()) {
+      std::string w = alpn_wire(opt.alpn);
+      SSL_set_alpn_protos(ssl, reinterpret_cast<const unsigned char*>(w.data()), static_cast<unsigned>(w.size()));
+    }
     if (SSL_connect(ssl) != 1) {
+      long vr = SSL_get_verify_result(ssl);
+      std::string why = vr != X509_V_OK ? std::string(": certificate ") + X509_verify_cert_error_string(vr) : "";
       SSL_free(ssl);
-      throw StorageError("TLS handshake with " + ep.host + " failed", true);
+      conn->fd_ = fd;  // closed by ~Conn
+      // a certificate failure will not fix itself: not retryable
+      throw StorageError("TLS handshake with " + ep.host + " failed" + why, vr == X509_V_OK);
     }
     conn->ssl_ = ssl;
   }
+  return conn;
+}
+
+std::unique_ptr<Conn> Conn::adopt_tls(int fd, const SocketOptions& opt, void* ssl_ctx) {
+  auto conn = adopt(fd, opt);
+  if (!ssl_ctx) return conn;
+  SSL* ssl = SSL_new(static_cast<SSL_CTX*>(ssl_ctx));
+  SSL_set_fd(ssl, fd);
+  if (SSL_accept(ssl) != 1) {
+    SSL_free(ssl);
+    throw StorageError("TLS accept failed", false);
+  }
+  conn->ssl_ = ssl;
   return conn;
 }
 

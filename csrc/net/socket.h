@@ -34,7 +34,18 @@ struct SocketOptions {
   bool nodelay = true;
   int connect_timeout_ms = 10000;
   int io_timeout_ms = 0;  // 0 = none (reference: http.Client.Timeout=0, main.go:94)
-  bool tls_verify = false;
+  // https endpoints: verify the server certificate chain and host name
+  // against the system roots (or tls_ca_file); ALPN protocol to offer
+  // ("h2" for gRPC, "http/1.1" for the HTTP client).
+  bool tls_verify = true;
+  std::string tls_ca_file;
+  std::string alpn;
+};
+
+// Server-side TLS context from PEM files (fake GCS endpoint over https);
+// ALPN selects "h2" when offered, else "http/1.1".
+struct TlsServer {
+  std::string cert_file, key_file;
 };
 
 class Conn {
@@ -46,6 +57,10 @@ class Conn {
 
   static std::unique_ptr<Conn> dial(const Endpoint& ep, const SocketOptions& opt);
   static std::unique_ptr<Conn> adopt(int fd, const SocketOptions& opt);
+  // Server side of a TLS connection (handshake done here); nullptr ctx = plain.
+  static std::unique_ptr<Conn> adopt_tls(int fd, const SocketOptions& opt, void* ssl_ctx);
+  // Negotiated ALPN protocol ("" if none / plain TCP).
+  std::string alpn() const;
 
   // Returns bytes read (0 = orderly EOF); throws StorageError(retryable) on reset.
   size_t read_some(void* buf, size_t n);
@@ -88,5 +103,8 @@ class Listener {
 };
 
 void apply_socket_options(int fd, const SocketOptions& opt);
+// SSL_CTX for a TLS server (throws on bad cert/key); owned by the caller (free_server_tls_ctx).
+void* make_server_tls_ctx(const TlsServer& t);
+void free_server_tls_ctx(void* ctx);
 
 }  // namespace gcsb

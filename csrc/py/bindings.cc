@@ -59,6 +59,8 @@ ClientConfig client_from(const py::dict& d) {
   c.sock.rcvbuf = get_or<int>(d, "rcvbuf", 0);
   c.sock.sndbuf = get_or<int>(d, "sndbuf", 0);
   c.sock.io_timeout_ms = get_or<int>(d, "io_timeout_ms", 0);
+  c.sock.tls_verify = get_or<bool>(d, "tls_verify", true);
+  c.sock.tls_ca_file = get_or<std::string>(d, "tls_ca_file", "");
   c.project = get_or<std::string>(d, "project", "gcs-fuse-test");
   if (d.contains("cpus") && !d["cpus"].is_none()) c.cpus = d["cpus"].cast<std::vector<int>>();
   std::string auth = get_or<std::string>(d, "auth", "none");
@@ -509,6 +511,8 @@ class PyServer {
     c.grpc_chunk = get_or<uint64_t>(d, "grpc_chunk", 2u << 20);
     c.sndbuf = get_or<int>(d, "sndbuf", 0);
     c.zero_copy = get_or<bool>(d, "zero_copy", true);
+    c.tls_cert_file = get_or<std::string>(d, "tls_cert_file", "");
+    c.tls_key_file = get_or<std::string>(d, "tls_key_file", "");
     if (d.contains("cpus") && !d["cpus"].is_none()) c.cpus = d["cpus"].cast<std::vector<int>>();
     store_ = std::make_shared<ObjectStore>(get_or<bool>(d, "md5", true));
     store_->set_retain_uploads(get_or<bool>(d, "retain_uploads", true));

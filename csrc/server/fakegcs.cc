@@ -16,12 +16,21 @@ namespace gcsb {
 FakeGcsServer::FakeGcsServer(ServerConfig cfg, std::shared_ptr<ObjectStore> store)
     : cfg_(std::move(cfg)), store_(std::move(store)) {}
 
-FakeGcsServer::~FakeGcsServer() { stop(); }
+FakeGcsServer::~FakeGcsServer() {
+  stop();
+  free_server_tls_ctx(tls_ctx_);
+}
 
 void FakeGcsServer::start() {
   // build the pattern buffer (+ its memfd for sendfile) before the first
   // request, so no read pays for it
   if (cfg_.zero_copy) PatternBuffer::instance().memfd();
+  if (!cfg_.tls_cert_file.empty() && !tls_ctx_) {
+    TlsServer t;
+    t.cert_file = cfg_.tls_cert_file;
+    t.key_file = cfg_.tls_key_file;
+    tls_ctx_ = make_server_tls_ctx(t);
+  }
   listener_ = std::make_unique<Listener>(cfg_.host, cfg_.port);
   port_ = listener_->port();
   stopping_ = false;
@@ -76,6 +85,17 @@ void FakeGcsServer::handle_conn(int fd) {
   SocketOptions so;
   so.sndbuf = cfg_.sndbuf;
   so.rcvbuf = 0;
+  if (tls_ctx_) {
+    // TLS: the protocol comes from ALPN (h2 = gRPC, else HTTP/1.1)
+    auto c = Conn::adopt_tls(fd, so, tls_ctx_);
+    const bool h2 = c->alpn() == "h2";
+    auto bc = std::make_unique<BufferedConn>(std::move(c));
+    if (h2)
+      serve_h2(std::move(bc));
+    else
+      serve_http1(std::move(bc));
+    return;
+  }
   auto bc = std::make_unique<BufferedConn>(Conn::adopt(fd, so));
   char peek[3];
   ssize_t k = 0;

@@ -38,6 +38,8 @@ struct ServerConfig {
   int sndbuf = 0;          // 0 = kernel autotuning (an explicit size disables it)
   bool zero_copy = true;   // sendfile() synthetic object bodies from a memfd
   std::vector<int> cpus;   // pin connection/handler threads (empty = unpinned)
+  // https / gRPC over TLS (ALPN h2 or http/1.1) when both are set (PEM files)
+  std::string tls_cert_file, tls_key_file;
 };
 
 struct ServerStats {
@@ -52,7 +54,9 @@ class FakeGcsServer {
   void start();
   void stop();
   int port() const { return port_; }
-  std::string url() const { return "http://" + cfg_.host + ":" + std::to_string(port_); }
+  std::string url() const {
+    return std::string(tls_ctx_ ? "https://" : "http://") + cfg_.host + ":" + std::to_string(port_);
+  }
   ObjectStore& store() { return *store_; }
   FaultConfig& faults() { return faults_; }
   ServerStats& stats() { return stats_; }
@@ -73,6 +77,7 @@ class FakeGcsServer {
   FaultConfig faults_;
   ServerStats stats_;
   std::unique_ptr<Listener> listener_;
+  void* tls_ctx_ = nullptr;  // SSL_CTX when serving TLS
   int port_ = 0;
   std::thread accept_thread_;
   std::atomic<bool> stopping_{false};

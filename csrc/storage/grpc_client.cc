@@ -498,6 +498,7 @@ class GrpcStorageClient : public StorageClient {
     int n = std::max(1, cfg.grpc_conn_pool_size);
     conns_.resize(static_cast<size_t>(n));
     opt_.sock = cfg.sock;
+    opt_.sock.alpn = "h2";  // gRPC over TLS negotiates HTTP/2 by ALPN
     opt_.cpus = cfg.cpus;
     // DirectPath (reference main.go:106-117: GOOGLE_CLOUD_ENABLE_DIRECT_PATH_XDS
     // is set only around NewGRPCClient, with the google-c2p xDS resolver and

@@ -11,6 +11,11 @@
 namespace gcsb {
 namespace {
 
+SocketOptions with_alpn(SocketOptions o, const char* alpn) {
+  o.alpn = alpn;
+  return o;
+}
+
 bool http_retryable(int status) { return status == 408 || status == 429 || status >= 500; }
 
 ObjectMeta meta_from_json(const Json& j) {
@@ -38,7 +43,7 @@ class HttpStorageClient : public StorageClient {
  public:
   explicit HttpStorageClient(const ClientConfig& cfg)
       : StorageClient(cfg),
-        pool_(cfg.endpoint, cfg.sock, cfg.protocol == "http2" ? 0 : cfg.max_conns_per_host,
+        pool_(cfg.endpoint, with_alpn(cfg.sock, "http/1.1"), cfg.protocol == "http2" ? 0 : cfg.max_conns_per_host,
               cfg.protocol == "http2" ? 0 : cfg.max_idle_conns_per_host),
         ua_(cfg.user_agent) {
     // Decorator order mirrors the reference: oauth2.Transport wraps the base

@@ -120,3 +120,12 @@ def test_cli_sets_directpath_env_only_during_client_creation(native):
     assert r.returncode == 0, r.stderr
     assert "gRPC transport: cloudpath (DirectPath requested" in r.stderr
     assert os.environ.get("GOOGLE_CLOUD_ENABLE_DIRECT_PATH_XDS") is None
+
+
+def test_connection_refused_is_a_clean_error(native):
+    # dial failures must surface as StorageError (a failed dial once crashed
+    # the connection's destructor, tests/test_tls.py found it)
+    c = native.Client({"protocol": "grpc", "endpoint": "http://127.0.0.1:1", "retry_max_attempts": 2,
+                       "retry_initial_s": 0.001})
+    with pytest.raises(native.StorageError, match="refused"):
+        c.read("b", "o")

@@ -33,6 +33,8 @@ int main(int argc, char** argv) {
   auto fail_status = f.Int("fail-status", 503, "HTTP status for injected failures");
   auto throttle = f.Int("throttle-bps", 0, "Per-response byte rate cap");
   auto latency = f.Int("latency-ms", 0, "Added time to first byte");
+  auto tls_cert = f.String("tls-cert", "", "PEM certificate: serve https / gRPC over TLS (ALPN h2)");
+  auto tls_key = f.String("tls-key", "", "PEM private key for -tls-cert");
   f.Parse(argc, argv);
 
   sigset_t set;
@@ -46,6 +48,8 @@ int main(int argc, char** argv) {
   cfg.port = static_cast<int>(*port);
   cfg.require_auth = *require_auth;
   cfg.grpc_chunk = static_cast<uint64_t>(*grpc_chunk);
+  cfg.tls_cert_file = *tls_cert;
+  cfg.tls_key_file = *tls_key;
   if (!jwt_key->empty()) {
     std::ifstream in(*jwt_key);
     std::stringstream ss;

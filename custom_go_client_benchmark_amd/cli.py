@@ -82,6 +82,8 @@ def build_flags() -> FlagSet:
     fs.string("key-file", "", "Service-account JSON key (-auth key_file)")
     fs.string("token-uri", "", "Override the key file's token_uri")
     fs.string("user-agent", "prince", "User-Agent (reference userAgentRoundTripper)")
+    fs.string("tls-ca-file", "", "PEM CA bundle for https endpoints (default: system roots)")
+    fs.bool("tls-insecure", False, "Skip TLS certificate verification (test endpoints only)")
     fs.duration("retry-initial", 1.0, "Initial backoff (gax default 1s)")
     fs.duration("retry-max", 30.0, "Max backoff (reference MaxRetryDuration 30s)")
     fs.float("retry-multiplier", 2.0, "Backoff multiplier (reference RetryMultiplier 2)")
@@ -174,7 +176,8 @@ def main(argv: list[str] | None = None) -> int:
         slice_min_bytes=fs.get("slice-min-bytes"),
         trace_sample_rate=fs.get("trace-sample-rate") if fs.get("enable-tracing") else 0.0,
         cpus=placement["client"], auth=fs.get("auth"), token=fs.get("token"), key_file=fs.get("key-file"),
-        token_uri=fs.get("token-uri"), user_agent=fs.get("user-agent"), retry_initial_s=fs.get("retry-initial"),
+        token_uri=fs.get("token-uri"), user_agent=fs.get("user-agent"), tls_ca_file=fs.get("tls-ca-file"),
+        tls_verify=not fs.get("tls-insecure"), retry_initial_s=fs.get("retry-initial"),
         retry_max_s=fs.get("retry-max"), retry_multiplier=fs.get("retry-multiplier"),
         retry_max_total_s=fs.get("retry-max-total"), retry_max_attempts=fs.get("retry-max-attempts"))
 

@@ -45,6 +45,8 @@ class RunOptions:
     key_file: str = ""
     token_uri: str = ""
     user_agent: str = "prince"
+    tls_ca_file: str = ""
+    tls_verify: bool = True
     retry_initial_s: float = 1.0
     retry_max_s: float = 30.0
     retry_multiplier: float = 2.0
@@ -64,6 +66,7 @@ class RunOptions:
             "user_agent": self.user_agent, "retry_initial_s": self.retry_initial_s, "retry_max_s": self.retry_max_s,
             "retry_multiplier": self.retry_multiplier, "retry_max_total_s": self.retry_max_total_s,
             "retry_max_attempts": self.retry_max_attempts, "cpus": list(self.cpus),
+            "tls_ca_file": self.tls_ca_file, "tls_verify": self.tls_verify,
         }
 
     def runner_dict(self) -> dict:

@@ -83,3 +83,23 @@ def test_sliced_read_over_tls(native, tls_server, cert):
     r.wait()
     s = r.summary()
     assert s["errors"] == 0 and s["verified"] == 2, s["first_error"]
+
+
+def test_cli_against_tls_fakegcs_subprocess(native, cert, tmp_path):
+    import sys
+
+    from custom_go_client_benchmark_amd import server as fs
+
+    crt, key = cert
+    ep = fs.start_subprocess(B, P, "", 0, 2, 1 << 20, extra_args=["-tls-cert", crt, "-tls-key", key])
+    try:
+        url = ep.url.replace("http://", "https://").replace("127.0.0.1", "localhost")
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        for proto in ("http", "grpc"):
+            r = subprocess.run([sys.executable, "-m", "custom_go_client_benchmark_amd", "-endpoint", url,
+                                "-client-protocol", proto, "-worker", "2", "-read-call-per-worker", "3",
+                                "-tls-ca-file", crt], capture_output=True, text=True, timeout=120, cwd=root)
+            assert r.returncode == 0, r.stderr[-2000:]
+            assert len([l for l in r.stdout.splitlines() if l.endswith("ms")]) == 6
+    finally:
+        ep.stop()

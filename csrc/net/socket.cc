@@ -205,6 +205,8 @@ std::unique_ptr<Conn> Conn::dial(const Endpoint& ep, const SocketOptions& opt) {
       throw StorageError("TLS handshake with " + ep.host + " failed" + why, vr == X509_V_OK);
     }
     conn->ssl_ = ssl;
+    conn->io_timeout_ms_ = opt.io_timeout_ms;
+    conn->tls_nonblocking();
   }
   return conn;
 }
@@ -219,7 +221,48 @@ std::unique_ptr<Conn> Conn::adopt_tls(int fd, const SocketOptions& opt, void* ss
     throw StorageError("TLS accept failed", false);
   }
   conn->ssl_ = ssl;
+  conn->io_timeout_ms_ = opt.io_timeout_ms;
+  conn->tls_nonblocking();
   return conn;
+}
+
+void Conn::tls_nonblocking() {
+  int fl = fcntl(fd_, F_GETFL, 0);
+  fcntl(fd_, F_SETFL, fl | O_NONBLOCK);
+}
+
+// Waits (without ssl_mu_) until the socket is ready for what SSL asked for.
+void Conn::wait_ready(int ssl_err) {
+  pollfd pfd{fd_, static_cast<short>(ssl_err == SSL_ERROR_WANT_WRITE ? POLLOUT : POLLIN), 0};
+  for (;;) {
+    int pr = ::poll(&pfd, 1, io_timeout_ms_ > 0 ? io_timeout_ms_ : -1);
+    if (pr > 0) return;
+    if (pr == 0) throw StorageError(ssl_err == SSL_ERROR_WANT_WRITE ? "write timeout" : "read timeout", true);
+    if (errno != EINTR) throw StorageError(std::string("poll: ") + std::strerror(errno), true);
+  }
+}
+
+// One SSL_read / SSL_write under ssl_mu_; returns > 0 bytes, 0 = clean EOF (read).
+int Conn::ssl_io(bool write, void* buf, size_t n) {
+  const int len = static_cast<int>(n > (1u << 30) ? (1u << 30) : n);
+  for (;;) {
+    int k, e;
+    {
+      std::lock_guard<std::mutex> lk(ssl_mu_);
+      if (!ssl_) throw StorageError("TLS connection closed", true);
+      ERR_clear_error();
+      k = write ? SSL_write(ssl_, buf, len) : SSL_read(ssl_, buf, len);
+      e = k > 0 ? SSL_ERROR_NONE : SSL_get_error(ssl_, k);
+    }
+    if (k > 0) return k;
+    if (e == SSL_ERROR_ZERO_RETURN && !write) return 0;
+    if (e == SSL_ERROR_WANT_READ || e == SSL_ERROR_WANT_WRITE) {
+      wait_ready(e);
+      continue;
+    }
+    if (e == SSL_ERROR_SYSCALL && errno == EINTR) continue;
+    throw StorageError(write ? "TLS write error" : "TLS read error", true);
+  }
 }
 
 std::unique_ptr<Conn> Conn::adopt(int fd, const SocketOptions& opt) {
@@ -233,7 +276,8 @@ Conn::~Conn() { close(); }
 
 void Conn::close() {
   if (ssl_) {
-    SSL_shutdown(ssl_);
+    std::lock_guard<std::mutex> lk(ssl_mu_);
+    SSL_shutdown(ssl_);  // best effort on the non-blocking socket
     SSL_free(ssl_);
     ssl_ = nullptr;
   }
@@ -252,13 +296,7 @@ size_t Conn::read_some(void* buf, size_t n) {
   for (;;) {
     ssize_t r;
     if (ssl_) {
-      int k = SSL_read(ssl_, buf, static_cast<int>(n > (1u << 30) ? (1u << 30) : n));
-      if (k <= 0) {
-        int e = SSL_get_error(ssl_, k);
-        if (e == SSL_ERROR_ZERO_RETURN) return 0;
-        throw StorageError("TLS read error", true);
-      }
-      r = k;
+      r = ssl_io(false, buf, n);
     } else {
       r = ::recv(fd_, buf, n, 0);
     }
@@ -306,8 +344,7 @@ void Conn::writev_all(struct iovec* iov, int cnt, bool more) {
       auto* p = static_cast<const uint8_t*>(iov[i].iov_base);
       size_t n = iov[i].iov_len;
       while (n > 0) {
-        int k = SSL_write(ssl_, p, static_cast<int>(n > (1u << 30) ? (1u << 30) : n));
-        if (k <= 0) throw StorageError("TLS write error", true);
+        int k = ssl_io(true, const_cast<uint8_t*>(p), n);
         p += k;
         n -= static_cast<size_t>(k);
         bytes_written_ += static_cast<uint64_t>(k);

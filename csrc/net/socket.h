@@ -12,6 +12,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <memory>
+#include <mutex>
 #include <string>
 
 typedef struct ssl_st SSL;
@@ -79,8 +80,17 @@ class Conn {
   uint64_t bytes_written() const { return bytes_written_; }
 
  private:
+  // TLS: an SSL object must not be entered by two threads at once, but an
+  // HTTP/2 connection reads on one thread while others write.  After the
+  // handshake the socket is non-blocking; each SSL_read / SSL_write runs under
+  // ssl_mu_ and the thread waits for readiness (poll) without holding it.
+  int ssl_io(bool write, void* buf, size_t n);
+  void wait_ready(int ssl_err);
+  void tls_nonblocking();
   int fd_ = -1;
   SSL* ssl_ = nullptr;
+  std::mutex ssl_mu_;
+  int io_timeout_ms_ = 0;
   uint64_t bytes_read_ = 0;
   uint64_t bytes_written_ = 0;
 };

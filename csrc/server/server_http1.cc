@@ -356,6 +356,9 @@ class Http1Handler {
   }
 
   void send_media(const Request& r, const StoredObject& o, bool xml) {
+    if (r.has_q("generation") && std::strtoll(r.q("generation").c_str(), nullptr, 10) != o.generation)
+      return respond(c_, 404, {}, json_error(404, "No such object: " + o.bucket + "/" + o.name + "#" + r.q("generation"),
+                                             "notFound"));
     if (maybe_fail(xml)) return;
     if (o.hollow)
       return respond(c_, 412, {}, json_error(412, "object content was not retained (server retain_uploads=false)",

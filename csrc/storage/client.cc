@@ -28,8 +28,9 @@ bool should_retry(const RetryPolicy& p, const StorageError& e, int attempt, int6
 }
 
 ReadResult StorageClient::read_object(const std::string& bucket, const std::string& object, Sink& sink,
-                                      int64_t offset, int64_t limit, const volatile bool* cancel) {
+                                      int64_t offset, int64_t limit, const volatile bool* cancel, int64_t generation) {
   ReadResult rr;
+  rr.pin_generation = generation;
   uint64_t delivered = 0;
   Backoff bo(cfg_.retry);
   int64_t t0 = now_ns();
@@ -52,6 +53,7 @@ ReadResult StorageClient::read_object(const std::string& bucket, const std::stri
         throw;
       }
       ++stats_.retries;
+      if (!rr.pin_generation && rr.info.generation) rr.pin_generation = rr.info.generation;
       if (begun) sink.resume_at(offset + static_cast<int64_t>(delivered));
       sleep_seconds(bo.pause(), cancel);
       if (cancel && *cancel) {

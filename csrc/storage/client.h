@@ -57,6 +57,11 @@ struct ReadResult {
   ObjectInfo info;
   SinkResult sink;
   bool sink_begun = false;  // transport called sink.begin() (set by read_attempt)
+  // Generation every attempt must read (0 = latest).  A retry/resume after a
+  // partial read pins the generation the first attempt saw, as the storage
+  // library's reader does, so the resumed bytes come from the same object
+  // version; sliced reads pin the stat's generation for every slice.
+  int64_t pin_generation = 0;
 };
 
 struct ListResult {
@@ -111,7 +116,7 @@ class StorageClient {
   // Full-object (limit<0) or ranged read into the sink, retried/resumed per
   // the retry policy. `cancel` aborts backoff sleeps.
   ReadResult read_object(const std::string& bucket, const std::string& object, Sink& sink, int64_t offset = 0,
-                         int64_t limit = -1, const volatile bool* cancel = nullptr);
+                         int64_t limit = -1, const volatile bool* cancel = nullptr, int64_t generation = 0);
   ObjectMeta stat_object(const std::string& bucket, const std::string& object);
   // objects.compose / ComposeObject (1..32 sources, same bucket).
   ObjectMeta compose_object(const std::string& bucket, const std::string& dest, const std::vector<std::string>& sources,

@@ -584,6 +584,7 @@ class GrpcStorageClient : public StorageClient {
     q.object = object;
     q.read_offset = offset;
     q.read_limit = limit > 0 ? limit : 0;
+    q.generation = rr->pin_generation;
     GrpcCall* raw = nullptr;
     ReadObjectHandler h(sink, rr, delivered, full, &raw);
     auto call = std::make_shared<GrpcCall>(&h);

@@ -73,6 +73,8 @@ class HttpStorageClient : public StorageClient {
       path = "/storage/v1/b/" + url_encode(bucket) + "/o/" + url_encode(object) + "?alt=media";
     else
       path = "/" + bucket + "/" + url_encode(object, true);
+    if (rr->pin_generation)
+      path += std::string(cfg_.http_api == "json" ? "&" : "?") + "generation=" + std::to_string(rr->pin_generation);
     const HttpResponseHead& head = ex.send("GET", path, h);
     if (head.status != 200 && head.status != 206) {
       std::string body = ex.read_body_string(1 << 20);

@@ -36,7 +36,7 @@ void SlicedReader::run_slice(int i) {
   Job& j = jobs_[i];
   try {
     j.rr = clients_[i]->read_object(j.bucket, j.object, *sinks_[i], static_cast<int64_t>(j.off),
-                                    static_cast<int64_t>(j.len), j.cancel);
+                                    static_cast<int64_t>(j.len), j.cancel, j.generation);
   } catch (const StorageError& e) {
     j.error = e.what();
     j.retryable = e.retryable();
@@ -85,6 +85,7 @@ ReadResult SlicedReader::read(const std::string& bucket, const std::string& obje
       j.off = ranges[i].first;
       j.len = ranges[i].second;
       j.cancel = cancel;
+      j.generation = m.generation;  // every slice reads the stat's object version
       j.rr = ReadResult();
       j.error.clear();
       j.retryable = false;

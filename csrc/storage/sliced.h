@@ -57,6 +57,7 @@ class SlicedReader {
   struct Job {
     std::string bucket, object;
     uint64_t off = 0, len = 0;
+    int64_t generation = 0;
     const volatile bool* cancel = nullptr;
     bool pending = false, done = false;
     ReadResult rr;

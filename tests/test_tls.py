@@ -103,3 +103,15 @@ def test_cli_against_tls_fakegcs_subprocess(native, cert, tmp_path):
             assert len([l for l in r.stdout.splitlines() if l.endswith("ms")]) == 6
     finally:
         ep.stop()
+
+
+def test_grpc_tls_many_streams_one_connection(native, tls_server, cert):
+    """HTTP/2 over TLS: one reader thread and many writer threads share one
+    SSL object (regression: concurrent SSL_read/SSL_write crashed)."""
+    r = native.Runner({"protocol": "grpc", "endpoint": tls_server.url, "tls_ca_file": cert[0], "bucket": B,
+                       "object_prefix": P, "workers": 8, "reads_per_worker": 6, "grpc_conn_pool_size": 1,
+                       "keep_records": False, "object_names": [P + "0"]})
+    r.start()
+    r.wait()
+    s = r.summary()
+    assert s["errors"] == 0 and s["verified"] == 48, s["first_error"]

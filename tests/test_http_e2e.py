@@ -100,3 +100,20 @@ def test_user_agent_and_auth_required(native):
         assert c.read(B, P + "0")["verified"]
     finally:
         srv.stop()
+
+
+def test_generation_pinned_media_reads(native, server):
+    """Resumed and sliced reads pin the object generation (?generation=N /
+    ReadObjectRequest.generation); a stale generation is a 404, not bytes of
+    another object version."""
+    import http.client
+
+    server.add_synthetic(B, P, "", 0, 1, 4096)
+    gen = server.object_info(B, P + "0")["generation"]
+    host, port = server.url.replace("http://", "").split(":")
+    for q, want in ((f"?generation={gen}", 200), (f"?generation={gen + 1}", 404)):
+        conn = http.client.HTTPConnection(host, int(port))
+        conn.request("GET", f"/{B}/{P}0{q}")
+        r = conn.getresponse()
+        r.read()
+        assert r.status == want, q

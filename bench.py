@@ -43,6 +43,37 @@ def parse_size(s: str) -> int:
     return int(s)
 
 
+def cpu_snapshot() -> dict:
+    """Process CPU time (client + node-local endpoint share this process) and
+    the cgroup's CFS throttling counters: on the GPU boxes the container runs
+    under a CPU quota (profiles/r1_gpu_box_env.txt), and loopback TCP costs CPU
+    at both ends, so these explain throughput and the p99 tail."""
+    import resource
+
+    ru = resource.getrusage(resource.RUSAGE_SELF)
+    snap = {"user_s": ru.ru_utime, "sys_s": ru.ru_stime}
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            for line in f:
+                k, _, v = line.partition(" ")
+                if k in ("usage_usec", "nr_periods", "nr_throttled", "throttled_usec"):
+                    snap[k] = int(v)
+    except OSError:
+        pass
+    return snap
+
+
+def cpu_delta(a: dict, b: dict, nbytes: float) -> dict:
+    gib = max(nbytes, 1.0) / (1 << 30)
+    out = {"process_cpu_s_per_gib": round((b["user_s"] + b["sys_s"] - a["user_s"] - a["sys_s"]) / gib, 4),
+           "process_sys_fraction": round((b["sys_s"] - a["sys_s"]) /
+                                         max(1e-9, b["user_s"] + b["sys_s"] - a["user_s"] - a["sys_s"]), 3)}
+    for k in ("nr_periods", "nr_throttled", "throttled_usec"):
+        if k in a and k in b:
+            out["cgroup_" + k] = b[k] - a[k]
+    return out
+
+
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
@@ -70,6 +101,7 @@ def main() -> int:
     import custom_go_client_benchmark_amd as pkg
     from custom_go_client_benchmark_amd.ops import hbm
     from custom_go_client_benchmark_amd.parallel import dist as gdist
+    from custom_go_client_benchmark_amd.utils import cpuacct
 
     n = pkg._native
     rank, world, local_rank = gdist.env_rank()
@@ -127,6 +159,8 @@ def main() -> int:
     gdist.barrier(ctx, "R1/R2 bench barrier")
     if torch.cuda.is_available():
         torch.cuda.synchronize()
+    c0 = cpu_snapshot()
+    th0 = cpuacct.thread_cpu()
     t0 = time.perf_counter()
     run.start()
     run.wait()
@@ -135,6 +169,9 @@ def main() -> int:
     gdist.barrier(ctx, "R1/R2 bench barrier")
     elapsed = time.perf_counter() - t0
     s = run.summary()
+    cpu = cpu_delta(c0, cpu_snapshot(), float(s["bytes"]))
+    cpu["cpu_s_per_gib_by_thread"] = cpuacct.per_gib(cpuacct.delta_by_group(th0, cpuacct.thread_cpu()),
+                                                     float(s["bytes"]))
 
     # single-stream comparison (slices=1: the reference's one stream per read)
     ss_steps = args.steps if args.single_stream_steps < 0 else args.single_stream_steps
@@ -203,6 +240,7 @@ def main() -> int:
             "host_landed_p50_ms": round(stats["host_p50_max"], 3),
             "endpoint": "loopback synthetic GCS (one per rank)",
             "affinity": args.affinity,
+            "rank0_cpu": cpu,
         }
         if ss_stats is not None:
             out["single_stream_mib_s"] = round(ss_stats["nbytes_sum"] / ss_stats["elapsed_max"] / (1 << 20), 2)

@@ -112,6 +112,7 @@ void Runner::record(ReadRecord&& r, double ms, double host_ms) {
 void Runner::worker_main(int w) {
   // pin before the sink allocates its pinned ring: NUMA-local first touch
   pin_current_thread(cfg_.client.cpus);
+  name_current_thread("gcsb-worker");
   try {
     if (cfg_.slices > 1 && !sliced_[w]) {
       SlicedReadConfig sc;

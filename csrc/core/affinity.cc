@@ -3,6 +3,7 @@
 #include <pthread.h>
 #include <sched.h>
 
+#include <cstdio>
 #include <cstdlib>
 
 #include "core/util.h"
@@ -33,6 +34,12 @@ bool pin_current_thread(const std::vector<int>& cpus) {
   for (int c : cpus)
     if (c >= 0 && c < CPU_SETSIZE) CPU_SET(c, &set);
   return pthread_setaffinity_np(pthread_self(), sizeof(set), &set) == 0;
+}
+
+void name_current_thread(const char* name) {
+  char buf[16];
+  std::snprintf(buf, sizeof(buf), "%s", name);
+  pthread_setname_np(pthread_self(), buf);
 }
 
 std::vector<int> cpus_for(const std::vector<int>& cpus, int k, bool spread) {

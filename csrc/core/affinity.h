@@ -19,5 +19,8 @@ bool pin_current_thread(const std::vector<int>& cpus);
 // Round-robin pick: thread k gets cpus[k % n] (single-CPU pinning) when
 // `spread` is set, else the whole set.
 std::vector<int> cpus_for(const std::vector<int>& cpus, int k, bool spread);
+// Names the calling thread (/proc/<pid>/task/<tid>/comm, 15 chars max) so the
+// bench can attribute process CPU time to client / endpoint / GPU threads.
+void name_current_thread(const char* name);
 
 }  // namespace gcsb

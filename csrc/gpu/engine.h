@@ -174,7 +174,11 @@ class GpuByteSource : public ByteSource {
   void seek(uint64_t off) override;
   bool has_crc32c() const override { return has_crc_; }
   uint32_t crc32c() const override { return crc_; }
+  // Ranges on the chunk grid (start on a grid multiple, end on one or at the
+  // object end) are answered from the GPU-computed chunk CRCs.
+  bool range_crc32c(uint64_t off, size_t len, uint32_t* crc) override;
   uint64_t copies() const { return copies_; }
+  uint64_t gpu_range_crcs() const { return range_hits_; }
 
  private:
   void restart(uint64_t off);
@@ -195,6 +199,9 @@ class GpuByteSource : public ByteSource {
   bool has_crc_ = false;
   uint32_t crc_ = 0;
   uint64_t copies_ = 0;
+  uint64_t grid_ = 0;                // chunk grid of chunk_crc_ (0 = none)
+  std::vector<uint32_t> chunk_crc_;  // CRC32C of [i*grid_, min((i+1)*grid_, n_))
+  uint64_t range_hits_ = 0;
 };
 
 // Grow-only HBM buffer (e.g. the landing zone a sliced read's slice sinks
@@ -215,8 +222,12 @@ class DeviceBuffer {
   size_t cap_ = 0;
 };
 
-// Device CRC32C of an arbitrary device range (test/verification utility).
-uint32_t gpu_crc32c(int device, const void* dptr, size_t n);
+// Device CRC32C of an arbitrary device range.  chunk > 0: the range is cut
+// into chunk-byte segments from its start and each segment's CRC32C is
+// appended to *chunks (upload messages' ChecksummedData CRCs); chunk 0 picks
+// segment sizes for throughput.
+uint32_t gpu_crc32c(int device, const void* dptr, size_t n, size_t chunk = 0,
+                    std::vector<uint32_t>* chunks = nullptr);
 // Kernel throughput probe: K1+K2 over [dptr, dptr+n) in segments of
 // seg_bytes (<= kMaxSeg of them), `iters` back-to-back batches, GB/s.
 double gpu_crc32c_throughput(int device, const void* dptr, size_t n, int iters, size_t seg_bytes, uint32_t* crc0);

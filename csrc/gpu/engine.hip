@@ -9,9 +9,11 @@
 #include <functional>
 #include <map>
 #include <mutex>
+#include <numeric>
 #include <thread>
 #include <stdexcept>
 
+#include "core/affinity.h"
 #include "core/crc32c.h"
 #include "core/util.h"
 #include "gpu/markers.h"
@@ -153,6 +155,7 @@ class DeviceSubmitter {
     std::thread([this] { loop(); }).detach();
   }
   void loop() {
+    name_current_thread("gcsb-submit");
     ensure_device(dev_);
     std::unique_lock<std::mutex> lk(mu_);
     for (;;) {
@@ -610,10 +613,28 @@ GpuByteSource::GpuByteSource(int device, const void* dptr, uint64_t n, size_t sl
     hip_check(hipEventCreateWithFlags(&ev_[i], hipEventDisableTiming), "hipEventCreate");
   }
   if (gpu_crc) {
-    crc_ = gpu_crc32c(device_, src_, n_);
+    // Chunk CRCs on a grid that the transport's upload messages fall on:
+    // messages are <= 2 MiB (gRPC MAX_WRITE_CHUNK_BYTES) and never cross a
+    // staging slot, so with slot-aligned slots gcd(slot, 2 MiB) tiles them.
+    const uint64_t g = std::gcd<uint64_t>(slot_bytes_, uint64_t(2) << 20);
+    if (g >= 65536) grid_ = g;
+    crc_ = gpu_crc32c(device_, src_, n_, grid_, grid_ ? &chunk_crc_ : nullptr);
     has_crc_ = true;
   }
   restart(0);
+}
+
+bool GpuByteSource::range_crc32c(uint64_t off, size_t len, uint32_t* crc) {
+  if (grid_ == 0 || len == 0 || off % grid_ != 0) return false;
+  const uint64_t end = off + len;
+  if (end > n_ || (end % grid_ != 0 && end != n_)) return false;
+  const size_t i = off / grid_, j = (end + grid_ - 1) / grid_;
+  if (j > chunk_crc_.size()) return false;
+  uint32_t c = chunk_crc_[i];
+  for (size_t k = i + 1; k < j; ++k) c = crc32c_combine(c, chunk_crc_[k], std::min<uint64_t>(grid_, n_ - k * grid_));
+  *crc = c;
+  ++range_hits_;
+  return true;
 }
 
 GpuByteSource::~GpuByteSource() {
@@ -697,7 +718,7 @@ uint8_t* DeviceBuffer::ensure(size_t n) {
   return p_;
 }
 
-uint32_t gpu_crc32c(int device, const void* dptr, size_t n) {
+uint32_t gpu_crc32c(int device, const void* dptr, size_t n, size_t chunk, std::vector<uint32_t>* chunks) {
   if (n == 0) return 0;
   hip_check(hipSetDevice(device), "hipSetDevice");
   const CrcTables* tabs = device_crc_tables(device);
@@ -707,6 +728,10 @@ uint32_t gpu_crc32c(int device, const void* dptr, size_t n) {
   // tile in parallel and K2 folds with kMaxSeg workgroups, not one.
   size_t seg = (n + kMaxSeg - 1) / kMaxSeg;
   seg = std::min<size_t>(std::max<size_t>((seg + kCrcTile - 1) / kCrcTile * kCrcTile, 1u << 20), 1u << 30);
+  if (chunk > 0) {
+    seg = std::min<size_t>(chunk, 1u << 30);
+    if (chunks) chunks->reserve(chunks->size() + (n + seg - 1) / seg);
+  }
   const uint8_t* p = static_cast<const uint8_t*>(dptr);
   uint32_t crc = 0;
   size_t off = 0;
@@ -728,7 +753,10 @@ uint32_t gpu_crc32c(int device, const void* dptr, size_t n) {
     }
     launch_crc32c_batch(b, tabs, c.d_tiles, c.d_res, c.st);
     hip_check(hipStreamSynchronize(c.st), "hipStreamSynchronize");
-    for (uint32_t i = 0; i < b.nseg; ++i) crc = crc32c_combine(crc, c.res[i].crc, b.seg[i].len);
+    for (uint32_t i = 0; i < b.nseg; ++i) {
+      crc = crc32c_combine(crc, c.res[i].crc, b.seg[i].len);
+      if (chunks) chunks->push_back(c.res[i].crc);
+    }
   }
   return crc;
 }

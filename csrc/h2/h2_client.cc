@@ -27,6 +27,7 @@ std::shared_ptr<H2ClientConn> H2ClientConn::dial(const Endpoint& ep, const H2Cli
   c->w_->write_window_update(0, static_cast<uint32_t>(h2::kMaxWindow - h2::kDefaultWindow));
   c->reader_ = std::thread([raw = c.get()] {
     pin_current_thread(raw->opt_.cpus);
+    name_current_thread("gcsb-h2-reader");
     raw->reader_loop();
   });
   return c;

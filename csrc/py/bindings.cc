@@ -349,7 +349,7 @@ class PyClient {
                              int device, bool resumable, size_t chunk_bytes, size_t slot_bytes, int slots) {
     ObjectMeta m;
     double crc_ms = 0, upload_ms = 0;
-    uint64_t copies = 0;
+    uint64_t copies = 0, range_crcs = 0;
     uint32_t crc = 0;
     {
       py::gil_scoped_release nogil;
@@ -364,10 +364,12 @@ class PyClient {
       crc_ms = (t1 - t0) / 1e6;
       upload_ms = (t2 - t1) / 1e6;
       copies = src.copies();
+      range_crcs = src.gpu_range_crcs();
       crc = src.crc32c();
     }
     py::dict d = meta_dict(m);
     d["gpu_crc32c"] = crc;
+    d["gpu_message_crcs"] = range_crcs;  // upload messages whose CRC came from the GPU
     d["gpu_crc_ms"] = crc_ms;
     d["upload_ms"] = upload_ms;
     d["d2h_copies"] = copies;

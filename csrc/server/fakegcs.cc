@@ -53,6 +53,7 @@ void FakeGcsServer::stop() {
 }
 
 void FakeGcsServer::accept_loop() {
+  name_current_thread("gcsb-srv-accept");
   for (;;) {
     int fd = listener_->accept_fd();
     if (fd < 0) break;
@@ -68,6 +69,7 @@ void FakeGcsServer::accept_loop() {
     ++live_threads_;
     std::thread([this, fd] {
       pin_current_thread(cfg_.cpus);
+      name_current_thread("gcsb-srv-conn");
       try {
         handle_conn(fd);
       } catch (...) {

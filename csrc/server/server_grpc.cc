@@ -270,6 +270,7 @@ class H2ServerConn {
 
   void pool_loop() {
     pin_current_thread(srv_.config().cpus);
+    name_current_thread("gcsb-srv-rpc");
     std::unique_lock<std::mutex> lk(mu_);
     for (;;) {
       ++idle_;

@@ -82,6 +82,13 @@ class ByteSource {
   virtual void seek(uint64_t offset) = 0;
   virtual bool has_crc32c() const { return false; }
   virtual uint32_t crc32c() const { return 0; }
+  // CRC32C of [off, off+len) when the source already holds it (the GPU
+  // source checksums the object in HBM up front, chunk by chunk); false = the
+  // caller computes it from the bytes.
+  virtual bool range_crc32c(uint64_t off, size_t len, uint32_t* crc) {
+    (void)off, (void)len, (void)crc;
+    return false;
+  }
 };
 
 class HostByteSource : public ByteSource {

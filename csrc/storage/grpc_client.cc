@@ -680,7 +680,10 @@ class GrpcStorageClient : public StorageClient {
       do {
         auto [p, k] = src.next(static_cast<size_t>(std::min<uint64_t>(kMsg, total - off)));
         bool last = off + k >= total;
-        uint32_t crc = k ? crc32c(p, k) : 0;
+        // per-message ChecksummedData CRC: precomputed on the GPU for HBM
+        // sources (no host pass over the bytes), else SSE4.2 on the host
+        uint32_t crc = 0;
+        if (k && !src.range_crc32c(off, k, &crc)) crc = crc32c(p, k);
         v2::WriteRequestParts parts = v2::encode_write_request(first ? upload_id : std::string(),
                                                                first ? spec : nullptr, static_cast<int64_t>(off), k,
                                                                k > 0, crc, last ? &object_checksums : nullptr, last);

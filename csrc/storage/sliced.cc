@@ -47,6 +47,7 @@ void SlicedReader::run_slice(int i) {
 
 void SlicedReader::thread_main(int i) {
   pin_current_thread(cfg_.cpus);
+  name_current_thread("gcsb-slice");
   std::unique_lock<std::mutex> lk(mu_);
   for (;;) {
     cv_.wait(lk, [&] { return stop_ || jobs_[i].pending; });
@@ -178,6 +179,7 @@ SlicedWriter::~SlicedWriter() {
 
 void SlicedWriter::thread_main(int i) {
   pin_current_thread(cfg_.cpus);
+  name_current_thread("gcsb-wslice");
   std::unique_lock<std::mutex> lk(mu_);
   for (;;) {
     cv_.wait(lk, [&] { return stop_ || jobs_[i].pending; });

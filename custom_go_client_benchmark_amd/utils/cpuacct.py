@@ -1,0 +1,81 @@
+"""Per-thread CPU accounting of this process, grouped by thread name.
+
+Loopback reads cost CPU at both ends (the client's receive copy into the
+pinned ring and the node-local endpoint's send path run in the same process),
+and the GPU boxes run under a CPU quota (profiles/r1_gpu_box_env.txt), so CPU
+seconds per GiB -- and WHERE they go -- bound throughput.  The native threads
+name themselves (csrc/core/affinity.h name_current_thread):
+
+  gcsb-worker     runner worker (also receives slice 0 of a sliced read)
+  gcsb-slice      sliced-read receive threads (slices 1..n-1)
+  gcsb-wslice     parallel-composite upload part threads
+  gcsb-h2-reader  HTTP/2 connection reader (gRPC receive path)
+  gcsb-submit     per-device slot hand-off thread (GCSB_ASYNC_SUBMIT=1)
+  gcsb-srv-*      synthetic endpoint (connection / RPC handler / accept)
+
+Everything else (HIP runtime threads, Python) is grouped by its own name.
+"""
+from __future__ import annotations
+
+import os
+
+_CLK = os.sysconf("SC_CLK_TCK") if hasattr(os, "sysconf") else 100
+
+GROUPS = (
+    ("client", ("gcsb-worker", "gcsb-slice", "gcsb-wslice", "gcsb-h2-reader")),
+    ("endpoint", ("gcsb-srv",)),
+    ("gpu_submit", ("gcsb-submit",)),
+)
+
+
+def thread_cpu() -> dict[str, float]:
+    """{thread name: user+sys CPU seconds} summed over this process's live
+    threads (threads that already exited are not included)."""
+    out: dict[str, float] = {}
+    base = "/proc/self/task"
+    try:
+        tids = os.listdir(base)
+    except OSError:
+        return out
+    for tid in tids:
+        try:
+            with open(f"{base}/{tid}/stat") as f:
+                s = f.read()
+        except OSError:
+            continue
+        # comm is parenthesised and may contain spaces: split after the last ')'
+        lp, rp = s.find("("), s.rfind(")")
+        if lp < 0 or rp < 0:
+            continue
+        name = s[lp + 1:rp]
+        fields = s[rp + 2:].split()
+        # fields[0] is state (field 3); utime/stime are fields 14/15
+        try:
+            cpu = (int(fields[11]) + int(fields[12])) / _CLK
+        except (IndexError, ValueError):
+            continue
+        out[name] = out.get(name, 0.0) + cpu
+    return out
+
+
+def group_of(name: str) -> str:
+    for g, prefixes in GROUPS:
+        if any(name.startswith(p) for p in prefixes):
+            return g
+    return "other"
+
+
+def delta_by_group(before: dict[str, float], after: dict[str, float]) -> dict[str, float]:
+    """CPU seconds per group between two thread_cpu() snapshots."""
+    out: dict[str, float] = {}
+    for name, v in after.items():
+        d = v - before.get(name, 0.0)
+        if d > 0:
+            g = group_of(name)
+            out[g] = out.get(g, 0.0) + d
+    return out
+
+
+def per_gib(groups: dict[str, float], nbytes: float) -> dict[str, float]:
+    gib = max(nbytes, 1.0) / (1 << 30)
+    return {k: round(v / gib, 4) for k, v in sorted(groups.items())}

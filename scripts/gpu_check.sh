@@ -22,8 +22,8 @@ step() {  # step <name> <timeout> <cmd...>
   return $rc
 }
 
-step build 900 make -j16 all || exit 1
-step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider
+step import 300 python -c "import custom_go_client_benchmark_amd as p; print(p._native.__file__)" || exit 1
+step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py --steps ${BENCH_STEPS:-20} --warmup 3 --json-out $OUT/bench.json
 if [ "${PROFILE:-1}" = "1" ]; then

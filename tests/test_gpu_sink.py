@@ -130,6 +130,10 @@ def test_write_path_hbm_to_server(native, server, gpu_available, proto, resumabl
     m = c.write_from_device(B, name, t.data_ptr(), size, 0, resumable, 4 << 20, 1 << 20, 3)
     assert m["size"] == size and m["crc32c"] == m["gpu_crc32c"] == native.crc32c(native.object_bytes(name, 0, size))
     assert m["d2h_copies"] >= 10
+    if proto == "grpc":
+        # every WriteObject message's ChecksummedData CRC came from the GPU
+        # chunk CRCs (the server rejects a wrong one with DATA_LOSS)
+        assert m["gpu_message_crcs"] == 10
     assert server.object_bytes(B, name, 0, size) == native.object_bytes(name, 0, size)
 
 

@@ -65,6 +65,8 @@ void Runner::reset_stats() {
   host_ms_.clear();
   pending_.clear();
   t_first_ = t_last_ = 0;
+  for (auto& s : sliced_)
+    if (s) s->reset_skew();
 }
 
 void Runner::start() {
@@ -280,6 +282,13 @@ RunSummary Runner::summary() const {
   std::sort(h.begin(), h.end());
   s.host_p50_ms = percentile_floor(h, 50);
   s.host_p99_ms = percentile_floor(h, 99);
+  int nsliced = 0;
+  for (const auto& sr : sliced_)
+    if (sr) {
+      s.slice_skew_ms += sr->mean_skew_ms();
+      ++nsliced;
+    }
+  if (nsliced) s.slice_skew_ms /= nsliced;
   for (const auto& g : gpu_stats_) {
     s.gpu.slots_submitted += g.slots_submitted;
     s.gpu.segments += g.segments;

@@ -80,6 +80,7 @@ struct RunSummary {
   double mb_per_s = 0;   // MiB/s over elapsed
   double avg_ms = 0, p20_ms = 0, p50_ms = 0, p90_ms = 0, p99_ms = 0, min_ms = 0, max_ms = 0;
   double host_p50_ms = 0, host_p99_ms = 0;  // host-landed latency (reference-equivalent stop)
+  double slice_skew_ms = 0;  // sliced reads: mean spread of the slices' host-landed times
   uint64_t oc_buckets[kOcBuckets] = {0};
   std::string first_error;
   GpuSinkStats gpu;

@@ -115,6 +115,16 @@ ReadResult SlicedReader::read(const std::string& bucket, const std::string& obje
   out.sink_begun = true;
   uint32_t crc = 0;
   bool all_verified = true;
+  int64_t first_done = 0, last_done = 0;
+  for (int i = 0; i < n; ++i) {
+    const int64_t d = jobs_[i].rr.host_done_ns;
+    if (d && (!first_done || d < first_done)) first_done = d;
+    if (d > last_done) last_done = d;
+  }
+  if (n > 1 && first_done) {
+    skew_ms_sum_ += (last_done - first_done) / 1e6;
+    ++reads_;
+  }
   for (int i = 0; i < n; ++i) {
     const Job& j = jobs_[i];
     if (!j.error.empty())

@@ -50,6 +50,10 @@ class SlicedReader {
 
   ReadResult read(const std::string& bucket, const std::string& object, const volatile bool* cancel = nullptr);
   int slices() const { return cfg_.slices; }
+  // Load balance of the reads so far: mean over reads of (last slice's
+  // host-landed time - first slice's), i.e. how long the fastest slice idled.
+  double mean_skew_ms() const { return reads_ ? skew_ms_sum_ / static_cast<double>(reads_) : 0.0; }
+  void reset_skew() { skew_ms_sum_ = 0, reads_ = 0; }
   Sink& sink(int i) { return *sinks_[i]; }
   StorageClient& client(int i) { return *clients_[i]; }
 
@@ -77,6 +81,8 @@ class SlicedReader {
   std::mutex mu_;
   std::condition_variable cv_, done_cv_;
   bool stop_ = false;
+  double skew_ms_sum_ = 0;
+  uint64_t reads_ = 0;
 };
 
 }  // namespace gcsb

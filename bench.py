@@ -238,6 +238,7 @@ def main() -> int:
             "p50_ms": round(stats["p50_max"], 3),
             "p99_ms": round(stats["p99_max"], 3),
             "host_landed_p50_ms": round(stats["host_p50_max"], 3),
+            "slice_skew_ms": round(s.get("slice_skew_ms", 0.0), 3),
             "endpoint": "loopback synthetic GCS (one per rank)",
             "affinity": args.affinity,
             "rank0_cpu": cpu,

@@ -12,6 +12,7 @@ from dataclasses import dataclass, field
 from typing import Callable
 
 from .. import _native
+from ..utils import cpuacct
 
 
 @dataclass
@@ -183,6 +184,7 @@ def run_write(opts: RunOptions, nobjects: int, size: int, name_prefix: str = "up
     lat = []
     setup = []
     total = 0
+    th0 = cpuacct.thread_cpu()
     t_all = time.perf_counter()
     for i in range(nobjects):
         gid = opts.worker_id_offset + i
@@ -220,4 +222,5 @@ def run_write(opts: RunOptions, nobjects: int, size: int, name_prefix: str = "up
                "mib_per_s": total / elapsed / 2**20 if elapsed else 0.0, "p50_ms": pct(50), "p99_ms": pct(99),
                "min_ms": s[0] if s else 0.0, "max_ms": s[-1] if s else 0.0, "avg_ms": sum(s) / len(s) if s else 0.0}
     summary["gpu_setup_p50_ms"] = sorted(setup)[len(setup) // 2] if setup else 0.0  # staging ring + GPU CRC32C
+    summary["cpu_s_per_gib_by_thread"] = cpuacct.per_gib(cpuacct.delta_by_group(th0, cpuacct.thread_cpu()), total)
     return WorkloadResult(summary, 0, {"latencies_ms": lat})

@@ -88,6 +88,8 @@ def main() -> int:
     ap.add_argument("--grpc-pool", type=int, default=1)
     ap.add_argument("--slices", type=int, default=8,
                     help="concurrent ranged streams per object read, each on its own connection (1 = one stream)")
+    ap.add_argument("--piece-bytes", default="0",
+                    help="sliced reads: streams pull pieces of this size from a shared cursor (0 = fixed shares)")
     ap.add_argument("--affinity", default="share",
                     help="CPU placement of client/endpoint threads: share|same|split|numa|none (see parallel/affinity.py)")
     ap.add_argument("--single-stream-steps", type=int, default=-1,
@@ -144,6 +146,7 @@ def main() -> int:
         "cpus": placement["client"],
         "retry_initial_s": 0.05,
         "slices": args.slices,
+        "slice_piece_bytes": parse_size(args.piece_bytes),
     }
     run = n.Runner(cfg)
     if args.warmup > 0:

@@ -120,6 +120,7 @@ void Runner::worker_main(int w) {
       SlicedReadConfig sc;
       sc.slices = cfg_.slices;
       sc.min_slice_bytes = cfg_.slice_min_bytes;
+      sc.piece_bytes = cfg_.slice_piece_bytes;
       sc.cpus = cfg_.client.cpus;
       const bool gpu = cfg_.sink == "gpu";
       sc.verify = gpu ? cfg_.gpu.verify : cfg_.host_crc;
@@ -238,7 +239,7 @@ void Runner::worker_main(int w) {
     gpu_stats_[w] = gsink->stats();
   } else if (sliced && cfg_.sink == "gpu") {
     GpuSinkStats t;
-    for (int i = 0; i < sliced->slices(); ++i) {
+    for (int i = 0; i < sliced->num_sinks(); ++i) {
       const GpuSinkStats& g = static_cast<GpuSink&>(sliced->sink(i)).stats();
       t.slots_submitted += g.slots_submitted;
       t.segments += g.segments;

@@ -58,6 +58,9 @@ struct RunnerConfig {
   // landing at their offsets of one HBM buffer; object CRC32C combined.
   int slices = 1;
   uint64_t slice_min_bytes = 8u << 20;
+  // >0: sliced reads pull pieces of this size from a shared cursor (dynamic
+  // load balance across the streams, storage/sliced.h); 0: fixed shares.
+  uint64_t slice_piece_bytes = 0;
   uint64_t seed = 0;
 };
 

@@ -28,7 +28,8 @@ bool should_retry(const RetryPolicy& p, const StorageError& e, int attempt, int6
 }
 
 ReadResult StorageClient::read_object(const std::string& bucket, const std::string& object, Sink& sink,
-                                      int64_t offset, int64_t limit, const volatile bool* cancel, int64_t generation) {
+                                      int64_t offset, int64_t limit, const volatile bool* cancel, int64_t generation,
+                                      bool defer_finish) {
   ReadResult rr;
   rr.pin_generation = generation;
   uint64_t delivered = 0;
@@ -44,7 +45,7 @@ ReadResult StorageClient::read_object(const std::string& bucket, const std::stri
       rr.bytes = delivered;
       rr.host_done_ns = now_ns();
       stats_.bytes_in += delivered;
-      rr.sink = sink.finish();
+      if (!defer_finish) rr.sink = sink.finish();
       return rr;
     } catch (const StorageError& e) {
       const bool begun = rr.sink_begun;

@@ -123,7 +123,8 @@ class StorageClient {
   // Full-object (limit<0) or ranged read into the sink, retried/resumed per
   // the retry policy. `cancel` aborts backoff sleeps.
   ReadResult read_object(const std::string& bucket, const std::string& object, Sink& sink, int64_t offset = 0,
-                         int64_t limit = -1, const volatile bool* cancel = nullptr, int64_t generation = 0);
+                         int64_t limit = -1, const volatile bool* cancel = nullptr, int64_t generation = 0,
+                         bool defer_finish = false);  // caller finishes the sink (overlaps its copy tail)
   ObjectMeta stat_object(const std::string& bucket, const std::string& object);
   // objects.compose / ComposeObject (1..32 sources, same bucket).
   ObjectMeta compose_object(const std::string& bucket, const std::string& dest, const std::vector<std::string>& sources,

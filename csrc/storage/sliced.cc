@@ -15,10 +15,12 @@ SlicedReader::SlicedReader(const ClientConfig& client_cfg, SlicedReadConfig cfg,
   if (cfg_.slices < 1) cfg_.slices = 1;
   ClientConfig cc = client_cfg;
   cc.grpc_conn_pool_size = 1;  // one connection per slice client
+  const int sinks_per_stream = cfg_.piece_bytes ? 2 : 1;
   for (int i = 0; i < cfg_.slices; ++i) {
     clients_.push_back(make_client(cc));
-    sinks_.push_back(make_sink(i));
+    for (int k = 0; k < sinks_per_stream; ++k) sinks_.push_back(make_sink(i * sinks_per_stream + k));
   }
+  stream_done_ns_.assign(cfg_.slices, 0);
   jobs_.resize(cfg_.slices);
   for (int i = 1; i < cfg_.slices; ++i) threads_.emplace_back([this, i] { thread_main(i); });
 }
@@ -32,7 +34,62 @@ SlicedReader::~SlicedReader() {
   for (auto& t : threads_) t.join();
 }
 
+void SlicedReader::finish_piece(Sink& s, Piece& p) {
+  try {
+    p.rr.sink = s.finish();
+  } catch (const std::exception& e) {
+    if (p.error.empty()) p.error = e.what();
+    piece_abort_ = true;
+  }
+}
+
+// Piece mode: pull pieces off the shared cursor until none are left.  The
+// stream alternates between its two sinks and finishes piece k (waits for its
+// last slot copies + CRC kernels) only after piece k+1 has been received, so
+// the copy tail of one piece overlaps the receive of the next.
+void SlicedReader::run_pieces(int i) {
+  const Job& j = jobs_[i];
+  Sink* prev = nullptr;
+  Piece* prev_piece = nullptr;
+  int which = 0;
+  for (;;) {
+    if (piece_abort_.load() || (j.cancel && *j.cancel)) break;
+    const size_t k = next_piece_.fetch_add(1);
+    if (k >= pieces_.size()) break;
+    Piece& p = pieces_[k];
+    Sink& sk = *sinks_[2 * static_cast<size_t>(i) + static_cast<size_t>(which)];
+    which ^= 1;
+    bool ok = false;
+    try {
+      place_(i, sk, p.off, p.len);
+      p.rr = clients_[i]->read_object(j.bucket, j.object, sk, static_cast<int64_t>(p.off),
+                                      static_cast<int64_t>(p.len), j.cancel, j.generation, /*defer_finish=*/true);
+      ok = true;
+    } catch (const StorageError& e) {
+      p.error = e.what();
+      p.retryable = e.retryable();
+    } catch (const std::exception& e) {
+      p.error = e.what();
+    }
+    if (prev) finish_piece(*prev, *prev_piece);
+    prev = nullptr;
+    prev_piece = nullptr;
+    if (!ok) {
+      piece_abort_ = true;
+      break;
+    }
+    prev = &sk;
+    prev_piece = &p;
+  }
+  if (prev) finish_piece(*prev, *prev_piece);
+  stream_done_ns_[static_cast<size_t>(i)] = now_ns();
+}
+
 void SlicedReader::run_slice(int i) {
+  if (!pieces_.empty()) {
+    run_pieces(i);
+    return;
+  }
   Job& j = jobs_[i];
   try {
     j.rr = clients_[i]->read_object(j.bucket, j.object, *sinks_[i], static_cast<int64_t>(j.off),
@@ -69,29 +126,47 @@ ReadResult SlicedReader::read(const std::string& bucket, const std::string& obje
   int n = cfg_.slices;
   if (cfg_.min_slice_bytes) n = static_cast<int>(std::min<uint64_t>(n, std::max<uint64_t>(1, total / cfg_.min_slice_bytes)));
   const uint64_t align = 2u << 20;
-  uint64_t per = (total + n - 1) / std::max(1, n);
-  per = (per + align - 1) / align * align;
+  const bool piece_mode = cfg_.piece_bytes > 0 && n > 1;
   std::vector<std::pair<uint64_t, uint64_t>> ranges;
-  for (uint64_t off = 0; off < total || ranges.empty(); off += per) {
-    ranges.emplace_back(off, std::min(per, total - off));
-    if (total == 0) break;
+  if (piece_mode) {
+    const uint64_t pb = std::max<uint64_t>(align, (cfg_.piece_bytes + align - 1) / align * align);
+    pieces_.clear();
+    for (uint64_t off = 0; off < total; off += pb) {
+      Piece p;
+      p.off = off;
+      p.len = std::min(pb, total - off);
+      pieces_.push_back(std::move(p));
+    }
+    n = static_cast<int>(std::min<size_t>(static_cast<size_t>(n), pieces_.size()));
+    next_piece_ = 0;
+    piece_abort_ = false;
+    std::fill(stream_done_ns_.begin(), stream_done_ns_.end(), 0);
+  } else {
+    uint64_t per = (total + n - 1) / std::max(1, n);
+    per = (per + align - 1) / align * align;
+    for (uint64_t off = 0; off < total || ranges.empty(); off += per) {
+      ranges.emplace_back(off, std::min(per, total - off));
+      if (total == 0) break;
+    }
+    n = static_cast<int>(ranges.size());
   }
-  n = static_cast<int>(ranges.size());
   {
     std::lock_guard<std::mutex> lk(mu_);
     for (int i = 0; i < n; ++i) {
       Job& j = jobs_[i];
       j.bucket = bucket;
       j.object = object;
-      j.off = ranges[i].first;
-      j.len = ranges[i].second;
       j.cancel = cancel;
       j.generation = m.generation;  // every slice reads the stat's object version
       j.rr = ReadResult();
       j.error.clear();
       j.retryable = false;
       j.done = false;
-      place_(i, *sinks_[i], j.off, j.len);
+      if (!piece_mode) {
+        j.off = ranges[i].first;
+        j.len = ranges[i].second;
+        place_(i, *sinks_[i], j.off, j.len);
+      }
       j.pending = i > 0;
     }
   }
@@ -115,9 +190,11 @@ ReadResult SlicedReader::read(const std::string& bucket, const std::string& obje
   out.sink_begun = true;
   uint32_t crc = 0;
   bool all_verified = true;
+  // parts in object order: the pieces (piece mode) or the slices
+  std::vector<Piece> parts;
   int64_t first_done = 0, last_done = 0;
   for (int i = 0; i < n; ++i) {
-    const int64_t d = jobs_[i].rr.host_done_ns;
+    const int64_t d = piece_mode ? stream_done_ns_[static_cast<size_t>(i)] : jobs_[i].rr.host_done_ns;
     if (d && (!first_done || d < first_done)) first_done = d;
     if (d > last_done) last_done = d;
   }
@@ -125,24 +202,39 @@ ReadResult SlicedReader::read(const std::string& bucket, const std::string& obje
     skew_ms_sum_ += (last_done - first_done) / 1e6;
     ++reads_;
   }
-  for (int i = 0; i < n; ++i) {
-    const Job& j = jobs_[i];
-    if (!j.error.empty())
-      throw StorageError("slice " + std::to_string(i) + " [" + std::to_string(j.off) + ", +" + std::to_string(j.len) +
-                             "): " + j.error,
-                         j.retryable);
-    out.bytes += j.rr.bytes;
-    out.attempts = std::max(out.attempts, j.rr.attempts);
-    if (j.rr.first_byte_ns && (!out.first_byte_ns || j.rr.first_byte_ns < out.first_byte_ns))
-      out.first_byte_ns = j.rr.first_byte_ns;
-    out.host_done_ns = std::max(out.host_done_ns, j.rr.host_done_ns);
-    out.sink.landed_ns = std::max(out.sink.landed_ns, j.rr.sink.landed_ns);
-    if (j.rr.sink.crc_mismatch && !out.sink.crc_mismatch) {
-      out.sink.crc_mismatch = true;
-      out.sink.detail = "slice " + std::to_string(i) + ": " + j.rr.sink.detail;
+  if (piece_mode) {
+    parts.swap(pieces_);  // pieces_ empty again: run_slice() is in static mode unless a read sets it
+  } else {
+    parts.resize(static_cast<size_t>(n));
+    for (int i = 0; i < n; ++i) {
+      Piece& p = parts[static_cast<size_t>(i)];
+      p.off = jobs_[i].off;
+      p.len = jobs_[i].len;
+      p.rr = jobs_[i].rr;
+      p.error = jobs_[i].error;
+      p.retryable = jobs_[i].retryable;
     }
-    all_verified = all_verified && j.rr.sink.verified;
-    crc = crc32c_combine(crc, j.rr.sink.computed_crc32c, j.rr.bytes);
+  }
+  const char* what = piece_mode ? "piece " : "slice ";
+  for (size_t i = 0; i < parts.size(); ++i) {
+    const Piece& p = parts[i];
+    if (!p.error.empty())
+      throw StorageError(what + std::to_string(i) + " [" + std::to_string(p.off) + ", +" + std::to_string(p.len) +
+                             "): " + p.error,
+                         p.retryable);
+    if (p.rr.bytes != p.len) break;  // not read (cancelled): the byte count check below reports it
+    out.bytes += p.rr.bytes;
+    out.attempts = std::max(out.attempts, p.rr.attempts);
+    if (p.rr.first_byte_ns && (!out.first_byte_ns || p.rr.first_byte_ns < out.first_byte_ns))
+      out.first_byte_ns = p.rr.first_byte_ns;
+    out.host_done_ns = std::max(out.host_done_ns, p.rr.host_done_ns);
+    out.sink.landed_ns = std::max(out.sink.landed_ns, p.rr.sink.landed_ns);
+    if (p.rr.sink.crc_mismatch && !out.sink.crc_mismatch) {
+      out.sink.crc_mismatch = true;
+      out.sink.detail = what + std::to_string(i) + ": " + p.rr.sink.detail;
+    }
+    all_verified = all_verified && p.rr.sink.verified;
+    crc = crc32c_combine(crc, p.rr.sink.computed_crc32c, p.rr.bytes);
   }
   out.sink.bytes = out.bytes;
   out.sink.computed_crc32c = crc;

@@ -12,6 +12,7 @@
 // verified end to end exactly like a single-stream read.  The timed region is
 // unchanged (request -> every byte landed + verified).
 #pragma once
+#include <atomic>
 #include <condition_variable>
 #include <functional>
 #include <memory>
@@ -30,6 +31,12 @@ struct SlicedReadConfig {
   uint64_t min_slice_bytes = 8u << 20;  // smaller objects use fewer slices (1 = plain read)
   std::vector<int> cpus;                // pin the slice threads
   bool verify = true;                   // sinks compute CRCs: check the combined object CRC32C
+  // 0: each stream reads one fixed 1/slices share of the object.  >0: the
+  // object is cut into pieces of this size (2 MiB multiples) that the streams
+  // pull from a shared counter (dynamic load balance: a stream on a slow core
+  // takes fewer pieces).  Each stream alternates between two sinks, so one
+  // piece's last H2D copies overlap the receive of the next.
+  uint64_t piece_bytes = 0;
 };
 
 class SlicedReader {
@@ -54,6 +61,7 @@ class SlicedReader {
   // host-landed time - first slice's), i.e. how long the fastest slice idled.
   double mean_skew_ms() const { return reads_ ? skew_ms_sum_ / static_cast<double>(reads_) : 0.0; }
   void reset_skew() { skew_ms_sum_ = 0, reads_ = 0; }
+  int num_sinks() const { return static_cast<int>(sinks_.size()); }
   Sink& sink(int i) { return *sinks_[i]; }
   StorageClient& client(int i) { return *clients_[i]; }
 
@@ -68,10 +76,23 @@ class SlicedReader {
     std::string error;
     bool retryable = false;
   };
+  struct Piece {
+    uint64_t off = 0, len = 0;
+    ReadResult rr;
+    std::string error;
+    bool retryable = false;
+  };
   void thread_main(int i);
   void run_slice(int i);
+  void run_pieces(int i);
+  void finish_piece(Sink& s, Piece& p);
 
   SlicedReadConfig cfg_;
+  // piece mode, per read: pieces_ and the shared cursor
+  std::vector<Piece> pieces_;
+  std::atomic<size_t> next_piece_{0};
+  std::atomic<bool> piece_abort_{false};
+  std::vector<int64_t> stream_done_ns_;
   Prepare prepare_;
   Place place_;
   std::vector<std::unique_ptr<StorageClient>> clients_;

@@ -151,13 +151,15 @@ def test_cli_gpu_sink(native, gpu_available):
 
 
 @pytest.mark.parametrize("proto", ["http", "grpc"])
-@pytest.mark.parametrize("slices", [2, 4])
-def test_sliced_read_lands_byte_exact_in_hbm(native, server, gpu_available, proto, slices):
+@pytest.mark.parametrize("slices,piece", [(2, 0), (4, 0), (4, 4 << 20), (3, 6 << 20)])
+def test_sliced_read_lands_byte_exact_in_hbm(native, server, gpu_available, proto, slices, piece):
+    """piece > 0: dynamic pieces pulled by the streams, two GPU sinks per
+    stream (one piece's copy tail overlapping the next piece's receive)."""
     size = (40 << 20) + 4097
     server.add_synthetic(B, P, "", 0, 1, size)
     r = native.Runner({"protocol": proto, "endpoint": server.url, "bucket": B, "object_prefix": P, "workers": 1,
                        "reads_per_worker": 2, "sink": "gpu", "slices": slices, "ring_slot_bytes": 4 << 20,
-                       "ring_slots": 4, "keep_records": False})
+                       "ring_slots": 4, "keep_records": False, "slice_piece_bytes": piece})
     r.start()
     r.wait()
     s = r.summary()

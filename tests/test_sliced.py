@@ -61,6 +61,39 @@ def test_sliced_read_resumes_a_dropped_slice(native, server, proto):
     assert recs[0]["attempts"] >= 2
 
 
+@pytest.mark.parametrize("proto", ["http", "grpc"])
+@pytest.mark.parametrize("piece_mib", [2, 4])
+def test_piece_mode_balances_and_verifies(native, server, proto, piece_mib):
+    """slice_piece_bytes > 0: the streams pull 2 MiB-aligned pieces from a
+    shared cursor (one ranged request per piece, two sinks per stream); the
+    object CRC32C is the in-order combine of the piece CRCs."""
+    size = (24 << 20) + 12345
+    server.add_synthetic(B, P, "", 0, 1, size)
+    s, recs = _run(native, server, proto, 4, slice_piece_bytes=piece_mib << 20)
+    assert s["errors"] == 0, s["first_error"]
+    assert s["reads"] == 2 and s["verified"] == 2 and s["bytes"] == 2 * size
+    assert all(r["bytes"] == size and r["verified"] for r in recs)
+    pieces = -(-size // (piece_mib << 20))
+    st = server.stats()
+    calls = st["grpc_calls"] if proto == "grpc" else st["http_requests"]
+    assert calls == 2 * (pieces + 1)  # one ranged request per piece (+1 stat) per read
+    assert s["slice_skew_ms"] >= 0.0
+
+
+@pytest.mark.parametrize("proto", ["http", "grpc"])
+def test_piece_mode_detects_corruption_and_resumes(native, server, proto):
+    size = 16 << 20
+    server.add_synthetic(B, P, "", 0, 1, size)
+    server.set_faults({"corrupt_at": (13 << 20) + 7, "corrupt_count": 1})
+    s, _ = _run(native, server, proto, 4, reads=1, slice_piece_bytes=2 << 20)
+    assert s["errors"] == 1
+    assert "mismatch" in s["first_error"] or "bad CRC" in s["first_error"]
+    server.set_faults({"disconnect_at": (9 << 20) + 100, "disconnect_count": 1})
+    s, recs = _run(native, server, proto, 4, reads=1, slice_piece_bytes=2 << 20)
+    assert s["errors"] == 0, s["first_error"]
+    assert s["verified"] == 1 and s["retries"] >= 1
+
+
 def test_sliced_discard_without_host_crc_is_unverified(native, server):
     server.add_synthetic(B, P, "", 0, 1, 16 << 20)
     s, _ = _run(native, server, "http", 4, host_crc=False)

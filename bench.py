@@ -88,8 +88,9 @@ def main() -> int:
     ap.add_argument("--grpc-pool", type=int, default=1)
     ap.add_argument("--slices", type=int, default=8,
                     help="concurrent ranged streams per object read, each on its own connection (1 = one stream)")
-    ap.add_argument("--piece-bytes", default="0",
-                    help="sliced reads: streams pull pieces of this size from a shared cursor (0 = fixed shares)")
+    ap.add_argument("--piece-bytes", default="8MiB",
+                    help="sliced reads: streams pull pieces of this size from a shared cursor (0 = fixed shares; "
+                         "8 MiB measured best: profiles/r1_pieces)")
     ap.add_argument("--affinity", default="share",
                     help="CPU placement of client/endpoint threads: share|same|split|numa|none (see parallel/affinity.py)")
     ap.add_argument("--single-stream-steps", type=int, default=-1,

@@ -57,6 +57,7 @@ class RunOptions:
     keep_records: bool = True
     slices: int = 1                        # >1: sliced (parallel ranged) reads, see csrc/storage/sliced.h
     slice_min_bytes: int = 8 << 20
+    slice_piece_bytes: int = 8 << 20       # sliced reads: dynamic pieces (0 = fixed shares)
 
     def client_dict(self) -> dict:
         return {
@@ -80,6 +81,7 @@ class RunOptions:
             "landing": self.landing, "gpu_verify": self.gpu_verify, "latency_fd": self.latency_fd,
             "trace_sample_rate": self.trace_sample_rate, "stop_on_error": self.stop_on_error,
             "keep_records": self.keep_records, "slices": self.slices, "slice_min_bytes": self.slice_min_bytes,
+            "slice_piece_bytes": self.slice_piece_bytes,
         })
         if self.object_names:
             d["object_names"] = list(self.object_names)

@@ -133,6 +133,11 @@ def main(argv: list[str] | None = None) -> int:
     aff = fs.get("affinity")
     if aff == "auto":
         aff = ("share" if fs.get("slices") > 1 else "same") if sink == "gpu" else "none"
+        if fs.get("workload") == "write":
+            # uploads: unpinned threads measured fastest on MI355X (64 MiB
+            # WriteObject 8.1 ms vs 13.8-14.4 ms pinned; resumable HTTP 6.5 vs
+            # 6.7-7.8 ms), profiles/r1_session4/
+            aff = "none"
     if aff != "none" and sink == "gpu":
         from .parallel import affinity
 

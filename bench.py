@@ -237,6 +237,7 @@ def main() -> int:
                 "sink": args.sink,
                 "ring": f"{args.slots}x{args.slot_bytes}",
                 "streams_per_read": args.slices,
+                "piece_bytes": parse_size(args.piece_bytes),
             },
             "per_gpu_mib_s": round(value / world, 2),
             "p50_ms": round(stats["p50_max"], 3),

@@ -91,13 +91,15 @@ int main(int argc, char** argv) {
       check(rr.sink.crc_mismatch, std::string(proto) + " corruption detected");
     }
     srv.faults().corrupt_count = 0;
-    // 3) sliced reads from two threads at once
+    // 3) sliced reads from two threads at once: fixed shares (t=0) and
+    //    dynamic 2 MiB pieces pulled from the shared cursor (t=1)
     std::vector<std::thread> th;
     for (int t = 0; t < 2; ++t)
-      th.emplace_back([&] {
+      th.emplace_back([&, t] {
         SlicedReadConfig c;
         c.slices = 4;
         c.min_slice_bytes = 1 << 20;
+        c.piece_bytes = t == 1 ? (2u << 20) : 0;
         SlicedReader sr(
             client_cfg(proto, srv.url()), c, [](int) { return std::make_unique<DiscardSink>(256 << 10, true); },
             [](uint64_t) {}, [](int, Sink&, uint64_t, uint64_t) {});

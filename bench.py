@@ -91,6 +91,9 @@ def main() -> int:
     ap.add_argument("--piece-bytes", default="8MiB",
                     help="sliced reads: streams pull pieces of this size from a shared cursor (0 = fixed shares; "
                          "8 MiB measured best: profiles/r1_pieces)")
+    ap.add_argument("--piece-min-bytes", default="0",
+                    help="sliced reads: taper the piece size toward the end of the object down to this "
+                         "(guided self-scheduling, storage/sliced.h; 0 = fixed-size pieces)")
     ap.add_argument("--affinity", default="share",
                     help="CPU placement of client/endpoint threads: share|same|split|numa|none (see parallel/affinity.py)")
     ap.add_argument("--single-stream-steps", type=int, default=-1,
@@ -148,6 +151,7 @@ def main() -> int:
         "retry_initial_s": 0.05,
         "slices": args.slices,
         "slice_piece_bytes": parse_size(args.piece_bytes),
+        "slice_piece_min_bytes": parse_size(args.piece_min_bytes),
     }
     run = n.Runner(cfg)
     if args.warmup > 0:
@@ -238,6 +242,7 @@ def main() -> int:
                 "ring": f"{args.slots}x{args.slot_bytes}",
                 "streams_per_read": args.slices,
                 "piece_bytes": parse_size(args.piece_bytes),
+                "piece_min_bytes": parse_size(args.piece_min_bytes),
             },
             "per_gpu_mib_s": round(value / world, 2),
             "p50_ms": round(stats["p50_max"], 3),

@@ -121,6 +121,7 @@ void Runner::worker_main(int w) {
       sc.slices = cfg_.slices;
       sc.min_slice_bytes = cfg_.slice_min_bytes;
       sc.piece_bytes = cfg_.slice_piece_bytes;
+      sc.piece_min_bytes = cfg_.slice_piece_min_bytes;
       sc.cpus = cfg_.client.cpus;
       const bool gpu = cfg_.sink == "gpu";
       sc.verify = gpu ? cfg_.gpu.verify : cfg_.host_crc;

@@ -61,6 +61,7 @@ struct RunnerConfig {
   // >0: sliced reads pull pieces of this size from a shared cursor (dynamic
   // load balance across the streams, storage/sliced.h); 0: fixed shares.
   uint64_t slice_piece_bytes = 0;
+  uint64_t slice_piece_min_bytes = 0;  // >0: tapered pieces down to this (storage/sliced.h)
   uint64_t seed = 0;
 };
 

@@ -209,6 +209,7 @@ struct PySlicedGpuReader {
     sc.slices = get_or<int>(d, "slices", 8);
     sc.min_slice_bytes = get_or<uint64_t>(d, "slice_min_bytes", 8u << 20);
     sc.piece_bytes = get_or<uint64_t>(d, "slice_piece_bytes", 0);
+    sc.piece_min_bytes = get_or<uint64_t>(d, "slice_piece_min_bytes", 0);
     sc.cpus = cc.cpus;
     sc.verify = g.verify;
     reader = std::make_unique<SlicedReader>(
@@ -433,6 +434,7 @@ class PyRunner {
     c.slices = get_or<int>(d, "slices", 1);
     c.slice_min_bytes = get_or<uint64_t>(d, "slice_min_bytes", 8u << 20);
     c.slice_piece_bytes = get_or<uint64_t>(d, "slice_piece_bytes", 0);
+    c.slice_piece_min_bytes = get_or<uint64_t>(d, "slice_piece_min_bytes", 0);
     c.seed = get_or<uint64_t>(d, "seed", 0);
     runner_ = std::make_unique<Runner>(std::move(c));
   }

@@ -130,11 +130,19 @@ ReadResult SlicedReader::read(const std::string& bucket, const std::string& obje
   std::vector<std::pair<uint64_t, uint64_t>> ranges;
   if (piece_mode) {
     const uint64_t pb = std::max<uint64_t>(align, (cfg_.piece_bytes + align - 1) / align * align);
+    const uint64_t streams = static_cast<uint64_t>(std::max(1, n));
+    const uint64_t floor_b = cfg_.piece_min_bytes ? std::max<uint64_t>(align, cfg_.piece_min_bytes / align * align) : pb;
     pieces_.clear();
-    for (uint64_t off = 0; off < total; off += pb) {
+    for (uint64_t off = 0; off < total;) {
+      uint64_t len = pb;
+      if (cfg_.piece_min_bytes) {
+        const uint64_t guided = ((total - off) / (2 * streams) + align - 1) / align * align;
+        len = std::max(std::min(pb, guided), std::min(floor_b, pb));
+      }
       Piece p;
       p.off = off;
-      p.len = std::min(pb, total - off);
+      p.len = std::min(len, total - off);
+      off += p.len;
       pieces_.push_back(std::move(p));
     }
     n = static_cast<int>(std::min<size_t>(static_cast<size_t>(n), pieces_.size()));

@@ -37,6 +37,12 @@ struct SlicedReadConfig {
   // takes fewer pieces).  Each stream alternates between two sinks, so one
   // piece's last H2D copies overlap the receive of the next.
   uint64_t piece_bytes = 0;
+  // >0: taper the piece size toward the end of the object (guided
+  // self-scheduling): each piece is min(piece_bytes, remaining / (2 * streams))
+  // rounded up to 2 MiB, but at least this.  The last pieces are small, so the
+  // streams finish together instead of one stream still receiving a whole
+  // piece while the others idle (the `slice_skew_ms` tail).
+  uint64_t piece_min_bytes = 0;
 };
 
 class SlicedReader {

@@ -71,6 +71,8 @@ def build_flags() -> FlagSet:
     fs.int("slice-min-bytes", 8 << 20, "Smallest slice; smaller objects use fewer slices")
     fs.int("slice-piece-bytes", 8 << 20, "Sliced reads: streams pull pieces of this size from a shared cursor "
            "(dynamic load balance; 0 = one fixed share per stream)")
+    fs.int("slice-piece-min-bytes", 0, "Sliced reads: taper pieces toward the end of the object down to this "
+           "(guided self-scheduling; 0 = fixed-size pieces)")
     fs.bool("host-crc", True, "discard sink: verify CRC32C on the host (what the Go library does)")
     fs.duration("duration", 0.0, "Stop after this long (0 = only -read-call-per-worker)")
     fs.string("latency-file", "", "Write per-read latency lines here instead of stdout")
@@ -181,6 +183,7 @@ def main(argv: list[str] | None = None) -> int:
         ring_slot_bytes=fs.get("ring-slot-bytes"), ring_slots=fs.get("ring-slots"), landing=fs.get("landing"),
         gpu_verify=fs.get("gpu-verify"), latency_fd=latency_fd, slices=fs.get("slices"),
         slice_min_bytes=fs.get("slice-min-bytes"), slice_piece_bytes=fs.get("slice-piece-bytes"),
+        slice_piece_min_bytes=fs.get("slice-piece-min-bytes"),
         trace_sample_rate=fs.get("trace-sample-rate") if fs.get("enable-tracing") else 0.0,
         cpus=placement["client"], auth=fs.get("auth"), token=fs.get("token"), key_file=fs.get("key-file"),
         token_uri=fs.get("token-uri"), user_agent=fs.get("user-agent"), tls_ca_file=fs.get("tls-ca-file"),

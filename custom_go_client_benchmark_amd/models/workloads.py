@@ -58,6 +58,7 @@ class RunOptions:
     slices: int = 1                        # >1: sliced (parallel ranged) reads, see csrc/storage/sliced.h
     slice_min_bytes: int = 8 << 20
     slice_piece_bytes: int = 8 << 20       # sliced reads: dynamic pieces (0 = fixed shares)
+    slice_piece_min_bytes: int = 0         # >0: taper pieces toward the end down to this
 
     def client_dict(self) -> dict:
         return {
@@ -82,6 +83,7 @@ class RunOptions:
             "trace_sample_rate": self.trace_sample_rate, "stop_on_error": self.stop_on_error,
             "keep_records": self.keep_records, "slices": self.slices, "slice_min_bytes": self.slice_min_bytes,
             "slice_piece_bytes": self.slice_piece_bytes,
+            "slice_piece_min_bytes": self.slice_piece_min_bytes,
         })
         if self.object_names:
             d["object_names"] = list(self.object_names)

@@ -151,15 +151,18 @@ def test_cli_gpu_sink(native, gpu_available):
 
 
 @pytest.mark.parametrize("proto", ["http", "grpc"])
-@pytest.mark.parametrize("slices,piece", [(2, 0), (4, 0), (4, 4 << 20), (3, 6 << 20)])
-def test_sliced_read_lands_byte_exact_in_hbm(native, server, gpu_available, proto, slices, piece):
+@pytest.mark.parametrize("slices,piece,taper", [(2, 0, 0), (4, 0, 0), (4, 4 << 20, 0), (3, 6 << 20, 0),
+                                                (4, 8 << 20, 2 << 20)])
+def test_sliced_read_lands_byte_exact_in_hbm(native, server, gpu_available, proto, slices, piece, taper):
     """piece > 0: dynamic pieces pulled by the streams, two GPU sinks per
-    stream (one piece's copy tail overlapping the next piece's receive)."""
+    stream (one piece's copy tail overlapping the next piece's receive).
+    taper > 0: guided schedule, pieces shrink toward the end of the object."""
     size = (40 << 20) + 4097
     server.add_synthetic(B, P, "", 0, 1, size)
     r = native.Runner({"protocol": proto, "endpoint": server.url, "bucket": B, "object_prefix": P, "workers": 1,
                        "reads_per_worker": 2, "sink": "gpu", "slices": slices, "ring_slot_bytes": 4 << 20,
-                       "ring_slots": 4, "keep_records": False, "slice_piece_bytes": piece})
+                       "ring_slots": 4, "keep_records": False, "slice_piece_bytes": piece,
+                       "slice_piece_min_bytes": taper})
     r.start()
     r.wait()
     s = r.summary()

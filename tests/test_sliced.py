@@ -80,6 +80,35 @@ def test_piece_mode_balances_and_verifies(native, server, proto, piece_mib):
     assert s["slice_skew_ms"] >= 0.0
 
 
+def _tapered_pieces(size, piece, floor, streams, align=2 << 20):
+    """Python model of SlicedReader::read's guided piece schedule."""
+    out, off = [], 0
+    while off < size:
+        guided = -(-((size - off) // (2 * streams)) // align) * align
+        n = min(max(min(piece, guided), min(max(align, floor // align * align), piece)), size - off)
+        out.append(n)
+        off += n
+    return out
+
+
+@pytest.mark.parametrize("proto", ["http", "grpc"])
+def test_piece_mode_tapers_toward_the_end(native, server, proto):
+    """slice_piece_min_bytes > 0: pieces shrink toward the end of the object
+    (min(piece, remaining / 2 streams), 2 MiB aligned, floor 2 MiB) so the
+    streams finish together; the object still verifies byte-exact."""
+    size = (40 << 20) + 777
+    server.add_synthetic(B, P, "", 0, 1, size)
+    s, recs = _run(native, server, proto, 4, slice_piece_bytes=8 << 20, slice_piece_min_bytes=2 << 20)
+    assert s["errors"] == 0, s["first_error"]
+    assert s["reads"] == 2 and s["verified"] == 2 and s["bytes"] == 2 * size
+    plan = _tapered_pieces(size, 8 << 20, 2 << 20, 4)
+    assert sum(plan) == size and plan[0] > plan[-2] == 2 << 20
+    assert plan == sorted(plan, reverse=True)
+    st = server.stats()
+    calls = st["grpc_calls"] if proto == "grpc" else st["http_requests"]
+    assert calls == 2 * (len(plan) + 1)  # one ranged request per piece (+1 stat) per read
+
+
 @pytest.mark.parametrize("proto", ["http", "grpc"])
 def test_piece_mode_detects_corruption_and_resumes(native, server, proto):
     size = 16 << 20

@@ -13,7 +13,9 @@ by default (--slices 8: stat, then 8 concurrent ranged streams on their own
 connections landing at their offsets in HBM, object CRC32C = combine of the
 slice CRCs, checked against the stored CRC32C); a single-stream read (the
 reference's one NewReader per object) is measured right after on the same
-endpoint and reported as `single_stream_*`.  W untimed warmup reads,
+endpoint and reported as `single_stream_*`, and the other transport (HTTP
+when the headline is gRPC) on the same sliced config as `compare`; both run
+after the timed region.  W untimed warmup reads,
 then K timed reads bracketed by an RCCL barrier + torch.cuda.synchronize();
 the elapsed time is the MAX over ranks and `value` is total bytes / that time.
 
@@ -98,6 +100,9 @@ def main() -> int:
                     help="CPU placement of client/endpoint threads: share|same|split|numa|none (see parallel/affinity.py)")
     ap.add_argument("--single-stream-steps", type=int, default=-1,
                     help="timed single-stream reads measured after the main run for comparison (-1: = --steps, 0: skip)")
+    ap.add_argument("--compare-steps", type=int, default=-1,
+                    help="timed reads over the other transport (HTTP vs gRPC) on the same config, reported "
+                         "as `compare` (-1: = --steps, 0: skip)")
     ap.add_argument("--json-out", default="")
     args = ap.parse_args()
 
@@ -181,34 +186,39 @@ def main() -> int:
     cpu["cpu_s_per_gib_by_thread"] = cpuacct.per_gib(cpuacct.delta_by_group(th0, cpuacct.thread_cpu()),
                                                      float(s["bytes"]))
 
+    def side_run(overrides: dict, steps: int, what: str):
+        """One untimed read, then `steps` timed reads of a variant config;
+        every rank joins (the reductions below are collective)."""
+        r1 = n.Runner({**cfg, **overrides, "reads_per_worker": 1})
+        r1.start()
+        r1.wait()
+        r1.reset_stats()
+        r1.set_reads_per_worker(steps)
+        gdist.barrier(ctx, f"R1/R2 {what} barrier")
+        t1 = time.perf_counter()
+        r1.start()
+        r1.wait()
+        gdist.barrier(ctx, f"R1/R2 {what} barrier")
+        e1 = time.perf_counter() - t1
+        s1 = r1.summary()
+        del r1
+        return gdist.reduce_stats(ctx, elapsed=e1, nbytes=float(s1["bytes"]), p50=s1["p50_ms"], p99=s1["p99_ms"],
+                                  ok=1.0 if s1["errors"] == 0 else 0.0)
+
     # single-stream comparison (slices=1: the reference's one stream per read)
     ss_steps = args.steps if args.single_stream_steps < 0 else args.single_stream_steps
-    ss = None
-    if args.slices > 1 and ss_steps > 0:
-        run1 = n.Runner({**cfg, "slices": 1, "reads_per_worker": 1})
-        run1.start()
-        run1.wait()
-        run1.reset_stats()
-        run1.set_reads_per_worker(ss_steps)
-        gdist.barrier(ctx, "R1/R2 single-stream barrier")
-        t1 = time.perf_counter()
-        run1.start()
-        run1.wait()
-        gdist.barrier(ctx, "R1/R2 single-stream barrier")
-        ss_elapsed = time.perf_counter() - t1
-        s1 = run1.summary()
-        ss = {"elapsed": ss_elapsed, "bytes": float(s1["bytes"]), "p50": s1["p50_ms"], "p99": s1["p99_ms"],
-              "ok": 1.0 if s1["errors"] == 0 else 0.0}
-        del run1
+    ss_stats = side_run({"slices": 1}, ss_steps, "single-stream") if args.slices > 1 and ss_steps > 0 else None
+    # the other transport on the same config (the metric is HTTP vs gRPC)
+    other = {"grpc": "http", "http": "grpc"}.get(protocol)
+    cmp_steps = args.steps if args.compare_steps < 0 else args.compare_steps
+    cmp_stats = None
+    if other and cmp_steps > 0 and other in hbm.available_protocols():
+        cmp_stats = side_run({"protocol": other}, cmp_steps, f"{other} comparison")
     srv.stop()
 
     ok = 1.0 if s["errors"] == 0 and s["reads"] == args.steps * args.workers else 0.0
     stats = gdist.reduce_stats(ctx, elapsed=elapsed, nbytes=float(s["bytes"]), ok=ok, p50=s["p50_ms"],
                                p99=s["p99_ms"], host_p50=s["host_p50_ms"])
-    ss_stats = None
-    if ss is not None:
-        ss_stats = gdist.reduce_stats(ctx, elapsed=ss["elapsed"], nbytes=ss["bytes"], p50=ss["p50"], p99=ss["p99"],
-                                      ok=ss["ok"])
     if rank == 0:
         if stats["ok_min"] < 1.0:
             print(f"benchmark failed: {s['first_error'] or 'incomplete reads'}", file=sys.stderr)
@@ -257,6 +267,10 @@ def main() -> int:
             out["single_stream_mib_s"] = round(ss_stats["nbytes_sum"] / ss_stats["elapsed_max"] / (1 << 20), 2)
             out["single_stream_p50_ms"] = round(ss_stats["p50_max"], 3)
             out["single_stream_p99_ms"] = round(ss_stats["p99_max"], 3)
+        if cmp_stats is not None:
+            out["compare"] = {"protocol": other, "ok": cmp_stats["ok_min"] >= 1.0,
+                              "mib_s": round(cmp_stats["nbytes_sum"] / cmp_stats["elapsed_max"] / (1 << 20), 2),
+                              "p50_ms": round(cmp_stats["p50_max"], 3), "p99_ms": round(cmp_stats["p99_max"], 3)}
         line = json.dumps(out)
         print(line, flush=True)
         if args.json_out:

@@ -40,6 +40,9 @@ def test_bench_two_ranks_gloo():
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["steps"] == 3 and out["config"]["global_batch"] == 2
     assert out["value"] > 0 and out["scaling"] == "weak" and out["config"]["parallelism"] == "dp2"
+    # the other transport on the same config, reduced over both ranks
+    other = {"grpc": "http", "http": "grpc"}[out["config"]["protocol"]]
+    assert out["compare"]["protocol"] == other and out["compare"]["ok"] and out["compare"]["mib_s"] > 0
 
 
 def test_cli_two_ranks_offsets_and_node_view(tmp_path):

@@ -100,6 +100,10 @@ def main() -> int:
                     help="CPU placement of client/endpoint threads: share|same|split|numa|none (see parallel/affinity.py)")
     ap.add_argument("--single-stream-steps", type=int, default=-1,
                     help="timed single-stream reads measured after the main run for comparison (-1: = --steps, 0: skip)")
+    ap.add_argument("--event-wait", default="block", choices=["spin", "block"],
+                    help="how GPU sinks wait on slot events: block (interrupt, the library default) or spin. "
+                         "Spin won 5 of 6 interleaved pairs but not on the mean, with one bad p99 "
+                         "(profiles/r1_session12, r1_session13)")
     ap.add_argument("--compare-steps", type=int, default=-1,
                     help="timed reads over the other transport (HTTP vs gRPC) on the same config, reported "
                          "as `compare` (-1: = --steps, 0: skip)")
@@ -157,6 +161,7 @@ def main() -> int:
         "slices": args.slices,
         "slice_piece_bytes": parse_size(args.piece_bytes),
         "slice_piece_min_bytes": parse_size(args.piece_min_bytes),
+        "blocking_sync": args.event_wait == "block",
     }
     run = n.Runner(cfg)
     if args.warmup > 0:
@@ -253,6 +258,7 @@ def main() -> int:
                 "streams_per_read": args.slices,
                 "piece_bytes": parse_size(args.piece_bytes),
                 "piece_min_bytes": parse_size(args.piece_min_bytes),
+                "event_wait": args.event_wait,
             },
             "per_gpu_mib_s": round(value / world, 2),
             "p50_ms": round(stats["p50_max"], 3),

@@ -3,30 +3,39 @@
 endpoint into MI355X HBM, one reader process per GPU.
 
 Metric (BASELINE.json): p50/p99 read latency (ms) + MB/s per GPU, HTTP vs gRPC
-at 1/2/4/8 MI355X.  Config: 256 MiB objects, gRPC ReadObject stream (HTTP with
---protocol http), bytes land in HBM through the pinned ring + hipMemcpyAsync
-and every ChecksummedData CRC32C is verified by the CDNA4 kernels.
+at 1/2/4/8 MI355X.  Config 2/4: 256 MiB objects, gRPC ReadObject, ONE stream
+per object read (the reference's one NewReader + io.CopyBuffer per read,
+/root/reference/main.go:134-140); bytes land in HBM through the pinned ring +
+hipMemcpyAsync and every ChecksummedData CRC32C and the object CRC32C are
+verified by the CDNA4 kernels.  One rank per GPU; rank r reads file_<r>, so
+per-GPU work is fixed as N grows (weak scaling, the reference's worker fan-out
+/root/reference/main.go:200-210 spread over GPUs).
 
-One step = every rank's reader reads its own 256 MiB object (file_<rank>) once,
-so per-GPU work is fixed as N grows (weak scaling).  Each read is a sliced read
-by default (--slices 8: stat, then 8 concurrent ranged streams on their own
-connections landing at their offsets in HBM, object CRC32C = combine of the
-slice CRCs, checked against the stored CRC32C); a single-stream read (the
-reference's one NewReader per object) is measured right after on the same
-endpoint and reported as `single_stream_*`, and the other transport (HTTP
-when the headline is gRPC) on the same sliced config as `compare`; both run
-after the timed region.  W untimed warmup reads,
-then K timed reads bracketed by an RCCL barrier + torch.cuda.synchronize();
-the elapsed time is the MAX over ranks and `value` is total bytes / that time.
+Timed region: W untimed warm-up reads, then K reads bracketed by an RCCL
+barrier + torch.cuda.synchronize() on both sides; `value` = all ranks' bytes /
+the slowest rank's elapsed time (MiB/s for the whole job).
 
-    python bench.py --gpus 1 --steps 20 --warmup 3
-    torchrun --nproc-per-node 8 bench.py --gpus 8 ...
+After the timed region, as labelled side blocks (same endpoint, every rank):
+  compare  the other transport (HTTP vs gRPC) on the headline config;
+  sliced   extension, not parity: each read split into N ranged streams on
+           their own connections pulling 8 MiB pieces (csrc/storage/sliced.h);
+  write    config 5: 64 MiB object in HBM -> D2H into the pinned ring ->
+           resumable upload (gRPC StartResumableWrite + WriteObject), GPU CRC.
+
+Launch:
+  python bench.py --gpus 1                         one rank on cuda:0
+  python bench.py --gpus 8                         spawns 8 rank processes itself
+  torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8
+`--workload write` makes config 5 the headline instead.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import signal
+import socket
+import subprocess
 import sys
 import time
 
@@ -65,22 +74,27 @@ def cpu_snapshot() -> dict:
     return snap
 
 
-def cpu_delta(a: dict, b: dict, nbytes: float) -> dict:
+def cpu_delta(a: dict, b: dict, nbytes: float, elapsed: float) -> dict:
     gib = max(nbytes, 1.0) / (1 << 30)
-    out = {"process_cpu_s_per_gib": round((b["user_s"] + b["sys_s"] - a["user_s"] - a["sys_s"]) / gib, 4),
-           "process_sys_fraction": round((b["sys_s"] - a["sys_s"]) /
-                                         max(1e-9, b["user_s"] + b["sys_s"] - a["user_s"] - a["sys_s"]), 3)}
+    cpu_s = b["user_s"] + b["sys_s"] - a["user_s"] - a["sys_s"]
+    out = {"process_cpu_s_per_gib": round(cpu_s / gib, 4),
+           "process_sys_fraction": round((b["sys_s"] - a["sys_s"]) / max(1e-9, cpu_s), 3),
+           # CPUs this rank kept busy during the timed region (client + its endpoint)
+           "cpus_busy": round(cpu_s / max(elapsed, 1e-9), 2)}
     for k in ("nr_periods", "nr_throttled", "throttled_usec"):
         if k in a and k in b:
             out["cgroup_" + k] = b[k] - a[k]
     return out
 
 
-def main() -> int:
+def build_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs = rank processes (one per GPU). Without torchrun env, N>1 spawns the ranks itself")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="read", choices=["read", "write"],
+                    help="read: configs 2/4 (headline); write: config 5 as the headline")
     ap.add_argument("--protocol", default="auto", help="grpc | http | auto (grpc when built)")
     ap.add_argument("--object-size", default="256MiB")
     ap.add_argument("--workers", type=int, default=1, help="readers per GPU (config: 1)")
@@ -88,53 +102,115 @@ def main() -> int:
     ap.add_argument("--slot-bytes", default="4MiB")
     ap.add_argument("--slots", type=int, default=4)
     ap.add_argument("--grpc-pool", type=int, default=1)
-    ap.add_argument("--slices", type=int, default=8,
-                    help="concurrent ranged streams per object read, each on its own connection (1 = one stream)")
+    ap.add_argument("--slices", type=int, default=1,
+                    help="streams per object read in the HEADLINE run (1 = the reference's sequential read)")
+    ap.add_argument("--sliced-streams", type=int, default=8,
+                    help="streams per read in the `sliced` extension block (0 = skip the block)")
     ap.add_argument("--piece-bytes", default="8MiB",
-                    help="sliced reads: streams pull pieces of this size from a shared cursor (0 = fixed shares; "
-                         "8 MiB measured best: profiles/r1_pieces)")
+                    help="sliced reads: streams pull pieces of this size from a shared cursor (0 = fixed shares)")
     ap.add_argument("--piece-min-bytes", default="0",
-                    help="sliced reads: taper the piece size toward the end of the object down to this "
-                         "(guided self-scheduling, storage/sliced.h; 0 = fixed-size pieces)")
+                    help="sliced reads: taper the piece size toward the end of the object down to this")
     ap.add_argument("--affinity", default="share",
-                    help="CPU placement of client/endpoint threads: share|same|split|numa|none (see parallel/affinity.py)")
-    ap.add_argument("--single-stream-steps", type=int, default=-1,
-                    help="timed single-stream reads measured after the main run for comparison (-1: = --steps, 0: skip)")
+                    help="CPU placement of client/endpoint threads: share|same|split|numa|none (parallel/affinity.py)")
     ap.add_argument("--event-wait", default="block", choices=["spin", "block"],
-                    help="how GPU sinks wait on slot events: block (interrupt, the library default) or spin. "
-                         "Spin won 5 of 6 interleaved pairs but not on the mean, with one bad p99 "
-                         "(profiles/r1_session12, r1_session13)")
-    ap.add_argument("--compare-steps", type=int, default=-1,
-                    help="timed reads over the other transport (HTTP vs gRPC) on the same config, reported "
-                         "as `compare` (-1: = --steps, 0: skip)")
+                    help="how GPU sinks wait on slot events: block (interrupt) or spin")
+    ap.add_argument("--side-steps", type=int, default=-1,
+                    help="timed reads/uploads per side block (compare / sliced / write); -1: = --steps, 0: skip all")
+    ap.add_argument("--write-size", default="64MiB", help="config 5 object size")
+    ap.add_argument("--write-chunk", default="16MiB", help="resumable upload chunk (HTTP) / message batch")
     ap.add_argument("--json-out", default="")
-    args = ap.parse_args()
+    return ap
 
+
+# ---------------------------------------------------------------------------
+# launcher: one process per GPU
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n: int, argv: list[str]) -> int:
+    """Spawns n rank processes (torchrun-style env) running this script and
+    waits for them.  The parent never imports torch or touches HIP, so no
+    process that initialised the GPU ever starts another program.  If a rank
+    fails, the others are terminated (their exact PIDs) and the worst exit
+    status is returned."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    live = set(range(n))
+    try:
+        while live:
+            for r in sorted(live):
+                c = procs[r].poll()
+                if c is None:
+                    continue
+                live.discard(r)
+                if c != 0:
+                    print(f"bench: rank {r} exited with status {c}; stopping the other ranks", file=sys.stderr)
+                    rc = rc or (c if c > 0 else 1)
+                    for q in live:
+                        procs[q].send_signal(signal.SIGTERM)
+            time.sleep(0.05)
+    except KeyboardInterrupt:
+        for q in live:
+            procs[q].send_signal(signal.SIGTERM)
+        for q in live:
+            procs[q].wait()
+        return 130
+    return rc
+
+
+# ---------------------------------------------------------------------------
+# one rank
+
+
+def run_rank(args) -> int:
     import torch
-    import torch.distributed as dist
 
     import custom_go_client_benchmark_amd as pkg
     from custom_go_client_benchmark_amd.ops import hbm
+    from custom_go_client_benchmark_amd.parallel import affinity
     from custom_go_client_benchmark_amd.parallel import dist as gdist
     from custom_go_client_benchmark_amd.utils import cpuacct
 
     n = pkg._native
     rank, world, local_rank = gdist.env_rank()
-    ctx = gdist.init(local_rank=local_rank, world=world, rank=rank)
+    if args.gpus != world:
+        print(f"bench: --gpus {args.gpus} but the launcher started {world} rank(s) (WORLD_SIZE); "
+              f"they must match", file=sys.stderr)
+        return 2
     use_gpu = args.sink == "gpu"
+    rehearsal = os.environ.get("GCSB_DIST_BACKEND") == "gloo"
     if use_gpu:
         hbm.gpu_required()
+        ndev = torch.cuda.device_count()
+        if world > ndev and not rehearsal:
+            print(f"bench: {world} ranks but only {ndev} visible GPU(s); one rank per GPU "
+                  f"(set GCSB_DIST_BACKEND=gloo for a shared-GPU rehearsal)", file=sys.stderr)
+            return 2
+    # process group even at world 1: RCCL init + barriers + reductions run in every GPU bench
+    ctx = gdist.init(local_rank=local_rank, world=world, rank=rank, always_pg=use_gpu)
     protocol = args.protocol
     if protocol == "auto":
         protocol = "grpc" if "grpc" in hbm.available_protocols() else "http"
     size = parse_size(args.object_size)
+    side_steps = args.steps if args.side_steps < 0 else args.side_steps
 
-    # Node-local synthetic GCS endpoint for this rank (no network on the box).
-    from custom_go_client_benchmark_amd.parallel import affinity
-
+    # node-local synthetic GCS endpoint for this rank (no network on the box)
     gpu = ctx.gpu if ctx.gpu >= 0 else 0
     placement = affinity.plan(gpu, args.affinity) if use_gpu else {"client": [], "server": []}
-    srv = n.Server({"port": 0, "md5": False, "cpus": placement["server"]})
+    srv = n.Server({"port": 0, "md5": False, "cpus": placement["server"], "retain_uploads": False})
     srv.start()
     bucket = "princer-working-dirs"
     prefix = "princer_100M_files/file_"
@@ -163,127 +239,244 @@ def main() -> int:
         "slice_piece_min_bytes": parse_size(args.piece_min_bytes),
         "blocking_sync": args.event_wait == "block",
     }
-    run = n.Runner(cfg)
-    if args.warmup > 0:
-        run.start()
-        run.wait()
-        s = run.summary()
+
+    def sync():
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+
+    def read_ok(s: dict, steps: int) -> tuple[bool, str]:
+        reads = steps * args.workers
         if s["errors"]:
-            print(f"[rank {rank}] warmup failed: {s['first_error']}", file=sys.stderr)
-            return 1
-    run.reset_stats()
-    run.set_reads_per_worker(args.steps)
+            return False, s["first_error"] or "read error"
+        if s["reads"] != reads:
+            return False, f"{s['reads']} of {reads} reads completed"
+        # every read must have had its checksums verified (GPU CRC or host CRC)
+        if (use_gpu or cfg.get("host_crc", True)) and s["verified"] != reads:
+            return False, f"only {s['verified']} of {reads} reads had their CRC32C verified"
+        return True, ""
 
-    gdist.barrier(ctx, "R1/R2 bench barrier")
-    if torch.cuda.is_available():
-        torch.cuda.synchronize()
-    c0 = cpu_snapshot()
-    th0 = cpuacct.thread_cpu()
-    t0 = time.perf_counter()
-    run.start()
-    run.wait()
-    if torch.cuda.is_available():
-        torch.cuda.synchronize()
-    gdist.barrier(ctx, "R1/R2 bench barrier")
-    elapsed = time.perf_counter() - t0
-    s = run.summary()
-    cpu = cpu_delta(c0, cpu_snapshot(), float(s["bytes"]))
-    cpu["cpu_s_per_gib_by_thread"] = cpuacct.per_gib(cpuacct.delta_by_group(th0, cpuacct.thread_cpu()),
-                                                     float(s["bytes"]))
-
-    def side_run(overrides: dict, steps: int, what: str):
-        """One untimed read, then `steps` timed reads of a variant config;
-        every rank joins (the reductions below are collective)."""
-        r1 = n.Runner({**cfg, **overrides, "reads_per_worker": 1})
-        r1.start()
-        r1.wait()
-        r1.reset_stats()
-        r1.set_reads_per_worker(steps)
-        gdist.barrier(ctx, f"R1/R2 {what} barrier")
+    def read_block(overrides: dict, steps: int, warmup: int, what: str) -> dict:
+        """warm-up reads, then `steps` timed reads of a config variant between
+        two barriers.  Every rank makes every collective call whatever happens
+        locally, so one rank's failure cannot strand the others in a barrier."""
+        err = ""
+        r1 = s1 = None
+        c0 = th0 = None
+        try:
+            r1 = n.Runner({**cfg, **overrides, "reads_per_worker": warmup})
+            if warmup > 0:
+                r1.start()
+                r1.wait()
+                sw = r1.summary()
+                if sw["errors"]:
+                    err = f"warmup: {sw['first_error']}"
+            r1.reset_stats()
+            r1.set_reads_per_worker(steps)
+        except Exception as e:  # noqa: BLE001 - reported in the block, collectives still run
+            err = err or f"{type(e).__name__}: {e}"
+        gdist.barrier(ctx, f"R1 {what} start barrier")
+        sync()
         t1 = time.perf_counter()
-        r1.start()
-        r1.wait()
-        gdist.barrier(ctx, f"R1/R2 {what} barrier")
+        if not err:
+            c0, th0 = cpu_snapshot(), cpuacct.thread_cpu()
+            t1 = time.perf_counter()
+            r1.start()
+            r1.wait()
+        sync()
+        gdist.barrier(ctx, f"R2 {what} stop barrier")
         e1 = time.perf_counter() - t1
-        s1 = r1.summary()
+        cpu = {}
+        if not err:
+            s1 = r1.summary()
+            ok, why = read_ok(s1, steps)
+            if not ok:
+                err = why
+            cpu = cpu_delta(c0, cpu_snapshot(), float(s1["bytes"]), e1)
+            cpu["cpu_s_per_gib_by_thread"] = cpuacct.per_gib(
+                cpuacct.delta_by_group(th0, cpuacct.thread_cpu()), float(s1["bytes"]))
+        s1 = s1 or {"bytes": 0, "p50_ms": 0.0, "p99_ms": 0.0, "host_p50_ms": 0.0, "slice_skew_ms": 0.0,
+                    "verified": 0, "reads": 0}
         del r1
-        return gdist.reduce_stats(ctx, elapsed=e1, nbytes=float(s1["bytes"]), p50=s1["p50_ms"], p99=s1["p99_ms"],
-                                  ok=1.0 if s1["errors"] == 0 else 0.0)
+        st = gdist.reduce_stats(ctx, elapsed=e1, nbytes=float(s1["bytes"]), p50=s1["p50_ms"], p99=s1["p99_ms"],
+                                host_p50=s1["host_p50_ms"], skew=s1.get("slice_skew_ms", 0.0),
+                                verified=float(s1["verified"]), ok=0.0 if err else 1.0)
+        st["error"] = err
+        st["cpu"] = cpu
+        return st
 
-    # single-stream comparison (slices=1: the reference's one stream per read)
-    ss_steps = args.steps if args.single_stream_steps < 0 else args.single_stream_steps
-    ss_stats = side_run({"slices": 1}, ss_steps, "single-stream") if args.slices > 1 and ss_steps > 0 else None
-    # the other transport on the same config (the metric is HTTP vs gRPC)
+    def write_block(steps: int, warmup: int) -> dict:
+        """Config 5: each rank uploads a 64 MiB object from HBM `steps` times
+        (HBM -> pinned ring D2H on a side stream -> resumable upload; the
+        object CRC32C is computed on the GPU and checked by the endpoint)."""
+        err = ""
+        lat = []
+        wsize = parse_size(args.write_size)
+        chunk = parse_size(args.write_chunk)
+        client = buf = None
+        try:
+            client = n.Client({"protocol": protocol, "endpoint": srv.url, "retry_initial_s": 0.05,
+                               "cpus": placement["client"]})
+            buf = torch.empty(wsize, dtype=torch.uint8, device=f"cuda:{gpu}")
+            n.gpu_fill_pattern(gpu, buf.data_ptr(), wsize, f"upload/rank{rank}", 0)
+            for i in range(warmup):
+                client.write_from_device(bucket, f"upload/warmup_{rank}_{i}", buf.data_ptr(), wsize, gpu, True,
+                                         chunk, parse_size(args.slot_bytes), args.slots)
+        except Exception as e:  # noqa: BLE001
+            err = f"{type(e).__name__}: {e}"
+        gdist.barrier(ctx, "R1 write start barrier")
+        sync()
+        t1 = time.perf_counter()
+        nbytes = 0
+        if not err:
+            try:
+                for i in range(steps):
+                    t0 = time.perf_counter()
+                    m = client.write_from_device(bucket, f"upload/rank{rank}_{i}", buf.data_ptr(), wsize, gpu,
+                                                 True, chunk, parse_size(args.slot_bytes), args.slots)
+                    lat.append((time.perf_counter() - t0) * 1e3)
+                    if m["size"] != wsize or m["crc32c"] != m["gpu_crc32c"]:
+                        err = f"upload {i} not confirmed: {m}"
+                        break
+                    nbytes += wsize
+            except Exception as e:  # noqa: BLE001
+                err = f"{type(e).__name__}: {e}"
+        sync()
+        gdist.barrier(ctx, "R2 write stop barrier")
+        e1 = time.perf_counter() - t1
+        s = sorted(lat)
+        p50 = s[len(s) * 50 // 100] if s else 0.0
+        p99 = s[min(len(s) - 1, len(s) * 99 // 100)] if s else 0.0
+        st = gdist.reduce_stats(ctx, elapsed=e1, nbytes=float(nbytes), p50=p50, p99=p99, ok=0.0 if err else 1.0)
+        st["error"] = err
+        return st
+
+    def mib_s(st: dict) -> float:
+        return st["nbytes_sum"] / max(st["elapsed_max"], 1e-12) / (1 << 20)
+
+    def block_json(st: dict, **extra) -> dict:
+        d = {"ok": st["ok_min"] >= 1.0, "mib_s": round(mib_s(st), 2), "p50_ms": round(st["p50_max"], 3),
+             "p99_ms": round(st["p99_max"], 3)}
+        d.update(extra)
+        if st.get("error"):
+            d["error"] = st["error"][:300]
+        return d
+
+    # ---- headline --------------------------------------------------------
+    if args.workload == "read":
+        head = read_block({}, args.steps, args.warmup, "headline")
+        headline_model = (f"{protocol} ReadObject {args.object_size} object, "
+                          f"{'one stream per read' if args.slices == 1 else f'{args.slices} ranged streams'}"
+                          + (" -> HBM (CRC32C on GPU)" if use_gpu else " -> discard (CPU baseline)"))
+    else:
+        if not use_gpu:
+            print("bench: --workload write needs --sink gpu (uploads are staged from HBM)", file=sys.stderr)
+            return 2
+        head = write_block(args.steps, args.warmup)
+        headline_model = f"{protocol} resumable upload {args.write_size} object from HBM (D2H -> pinned -> upload)"
+
+    # ---- side blocks (after the timed region) ----------------------------
     other = {"grpc": "http", "http": "grpc"}.get(protocol)
-    cmp_steps = args.steps if args.compare_steps < 0 else args.compare_steps
-    cmp_stats = None
-    if other and cmp_steps > 0 and other in hbm.available_protocols():
-        cmp_stats = side_run({"protocol": other}, cmp_steps, f"{other} comparison")
+    blocks = {}
+    if side_steps > 0 and args.workload == "read":
+        if other and other in hbm.available_protocols():
+            blocks["compare"] = ("compare", read_block({"protocol": other}, side_steps, 1, f"{other} compare"),
+                                 {"protocol": other})
+        if args.sliced_streams > 1 and args.slices == 1:
+            blocks["sliced"] = ("sliced", read_block({"slices": args.sliced_streams}, side_steps, 1, "sliced"),
+                                {"streams_per_read": args.sliced_streams,
+                                 "piece_bytes": parse_size(args.piece_bytes), "note": "extension, not parity"})
+        if use_gpu:
+            blocks["write"] = ("write", write_block(side_steps, 1),
+                               {"protocol": protocol, "object_bytes": parse_size(args.write_size),
+                                "config": "BASELINE config 5"})
+    elif side_steps > 0 and other and other in hbm.available_protocols():
+        pass  # write headline: no read side blocks
     srv.stop()
 
-    ok = 1.0 if s["errors"] == 0 and s["reads"] == args.steps * args.workers else 0.0
-    stats = gdist.reduce_stats(ctx, elapsed=elapsed, nbytes=float(s["bytes"]), ok=ok, p50=s["p50_ms"],
-                               p99=s["p99_ms"], host_p50=s["host_p50_ms"])
+    # R4: which HIP device each rank used -> distinct GPUs in the job
+    devs = gdist.gather_floats(ctx, [float(ctx.gpu if use_gpu else -1)])
+    distinct = sorted({int(d[0]) for d in devs if d[0] >= 0})
+    n_gpus = len(distinct) if use_gpu else world
+
+    rc = 0
     if rank == 0:
-        if stats["ok_min"] < 1.0:
-            print(f"benchmark failed: {s['first_error'] or 'incomplete reads'}", file=sys.stderr)
-            return 1
-        total = stats["nbytes_sum"]
-        tmax = stats["elapsed_max"]
-        value = total / tmax / (1 << 20)
-        out = {
-            "metric": METRIC,
-            "value": round(value, 2),
-            "unit": "MiB/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(tmax / args.steps * 1000.0, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "uint8",
-            "data": "synthetic",
-            "config": {
-                "model": f"{protocol} ReadObject {args.object_size} object -> HBM (CRC32C on GPU)"
-                if use_gpu else f"{protocol} read {args.object_size} -> discard (CPU baseline)",
-                "global_batch": world * args.workers,
-                "seq_len": size,
-                "parallelism": f"dp{world}",
-                "protocol": protocol,
-                "object_bytes": size,
-                "readers_per_gpu": args.workers,
-                "sink": args.sink,
-                "ring": f"{args.slots}x{args.slot_bytes}",
-                "streams_per_read": args.slices,
-                "piece_bytes": parse_size(args.piece_bytes),
-                "piece_min_bytes": parse_size(args.piece_min_bytes),
-                "event_wait": args.event_wait,
-            },
-            "per_gpu_mib_s": round(value / world, 2),
-            "p50_ms": round(stats["p50_max"], 3),
-            "p99_ms": round(stats["p99_max"], 3),
-            "host_landed_p50_ms": round(stats["host_p50_max"], 3),
-            "slice_skew_ms": round(s.get("slice_skew_ms", 0.0), 3),
-            "endpoint": "loopback synthetic GCS (one per rank)",
-            "affinity": args.affinity,
-            "rank0_cpu": cpu,
-        }
-        if ss_stats is not None:
-            out["single_stream_mib_s"] = round(ss_stats["nbytes_sum"] / ss_stats["elapsed_max"] / (1 << 20), 2)
-            out["single_stream_p50_ms"] = round(ss_stats["p50_max"], 3)
-            out["single_stream_p99_ms"] = round(ss_stats["p99_max"], 3)
-        if cmp_stats is not None:
-            out["compare"] = {"protocol": other, "ok": cmp_stats["ok_min"] >= 1.0,
-                              "mib_s": round(cmp_stats["nbytes_sum"] / cmp_stats["elapsed_max"] / (1 << 20), 2),
-                              "p50_ms": round(cmp_stats["p50_max"], 3), "p99_ms": round(cmp_stats["p99_max"], 3)}
-        line = json.dumps(out)
-        print(line, flush=True)
-        if args.json_out:
-            with open(args.json_out, "w") as f:
-                f.write(line + "\n")
+        if head["ok_min"] < 1.0:
+            print(f"benchmark failed: {head['error'] or 'a rank failed'}", file=sys.stderr)
+            rc = 1
+        else:
+            value = mib_s(head)
+            tmax = head["elapsed_max"]
+            out = {
+                "metric": METRIC,
+                "value": round(value, 2),
+                "unit": "MiB/s",
+                "n_gpus": n_gpus,
+                "steps": args.steps,
+                "warmup": args.warmup,
+                "ms_per_step": round(tmax / args.steps * 1000.0, 3),
+                "higher_is_better": True,
+                "scaling": "weak",
+                "vs_baseline": None,
+                "dtype": "uint8",
+                "data": "synthetic",
+                "config": {
+                    "model": headline_model,
+                    "global_batch": world * args.workers,
+                    "seq_len": size if args.workload == "read" else parse_size(args.write_size),
+                    "parallelism": f"dp{world}",
+                    "workload": args.workload,
+                    "protocol": protocol,
+                    "object_bytes": size if args.workload == "read" else parse_size(args.write_size),
+                    "readers_per_gpu": args.workers,
+                    "sink": args.sink,
+                    "ring": f"{args.slots}x{args.slot_bytes}",
+                    "streams_per_read": args.slices if args.workload == "read" else 1,
+                    "event_wait": args.event_wait,
+                },
+                "ranks": world,
+                "devices": distinct if use_gpu else "none (cpu rehearsal)",
+                "per_gpu_mib_s": round(value / max(1, n_gpus), 2),
+                "p50_ms": round(head["p50_max"], 3),
+                "p99_ms": round(head["p99_max"], 3),
+                "per_rank_mib_s": [round(b / max(e, 1e-12) / (1 << 20), 1)
+                                   for b, e in zip(head["nbytes_per_rank"], head["elapsed_per_rank"])],
+                "endpoint": "loopback synthetic GCS (one per rank)",
+                "affinity": args.affinity,
+            }
+            if args.workload == "read":
+                out["host_landed_p50_ms"] = round(head["host_p50_max"], 3)
+                out["verified_reads"] = int(head["verified_sum"])
+                out["rank0_cpu"] = head["cpu"]
+                if head["cpu"]:
+                    gib_s = value / max(1, world) / 1024.0
+                    out["cpus_needed_per_gpu"] = round(head["cpu"]["process_cpu_s_per_gib"] * gib_s, 2)
+            for key, (_, st, extra) in blocks.items():
+                b = block_json(st, **extra)
+                if key == "sliced":
+                    b["host_landed_p50_ms"] = round(st["host_p50_max"], 3)
+                    b["slice_skew_ms"] = round(st["skew_max"], 3)
+                    if st.get("cpu"):
+                        b["process_cpu_s_per_gib"] = st["cpu"]["process_cpu_s_per_gib"]
+                out[key] = b
+            line = json.dumps(out)
+            print(line, flush=True)
+            if args.json_out:
+                with open(args.json_out, "w") as f:
+                    f.write(line + "\n")
+    elif head["ok_min"] < 1.0:
+        rc = 1
     gdist.shutdown(ctx)
-    return 0
+    return rc
+
+
+def main() -> int:
+    args = build_parser().parse_args()
+    if args.gpus < 1:
+        print("bench: --gpus must be >= 1", file=sys.stderr)
+        return 2
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args.gpus, sys.argv[1:])
+    return run_rank(args)
 
 
 if __name__ == "__main__":

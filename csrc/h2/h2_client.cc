@@ -198,7 +198,10 @@ void H2ClientConn::reader_loop() {
           uint32_t n = fh.length;
           uint8_t pad = 0;
           if (fh.flags & h2::kFlagPadded) {
+            // RFC 7540 6.1: padding >= payload length is a PROTOCOL_ERROR
+            if (n < 1) throw StorageError("http2: padded DATA frame without a pad length", false);
             pad = bc_->read_byte();
+            if (static_cast<uint32_t>(pad) + 1 > n) throw StorageError("http2: DATA padding exceeds frame", false);
             n -= 1 + pad;
           }
           auto s = find(fh.stream);
@@ -225,11 +228,14 @@ void H2ClientConn::reader_loop() {
             hend_stream = fh.flags & h2::kFlagEndStream;
             hblock.clear();
             if (fh.flags & h2::kFlagPadded) {
+              if (frag.empty()) throw StorageError("http2: padded HEADERS frame without a pad length", false);
               uint8_t pad = static_cast<uint8_t>(frag[0]);
               b = 1;
+              if (static_cast<size_t>(pad) + 1 > e) throw StorageError("http2: HEADERS padding exceeds frame", false);
               e -= pad;
             }
             if (fh.flags & h2::kFlagPriority) b += 5;
+            if (b > e) throw StorageError("http2: HEADERS frame too short", false);
           }
           hblock.append(frag, b, e - b);
           if (fh.flags & h2::kFlagEndHeaders) {
@@ -240,6 +246,7 @@ void H2ClientConn::reader_loop() {
           break;
         }
         case h2::kRstStream: {
+          if (fh.length != 4) throw StorageError("http2: RST_STREAM length != 4", false);
           uint8_t v[4];
           bc_->read_exact(v, 4);
           if (auto s = find(fh.stream)) s->on_reset(be32(v));
@@ -258,12 +265,14 @@ void H2ClientConn::reader_loop() {
           break;
         }
         case h2::kPing: {
+          if (fh.length != 8) throw StorageError("http2: PING length != 8", false);
           uint8_t op[8];
           bc_->read_exact(op, 8);
           if (!(fh.flags & h2::kFlagAck)) w_->write_ping_ack(op);
           break;
         }
         case h2::kGoaway: {
+          if (fh.length < 8) throw StorageError("http2: GOAWAY shorter than 8 bytes", false);
           std::string p(fh.length, '\0');
           bc_->read_exact(&p[0], fh.length);
           goaway_last_ = be32(reinterpret_cast<const uint8_t*>(p.data())) & 0x7FFFFFFF;
@@ -284,6 +293,7 @@ void H2ClientConn::reader_loop() {
           break;
         }
         case h2::kWindowUpdate: {
+          if (fh.length != 4) throw StorageError("http2: WINDOW_UPDATE length != 4", false);
           uint8_t v[4];
           bc_->read_exact(v, 4);
           w_->on_window_update(fh.stream, be32(v) & 0x7FFFFFFF);

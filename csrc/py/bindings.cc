@@ -585,6 +585,7 @@ class PyServer {
     if (d.contains("corrupt_count")) f.corrupt_count = d["corrupt_count"].cast<int>();
     if (d.contains("throttle_bps")) f.throttle_bps = d["throttle_bps"].cast<int64_t>();
     if (d.contains("latency_ms")) f.latency_ms = d["latency_ms"].cast<int>();
+    if (d.contains("drop_trailers_count")) f.drop_trailers_count = d["drop_trailers_count"].cast<int>();
   }
   py::dict stats() {
     auto& s = srv_->stats();

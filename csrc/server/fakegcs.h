@@ -27,6 +27,7 @@ struct FaultConfig {
   std::atomic<int> corrupt_count{0};        // ...in this many responses
   std::atomic<int64_t> throttle_bps{0};     // per-response rate cap (bytes/s), 0 = none
   std::atomic<int> latency_ms{0};           // added time-to-first-byte
+  std::atomic<int> drop_trailers_count{0};  // gRPC: cut the connection after the last DATA, before trailers
 };
 
 struct ServerConfig {

@@ -118,10 +118,13 @@ class H2ServerConn {
               hend = fh.flags & h2::kFlagEndStream;
               hblock.clear();
               if (fh.flags & h2::kFlagPadded) {
+                // RFC 7540 6.2: padding >= payload is a connection PROTOCOL_ERROR
+                if (frag.empty() || static_cast<size_t>(static_cast<uint8_t>(frag[0])) + 1 > e) return;
                 b = 1;
                 e -= static_cast<uint8_t>(frag[0]);
               }
               if (fh.flags & h2::kFlagPriority) b += 5;
+              if (b > e) return;
             }
             hblock.append(frag, b, e - b);
             if (fh.flags & h2::kFlagEndHeaders) on_headers(hstream, hblock, hend);
@@ -131,7 +134,9 @@ class H2ServerConn {
             uint32_t n = fh.length;
             uint8_t pad = 0;
             if (fh.flags & h2::kFlagPadded) {
+              if (n < 1) return;
               pad = bc_.read_byte();
+              if (static_cast<uint32_t>(pad) + 1 > n) return;
               n -= 1 + pad;
             }
             auto s = find(fh.stream);
@@ -154,6 +159,7 @@ class H2ServerConn {
             break;
           }
           case h2::kRstStream: {
+            if (fh.length != 4) return;
             uint8_t v[4];
             bc_.read_exact(v, 4);
             if (auto s = find(fh.stream)) s->cancelled = true;
@@ -172,12 +178,14 @@ class H2ServerConn {
             break;
           }
           case h2::kPing: {
+            if (fh.length != 8) return;
             uint8_t op[8];
             bc_.read_exact(op, 8);
             if (!(fh.flags & h2::kFlagAck)) w_.write_ping_ack(op);
             break;
           }
           case h2::kWindowUpdate: {
+            if (fh.length != 4) return;
             uint8_t v[4];
             bc_.read_exact(v, 4);
             w_.on_window_update(fh.stream, be32(v) & 0x7FFFFFFF);
@@ -502,6 +510,12 @@ class H2ServerConn {
       }
     } while (off < end);
     srv_.stats().bytes_sent += sent;
+    if (f.drop_trailers_count.load() > 0 && f.drop_trailers_count.fetch_sub(1) > 0) {
+      // every requested byte is out, the status never comes (reset / GOAWAY race)
+      ++srv_.stats().faults_injected;
+      ::shutdown(bc_.conn().fd(), SHUT_RDWR);
+      throw Cancelled{};
+    }
     send_trailers(s.id, kOk, "", true);
   }
 

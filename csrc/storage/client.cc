@@ -40,7 +40,14 @@ ReadResult StorageClient::read_object(const std::string& bucket, const std::stri
     ++stats_.requests;
     try {
       int64_t lim = limit < 0 ? -1 : limit - static_cast<int64_t>(delivered);
-      read_attempt(bucket, object, sink, offset + static_cast<int64_t>(delivered), lim, !rr.sink_begun, &rr,
+      // A retry after the stream broke with every requested byte already
+      // delivered (reset / GOAWAY before the trailers) has nothing left to
+      // fetch: re-asking would send read_limit=0 ("to the end") over gRPC or
+      // an empty Range over HTTP.  The read is complete.
+      const bool nothing_left = rr.sink_begun && ((limit >= 0 && lim <= 0) ||
+          (limit < 0 && rr.info.size >= 0 && offset + static_cast<int64_t>(delivered) >= rr.info.size));
+      if (!nothing_left)
+        read_attempt(bucket, object, sink, offset + static_cast<int64_t>(delivered), lim, !rr.sink_begun, &rr,
                    &delivered);
       rr.bytes = delivered;
       rr.host_done_ns = now_ns();

@@ -233,8 +233,12 @@ class GrpcCall : public H2ClientStream {
 // Streaming ReadObjectResponse parser -> Sink.
 class ReadObjectHandler : public MessageHandler {
  public:
-  ReadObjectHandler(Sink& sink, ReadResult* rr, uint64_t* delivered, bool full_read, GrpcCall** call)
-      : sink_(sink), rr_(rr), delivered_(delivered), full_read_(full_read), call_(call) {}
+  // cap: the most bytes *delivered may reach in this read (ranged reads);
+  // a server sending past read_limit is a protocol error, never written into
+  // the sink (a piece sink's neighbour in HBM belongs to another stream).
+  ReadObjectHandler(Sink& sink, ReadResult* rr, uint64_t* delivered, bool full_read, GrpcCall** call,
+                    uint64_t cap = ~0ull)
+      : sink_(sink), rr_(rr), delivered_(delivered), full_read_(full_read), call_(call), cap_(cap) {}
 
   void begin(uint32_t len) override {
     msg_left_ = len;
@@ -251,6 +255,7 @@ class ReadObjectHandler : public MessageHandler {
     while (n > 0) {
       if (st_ == kContent) {
         uint64_t k = std::min<uint64_t>(n, content_left_);
+        if (*delivered_ + k > cap_) throw StorageError("ReadObject: server sent more than read_limit bytes", false);
         while (k > 0) {
           Window w;
           if (!sink_failed_) {
@@ -477,6 +482,7 @@ class ReadObjectHandler : public MessageHandler {
   uint64_t* delivered_;
   bool full_read_;
   GrpcCall** call_;
+  uint64_t cap_ = ~0ull;
   St st_ = kTopTag;
   uint64_t msg_left_ = 0, cd_left_ = 0, content_left_ = 0, skip_left_ = 0, fbuf_len_ = 0;
   bool in_cd_ = false, content_seen_ = false, has_crc_ = false;
@@ -586,7 +592,7 @@ class GrpcStorageClient : public StorageClient {
     q.read_limit = limit > 0 ? limit : 0;
     q.generation = rr->pin_generation;
     GrpcCall* raw = nullptr;
-    ReadObjectHandler h(sink, rr, delivered, full, &raw);
+    ReadObjectHandler h(sink, rr, delivered, full, &raw, limit >= 0 ? *delivered + limit : ~0ull);
     auto call = std::make_shared<GrpcCall>(&h);
     raw = call.get();
     auto c = conn();

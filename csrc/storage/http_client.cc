@@ -115,9 +115,13 @@ class HttpStorageClient : public StorageClient {
       }
     }
     const size_t chunk = cfg_.read_chunk;
+    // ranged read: never more than `limit` bytes into the sink
+    const uint64_t cap_total = limit >= 0 ? *delivered + static_cast<uint64_t>(limit) : ~0ull;
     while (!ex.body_done()) {
+      if (*delivered >= cap_total) throw StorageError("GET: server sent more than the requested range", false);
       Window w = sink.acquire(chunk);
       size_t cap = w.cap < chunk ? w.cap : chunk;
+      if (cap > cap_total - *delivered) cap = static_cast<size_t>(cap_total - *delivered);
       size_t r = ex.read_body(w.ptr, cap);
       if (r == 0) break;
       if (!rr->first_byte_ns) rr->first_byte_ns = now_ns();

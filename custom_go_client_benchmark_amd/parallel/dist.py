@@ -31,6 +31,7 @@ class DistContext:
     gpu: int = -1               # this rank's HIP device, -1 without a GPU
     backend: str = "none"
     initialized_here: bool = False
+    pg: bool = False            # a process group exists (collectives run even at world 1)
 
 
 def env_rank() -> tuple[int, int, int]:
@@ -50,11 +51,26 @@ def local_device(local_rank: int) -> int:
     return local_rank % n if n > 0 else -1
 
 
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
 def init(local_rank: int | None = None, world: int | None = None, rank: int | None = None,
-         backend: str | None = None, timeout_s: float = 600.0) -> DistContext:
+         backend: str | None = None, timeout_s: float = 600.0, always_pg: bool = False) -> DistContext:
     """backend None: "nccl" (RCCL) with a GPU, "gloo" without.  The
     GCSB_DIST_BACKEND env var overrides it (gloo rehearsals of N ranks on a
-    box with fewer GPUs: RCCL rejects two ranks on one GPU)."""
+    box with fewer GPUs: RCCL rejects two ranks on one GPU).
+
+    always_pg: create the process group at world 1 too, so a 1-GPU run still
+    initialises an RCCL communicator and every barrier / reduction below goes
+    through it (the bench does this: the R0-R4 path then runs on MI355X in
+    every 1-GPU run, not only on an 8-GPU node)."""
     import torch
     import torch.distributed as dist
 
@@ -71,11 +87,11 @@ def init(local_rank: int | None = None, world: int | None = None, rank: int | No
         ctx.device = torch.device("cuda", ctx.gpu) if backend in (None, "nccl") else torch.device("cpu")
     else:
         ctx.device = torch.device("cpu")
-    if world > 1:
+    if world > 1 or always_pg:
         if backend is None:
             backend = "nccl" if use_cuda else "gloo"
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29512")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()) if world == 1 else "29512")
         if not dist.is_initialized():
             kw = {}
             if backend == "nccl" and use_cuda:
@@ -84,6 +100,7 @@ def init(local_rank: int | None = None, world: int | None = None, rank: int | No
                                     timeout=datetime.timedelta(seconds=timeout_s), **kw)
             ctx.initialized_here = True
         ctx.backend = backend
+        ctx.pg = True
     return ctx
 
 
@@ -117,7 +134,7 @@ def _watchdog(ctx: DistContext, what: str, timeout_s: float, done: threading.Eve
 def barrier(ctx: DistContext, what: str = "barrier", timeout_s: float | None = None) -> None:
     """R1/R2: RCCL all_reduce of one int32 + device sync (gloo on CPU), under a
     watchdog (GCSB_BARRIER_TIMEOUT_S, default 300 s)."""
-    if ctx.world <= 1:
+    if not ctx.pg:
         return
     import torch
     import torch.distributed as dist
@@ -147,7 +164,7 @@ def reduce_stats(ctx: DistContext, **vals: float) -> dict:
 
     keys = sorted(vals)
     out: dict = {}
-    if ctx.world <= 1:
+    if not ctx.pg:
         for k in keys:
             v = float(vals[k])
             out[k + "_sum"] = out[k + "_max"] = out[k + "_min"] = v
@@ -172,7 +189,7 @@ def reduce_stats(ctx: DistContext, **vals: float) -> dict:
 
 def reduce_histogram(ctx: DistContext, buckets: list[int]) -> list[int]:
     """Sum the OpenCensus latency buckets over ranks (node-level view)."""
-    if ctx.world <= 1:
+    if not ctx.pg:
         return list(buckets)
     import torch
     import torch.distributed as dist
@@ -182,8 +199,21 @@ def reduce_histogram(ctx: DistContext, buckets: list[int]) -> list[int]:
     return [int(x) for x in t.tolist()]
 
 
+def gather_floats(ctx: DistContext, vals: list[float]) -> list[list[float]]:
+    """R4: every rank's small float vector, in rank order (all_gather)."""
+    if not ctx.pg:
+        return [list(map(float, vals))]
+    import torch
+    import torch.distributed as dist
+
+    base = torch.tensor([float(v) for v in vals], dtype=torch.float64, device=ctx.device)
+    out = [torch.zeros_like(base) for _ in range(ctx.world)]
+    dist.all_gather(out, base)
+    return [[float(x) for x in t.tolist()] for t in out]
+
+
 def shutdown(ctx: DistContext) -> None:
-    if ctx.world > 1 and ctx.initialized_here:
+    if ctx.initialized_here:
         import torch.distributed as dist
 
         if dist.is_initialized():

@@ -31,18 +31,59 @@ def torchrun(args, nproc=2, timeout=240):
     return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT, env=env)
 
 
+def _bench_line(stdout):
+    lines = [l for l in stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, stdout  # rank 0 only
+    return json.loads(lines[0])
+
+
 def test_bench_two_ranks_gloo():
     r = torchrun(["bench.py", "--gpus", "2", "--sink", "discard", "--steps", "3", "--warmup", "1",
                   "--object-size", "4MiB"])
     assert r.returncode == 0, r.stderr[-3000:]
-    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1  # rank 0 only
-    out = json.loads(lines[0])
-    assert out["n_gpus"] == 2 and out["steps"] == 3 and out["config"]["global_batch"] == 2
+    out = _bench_line(r.stdout)
+    assert out["n_gpus"] == 2 and out["ranks"] == 2 and out["steps"] == 3 and out["config"]["global_batch"] == 2
     assert out["value"] > 0 and out["scaling"] == "weak" and out["config"]["parallelism"] == "dp2"
+    # headline = the reference's one stream per object read
+    assert out["config"]["streams_per_read"] == 1 and out["verified_reads"] == 6
+    assert len(out["per_rank_mib_s"]) == 2
     # the other transport on the same config, reduced over both ranks
     other = {"grpc": "http", "http": "grpc"}[out["config"]["protocol"]]
     assert out["compare"]["protocol"] == other and out["compare"]["ok"] and out["compare"]["mib_s"] > 0
+    assert out["sliced"]["ok"] and out["sliced"]["streams_per_read"] == 8
+
+
+def _bench_env():
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return env
+
+
+def test_bench_self_launches_ranks():
+    """`python bench.py --gpus N` (no torchrun) spawns N rank processes itself."""
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--sink", "discard", "--steps", "2",
+                        "--warmup", "1", "--object-size", "4MiB", "--side-steps", "0"],
+                       capture_output=True, text=True, timeout=240, cwd=ROOT, env=_bench_env())
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = _bench_line(r.stdout)
+    assert out["n_gpus"] == 2 and out["ranks"] == 2 and out["config"]["parallelism"] == "dp2"
+    assert "compare" not in out and "sliced" not in out
+
+
+def test_bench_refuses_gpus_world_mismatch():
+    r = torchrun(["bench.py", "--gpus", "3", "--sink", "discard", "--steps", "1", "--warmup", "0",
+                  "--object-size", "64KiB", "--side-steps", "0"])
+    assert r.returncode != 0
+    assert "must match" in r.stderr
+
+
+def test_bench_write_workload_two_ranks_rehearsal_needs_gpu():
+    r = subprocess.run([sys.executable, "bench.py", "--workload", "write", "--sink", "discard", "--steps", "1"],
+                       capture_output=True, text=True, timeout=240, cwd=ROOT, env=_bench_env())
+    assert r.returncode == 2 and "needs --sink gpu" in r.stderr
 
 
 def test_cli_two_ranks_offsets_and_node_view(tmp_path):

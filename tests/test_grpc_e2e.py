@@ -129,3 +129,22 @@ def test_connection_refused_is_a_clean_error(native):
                        "retry_initial_s": 0.001})
     with pytest.raises(native.StorageError, match="refused"):
         c.read("b", "o")
+
+
+@pytest.mark.parametrize("ranged", [True, False])
+def test_stream_cut_after_last_byte_completes_without_refetch(native, server, ranged):
+    """All requested bytes arrived but the connection died before the
+    trailers: the retry must not ask again (read_limit=0 would mean "to the
+    end of the object" and overrun a ranged/piece sink).  ADVICE r1."""
+    size = 10 << 20
+    server.add_synthetic(B, P, "", 0, 1, size)
+    server.set_faults({"drop_trailers_count": 1})
+    c = _c(native, server)
+    off, lim = ((3 << 20) + 5, (2 << 20) + 7) if ranged else (0, -1)
+    r = c.read(B, P + "0", offset=off, limit=lim)
+    want = lim if ranged else size
+    assert r["bytes"] == want and r["attempts"] == 2, r
+    assert server.stats()["faults_injected"] == 1
+    if not ranged:
+        assert r["verified"]
+    assert c.read_bytes(B, P + "0", off, want) == native.object_bytes(P + "0", off, want)

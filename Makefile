@@ -34,7 +34,7 @@ GPU_OBJS  := $(patsubst csrc/%.hip,$(BUILD)/%.o,$(GPU_SRCS))
 PY_OBJS   := $(patsubst csrc/%.cc,$(BUILD)/%.o,$(PY_SRCS))
 
 EXT := $(PKG)/_native$(EXT_SUFFIX)
-TOOLS := fakegcs read_operation ssd_test write_operations list_operation open_file small_poc
+TOOLS := fakegcs read_operation ssd_test write_operations list_operation open_file small_poc loopback_ceiling
 TOOL_BINS := $(addprefix $(PKG)/bin/,$(TOOLS))
 
 .PHONY: all clean ext tools asan tsan stress

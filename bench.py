@@ -99,8 +99,15 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--object-size", default="256MiB")
     ap.add_argument("--workers", type=int, default=1, help="readers per GPU (config: 1)")
     ap.add_argument("--sink", default="gpu", help="gpu (HBM landing + GPU CRC) | discard (CPU baseline)")
-    ap.add_argument("--slot-bytes", default="4MiB")
-    ap.add_argument("--slots", type=int, default=4)
+    ap.add_argument("--slot-bytes", default="2MiB",
+                    help="pinned ring slot (one H2D copy + CRC launch each); 2 MiB x 8 measured best for one "
+                         "stream per read (profiles/r2_single_stream)")
+    ap.add_argument("--slots", type=int, default=8)
+    ap.add_argument("--async-submit", type=int, default=1, choices=[0, 1],
+                    help="slot hand-off (H2D copy + CRC launches) on a per-device submitter thread instead of the "
+                         "receiving thread: one stream per read is bound by its receiving core, so taking the HIP "
+                         "calls off it gave +15-35%% (profiles/r2_single_stream)")
+    ap.add_argument("--rcvbuf", default="0", help="client SO_RCVBUF (0 = kernel autotuning)")
     ap.add_argument("--grpc-pool", type=int, default=1)
     ap.add_argument("--slices", type=int, default=1,
                     help="streams per object read in the HEADLINE run (1 = the reference's sequential read)")
@@ -238,7 +245,13 @@ def run_rank(args) -> int:
         "slice_piece_bytes": parse_size(args.piece_bytes),
         "slice_piece_min_bytes": parse_size(args.piece_min_bytes),
         "blocking_sync": args.event_wait == "block",
+        "async_submit": bool(args.async_submit),
+        "rcvbuf": parse_size(args.rcvbuf),
     }
+    # the sliced extension keeps the geometry tuned for 8 streams in round 1
+    # (4 x 4 MiB per sink, inline submit: profiles/r1_pieces, r1_submit_ab)
+    sliced_cfg = {"slices": args.sliced_streams, "ring_slot_bytes": 4 << 20, "ring_slots": 4,
+                  "async_submit": False}
 
     def sync():
         if torch.cuda.is_available():
@@ -382,8 +395,8 @@ def run_rank(args) -> int:
             blocks["compare"] = ("compare", read_block({"protocol": other}, side_steps, 1, f"{other} compare"),
                                  {"protocol": other})
         if args.sliced_streams > 1 and args.slices == 1:
-            blocks["sliced"] = ("sliced", read_block({"slices": args.sliced_streams}, side_steps, 1, "sliced"),
-                                {"streams_per_read": args.sliced_streams,
+            blocks["sliced"] = ("sliced", read_block(sliced_cfg, side_steps, 1, "sliced"),
+                                {"streams_per_read": args.sliced_streams, "ring": "4x4MiB",
                                  "piece_bytes": parse_size(args.piece_bytes), "note": "extension, not parity"})
         if use_gpu:
             blocks["write"] = ("write", write_block(side_steps, 1),
@@ -432,6 +445,7 @@ def run_rank(args) -> int:
                     "ring": f"{args.slots}x{args.slot_bytes}",
                     "streams_per_read": args.slices if args.workload == "read" else 1,
                     "event_wait": args.event_wait,
+                    "async_submit": bool(args.async_submit),
                 },
                 "ranks": world,
                 "devices": distinct if use_gpu else "none (cpu rehearsal)",

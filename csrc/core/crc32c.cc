@@ -19,6 +19,9 @@ struct Tables {
 
 constexpr size_t kBlk = 8192;  // bytes per lane of the 3-way interleave
 
+// GF(2) polynomial product mod P and x^(2^k) powers: the standard CRC
+// combine algebra, structured after zlib's multmodp()/x2nmodp() (crc32.c,
+// zlib licence, Mark Adler), here for the Castagnoli polynomial.
 uint32_t multmodp_impl(uint32_t a, uint32_t b) {
   uint32_t m = 1u << 31, p = 0;
   for (;;) {

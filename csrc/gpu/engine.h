@@ -38,9 +38,6 @@ struct GpuSinkConfig {
   int slots = 4;
   bool verify = true;  // run the CRC kernels
   Landing landing = Landing::kObject;
-  // Submit a partially filled slot when at least this many bytes are waiting
-  // and the socket has nothing more right now (0 = only full slots).
-  size_t eager_submit_bytes = 0;
   // Slot hand-off (H2D copy + CRC launches + events) on one per-device
   // submitter thread instead of the transport thread.  Cuts the transport
   // thread's hand-off from ~170 us to ~3 us per slot with 8 sliced streams

@@ -263,6 +263,16 @@ def main(argv: list[str] | None = None) -> int:
     if lat_file:
         lat_file.close()
 
+    # node-level latency distribution (R3): the per-rank histograms summed
+    # over the process group; rank 0 exports it under the un-suffixed names
+    if exporter and ctx is not None and ctx.world > 1 and "oc_buckets" in s:
+        node = metrics_exporter.node_distribution(ctx, metrics_exporter.distribution_from_summary(s))
+        if rank == 0:
+            metrics_exporter.write_once(node, fs.get("project"), prom_file=fs.get("metrics-file"),
+                                        jsonl_file=fs.get("metrics-jsonl"),
+                                        labels={"scope": "node", "ranks": str(ctx.world)})
+            _err(f"node latency distribution: {node.count} reads over {ctx.world} ranks")
+
     # node view (R3/R4)
     if ctx is not None and ctx.world > 1:
         st = dist.reduce_stats(ctx, nbytes=float(s["bytes"]), reads=float(s.get("reads", 0) + s.get("writes", 0)),

@@ -197,3 +197,33 @@ def distribution_from_summary(summary: dict) -> Distribution:
     # the measured float latencies
     d.sum_ms = summary["avg_ms"] * d.count
     return d
+
+
+def write_once(dist: Distribution, project: str, prom_file: str = "", jsonl_file: str = "",
+               labels: dict[str, str] | None = None, start_time: float | None = None) -> None:
+    """One export of `dist` (e.g. the node-level view rank 0 writes after the
+    per-rank histograms were summed over RCCL, parallel/dist.py R3)."""
+    view = _registered.get(VIEW_NAME) or register_latency_view()
+    if prom_file:
+        tmp = prom_file + ".tmp"
+        with open(tmp, "w") as f:
+            f.write(prometheus_text(view, dist, labels))
+        os.replace(tmp, prom_file)
+    if jsonl_file:
+        with open(jsonl_file, "a") as f:
+            f.write(json.dumps(timeseries_record(view, dist, project, start_time or time.time(), labels)) + "\n")
+
+
+def node_distribution(ctx, local: Distribution) -> Distribution:
+    """Sum a rank's distribution over all ranks (collective: every rank calls
+    it).  One node-level distribution, like the reference's single process
+    exports (metrics_exporter.go:22-34), out of one histogram per GPU rank."""
+    from ..parallel import dist as gdist
+
+    counts = gdist.reduce_histogram(ctx, list(local.bucket_counts) + [local.count])
+    st = gdist.reduce_stats(ctx, sum_ms=float(local.sum_ms))
+    d = Distribution()
+    d.bucket_counts = counts[:-1]
+    d.count = counts[-1]
+    d.sum_ms = st["sum_ms_sum"]
+    return d

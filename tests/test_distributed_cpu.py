@@ -100,6 +100,31 @@ def test_cli_two_ranks_offsets_and_node_view(tmp_path):
     assert r.stderr.count("Read benchmark completed successfully!") == 2
 
 
+def test_cli_node_histogram_is_sum_of_ranks(tmp_path):
+    """R3 node view: rank 0 exports one distribution whose bucket counts are
+    the sum of the per-rank histograms (same view name / buckets as
+    reference metrics_exporter.go:22-34)."""
+    prom = tmp_path / "lat.prom"
+    jsonl = tmp_path / "lat.jsonl"
+    r = torchrun(["-m", "custom_go_client_benchmark_amd", "-worker", "3", "-read-call-per-worker", "4",
+                  "-start-fake-server", "-fake-object-size", "65536", "-client-protocol", "http",
+                  "-metrics-file", str(prom), "-metrics-jsonl", str(jsonl)])
+    assert r.returncode == 0, r.stderr[-3000:]
+
+    def counts(path):
+        recs = [json.loads(l) for l in open(path)]
+        return recs[-1]["points"][0]["value"]["distributionValue"], recs[-1]["metric"]
+
+    d0, _ = counts(str(jsonl) + ".rank0")
+    d1, _ = counts(str(jsonl) + ".rank1")
+    node, meta = counts(jsonl)
+    assert meta["type"].endswith("princer_go_client_read_latency") and meta["labels"]["scope"] == "node"
+    assert d0["count"] == 12 and d1["count"] == 12 and node["count"] == 24
+    assert node["bucketCounts"] == [a + b for a, b in zip(d0["bucketCounts"], d1["bucketCounts"])]
+    text = prom.read_text()
+    assert 'princer_go_client_read_latency_count{scope="node",ranks="2",princer_read_latency=""} 24' in text
+
+
 def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))

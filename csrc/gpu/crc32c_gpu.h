@@ -5,16 +5,21 @@
 // A "segment" is one contiguous device byte range [addr, addr+len) whose
 // CRC32C is wanted (one gRPC ChecksummedData message, or the part of it that
 // landed in one ring slot, or one slot's share of an HTTP body).  A batch of up
-// to kMaxSeg segments is processed by two launches on the caller's stream:
-//   K1 crc32c_tiles    : every wave CRCs one 16 KiB tile (4 rounds x 64 lanes x
-//                        64-byte chunks, slice-by-16 + gap/tree shift tables
-//                        staged in LDS, 6-level wave tree), tiles
-//                        right-aligned to the segment end so a ragged head is
-//                        just leading zeros (free for a raw CRC);
-//   K2 crc32c_segments : one workgroup per segment folds its tiles (strided
-//                        Horner + 8-level tree), adds the <16-byte tail, applies
-//                        the init/xorout fixup and compares with the expected
-//                        CRC, writing {raw, crc, status} to host-mapped memory.
+// to kMaxSeg segments is ONE launch on the caller's stream when every segment
+// fits kCrcFusedMaxTiles tiles (always true for ring slots):
+//   crc32c_tiles_kernel : every wave CRCs one tile (4 or 16 KiB; 64 lanes x
+//                         64-byte chunks, slice-by-16 + gap/tree shift tables
+//                         staged in LDS, 6-level wave tree), tiles
+//                         right-aligned to the segment end so a ragged head is
+//                         just leading zeros (free for a raw CRC); the last
+//                         workgroup to finish then folds each segment (one
+//                         wave per segment: Horner + wave tree with LDS shift
+//                         tables), adds the 1..16-byte tail in parallel,
+//                         applies the init/xorout fixup and compares with the
+//                         expected CRC, writing {raw, crc, status} to
+//                         host-mapped memory.
+// Longer segments add crc32c_fold_kernel (8 waves per segment) after the
+// tiles.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -27,9 +32,12 @@ namespace gcsb {
 // Per-device, lazily uploaded tables.
 const CrcTables* device_crc_tables(int device);
 
-// Enqueue K1 + K2. tile_scratch must hold batch.total_tiles words.
-void launch_crc32c_batch(const CrcBatch& b, const CrcTables* d_tables, uint32_t* d_tile_scratch,
+// Enqueue the batch (finalize_crc_batch first).  d_scratch: from
+// crc_scratch_alloc(>= batch.total_tiles); batches sharing one scratch must be
+// stream-ordered (its header word is the fused kernel's completion counter).
+void launch_crc32c_batch(const CrcBatch& b, const CrcTables* d_tables, uint32_t* d_scratch,
                          CrcSegResult* d_results, hipStream_t stream);
+uint32_t* crc_scratch_alloc(uint64_t tiles);
 
 // Pattern kernels (K3): object bytes of the synthetic content (csrc/core/content.h).
 void launch_fill_pattern(uint8_t* dst, uint64_t n, uint64_t rot, uint64_t obj_off, hipStream_t stream);

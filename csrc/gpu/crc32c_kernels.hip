@@ -1,21 +1,31 @@
 // CDNA4 (gfx950) CRC32C kernels + synthetic-pattern fill/verify kernels.
-// Design notes in crc32c_gpu.h and crc_types.h (tile geometry).  Wave64
-// throughout: a wave owns a 16 KiB tile, read in 4 rounds of 4 KiB where lane
-// l takes its own contiguous 64-byte chunk (4 x global_load_dwordx4; each
-// 128-byte line is consumed by two lanes within 4 consecutive loads, so L1
-// absorbs the 16 B-per-lane pattern).  The data has no reuse and never touches
-// LDS; the LDS holds the 44 KiB of lookup tables: slice-by-16 (16 lookups per
-// 16 B), one gap-shift table (a lane's state jumps 4032 B to its next chunk:
-// 0.75 lookups per 16 B) and 6 wave-tree shift tables (1.5 per 16 B).
+// Geometry in crc_types.h.  Wave64 throughout: a wave owns a tile of R x 4 KiB
+// (R = 1 or 4), read in R rounds where lane l takes its own contiguous 64-byte
+// chunk (4 x global_load_dwordx4; each 128-byte line is consumed by two lanes
+// within 4 consecutive loads, so L1 absorbs the 16 B-per-lane pattern).  The
+// data has no reuse and never touches LDS; the LDS holds the 44 KiB of lookup
+// tables: slice-by-16 (16 lookups per 16 B), one gap-shift table (a lane's
+// state jumps 4032 B to its next chunk) and 6 wave-tree shift tables.
 //
-// Measured (profiles/r1_k1, scripts/crc_kernel_bench.py, 1 GiB in 32 MiB
-// segments): round-0 kernel (4 KiB tiles, 16 B-strided lanes, 36 % of lookups
-// spent on gap shifts) 2.4 TB/s -> lane-contiguous 256 B runs 3.0-3.1 TB/s
-// (fewer lookups but L1-hostile 256 B lane strides) -> 64 B chunks in 4 KiB
-// rounds 3.5-3.7 TB/s.  Random ds_read_b32 table lookups still cost ~4
-// bank-conflict cycles per instruction; the conflict-free "nib" variant
-// (nibble tables replicated per LDS bank, GCSB_CRC_K1=nib) removes them
-// (0.16/instr) but doubles lookups and VALU and runs at 3.2 TB/s.
+// One launch per ring slot (round 2): the tile kernel's last workgroup to
+// finish (a "workgroups done" counter in the tile scratch, release/acquire
+// fences at agent scope so tiles written on other XCDs' L2s are visible)
+// restages the tile-fold shift tables into its LDS and folds every segment,
+// one wave per segment: Horner over 64-tile strides, a 6-level wave tree, the
+// 1..16-byte tail as one independent slice-by-r lookup per lane + an XOR
+// reduction, the init/xorout fixup and the compare against the server's CRC,
+// written to host-mapped memory.  Round 1 ran a second kernel for that fold
+// with its shift tables read from global memory (7.1 us per slot, as long as
+// the tile kernel; profiles/r1_bench_sliced4_kernel_stats.csv).  Segments over
+// kCrcFusedMaxTiles tiles (bulk gpu_crc32c of large buffers) keep a separate
+// fold kernel, 8 waves per segment, tables in LDS.
+//
+// Measured history (profiles/r1_k1, 1 GiB in 32 MiB segments): 4 KiB tiles
+// with 16 B-strided lanes 2.4 TB/s -> lane-contiguous 256 B runs 3.0-3.1 TB/s
+// -> 64 B chunks in 4 KiB rounds (16 KiB tiles) 3.5-3.7 TB/s.  Random
+// ds_read_b32 table lookups cost ~4 bank-conflict cycles per instruction; a
+// conflict-free variant (nibble tables replicated per bank) removed them but
+// doubled the lookups and ran at 3.2 TB/s, so it was dropped in round 2.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -36,8 +46,11 @@ void hip_check(hipError_t e, const char* what) {
 
 namespace {
 
-constexpr int kK1Threads = 512;                       // 8 waves (tiles) per workgroup: amortise the table fill
-constexpr int kLdsWords = 16 * 256 + 7 * 4 * 256;     // slice16 + 6 tree + 1 gap shift tables = 11264 words (44 KiB)
+constexpr int kThreads = 512;                      // 8 waves (tiles) per workgroup: amortise the table fill
+constexpr int kWaves = kThreads / 64;
+constexpr int kSliceWords = 16 * 256;
+constexpr int kFoldLevels = 7;                     // fused fold: 1..64-tile shifts (levels 0..6)
+constexpr int kK2Levels = 10;                      // 8-wave fold: levels 0..9 (512-tile Horner stride)
 
 __device__ __forceinline__ uint32_t shift4(const uint32_t* __restrict__ tab, uint32_t s) {
   return tab[s & 0xff] ^ tab[256 + ((s >> 8) & 0xff)] ^ tab[512 + ((s >> 16) & 0xff)] ^ tab[768 + (s >> 24)];
@@ -64,15 +77,29 @@ __device__ __forceinline__ uint32_t mask_low_bytes(uint32_t w, int keep_from) {
   return w & (0xFFFFFFFFu << (8 * keep_from));
 }
 
-// Lane `lane`'s 16 pieces of the tile starting at tstart, in CRC order:
-// piece (k, j) = round k, chunk piece j at tstart + 4096 k + 64 lane + 16 j.
-// Pieces before the segment start read as zeros (free for a raw CRC); the
-// piece straddling it is masked.  Tiles are right-aligned to the segment end,
-// so only the first tile of a segment has such a head.
-__device__ __forceinline__ void load_lane_pieces(uint4 (&v)[kCrcRounds * kCrcChunkPieces], intptr_t tstart, int lane,
-                                                 uintptr_t addr) {
+__device__ __forceinline__ void stage(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src, int words) {
+  const uint4* s4 = reinterpret_cast<const uint4*>(src);
+  uint4* d4 = reinterpret_cast<uint4*>(dst);
+  for (int i = threadIdx.x; i < words / 4; i += blockDim.x) d4[i] = s4[i];
+}
+
+// Tile `gt` of the batch: raw CRC (valid in lane 0).  Pieces before the
+// segment start read as zeros (free for a raw CRC); the piece straddling it is
+// masked.  Tiles are right-aligned to the segment end, so only the first tile
+// of a segment has such a head.
+template <int R>
+__device__ __forceinline__ uint32_t tile_crc(const CrcBatch& b, uint32_t s, uint32_t gt, const uint32_t* sl,
+                                             const uint32_t* lane_shift, int lane) {
+  const uintptr_t addr = reinterpret_cast<uintptr_t>(b.seg[s].addr);
+  const uint32_t len = b.seg[s].len;
+  const uint32_t t = gt - b.seg[s].tile_base;
+  const uintptr_t a16 = addr & ~uintptr_t(15);
+  const uint64_t full = (addr + len - a16 + 15) / 16 - 1;
+  const intptr_t vend = static_cast<intptr_t>(a16 + 16 * full);
+  const intptr_t tstart = vend - (static_cast<intptr_t>(R) * kCrcRoundBytes) * static_cast<intptr_t>(b.seg[s].ntiles - t);
+  uint4 v[R * kCrcChunkPieces];
 #pragma unroll
-  for (int k = 0; k < kCrcRounds; ++k)
+  for (int k = 0; k < R; ++k)
 #pragma unroll
     for (int j = 0; j < kCrcChunkPieces; ++j) {
       const intptr_t p = tstart + kCrcRoundBytes * k + kCrcChunkBytes * lane + 16 * j;
@@ -87,176 +114,196 @@ __device__ __forceinline__ void load_lane_pieces(uint4 (&v)[kCrcRounds * kCrcChu
       }
       v[k * kCrcChunkPieces + j] = x;
     }
-}
-
-// K1: raw CRC of every 4 KiB tile of every segment in the batch.
-template <bool kK1LoadsFirst>
-__global__ __launch_bounds__(kK1Threads) void crc32c_tiles_kernel(const CrcBatch b, const uint32_t* __restrict__ tabs,
-                                                                   uint32_t* __restrict__ tile_out) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_tab[kLdsWords];
-  {
-    const uint4* src = reinterpret_cast<const uint4*>(tabs);
-    uint4* dst = reinterpret_cast<uint4*>(s_tab);
+  // keep all the tile's loads in flight before the first lookup (the
+  // scheduler otherwise sinks them into the lookup chain)
+  __builtin_amdgcn_sched_barrier(0);
+  uint32_t state = 0;
 #pragma unroll
-    for (int i = threadIdx.x; i < kLdsWords / 4; i += kK1Threads) dst[i] = src[i];
+  for (int k = 0; k < R; ++k) {
+    if (k) state = shift4(lane_shift + 6 * 1024, state);  // over the 4032-byte gap to this lane's next chunk
+#pragma unroll
+    for (int j = 0; j < kCrcChunkPieces; ++j) state = update16(sl, state, v[k * kCrcChunkPieces + j]);
   }
-  __syncthreads();
-  const uint32_t* sl = s_tab;
-  const uint32_t* lane_shift = s_tab + 16 * 256;
-  const int lane = threadIdx.x & 63;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t nwaves = gridDim.x * (kK1Threads / 64);
-  // gt only grows, so the segment search resumes where the last tile left it
-  // (restarting from 0 cost up to kMaxSeg dependent scalar loads per tile)
-  uint32_t s = 0;
-  for (uint32_t gt = blockIdx.x * (kK1Threads / 64) + wave; gt < b.total_tiles; gt += nwaves) {
-    while (s + 1 < b.nseg && b.seg[s + 1].tile_base <= gt) ++s;
-    const uintptr_t addr = reinterpret_cast<uintptr_t>(b.seg[s].addr);
-    const uint32_t len = b.seg[s].len;
-    const uint32_t t = gt - b.seg[s].tile_base;
-    const uintptr_t a16 = addr & ~uintptr_t(15);
-    const uint64_t full = (addr + len - a16 + 15) / 16 - 1;
-    const intptr_t vend = static_cast<intptr_t>(a16 + 16 * full);
-    const intptr_t tstart = vend - static_cast<intptr_t>(kCrcTile) * static_cast<intptr_t>(b.seg[s].ntiles - t);
-    uint4 v[kCrcRounds * kCrcChunkPieces];
-    load_lane_pieces(v, tstart, lane, addr);
-    // keep all 16 loads of the tile in flight before the first lookup (the
-    // scheduler otherwise sinks them into the lookup chain: fewer bytes in
-    // flight per wave)
-    if (kK1LoadsFirst) __builtin_amdgcn_sched_barrier(0);
-    uint32_t state = 0;
+  // wave tree: lane l's last chunk ends 64 (63 - l) bytes before the tile end
 #pragma unroll
-    for (int k = 0; k < kCrcRounds; ++k) {
-      if (k) state = shift4(lane_shift + 6 * 1024, state);  // over the 4032-byte gap to this lane's next chunk
-#pragma unroll
-      for (int j = 0; j < kCrcChunkPieces; ++j) state = update16(sl, state, v[k * kCrcChunkPieces + j]);
-    }
-    // wave tree: lane l's last chunk ends 64 (63 - l) bytes before the tile end
-#pragma unroll
-    for (int lv = 0; lv < 6; ++lv) {
-      const uint32_t other = __shfl_down(state, 1 << lv, 64);
-      const uint32_t shifted = shift4(lane_shift + lv * 1024, state);
-      if ((lane & ((2 << lv) - 1)) == 0) state = shifted ^ other;
-    }
-    if (lane == 0) tile_out[gt] = state;
+  for (int lv = 0; lv < 6; ++lv) {
+    const uint32_t other = __shfl_down(state, 1 << lv, 64);
+    const uint32_t shifted = shift4(lane_shift + lv * 1024, state);
+    if ((lane & ((2 << lv) - 1)) == 0) state = shifted ^ other;
   }
+  return state;
 }
 
-// K1, conflict-free variant ("nib"): the slice-by-16 lookups are split into
-// 32 nibble tables (16 entries each) and the whole 2 KiB nibble set is
-// replicated 32x in LDS so that lane l of each 32-lane LDS group reads only
-// bank l: every lookup is one LDS cycle per group (random byte tables cost
-// 2 + ~4 conflict cycles per wave instruction, profiles/r1_crc_pmc_*).  Twice
-// the lookups (32 per 16 B) at a third of the cycles each; 88 KiB of LDS, so
-// one 16-wave workgroup per CU.
-constexpr int kK1NibThreads = 1024;
-constexpr int kNibWords = 32 * 16 * 32;                  // 64 KiB replicated nibble tables
-constexpr int kLdsNibWords = kNibWords + 7 * 4 * 256;    // + tree/gap shift tables = 92 KiB
-
-__device__ __forceinline__ uint32_t nib_word(const uint32_t* __restrict__ lbase, uint32_t w, int t0) {
-  uint32_t c = 0;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) c ^= lbase[((t0 + j) * 16 + ((w >> (4 * j)) & 15)) * 32];
-  return c;
-}
-
-__device__ __forceinline__ uint32_t update16_nib(const uint32_t* __restrict__ lbase, uint32_t state, uint4 v) {
-  return nib_word(lbase, state ^ v.x, 0) ^ nib_word(lbase, v.y, 8) ^ nib_word(lbase, v.z, 16) ^
-         nib_word(lbase, v.w, 24);
-}
-
-__global__ __launch_bounds__(kK1NibThreads) void crc32c_tiles_nib_kernel(const CrcBatch b,
-                                                                         const CrcTables* __restrict__ tabs,
-                                                                         uint32_t* __restrict__ tile_out) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_tab[kLdsNibWords];
-  {
-    const uint32_t* nib = &tabs->nib[0][0];
-    for (int i = threadIdx.x; i < kNibWords; i += kK1NibThreads) s_tab[i] = nib[i >> 5];
-    const uint4* src = reinterpret_cast<const uint4*>(&tabs->lane_shift[0][0][0]);
-    uint4* dst = reinterpret_cast<uint4*>(s_tab + kNibWords);
-    for (int i = threadIdx.x; i < 7 * 256; i += kK1NibThreads) dst[i] = src[i];
+// The last 1..16 bytes of a segment (after its tiles) folded into `raw`: lane
+// i < r looks up slice16[r-1-i][byte_i ^ state byte i] independently, an XOR
+// reduction over 16 lanes combines them (slice-by-r).  Result in every lane.
+__device__ __forceinline__ uint32_t add_tail(const CrcSeg& sg, uint32_t raw, const uint32_t* sl, int lane) {
+  if (sg.len == 0) return raw;
+  const uintptr_t addr = reinterpret_cast<uintptr_t>(sg.addr);
+  const uintptr_t a16 = addr & ~uintptr_t(15);
+  const uintptr_t e = addr + sg.len;
+  const uintptr_t vend = a16 + 16 * ((e - a16 + 15) / 16 - 1);
+  const uintptr_t p0 = vend > addr ? vend : addr;
+  const int r = static_cast<int>(e - p0);
+  uint32_t x = 0;
+  if (lane < r) {
+    const uint32_t sb = lane < 4 ? (raw >> (8 * lane)) & 0xff : 0u;
+    x = sl[(r - 1 - lane) * 256 + ((*reinterpret_cast<const uint8_t*>(p0 + lane) ^ sb) & 0xff)];
   }
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const uint32_t* lbase = s_tab + (lane & 31);
-  const uint32_t* lane_shift = s_tab + kNibWords;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t nwaves = gridDim.x * (kK1NibThreads / 64);
-  uint32_t s = 0;
-  for (uint32_t gt = blockIdx.x * (kK1NibThreads / 64) + wave; gt < b.total_tiles; gt += nwaves) {
-    while (s + 1 < b.nseg && b.seg[s + 1].tile_base <= gt) ++s;
-    const uintptr_t addr = reinterpret_cast<uintptr_t>(b.seg[s].addr);
-    const uint32_t len = b.seg[s].len;
-    const uint32_t t = gt - b.seg[s].tile_base;
-    const uintptr_t a16 = addr & ~uintptr_t(15);
-    const uint64_t full = (addr + len - a16 + 15) / 16 - 1;
-    const intptr_t vend = static_cast<intptr_t>(a16 + 16 * full);
-    const intptr_t tstart = vend - static_cast<intptr_t>(kCrcTile) * static_cast<intptr_t>(b.seg[s].ntiles - t);
-    uint4 v[kCrcRounds * kCrcChunkPieces];
-    load_lane_pieces(v, tstart, lane, addr);
-    uint32_t state = 0;
 #pragma unroll
-    for (int k = 0; k < kCrcRounds; ++k) {
-      if (k) state = shift4(lane_shift + 6 * 1024, state);
-#pragma unroll
-      for (int j = 0; j < kCrcChunkPieces; ++j) state = update16_nib(lbase, state, v[k * kCrcChunkPieces + j]);
-    }
-#pragma unroll
-    for (int lv = 0; lv < 6; ++lv) {
-      const uint32_t other = __shfl_down(state, 1 << lv, 64);
-      const uint32_t shifted = shift4(lane_shift + lv * 1024, state);
-      if ((lane & ((2 << lv) - 1)) == 0) state = shifted ^ other;
-    }
-    if (lane == 0) tile_out[gt] = state;
-  }
+  for (int o = 8; o > 0; o >>= 1) x ^= __shfl_xor(x, o, 64);
+  return x ^ (r < 4 ? raw >> (8 * r) : 0u);
 }
 
-// K2: fold tiles -> segment raw CRC, add the tail, fixup, compare.
-__global__ __launch_bounds__(256) void crc32c_segments_kernel(const CrcBatch b, const CrcTables* __restrict__ t,
-                                                              const uint32_t* __restrict__ tiles,
-                                                              CrcSegResult* __restrict__ out) {
-  const uint32_t s = blockIdx.x;
-  if (s >= b.nseg) return;
-  const uint32_t T = b.seg[s].ntiles;
-  const uint32_t base = b.seg[s].tile_base;
-  const int k = threadIdx.x;
-  const int lane = k & 63;
+__device__ __forceinline__ CrcSegResult seg_result(const CrcSeg& sg, uint32_t raw) {
+  const uint32_t crc = raw ^ sg.fixup;
+  CrcSegResult r;
+  r.raw = raw;
+  r.crc = crc;
+  r.status = (sg.flags & 1) ? (crc == sg.expected ? 1u : 2u) : 0u;
+  r.pad = 0;
+  return r;
+}
+
+// One wave folds one segment's tiles (ntiles <= kCrcFusedMaxTiles): lane k
+// takes tiles T-1-(k + 64 m) by Horner (64-tile shift), then the wave tree.
+// ts = tile_shift tables, level 0 = a shift by one tile.  Tile values are
+// loaded 8 at a time ahead of their Horner steps (one memory latency per 8
+// steps instead of one per step).  kCoherent: tiles written by other
+// workgroups in this launch -> agent-scope loads (sc1: past this XCD's L2).
+template <bool kCoherent>
+__device__ __forceinline__ uint32_t fold_wave(const CrcSeg& sg, const uint32_t* __restrict__ tiles,
+                                              const uint32_t* ts, int lane) {
+  const uint32_t T = sg.ntiles;
+  const uint32_t* tp = tiles + sg.tile_base;
   uint32_t acc = 0;
-  const int M = static_cast<int>((T + 255) >> 8);
-  for (int m = M - 1; m >= 0; --m) {
-    acc = shift4(&t->tile_shift[8][0][0], acc);
-    const uint32_t j = static_cast<uint32_t>(k) + 256u * static_cast<uint32_t>(m);
-    if (j < T) acc ^= tiles[base + T - 1 - j];
+  const int M = static_cast<int>((T + 63) >> 6);
+  for (int m0 = M - 1; m0 >= 0; m0 -= 8) {
+    uint32_t tv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = m0 - i;
+      const uint32_t j = static_cast<uint32_t>(lane) + 64u * static_cast<uint32_t>(m);
+      tv[i] = 0;
+      if (m >= 0 && j < T) {
+        if constexpr (kCoherent)
+          tv[i] = __hip_atomic_load(tp + (T - 1 - j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+          tv[i] = tp[T - 1 - j];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (m0 - i >= 0) acc = shift4(ts + 6 * 1024, acc) ^ tv[i];
   }
 #pragma unroll
   for (int lv = 0; lv < 6; ++lv) {
     const uint32_t other = __shfl_down(acc, 1 << lv, 64);
-    if ((lane & ((2 << lv) - 1)) == 0) acc ^= shift4(&t->tile_shift[lv][0][0], other);
+    if ((lane & ((2 << lv) - 1)) == 0) acc ^= shift4(ts + lv * 1024, other);
   }
-  __shared__ uint32_t part[4];
+  return __shfl(acc, 0, 64);
+}
+
+// Tile kernel; kFused: the last workgroup to finish folds every segment.
+template <int R, bool kFused>
+__global__ __launch_bounds__(kThreads) void crc32c_tiles_kernel(const CrcBatch b, const CrcTables* __restrict__ tabs,
+                                                                uint32_t* __restrict__ scratch,
+                                                                CrcSegResult* __restrict__ out) {
+  // LDS: slice16 | 6 wave-tree shifts | gap shift (R > 1) | tile-fold shifts
+  // (fused: staged up front with the rest, so the last workgroup folds at
+  // once instead of restaging; 68 KiB for R = 1, 2 workgroups per CU)
+  constexpr int kGapWords = R > 1 ? 1024 : 0;
+  constexpr int kFoldWords = kFused ? kFoldLevels * 1024 : 0;
+  constexpr int kTreeWords = 6 * 1024;
+  __shared__ __attribute__((aligned(16))) uint32_t s_tab[kSliceWords + kTreeWords + kGapWords + kFoldWords];
+  __shared__ uint32_t s_last;
+  stage(s_tab, &tabs->slice16[0][0], kSliceWords);
+  stage(s_tab + kSliceWords, &tabs->lane_shift[0][0][0], kTreeWords + kGapWords);
+  if constexpr (kFused)
+    stage(s_tab + kSliceWords + kTreeWords + kGapWords,
+          &tabs->tile_shift[static_cast<int>(b.tile_log2) - kCrcMinTileLog2][0][0], kFoldWords);
+  __syncthreads();
+  const uint32_t* sl = s_tab;
+  const uint32_t* lane_shift = s_tab + kSliceWords;
+  uint32_t* tiles = scratch + kCrcScratchHeader;
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t nwaves = gridDim.x * kWaves;
+  // gt only grows, so the segment search resumes where the last tile left it
+  uint32_t s = 0;
+  for (uint32_t gt = blockIdx.x * kWaves + wave; gt < b.total_tiles; gt += nwaves) {
+    while (s + 1 < b.nseg && b.seg[s + 1].tile_base <= gt) ++s;
+    const uint32_t c = tile_crc<R>(b, s, gt, sl, lane_shift, lane);
+    if (lane == 0) {
+      if constexpr (kFused)  // written through to the agent coherence point (sc1): no L2 writeback needed
+        __hip_atomic_store(tiles + gt, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        tiles[gt] = c;
+    }
+  }
+  if constexpr (kFused) {
+    // Every wave's tile stores must have completed (vmcnt 0) before thread 0
+    // counts this workgroup done; __syncthreads alone does not wait for them.
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (threadIdx.x == 0)
+      s_last = __hip_atomic_fetch_add(scratch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1
+                   ? 1u : 0u;
+    __syncthreads();
+    if (!s_last) return;
+    for (uint32_t g = wave; g < b.nseg; g += kWaves) {
+      const CrcSeg& sg = b.seg[g];
+      uint32_t raw = fold_wave<true>(sg, tiles, s_tab + kSliceWords + kTreeWords + kGapWords, lane);
+      raw = add_tail(sg, raw, sl, lane);
+      if (lane == 0) out[g] = seg_result(sg, raw);
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(scratch, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// Separate fold for long segments: one 8-wave workgroup per segment, Horner
+// over 512-tile strides, wave tree, then a 3-level tree across the waves.
+__global__ __launch_bounds__(kThreads) void crc32c_fold_kernel(const CrcBatch b, const CrcTables* __restrict__ tabs,
+                                                               const uint32_t* __restrict__ scratch,
+                                                               CrcSegResult* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_tab[kSliceWords + kK2Levels * 1024];
+  __shared__ uint32_t part[kWaves];
+  const uint32_t g = blockIdx.x;
+  if (g >= b.nseg) return;
+  const int lvl0 = static_cast<int>(b.tile_log2) - kCrcMinTileLog2;
+  stage(s_tab, &tabs->slice16[0][0], kSliceWords);
+  stage(s_tab + kSliceWords, &tabs->tile_shift[lvl0][0][0], kK2Levels * 1024);
+  __syncthreads();
+  const uint32_t* ts = s_tab + kSliceWords;
+  const CrcSeg& sg = b.seg[g];
+  const uint32_t T = sg.ntiles;
+  const uint32_t* tp = scratch + kCrcScratchHeader + sg.tile_base;
+  const int k = threadIdx.x;
+  const int lane = k & 63;
+  uint32_t acc = 0;
+  const int M = static_cast<int>((T + kThreads - 1) / kThreads);
+  for (int m = M - 1; m >= 0; --m) {
+    acc = shift4(ts + 9 * 1024, acc);
+    const uint32_t j = static_cast<uint32_t>(k) + static_cast<uint32_t>(kThreads) * static_cast<uint32_t>(m);
+    if (j < T) acc ^= tp[T - 1 - j];
+  }
+#pragma unroll
+  for (int lv = 0; lv < 6; ++lv) {
+    const uint32_t other = __shfl_down(acc, 1 << lv, 64);
+    if ((lane & ((2 << lv) - 1)) == 0) acc ^= shift4(ts + lv * 1024, other);
+  }
   if (lane == 0) part[k >> 6] = acc;
   __syncthreads();
-  if (k == 0) {
-    const uint32_t v0 = part[0] ^ shift4(&t->tile_shift[6][0][0], part[1]);
-    const uint32_t v2 = part[2] ^ shift4(&t->tile_shift[6][0][0], part[3]);
-    uint32_t raw = v0 ^ shift4(&t->tile_shift[7][0][0], v2);
-    const uint32_t len = b.seg[s].len;
-    if (len > 0) {
-      const uintptr_t addr = reinterpret_cast<uintptr_t>(b.seg[s].addr);
-      const uintptr_t a16 = addr & ~uintptr_t(15);
-      const uintptr_t e = addr + len;
-      const uintptr_t vend = a16 + 16 * ((e - a16 + 15) / 16 - 1);
-      const uint8_t* p = reinterpret_cast<const uint8_t*>(vend > addr ? vend : addr);
-      const uint8_t* pe = reinterpret_cast<const uint8_t*>(e);
-      for (; p < pe; ++p) raw = (raw >> 8) ^ t->slice16[0][(raw ^ *p) & 0xff];
+  if (k < 64) {
+    uint32_t p = lane < kWaves ? part[lane] : 0u;
+#pragma unroll
+    for (int lv = 0; lv < 3; ++lv) {
+      const uint32_t other = __shfl_down(p, 1 << lv, 64);
+      if ((lane & ((2 << lv) - 1)) == 0) p ^= shift4(ts + (6 + lv) * 1024, other);
     }
-    const uint32_t crc = raw ^ b.seg[s].fixup;
-    CrcSegResult r;
-    r.raw = raw;
-    r.crc = crc;
-    r.status = (b.seg[s].flags & 1) ? (crc == b.seg[s].expected ? 1u : 2u) : 0u;
-    r.pad = 0;
-    out[s] = r;
+    uint32_t raw = __shfl(p, 0, 64);
+    raw = add_tail(sg, raw, s_tab, lane);
+    if (lane == 0) out[g] = seg_result(sg, raw);
   }
 }
 
@@ -328,29 +375,6 @@ __global__ __launch_bounds__(256) void verify_pattern_kernel(const uint8_t* __re
   }
 }
 
-enum class K1Variant { kSlice16, kNib };
-
-// GCSB_CRC_K1=slice16|nib selects the tile kernel (A/B switch; default below).
-K1Variant k1_variant() {
-  static K1Variant v = [] {
-    const char* e = std::getenv("GCSB_CRC_K1");
-    if (e && std::string(e) == "slice16") return K1Variant::kSlice16;
-    if (e && std::string(e) == "nib") return K1Variant::kNib;
-    return K1Variant::kSlice16;
-  }();
-  return v;
-}
-
-// GCSB_K1_LOADS_FIRST=0 lets the scheduler interleave the tile loads with the
-// lookups (A/B switch; default: all 16 loads issued first).
-bool k1_loads_first() {
-  static bool v = [] {
-    const char* e = std::getenv("GCSB_K1_LOADS_FIRST");
-    return !(e && *e == '0');
-  }();
-  return v;
-}
-
 }  // namespace
 
 const CrcTables* device_crc_tables(int device) {
@@ -376,33 +400,41 @@ const CrcTables* device_crc_tables(int device) {
   return per_dev[device];
 }
 
-void launch_crc32c_batch(const CrcBatch& b, const CrcTables* d_tables, uint32_t* d_tile_scratch,
+void launch_crc32c_batch(const CrcBatch& b, const CrcTables* d_tables, uint32_t* d_scratch,
                          CrcSegResult* d_results, hipStream_t stream) {
   if (b.nseg == 0) return;
-  if (b.total_tiles > 0) {
-    if (k1_variant() == K1Variant::kNib) {
-      constexpr uint32_t tiles_per_block = kK1NibThreads / 64;
-      uint32_t blocks = (b.total_tiles + tiles_per_block - 1) / tiles_per_block;
-      if (blocks > 256) blocks = 256;  // one 88 KiB workgroup per CU, grid-stride over tiles
-      hipLaunchKernelGGL(crc32c_tiles_nib_kernel, dim3(blocks), dim3(kK1NibThreads), 0, stream, b, d_tables,
-                         d_tile_scratch);
-      hip_check(hipGetLastError(), "crc32c_tiles_nib_kernel");
-    } else {
-      constexpr uint32_t tiles_per_block = kK1Threads / 64;
-      uint32_t blocks = (b.total_tiles + tiles_per_block - 1) / tiles_per_block;
-      if (blocks > 1024) blocks = 1024;
-      if (k1_loads_first())
-        hipLaunchKernelGGL(crc32c_tiles_kernel<true>, dim3(blocks), dim3(kK1Threads), 0, stream, b,
-                           reinterpret_cast<const uint32_t*>(d_tables), d_tile_scratch);
-      else
-        hipLaunchKernelGGL(crc32c_tiles_kernel<false>, dim3(blocks), dim3(kK1Threads), 0, stream, b,
-                           reinterpret_cast<const uint32_t*>(d_tables), d_tile_scratch);
-      hip_check(hipGetLastError(), "crc32c_tiles_kernel");
-    }
+  uint32_t blocks = (b.total_tiles + kWaves - 1) / kWaves;
+  if (blocks > 1024) blocks = 1024;  // grid-stride over the rest
+  if (blocks == 0) blocks = 1;       // tail-only segments: the fused fold still runs
+  const bool fused = b.max_seg_tiles <= kCrcFusedMaxTiles;
+  const bool small = b.tile_log2 == static_cast<uint32_t>(kCrcMinTileLog2);
+  if (fused) {
+    if (small)
+      hipLaunchKernelGGL((crc32c_tiles_kernel<1, true>), dim3(blocks), dim3(kThreads), 0, stream, b, d_tables,
+                         d_scratch, d_results);
+    else
+      hipLaunchKernelGGL((crc32c_tiles_kernel<4, true>), dim3(blocks), dim3(kThreads), 0, stream, b, d_tables,
+                         d_scratch, d_results);
+    hip_check(hipGetLastError(), "crc32c_tiles_kernel(fused)");
+    return;
   }
-  hipLaunchKernelGGL(crc32c_segments_kernel, dim3(b.nseg), dim3(256), 0, stream, b, d_tables, d_tile_scratch,
-                     d_results);
-  hip_check(hipGetLastError(), "crc32c_segments_kernel");
+  if (small)
+    hipLaunchKernelGGL((crc32c_tiles_kernel<1, false>), dim3(blocks), dim3(kThreads), 0, stream, b, d_tables,
+                       d_scratch, d_results);
+  else
+    hipLaunchKernelGGL((crc32c_tiles_kernel<4, false>), dim3(blocks), dim3(kThreads), 0, stream, b, d_tables,
+                       d_scratch, d_results);
+  hip_check(hipGetLastError(), "crc32c_tiles_kernel");
+  hipLaunchKernelGGL(crc32c_fold_kernel, dim3(b.nseg), dim3(kThreads), 0, stream, b, d_tables, d_scratch, d_results);
+  hip_check(hipGetLastError(), "crc32c_fold_kernel");
+}
+
+uint32_t* crc_scratch_alloc(uint64_t tiles) {
+  uint32_t* p = nullptr;
+  const size_t bytes = sizeof(uint32_t) * crc_scratch_words(tiles);
+  hip_check(hipMalloc(reinterpret_cast<void**>(&p), bytes), "hipMalloc(crc scratch)");
+  hip_check(hipMemset(p, 0, sizeof(uint32_t) * kCrcScratchHeader), "hipMemset(crc scratch)");
+  return p;
 }
 
 void launch_fill_pattern(uint8_t* dst, uint64_t n, uint64_t rot, uint64_t obj_off, hipStream_t stream) {

@@ -1,5 +1,6 @@
 // Host half of the GPU CRC32C engine: table construction, batch geometry and a
 // bit-exact emulator of kernels K1/K2 (the CPU-side oracle for their math).
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -12,24 +13,38 @@ void build_crc_tables(CrcTables* t) {
   crc32c_build_slice16(t->slice16);
   for (int lv = 0; lv < 6; ++lv) crc32c_build_shift_table(static_cast<uint64_t>(kCrcChunkBytes) << lv, t->lane_shift[lv]);
   crc32c_build_shift_table(kCrcLaneGap, t->lane_shift[6]);
-  for (int lv = 0; lv < 9; ++lv) crc32c_build_shift_table(static_cast<uint64_t>(kCrcTile) << lv, t->tile_shift[lv]);
-  for (int p = 0; p < 16; ++p)
-    for (int n = 0; n < 16; ++n) {
-      t->nib[2 * p][n] = t->slice16[15 - p][n];
-      t->nib[2 * p + 1][n] = t->slice16[15 - p][n << 4];
-    }
+  for (int lv = 0; lv < kCrcTileShiftLevels; ++lv)
+    crc32c_build_shift_table(static_cast<uint64_t>(kCrcRoundBytes) << lv, t->tile_shift[lv]);
 }
 
-void finalize_crc_batch(CrcBatch* b) {
-  uint32_t tiles = 0;
+namespace {
+uint32_t auto_tile_log2(uint64_t total_bytes) {
+  static const uint32_t forced = [] {
+    const char* e = std::getenv("GCSB_CRC_TILE");
+    if (e && std::strcmp(e, "4k") == 0) return uint32_t(kCrcMinTileLog2);
+    if (e && std::strcmp(e, "16k") == 0) return uint32_t(kCrcMaxTileLog2);
+    return 0u;
+  }();
+  if (forced) return forced;
+  return total_bytes <= (4u << 20) ? kCrcMinTileLog2 : kCrcMaxTileLog2;
+}
+}  // namespace
+
+void finalize_crc_batch(CrcBatch* b, uint32_t tile_log2) {
+  uint64_t bytes = 0;
+  for (uint32_t i = 0; i < b->nseg; ++i) bytes += b->seg[i].len;
+  b->tile_log2 = tile_log2 ? tile_log2 : auto_tile_log2(bytes);
+  uint32_t tiles = 0, mx = 0;
   for (uint32_t i = 0; i < b->nseg; ++i) {
     CrcSeg& s = b->seg[i];
     s.tile_base = tiles;
-    crc_segment_geometry(reinterpret_cast<uintptr_t>(s.addr), s.len, &s.ntiles);
+    crc_segment_geometry(reinterpret_cast<uintptr_t>(s.addr), s.len, b->tile_log2, &s.ntiles);
     s.fixup = crc32c_fixup(s.len);
     tiles += s.ntiles;
+    if (s.ntiles > mx) mx = s.ntiles;
   }
   b->total_tiles = tiles;
+  b->max_seg_tiles = mx;
 }
 
 namespace {
@@ -50,21 +65,24 @@ uint32_t mask_low_bytes(uint32_t w, int keep_from) {
 }  // namespace
 
 CrcSegResult emulate_crc32c_segment(const uint8_t* addr_p, uint32_t len, const CrcTables& t, uint32_t expected,
-                                    bool check) {
+                                    bool check, uint32_t tile_log2, int fold_waves) {
   const uintptr_t addr = reinterpret_cast<uintptr_t>(addr_p);
+  const int rounds = 1 << (tile_log2 - kCrcMinTileLog2);
+  const intptr_t tile_bytes = intptr_t(1) << tile_log2;
+  const int lvl0 = static_cast<int>(tile_log2) - kCrcMinTileLog2;  // tile_shift index of a 1-tile shift
   uint32_t T = 0;
-  crc_segment_geometry(addr, len, &T);
+  crc_segment_geometry(addr, len, tile_log2, &T);
   std::vector<uint32_t> tiles(T);
-  // K1
+  // tile kernel: per-lane chains over R rounds, 6-level wave tree
   for (uint32_t tt = 0; tt < T; ++tt) {
     const uintptr_t a16 = addr & ~uintptr_t(15);
     const uint64_t full = (addr + len - a16 + 15) / 16 - 1;
     const intptr_t vend = static_cast<intptr_t>(a16 + 16 * full);
-    const intptr_t tstart = vend - static_cast<intptr_t>(kCrcTile) * static_cast<intptr_t>(T - tt);
+    const intptr_t tstart = vend - tile_bytes * static_cast<intptr_t>(T - tt);
     uint32_t lanes[64];
     for (int lane = 0; lane < 64; ++lane) {
       uint32_t state = 0;
-      for (int k = 0; k < kCrcRounds; ++k) {
+      for (int k = 0; k < rounds; ++k) {
         if (k) state = shift4(t.lane_shift[6], state);
         for (int j = 0; j < kCrcChunkPieces; ++j) {
           const intptr_t p = tstart + static_cast<intptr_t>(kCrcRoundBytes) * k +
@@ -94,34 +112,46 @@ CrcSegResult emulate_crc32c_segment(const uint8_t* addr_p, uint32_t len, const C
     }
     tiles[tt] = lanes[0];
   }
-  // K2
-  uint32_t acc[256];
-  const int M = static_cast<int>((T + 255) >> 8);
-  for (int k = 0; k < 256; ++k) {
+  // fold: W waves, thread k folds tiles T-1-(k + S m) by Horner with stride
+  // S = 64 W tiles, then a tree over the 64 W threads (shift 2^lv tiles)
+  const int W = fold_waves;
+  int logw = 0;
+  while ((1 << logw) < W) ++logw;
+  const int S = 64 * W;
+  std::vector<uint32_t> acc(static_cast<size_t>(S));
+  const int M = static_cast<int>((T + S - 1) / S);
+  for (int k = 0; k < S; ++k) {
     uint32_t a = 0;
     for (int m = M - 1; m >= 0; --m) {
-      a = shift4(t.tile_shift[8], a);
-      uint32_t j = static_cast<uint32_t>(k) + 256u * static_cast<uint32_t>(m);
+      a = shift4(t.tile_shift[lvl0 + 6 + logw], a);
+      uint32_t j = static_cast<uint32_t>(k) + static_cast<uint32_t>(S) * static_cast<uint32_t>(m);
       if (j < T) a ^= tiles[T - 1 - j];
     }
-    acc[k] = a;
+    acc[static_cast<size_t>(k)] = a;
   }
-  for (int lv = 0; lv < 8; ++lv)
-    for (int k = 0; k < 256; k += (2 << lv)) acc[k] ^= shift4(t.tile_shift[lv], acc[k + (1 << lv)]);
+  for (int lv = 0; lv < 6 + logw; ++lv)
+    for (int k = 0; k < S; k += (2 << lv)) acc[k] ^= shift4(t.tile_shift[lvl0 + lv], acc[k + (1 << lv)]);
   uint32_t raw = acc[0];
+  // tail: the last 1..16 bytes, slice-by-r with one independent lookup per byte
   if (len > 0) {
     const uintptr_t a16 = addr & ~uintptr_t(15);
     const uintptr_t e = addr + len;
     const uintptr_t vend = a16 + 16 * ((e - a16 + 15) / 16 - 1);
-    for (uintptr_t p = vend > addr ? vend : addr; p < e; ++p)
-      raw = (raw >> 8) ^ t.slice16[0][(raw ^ *reinterpret_cast<const uint8_t*>(p)) & 0xff];
+    const uintptr_t p0 = vend > addr ? vend : addr;
+    const int r = static_cast<int>(e - p0);
+    uint32_t x = 0;
+    for (int i = 0; i < r; ++i) {
+      const uint32_t sb = i < 4 ? (raw >> (8 * i)) & 0xff : 0;
+      x ^= t.slice16[r - 1 - i][(*reinterpret_cast<const uint8_t*>(p0 + i) ^ sb) & 0xff];
+    }
+    raw = x ^ (r < 4 ? raw >> (8 * r) : 0u);
   }
-  CrcSegResult r;
-  r.raw = raw;
-  r.crc = raw ^ crc32c_fixup(len);
-  r.status = check ? (r.crc == expected ? 1u : 2u) : 0u;
-  r.pad = 0;
-  return r;
+  CrcSegResult res;
+  res.raw = raw;
+  res.crc = raw ^ crc32c_fixup(len);
+  res.status = check ? (res.crc == expected ? 1u : 2u) : 0u;
+  res.pad = 0;
+  return res;
 }
 
 }  // namespace gcsb

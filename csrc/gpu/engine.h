@@ -227,7 +227,9 @@ uint32_t gpu_crc32c(int device, const void* dptr, size_t n, size_t chunk = 0,
                     std::vector<uint32_t>* chunks = nullptr);
 // Kernel throughput probe: K1+K2 over [dptr, dptr+n) in segments of
 // seg_bytes (<= kMaxSeg of them), `iters` back-to-back batches, GB/s.
-double gpu_crc32c_throughput(int device, const void* dptr, size_t n, int iters, size_t seg_bytes, uint32_t* crc0);
+// tile_log2: 0 = automatic (finalize_crc_batch), 12 / 14 forces 4 / 16 KiB tiles.
+double gpu_crc32c_throughput(int device, const void* dptr, size_t n, int iters, size_t seg_bytes, uint32_t* crc0,
+                             int tile_log2 = 0);
 // Fill / verify device memory with synthetic object bytes.
 void gpu_fill_pattern(int device, void* dptr, uint64_t n, uint64_t rot, uint64_t obj_off);
 uint64_t gpu_verify_pattern(int device, const void* dptr, uint64_t n, uint64_t rot, uint64_t obj_off,

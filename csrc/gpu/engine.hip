@@ -189,8 +189,8 @@ GpuSink::GpuSink(const GpuSinkConfig& cfg) : cfg_(cfg) {
   hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
   hip_check(hipStreamCreateWithFlags(&crc_stream_, hipStreamNonBlocking), "hipStreamCreate");
   d_tables_ = device_crc_tables(cfg_.device);
-  tiles_cap_ = cfg_.slot_bytes / kCrcTile + 2 * kMaxSeg + 8;
-  hip_check(hipMalloc(reinterpret_cast<void**>(&d_tiles_), tiles_cap_ * sizeof(uint32_t)), "hipMalloc(tiles)");
+  tiles_cap_ = cfg_.slot_bytes / kCrcMinTile + 2 * kMaxSeg + 8;
+  d_tiles_ = crc_scratch_alloc(tiles_cap_);
   hip_check(hipHostMalloc(reinterpret_cast<void**>(&res_host_), sizeof(CrcSegResult) * kMaxSeg * cfg_.slots,
                           hipHostMallocMapped | hipHostMallocCoherent),
             "hipHostMalloc(results)");
@@ -727,7 +727,8 @@ uint32_t gpu_crc32c(int device, const void* dptr, size_t n, size_t chunk, std::v
   // kMaxSeg segments per batch (>= 1 MiB, 4 KiB multiples): K1 covers every
   // tile in parallel and K2 folds with kMaxSeg workgroups, not one.
   size_t seg = (n + kMaxSeg - 1) / kMaxSeg;
-  seg = std::min<size_t>(std::max<size_t>((seg + kCrcTile - 1) / kCrcTile * kCrcTile, 1u << 20), 1u << 30);
+  seg = std::min<size_t>(std::max<size_t>((seg + kCrcRoundBytes - 1) / kCrcRoundBytes * kCrcRoundBytes, 1u << 20),
+                         1u << 30);
   if (chunk > 0) {
     seg = std::min<size_t>(chunk, 1u << 30);
     if (chunks) chunks->reserve(chunks->size() + (n + seg - 1) / seg);
@@ -746,10 +747,10 @@ uint32_t gpu_crc32c(int device, const void* dptr, size_t n, size_t chunk, std::v
       off += len;
     }
     finalize_crc_batch(&b);
-    if (b.total_tiles + 1 > c.tiles_cap) {
+    if (b.total_tiles + 1 > c.tiles_cap || !c.d_tiles) {
       if (c.d_tiles) (void)hipFree(c.d_tiles);
       c.tiles_cap = b.total_tiles + 1;
-      hip_check(hipMalloc(reinterpret_cast<void**>(&c.d_tiles), sizeof(uint32_t) * c.tiles_cap), "hipMalloc(tiles)");
+      c.d_tiles = crc_scratch_alloc(c.tiles_cap);
     }
     launch_crc32c_batch(b, tabs, c.d_tiles, c.d_res, c.st);
     hip_check(hipStreamSynchronize(c.st), "hipStreamSynchronize");
@@ -761,7 +762,8 @@ uint32_t gpu_crc32c(int device, const void* dptr, size_t n, size_t chunk, std::v
   return crc;
 }
 
-double gpu_crc32c_throughput(int device, const void* dptr, size_t n, int iters, size_t seg_bytes, uint32_t* raw0) {
+double gpu_crc32c_throughput(int device, const void* dptr, size_t n, int iters, size_t seg_bytes, uint32_t* raw0,
+                             int tile_log2) {
   hip_check(hipSetDevice(device), "hipSetDevice");
   const CrcTables* tabs = device_crc_tables(device);
   hipStream_t st;
@@ -778,9 +780,8 @@ double gpu_crc32c_throughput(int device, const void* dptr, size_t n, int iters, 
     ++b.nseg;
     off += len;
   }
-  finalize_crc_batch(&b);
-  uint32_t* d_tiles = nullptr;
-  hip_check(hipMalloc(reinterpret_cast<void**>(&d_tiles), sizeof(uint32_t) * (b.total_tiles + 1)), "hipMalloc");
+  finalize_crc_batch(&b, static_cast<uint32_t>(tile_log2));
+  uint32_t* d_tiles = crc_scratch_alloc(b.total_tiles + 1);
   CrcSegResult* res = nullptr;
   hip_check(hipHostMalloc(reinterpret_cast<void**>(&res), sizeof(CrcSegResult) * kMaxSeg,
                           hipHostMallocMapped | hipHostMallocCoherent),

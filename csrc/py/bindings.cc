@@ -639,16 +639,21 @@ PYBIND11_MODULE(_native, m) {
   m.def("crc32c_hw_available", &crc32c_hw_available);
   m.def(
       "emulate_gpu_crc32c",
-      [](const py::bytes& b, size_t misalign, uint32_t expected, bool check) {
+      [](const py::bytes& b, size_t misalign, uint32_t expected, bool check, uint32_t tile_log2, int fold_waves) {
         std::string s = b;
         std::vector<uint8_t> buf(s.size() + 64);
         uint8_t* base = reinterpret_cast<uint8_t*>((reinterpret_cast<uintptr_t>(buf.data()) + 15) & ~uintptr_t(15));
         uint8_t* p = base + (misalign % 16);
         std::memcpy(p, s.data(), s.size());
-        CrcSegResult r = emulate_crc32c_segment(p, static_cast<uint32_t>(s.size()), host_tables(), expected, check);
+        if (tile_log2 != kCrcMinTileLog2 && tile_log2 != kCrcMaxTileLog2)
+          throw std::invalid_argument("tile_log2 must be 12 or 14");
+        if (fold_waves != 1 && fold_waves != 8) throw std::invalid_argument("fold_waves must be 1 or 8");
+        CrcSegResult r = emulate_crc32c_segment(p, static_cast<uint32_t>(s.size()), host_tables(), expected, check,
+                                                tile_log2, fold_waves);
         return py::make_tuple(r.raw, r.crc, r.status);
       },
-      py::arg("data"), py::arg("misalign") = 0, py::arg("expected") = 0, py::arg("check") = false);
+      py::arg("data"), py::arg("misalign") = 0, py::arg("expected") = 0, py::arg("check") = false,
+      py::arg("tile_log2") = kCrcMaxTileLog2, py::arg("fold_waves") = 8);
   m.def("object_rotation", &object_rotation);
   m.def("object_bytes", [](const std::string& name, uint64_t off, uint64_t n) {
     std::string out(n, '\0');
@@ -785,16 +790,17 @@ PYBIND11_MODULE(_native, m) {
   });
   m.def(
       "gpu_crc32c_throughput",
-      [](int dev, uintptr_t ptr, size_t n, int iters, size_t seg_bytes) {
+      [](int dev, uintptr_t ptr, size_t n, int iters, size_t seg_bytes, int tile_log2) {
         uint32_t c0 = 0;
         double gbs;
         {
           py::gil_scoped_release nogil;
-          gbs = gpu_crc32c_throughput(dev, reinterpret_cast<const void*>(ptr), n, iters, seg_bytes, &c0);
+          gbs = gpu_crc32c_throughput(dev, reinterpret_cast<const void*>(ptr), n, iters, seg_bytes, &c0, tile_log2);
         }
         return py::make_tuple(gbs, c0);
       },
-      py::arg("device"), py::arg("ptr"), py::arg("n"), py::arg("iters") = 20, py::arg("seg_bytes") = 64u << 20);
+      py::arg("device"), py::arg("ptr"), py::arg("n"), py::arg("iters") = 20, py::arg("seg_bytes") = 64u << 20,
+      py::arg("tile_log2") = 0);
   m.def("gpu_read_bytes",[](int dev, uintptr_t ptr, size_t n) {
     std::string out(n, '\0');
     {

@@ -37,20 +37,25 @@ def test_large_buffer_interleaved_path(native):
 @pytest.mark.parametrize("misalign", [0, 1, 3, 8, 15])
 @pytest.mark.parametrize("n", [0, 1, 15, 16, 17, 255, 256, 257, 4095, 4096, 4097, 16383, 16384, 16385, 16400,
                                65536 + 5, (1 << 20) + 3])
-def test_gpu_algorithm_emulation(native, misalign, n):
+@pytest.mark.parametrize("geom", [(14, 8), (12, 1), (14, 1), (12, 8)])
+def test_gpu_algorithm_emulation(native, misalign, n, geom):
+    """Kernel math on the CPU: 16 KiB / 4 KiB tiles x fused (1 wave per
+    segment) / separate (8 waves per segment) fold, parallel 1..16 B tail."""
+    tl, fw = geom
     d = os.urandom(n)
     want = native.crc32c(d)
-    raw, crc, status = native.emulate_gpu_crc32c(d, misalign, want, True)
+    raw, crc, status = native.emulate_gpu_crc32c(d, misalign, want, True, tl, fw)
     assert crc == want and status == 1
     assert raw == native.crc32c_raw(d)
-    _, _, bad = native.emulate_gpu_crc32c(d, misalign, want ^ 1, True)
+    _, _, bad = native.emulate_gpu_crc32c(d, misalign, want ^ 1, True, tl, fw)
     assert bad == 2
 
 
-def test_emulation_multi_megabyte_tile_fold(native):
-    # > 256 tiles exercises the strided Horner (256-tile shift) in K2
+@pytest.mark.parametrize("geom", [(14, 8), (12, 1), (14, 1)])
+def test_emulation_multi_megabyte_tile_fold(native, geom):
+    # more tiles than fold threads exercises the strided Horner step
     d = os.urandom(9 * (1 << 20) + 999)
-    raw, crc, _ = native.emulate_gpu_crc32c(d, 5, 0, False)
+    raw, crc, _ = native.emulate_gpu_crc32c(d, 5, 0, False, *geom)
     assert crc == native.crc32c(d)
 
 

@@ -433,7 +433,12 @@ uint32_t* crc_scratch_alloc(uint64_t tiles) {
   uint32_t* p = nullptr;
   const size_t bytes = sizeof(uint32_t) * crc_scratch_words(tiles);
   hip_check(hipMalloc(reinterpret_cast<void**>(&p), bytes), "hipMalloc(crc scratch)");
-  hip_check(hipMemset(p, 0, sizeof(uint32_t) * kCrcScratchHeader), "hipMemset(crc scratch)");
+  // all of it: callers carve per-slot scratches (each with its own header
+  // counter) out of one allocation
+  // hipMemset may still be running when it returns, and the kernels that use
+  // this scratch go on non-blocking streams that do not order after it: wait
+  hip_check(hipMemsetAsync(p, 0, bytes, nullptr), "hipMemsetAsync(crc scratch)");
+  hip_check(hipStreamSynchronize(nullptr), "hipStreamSynchronize(crc scratch)");
   return p;
 }
 

@@ -9,6 +9,15 @@
 // read's timer stops in finish() once the last slot's event has fired: every
 // byte is in HBM and every checksum the server sent has been checked.
 //
+// Streams (round 2): every sink and upload source of a process draws from ONE
+// per-device pool of GCSB_STREAMS (default 8; 0 = a private stream per sink)
+// non-blocking streams.  A slot's H2D copy, its CRC launch and its
+// completion event go on one pool stream, in order, so no cross-stream event
+// wait exists; consecutive slots of a sink use consecutive pool streams, so
+// slot i's CRC overlaps slot i+1's copy.  Round 1 gave every sink two streams
+// of its own (32 streams with 8 sliced streams x 2 sinks, multiplexed on 4
+// hardware queues, where one stream's event wait head-of-line blocks others).
+//
 // Slot state machine (debuggable with GCSB_DEBUG_RING=1 asserts):
 //   FREE -> FILLING (transport writes) -> INFLIGHT (copy+kernels queued)
 //        -> harvested (event complete, results folded) -> FREE
@@ -74,7 +83,6 @@ class GpuSink : public Sink {
   void set_external_destination(void* dptr, size_t cap);
   void* object_device_ptr() const { return obj_dst_; }
   size_t object_capacity() const { return obj_cap_; }
-  hipStream_t stream() const { return stream_; }
   const GpuSinkStats& stats() const { return stats_; }
   const GpuSinkConfig& config() const { return cfg_; }
 
@@ -106,8 +114,9 @@ class GpuSink : public Sink {
     size_t used = 0;
     uint64_t obj_off = 0;
     std::vector<SegInfo> segs;
-    hipEvent_t ev = nullptr;      // slot done: copy landed + CRC kernels finished
-    hipEvent_t copied = nullptr;  // copy landed (CRC stream waits on it)
+    hipStream_t st = nullptr;     // device pool stream: this slot's copy, CRC launch and event, in order
+    hipEvent_t ev = nullptr;      // slot done: copy landed + CRC kernel finished
+    uint32_t* tiles = nullptr;    // this slot's CRC tile scratch (slots on different streams run concurrently)
     bool inflight = false;
     bool submitted = false;       // async: the submitter has recorded `ev` (guarded by sub_mu_)
     CrcSegResult* res = nullptr;  // host-mapped, kMaxSeg entries
@@ -124,14 +133,13 @@ class GpuSink : public Sink {
   void set_device() const;
 
   GpuSinkConfig cfg_;
-  hipStream_t stream_ = nullptr;      // H2D copies
-  hipStream_t crc_stream_ = nullptr;  // CRC32C kernels
   std::vector<Slot> slots_;
   int cur_ = -1;         // FILLING slot index or -1
   int next_ = 0;         // next slot to take
   const CrcTables* d_tables_ = nullptr;
-  uint32_t* d_tiles_ = nullptr;
-  size_t tiles_cap_ = 0;
+  hipStream_t own_stream_ = nullptr;  // GCSB_STREAMS=0: private stream instead of the pool
+  uint32_t* d_tiles_ = nullptr;  // slots x tile scratch
+  size_t tiles_cap_ = 0;         // tiles per slot scratch
   CrcSegResult* res_host_ = nullptr;
   uint8_t* own_obj_ = nullptr;
   uint8_t* obj_dst_ = nullptr;
@@ -180,12 +188,14 @@ class GpuByteSource : public ByteSource {
  private:
   void restart(uint64_t off);
   void issue(int slot, uint64_t off);
+  void wait_all();
   int device_;
   const uint8_t* src_;
   uint64_t n_;
   size_t slot_bytes_;
   int nslots_;
-  hipStream_t stream_ = nullptr;
+  std::vector<hipStream_t> st_;  // per slot, from the device stream pool
+  hipStream_t own_stream_ = nullptr;
   std::vector<uint8_t*> host_;
   std::vector<hipEvent_t> ev_;
   std::vector<uint64_t> slot_off_;  // object offset held by each slot (~0 = idle)

@@ -2,6 +2,7 @@
 #include "gpu/engine.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -174,6 +175,38 @@ class DeviceSubmitter {
 };
 }  // namespace
 
+// Per-device stream pool shared by every sink / upload source (engine.h).
+class DeviceStreamPool {
+ public:
+  static DeviceStreamPool& get(int dev) {
+    static std::mutex mu;
+    static std::map<int, DeviceStreamPool*> all;  // process lifetime
+    std::lock_guard<std::mutex> lk(mu);
+    auto& p = all[dev];
+    if (!p) p = new DeviceStreamPool(dev);
+    return *p;
+  }
+  hipStream_t at(unsigned i) const { return st_[i % st_.size()]; }
+  unsigned next_base() { return rr_.fetch_add(1); }
+  // GCSB_STREAMS=0: no pool, every sink / source owns one private stream
+  // (A/B switch against the shared pool).
+  bool private_streams() const { return st_.empty(); }
+
+ private:
+  explicit DeviceStreamPool(int dev) {
+    // 8: sliced reads (16 sinks) p99 6.0-6.2 ms vs 6.7-13.3 with 4 and
+    // 10-16 with a private stream per sink; one stream per read: equal within
+    // run-to-run spread (profiles/r2_streams_ab)
+    int n = 8;
+    if (const char* e = std::getenv("GCSB_STREAMS")) n = std::max(0, std::min(32, std::atoi(e)));
+    ensure_device(dev);
+    st_.resize(static_cast<size_t>(n));
+    for (auto& st : st_) hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate(pool)");
+  }
+  std::vector<hipStream_t> st_;
+  std::atomic<unsigned> rr_{0};
+};
+
 void GpuSink::set_device() const { ensure_device(cfg_.device); }
 
 GpuSink::GpuSink(const GpuSinkConfig& cfg) : cfg_(cfg) {
@@ -183,14 +216,13 @@ GpuSink::GpuSink(const GpuSinkConfig& cfg) : cfg_(cfg) {
   cfg_.slot_bytes = (cfg_.slot_bytes + 4095) / 4096 * 4096;
   if (cfg_.slot_bytes < 65536) cfg_.slot_bytes = 65536;
   set_device();
-  // Two streams: back-to-back SDMA copies on one, CRC kernels on the other
-  // (each slot's kernels wait on that slot's copy event), so checksumming
-  // slot i overlaps the copy of slot i+1 instead of serializing behind it.
-  hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
-  hip_check(hipStreamCreateWithFlags(&crc_stream_, hipStreamNonBlocking), "hipStreamCreate");
+  DeviceStreamPool& pool = DeviceStreamPool::get(cfg_.device);
+  const unsigned base = pool.next_base() * static_cast<unsigned>(cfg_.slots);
+  if (pool.private_streams())
+    hip_check(hipStreamCreateWithFlags(&own_stream_, hipStreamNonBlocking), "hipStreamCreate");
   d_tables_ = device_crc_tables(cfg_.device);
   tiles_cap_ = cfg_.slot_bytes / kCrcMinTile + 2 * kMaxSeg + 8;
-  d_tiles_ = crc_scratch_alloc(tiles_cap_);
+  d_tiles_ = crc_scratch_alloc(crc_scratch_words(tiles_cap_) * cfg_.slots);
   hip_check(hipHostMalloc(reinterpret_cast<void**>(&res_host_), sizeof(CrcSegResult) * kMaxSeg * cfg_.slots,
                           hipHostMallocMapped | hipHostMallocCoherent),
             "hipHostMalloc(results)");
@@ -205,7 +237,8 @@ GpuSink::GpuSink(const GpuSinkConfig& cfg) : cfg_(cfg) {
       hip_check(hipMalloc(reinterpret_cast<void**>(&s.dev_ring), cfg_.slot_bytes), "hipMalloc(ring slot)");
     const unsigned evf = hipEventDisableTiming | (cfg_.blocking_sync ? hipEventBlockingSync : 0u);
     hip_check(hipEventCreateWithFlags(&s.ev, evf), "hipEventCreate");
-    hip_check(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming), "hipEventCreate");
+    s.st = own_stream_ ? own_stream_ : pool.at(base + static_cast<unsigned>(i));
+    s.tiles = d_tiles_ + crc_scratch_words(tiles_cap_) * static_cast<size_t>(i);
     s.res = res_host_ + static_cast<size_t>(i) * kMaxSeg;
     hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&s.d_res), s.res, 0), "hipHostGetDevicePointer");
   }
@@ -215,27 +248,22 @@ GpuSink::~GpuSink() {
   try {
     for (Slot& sl : slots_) wait_slot(sl);  // no queued hand-off may outlive the sink
     set_device();
-    if (stream_) (void)hipStreamSynchronize(stream_);
-    if (crc_stream_) (void)hipStreamSynchronize(crc_stream_);
   } catch (...) {
   }
   for (Slot& s : slots_) {
     PinnedPool::put(s.host, cfg_.slot_bytes);
     if (s.dev_ring) (void)hipFree(s.dev_ring);
     if (s.ev) (void)hipEventDestroy(s.ev);
-    if (s.copied) (void)hipEventDestroy(s.copied);
   }
-  if (crc_stream_) (void)hipStreamDestroy(crc_stream_);
   if (res_host_) (void)hipHostFree(res_host_);
   if (d_tiles_) (void)hipFree(d_tiles_);
   if (own_obj_) (void)hipFree(own_obj_);
-  if (stream_) (void)hipStreamDestroy(stream_);
+  if (own_stream_) (void)hipStreamDestroy(own_stream_);
 }
 
 void GpuSink::set_external_destination(void* dptr, size_t cap) {
   set_device();
-  hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
-  hip_check(hipStreamSynchronize(crc_stream_), "hipStreamSynchronize");
+  for (Slot& sl : slots_) wait_slot(sl);  // this sink's queued work (its slot events), not the shared streams
   if (own_obj_) {
     (void)hipFree(own_obj_);
     own_obj_ = nullptr;
@@ -260,8 +288,6 @@ void GpuSink::grow_object_buffer(uint64_t need) {
     throw StorageError("object larger than the external HBM destination (" + std::to_string(obj_cap_) + " B)", false);
   set_device();
   for (int k = 0; k < cfg_.slots; ++k) wait_slot(slots_[(next_ + k) % cfg_.slots]);
-  hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
-  hip_check(hipStreamSynchronize(crc_stream_), "hipStreamSynchronize");
   const uint64_t landed = cur_ >= 0 ? slots_[cur_].obj_off : delivered_;
   size_t cap = (need + (2u << 20) - 1) / (2u << 20) * (2u << 20);
   uint8_t* nb = nullptr;
@@ -450,15 +476,10 @@ void GpuSink::submit_current() {
 void GpuSink::enqueue_slot(Slot& s, uint8_t* dst, const CrcBatch* batch) {
   auto issue = [this, &s, dst](const CrcBatch* b) {
     ensure_device(cfg_.device);
-    hip_check(hipMemcpyAsync(dst, s.host, s.used, hipMemcpyHostToDevice, stream_), "hipMemcpyAsync(H2D)");
-    if (b) {
-      hip_check(hipEventRecord(s.copied, stream_), "hipEventRecord");
-      hip_check(hipStreamWaitEvent(crc_stream_, s.copied, 0), "hipStreamWaitEvent");
-      launch_crc32c_batch(*b, d_tables_, d_tiles_, s.d_res, crc_stream_);
-      hip_check(hipEventRecord(s.ev, crc_stream_), "hipEventRecord");
-    } else {
-      hip_check(hipEventRecord(s.ev, stream_), "hipEventRecord");
-    }
+    // copy, CRC and completion event in one stream's order: no cross-stream wait
+    hip_check(hipMemcpyAsync(dst, s.host, s.used, hipMemcpyHostToDevice, s.st), "hipMemcpyAsync(H2D)");
+    if (b) launch_crc32c_batch(*b, d_tables_, s.tiles, s.d_res, s.st);
+    hip_check(hipEventRecord(s.ev, s.st), "hipEventRecord");
   };
   if (!cfg_.async_submit) {
     s.submitted = true;
@@ -603,7 +624,12 @@ GpuByteSource::GpuByteSource(int device, const void* dptr, uint64_t n, size_t sl
       slot_bytes_(std::max<size_t>(std::min<uint64_t>(slot_bytes, (n + 65535) / 65536 * 65536), 65536)),
       nslots_(std::max(2, slots)) {
   hip_check(hipSetDevice(device_), "hipSetDevice");
-  hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
+  DeviceStreamPool& pool = DeviceStreamPool::get(device_);
+  const unsigned base = pool.next_base() * static_cast<unsigned>(nslots_);
+  if (pool.private_streams())
+    hip_check(hipStreamCreateWithFlags(&own_stream_, hipStreamNonBlocking), "hipStreamCreate");
+  st_.resize(nslots_);
+  for (int i = 0; i < nslots_; ++i) st_[i] = own_stream_ ? own_stream_ : pool.at(base + static_cast<unsigned>(i));
   host_.resize(nslots_);
   ev_.resize(nslots_);
   slot_off_.assign(nslots_, ~0ull);
@@ -638,26 +664,35 @@ bool GpuByteSource::range_crc32c(uint64_t off, size_t len, uint32_t* crc) {
 }
 
 GpuByteSource::~GpuByteSource() {
-  if (stream_) (void)hipStreamSynchronize(stream_);
+  try {
+    wait_all();
+  } catch (...) {
+  }
   for (int i = 0; i < nslots_; ++i) {
     PinnedPool::put(host_[i], slot_bytes_);
     if (ev_[i]) (void)hipEventDestroy(ev_[i]);
   }
-  if (stream_) (void)hipStreamDestroy(stream_);
+  if (own_stream_) (void)hipStreamDestroy(own_stream_);
+}
+
+// This source's queued copies (its slot events; the pool streams are shared).
+void GpuByteSource::wait_all() {
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  for (int i = 0; i < nslots_; ++i)
+    if (slot_off_[i] != ~0ull) hip_check(hipEventSynchronize(ev_[i]), "hipEventSynchronize");
 }
 
 void GpuByteSource::issue(int slot, uint64_t off) {
   size_t len = static_cast<size_t>(std::min<uint64_t>(slot_bytes_, n_ - off));
   slot_off_[slot] = off;
   slot_len_[slot] = len;
-  hip_check(hipMemcpyAsync(host_[slot], src_ + off, len, hipMemcpyDeviceToHost, stream_), "hipMemcpyAsync(D2H)");
-  hip_check(hipEventRecord(ev_[slot], stream_), "hipEventRecord");
+  hip_check(hipMemcpyAsync(host_[slot], src_ + off, len, hipMemcpyDeviceToHost, st_[slot]), "hipMemcpyAsync(D2H)");
+  hip_check(hipEventRecord(ev_[slot], st_[slot]), "hipEventRecord");
   ++copies_;
 }
 
 void GpuByteSource::restart(uint64_t off) {
-  hip_check(hipSetDevice(device_), "hipSetDevice");
-  hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+  wait_all();
   pos_ = off;
   uint64_t base = off / slot_bytes_ * slot_bytes_;
   next_issue_ = base;

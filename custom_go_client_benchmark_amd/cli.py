@@ -30,7 +30,7 @@ import time
 
 from . import _native
 from .models import workloads
-from .utils import metrics_exporter, trace_exporter
+from .utils import cpuacct, metrics_exporter, trace_exporter
 from .utils.goflags import FlagSet
 
 
@@ -229,6 +229,8 @@ def main(argv: list[str] | None = None) -> int:
             tracer.on_records(recs)
 
     t0 = time.perf_counter()
+    cg0 = cpuacct.cgroup_cpu_stat()
+    th0 = cpuacct.thread_cpu()
     rc = 0
     try:
         wl = fs.get("workload")
@@ -256,6 +258,9 @@ def main(argv: list[str] | None = None) -> int:
                 pass
     wall = time.perf_counter() - t0
     s = res.summary
+    s.update(cpuacct.cgroup_delta(cg0, cpuacct.cgroup_cpu_stat()))
+    s["cpu_s_by_group"] = {k: round(v, 4) for k, v in
+                           cpuacct.delta_by_group(th0, cpuacct.thread_cpu()).items()}
     if exporter:
         exporter.close()  # flushes (reference Q2)
     if trace_cleanup:
@@ -283,6 +288,7 @@ def main(argv: list[str] | None = None) -> int:
                  f"p99 {['%.2f' % x for x in st['p99_per_rank']]} ms")
     if fs.get("summary-json") and rank == 0:
         out = {k: v for k, v in s.items() if isinstance(v, (int, float, str, bool))}
+        out["cpu_s_by_group"] = s.get("cpu_s_by_group", {})
         out.update({"workload": fs.get("workload"), "protocol": proto, "sink": sink, "workers": workers,
                     "world": world, "wall_s": wall, "extra": res.extra})
         if ctx is not None and ctx.world > 1:

@@ -79,3 +79,29 @@ def delta_by_group(before: dict[str, float], after: dict[str, float]) -> dict[st
 def per_gib(groups: dict[str, float], nbytes: float) -> dict[str, float]:
     gib = max(nbytes, 1.0) / (1 << 30)
     return {k: round(v / gib, 4) for k, v in sorted(groups.items())}
+
+
+def cgroup_cpu_stat() -> dict[str, int]:
+    """The container's CFS counters (cgroup v2 cpu.stat): on the GPU boxes the
+    benchmark runs under a CPU quota, and a period whose quota is spent stalls
+    every thread until the next one -- a latency tail of tens of ms."""
+    out: dict[str, int] = {}
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            for line in f:
+                k, _, v = line.partition(" ")
+                if k in ("usage_usec", "nr_periods", "nr_throttled", "throttled_usec"):
+                    out[k] = int(v)
+    except OSError:
+        pass
+    return out
+
+
+def cgroup_delta(a: dict[str, int], b: dict[str, int]) -> dict[str, float]:
+    out: dict[str, float] = {}
+    for k in ("nr_periods", "nr_throttled"):
+        if k in a and k in b:
+            out["cgroup_" + k] = b[k] - a[k]
+    if "throttled_usec" in a and "throttled_usec" in b:
+        out["cgroup_throttled_ms"] = (b["throttled_usec"] - a["throttled_usec"]) / 1e3
+    return out

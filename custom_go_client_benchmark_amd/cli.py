@@ -93,7 +93,7 @@ def build_flags() -> FlagSet:
     fs.float("retry-multiplier", 2.0, "Backoff multiplier (reference RetryMultiplier 2)")
     fs.duration("retry-max-total", 0.0, "Give up retrying after this long (0 = never, as the reference)")
     fs.int("retry-max-attempts", 0, "Give up after this many attempts (0 = unlimited)")
-    fs.string("affinity", "auto", "CPU placement: auto | share | same | split | numa | none")
+    fs.string("affinity", "auto", "CPU placement: auto | quota | share | same | split | numa | none")
     fs.bool("start-fake-server", False, "Start a node-local synthetic GCS endpoint (no network)")
     fs.int("fake-object-size", 100 << 20, "Synthetic object size (reference objects are ~100 MB)")
     fs.int("fake-objects", -1, "Synthetic objects per rank (default: -worker)")
@@ -134,13 +134,15 @@ def main(argv: list[str] | None = None) -> int:
     placement = {"client": [], "server": []}
     aff = fs.get("affinity")
     if aff == "auto":
-        aff = ("share" if fs.get("slices") > 1 else "same") if sink == "gpu" else "none"
+        # discard sink: no GPU to be near; under a CPU quota keep the threads
+        # on as many cores as the quota pays for (parallel/affinity.py)
+        aff = ("share" if fs.get("slices") > 1 else "same") if sink == "gpu" else "quota"
         if fs.get("workload") == "write":
             # uploads: unpinned threads measured fastest on MI355X (64 MiB
             # WriteObject 8.1 ms vs 13.8-14.4 ms pinned; resumable HTTP 6.5 vs
             # 6.7-7.8 ms), profiles/r1_session4/
             aff = "none"
-    if aff != "none" and sink == "gpu":
+    if aff != "none" and (sink == "gpu" or aff == "quota"):
         from .parallel import affinity
 
         placement = affinity.plan(device, aff)

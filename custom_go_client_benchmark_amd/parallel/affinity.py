@@ -57,10 +57,64 @@ def l3_groups(cpus: list[int]) -> list[list[int]]:
     return sorted(groups.values(), key=lambda g: g[0])
 
 
+def cpu_quota() -> float:
+    """CPUs' worth of the container's CFS quota (cgroup v2 cpu.max), 0 if
+    unlimited.  The GPU boxes run under one (16 CPUs per GPU,
+    profiles/r1_gpu_box_env.txt)."""
+    v = _read("/sys/fs/cgroup/cpu.max")
+    if not v:
+        return 0.0
+    parts = v.split()
+    if len(parts) != 2 or parts[0] == "max":
+        return 0.0
+    try:
+        return float(parts[0]) / float(parts[1])
+    except ValueError:
+        return 0.0
+
+
+def core_first(cpus: list[int]) -> list[int]:
+    """cpus reordered so one hardware thread of every physical core comes
+    before any SMT sibling (a receive thread gets a core to itself first)."""
+    seen, first, rest = set(), [], []
+    for c in cpus:
+        core = (_read(f"/sys/devices/system/cpu/cpu{c}/topology/physical_package_id"),
+                _read(f"/sys/devices/system/cpu/cpu{c}/topology/core_id"))
+        if core[1] is None or core not in seen:
+            seen.add(core)
+            first.append(c)
+        else:
+            rest.append(c)
+    return first + rest
+
+
+def quota_budget() -> int:
+    """CPUs one rank may keep busy without the container being throttled:
+    the CFS quota split over the node's ranks (LOCAL_WORLD_SIZE), 0 = no
+    limit.  Running more threads than this at once buys no throughput -- the
+    quota caps it -- but every quota-exhausted period stalls all threads for
+    the rest of the period: tens of ms of p99 (profiles/r2_streams_ab/w48.txt:
+    48 HTTP workers unpinned, 3 of 3 periods throttled, p99 36-46 ms)."""
+    q = cpu_quota()
+    if q <= 0:
+        return 0
+    ranks = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1))
+    return max(2, int(q // ranks))
+
+
+def trim_to_quota(cpus: list[int]) -> list[int]:
+    b = quota_budget()
+    if b <= 0 or len(cpus) <= b:
+        return cpus
+    return sorted(core_first(cpus)[:b])
+
+
 def plan(device: int, mode: str = "split") -> dict:
     """CPU sets for this rank: {"client": [...], "server": [...]}.
 
-    mode: "share" (this rank's fair share of its NUMA node's L3 domains --
+    mode: "quota" (no GPU locality: as many cores as the container's CPU
+                   quota allows this rank, see quota_budget),
+          "share" (this rank's fair share of its NUMA node's L3 domains --
                    node L3 domains / GPUs on the node -- shared by client and
                    endpoint threads: all 8 domains on a 1-GPU box, 2 per rank
                    on a full 8-GPU node; best for sliced reads),
@@ -69,6 +123,10 @@ def plan(device: int, mode: str = "split") -> dict:
     """
     if mode == "none":
         return {"client": [], "server": [], "mode": mode}
+    if mode == "quota":
+        # no GPU locality: the first quota-budget cores this process may use
+        mine = trim_to_quota(sorted(os.sched_getaffinity(0)))
+        return {"client": mine, "server": mine, "mode": mode, "quota_cpus": quota_budget()}
     cpus = gpu_local_cpus(device)
     if mode == "numa":
         return {"client": cpus, "server": cpus, "mode": mode}
@@ -83,9 +141,9 @@ def plan(device: int, mode: str = "split") -> dict:
     share = max(1, len(groups) // max(1, len(peers)))
     base = (k * share) % max(1, len(groups))
     if mode == "share":
-        mine = [c for g in groups[base:base + share] for c in g] or cpus
+        mine = trim_to_quota([c for g in groups[base:base + share] for c in g] or cpus)
         return {"client": mine, "server": mine, "mode": mode, "numa_node": node, "gpu_index_on_node": k,
-                "l3_domains": share}
+                "l3_domains": share, "quota_cpus": quota_budget()}
     client = groups[base] if groups else cpus
     if mode == "same" or share < 2:
         server = client

@@ -141,9 +141,13 @@ def plan(device: int, mode: str = "split") -> dict:
     share = max(1, len(groups) // max(1, len(peers)))
     base = (k * share) % max(1, len(groups))
     if mode == "share":
-        mine = trim_to_quota([c for g in groups[base:base + share] for c in g] or cpus)
+        # not trimmed to the quota: a handful of busy threads (one stream per
+        # read, or 8 sliced streams) did better spread over the share's 64
+        # CPUs than packed onto 16 cores (sliced 32-34k vs 40-43k MiB/s,
+        # profiles/r2_quota); quota packing pays off with many threads
+        mine = [c for g in groups[base:base + share] for c in g] or cpus
         return {"client": mine, "server": mine, "mode": mode, "numa_node": node, "gpu_index_on_node": k,
-                "l3_domains": share, "quota_cpus": quota_budget()}
+                "l3_domains": share}
     client = groups[base] if groups else cpus
     if mode == "same" or share < 2:
         server = client

@@ -117,8 +117,11 @@ def build_parser() -> argparse.ArgumentParser:
                     help="sliced reads: streams pull pieces of this size from a shared cursor (0 = fixed shares)")
     ap.add_argument("--piece-min-bytes", default="0",
                     help="sliced reads: taper the piece size toward the end of the object down to this")
-    ap.add_argument("--affinity", default="share",
-                    help="CPU placement of client/endpoint threads: share|same|split|numa|none (parallel/affinity.py)")
+    ap.add_argument("--affinity", default="auto",
+                    help="CPU placement of client/endpoint threads: auto|pair|share|same|split|numa|none "
+                         "(parallel/affinity.py). auto: pair for one stream per read (won 3 of 3 interleaved "
+                         "reps, profiles/r2_placement), share for sliced reads; the sliced block always runs "
+                         "on its own share-placed endpoint")
     ap.add_argument("--event-wait", default="block", choices=["spin", "block"],
                     help="how GPU sinks wait on slot events: block (interrupt) or spin")
     ap.add_argument("--side-steps", type=int, default=-1,
@@ -216,7 +219,12 @@ def run_rank(args) -> int:
 
     # node-local synthetic GCS endpoint for this rank (no network on the box)
     gpu = ctx.gpu if ctx.gpu >= 0 else 0
-    placement = affinity.plan(gpu, args.affinity) if use_gpu else {"client": [], "server": []}
+    aff = args.affinity
+    if aff == "auto":
+        aff = "pair" if args.slices == 1 else "share"
+    # ranks sharing one GPU (rehearsal) spread over L3 domains instead of stacking
+    slot = local_rank // max(1, torch.cuda.device_count()) if use_gpu and rehearsal else 0
+    placement = affinity.plan(gpu, aff, slot) if use_gpu else {"client": [], "server": []}
     srv = n.Server({"port": 0, "md5": False, "cpus": placement["server"], "retain_uploads": False})
     srv.start()
     bucket = "princer-working-dirs"
@@ -395,8 +403,16 @@ def run_rank(args) -> int:
             blocks["compare"] = ("compare", read_block({"protocol": other}, side_steps, 1, f"{other} compare"),
                                  {"protocol": other})
         if args.sliced_streams > 1 and args.slices == 1:
-            blocks["sliced"] = ("sliced", read_block(sliced_cfg, side_steps, 1, "sliced"),
-                                {"streams_per_read": args.sliced_streams, "ring": "4x4MiB",
+            # 8 receive + 8 send threads: a share-placed endpoint of its own
+            sh = affinity.plan(gpu, "share", slot) if use_gpu else {"client": [], "server": []}
+            srv_sl = n.Server({"port": 0, "md5": False, "cpus": sh["server"], "retain_uploads": False})
+            srv_sl.start()
+            srv_sl.add_synthetic(bucket, prefix, "", first, args.workers, size)
+            sliced_cfg.update({"endpoint": srv_sl.url, "cpus": sh["client"]})
+            st_sl = read_block(sliced_cfg, side_steps, 1, "sliced")
+            srv_sl.stop()
+            blocks["sliced"] = ("sliced", st_sl,
+                                {"streams_per_read": args.sliced_streams, "ring": "4x4MiB", "affinity": "share",
                                  "piece_bytes": parse_size(args.piece_bytes), "note": "extension, not parity"})
         if use_gpu:
             blocks["write"] = ("write", write_block(side_steps, 1),
@@ -455,7 +471,7 @@ def run_rank(args) -> int:
                 "per_rank_mib_s": [round(b / max(e, 1e-12) / (1 << 20), 1)
                                    for b, e in zip(head["nbytes_per_rank"], head["elapsed_per_rank"])],
                 "endpoint": "loopback synthetic GCS (one per rank)",
-                "affinity": args.affinity,
+                "affinity": aff,
             }
             if args.workload == "read":
                 out["host_landed_p50_ms"] = round(head["host_p50_max"], 3)

@@ -47,14 +47,14 @@ struct GpuSinkConfig {
   int slots = 4;
   bool verify = true;  // run the CRC kernels
   Landing landing = Landing::kObject;
-  // Slot hand-off (H2D copy + CRC launches + events) on one per-device
-  // submitter thread instead of the transport thread.  Cuts the transport
-  // thread's hand-off from ~170 us to ~3 us per slot with 8 sliced streams
-  // (HIP runtime lock contention, profiles/r1_markers), but the A/B on the
-  // headline bench (profiles/r1_submit_ab) shows equal throughput and ~2 ms
-  // worse p99 under the box's 16-CPU quota (one more thread to throttle), so
-  // it is opt-in.  Env GCSB_ASYNC_SUBMIT=1.
-  bool async_submit = false;
+  // Slot hand-off (H2D copy + CRC launch + event) on one per-device
+  // submitter thread instead of the transport thread.  A stream's receive is
+  // bound by its receiving core, and the hand-off's HIP calls (~3 us per slot
+  // on the submitter vs ~170 us on a transport thread under HIP runtime lock
+  // contention, profiles/r1_markers) come off it: one stream per 256 MiB
+  // read 12.5k -> 14.4k MiB/s with 2 MiB slots (profiles/r2_single_stream).
+  // On by default from round 2; env GCSB_ASYNC_SUBMIT=0 turns it off.
+  bool async_submit = true;
   // Wait on slot events by blocking (interrupt) instead of spinning: under the
   // GPU box's CPU quota (16 CPUs) spinning waiters steal cycles from the
   // receiving threads.  Env GCSB_EVENT_SPIN=1 selects spinning.

@@ -88,6 +88,14 @@ def core_first(cpus: list[int]) -> list[int]:
     return first + rest
 
 
+def _same_core(a: int, b: int) -> bool:
+    def key(c):
+        return (_read(f"/sys/devices/system/cpu/cpu{c}/topology/physical_package_id"),
+                _read(f"/sys/devices/system/cpu/cpu{c}/topology/core_id"))
+    ka = key(a)
+    return ka[1] is not None and ka == key(b)
+
+
 def quota_budget() -> int:
     """CPUs one rank may keep busy without the container being throttled:
     the CFS quota split over the node's ranks (LOCAL_WORLD_SIZE), 0 = no
@@ -109,11 +117,15 @@ def trim_to_quota(cpus: list[int]) -> list[int]:
     return sorted(core_first(cpus)[:b])
 
 
-def plan(device: int, mode: str = "split") -> dict:
+def plan(device: int, mode: str = "split", slot: int = 0) -> dict:
     """CPU sets for this rank: {"client": [...], "server": [...]}.
 
+    slot: ranks sharing one GPU (GCSB_DIST_BACKEND=gloo rehearsals) pass
+    their index so they land on different L3 domains.
     mode: "quota" (no GPU locality: as many cores as the container's CPU
                    quota allows this rank, see quota_budget),
+          "pair" (one physical core + SMT sibling for the client's threads,
+                  the next core of the same L3 domain for the endpoint's),
           "share" (this rank's fair share of its NUMA node's L3 domains --
                    node L3 domains / GPUs on the node -- shared by client and
                    endpoint threads: all 8 domains on a 1-GPU box, 2 per rank
@@ -139,7 +151,9 @@ def plan(device: int, mode: str = "split") -> dict:
     k = [d for _, d in peers].index(device) if any(d == device for _, d in peers) else 0
     groups = l3_groups(cpus)
     share = max(1, len(groups) // max(1, len(peers)))
-    base = (k * share) % max(1, len(groups))
+    # slot: this rank's index among ranks sharing ONE GPU (shared-GPU
+    # rehearsals only; 0 on a node with a GPU per rank) -> the next L3 domains
+    base = (k * share + slot) % max(1, len(groups))
     if mode == "share":
         # not trimmed to the quota: a handful of busy threads (one stream per
         # read, or 8 sliced streams) did better spread over the share's 64
@@ -148,6 +162,15 @@ def plan(device: int, mode: str = "split") -> dict:
         mine = [c for g in groups[base:base + share] for c in g] or cpus
         return {"client": mine, "server": mine, "mode": mode, "numa_node": node, "gpu_index_on_node": k,
                 "l3_domains": share}
+    if mode == "pair":
+        # two physical cores of the rank's first L3 domain (with their SMT
+        # siblings): one for the client's threads, one for the endpoint's
+        g = core_first(groups[base] if groups else cpus)
+        sib = {c: [d for d in (groups[base] if groups else cpus) if d != c and _same_core(c, d)] for c in g[:2]}
+        if len(g) < 2:
+            return {"client": g, "server": g, "mode": mode}
+        return {"client": [g[0]] + sib[g[0]], "server": [g[1]] + sib[g[1]], "mode": mode, "numa_node": node,
+                "gpu_index_on_node": k}
     client = groups[base] if groups else cpus
     if mode == "same" or share < 2:
         server = client

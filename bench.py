@@ -335,8 +335,8 @@ def run_rank(args) -> int:
         chunk = parse_size(args.write_chunk)
         client = buf = None
         try:
-            client = n.Client({"protocol": protocol, "endpoint": srv.url, "retry_initial_s": 0.05,
-                               "cpus": placement["client"]})
+            # uploads: client threads unpinned (measured fastest, profiles/r1_session4)
+            client = n.Client({"protocol": protocol, "endpoint": srv.url, "retry_initial_s": 0.05})
             buf = torch.empty(wsize, dtype=torch.uint8, device=f"cuda:{gpu}")
             n.gpu_fill_pattern(gpu, buf.data_ptr(), wsize, f"upload/rank{rank}", 0)
             for i in range(warmup):

@@ -107,6 +107,9 @@ def build_parser() -> argparse.ArgumentParser:
                     help="slot hand-off (H2D copy + CRC launches) on a per-device submitter thread instead of the "
                          "receiving thread: one stream per read is bound by its receiving core, so taking the HIP "
                          "calls off it gave +15-35%% (profiles/r2_single_stream)")
+    ap.add_argument("--submit-cpus", default="aux", choices=["aux", "inherit"],
+                    help="aux: the per-device submitter thread gets a core of its own from the placement plan; "
+                         "inherit: it keeps the first posting transport thread's CPU set")
     ap.add_argument("--rcvbuf", default="0", help="client SO_RCVBUF (0 = kernel autotuning)")
     ap.add_argument("--grpc-pool", type=int, default=1)
     ap.add_argument("--slices", type=int, default=1,
@@ -225,6 +228,8 @@ def run_rank(args) -> int:
     # ranks sharing one GPU (rehearsal) spread over L3 domains instead of stacking
     slot = local_rank // max(1, torch.cuda.device_count()) if use_gpu and rehearsal else 0
     placement = affinity.plan(gpu, aff, slot) if use_gpu else {"client": [], "server": []}
+    if use_gpu and args.submit_cpus == "aux" and placement.get("aux"):
+        n.set_submitter_cpus(placement["aux"])
     srv = n.Server({"port": 0, "md5": False, "cpus": placement["server"], "retain_uploads": False})
     srv.start()
     bucket = "princer-working-dirs"
@@ -315,6 +320,7 @@ def run_rank(args) -> int:
             cpu = cpu_delta(c0, cpu_snapshot(), float(s1["bytes"]), e1)
             cpu["cpu_s_per_gib_by_thread"] = cpuacct.per_gib(
                 cpuacct.delta_by_group(th0, cpuacct.thread_cpu()), float(s1["bytes"]))
+        ring_numa = r1.ring_numa(0) if (r1 is not None and use_gpu) else []
         s1 = s1 or {"bytes": 0, "p50_ms": 0.0, "p99_ms": 0.0, "host_p50_ms": 0.0, "slice_skew_ms": 0.0,
                     "verified": 0, "reads": 0}
         del r1
@@ -323,6 +329,7 @@ def run_rank(args) -> int:
                                 verified=float(s1["verified"]), ok=0.0 if err else 1.0)
         st["error"] = err
         st["cpu"] = cpu
+        st["ring_numa"] = ring_numa
         return st
 
     def write_block(steps: int, warmup: int) -> dict:
@@ -472,7 +479,21 @@ def run_rank(args) -> int:
                                    for b, e in zip(head["nbytes_per_rank"], head["elapsed_per_rank"])],
                 "endpoint": "loopback synthetic GCS (one per rank)",
                 "affinity": aff,
+                "placement": {k: placement.get(k) for k in ("client", "server", "aux", "picked_by", "busy")
+                              if placement.get(k) is not None},
             }
+            def by_node(counts):
+                d = {str(i): c for i, c in enumerate(counts[:-1]) if c}
+                if counts and counts[-1]:
+                    d["absent"] = counts[-1]
+                return d
+            # host-memory placement: the object's page cache (read by the send
+            # path) and the pinned ring (written by the receive thread, read
+            # by SDMA) should sit on the GPU's NUMA node
+            out["numa"] = {"gpu_node": placement.get("numa_node"),
+                           "object_pages": by_node(n.pattern_memfd_numa())}
+            if head.get("ring_numa"):
+                out["numa"]["ring_pages"] = by_node(head["ring_numa"])
             if args.workload == "read":
                 out["host_landed_p50_ms"] = round(head["host_p50_max"], 3)
                 out["verified_reads"] = int(head["verified_sum"])

@@ -16,6 +16,16 @@ namespace gcsb {
 std::vector<int> parse_cpulist(const std::string& s);
 // Pins the calling thread to the given CPUs (no-op if empty). Returns success.
 bool pin_current_thread(const std::vector<int>& cpus);
+// NUMA node of the pages of [p, p+len), sampled every `stride` bytes
+// (move_pages query, nothing moves): counts[node] (index kNumaAbsent counts
+// pages not present / not queryable).  Diagnostics for host-memory placement.
+constexpr int kNumaMaxNodes = 8;
+constexpr int kNumaAbsent = kNumaMaxNodes;
+std::vector<long> numa_nodes_of(const void* p, size_t len, size_t stride = 1 << 16);
+// NUMA node of the CPU this thread runs on now (-1 if unknown).
+int current_numa_node();
+// Memory policy of this thread: prefer `node` for new pages (-1 = local).
+bool prefer_numa_node(int node);
 // Round-robin pick: thread k gets cpus[k % n] (single-CPU pinning) when
 // `spread` is set, else the whole set.
 std::vector<int> cpus_for(const std::vector<int>& cpus, int k, bool spread);

@@ -1,5 +1,7 @@
 #include "core/content.h"
 
+#include <sys/mman.h>
+
 #include <sys/syscall.h>
 #include <unistd.h>
 
@@ -9,6 +11,7 @@
 #include <stdexcept>
 #include <thread>
 
+#include "core/affinity.h"
 #include "core/crc32c.h"
 
 namespace gcsb {
@@ -78,6 +81,15 @@ int PatternBuffer::memfd() const {
   }
   memfd_ = fd;
   return memfd_;
+}
+
+std::vector<long> PatternBuffer::memfd_numa() const {
+  if (memfd_ < 0) return {};
+  void* m = ::mmap(nullptr, buf_.size(), PROT_READ, MAP_SHARED | MAP_POPULATE, memfd_, 0);
+  if (m == MAP_FAILED) return {};
+  std::vector<long> c = numa_nodes_of(m, buf_.size());
+  ::munmap(m, buf_.size());
+  return c;
 }
 
 const PatternBuffer& PatternBuffer::instance() {

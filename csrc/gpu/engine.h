@@ -84,6 +84,12 @@ class GpuSink : public Sink {
   void* object_device_ptr() const { return obj_dst_; }
   size_t object_capacity() const { return obj_cap_; }
   const GpuSinkStats& stats() const { return stats_; }
+  // host ring slots (ptr, bytes): placement diagnostics
+  std::vector<std::pair<const void*, size_t>> ring_ranges() const {
+    std::vector<std::pair<const void*, size_t>> r;
+    for (const Slot& s : slots_) r.emplace_back(s.host, cfg_.slot_bytes);
+    return r;
+  }
   const GpuSinkConfig& config() const { return cfg_; }
 
   void begin(const ObjectInfo& info) override;
@@ -245,5 +251,8 @@ void gpu_fill_pattern(int device, void* dptr, uint64_t n, uint64_t rot, uint64_t
 uint64_t gpu_verify_pattern(int device, const void* dptr, uint64_t n, uint64_t rot, uint64_t obj_off,
                             uint64_t* first_bad);
 int gpu_device_count();
+// CPU set of the per-device submitter threads (slot H2D copy + CRC launch
+// hand-off); empty = inherit.  Also GCSB_SUBMIT_CPUS=<cpulist>.
+void set_submitter_cpus(const std::vector<int>& cpus);
 
 }  // namespace gcsb

@@ -14,6 +14,8 @@
 #include <thread>
 #include <stdexcept>
 
+#include <sys/mman.h>
+
 #include "core/affinity.h"
 #include "core/crc32c.h"
 #include "core/util.h"
@@ -61,6 +63,27 @@ DeviceCtx& device_ctx(int dev) {
 
 // Page-locked staging buffers recycled by size (upload rings, per-call
 // sinks): hipHostMalloc of tens of MiB is far slower than the D2H it feeds.
+//
+// Two ways to get page-locked memory (GCSB_RING_ALLOC):
+//   hip  hipHostMalloc(NumaUser): 4 KiB pages;
+//   thp  2 MiB-aligned anonymous memory with MADV_HUGEPAGE, first-touched by
+//        the calling (GPU-local, pinned) thread, then hipHostRegister'ed.  The
+//        receiving core's copy_to_user writes every object byte into these
+//        pages, so 512x fewer TLB misses per slot is on the one-stream
+//        critical path; the SDMA engine reads them through the same IOMMU
+//        mappings either way.
+enum class PinKind { kHip, kThp };
+
+PinKind pin_kind() {
+  static PinKind k = [] {
+    const char* e = std::getenv("GCSB_RING_ALLOC");
+    if (e && std::strcmp(e, "hip") == 0) return PinKind::kHip;
+    if (e && std::strcmp(e, "thp") == 0) return PinKind::kThp;
+    return PinKind::kThp;
+  }();
+  return k;
+}
+
 class PinnedPool {
  public:
   static void* get(size_t n) {
@@ -74,12 +97,29 @@ class PinnedPool {
         return p;
       }
     }
+    if (pin_kind() == PinKind::kThp) {
+      const size_t huge = size_t(2) << 20;
+      const size_t len = (n + huge - 1) / huge * huge;
+      void* p = nullptr;
+      if (posix_memalign(&p, huge, len) == 0) {
+        (void)madvise(p, len, MADV_HUGEPAGE);
+        std::memset(p, 0, len);  // fault in now, on this thread's NUMA node
+        if (hipHostRegister(p, len, hipHostRegisterDefault) == hipSuccess) {
+          std::lock_guard<std::mutex> lk(mu());
+          registered()[p] = len;
+          return p;
+        }
+        (void)hipGetLastError();
+        std::free(p);
+      }
+    }
     void* p = nullptr;
     hip_check(hipHostMalloc(&p, n, hipHostMallocNumaUser), "hipHostMalloc(staging)");
     return p;
   }
   static void put(void* p, size_t n) {
     if (!p) return;
+    bool reg = false;
     {
       std::lock_guard<std::mutex> lk(mu());
       if (held() + n <= kMaxHeld) {
@@ -87,12 +127,26 @@ class PinnedPool {
         held() += n;
         return;
       }
+      auto it = registered().find(p);
+      if (it != registered().end()) {
+        registered().erase(it);
+        reg = true;
+      }
+    }
+    if (reg) {
+      (void)hipHostUnregister(p);
+      std::free(p);
+      return;
     }
     (void)hipHostFree(p);
   }
 
  private:
   static constexpr size_t kMaxHeld = size_t(1) << 30;
+  static std::map<void*, size_t>& registered() {
+    static std::map<void*, size_t> r;
+    return r;
+  }
   static std::mutex& mu() {
     static std::mutex m;
     return m;
@@ -122,6 +176,19 @@ void ensure_device(int dev) {
     hip_check(hipSetDevice(dev), "hipSetDevice");
     cur = dev;
   }
+}
+
+std::mutex g_submit_mu;
+std::vector<int> g_submit_cpus;
+bool g_submit_cpus_set = false;
+
+std::vector<int> submitter_cpus() {
+  std::lock_guard<std::mutex> lk(g_submit_mu);
+  if (!g_submit_cpus_set) {
+    if (const char* e = std::getenv("GCSB_SUBMIT_CPUS")) g_submit_cpus = parse_cpulist(e);
+    g_submit_cpus_set = true;
+  }
+  return g_submit_cpus;
 }
 
 bool env_flag(const char* name, bool dflt) {
@@ -157,6 +224,9 @@ class DeviceSubmitter {
   }
   void loop() {
     name_current_thread("gcsb-submit");
+    // off the receiving core: inherited from the first posting thread (a
+    // pinned transport thread) it would share that core's SMT pair
+    pin_current_thread(submitter_cpus());
     ensure_device(dev_);
     std::unique_lock<std::mutex> lk(mu_);
     for (;;) {
@@ -174,6 +244,12 @@ class DeviceSubmitter {
   std::deque<std::function<void()>> q_;
 };
 }  // namespace
+
+void set_submitter_cpus(const std::vector<int>& cpus) {
+  std::lock_guard<std::mutex> lk(g_submit_mu);
+  g_submit_cpus = cpus;
+  g_submit_cpus_set = true;
+}
 
 // Per-device stream pool shared by every sink / upload source (engine.h).
 class DeviceStreamPool {

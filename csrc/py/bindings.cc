@@ -499,6 +499,7 @@ class PyRunner {
   }
   std::string object_for(int w, int64_t seq) { return runner_->object_for(w, seq); }
   uintptr_t landing_ptr(int w) { return runner_->landing_ptr(w); }
+  std::vector<long> ring_numa(int w) { return runner_->ring_numa(w); }
   std::string transport_path() { return runner_->client().transport_path(); }
   void set_reads_per_worker(int64_t n) { runner_->set_reads_per_worker(n); }
   void reset_stats() { runner_->reset_stats(); }
@@ -780,6 +781,10 @@ PYBIND11_MODULE(_native, m) {
   });
   m.def("parse_cpulist", &parse_cpulist);
   m.def("pin_current_thread", &pin_current_thread);
+  m.def("set_submitter_cpus", &set_submitter_cpus);
+  m.def("numa_nodes_of", [](uintptr_t p, size_t n) { return numa_nodes_of(reinterpret_cast<const void*>(p), n); });
+  m.def("pattern_memfd_numa", [] { return PatternBuffer::instance().memfd_numa(); });
+  m.def("current_numa_node", &current_numa_node);
   m.def("gpu_crc32c", [](int dev, uintptr_t ptr, size_t n) {
     py::gil_scoped_release nogil;
     return gpu_crc32c(dev, reinterpret_cast<const void*>(ptr), n);
@@ -875,6 +880,7 @@ PYBIND11_MODULE(_native, m) {
       .def("summary", &PyRunner::summary)
       .def("object_for", &PyRunner::object_for)
       .def("landing_ptr", &PyRunner::landing_ptr)
+      .def("ring_numa", &PyRunner::ring_numa)
       .def("transport_path", &PyRunner::transport_path)
       .def("set_reads_per_worker", &PyRunner::set_reads_per_worker)
       .def("reset_stats", &PyRunner::reset_stats);

@@ -4,6 +4,7 @@
 #include <unistd.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 
 #include "core/affinity.h"
@@ -24,7 +25,25 @@ FakeGcsServer::~FakeGcsServer() {
 void FakeGcsServer::start() {
   // build the pattern buffer (+ its memfd for sendfile) before the first
   // request, so no read pays for it
-  if (cfg_.zero_copy) PatternBuffer::instance().memfd();
+  //
+  // The memfd's page cache lands on the NUMA node of the thread that writes
+  // it; every served byte is read from there by the send path and copied by
+  // the client's receive thread.  Build it on a thread pinned to the
+  // endpoint's CPUs (the rank's GPU-local node), not on whichever node the
+  // caller (the Python main thread) happens to run.
+  if (cfg_.zero_copy) {
+    const char* e = std::getenv("GCSB_MEMFD_PINNED");  // A/B switch: 0 = build on the caller's thread
+    if (cfg_.cpus.empty() || (e && *e == '0')) {
+      PatternBuffer::instance().memfd();
+    } else {
+      std::thread([this] {
+        pin_current_thread(cfg_.cpus);
+        prefer_numa_node(current_numa_node());
+        PatternBuffer::instance().memfd();
+        prefer_numa_node(-1);
+      }).join();
+    }
+  }
   if (!cfg_.tls_cert_file.empty() && !tls_ctx_) {
     TlsServer t;
     t.cert_file = cfg_.tls_cert_file;

@@ -16,7 +16,7 @@
 //
 //   loopback_ceiling [--mode tcp|memcpy|both] [--object-mib 256] [--reads 10]
 //                    [--ring-kib 16384] [--recv-kib 4096] [--rcvbuf-kib 0]
-//                    [--send-cpu N] [--recv-cpu N] [--zerocopy-send 1]
+//                    [--send-cpu N] [--recv-cpu N] [--zerocopy-send 1] [--ring-pages 0|1|2]
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
@@ -65,9 +65,14 @@ struct Result {
   double gbps = 0, recv_cpu_per_gib = 0, send_cpu_per_gib = 0, p50_ms = 0;
 };
 
+// ring pages: 0 = system default, 1 = MADV_HUGEPAGE, 2 = MADV_NOHUGEPAGE
+int g_ring_pages = 0;
+
 uint8_t* alloc_ring(size_t n) {
-  void* p = mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_POPULATE, -1, 0);
+  void* p = mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
   if (p == MAP_FAILED) die("mmap(ring)");
+  if (g_ring_pages == 1) (void)madvise(p, n, MADV_HUGEPAGE);
+  if (g_ring_pages == 2) (void)madvise(p, n, MADV_NOHUGEPAGE);
   (void)mlock(p, n);  // page-locked like the pinned ring when allowed
   std::memset(p, 0, n);
   return static_cast<uint8_t*>(p);
@@ -212,7 +217,9 @@ int main(int argc, char** argv) {
   auto* send_cpu = fs.Int("send-cpu", -1, "pin the sender to this CPU (-1 = unpinned)");
   auto* recv_cpu = fs.Int("recv-cpu", -1, "pin the receiver to this CPU (-1 = unpinned)");
   auto* zc = fs.Bool("zerocopy-send", true, "sender uses sendfile() (the endpoint's path)");
+  auto* pages = fs.Int("ring-pages", 0, "ring pages: 0 system default, 1 huge (MADV_HUGEPAGE), 2 small");
   fs.Parse(argc, argv);
+  g_ring_pages = static_cast<int>(*pages);
   const size_t obj = static_cast<size_t>(*obj_mib) << 20;
   const size_t ring = static_cast<size_t>(*ring_kib) << 10;
   std::printf("{\"object_mib\": %lld, \"reads\": %lld, \"ring_kib\": %lld, \"recv_kib\": %lld",

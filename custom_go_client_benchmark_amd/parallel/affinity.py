@@ -96,6 +96,53 @@ def _same_core(a: int, b: int) -> bool:
     return ka[1] is not None and ka == key(b)
 
 
+def cpu_busy(sample_s: float = 0.15) -> dict[int, float]:
+    """Busy fraction of every host CPU over `sample_s` (/proc/stat is host-wide
+    inside the container).  The GPU boxes are slices of shared hosts: a
+    receive thread on a core whose SMT sibling runs someone else's work moves
+    bytes ~2x slower (profiles/r2_cores: identical single-stream reads at
+    0.066 vs 0.148 CPU-s/GiB on the same box)."""
+    import time
+
+    def snap():
+        out = {}
+        try:
+            with open("/proc/stat") as f:
+                for line in f:
+                    if line.startswith("cpu") and line[3:4].isdigit():
+                        p = line.split()
+                        v = [int(x) for x in p[1:]]
+                        out[int(p[0][3:])] = (sum(v), v[3] + (v[4] if len(v) > 4 else 0))
+        except OSError:
+            pass
+        return out
+
+    a = snap()
+    if not a:
+        return {}
+    time.sleep(sample_s)
+    b = snap()
+    return {c: 1.0 - (b[c][1] - a[c][1]) / max(1, b[c][0] - a[c][0]) for c in b if c in a}
+
+
+def _core_key(c: int):
+    return (_read(f"/sys/devices/system/cpu/cpu{c}/topology/physical_package_id"),
+            _read(f"/sys/devices/system/cpu/cpu{c}/topology/core_id"))
+
+
+def quiet_cores(cpus: list[int], busy: dict[int, float]) -> list[list[int]]:
+    """Physical cores of `cpus` (each as [cpu, siblings...]) ordered from the
+    least to the most busy (both hardware threads counted).  The core of CPU 0
+    goes last: it carries the host's housekeeping (timers, IRQ defaults)."""
+    cores: dict = {}
+    for c in cpus:
+        cores.setdefault(_core_key(c), []).append(c)
+    def load(core):
+        pen = 1.0 if 0 in core else 0.0
+        return (pen + sum(busy.get(c, 0.0) for c in core), core[0])
+    return [sorted(v) for v in sorted(cores.values(), key=load)]
+
+
 def quota_budget() -> int:
     """CPUs one rank may keep busy without the container being throttled:
     the CFS quota split over the node's ranks (LOCAL_WORLD_SIZE), 0 = no
@@ -163,14 +210,37 @@ def plan(device: int, mode: str = "split", slot: int = 0) -> dict:
         return {"client": mine, "server": mine, "mode": mode, "numa_node": node, "gpu_index_on_node": k,
                 "l3_domains": share}
     if mode == "pair":
-        # two physical cores of the rank's first L3 domain (with their SMT
-        # siblings): one for the client's threads, one for the endpoint's
+        # three quiet physical cores of one L3 domain of the rank's share
+        # (with their SMT siblings): the client's receive thread, the
+        # endpoint's send thread, the device submitter.  The domain and the
+        # cores are the least busy ones right now (cpu_busy); one domain keeps
+        # the loopback copy in one L3 (profiles/r2_placement)
+        doms = groups[base:base + share] if groups else [cpus]
+        busy = cpu_busy() if os.environ.get("GCSB_QUIET_CORES", "1") != "0" else {}
+        if busy:
+            best = None
+            for dom in doms:
+                q = quiet_cores(dom, busy)
+                if len(q) < 3:
+                    continue
+                load = sum(busy.get(c, 0.0) for core in q[:3] for c in core) + (1.0 if 0 in q[0] + q[1] else 0.0)
+                if best is None or load < best[0]:
+                    best = (load, q)
+            if best is not None:
+                q = best[1]
+                return {"client": q[0], "server": q[1], "aux": q[2], "mode": mode, "numa_node": node,
+                        "gpu_index_on_node": k, "picked_by": "quiet",
+                        "busy": round(best[0], 3)}
         g = core_first(groups[base] if groups else cpus)
         sib = {c: [d for d in (groups[base] if groups else cpus) if d != c and _same_core(c, d)] for c in g[:2]}
         if len(g) < 2:
             return {"client": g, "server": g, "mode": mode}
-        return {"client": [g[0]] + sib[g[0]], "server": [g[1]] + sib[g[1]], "mode": mode, "numa_node": node,
-                "gpu_index_on_node": k}
+        # a third core (when the domain has one) for the per-device submitter
+        # thread, so slot hand-offs never run on the receiving core's SMT pair
+        aux = [g[2]] + [d for d in (groups[base] if groups else cpus) if d != g[2] and _same_core(g[2], d)] \
+            if len(g) > 2 else []
+        return {"client": [g[0]] + sib[g[0]], "server": [g[1]] + sib[g[1]], "aux": aux, "mode": mode,
+                "numa_node": node, "gpu_index_on_node": k}
     client = groups[base] if groups else cpus
     if mode == "same" or share < 2:
         server = client

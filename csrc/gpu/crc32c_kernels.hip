@@ -70,6 +70,18 @@ __device__ __forceinline__ uint32_t update16(const uint32_t* __restrict__ sl, ui
   return c;
 }
 
+// The same 16-byte update from the bank-replicated nibble tables (CrcTables::nib):
+// nb = nib + (lane & 31); table t of nibble n at nb[t * 512 + n * 32].
+__device__ __forceinline__ uint32_t update16_nib(const uint32_t* __restrict__ nb, uint32_t state, uint4 v) {
+  const uint32_t w[4] = {state ^ v.x, v.y, v.z, v.w};
+  uint32_t c = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c ^= nb[(q * 8 + k) * 512 + ((w[q] >> (4 * k)) & 15u) * 32];
+  return c;
+}
+
 __device__ __forceinline__ uint32_t mask_low_bytes(uint32_t w, int keep_from) {
   // zero bytes [0, keep_from) of a little-endian word (keep_from in 0..4)
   if (keep_from <= 0) return w;
@@ -83,13 +95,10 @@ __device__ __forceinline__ void stage(uint32_t* __restrict__ dst, const uint32_t
   for (int i = threadIdx.x; i < words / 4; i += blockDim.x) d4[i] = s4[i];
 }
 
-// Tile `gt` of the batch: raw CRC (valid in lane 0).  Pieces before the
-// segment start read as zeros (free for a raw CRC); the piece straddling it is
-// masked.  Tiles are right-aligned to the segment end, so only the first tile
-// of a segment has such a head.
+// The tile's 16-byte pieces for this lane (R rounds x kCrcChunkPieces).
 template <int R>
-__device__ __forceinline__ uint32_t tile_crc(const CrcBatch& b, uint32_t s, uint32_t gt, const uint32_t* sl,
-                                             const uint32_t* lane_shift, int lane) {
+__device__ __forceinline__ void load_tile(const CrcBatch& b, uint32_t s, uint32_t gt, int lane,
+                                          uint4 (&v)[R * kCrcChunkPieces]) {
   const uintptr_t addr = reinterpret_cast<uintptr_t>(b.seg[s].addr);
   const uint32_t len = b.seg[s].len;
   const uint32_t t = gt - b.seg[s].tile_base;
@@ -97,7 +106,6 @@ __device__ __forceinline__ uint32_t tile_crc(const CrcBatch& b, uint32_t s, uint
   const uint64_t full = (addr + len - a16 + 15) / 16 - 1;
   const intptr_t vend = static_cast<intptr_t>(a16 + 16 * full);
   const intptr_t tstart = vend - (static_cast<intptr_t>(R) * kCrcRoundBytes) * static_cast<intptr_t>(b.seg[s].ntiles - t);
-  uint4 v[R * kCrcChunkPieces];
 #pragma unroll
   for (int k = 0; k < R; ++k)
 #pragma unroll
@@ -114,16 +122,46 @@ __device__ __forceinline__ uint32_t tile_crc(const CrcBatch& b, uint32_t s, uint
       }
       v[k * kCrcChunkPieces + j] = x;
     }
-  // keep all the tile's loads in flight before the first lookup (the
-  // scheduler otherwise sinks them into the lookup chain)
-  __builtin_amdgcn_sched_barrier(0);
+}
+
+// The lane's CRC register over its chunks of the tile.
+template <int R, bool kNib = false>
+__device__ __forceinline__ uint32_t lane_chain(const uint4 (&v)[R * kCrcChunkPieces], const uint32_t* sl,
+                                               const uint32_t* lane_shift, int lane) {
   uint32_t state = 0;
 #pragma unroll
   for (int k = 0; k < R; ++k) {
     if (k) state = shift4(lane_shift + 6 * 1024, state);  // over the 4032-byte gap to this lane's next chunk
 #pragma unroll
-    for (int j = 0; j < kCrcChunkPieces; ++j) state = update16(sl, state, v[k * kCrcChunkPieces + j]);
+    for (int j = 0; j < kCrcChunkPieces; ++j) {
+      if constexpr (kNib)
+        state = update16_nib(sl + (lane & 31), state, v[k * kCrcChunkPieces + j]);
+      else
+        state = update16(sl, state, v[k * kCrcChunkPieces + j]);
+    }
   }
+  return state;
+}
+
+// Tile `gt` of the batch: per-lane register.  Pieces before the segment
+// start read as zeros (free for a raw CRC); the piece straddling it is masked.
+// Tiles are right-aligned to the segment end, so only the first tile of a
+// segment has such a head.
+template <int R, bool kNib = false>
+__device__ __forceinline__ uint32_t lane_state(const CrcBatch& b, uint32_t s, uint32_t gt, const uint32_t* sl,
+                                               const uint32_t* lane_shift, int lane) {
+  uint4 v[R * kCrcChunkPieces];
+  load_tile<R>(b, s, gt, lane, v);
+  // keep all the tile's loads in flight before the first lookup (the
+  // scheduler otherwise sinks them into the lookup chain)
+  __builtin_amdgcn_sched_barrier(0);
+  return lane_chain<R, kNib>(v, sl, lane_shift, lane);
+}
+
+template <int R>
+__device__ __forceinline__ uint32_t tile_crc(const CrcBatch& b, uint32_t s, uint32_t gt, const uint32_t* sl,
+                                             const uint32_t* lane_shift, int lane) {
+  uint32_t state = lane_state<R>(b, s, gt, sl, lane_shift, lane);
   // wave tree: lane l's last chunk ends 64 (63 - l) bytes before the tile end
 #pragma unroll
   for (int lv = 0; lv < 6; ++lv) {
@@ -149,6 +187,43 @@ __device__ __forceinline__ uint32_t add_tail(const CrcSeg& sg, uint32_t raw, con
   if (lane < r) {
     const uint32_t sb = lane < 4 ? (raw >> (8 * lane)) & 0xff : 0u;
     x = sl[(r - 1 - lane) * 256 + ((*reinterpret_cast<const uint8_t*>(p0 + lane) ^ sb) & 0xff)];
+  }
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) x ^= __shfl_xor(x, o, 64);
+  return x ^ (r < 4 ? raw >> (8 * r) : 0u);
+}
+
+// Split add_tail for prefetching: the segment's last r (1..16) bytes, byte
+// `lane` of them in lanes < r (0 elsewhere)...
+__device__ __forceinline__ uint32_t tail_byte(const CrcSeg& sg, int lane, int* r_out) {
+  *r_out = 0;
+  if (sg.len == 0) return 0u;
+  const uintptr_t addr = reinterpret_cast<uintptr_t>(sg.addr);
+  const uintptr_t a16 = addr & ~uintptr_t(15);
+  const uintptr_t e = addr + sg.len;
+  const uintptr_t vend = a16 + 16 * ((e - a16 + 15) / 16 - 1);
+  const uintptr_t p0 = vend > addr ? vend : addr;
+  const int r = static_cast<int>(e - p0);
+  *r_out = r;
+  return lane < r ? static_cast<uint32_t>(*reinterpret_cast<const uint8_t*>(p0 + lane)) : 0u;
+}
+
+// ... folded into `raw` (slice-by-r, one independent lookup per lane)
+template <bool kNib>
+__device__ __forceinline__ uint32_t fold_tail(uint32_t byte, int r, uint32_t raw, const uint32_t* tab, int lane) {
+  if (r == 0) return raw;
+  uint32_t x = 0;
+  if (lane < r) {
+    const uint32_t sb = lane < 4 ? (raw >> (8 * lane)) & 0xff : 0u;
+    const uint32_t bv = (byte ^ sb) & 0xff;
+    const int m = r - 1 - lane;  // slice16 table index
+    if constexpr (kNib) {
+      const uint32_t* nb = tab + (lane & 31);
+      const int t = 2 * (15 - m);
+      x = nb[t * 512 + (bv & 15u) * 32] ^ nb[(t + 1) * 512 + (bv >> 4) * 32];
+    } else {
+      x = tab[m * 256 + bv];
+    }
   }
 #pragma unroll
   for (int o = 8; o > 0; o >>= 1) x ^= __shfl_xor(x, o, 64);
@@ -217,12 +292,14 @@ __global__ __launch_bounds__(kThreads) void crc32c_tiles_kernel(const CrcBatch b
   constexpr int kTreeWords = 6 * 1024;
   __shared__ __attribute__((aligned(16))) uint32_t s_tab[kSliceWords + kTreeWords + kGapWords + kFoldWords];
   __shared__ uint32_t s_last;
+  if (b.probe == 2) return;
   stage(s_tab, &tabs->slice16[0][0], kSliceWords);
   stage(s_tab + kSliceWords, &tabs->lane_shift[0][0][0], kTreeWords + kGapWords);
   if constexpr (kFused)
     stage(s_tab + kSliceWords + kTreeWords + kGapWords,
           &tabs->tile_shift[static_cast<int>(b.tile_log2) - kCrcMinTileLog2][0][0], kFoldWords);
   __syncthreads();
+  if (b.probe == 1) return;
   const uint32_t* sl = s_tab;
   const uint32_t* lane_shift = s_tab + kSliceWords;
   uint32_t* tiles = scratch + kCrcScratchHeader;
@@ -241,6 +318,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_tiles_kernel(const CrcBatch b
         tiles[gt] = c;
     }
   }
+  if (b.probe == 4) return;
   if constexpr (kFused) {
     // Every wave's tile stores must have completed (vmcnt 0) before thread 0
     // counts this workgroup done; __syncthreads alone does not wait for them.
@@ -251,6 +329,10 @@ __global__ __launch_bounds__(kThreads) void crc32c_tiles_kernel(const CrcBatch b
                    ? 1u : 0u;
     __syncthreads();
     if (!s_last) return;
+    if (b.probe == 3) {
+      if (threadIdx.x == 0) __hip_atomic_store(scratch, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
     for (uint32_t g = wave; g < b.nseg; g += kWaves) {
       const CrcSeg& sg = b.seg[g];
       uint32_t raw = fold_wave<true>(sg, tiles, s_tab + kSliceWords + kTreeWords + kGapWords, lane);
@@ -258,6 +340,131 @@ __global__ __launch_bounds__(kThreads) void crc32c_tiles_kernel(const CrcBatch b
       if (lane == 0) out[g] = seg_result(sg, raw);
     }
     if (threadIdx.x == 0) __hip_atomic_store(scratch, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__device__ __forceinline__ uint32_t xor_over_lanes(uint32_t x, int width) {
+  for (int o = width >> 1; o > 0; o >>= 1) x ^= __shfl_xor(x, o, 64);
+  return x;
+}
+
+// Slot kernel (4 KiB tiles, segments <= kCrcFusedMaxTiles tiles: every ring
+// slot).  Same lane chains as tile_crc<1>, but no lookup-table wave tree and
+// no Horner fold: CRC shifts are GF(2)-linear, so each lane's state goes
+// straight to its tile's end through a 32x32 bit matrix held in 32 VGPRs
+// (lane_k, loaded once per wave), the XOR over the 64 lanes is the tile's raw
+// CRC, and one more matrix (tile_k[d], a coalesced 128 B load issued with the
+// tile's data) moves it to the segment end.  Each wave stores that
+// contribution (write-through to the device coherence point); the last
+// workgroup, found through a two-level done counter, XORs each segment's
+// contributions (independent loads, no chain), adds the 1..16-byte tail,
+// fixes up, compares and writes the result.
+// Decomposition of the round-2 fused tile kernel on a 2 MiB slot
+// (profiles/r2_crc_slot): 2.7 us in tiles (64 CUs busy, 88 LDS lookups per
+// lane, a 6-level lookup chain), 1.0 us on the done counter, 2.5 us in the
+// last workgroup's Horner + tree fold.  W (waves per workgroup) is picked so
+// the grid puts a tile on every CU.
+template <int W, bool kNib>
+__global__ __launch_bounds__(64 * W) void crc32c_slot_kernel(const CrcBatch b, const CrcTables* __restrict__ tabs,
+                                                            uint32_t* __restrict__ scratch,
+                                                            CrcSegResult* __restrict__ out) {
+  constexpr int kTabWords = kNib ? 32 * 16 * 32 : kSliceWords;
+  __shared__ __attribute__((aligned(16))) uint32_t s_sl[kTabWords];
+  __shared__ uint32_t s_last;
+  if (b.probe == 2) return;
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // the first tile's data and matrix go out before the tables: their memory
+  // latency overlaps the staging's instead of following it (the slot's bytes
+  // were just written by SDMA, the tables are L2-cold between slots)
+  const uint32_t gt0 = blockIdx.x * W + wave;
+  uint32_t s = 0;
+  uint4 v[kCrcChunkPieces];
+  uint32_t kt = 0;
+  if (gt0 < b.total_tiles) {
+    while (s + 1 < b.nseg && b.seg[s + 1].tile_base <= gt0) ++s;
+    kt = tabs->tile_k[b.seg[s].ntiles - 1 - (gt0 - b.seg[s].tile_base)][lane & 31];
+    load_tile<1>(b, s, gt0, lane, v);
+  }
+  // this lane's chunk -> tile end: 32 matrix columns, in registers
+  uint32_t kl[32];
+  {
+    const uint4* kp = reinterpret_cast<const uint4*>(&tabs->lane_k[lane][0]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint4 q = kp[j];
+      kl[4 * j] = q.x;
+      kl[4 * j + 1] = q.y;
+      kl[4 * j + 2] = q.z;
+      kl[4 * j + 3] = q.w;
+    }
+  }
+  if constexpr (kNib)
+    stage(s_sl, &tabs->nib[0][0][0], kTabWords);
+  else
+    stage(s_sl, &tabs->slice16[0][0], kTabWords);
+  __syncthreads();
+  if (b.probe == 1) return;
+  uint32_t* tiles = scratch + kCrcScratchHeader;
+  for (uint32_t gt = gt0; gt < b.total_tiles; gt += gridDim.x * W) {
+    if (gt != gt0) {
+      while (s + 1 < b.nseg && b.seg[s + 1].tile_base <= gt) ++s;
+      kt = tabs->tile_k[b.seg[s].ntiles - 1 - (gt - b.seg[s].tile_base)][lane & 31];
+      load_tile<1>(b, s, gt, lane, v);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const uint32_t state = lane_chain<1, kNib>(v, s_sl, nullptr, lane);
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) c ^= kl[i] & (0u - ((state >> i) & 1u));
+    c = xor_over_lanes(c, 64);  // the tile's raw CRC, in every lane
+    uint32_t x = lane < 32 ? (kt & (0u - ((c >> lane) & 1u))) : 0u;
+    x = xor_over_lanes(x, 32);
+    if (lane == 0) __hip_atomic_store(tiles + gt, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (b.probe == 4) return;
+  // this workgroup's stores complete before it counts itself done
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    // two-level done counter: a group counter per 1/16 of the grid, the
+    // group's last workgroup counts the group on the root counter
+    const uint32_t groups = gridDim.x < kCrcCounterGroups ? gridDim.x : kCrcCounterGroups;
+    const uint32_t j = blockIdx.x % groups;
+    const uint32_t members = gridDim.x / groups + (j < gridDim.x % groups ? 1u : 0u);
+    uint32_t* gc = scratch + kCrcCounterStride * (1 + j);
+    uint32_t last = 0;
+    if (__hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == members - 1) {
+      __hip_atomic_store(gc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__hip_atomic_fetch_add(scratch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == groups - 1) {
+        __hip_atomic_store(scratch, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = 1;
+      }
+    }
+    s_last = last;
+  }
+  __syncthreads();
+  if (!s_last || b.probe == 3) return;
+  for (uint32_t g = wave; g < b.nseg; g += W) {
+    const CrcSeg& sg = b.seg[g];
+    const uint32_t* tp = tiles + sg.tile_base;
+    // the tail bytes and every contribution in flight at once (<= 16 per
+    // lane), then the XORs: a rolled loop waits one device-scope round trip
+    // per step (3.1 us for 8 steps)
+    int r = 0;
+    const uint32_t tb = tail_byte(sg, lane, &r);
+    uint32_t v[kCrcFusedMaxTiles / 64];
+#pragma unroll
+    for (int k = 0; k < static_cast<int>(kCrcFusedMaxTiles / 64); ++k) {
+      const uint32_t j = static_cast<uint32_t>(lane) + 64u * static_cast<uint32_t>(k);
+      v[k] = j < sg.ntiles ? __hip_atomic_load(tp + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    }
+    uint32_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < static_cast<int>(kCrcFusedMaxTiles / 64); ++k) acc ^= v[k];
+    uint32_t raw = xor_over_lanes(acc, 64);
+    raw = fold_tail<kNib>(tb, r, raw, s_sl, lane);
+    if (lane == 0) out[g] = seg_result(sg, raw);
   }
 }
 
@@ -408,6 +615,47 @@ void launch_crc32c_batch(const CrcBatch& b, const CrcTables* d_tables, uint32_t*
   if (blocks == 0) blocks = 1;       // tail-only segments: the fused fold still runs
   const bool fused = b.max_seg_tiles <= kCrcFusedMaxTiles;
   const bool small = b.tile_log2 == static_cast<uint32_t>(kCrcMinTileLog2);
+  static const bool slot_kernel = [] {
+    const char* e = std::getenv("GCSB_CRC_SLOT");  // A/B switch: 0 = round-2 fused tile kernel
+    return !(e && *e == '0');
+  }();
+  if (fused && small && slot_kernel) {
+    // waves per workgroup: enough workgroups to put a tile on every CU first
+    const uint32_t t = b.total_tiles;
+    static const int forced_w = [] {
+      const char* e = std::getenv("GCSB_CRC_SLOT_WAVES");  // A/B: waves per workgroup (1, 2, 4, 8)
+      return e ? std::atoi(e) : 0;
+    }();
+    int w = t <= 256 ? 1 : t <= 512 ? 2 : t <= 1024 ? 4 : 8;
+    if (forced_w == 1 || forced_w == 2 || forced_w == 4 || forced_w == 8) w = forced_w;
+    uint32_t g = (t + w - 1) / w;
+    if (g > 2048) g = 2048;
+    if (g == 0) g = 1;
+    static const bool nib = [] {
+      const char* e = std::getenv("GCSB_CRC_NIB");  // A/B: 0 = byte tables (bank conflicts), 1 = nibble tables
+      return e && *e == '1';
+    }();
+#define GCSB_SLOT(WV, NB) \
+  hipLaunchKernelGGL((crc32c_slot_kernel<WV, NB>), dim3(g), dim3(64 * WV), 0, stream, b, d_tables, d_scratch, d_results)
+    if (nib) {
+      switch (w) {
+        case 1: GCSB_SLOT(1, true); break;
+        case 2: GCSB_SLOT(2, true); break;
+        case 4: GCSB_SLOT(4, true); break;
+        default: GCSB_SLOT(8, true); break;
+      }
+    } else {
+      switch (w) {
+        case 1: GCSB_SLOT(1, false); break;
+        case 2: GCSB_SLOT(2, false); break;
+        case 4: GCSB_SLOT(4, false); break;
+        default: GCSB_SLOT(8, false); break;
+      }
+    }
+#undef GCSB_SLOT
+    hip_check(hipGetLastError(), "crc32c_slot_kernel");
+    return;
+  }
   if (fused) {
     if (small)
       hipLaunchKernelGGL((crc32c_tiles_kernel<1, true>), dim3(blocks), dim3(kThreads), 0, stream, b, d_tables,

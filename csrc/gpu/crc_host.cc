@@ -15,6 +15,18 @@ void build_crc_tables(CrcTables* t) {
   crc32c_build_shift_table(kCrcLaneGap, t->lane_shift[6]);
   for (int lv = 0; lv < kCrcTileShiftLevels; ++lv)
     crc32c_build_shift_table(static_cast<uint64_t>(kCrcRoundBytes) << lv, t->tile_shift[lv]);
+  for (int l = 0; l < 64; ++l)
+    for (int i = 0; i < 32; ++i)
+      t->lane_k[l][i] = crc32c_shift(1u << i, static_cast<uint64_t>(kCrcChunkBytes) * (63 - l));
+  for (int j = 0; j < 16; ++j)
+    for (int h = 0; h < 2; ++h)
+      for (int n = 0; n < 16; ++n)
+        for (int r = 0; r < 32; ++r) t->nib[2 * j + h][n][r] = t->slice16[15 - j][n << (4 * h)];
+  for (uint32_t d = 0; d < kCrcFusedMaxTiles; ++d) {
+    // column i of shift by d tiles = shift of column i by one tile, d times
+    for (int i = 0; i < 32; ++i)
+      t->tile_k[d][i] = d == 0 ? (1u << i) : crc32c_shift(t->tile_k[d - 1][i], kCrcMinTile);
+  }
 }
 
 namespace {
@@ -73,6 +85,13 @@ CrcSegResult emulate_crc32c_segment(const uint8_t* addr_p, uint32_t len, const C
   uint32_t T = 0;
   crc_segment_geometry(addr, len, tile_log2, &T);
   std::vector<uint32_t> tiles(T);
+  const bool slot = fold_waves == 0;
+  if (slot && (tile_log2 != static_cast<uint32_t>(kCrcMinTileLog2) || T > kCrcFusedMaxTiles)) {
+    CrcSegResult bad{};
+    bad.status = 3;  // outside the slot kernel's domain
+    return bad;
+  }
+  uint32_t slot_acc = 0;
   // tile kernel: per-lane chains over R rounds, 6-level wave tree
   for (uint32_t tt = 0; tt < T; ++tt) {
     const uintptr_t a16 = addr & ~uintptr_t(15);
@@ -101,6 +120,13 @@ CrcSegResult emulate_crc32c_segment(const uint8_t* addr_p, uint32_t len, const C
       }
       lanes[lane] = state;
     }
+    if (slot) {
+      // slot kernel: lane -> tile end (lane_k), tile -> segment end (tile_k)
+      uint32_t c = 0;
+      for (int lane = 0; lane < 64; ++lane) c ^= crc_apply_columns(t.lane_k[lane], lanes[lane]);
+      slot_acc ^= crc_apply_columns(t.tile_k[T - 1 - tt], c);
+      continue;
+    }
     for (int lv = 0; lv < 6; ++lv) {
       uint32_t nxt[64];
       for (int lane = 0; lane < 64; ++lane) {
@@ -114,7 +140,7 @@ CrcSegResult emulate_crc32c_segment(const uint8_t* addr_p, uint32_t len, const C
   }
   // fold: W waves, thread k folds tiles T-1-(k + S m) by Horner with stride
   // S = 64 W tiles, then a tree over the 64 W threads (shift 2^lv tiles)
-  const int W = fold_waves;
+  const int W = slot ? 1 : fold_waves;
   int logw = 0;
   while ((1 << logw) < W) ++logw;
   const int S = 64 * W;
@@ -131,7 +157,7 @@ CrcSegResult emulate_crc32c_segment(const uint8_t* addr_p, uint32_t len, const C
   }
   for (int lv = 0; lv < 6 + logw; ++lv)
     for (int k = 0; k < S; k += (2 << lv)) acc[k] ^= shift4(t.tile_shift[lvl0 + lv], acc[k + (1 << lv)]);
-  uint32_t raw = acc[0];
+  uint32_t raw = slot ? slot_acc : acc[0];
   // tail: the last 1..16 bytes, slice-by-r with one independent lookup per byte
   if (len > 0) {
     const uintptr_t a16 = addr & ~uintptr_t(15);

@@ -30,9 +30,15 @@ constexpr int kCrcTileShiftLevels = 13;               // tile_shift[s] = shift b
 // gpu_crc32c) get a separate fold kernel with 8 waves per segment.
 constexpr uint32_t kCrcFusedMaxTiles = 64 * 16;  // <= 16 Horner steps per lane (2 prefetch rounds)
 constexpr int kMaxSeg = 32;
-// Tile scratch layout: word 0 = the fused kernel's "workgroups done" counter
-// (zero between launches), tiles from word kCrcScratchHeader.
-constexpr int kCrcScratchHeader = 64;
+// Tile scratch layout: word 0 = the fused kernels' "workgroups done" counter
+// (the slot kernel's root counter), then kCrcCounterGroups group counters of
+// the slot kernel kCrcCounterStride words apart (all zero between launches),
+// tiles from word kCrcScratchHeader.  Same-address device-scope atomics
+// serialise at ~14 ns each on MI355X (profiles/r2_crc_slot): 256 workgroups
+// on one counter cost 3.6 us, split over 16 lines 0.4 us.
+constexpr int kCrcCounterGroups = 16;
+constexpr int kCrcCounterStride = 1024;  // 4 KiB apart: different memory channels
+constexpr int kCrcScratchHeader = kCrcCounterStride * (kCrcCounterGroups + 1);
 
 struct CrcSeg {
   const uint8_t* addr;
@@ -49,6 +55,8 @@ struct CrcBatch {
   uint32_t total_tiles;
   uint32_t tile_log2;  // 12 or 14, chosen by finalize_crc_batch
   uint32_t max_seg_tiles;
+  uint32_t probe;      // latency probe (kernel bench only): 2 = exit at entry, 1 = after the LDS
+                       // table staging, 4 = after the tiles, 3 = after the done counter (no fold)
   CrcSeg seg[kMaxSeg];
 };
 
@@ -63,6 +71,20 @@ struct CrcTables {
   uint32_t slice16[16][256];
   uint32_t lane_shift[7][4][256];  // [0..5]: shift by kCrcChunkBytes * 2^lv (wave tree); [6]: kCrcLaneGap
   uint32_t tile_shift[kCrcTileShiftLevels][4][256];  // shift by 4 KiB * 2^s
+  // GF(2) shift matrices of the slot kernel (4 KiB tiles), column i = the
+  // shift of the register value 1 << i: shift(s) = XOR_i bit_i(s) * col_i.
+  //   lane_k[l]: lane l's 64-byte chunk ends 64 (63 - l) bytes before its
+  //              tile's end;
+  //   tile_k[d]: a tile ends 4 KiB * d bytes before its segment's last
+  //              16-byte boundary (d < kCrcFusedMaxTiles).
+  uint32_t lane_k[64][32];
+  uint32_t tile_k[kCrcFusedMaxTiles][32];
+  // slice-by-16 split into nibbles and replicated per LDS bank:
+  // nib[2j + h][n][r] = slice16[15 - j][n << 4h] for every replica r < 32,
+  // so lane l reads replica l & 31 and a ds_read_b32 never conflicts
+  // (banks = (addr / 4) mod 32 per 32-lane group).  Twice the lookups of the
+  // byte tables, none of their ~4-way conflicts.
+  uint32_t nib[32][16][32];
 };
 
 // Number of tiles (of 2^tile_log2 bytes) covering a segment's 16-byte pieces
@@ -90,7 +112,15 @@ inline uint64_t crc_scratch_words(uint64_t tiles) { return tiles + kCrcScratchHe
 // Host emulation of the kernels' math (same tables, same tile/lane/fold
 // decomposition): the CPU test oracle.  fold_waves = 1 mirrors the fused
 // epilogue, 8 the separate fold kernel.
+// fold_waves = 0 mirrors the slot kernel (4 KiB tiles, <= kCrcFusedMaxTiles
+// tiles): lane states through lane_k, tile values through tile_k, XOR.
 CrcSegResult emulate_crc32c_segment(const uint8_t* addr, uint32_t len, const CrcTables& t, uint32_t expected,
                                     bool check, uint32_t tile_log2 = kCrcMaxTileLog2, int fold_waves = 8);
+// s * (GF(2) matrix with columns col[0..31])
+inline uint32_t crc_apply_columns(const uint32_t col[32], uint32_t s) {
+  uint32_t r = 0;
+  for (int i = 0; i < 32; ++i) r ^= col[i] & (0u - ((s >> i) & 1u));
+  return r;
+}
 
 }  // namespace gcsb

@@ -892,6 +892,7 @@ double gpu_crc32c_throughput(int device, const void* dptr, size_t n, int iters, 
     off += len;
   }
   finalize_crc_batch(&b, static_cast<uint32_t>(tile_log2));
+  if (const char* e = std::getenv("GCSB_CRC_PROBE")) b.probe = static_cast<uint32_t>(std::atoi(e));
   uint32_t* d_tiles = crc_scratch_alloc(b.total_tiles + 1);
   CrcSegResult* res = nullptr;
   hip_check(hipHostMalloc(reinterpret_cast<void**>(&res), sizeof(CrcSegResult) * kMaxSeg,

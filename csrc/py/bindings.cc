@@ -648,7 +648,8 @@ PYBIND11_MODULE(_native, m) {
         std::memcpy(p, s.data(), s.size());
         if (tile_log2 != kCrcMinTileLog2 && tile_log2 != kCrcMaxTileLog2)
           throw std::invalid_argument("tile_log2 must be 12 or 14");
-        if (fold_waves != 1 && fold_waves != 8) throw std::invalid_argument("fold_waves must be 1 or 8");
+        if (fold_waves != 0 && fold_waves != 1 && fold_waves != 8)
+          throw std::invalid_argument("fold_waves must be 0 (slot kernel), 1 or 8");
         CrcSegResult r = emulate_crc32c_segment(p, static_cast<uint32_t>(s.size()), host_tables(), expected, check,
                                                 tile_log2, fold_waves);
         return py::make_tuple(r.raw, r.crc, r.status);

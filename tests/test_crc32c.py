@@ -37,10 +37,11 @@ def test_large_buffer_interleaved_path(native):
 @pytest.mark.parametrize("misalign", [0, 1, 3, 8, 15])
 @pytest.mark.parametrize("n", [0, 1, 15, 16, 17, 255, 256, 257, 4095, 4096, 4097, 16383, 16384, 16385, 16400,
                                65536 + 5, (1 << 20) + 3])
-@pytest.mark.parametrize("geom", [(14, 8), (12, 1), (14, 1), (12, 8)])
+@pytest.mark.parametrize("geom", [(14, 8), (12, 1), (14, 1), (12, 8), (12, 0)])
 def test_gpu_algorithm_emulation(native, misalign, n, geom):
     """Kernel math on the CPU: 16 KiB / 4 KiB tiles x fused (1 wave per
-    segment) / separate (8 waves per segment) fold, parallel 1..16 B tail."""
+    segment) / separate (8 waves per segment) fold / slot kernel (GF(2) lane
+    and tile matrices, fold_waves=0), parallel 1..16 B tail."""
     tl, fw = geom
     d = os.urandom(n)
     want = native.crc32c(d)
@@ -57,6 +58,31 @@ def test_emulation_multi_megabyte_tile_fold(native, geom):
     d = os.urandom(9 * (1 << 20) + 999)
     raw, crc, _ = native.emulate_gpu_crc32c(d, 5, 0, False, *geom)
     assert crc == native.crc32c(d)
+
+
+@pytest.mark.parametrize("n,misalign", [((4 << 20) - 5, 3), (4 << 20, 0), ((4 << 20) + 16, 0)])
+def test_emulation_slot_kernel_longest_segment(native, n, misalign):
+    """The slot kernel's tile matrices cover segments of up to 1024 tiles
+    (4 MiB + up to 16 tail bytes); one more tile is outside its domain."""
+    d = os.urandom(n)
+    raw, crc, status = native.emulate_gpu_crc32c(d, misalign, native.crc32c(d), True, 12, 0)
+    assert crc == native.crc32c(d) and status == 1
+    _, _, st = native.emulate_gpu_crc32c(d + b"x" * 4096, 3, 0, True, 12, 0)
+    assert st == 3
+
+
+def test_slot_matrices_match_shift_tables(native):
+    """lane_k / tile_k columns are the GF(2) shifts the tree and fold tables
+    apply: shift(v, n) == XOR of the columns of v's set bits."""
+    import random
+    for nbytes in (64, 64 * 63, 4096, 4096 * 1023):
+        v = random.getrandbits(32)
+        cols = [native.crc32c_shift(1 << i, nbytes) for i in range(32)]
+        acc = 0
+        for i in range(32):
+            if v >> i & 1:
+                acc ^= cols[i]
+        assert acc == native.crc32c_shift(v, nbytes)
 
 
 def test_goog_hash_parsing(native):

@@ -400,6 +400,8 @@ class PyClient {
     d["bytes_in"] = s.bytes_in.load();
     d["bytes_out"] = s.bytes_out.load();
     d["path"] = client_->transport_path();
+    d["transport"] = client_->transport_name();
+    d["dials"] = client_->stats().dials.load();
     return d;
   }
   StorageClient& client() { return *client_; }

@@ -23,6 +23,7 @@
 #include "net/buffered.h"
 #include "proto/storage_v2.h"
 #include "server/fakegcs.h"
+#include "server/media.h"
 
 namespace gcsb {
 namespace {
@@ -61,6 +62,9 @@ struct ServerStream {
   uint32_t id = 0;
   HeaderList headers;
   std::string path, authorization;
+  // a plain HTTP/2 request (GET/HEAD of XML / JSON API paths), not gRPC
+  bool http = false;
+  std::string method, range;
   RecvBuf buf;  // unparsed request bytes
   std::vector<std::string> messages;
   std::atomic<bool> cancelled{false};
@@ -221,20 +225,34 @@ class H2ServerConn {
     auto s = std::make_shared<ServerStream>();
     s->id = id;
     s->headers = hl;
+    bool grpc = false;
     for (const auto& kv : hl) {
       if (kv.first == ":path") {
         const std::string svc = v2::kService;
         s->path = starts_with(kv.second, svc) ? kv.second.substr(svc.size()) : kv.second;
       } else if (kv.first == "authorization") {
         s->authorization = kv.second;
+      } else if (kv.first == ":method") {
+        s->method = kv.second;
+      } else if (kv.first == "content-type") {
+        grpc = starts_with(kv.second, "application/grpc");
+      } else if (kv.first == "range") {
+        s->range = kv.second;
       }
     }
+    // HTTP/2 media requests (the reference's http2 client mode, main.go:74-81)
+    // share the connection machinery with gRPC: GET/HEAD without a gRPC
+    // content-type
+    s->http = !grpc && (s->method == "GET" || s->method == "HEAD");
     {
       std::lock_guard<std::mutex> lk(mu_);
       streams_[id] = s;
     }
     w_.register_stream(id);
-    ++srv_.stats().grpc_calls;
+    if (s->http)
+      ++srv_.stats().http_requests;
+    else
+      ++srv_.stats().grpc_calls;
     if (end_stream) dispatch(s);
   }
 
@@ -408,6 +426,7 @@ class H2ServerConn {
 
   void handle(ServerStream& s) {
     try {
+      if (s.http) return http_request(s);
       if (!auth_ok(s)) return;
       if (s.path == "ReadObject") return read_object(s);
       if (s.path == "GetObject") return get_object(s);
@@ -426,6 +445,136 @@ class H2ServerConn {
         }
       }
     }
+  }
+
+  // --- plain HTTP/2 requests ---------------------------------------------------
+  void http_respond(ServerStream& s, int status, const MediaHeaders& h, const std::string& body,
+                    const std::string& ctype, bool head_only = false) {
+    HeaderList hl{{":status", std::to_string(status)}};
+    for (const auto& kv : h) hl.emplace_back(to_lower(kv.first), kv.second);
+    if (!body.empty()) hl.emplace_back("content-type", ctype);
+    hl.emplace_back("content-length", std::to_string(body.size()));
+    std::string block;
+    enc_.encode(hl, &block);
+    if (body.empty() || head_only) return w_.write_headers(s.id, block, true);
+    w_.write_headers(s.id, block, false);
+    size_t off = 0;
+    while (off < body.size()) {
+      size_t n = w_.reserve(s.id, body.size() - off);
+      if (n == 0) throw Cancelled{};
+      w_.write_frame(h2::kData, off + n == body.size() ? h2::kFlagEndStream : 0, s.id, body.data() + off, n);
+      off += n;
+    }
+  }
+
+  void http_request(ServerStream& s) {
+    const std::string json_ct = "application/json; charset=UTF-8";
+    if (srv_.config().require_auth &&
+        !(starts_with(s.authorization, "Bearer ") && srv_.token_valid(s.authorization.substr(7)))) {
+      ++srv_.stats().auth_failures;
+      return http_respond(s, 401, {{"WWW-Authenticate", "Bearer realm=\"https://accounts.google.com/\""}},
+                          json_error(401, "Invalid Credentials", "authError"), json_ct);
+    }
+    std::string path = s.path, query;
+    if (size_t q = path.find('?'); q != std::string::npos) {
+      query = path.substr(q + 1);
+      path.resize(q);
+    }
+    std::string alt, generation;
+    bool has_gen = false;
+    for (const auto& kv : parse_query(query)) {
+      if (kv.first == "alt") alt = kv.second;
+      if (kv.first == "generation") {
+        generation = kv.second;
+        has_gen = true;
+      }
+    }
+    const MediaTarget t = route_object_path(path, alt);
+    if (t.kind == MediaTarget::kNone) return http_respond(s, 404, {}, json_error(404, "Not Found", "notFound"), json_ct);
+    auto o = srv_.store().get(t.bucket, t.name);
+    if (!o)
+      return http_respond(s, 404, {}, json_error(404, "No such object: " + t.bucket + "/" + t.name, "notFound"),
+                          json_ct);
+    if (t.kind == MediaTarget::kJsonMeta) return http_respond(s, 200, {}, object_json(*o).dump(), json_ct);
+    auto& f = srv_.faults();
+    for (int n = f.fail_next.load(); n > 0;) {
+      if (f.fail_next.compare_exchange_weak(n, n - 1)) {
+        ++srv_.stats().faults_injected;
+        const int st = f.fail_status.load();
+        return http_respond(s, st, {}, json_error(st, "injected fault", "backendError"), json_ct);
+      }
+    }
+    MediaPlan mp = plan_media(*o, s.range.empty() ? nullptr : &s.range, has_gen ? &generation : nullptr);
+    if (mp.status >= 400) return http_respond(s, mp.status, mp.headers, mp.body, mp.content_type);
+    if (int lat = f.latency_ms.load()) std::this_thread::sleep_for(std::chrono::milliseconds(lat));
+    HeaderList hl{{":status", std::to_string(mp.status)}};
+    for (const auto& kv : mp.headers) hl.emplace_back(to_lower(kv.first), kv.second);
+    hl.emplace_back("content-length", std::to_string(mp.len));
+    std::string block;
+    enc_.encode(hl, &block);
+    const bool empty = s.method == "HEAD" || mp.len == 0;
+    w_.write_headers(s.id, block, empty);
+    if (!empty) send_object_body(s, *o, mp.start, mp.len);
+  }
+
+  // Object bytes [start, start + len) as DATA frames (END_STREAM on the last),
+  // zero-copy from the memfd, within the peer's flow-control windows; the
+  // fault knobs cut the connection / flip a byte as on HTTP/1.1.
+  void send_object_body(ServerStream& s, const StoredObject& o, uint64_t start, uint64_t len) {
+    auto& f = srv_.faults();
+    int64_t disc = f.disconnect_count.load() > 0 ? f.disconnect_at.load() : -1;
+    int64_t corrupt = f.corrupt_count.load() > 0 ? f.corrupt_at.load() : -1;
+    const int64_t bps = f.throttle_bps.load();
+    const int64_t t0 = now_ns();
+    uint64_t sent = 0;
+    while (sent < len) {
+      if (s.cancelled) throw Cancelled{};
+      const uint64_t off = start + sent;
+      uint64_t want = std::min<uint64_t>(len - sent, 8u << 20);
+      if (bps > 0) want = std::min<uint64_t>(want, std::max<int64_t>(4096, bps / 100));
+      const size_t n = w_.reserve(s.id, want);
+      if (n == 0) throw Cancelled{};
+      if (disc >= 0 && static_cast<int64_t>(off + n) > disc && static_cast<int64_t>(off) <= disc) {
+        disc = -1;
+        if (f.disconnect_count.fetch_sub(1) > 0) {
+          ++srv_.stats().faults_injected;
+          srv_.stats().bytes_sent += sent;
+          ::shutdown(bc_.conn().fd(), SHUT_RDWR);
+          throw Cancelled{};
+        }
+      }
+      const uint8_t* p = o.bytes(off, n);
+      std::vector<SendPiece> pieces;
+      uint8_t bad = 0;
+      int ffd = -1;
+      uint64_t foff = 0;
+      if (corrupt >= 0 && static_cast<int64_t>(off) <= corrupt && static_cast<int64_t>(off + n) > corrupt &&
+          f.corrupt_count.fetch_sub(1) > 0) {
+        const uint64_t k = static_cast<uint64_t>(corrupt) - off;
+        bad = static_cast<uint8_t>(p[k] ^ 0x5A);
+        if (k) pieces.push_back(mem(p, k));
+        pieces.push_back(mem(&bad, 1));
+        if (n - k - 1) pieces.push_back(mem(p + k + 1, n - k - 1));
+        ++srv_.stats().faults_injected;
+        corrupt = -1;
+      } else if (srv_.config().zero_copy && o.file_range(off, &ffd, &foff)) {
+        SendPiece fp;
+        fp.n = n;
+        fp.fd = ffd;
+        fp.foff = foff;
+        pieces.push_back(fp);
+      } else {
+        pieces.push_back(mem(p, n));
+      }
+      w_.write_frame_pieces(h2::kData, sent + n == len ? h2::kFlagEndStream : 0, s.id, pieces, n);
+      sent += n;
+      if (bps > 0) {
+        int64_t due = t0 + static_cast<int64_t>(sent * 1e9 / static_cast<double>(bps));
+        int64_t now = now_ns();
+        if (due > now) std::this_thread::sleep_for(std::chrono::nanoseconds(due - now));
+      }
+    }
+    srv_.stats().bytes_sent += sent;
   }
 
   void read_object(ServerStream& s) {

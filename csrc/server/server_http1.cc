@@ -14,6 +14,7 @@
 #include "http1/http1.h"
 #include "net/buffered.h"
 #include "server/fakegcs.h"
+#include "server/media.h"
 #include "storage/auth.h"
 #include "storage/client.h"
 
@@ -43,25 +44,6 @@ struct Request {
 };
 
 struct CloseConnection {};
-
-std::string rfc3339(int64_t us) {
-  time_t s = static_cast<time_t>(us / 1000000);
-  tm t{};
-  gmtime_r(&s, &t);
-  char b[64];
-  std::snprintf(b, sizeof(b), "%04d-%02d-%02dT%02d:%02d:%02d.%03dZ", t.tm_year + 1900, t.tm_mon + 1, t.tm_mday,
-                t.tm_hour, t.tm_min, t.tm_sec, static_cast<int>((us / 1000) % 1000));
-  return b;
-}
-
-std::string http_date(int64_t us) {
-  time_t s = static_cast<time_t>(us / 1000000);
-  tm t{};
-  gmtime_r(&s, &t);
-  char b[64];
-  std::strftime(b, sizeof(b), "%a, %d %b %Y %H:%M:%S GMT", &t);
-  return b;
-}
 
 const char* reason_phrase(int st) {
   switch (st) {
@@ -99,44 +81,6 @@ void respond(Conn& c, int status, Headers h, const std::string& body,
   h.emplace_back("Server", "gcsb-fakegcs");
   write_head(c, status, h, body.size());
   if (!body.empty()) c.write_all(body.data(), body.size());
-}
-
-std::string json_error(int code, const std::string& msg, const std::string& reason) {
-  Json e = Json::object();
-  Json err = Json::object();
-  err.set("code", Json::num(code));
-  err.set("message", Json::str(msg));
-  Json arr = Json::array();
-  Json one = Json::object();
-  one.set("message", Json::str(msg));
-  one.set("reason", Json::str(reason));
-  one.set("domain", Json::str("global"));
-  arr.push(one);
-  err.set("errors", arr);
-  e.set("error", err);
-  return e.dump();
-}
-
-Json object_json(const StoredObject& o, bool force_md5 = true) {
-  Json j = Json::object();
-  j.set("kind", Json::str("storage#object"));
-  j.set("id", Json::str(o.bucket + "/" + o.name + "/" + std::to_string(o.generation)));
-  j.set("selfLink", Json::str("/storage/v1/b/" + o.bucket + "/o/" + url_encode(o.name)));
-  j.set("mediaLink", Json::str("/download/storage/v1/b/" + o.bucket + "/o/" + url_encode(o.name) +
-                               "?generation=" + std::to_string(o.generation) + "&alt=media"));
-  j.set("name", Json::str(o.name));
-  j.set("bucket", Json::str(o.bucket));
-  j.set("generation", Json::str(std::to_string(o.generation)));
-  j.set("metageneration", Json::str(std::to_string(o.metageneration)));
-  j.set("contentType", Json::str(o.content_type));
-  j.set("storageClass", Json::str("STANDARD"));
-  j.set("size", Json::str(std::to_string(o.size)));
-  if ((force_md5 || o.md5_ready()) && !o.md5().empty()) j.set("md5Hash", Json::str(base64_encode(o.md5())));
-  j.set("crc32c", Json::str(crc32c_b64(o.crc32c)));
-  j.set("etag", Json::str("CK" + std::to_string(o.generation % 1000000) + "E="));
-  j.set("timeCreated", Json::str(rfc3339(o.created_us)));
-  j.set("updated", Json::str(rfc3339(o.created_us)));
-  return j;
 }
 
 class Http1Handler {
@@ -337,64 +281,19 @@ class Http1Handler {
     respond(c_, 200, {}, "{}");
   }
 
-  // Parses a Range header "bytes=a-b" / "bytes=a-" / "bytes=-n".
-  static bool parse_range(const std::string& v, uint64_t size, uint64_t* a, uint64_t* b) {
-    if (!starts_with(v, "bytes=")) return false;
-    std::string s = v.substr(6);
-    size_t dash = s.find('-');
-    if (dash == std::string::npos) return false;
-    std::string x = s.substr(0, dash), y = s.substr(dash + 1);
-    if (x.empty()) {
-      uint64_t n = std::stoull(y);
-      *a = n >= size ? 0 : size - n;
-      *b = size ? size - 1 : 0;
-      return true;
-    }
-    *a = std::stoull(x);
-    *b = y.empty() ? (size ? size - 1 : 0) : std::min<uint64_t>(std::stoull(y), size ? size - 1 : 0);
-    return true;
-  }
-
   void send_media(const Request& r, const StoredObject& o, bool xml) {
-    if (r.has_q("generation") && std::strtoll(r.q("generation").c_str(), nullptr, 10) != o.generation)
-      return respond(c_, 404, {}, json_error(404, "No such object: " + o.bucket + "/" + o.name + "#" + r.q("generation"),
+    const std::string gen = r.q("generation");
+    if (r.has_q("generation") && std::strtoll(gen.c_str(), nullptr, 10) != o.generation)
+      return respond(c_, 404, {}, json_error(404, "No such object: " + o.bucket + "/" + o.name + "#" + gen,
                                              "notFound"));
     if (maybe_fail(xml)) return;
-    if (o.hollow)
-      return respond(c_, 412, {}, json_error(412, "object content was not retained (server retain_uploads=false)",
-                                             "conditionNotMet"));
-    uint64_t a = 0, b = o.size ? o.size - 1 : 0;
-    bool partial = false;
-    if (const auto* rg = r.header("Range"); rg && o.size > 0) {
-      if (parse_range(*rg, o.size, &a, &b)) {
-        if (a >= o.size) {
-          return respond(c_, 416, {{"Content-Range", "bytes */" + std::to_string(o.size)}},
-                         json_error(416, "Requested range not satisfiable", "requestedRangeNotSatisfiable"));
-        }
-        partial = true;
-      }
-    }
-    uint64_t len = o.size ? b - a + 1 : 0;
-    Headers h{{"Content-Type", o.content_type},
-              {"Accept-Ranges", "bytes"},
-              {"x-goog-generation", std::to_string(o.generation)},
-              {"x-goog-metageneration", std::to_string(o.metageneration)},
-              {"x-goog-stored-content-length", std::to_string(o.size)},
-              {"x-goog-stored-content-encoding", "identity"},
-              {"x-goog-storage-class", "STANDARD"},
-              {"x-goog-hash", "crc32c=" + crc32c_b64(o.crc32c)},
-              {"ETag", "\"" + std::to_string(o.generation) + "\""},
-              {"Last-Modified", http_date(o.created_us)},
-              {"Server", "gcsb-fakegcs"}};
-    if (!o.md5().empty()) h.emplace_back("x-goog-hash", "md5=" + base64_encode(o.md5()));
-    if (partial)
-      h.emplace_back("Content-Range",
-                     "bytes " + std::to_string(a) + "-" + std::to_string(b) + "/" + std::to_string(o.size));
+    MediaPlan mp = plan_media(o, r.header("Range"), nullptr);
+    if (mp.status >= 400) return respond(c_, mp.status, mp.headers, mp.body, mp.content_type);
     auto& f = srv_.faults();
     if (int lat = f.latency_ms.load()) std::this_thread::sleep_for(std::chrono::milliseconds(lat));
-    write_head(c_, partial ? 206 : 200, h, len);
+    write_head(c_, mp.status, mp.headers, mp.len);
     if (r.method == "HEAD") return;
-    stream_bytes(o, a, len);
+    stream_bytes(o, mp.start, mp.len);
   }
 
   void stream_bytes(const StoredObject& o, uint64_t start, uint64_t len) {

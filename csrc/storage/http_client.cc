@@ -1,10 +1,14 @@
 // HTTP transport for the storage client: XML API media reads (the library's
 // default read path), JSON API reads (alt=media), JSON
 // metadata/list, and resumable / single-request uploads.
+#include <atomic>
+#include <condition_variable>
 #include <cstring>
+#include <mutex>
 
 #include "core/json.h"
 #include "core/util.h"
+#include "h2/h2_client.h"
 #include "http1/http1.h"
 #include "storage/client.h"
 
@@ -39,6 +43,163 @@ ObjectMeta meta_from_json(const Json& j) {
   throw StorageError(msg, http_retryable(status), status);
 }
 
+// ObjectInfo of a media response from its headers (name -> value lookups are
+// case-insensitive: HTTP/1.1 names as sent, HTTP/2 names lower-case).
+template <typename Get, typename Each>
+ObjectInfo media_info(int status, int64_t content_length, int64_t offset, Get get, Each each_hash) {
+  ObjectInfo info;
+  info.start_offset = offset;
+  if (const std::string* g = get("x-goog-generation")) info.generation = std::stoll(*g);
+  each_hash([&](const std::string& v) { parse_goog_hash(v, &info.has_crc32c, &info.crc32c, &info.md5); });
+  if (status == 206) {
+    if (const std::string* cr = get("content-range")) {
+      size_t slash = cr->find('/');
+      if (slash != std::string::npos && (*cr)[slash + 1] != '*') info.size = std::stoll(cr->substr(slash + 1));
+    }
+  } else if (content_length >= 0) {
+    info.size = content_length;
+  }
+  if (const std::string* sl = get("x-goog-stored-content-length"); sl && info.size < 0) info.size = std::stoll(*sl);
+  return info;
+}
+
+// One media GET on an HTTP/2 stream.  The connection's reader thread hands
+// DATA to it on the socket, so body bytes are recv()'d straight into the sink
+// window (one copy, as on HTTP/1.1 and gRPC).  Sink errors are recorded and
+// the rest of the body skipped; the caller rethrows after completion.
+class H2MediaGet : public H2ClientStream {
+ public:
+  H2MediaGet(Sink& sink, ReadResult* rr, uint64_t* delivered, int64_t offset, int64_t limit, bool first_attempt)
+      : sink_(sink), rr_(rr), delivered_(delivered), offset_(offset), limit_(limit), first_(first_attempt),
+        cap_total_(limit >= 0 ? *delivered + static_cast<uint64_t>(limit) : ~0ull) {}
+
+  void on_headers(const HeaderList& h, bool end_stream) override {
+    if (!got_head_) {
+      got_head_ = true;
+      int64_t clen = -1;
+      for (const auto& kv : h) {
+        if (kv.first == ":status") status_ = std::atoi(kv.second.c_str());
+        if (kv.first == "content-length") clen = std::stoll(kv.second);
+      }
+      if (status_ == 200 || status_ == 206) {
+        auto get = [&](const char* n) -> const std::string* {
+          for (const auto& kv : h)
+            if (kv.first == n) return &kv.second;
+          return nullptr;
+        };
+        auto each = [&](auto&& f) {
+          for (const auto& kv : h)
+            if (kv.first == "x-goog-hash") f(kv.second);
+        };
+        try {
+          ObjectInfo info = media_info(status_, clen, offset_, get, each);
+          if (status_ == 200 && offset_ > 0) throw StorageError("http2 GET: server ignored Range", true);
+          const bool full = offset_ == 0 && limit_ < 0 && status_ == 200;
+          if (first_) {
+            ObjectInfo bi = info;
+            if (!full) bi.has_crc32c = false;
+            sink_.begin(bi);
+            rr_->sink_begun = true;
+            rr_->info = info;
+          }
+        } catch (const std::exception& e) {
+          fail(e.what(), false);
+        }
+      }
+    }
+    if (end_stream) done();
+  }
+
+  void on_data(BufferedConn& bc, uint32_t n, bool end_stream) override {
+    if (status_ != 200 && status_ != 206) {
+      // error body (JSON / XML), kept for the message
+      while (n > 0) {
+        char tmp[4096];
+        size_t k = std::min<size_t>(n, sizeof(tmp));
+        bc.read_exact(tmp, k);
+        if (err_body_.size() < 4096) err_body_.append(tmp, k);
+        n -= static_cast<uint32_t>(k);
+      }
+    } else {
+      while (n > 0) {
+        if (failed_.load() || *delivered_ >= cap_total_) {
+          if (!failed_.load()) fail("http2 GET: server sent more than the requested range", false);
+          bc.skip(n);
+          break;
+        }
+        Window w;
+        try {
+          w = sink_.acquire(n);
+        } catch (const std::exception& e) {
+          fail(std::string("sink: ") + e.what(), false);
+          continue;
+        }
+        size_t cap = std::min<uint64_t>({static_cast<uint64_t>(n), w.cap, cap_total_ - *delivered_});
+        size_t m = bc.read_some(w.ptr, cap);
+        if (m == 0) throw StorageError("connection closed inside a DATA frame", true);
+        if (!rr_->first_byte_ns) rr_->first_byte_ns = now_ns();
+        try {
+          sink_.commit(m);
+        } catch (const std::exception& e) {
+          fail(std::string("sink: ") + e.what(), false);
+        }
+        *delivered_ += m;
+        n -= static_cast<uint32_t>(m);
+      }
+    }
+    if (end_stream) done();
+  }
+
+  void on_reset(uint32_t code) override {
+    fail("http2 GET: RST_STREAM code " + std::to_string(code), true);
+    done();
+  }
+  void on_conn_error(const std::string& msg) override {
+    fail("http2 connection error: " + msg, true);
+    done();
+  }
+
+  // Waits for END_STREAM / reset; returns the HTTP status, throws on
+  // transport or sink errors.
+  int wait(std::string* body) {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [&] { return done_; });
+    if (!error_.empty()) throw StorageError(error_, retryable_);
+    if (!got_head_) throw StorageError("http2 GET: stream ended without a response", true);
+    *body = err_body_;
+    return status_;
+  }
+
+ private:
+  void fail(const std::string& msg, bool retryable) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (error_.empty()) {
+      error_ = msg;
+      retryable_ = retryable;
+    }
+    failed_ = true;
+  }
+  void done() {
+    std::lock_guard<std::mutex> lk(mu_);
+    done_ = true;
+    cv_.notify_all();
+  }
+  Sink& sink_;
+  ReadResult* rr_;
+  uint64_t* delivered_;
+  int64_t offset_, limit_;
+  bool first_;
+  uint64_t cap_total_;
+  bool got_head_ = false;
+  int status_ = 0;
+  std::string err_body_;
+  std::atomic<bool> failed_{false};
+  std::mutex mu_;
+  std::condition_variable cv_;
+  bool done_ = false, retryable_ = false;
+  std::string error_;
+};
+
 class HttpStorageClient : public StorageClient {
  public:
   explicit HttpStorageClient(const ClientConfig& cfg)
@@ -55,11 +216,69 @@ class HttpStorageClient : public StorageClient {
     decorators_.push_back(&ua_);
   }
 
-  std::string transport_name() const override { return "http1"; }
+  std::string transport_name() const override { return h2_media_ ? "http2" : "http1"; }
 
  protected:
+  std::string media_path(const std::string& bucket, const std::string& object, int64_t pin_generation) const {
+    std::string path;
+    if (cfg_.http_api == "json")
+      path = "/storage/v1/b/" + url_encode(bucket) + "/o/" + url_encode(object) + "?alt=media";
+    else
+      path = "/" + bucket + "/" + url_encode(object, true);
+    if (pin_generation)
+      path += std::string(cfg_.http_api == "json" ? "&" : "?") + "generation=" + std::to_string(pin_generation);
+    return path;
+  }
+
+  std::shared_ptr<H2ClientConn> h2_conn() {
+    std::lock_guard<std::mutex> lk(h2_mu_);
+    if (!h2_ || !h2_->usable()) {
+      if (h2_) h2_->close();
+      h2_ = H2ClientConn::dial(cfg_.endpoint, h2_opt_);
+      ++stats_.dials;
+    }
+    return h2_;
+  }
+
+  // -client-protocol http2: the media GET on an HTTP/2 stream (h2c with prior
+  // knowledge on http://, ALPN h2 on https://), all GETs of the client
+  // multiplexed on one connection.  The reference's http2 transport
+  // (main.go:74-81) forces HTTP/2 with keep-alives disabled; metadata, list
+  // and upload requests here stay on the HTTP/1.1 pool, which runs without
+  // keep-alive in this mode.
+  void read_attempt_h2(const std::string& bucket, const std::string& object, Sink& sink, int64_t offset,
+                       int64_t limit, bool first_attempt, ReadResult* rr, uint64_t* delivered) {
+    Headers dh;
+    for (RequestDecorator* d : decorators_) d->decorate(dh);
+    HeaderList h = {{":method", "GET"},
+                    {":scheme", cfg_.endpoint.scheme == "https" ? "https" : "http"},
+                    {":path", media_path(bucket, object, rr->pin_generation)},
+                    {":authority", cfg_.endpoint.host_header()}};
+    for (const auto& kv : dh) h.emplace_back(to_lower(kv.first), kv.second);
+    if (offset > 0 || limit >= 0) {
+      std::string r = "bytes=" + std::to_string(offset) + "-";
+      if (limit >= 0) r += std::to_string(offset + limit - 1);
+      h.emplace_back("range", r);
+    }
+    h.emplace_back("x-goog-api-client", "gccl/1.33.0 gcsb-native");
+    auto call = std::make_shared<H2MediaGet>(sink, rr, delivered, offset, limit, first_attempt);
+    auto c = h2_conn();
+    std::string body;
+    int status = 0;
+    try {
+      c->start_stream(call, h, true);
+      status = call->wait(&body);
+    } catch (...) {
+      c->end_stream(*call, true);
+      throw;
+    }
+    c->end_stream(*call, false);
+    if (status != 200 && status != 206) throw_status(status, "GET " + bucket + "/" + object, body);
+  }
+
   void read_attempt(const std::string& bucket, const std::string& object, Sink& sink, int64_t offset, int64_t limit,
                     bool first_attempt, ReadResult* rr, uint64_t* delivered) override {
+    if (h2_media_) return read_attempt_h2(bucket, object, sink, offset, limit, first_attempt, rr, delivered);
     Http1Exchange ex(pool_, decorators_);
     Headers h;
     if (offset > 0 || limit >= 0) {
@@ -68,32 +287,17 @@ class HttpStorageClient : public StorageClient {
       h.emplace_back("Range", r);
     }
     h.emplace_back("x-goog-api-client", "gccl/1.33.0 gcsb-native");
-    std::string path;
-    if (cfg_.http_api == "json")
-      path = "/storage/v1/b/" + url_encode(bucket) + "/o/" + url_encode(object) + "?alt=media";
-    else
-      path = "/" + bucket + "/" + url_encode(object, true);
-    if (rr->pin_generation)
-      path += std::string(cfg_.http_api == "json" ? "&" : "?") + "generation=" + std::to_string(rr->pin_generation);
-    const HttpResponseHead& head = ex.send("GET", path, h);
+    const HttpResponseHead& head = ex.send("GET", media_path(bucket, object, rr->pin_generation), h);
     if (head.status != 200 && head.status != 206) {
       std::string body = ex.read_body_string(1 << 20);
       throw_status(head.status, "GET " + bucket + "/" + object, body);
     }
-    ObjectInfo info;
-    info.start_offset = offset;
-    if (const auto* g = head.get("x-goog-generation")) info.generation = std::stoll(*g);
-    for (const auto& kv : head.headers)
-      if (iequals(kv.first, "x-goog-hash")) parse_goog_hash(kv.second, &info.has_crc32c, &info.crc32c, &info.md5);
-    if (head.status == 206) {
-      if (const auto* cr = head.get("Content-Range")) {
-        size_t slash = cr->find('/');
-        if (slash != std::string::npos && (*cr)[slash + 1] != '*') info.size = std::stoll(cr->substr(slash + 1));
-      }
-    } else if (head.content_length >= 0) {
-      info.size = head.content_length;
-    }
-    if (const auto* sl = head.get("x-goog-stored-content-length"); sl && info.size < 0) info.size = std::stoll(*sl);
+    ObjectInfo info = media_info(
+        head.status, head.content_length, offset, [&](const char* n) { return head.get(n); },
+        [&](auto&& f) {
+          for (const auto& kv : head.headers)
+            if (iequals(kv.first, "x-goog-hash")) f(kv.second);
+        });
     // A whole-object CRC only applies to a full read (the library skips the
     // check for ranged reads).
     bool full = offset == 0 && limit < 0 && head.status == 200;
@@ -314,6 +518,15 @@ class HttpStorageClient : public StorageClient {
 
  private:
   Http1Pool pool_;
+  const bool h2_media_ = cfg_.protocol == "http2";
+  H2ClientOptions h2_opt_ = [this] {
+    H2ClientOptions o;
+    o.sock = with_alpn(cfg_.sock, "h2");
+    o.cpus = cfg_.cpus;
+    return o;
+  }();
+  std::mutex h2_mu_;
+  std::shared_ptr<H2ClientConn> h2_;
   UserAgentDecorator ua_;
   std::unique_ptr<AuthDecorator> auth_;
   std::vector<RequestDecorator*> decorators_;

@@ -69,6 +69,20 @@ bool prefer_numa_node(int node) {
   return ::syscall(SYS_set_mempolicy, kMpolPreferred, &mask, 64) == 0;
 }
 
+bool bind_numa_node(int node) {
+  constexpr int kMpolDefault = 0, kMpolBind = 2;
+  if (node < 0 || node >= 64) return ::syscall(SYS_set_mempolicy, kMpolDefault, nullptr, 0) == 0;
+  unsigned long mask = 1ul << node;
+  return ::syscall(SYS_set_mempolicy, kMpolBind, &mask, 64) == 0;
+}
+
+bool bind_range_to_node(void* p, size_t len, int node) {
+  constexpr int kMpolBind = 2;
+  if (node < 0 || node >= 64) return false;
+  unsigned long mask = 1ul << node;
+  return ::syscall(SYS_mbind, p, len, kMpolBind, &mask, 64, 0) == 0;
+}
+
 void name_current_thread(const char* name) {
   char buf[16];
   std::snprintf(buf, sizeof(buf), "%s", name);

@@ -26,6 +26,11 @@ std::vector<long> numa_nodes_of(const void* p, size_t len, size_t stride = 1 << 
 int current_numa_node();
 // Memory policy of this thread: prefer `node` for new pages (-1 = local).
 bool prefer_numa_node(int node);
+// Memory policy of this thread: new pages only from `node` (-1 = default).
+bool bind_numa_node(int node);
+// Pages of [p, p+len) (not yet faulted in) only from `node`; false if the
+// kernel refused (then placement falls back to first touch).
+bool bind_range_to_node(void* p, size_t len, int node);
 // Round-robin pick: thread k gets cpus[k % n] (single-CPU pinning) when
 // `spread` is set, else the whole set.
 std::vector<int> cpus_for(const std::vector<int>& cpus, int k, bool spread);

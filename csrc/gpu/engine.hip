@@ -103,7 +103,11 @@ class PinnedPool {
       void* p = nullptr;
       if (posix_memalign(&p, huge, len) == 0) {
         (void)madvise(p, len, MADV_HUGEPAGE);
-        std::memset(p, 0, len);  // fault in now, on this thread's NUMA node
+        // the calling (pinned, GPU-local) thread's node, strictly: first touch
+        // alone let a 2 MiB page land on the other socket when the local node
+        // had no free huge page (bench numa.ring_pages, profiles/r2_session_c)
+        (void)bind_range_to_node(p, len, current_numa_node());
+        std::memset(p, 0, len);  // fault in now
         if (hipHostRegister(p, len, hipHostRegisterDefault) == hipSuccess) {
           std::lock_guard<std::mutex> lk(mu());
           registered()[p] = len;

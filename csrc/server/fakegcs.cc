@@ -38,9 +38,9 @@ void FakeGcsServer::start() {
     } else {
       std::thread([this] {
         pin_current_thread(cfg_.cpus);
-        prefer_numa_node(current_numa_node());
+        bind_numa_node(current_numa_node());
         PatternBuffer::instance().memfd();
-        prefer_numa_node(-1);
+        bind_numa_node(-1);
       }).join();
     }
   }

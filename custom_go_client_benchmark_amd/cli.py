@@ -136,7 +136,13 @@ def main(argv: list[str] | None = None) -> int:
     if aff == "auto":
         # discard sink: no GPU to be near; under a CPU quota keep the threads
         # on as many cores as the quota pays for (parallel/affinity.py)
-        aff = ("share" if fs.get("slices") > 1 else "same") if sink == "gpu" else "quota"
+        # one GPU reader with one stream per read: the bench's placement (a
+        # quiet core each for the receive thread, the endpoint and the GPU
+        # submitter, profiles/r2_placement); several readers share one L3 domain
+        if sink == "gpu":
+            aff = "share" if fs.get("slices") > 1 else ("pair" if fs.get("worker") == 1 else "same")
+        else:
+            aff = "quota"
         if fs.get("workload") == "write":
             # uploads: unpinned threads measured fastest on MI355X (64 MiB
             # WriteObject 8.1 ms vs 13.8-14.4 ms pinned; resumable HTTP 6.5 vs
@@ -146,6 +152,8 @@ def main(argv: list[str] | None = None) -> int:
         from .parallel import affinity
 
         placement = affinity.plan(device, aff)
+        if placement.get("aux"):
+            _native.set_submitter_cpus(placement["aux"])
 
     endpoint = fs.get("endpoint") or os.environ.get("GCSB_ENDPOINT", "") or os.environ.get("STORAGE_EMULATOR_HOST", "")
     ep_handle = None

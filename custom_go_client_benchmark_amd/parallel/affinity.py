@@ -25,18 +25,24 @@ def _read(path: str) -> str | None:
         return None
 
 
-def gpu_local_cpus(device: int) -> list[int]:
-    """CPUs of the GPU's NUMA node (intersected with our affinity)."""
+def _gpu_local(device: int) -> tuple[list[int], bool]:
+    """(CPUs of the GPU's NUMA node within our affinity, True) or, when that
+    is unknown or empty, (every CPU we may use, False)."""
     allowed = sorted(os.sched_getaffinity(0))
     try:
         bus = _native.gpu_pci_bus_id(device).lower()
     except Exception:
-        return allowed
+        return allowed, False
     cl = _read(f"/sys/bus/pci/devices/{bus}/local_cpulist")
     if not cl:
-        return allowed
+        return allowed, False
     local = [c for c in _native.parse_cpulist(cl) if c in set(allowed)]
-    return local or allowed
+    return (local, True) if local else (allowed, False)
+
+
+def gpu_local_cpus(device: int) -> list[int]:
+    """CPUs of the GPU's NUMA node (intersected with our affinity)."""
+    return _gpu_local(device)[0]
 
 
 def gpu_numa_node(device: int) -> int:
@@ -186,7 +192,7 @@ def plan(device: int, mode: str = "split", slot: int = 0) -> dict:
         # no GPU locality: the first quota-budget cores this process may use
         mine = trim_to_quota(sorted(os.sched_getaffinity(0)))
         return {"client": mine, "server": mine, "mode": mode, "quota_cpus": quota_budget()}
-    cpus = gpu_local_cpus(device)
+    cpus, local_ok = _gpu_local(device)
     if mode == "numa":
         return {"client": cpus, "server": cpus, "mode": mode}
     node = gpu_numa_node(device)
@@ -198,6 +204,13 @@ def plan(device: int, mode: str = "split", slot: int = 0) -> dict:
     k = [d for _, d in peers].index(device) if any(d == device for _, d in peers) else 0
     groups = l3_groups(cpus)
     share = max(1, len(groups) // max(1, len(peers)))
+    if not local_ok:
+        # no GPU-local CPUs in our cpuset (gpu_local_cpus fell back to all we
+        # may use): split those among the node's ranks by local rank instead,
+        # so ranks of different NUMA nodes do not pick the same domains
+        ranks = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1))
+        k = int(os.environ.get("LOCAL_RANK", "0") or 0) % ranks
+        share = max(1, len(groups) // ranks)
     # slot: this rank's index among ranks sharing ONE GPU (shared-GPU
     # rehearsals only; 0 on a node with a GPU per rank) -> the next L3 domains
     base = (k * share + slot) % max(1, len(groups))

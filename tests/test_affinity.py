@@ -69,3 +69,68 @@ def test_cpu_quota_and_trim(monkeypatch):
     assert a.trim_to_quota(list(range(8))) == list(range(8))  # 16-CPU budget > 8 CPUs
     files["/sys/fs/cgroup/cpu.max"] = "max 100000"
     assert a.cpu_quota() == 0.0 and a.quota_budget() == 0
+
+
+def _fake_topology(monkeypatch, a, ncpu=16, per_l3=8):
+    """ncpu CPUs: SMT siblings c and c + ncpu/2, L3 domains of per_l3 CPUs
+    (both siblings of a core in the same domain)."""
+    half = ncpu // 2
+    files = {}
+    for c in range(ncpu):
+        core = c % half
+        files[f"/sys/devices/system/cpu/cpu{c}/topology/physical_package_id"] = "0"
+        files[f"/sys/devices/system/cpu/cpu{c}/topology/core_id"] = str(core)
+        dom = core // (per_l3 // 2)
+        lo = dom * (per_l3 // 2)
+        files[f"/sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list"] = \
+            f"{lo}-{lo + per_l3 // 2 - 1},{lo + half}-{lo + half + per_l3 // 2 - 1}"
+    monkeypatch.setattr(a, "_read", lambda p: files.get(p))
+    monkeypatch.setattr(a.os, "sched_getaffinity", lambda pid: set(range(ncpu)))
+
+
+def test_quiet_cores_order_and_cpu0_last(monkeypatch):
+    from custom_go_client_benchmark_amd.parallel import affinity as a
+
+    _fake_topology(monkeypatch, a)
+    busy = {c: 0.0 for c in range(16)}
+    busy[1] = 0.9   # core 1 busy on its first thread
+    busy[10] = 0.5  # core 2 busy on its SMT sibling
+    q = a.quiet_cores(list(range(8)) + list(range(8, 16)), busy)
+    flat = [core[0] for core in q]
+    assert flat[-1] == 0            # CPU 0's core goes last (housekeeping)
+    assert flat.index(1) > flat.index(3) and flat.index(2) > flat.index(3)
+    assert all(len(core) == 2 for core in q)
+
+
+def test_pair_plan_picks_quiet_disjoint_cores_in_one_domain(monkeypatch):
+    from custom_go_client_benchmark_amd.parallel import affinity as a
+
+    _fake_topology(monkeypatch, a)
+    busy = {c: 0.0 for c in range(16)}
+    for c in (4, 5, 12):  # domain 1 partly busy
+        busy[c] = 0.8
+    monkeypatch.setattr(a, "cpu_busy", lambda sample_s=0.15: busy)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
+    monkeypatch.setenv("LOCAL_RANK", "0")
+    p = a.plan(0, "pair")
+    assert p["picked_by"] == "quiet"
+    cl, sv, ax = set(p["client"]), set(p["server"]), set(p["aux"])
+    assert not (cl & sv) and not (cl & ax) and not (sv & ax)
+    dom0 = {0, 1, 2, 3, 8, 9, 10, 11}
+    assert cl | sv | ax <= dom0       # the quiet domain, one L3
+    assert 0 not in cl | sv | ax      # CPU 0's core avoided while others are free
+
+
+def test_plan_without_gpu_locality_splits_by_local_rank(monkeypatch):
+    from custom_go_client_benchmark_amd.parallel import affinity as a
+
+    _fake_topology(monkeypatch, a, ncpu=32, per_l3=8)
+    monkeypatch.setenv("GCSB_QUIET_CORES", "0")
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "4")
+    seen = []
+    for r in range(4):
+        monkeypatch.setenv("LOCAL_RANK", str(r))
+        seen.append(set(a.plan(0, "share")["client"]))
+    for i in range(4):
+        for j in range(i + 1, 4):
+            assert not (seen[i] & seen[j])  # ranks never share a domain

@@ -116,6 +116,12 @@ def build_parser() -> argparse.ArgumentParser:
                     help="streams per object read in the HEADLINE run (1 = the reference's sequential read)")
     ap.add_argument("--sliced-streams", type=int, default=8,
                     help="streams per read in the `sliced` extension block (0 = skip the block)")
+    ap.add_argument("--sliced-slot-bytes", default="2MiB",
+                    help="sliced block: ring slot per sink (2 MiB x 8 won 2 of 2 interleaved reps against 4 x 4 MiB, "
+                         "8 MiB x 2, 4/16 pool streams and async hand-off: profiles/r2_sliced)")
+    ap.add_argument("--sliced-slots", type=int, default=8, help="sliced block: ring slots per sink")
+    ap.add_argument("--sliced-async-submit", type=int, default=0, choices=[0, 1],
+                    help="sliced block: slot hand-off on the device submitter thread (default inline)")
     ap.add_argument("--piece-bytes", default="8MiB",
                     help="sliced reads: streams pull pieces of this size from a shared cursor (0 = fixed shares)")
     ap.add_argument("--piece-min-bytes", default="0",
@@ -261,10 +267,10 @@ def run_rank(args) -> int:
         "async_submit": bool(args.async_submit),
         "rcvbuf": parse_size(args.rcvbuf),
     }
-    # the sliced extension keeps the geometry tuned for 8 streams in round 1
-    # (4 x 4 MiB per sink, inline submit: profiles/r1_pieces, r1_submit_ab)
-    sliced_cfg = {"slices": args.sliced_streams, "ring_slot_bytes": 4 << 20, "ring_slots": 4,
-                  "async_submit": False}
+    # the sliced extension: inline slot hand-off (r1_submit_ab), 2 MiB x 8
+    # ring per sink (profiles/r2_sliced)
+    sliced_cfg = {"slices": args.sliced_streams, "ring_slot_bytes": parse_size(args.sliced_slot_bytes),
+                  "ring_slots": args.sliced_slots, "async_submit": bool(args.sliced_async_submit)}
 
     def sync():
         if torch.cuda.is_available():
@@ -419,7 +425,8 @@ def run_rank(args) -> int:
             st_sl = read_block(sliced_cfg, side_steps, 1, "sliced")
             srv_sl.stop()
             blocks["sliced"] = ("sliced", st_sl,
-                                {"streams_per_read": args.sliced_streams, "ring": "4x4MiB", "affinity": "share",
+                                {"streams_per_read": args.sliced_streams,
+                                 "ring": f"{args.sliced_slots}x{args.sliced_slot_bytes}", "affinity": "share",
                                  "piece_bytes": parse_size(args.piece_bytes), "note": "extension, not parity"})
         if use_gpu:
             blocks["write"] = ("write", write_block(side_steps, 1),
@@ -508,6 +515,9 @@ def run_rank(args) -> int:
                     b["slice_skew_ms"] = round(st["skew_max"], 3)
                     if st.get("cpu"):
                         b["process_cpu_s_per_gib"] = st["cpu"]["process_cpu_s_per_gib"]
+                        b["cpus_busy"] = st["cpu"].get("cpus_busy")
+                        if "cgroup_nr_throttled" in st["cpu"]:
+                            b["cgroup_nr_throttled"] = st["cpu"]["cgroup_nr_throttled"]
                 out[key] = b
             line = json.dumps(out)
             print(line, flush=True)

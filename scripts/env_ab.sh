@@ -1,8 +1,9 @@
 #!/bin/bash
 # Interleaved A/B of bench variants on one box (identical runs vary up to 2x
 # between and within boxes, so variants alternate within each rep).
-#   VARIANTS="A=ENV1=x,ENV2=y;B=ENV1=z"  REPS=4  ARGS="--side-steps 0"
-# Each variant is "<label>=<comma-separated env assignments>" (may be empty).
+#   VARIANTS="A=ENV1=x,ENV2=y;B=ENV1=z|--rcvbuf 32MiB"  REPS=4  ARGS="--side-steps 0"
+# Each variant is "<label>=<comma-separated env assignments>[|extra bench args]"
+# (either part may be empty).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=${OUT:-gpurun_out/env_ab}
@@ -12,9 +13,10 @@ ARGS=${ARGS:---steps 20 --warmup 3 --side-steps 0}
 IFS=';' read -ra VS <<< "$VARIANTS"
 for rep in $(seq 1 ${REPS:-3}); do
   for v in "${VS[@]}"; do
-    label=${v%%=*}; envs=${v#*=}
+    label=${v%%=*}; rest=${v#*=}; envs=${rest%%|*}; extra=""
+    [[ "$rest" == *"|"* ]] && extra=${rest#*|}
     IFS=',' read -ra EA <<< "$envs"
-    env "${EA[@]}" timeout -k 10 180 python bench.py $ARGS > $OUT/bench.log 2>&1 \
+    env "${EA[@]}" timeout -k 10 180 python bench.py $ARGS $extra > $OUT/bench.log 2>&1 \
       || { tail -20 $OUT/bench.log; exit 1; }
     grep -h '^{' $OUT/bench.log | sed "s/^{/{\"variant\": \"$label\", /" >> $OUT/runs.jsonl
     python3 - "$label" "$OUT/bench.log" <<'PY' | tee -a $OUT/ab.txt

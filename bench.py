@@ -524,7 +524,12 @@ def run_rank(args) -> int:
             out["numa"] = {"gpu_node": placement.get("numa_node"),
                            "object_pages": by_node(n.pattern_memfd_numa())}
             if head.get("ring_numa"):
-                out["numa"]["ring_pages"] = by_node(head["ring_numa"])
+                slots = head["ring_numa"]
+                total = [sum(c[i] for c in slots) for i in range(len(slots[0]))]
+                out["numa"]["ring_pages"] = by_node(total)
+                # per slot: the node holding most of its pages (-1 = not resident)
+                out["numa"]["ring_slot_nodes"] = [max(range(len(c) - 1), key=lambda i: c[i]) if sum(c[:-1]) else -1
+                                                  for c in slots]
             if args.workload == "read":
                 out["host_landed_p50_ms"] = round(head["host_p50_max"], 3)
                 out["verified_reads"] = int(head["verified_sum"])

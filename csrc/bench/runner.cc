@@ -58,14 +58,11 @@ uintptr_t Runner::landing_ptr(int w) const {
   return 0;
 }
 
-std::vector<long> Runner::ring_numa(int w) const {
-  std::vector<long> c(kNumaMaxNodes + 1, 0);
-  if (w < 0 || w >= static_cast<int>(gpu_sinks_.size()) || !gpu_sinks_[w]) return c;
-  for (const auto& [p, n] : gpu_sinks_[w]->ring_ranges()) {
-    std::vector<long> k = numa_nodes_of(p, n);
-    for (size_t i = 0; i < c.size(); ++i) c[i] += k[i];
-  }
-  return c;
+std::vector<std::vector<long>> Runner::ring_numa(int w) const {
+  std::vector<std::vector<long>> out;
+  if (w < 0 || w >= static_cast<int>(gpu_sinks_.size()) || !gpu_sinks_[w]) return out;
+  for (const auto& [p, n] : gpu_sinks_[w]->ring_ranges()) out.push_back(numa_nodes_of(p, n));
+  return out;
 }
 
 void Runner::reset_stats() {

@@ -114,8 +114,8 @@ class Runner {
   // HBM address worker w's last object landed at (GPU sink, object landing;
   // sliced reads: the shared landing buffer), 0 if none.
   uintptr_t landing_ptr(int w) const;
-  // NUMA placement of worker w's pinned ring (affinity.h numa_nodes_of)
-  std::vector<long> ring_numa(int w) const;
+  // NUMA placement of worker w's pinned ring, per slot (affinity.h numa_nodes_of)
+  std::vector<std::vector<long>> ring_numa(int w) const;
 
  private:
   void worker_main(int w);

@@ -501,7 +501,7 @@ class PyRunner {
   }
   std::string object_for(int w, int64_t seq) { return runner_->object_for(w, seq); }
   uintptr_t landing_ptr(int w) { return runner_->landing_ptr(w); }
-  std::vector<long> ring_numa(int w) { return runner_->ring_numa(w); }
+  std::vector<std::vector<long>> ring_numa(int w) { return runner_->ring_numa(w); }
   std::string transport_path() { return runner_->client().transport_path(); }
   void set_reads_per_worker(int64_t n) { runner_->set_reads_per_worker(n); }
   void reset_stats() { runner_->reset_stats(); }
@@ -850,7 +850,13 @@ PYBIND11_MODULE(_native, m) {
            [](PyGpuSink& s, uintptr_t ptr, size_t cap) { s.sink->set_external_destination(reinterpret_cast<void*>(ptr), cap); })
       .def_property_readonly("device_ptr", [](PyGpuSink& s) { return reinterpret_cast<uintptr_t>(s.sink->object_device_ptr()); })
       .def_property_readonly("capacity", [](PyGpuSink& s) { return s.sink->object_capacity(); })
-      .def("stats", [](PyGpuSink& s) { return gpu_stats_dict(s.sink->stats()); });
+      .def("stats", [](PyGpuSink& s) { return gpu_stats_dict(s.sink->stats()); })
+      .def("ring_numa", [](PyGpuSink& s) {
+        // per ring slot: pages by NUMA node (affinity.h numa_nodes_of)
+        py::list out;
+        for (const auto& [p, n] : s.sink->ring_ranges()) out.append(numa_nodes_of(p, n));
+        return out;
+      });
 
   py::class_<PyClient>(m, "Client")
       .def(py::init<const py::dict&>())

@@ -100,12 +100,19 @@ class PinnedPool {
     if (pin_kind() == PinKind::kThp) {
       const size_t huge = size_t(2) << 20;
       const size_t len = (n + huge - 1) / huge * huge;
-      void* p = nullptr;
-      if (posix_memalign(&p, huge, len) == 0) {
+      // a fresh mapping, never touched: malloc'd memory (even 2 MiB-aligned)
+      // can reuse pages another thread already faulted in on the other
+      // socket, which no memory policy moves (bench numa.ring_slot_nodes
+      // showed slot 0 there in 1 of 3 runs)
+      void* raw = ::mmap(nullptr, len + huge, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+      if (raw != MAP_FAILED) {
+        const uintptr_t a = (reinterpret_cast<uintptr_t>(raw) + huge - 1) & ~(huge - 1);
+        const size_t head = a - reinterpret_cast<uintptr_t>(raw);
+        if (head) ::munmap(raw, head);
+        if (huge - head) ::munmap(reinterpret_cast<void*>(a + len), huge - head);
+        void* p = reinterpret_cast<void*>(a);
         (void)madvise(p, len, MADV_HUGEPAGE);
-        // the calling (pinned, GPU-local) thread's node, strictly: first touch
-        // alone let a 2 MiB page land on the other socket when the local node
-        // had no free huge page (bench numa.ring_pages, profiles/r2_session_c)
+        // the calling (pinned, GPU-local) thread's node, strictly
         (void)bind_range_to_node(p, len, current_numa_node());
         std::memset(p, 0, len);  // fault in now
         if (hipHostRegister(p, len, hipHostRegisterDefault) == hipSuccess) {
@@ -114,7 +121,7 @@ class PinnedPool {
           return p;
         }
         (void)hipGetLastError();
-        std::free(p);
+        ::munmap(p, len);
       }
     }
     void* p = nullptr;
@@ -123,7 +130,7 @@ class PinnedPool {
   }
   static void put(void* p, size_t n) {
     if (!p) return;
-    bool reg = false;
+    size_t reg_len = 0;
     {
       std::lock_guard<std::mutex> lk(mu());
       if (held() + n <= kMaxHeld) {
@@ -133,13 +140,13 @@ class PinnedPool {
       }
       auto it = registered().find(p);
       if (it != registered().end()) {
+        reg_len = it->second;
         registered().erase(it);
-        reg = true;
       }
     }
-    if (reg) {
+    if (reg_len) {
       (void)hipHostUnregister(p);
-      std::free(p);
+      ::munmap(p, reg_len);
       return;
     }
     (void)hipHostFree(p);

@@ -175,7 +175,7 @@ size_t H2Writer::reserve(uint32_t stream, size_t want) {
     if (it == stream_window_.end()) return 0;
     int64_t avail = std::min(conn_window_, it->second);
     if (avail > 0) {
-      size_t n = std::min<size_t>({want, static_cast<size_t>(avail), static_cast<size_t>(peer_max_frame_)});
+      size_t n = std::min<size_t>({want, static_cast<size_t>(avail), static_cast<size_t>(peer_max_frame_.load())});
       conn_window_ -= static_cast<int64_t>(n);
       it->second -= static_cast<int64_t>(n);
       return n;
@@ -186,7 +186,7 @@ size_t H2Writer::reserve(uint32_t stream, size_t want) {
 
 void H2Writer::register_stream(uint32_t stream) {
   std::lock_guard<std::mutex> lk(fmu_);
-  stream_window_[stream] = peer_initial_window_;
+  stream_window_[stream] = peer_initial_window_.load();
 }
 
 void H2Writer::unregister_stream(uint32_t stream) {

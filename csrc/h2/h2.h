@@ -7,6 +7,7 @@
 // ReadObject stream over ONE HTTP/2 connection when the pool size is 1
 // (reference main.go:30,111; SURVEY.md §3.3 "the key contention point").
 #pragma once
+#include <atomic>
 #include <condition_variable>
 #include <cstdint>
 #include <functional>
@@ -112,8 +113,10 @@ class H2Writer {
   std::condition_variable fcv_;
   int64_t conn_window_ = h2::kDefaultWindow;
   std::map<uint32_t, int64_t> stream_window_;
-  uint32_t peer_max_frame_ = h2::kDefaultMaxFrame;
-  uint32_t peer_initial_window_ = h2::kDefaultWindow;
+  // written by the connection's reader thread (SETTINGS), read by writers
+  // that do not hold fmu_ (header blocks are split by the max frame size)
+  std::atomic<uint32_t> peer_max_frame_{h2::kDefaultMaxFrame};
+  std::atomic<uint32_t> peer_initial_window_{h2::kDefaultWindow};
   bool dead_ = false;
 };
 

@@ -73,7 +73,7 @@ int main(int argc, char** argv) {
   for (int i = 0; i < nobj; ++i) store->add_synthetic(bucket, "obj_" + std::to_string(i), (3u << 20) + 4097 * i);
   store->add_synthetic(bucket, "big", 12u << 20);
 
-  for (const char* proto : {"http", "grpc"}) {
+  for (const char* proto : {"http", "http2", "grpc"}) {
     auto cli = make_client(client_cfg(proto, srv.url()));
     // 1) many concurrent readers on one client (gRPC: streams multiplexed on one connection)
     readers(*cli, bucket, nobj, 6, 4 * scale);

@@ -134,3 +134,26 @@ def test_plan_without_gpu_locality_splits_by_local_rank(monkeypatch):
     for i in range(4):
         for j in range(i + 1, 4):
             assert not (seen[i] & seen[j])  # ranks never share a domain
+
+
+def test_numa_placement_queries(native):
+    """numa_nodes_of / pattern_memfd_numa report where pages live (the bench
+    line's `numa` block): touched pages are resident on some node, untouched
+    ones are reported absent (last entry)."""
+    import numpy as np
+
+    a = np.empty(8 << 20, dtype=np.uint8)
+    untouched = native.numa_nodes_of(a.ctypes.data, a.nbytes)
+    a[:] = 1
+    touched = native.numa_nodes_of(a.ctypes.data, a.nbytes)
+    assert len(touched) == 9 and sum(touched) == sum(untouched) > 0
+    assert touched[-1] == 0 and sum(touched[:-1]) == sum(touched)
+    node = native.current_numa_node()
+    assert node >= 0
+    srv = native.Server({"port": 0, "cpus": sorted(os.sched_getaffinity(0))[:2]})
+    srv.start()
+    try:
+        memfd = native.pattern_memfd_numa()
+        assert memfd and sum(memfd[:-1]) > 0 and memfd[-1] == 0
+    finally:
+        srv.stop()

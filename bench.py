@@ -349,11 +349,12 @@ def run_rank(args) -> int:
             cpu["cpu_s_per_gib_by_thread"] = cpuacct.per_gib(
                 cpuacct.delta_by_group(th0, cpuacct.thread_cpu()), float(s1["bytes"]))
         ring_numa = r1.ring_numa(0) if (r1 is not None and use_gpu) else []
-        s1 = s1 or {"bytes": 0, "p50_ms": 0.0, "p99_ms": 0.0, "host_p50_ms": 0.0, "slice_skew_ms": 0.0,
+        s1 = s1 or {"bytes": 0, "p50_ms": 0.0, "p99_ms": 0.0, "host_p50_ms": 0.0, "ttfb_p50_ms": 0.0, "slice_skew_ms": 0.0,
                     "verified": 0, "reads": 0}
         del r1
         st = gdist.reduce_stats(ctx, elapsed=e1, nbytes=float(s1["bytes"]), p50=s1["p50_ms"], p99=s1["p99_ms"],
-                                host_p50=s1["host_p50_ms"], skew=s1.get("slice_skew_ms", 0.0),
+                                host_p50=s1["host_p50_ms"], ttfb_p50=s1.get("ttfb_p50_ms", 0.0),
+                                skew=s1.get("slice_skew_ms", 0.0),
                                 verified=float(s1["verified"]), ok=0.0 if err else 1.0)
         st["error"] = err
         st["cpu"] = cpu
@@ -531,6 +532,9 @@ def run_rank(args) -> int:
                 out["numa"]["ring_slot_nodes"] = [max(range(len(c) - 1), key=lambda i: c[i]) if sum(c[:-1]) else -1
                                                   for c in slots]
             if args.workload == "read":
+                # where a read's time goes: request -> first byte (TTFB), -> last
+                # byte in host memory (host_landed), -> last byte + CRC in HBM (p50)
+                out["ttfb_p50_ms"] = round(head["ttfb_p50_max"], 3)
                 out["host_landed_p50_ms"] = round(head["host_p50_max"], 3)
                 out["verified_reads"] = int(head["verified_sum"])
                 out["rank0_cpu"] = head["cpu"]

@@ -70,6 +70,7 @@ void Runner::reset_stats() {
   acc_ = RunSummary();
   lat_ms_.clear();
   host_ms_.clear();
+  ttfb_ms_.clear();
   pending_.clear();
   t_first_ = t_last_ = 0;
   for (auto& s : sliced_)
@@ -109,6 +110,7 @@ void Runner::record(ReadRecord&& r, double ms, double host_ms) {
     if (r.verified) ++acc_.verified;
     lat_ms_.push_back(ms);
     host_ms_.push_back(host_ms);
+    if (r.ttfb_ns > r.start_ns) ttfb_ms_.push_back((r.ttfb_ns - r.start_ns) / 1e6);
     // metric semantics: integer-truncated milliseconds (reference main.go:146)
     acc_.oc_buckets[oc_bucket_index(std::floor(ms))]++;
   }
@@ -291,6 +293,12 @@ RunSummary Runner::summary() const {
   std::sort(h.begin(), h.end());
   s.host_p50_ms = percentile_floor(h, 50);
   s.host_p99_ms = percentile_floor(h, 99);
+  std::vector<double> tf = ttfb_ms_;
+  std::sort(tf.begin(), tf.end());
+  if (!tf.empty()) {
+    s.ttfb_p50_ms = percentile_floor(tf, 50);
+    s.ttfb_p99_ms = percentile_floor(tf, 99);
+  }
   int nsliced = 0;
   for (const auto& sr : sliced_)
     if (sr) {

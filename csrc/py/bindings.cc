@@ -491,6 +491,8 @@ class PyRunner {
     d["max_ms"] = s.max_ms;
     d["host_p50_ms"] = s.host_p50_ms;
     d["host_p99_ms"] = s.host_p99_ms;
+    d["ttfb_p50_ms"] = s.ttfb_p50_ms;
+    d["ttfb_p99_ms"] = s.ttfb_p99_ms;
     d["slice_skew_ms"] = s.slice_skew_ms;
     py::list b;
     for (int i = 0; i < kOcBuckets; ++i) b.append(s.oc_buckets[i]);

@@ -3,6 +3,7 @@
 // metadata/list, and resumable / single-request uploads.
 #include <atomic>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 
@@ -79,7 +80,7 @@ class H2MediaGet : public H2ClientStream {
       int64_t clen = -1;
       for (const auto& kv : h) {
         if (kv.first == ":status") status_ = std::atoi(kv.second.c_str());
-        if (kv.first == "content-length") clen = std::stoll(kv.second);
+        if (kv.first == "content-length") clen = std::strtoll(kv.second.c_str(), nullptr, 10);
       }
       if (status_ == 200 || status_ == 206) {
         auto get = [&](const char* n) -> const std::string* {

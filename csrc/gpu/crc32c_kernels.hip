@@ -468,6 +468,141 @@ __global__ __launch_bounds__(64 * W) void crc32c_slot_kernel(const CrcBatch b, c
   }
 }
 
+// --- int8-MFMA tile CRC ---------------------------------------------------------
+// 4 KiB tiles as for tile_crc<1>, one wave per tile, but the GF(2) algebra runs
+// on the matrix cores instead of LDS lookups (CrcTables::mfma, crc_types.h):
+// lane l reads 16 bytes of interleaved chunk l & 31 per piece (each load
+// instruction covers 1 KiB contiguous), and for each of the
+// 8 bit planes feeds them shifted right by k as the B operand of one
+// v_mfma_i32_32x32x32_i8 against a constant 0/1 A fragment held in VGPRs
+// (32 fragments, 128 VGPRs, loaded once per wave).  The low bit of each int32
+// accumulator is one bit of one chunk's raw CRC; 16 per-lane shift columns and
+// an XOR over the lanes give the tile's raw CRC.  No LDS at all.  The next
+// tile's loads are issued before the current tile's MFMAs.
+typedef int gcsb_v4i __attribute__((ext_vector_type(4)));
+typedef int gcsb_v16i __attribute__((ext_vector_type(16)));
+
+// The lane's 4 x 16 bytes of tile gt (global_load_dwordx4 through an
+// address-space-1 pointer: flat loads would also count against lgkmcnt).  The
+// head mask (bytes before the segment start, first tile only) is returned in
+// *zb (5 bits per piece: leading bytes to zero, 16 = the whole piece) and
+// applied by the consumer, so a prefetch never waits for its own data.
+__device__ __forceinline__ void load_mfma_tile(const CrcBatch& b, uint32_t s, uint32_t gt, int lane, uint4 (&x)[4],
+                                               uint32_t* zb) {
+  typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+  typedef const u4v __attribute__((address_space(1)))* gptr;
+  const uintptr_t addr = reinterpret_cast<uintptr_t>(b.seg[s].addr);
+  const uint32_t len = b.seg[s].len;
+  const uint32_t t = gt - b.seg[s].tile_base;
+  const uintptr_t a16 = addr & ~uintptr_t(15);
+  const uint64_t full = (addr + len - a16 + 15) / 16 - 1;
+  const intptr_t vend = static_cast<intptr_t>(a16 + 16 * full);
+  const intptr_t tstart = vend - static_cast<intptr_t>(kCrcRoundBytes) * static_cast<intptr_t>(b.seg[s].ntiles - t);
+  uint32_t z = 0;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const intptr_t q = tstart + 16 * (lane & 31) + 1024 * p + 512 * (lane >> 5);
+    const intptr_t lead = static_cast<intptr_t>(addr) - q;  // bytes of this piece before the segment
+    x[p] = make_uint4(0, 0, 0, 0);
+    if (lead < 16) {
+      const u4v v = *reinterpret_cast<gptr>(q);
+      x[p] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+    const uint32_t zp = lead <= 0 ? 0u : (lead >= 16 ? 16u : static_cast<uint32_t>(lead));
+    z |= zp << (5 * p);
+  }
+  *zb = z;
+}
+
+__device__ __forceinline__ uint4 apply_head_mask(uint4 v, uint32_t zp) {
+  if (zp == 0) return v;
+  const int h = static_cast<int>(zp);
+  v.x = mask_low_bytes(v.x, h);
+  v.y = mask_low_bytes(v.y, h - 4);
+  v.z = mask_low_bytes(v.z, h - 8);
+  v.w = mask_low_bytes(v.w, h - 12);
+  return v;
+}
+
+// One tile through the 32 MFMAs; returns its raw CRC (every lane).
+__device__ __forceinline__ uint32_t mfma_tile_crc(const uint4 (&xr)[4], uint32_t zb, const gcsb_v4i* __restrict__ a,
+                                                  const uint32_t (&kc)[16]) {
+  // the A fragments are loop-invariant LDS data: without this the compiler
+  // hoists all 32 reads out of the tile loop into 128 VGPRs again
+  __asm__ __volatile__("" ::: "memory");
+  gcsb_v16i acc = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    // at most one piece's 8 A fragments live at a time
+    if (p) __asm__ __volatile__("" ::: "memory");
+    const uint4 xp = apply_head_mask(xr[p], (zb >> (5 * p)) & 31u);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const gcsb_v4i bv = {static_cast<int>(xp.x >> k), static_cast<int>(xp.y >> k),
+                           static_cast<int>(xp.z >> k), static_cast<int>(xp.w >> k)};
+      acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[(8 * p + k) * 64], bv, acc, 0, 0, 0);
+    }
+  }
+  uint32_t c = 0;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) c ^= kc[r] & (0u - (static_cast<uint32_t>(acc[r]) & 1u));
+  return xor_over_lanes(c, 64);
+}
+
+__global__ __launch_bounds__(256) void crc32c_mfma_tiles_kernel(const CrcBatch b, const CrcTables* __restrict__ tabs,
+                                                                uint32_t* __restrict__ scratch) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+  const uint32_t g0 = blockIdx.x * (blockDim.x >> 6) + wave;
+  const uint32_t T = b.total_tiles;
+  // three tile buffers in rotation, indexed statically (the loop is unrolled
+  // by 3): two tiles' loads stay in flight while one runs through the MFMAs.
+  // Rotating one buffer array by register moves made the compiler wait for
+  // every outstanding load at the top of each tile.
+  uint4 x0[4], x1[4], x2[4];
+  uint32_t s = 0, z0 = 0, z1 = 0, z2 = 0;
+  auto fetch = [&](uint32_t g, uint4 (&x)[4], uint32_t& z) {
+    while (s + 1 < b.nseg && b.seg[s + 1].tile_base <= g) ++s;
+    load_mfma_tile(b, s, g, lane, x, &z);
+  };
+  if (g0 < T) fetch(g0, x0, z0);
+  if (g0 + nw < T) fetch(g0 + nw, x1, z1);
+  // the 32 A fragments (32 KiB) in LDS, one ds_read_b128 per lane per MFMA
+  // (contiguous across lanes: conflict-free); in VGPRs they held occupancy at
+  // 2 waves per SIMD and the memory waits at 36 % of wave cycles
+  __shared__ __attribute__((aligned(16))) gcsb_v4i s_a[32 * 64];
+  {
+    const gcsb_v4i* src = reinterpret_cast<const gcsb_v4i*>(&tabs->mfma.a[0][0][0]);
+    for (int i = threadIdx.x; i < 32 * 64; i += blockDim.x) s_a[i] = src[i];
+  }
+  __syncthreads();
+  const gcsb_v4i* a = s_a + lane;
+  uint32_t kc[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) kc[r] = tabs->mfma.kc[lane][r];
+  uint32_t* tiles = scratch + kCrcScratchHeader;
+  for (uint32_t g = g0; g < T; g += 3 * nw) {
+    if (g + 2 * nw < T) fetch(g + 2 * nw, x2, z2);
+    {
+      const uint32_t c = mfma_tile_crc(x0, z0, a, kc);
+      if (lane == 0) tiles[g] = c;
+    }
+    if (g + nw >= T) break;
+    if (g + 3 * nw < T) fetch(g + 3 * nw, x0, z0);
+    {
+      const uint32_t c = mfma_tile_crc(x1, z1, a, kc);
+      if (lane == 0) tiles[g + nw] = c;
+    }
+    if (g + 2 * nw >= T) break;
+    if (g + 4 * nw < T) fetch(g + 4 * nw, x1, z1);
+    {
+      const uint32_t c = mfma_tile_crc(x2, z2, a, kc);
+      if (lane == 0) tiles[g + 2 * nw] = c;
+    }
+  }
+}
+
 // Separate fold for long segments: one 8-wave workgroup per segment, Horner
 // over 512-tile strides, wave tree, then a 3-level tree across the waves.
 __global__ __launch_bounds__(kThreads) void crc32c_fold_kernel(const CrcBatch b, const CrcTables* __restrict__ tabs,
@@ -666,7 +801,15 @@ void launch_crc32c_batch(const CrcBatch& b, const CrcTables* d_tables, uint32_t*
     hip_check(hipGetLastError(), "crc32c_tiles_kernel(fused)");
     return;
   }
-  if (small)
+  static const bool mfma = [] {
+    const char* e = std::getenv("GCSB_CRC_MFMA");  // int8-MFMA tile CRC for bulk 4 KiB-tile batches
+    return e && *e == '1';
+  }();
+  if (small && mfma) {
+    uint32_t g = (b.total_tiles + 3) / 4;
+    if (g > 2048) g = 2048;
+    hipLaunchKernelGGL(crc32c_mfma_tiles_kernel, dim3(g), dim3(256), 0, stream, b, d_tables, d_scratch);
+  } else if (small)
     hipLaunchKernelGGL((crc32c_tiles_kernel<1, false>), dim3(blocks), dim3(kThreads), 0, stream, b, d_tables,
                        d_scratch, d_results);
   else

@@ -660,6 +660,16 @@ PYBIND11_MODULE(_native, m) {
       },
       py::arg("data"), py::arg("misalign") = 0, py::arg("expected") = 0, py::arg("check") = false,
       py::arg("tile_log2") = kCrcMaxTileLog2, py::arg("fold_waves") = 8);
+  m.def("emulate_mfma_tile_crc", [](const py::bytes& b) {
+    static MfmaCrcTables* t = [] {
+      auto* x = new MfmaCrcTables();
+      build_mfma_crc_tables(x);
+      return x;
+    }();
+    std::string s = b;
+    if (s.size() != 4096) throw std::invalid_argument("a tile is 4096 bytes");
+    return emulate_mfma_tile_crc(reinterpret_cast<const uint8_t*>(s.data()), *t);
+  });
   m.def("object_rotation", &object_rotation);
   m.def("object_bytes", [](const std::string& name, uint64_t off, uint64_t n) {
     std::string out(n, '\0');

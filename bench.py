@@ -331,6 +331,7 @@ def run_rank(args) -> int:
         gdist.barrier(ctx, f"R1 {what} start barrier")
         sync()
         t1 = time.perf_counter()
+        rv0 = n.recv_stats()
         if not err:
             c0, th0 = cpu_snapshot(), cpuacct.thread_cpu()
             t1 = time.perf_counter()
@@ -348,6 +349,13 @@ def run_rank(args) -> int:
             cpu = cpu_delta(c0, cpu_snapshot(), float(s1["bytes"]), e1)
             cpu["cpu_s_per_gib_by_thread"] = cpuacct.per_gib(
                 cpuacct.delta_by_group(th0, cpuacct.thread_cpu()), float(s1["bytes"]))
+            rv1 = n.recv_stats()
+            calls = rv1[0] - rv0[0]
+            if calls:
+                # average bytes per recv() on the client's sockets (every
+                # Conn::read_some of the process: client side only here)
+                cpu["recv_calls"] = calls
+                cpu["recv_avg_kib"] = round((rv1[1] - rv0[1]) / calls / 1024.0, 1)
         ring_numa = r1.ring_numa(0) if (r1 is not None and use_gpu) else []
         s1 = s1 or {"bytes": 0, "p50_ms": 0.0, "p99_ms": 0.0, "host_p50_ms": 0.0, "ttfb_p50_ms": 0.0, "slice_skew_ms": 0.0,
                     "verified": 0, "reads": 0}

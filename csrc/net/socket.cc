@@ -1,5 +1,7 @@
 #include "net/socket.h"
 
+#include <atomic>
+
 #include <arpa/inet.h>
 #include <fcntl.h>
 #include <netdb.h>
@@ -291,6 +293,10 @@ void Conn::shutdown_write() {
   if (fd_ >= 0) ::shutdown(fd_, SHUT_WR);
 }
 
+std::atomic<uint64_t> g_recv_calls{0}, g_recv_bytes{0};
+
+RecvStats recv_stats() { return RecvStats{g_recv_calls.load(), g_recv_bytes.load()}; }
+
 size_t Conn::read_some(void* buf, size_t n) {
   if (fd_ < 0) throw StorageError("read on closed connection", true);
   for (;;) {
@@ -302,6 +308,8 @@ size_t Conn::read_some(void* buf, size_t n) {
     }
     if (r >= 0) {
       bytes_read_ += static_cast<uint64_t>(r);
+      g_recv_calls.fetch_add(1, std::memory_order_relaxed);
+      g_recv_bytes.fetch_add(static_cast<uint64_t>(r), std::memory_order_relaxed);
       return static_cast<size_t>(r);
     }
     if (errno == EINTR) continue;

@@ -49,6 +49,13 @@ struct TlsServer {
   std::string cert_file, key_file;
 };
 
+// Process-wide count of Conn::read_some calls (one recv() each) and their
+// bytes: the average receive size of a read path (diagnostics).
+struct RecvStats {
+  uint64_t calls = 0, bytes = 0;
+};
+RecvStats recv_stats();
+
 class Conn {
  public:
   Conn() = default;

@@ -797,6 +797,10 @@ PYBIND11_MODULE(_native, m) {
   m.def("parse_cpulist", &parse_cpulist);
   m.def("pin_current_thread", &pin_current_thread);
   m.def("set_submitter_cpus", &set_submitter_cpus);
+  m.def("recv_stats", [] {
+    RecvStats r = recv_stats();
+    return py::make_tuple(r.calls, r.bytes);
+  });
   m.def("numa_nodes_of", [](uintptr_t p, size_t n) { return numa_nodes_of(reinterpret_cast<const void*>(p), n); });
   m.def("pattern_memfd_numa", [] { return PatternBuffer::instance().memfd_numa(); });
   m.def("current_numa_node", &current_numa_node);

@@ -157,6 +157,9 @@ def build_parser() -> argparse.ArgumentParser:
                     help="how GPU sinks wait on slot events: block (interrupt) or spin")
     ap.add_argument("--side-steps", type=int, default=-1,
                     help="timed reads/uploads per side block (compare / sliced / write); -1: = --steps, 0: skip all")
+    ap.add_argument("--fanout", default="on", choices=["on", "off"],
+                    help="N > 1 side block: each rank reads 1/N of one shared object, an all-gather over the "
+                         "GPUs gives every GPU the whole object (extension)")
     ap.add_argument("--write-size", default="64MiB", help="config 5 object size")
     ap.add_argument("--write-chunk", default="16MiB", help="resumable upload chunk (HTTP) / message batch")
     ap.add_argument("--json-out", default="")
@@ -415,6 +418,87 @@ def run_rank(args) -> int:
         st["error"] = err
         return st
 
+    def fanout_block(steps: int, warmup: int) -> dict:
+        """[extension, N > 1] read once per node, fan out over xGMI: every rank
+        reads only its 1/N slice of ONE shared 256 MiB object (ranged gRPC
+        read into HBM, per-message CRC32C on the GPU), then an RCCL
+        all-gather over the node's GPUs gives every GPU the whole object,
+        whose CRC32C each GPU then checks.  Against the headline (every GPU
+        pulls the whole object over its own stream) the network/loopback
+        bytes drop N-fold and the rest rides xGMI."""
+        err = ""
+        lat = []
+        crc_ok = 0
+        part_n = size // world
+        name = "fanout/obj_0"
+        full = part = sink = client = None
+        try:
+            if size % world:
+                raise ValueError(f"object size {size} not divisible by {world} ranks")
+            srv.add_synthetic(bucket, "fanout/obj_", "", 0, 1, size)
+            want = srv.object_info(bucket, name)["crc32c"]
+            client = n.Client({"protocol": protocol, "endpoint": srv.url, "retry_initial_s": 0.05,
+                               "cpus": placement["client"], "rcvbuf": parse_size(args.rcvbuf)})
+            full = torch.empty(size, dtype=torch.uint8, device=f"cuda:{gpu}" if use_gpu else "cpu")
+            # this rank's slice lands in place: the all-gather's input is the
+            # slice of its output at rank * part_n (in-place all-gather)
+            part = full[rank * part_n:(rank + 1) * part_n]
+            if use_gpu:
+                sink = n.GpuSink({"device": gpu, "ring_slot_bytes": parse_size(args.slot_bytes),
+                                  "ring_slots": args.slots})
+                # capacity to the end of the buffer: a ranged read learns the
+                # whole object's size and the sink checks it fits
+                sink.set_external_destination(part.data_ptr(), size - rank * part_n)
+        except Exception as e:  # noqa: BLE001 - reported in the block, collectives still run
+            err = f"{type(e).__name__}: {e}"
+
+        for i in range(warmup + steps):
+            # every rank makes the same collective calls whatever happened
+            # locally: a failed slice read is reported after the all-gather
+            flags = gdist.reduce_stats(ctx, ok=0.0 if err else 1.0)
+            if flags["ok_min"] < 1.0:
+                err = err or "a peer rank failed"
+                break
+            gdist.barrier(ctx, "fan-out start")
+            t0 = time.perf_counter()
+            local = ""
+            try:
+                if use_gpu:
+                    r = client.read_gpu(bucket, name, sink, rank * part_n, part_n)
+                    if r["bytes"] != part_n or r["crc_mismatch"]:
+                        local = f"slice read failed: {r}"
+                else:  # CPU rehearsal: the slice through host memory
+                    b = client.read_bytes(bucket, name, rank * part_n, part_n)
+                    part.copy_(torch.frombuffer(bytearray(b), dtype=torch.uint8))
+            except Exception as e:  # noqa: BLE001
+                local = f"{type(e).__name__}: {e}"
+            try:
+                gdist.all_gather_bytes(ctx, full, part, "fan-out all-gather")
+                sync()
+            except Exception as e:  # noqa: BLE001 - the process group is gone: no more collectives
+                err = f"all-gather: {type(e).__name__}: {e}"
+                return {"ok_min": 0.0, "p50_max": 0.0, "p99_max": 0.0, "crc_ok_sum": 0.0, "nbytes_sum": 0.0,
+                        "elapsed_max": 0.0, "error": err}
+            gdist.barrier(ctx, "fan-out stop")
+            if local:
+                err = local
+            elif i >= warmup:
+                lat.append((time.perf_counter() - t0) * 1e3)
+        if not err:
+            got = n.gpu_crc32c(gpu, full.data_ptr(), size) if use_gpu else n.crc32c(full.numpy().tobytes())
+            crc_ok = int(got == want)
+            if not crc_ok:
+                err = "CRC32C of the gathered object does not match"
+        s_ = sorted(lat)
+        p50 = s_[len(s_) * 50 // 100] if s_ else 0.0
+        p99 = s_[min(len(s_) - 1, len(s_) * 99 // 100)] if s_ else 0.0
+        # every GPU ends each step with the whole object: size bytes per rank per step
+        st = gdist.reduce_stats(ctx, elapsed=sum(lat) / 1e3, nbytes=float(size * len(lat)), p50=p50, p99=p99,
+                                ok=0.0 if err else 1.0, crc_ok=float(crc_ok))
+        st["error"] = err
+        del part, full, sink
+        return st
+
     def mib_s(st: dict) -> float:
         return st["nbytes_sum"] / max(st["elapsed_max"], 1e-12) / (1 << 20)
 
@@ -463,6 +547,12 @@ def run_rank(args) -> int:
             blocks["write"] = ("write", write_block(side_steps, 1),
                                {"protocol": protocol, "object_bytes": parse_size(args.write_size),
                                 "config": "BASELINE config 5"})
+        if world > 1 and args.fanout == "on":
+            blocks["fanout"] = ("fanout", fanout_block(side_steps, 1),
+                                {"object_bytes": size, "slice_bytes": size // world,
+                                 "collective": f"{ctx.backend} all_gather_into_tensor" if ctx.device.type == "cuda"
+                                 else f"{ctx.backend} all_gather via host",
+                                 "note": "extension: read once per node, fan out over xGMI"})
     elif side_steps > 0 and other and other in hbm.available_protocols():
         pass  # write headline: no read side blocks
     srv.stop()
@@ -551,6 +641,10 @@ def run_rank(args) -> int:
                     out["cpus_needed_per_gpu"] = round(head["cpu"]["process_cpu_s_per_gib"] * gib_s, 2)
             for key, (_, st, extra) in blocks.items():
                 b = block_json(st, **extra)
+                if key == "fanout":
+                    # mib_s: whole objects landed in every GPU's HBM, job-wide
+                    b["per_gpu_mib_s"] = round(b["mib_s"] / max(1, world), 2)
+                    b["crc_verified_ranks"] = int(st["crc_ok_sum"])
                 if key == "sliced":
                     b["host_landed_p50_ms"] = round(st["host_p50_max"], 3)
                     b["slice_skew_ms"] = round(st["skew_max"], 3)

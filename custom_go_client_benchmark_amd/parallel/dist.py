@@ -32,6 +32,7 @@ class DistContext:
     backend: str = "none"
     initialized_here: bool = False
     pg: bool = False            # a process group exists (collectives run even at world 1)
+    fallback: bool = False      # RCCL failed to initialise; the control plane runs on gloo
 
 
 def env_rank() -> tuple[int, int, int]:
@@ -96,8 +97,26 @@ def init(local_rank: int | None = None, world: int | None = None, rank: int | No
             kw = {}
             if backend == "nccl" and use_cuda:
                 kw["device_id"] = ctx.device
-            dist.init_process_group(backend=backend, rank=rank, world_size=world,
-                                    timeout=datetime.timedelta(seconds=timeout_s), **kw)
+            explicit = os.environ.get("GCSB_DIST_BACKEND")
+            try:
+                dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                        timeout=datetime.timedelta(seconds=timeout_s), **kw)
+            except Exception as e:  # noqa: BLE001
+                if backend != "nccl" or explicit:
+                    raise
+                # RCCL refused to initialise (same on every rank, e.g. no
+                # peer-memory IPC on the host): keep the run alive on a gloo
+                # control plane (CPU tensors) at the next port, and say so
+                sys.stderr.write(f"[rank {rank}] RCCL init failed ({type(e).__name__}: {e}); "
+                                 f"falling back to a gloo control plane\n")
+                if dist.is_initialized():
+                    dist.destroy_process_group()
+                os.environ["MASTER_PORT"] = str(int(os.environ["MASTER_PORT"]) + 1)
+                backend = "gloo"
+                ctx.device = torch.device("cpu")
+                ctx.fallback = True
+                dist.init_process_group(backend="gloo", rank=rank, world_size=world,
+                                        timeout=datetime.timedelta(seconds=timeout_s))
             ctx.initialized_here = True
         ctx.backend = backend
         ctx.pg = True
@@ -156,6 +175,43 @@ def barrier(ctx: DistContext, what: str = "barrier", timeout_s: float | None = N
         done.set()
     if int(t.item()) != ctx.world:
         raise RuntimeError(f"barrier mismatch: {int(t.item())} != {ctx.world}")
+
+
+class _Guard:
+    """Watchdog around one collective (see _watchdog)."""
+
+    def __init__(self, ctx: DistContext, what: str, timeout_s: float):
+        self.done = threading.Event()
+        self.t = threading.Thread(target=_watchdog, args=(ctx, what, timeout_s, self.done),
+                                  name="gcsb-collective-watchdog", daemon=True)
+
+    def __enter__(self):
+        self.t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.done.set()
+        return False
+
+
+def all_gather_bytes(ctx: DistContext, out, part, what: str = "all-gather", timeout_s: float = 120.0) -> None:
+    """Every rank's `part` (uint8, equal sizes) into `out` in rank order.
+    RCCL: all_gather_into_tensor on the GPUs (peer-to-peer over xGMI within a
+    node).  gloo: the parts go through host memory."""
+    if not ctx.pg or ctx.world == 1:
+        out.copy_(part)
+        return
+    import torch
+    import torch.distributed as dist
+
+    with _Guard(ctx, what, timeout_s):
+        if ctx.device.type == "cuda":
+            dist.all_gather_into_tensor(out, part)
+        else:
+            host = part.cpu()
+            parts = [torch.empty_like(host) for _ in range(ctx.world)]
+            dist.all_gather(parts, host)
+            out.copy_(torch.cat(parts).to(out.device))
 
 
 def reduce_stats(ctx: DistContext, **vals: float) -> dict:

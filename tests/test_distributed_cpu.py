@@ -73,6 +73,22 @@ def test_bench_self_launches_ranks():
     assert "compare" not in out and "sliced" not in out
 
 
+def test_bench_fanout_block_two_ranks():
+    """N > 1 side block: each rank reads half of one shared object, the
+    all-gather (gloo here, RCCL on GPUs) gives every rank the whole object and
+    every rank checks its CRC32C."""
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--sink", "discard", "--steps", "1",
+                        "--warmup", "0", "--object-size", "2MiB", "--side-steps", "2"],
+                       capture_output=True, text=True, timeout=240, cwd=ROOT, env=_bench_env())
+    assert r.returncode == 0, r.stderr[-3000:]
+    f = _bench_line(r.stdout)["fanout"]
+    assert f["ok"] and f["crc_verified_ranks"] == 2 and f["slice_bytes"] == 1 << 20, f
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--sink", "discard", "--steps", "1",
+                        "--warmup", "0", "--object-size", "2MiB", "--side-steps", "1", "--fanout", "off"],
+                       capture_output=True, text=True, timeout=240, cwd=ROOT, env=_bench_env())
+    assert r.returncode == 0 and "fanout" not in _bench_line(r.stdout)
+
+
 def test_bench_refuses_gpus_world_mismatch():
     r = torchrun(["bench.py", "--gpus", "3", "--sink", "discard", "--steps", "1", "--warmup", "0",
                   "--object-size", "64KiB", "--side-steps", "0"])

@@ -100,6 +100,16 @@ def test_bench_shared_gpu_rehearsal_counts_distinct_devices(gpu_available):
     assert out["n_gpus"] == 1 and out["ranks"] == 2 and out["devices"] == [0]
 
 
+def test_bench_fanout_block_shared_gpu(gpu_available):
+    """Fan-out block on the GPU path (ranged slice reads into HBM in place,
+    GPU CRC of the gathered object); the all-gather goes through host memory
+    on this 1-GPU box's gloo control plane."""
+    out = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0", "--object-size", "32MiB", "--side-steps", "2",
+                  "--sliced-streams", "0"], {"GCSB_DIST_BACKEND": "gloo"})
+    f = out["fanout"]
+    assert f["ok"] and f["crc_verified_ranks"] == 2, f
+
+
 def test_bench_refuses_more_ranks_than_gpus(gpu_available):
     import torch
 

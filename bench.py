@@ -601,6 +601,7 @@ def run_rank(args) -> int:
                     "sysctl": tcp_sysctls(),
                 },
                 "ranks": world,
+                "control_plane": ctx.backend + (" (RCCL init failed: fallback)" if ctx.fallback else ""),
                 "devices": distinct if use_gpu else "none (cpu rehearsal)",
                 "per_gpu_mib_s": round(value / max(1, n_gpus), 2),
                 "p50_ms": round(head["p50_max"], 3),

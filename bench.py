@@ -523,6 +523,12 @@ def run_rank(args) -> int:
         head = write_block(args.steps, args.warmup)
         headline_model = f"{protocol} resumable upload {args.write_size} object from HBM (D2H -> pinned -> upload)"
 
+    # R4: which HIP device each rank used -> distinct GPUs in the job (before
+    # the side blocks: the fan-out block may leave the communicator aborted)
+    devs = gdist.gather_floats(ctx, [float(ctx.gpu if use_gpu else -1)])
+    distinct = sorted({int(d[0]) for d in devs if d[0] >= 0})
+    n_gpus = len(distinct) if use_gpu else world
+
     # ---- side blocks (after the timed region) ----------------------------
     other = {"grpc": "http", "http": "grpc"}.get(protocol)
     blocks = {}
@@ -557,10 +563,6 @@ def run_rank(args) -> int:
         pass  # write headline: no read side blocks
     srv.stop()
 
-    # R4: which HIP device each rank used -> distinct GPUs in the job
-    devs = gdist.gather_floats(ctx, [float(ctx.gpu if use_gpu else -1)])
-    distinct = sorted({int(d[0]) for d in devs if d[0] >= 0})
-    n_gpus = len(distinct) if use_gpu else world
 
     rc = 0
     if rank == 0:

@@ -127,7 +127,7 @@ class BarrierTimeout(RuntimeError):
     """A peer rank did not reach a barrier in time (dead or stuck)."""
 
 
-def _watchdog(ctx: DistContext, what: str, timeout_s: float, done: threading.Event) -> None:
+def _watchdog(ctx: DistContext, what: str, timeout_s: float, done: threading.Event, hard_exit: bool = True) -> None:
     """SURVEY.md §5 failure detection: a rank whose peer died would otherwise
     sit in the collective until the process-group timeout (10 min).  After
     `timeout_s` the watchdog names the barrier, aborts the communicator
@@ -145,7 +145,7 @@ def _watchdog(ctx: DistContext, what: str, timeout_s: float, done: threading.Eve
         c10d._abort_process_group()
     except Exception as e:  # gloo has no abort; fall through to the hard exit
         sys.stderr.write(f"[rank {ctx.rank}] communicator abort unavailable: {e}\n")
-    if not done.wait(5.0):
+    if hard_exit and not done.wait(5.0):
         sys.stderr.flush()
         os._exit(3)
 
@@ -182,7 +182,9 @@ class _Guard:
 
     def __init__(self, ctx: DistContext, what: str, timeout_s: float):
         self.done = threading.Event()
-        self.t = threading.Thread(target=_watchdog, args=(ctx, what, timeout_s, self.done),
+        # abort the communicator but keep the process: the caller reports the
+        # failed block and prints the rest of its results
+        self.t = threading.Thread(target=_watchdog, args=(ctx, what, timeout_s, self.done, False),
                                   name="gcsb-collective-watchdog", daemon=True)
 
     def __enter__(self):
@@ -273,4 +275,7 @@ def shutdown(ctx: DistContext) -> None:
         import torch.distributed as dist
 
         if dist.is_initialized():
-            dist.destroy_process_group()
+            try:
+                dist.destroy_process_group()
+            except Exception as e:  # noqa: BLE001 - an aborted communicator
+                sys.stderr.write(f"[rank {ctx.rank}] process group teardown: {e}\n")

@@ -372,6 +372,17 @@ def run_rank(args) -> int:
         st["ring_numa"] = ring_numa
         return st
 
+    def share_endpoint():
+        """An endpoint of its own on the rank's share of L3 domains: the
+        sliced block's 8 send threads, and uploads, whose receive + CRC32C
+        on the endpoint is as heavy as the client's send (the headline's
+        one-core pair endpoint halved the upload rate)."""
+        sh = affinity.plan(gpu, "share", slot) if use_gpu else {"client": [], "server": []}
+        e = n.Server({"port": 0, "md5": False, "cpus": sh["server"], "retain_uploads": False})
+        e.start()
+        e.add_synthetic(bucket, prefix, "", first, args.workers, size)
+        return e, sh
+
     def write_block(steps: int, warmup: int) -> dict:
         """Config 5: each rank uploads a 64 MiB object from HBM `steps` times
         (HBM -> pinned ring D2H on a side stream -> resumable upload; the
@@ -381,9 +392,18 @@ def run_rank(args) -> int:
         wsize = parse_size(args.write_size)
         chunk = parse_size(args.write_chunk)
         client = buf = None
+        ep = None
+        saved_aff = os.sched_getaffinity(0)
         try:
-            # uploads: client threads unpinned (measured fastest, profiles/r1_session4)
-            client = n.Client({"protocol": protocol, "endpoint": srv.url, "retry_initial_s": 0.05})
+            ep, sh = share_endpoint()
+            # the upload runs on this (Python main) thread: keep it, its
+            # connection reader and the pinned staging ring it allocates on
+            # the GPU's NUMA node (the rank's share of L3 domains); unpinned
+            # it could stage from the other socket (p50 6.9 vs 14.3 ms
+            # between otherwise identical runs)
+            if sh["client"]:
+                os.sched_setaffinity(0, sh["client"])
+            client = n.Client({"protocol": protocol, "endpoint": ep.url, "retry_initial_s": 0.05})
             buf = torch.empty(wsize, dtype=torch.uint8, device=f"cuda:{gpu}")
             n.gpu_fill_pattern(gpu, buf.data_ptr(), wsize, f"upload/rank{rank}", 0)
             for i in range(warmup):
@@ -414,6 +434,10 @@ def run_rank(args) -> int:
         s = sorted(lat)
         p50 = s[len(s) * 50 // 100] if s else 0.0
         p99 = s[min(len(s) - 1, len(s) * 99 // 100)] if s else 0.0
+        if ep is not None:
+            del client
+            ep.stop()
+        os.sched_setaffinity(0, saved_aff)
         st = gdist.reduce_stats(ctx, elapsed=e1, nbytes=float(nbytes), p50=p50, p99=p99, ok=0.0 if err else 1.0)
         st["error"] = err
         return st
@@ -538,10 +562,7 @@ def run_rank(args) -> int:
                                  {"protocol": other})
         if args.sliced_streams > 1 and args.slices == 1:
             # 8 receive + 8 send threads: a share-placed endpoint of its own
-            sh = affinity.plan(gpu, "share", slot) if use_gpu else {"client": [], "server": []}
-            srv_sl = n.Server({"port": 0, "md5": False, "cpus": sh["server"], "retain_uploads": False})
-            srv_sl.start()
-            srv_sl.add_synthetic(bucket, prefix, "", first, args.workers, size)
+            srv_sl, sh = share_endpoint()
             sliced_cfg.update({"endpoint": srv_sl.url, "cpus": sh["client"]})
             st_sl = read_block(sliced_cfg, side_steps, 1, "sliced")
             srv_sl.stop()

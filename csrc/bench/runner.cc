@@ -71,6 +71,8 @@ void Runner::reset_stats() {
   lat_ms_.clear();
   host_ms_.clear();
   ttfb_ms_.clear();
+  first_ms_.clear();
+  steady_ms_.clear();
   pending_.clear();
   t_first_ = t_last_ = 0;
   for (auto& s : sliced_)
@@ -109,6 +111,7 @@ void Runner::record(ReadRecord&& r, double ms, double host_ms) {
     acc_.bytes += r.bytes;
     if (r.verified) ++acc_.verified;
     lat_ms_.push_back(ms);
+    (r.seq == 0 ? first_ms_ : steady_ms_).push_back(ms);
     host_ms_.push_back(host_ms);
     if (r.ttfb_ns > r.start_ns) ttfb_ms_.push_back((r.ttfb_ns - r.start_ns) / 1e6);
     // metric semantics: integer-truncated milliseconds (reference main.go:146)
@@ -298,6 +301,17 @@ RunSummary Runner::summary() const {
   if (!tf.empty()) {
     s.ttfb_p50_ms = percentile_floor(tf, 50);
     s.ttfb_p99_ms = percentile_floor(tf, 99);
+  }
+  std::vector<double> fr = first_ms_, st = steady_ms_;
+  std::sort(fr.begin(), fr.end());
+  std::sort(st.begin(), st.end());
+  if (!fr.empty()) {
+    s.first_read_p50_ms = percentile_floor(fr, 50);
+    s.first_read_max_ms = fr.back();
+  }
+  if (!st.empty()) {
+    s.steady_p50_ms = percentile_floor(st, 50);
+    s.steady_p99_ms = percentile_floor(st, 99);
   }
   int nsliced = 0;
   for (const auto& sr : sliced_)

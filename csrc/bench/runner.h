@@ -85,6 +85,10 @@ struct RunSummary {
   double avg_ms = 0, p20_ms = 0, p50_ms = 0, p90_ms = 0, p99_ms = 0, min_ms = 0, max_ms = 0;
   double host_p50_ms = 0, host_p99_ms = 0;  // host-landed latency (reference-equivalent stop)
   double ttfb_p50_ms = 0, ttfb_p99_ms = 0;  // request -> first body byte (0 if not recorded)
+  // Each worker's first read dials its connection (the reference's lazy
+  // http.Client / grpc dial does the same); with few reads per worker those
+  // reads are the p99.  Split out so the steady-state tail is visible.
+  double first_read_p50_ms = 0, first_read_max_ms = 0, steady_p50_ms = 0, steady_p99_ms = 0;
   double slice_skew_ms = 0;  // sliced reads: mean spread of the slices' host-landed times
   uint64_t oc_buckets[kOcBuckets] = {0};
   std::string first_error;
@@ -128,7 +132,7 @@ class Runner {
   volatile bool stop_flag_ = false;
   mutable std::mutex mu_;
   std::vector<ReadRecord> pending_;
-  std::vector<double> lat_ms_, host_ms_, ttfb_ms_;
+  std::vector<double> lat_ms_, host_ms_, ttfb_ms_, first_ms_, steady_ms_;
   RunSummary acc_;
   int64_t t_first_ = 0, t_last_ = 0;
   std::mutex out_mu_;

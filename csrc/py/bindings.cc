@@ -493,6 +493,10 @@ class PyRunner {
     d["host_p99_ms"] = s.host_p99_ms;
     d["ttfb_p50_ms"] = s.ttfb_p50_ms;
     d["ttfb_p99_ms"] = s.ttfb_p99_ms;
+    d["first_read_p50_ms"] = s.first_read_p50_ms;
+    d["first_read_max_ms"] = s.first_read_max_ms;
+    d["steady_p50_ms"] = s.steady_p50_ms;
+    d["steady_p99_ms"] = s.steady_p99_ms;
     d["slice_skew_ms"] = s.slice_skew_ms;
     py::list b;
     for (int i = 0; i < kOcBuckets; ++i) b.append(s.oc_buckets[i]);

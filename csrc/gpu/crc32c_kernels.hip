@@ -371,7 +371,8 @@ __global__ __launch_bounds__(64 * W) void crc32c_slot_kernel(const CrcBatch b, c
   constexpr int kTabWords = kNib ? 32 * 16 * 32 : kSliceWords;
   __shared__ __attribute__((aligned(16))) uint32_t s_sl[kTabWords];
   __shared__ uint32_t s_last;
-  if (b.probe == 2) return;
+  const uint32_t probe = b.probe & 0xffu;  // bit 8: A/B switch, per-tile stores + counters only
+  if (probe == 2) return;
   const int lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // the first tile's data and matrix go out before the tables: their memory
@@ -404,8 +405,19 @@ __global__ __launch_bounds__(64 * W) void crc32c_slot_kernel(const CrcBatch b, c
   else
     stage(s_sl, &tabs->slice16[0][0], kTabWords);
   __syncthreads();
-  if (b.probe == 1) return;
+  if (probe == 1) return;
   uint32_t* tiles = scratch + kCrcScratchHeader;
+  // One segment (every slot that does not straddle two objects) and at most
+  // 32 workgroups per counter group: no per-tile stores.  Each workgroup's
+  // contribution and its arrival bit go into one 64-bit atomic XOR per level
+  // (low word: XOR of contributions, high word: arrival mask); the returned
+  // old value tells the last arriver the whole XOR.  Two device-scope round
+  // trips instead of store + wait + counter + counter + loads.
+  const uint32_t groups = gridDim.x < kCrcCounterGroups ? gridDim.x : kCrcCounterGroups;
+  const bool xor_path = b.nseg == 1 && gridDim.x <= 32u * groups && !(b.probe & 0x100u);
+  int tail_r = 0;
+  const uint32_t tail_b = xor_path && wave == 0 ? tail_byte(b.seg[0], lane, &tail_r) : 0u;
+  uint32_t wsum = 0;
   for (uint32_t gt = gt0; gt < b.total_tiles; gt += gridDim.x * W) {
     if (gt != gt0) {
       while (s + 1 < b.nseg && b.seg[s + 1].tile_base <= gt) ++s;
@@ -420,9 +432,54 @@ __global__ __launch_bounds__(64 * W) void crc32c_slot_kernel(const CrcBatch b, c
     c = xor_over_lanes(c, 64);  // the tile's raw CRC, in every lane
     uint32_t x = lane < 32 ? (kt & (0u - ((c >> lane) & 1u))) : 0u;
     x = xor_over_lanes(x, 32);
-    if (lane == 0) __hip_atomic_store(tiles + gt, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (xor_path)
+      wsum ^= x;
+    else if (lane == 0)
+      __hip_atomic_store(tiles + gt, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (b.probe == 4) return;
+  if (probe == 4) return;
+  if (xor_path) {
+    __shared__ uint32_t s_part[W];
+    __shared__ uint32_t s_raw;
+    if (lane == 0) s_part[wave] = wsum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t mine = 0;
+#pragma unroll
+      for (int i = 0; i < W; ++i) mine ^= s_part[i];
+      const uint32_t j = blockIdx.x % groups;
+      const uint32_t m = blockIdx.x / groups;
+      const uint32_t members = gridDim.x / groups + (j < gridDim.x % groups ? 1u : 0u);
+      const uint32_t full = members >= 32 ? ~0u : (1u << members) - 1u;
+      // 8-byte aligned words inside the header's group / root slots
+      auto word = [](uint32_t* p) {
+        return reinterpret_cast<uint64_t*>((reinterpret_cast<uintptr_t>(p) + 8 + 7) & ~uintptr_t(7));
+      };
+      uint64_t* gw = word(scratch + kCrcCounterStride * (1 + j));
+      uint32_t last = 0;
+      const uint64_t og = __hip_atomic_fetch_xor(gw, (uint64_t{1} << (32 + m)) | mine, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+      if ((static_cast<uint32_t>(og >> 32) ^ (1u << m)) == full) {
+        __hip_atomic_store(gw, uint64_t{0}, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t gx = static_cast<uint32_t>(og) ^ mine;
+        const uint32_t gfull = groups >= 32 ? ~0u : (1u << groups) - 1u;
+        uint64_t* rw = word(scratch);
+        const uint64_t orr = __hip_atomic_fetch_xor(rw, (uint64_t{1} << (32 + j)) | gx, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+        if ((static_cast<uint32_t>(orr >> 32) ^ (1u << j)) == gfull) {
+          __hip_atomic_store(rw, uint64_t{0}, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          s_raw = static_cast<uint32_t>(orr) ^ gx;
+          last = 1;
+        }
+      }
+      s_last = last;
+    }
+    __syncthreads();
+    if (!s_last || probe == 3 || wave != 0) return;
+    const uint32_t raw = fold_tail<kNib>(tail_b, tail_r, s_raw, s_sl, lane);
+    if (lane == 0) out[0] = seg_result(b.seg[0], raw);
+    return;
+  }
   // this workgroup's stores complete before it counts itself done
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
@@ -444,7 +501,7 @@ __global__ __launch_bounds__(64 * W) void crc32c_slot_kernel(const CrcBatch b, c
     s_last = last;
   }
   __syncthreads();
-  if (!s_last || b.probe == 3) return;
+  if (!s_last || probe == 3) return;
   for (uint32_t g = wave; g < b.nseg; g += W) {
     const CrcSeg& sg = b.seg[g];
     const uint32_t* tp = tiles + sg.tile_base;
@@ -765,13 +822,23 @@ void launch_crc32c_batch(const CrcBatch& b, const CrcTables* d_tables, uint32_t*
     if (forced_w == 1 || forced_w == 2 || forced_w == 4 || forced_w == 8) w = forced_w;
     uint32_t g = (t + w - 1) / w;
     if (g > 2048) g = 2048;
+    static const bool no_xor = [] {
+      const char* e = std::getenv("GCSB_CRC_XOR");  // A/B: 0 = per-tile stores + done counters for every batch
+      return e && *e == '0';
+    }();
+    CrcBatch bx;
+    if (no_xor) {
+      bx = b;
+      bx.probe |= 0x100u;
+    }
     if (g == 0) g = 1;
     static const bool nib = [] {
       const char* e = std::getenv("GCSB_CRC_NIB");  // A/B: 0 = byte tables (bank conflicts), 1 = nibble tables
       return e && *e == '1';
     }();
 #define GCSB_SLOT(WV, NB) \
-  hipLaunchKernelGGL((crc32c_slot_kernel<WV, NB>), dim3(g), dim3(64 * WV), 0, stream, b, d_tables, d_scratch, d_results)
+  hipLaunchKernelGGL((crc32c_slot_kernel<WV, NB>), dim3(g), dim3(64 * WV), 0, stream, no_xor ? bx : b, d_tables, \
+                     d_scratch, d_results)
     if (nib) {
       switch (w) {
         case 1: GCSB_SLOT(1, true); break;

@@ -5,6 +5,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstdio>
 #include <random>
@@ -13,6 +14,20 @@
 #include "core/util.h"
 
 namespace gcsb {
+
+namespace {
+// gRPC multiplexes every worker's stream on the pool's connections: the host
+// CRC of a discard sink runs on the worker, not the connection's reader
+// (DiscardSink deferred mode).  GCSB_DEFER_CRC=0 keeps it inline (A/B).
+bool defer_host_crc(const ClientConfig& c) {
+  static const bool on = [] {
+    const char* e = std::getenv("GCSB_DEFER_CRC");
+    return !(e && *e == '0');
+  }();
+  return on && c.protocol == "grpc";
+}
+}  // namespace
+
 
 const double kOcLatencyBoundsMs[34] = {1,   2,   3,   4,   5,   6,    8,    10,   13,    16,    20,    25,
                                        30,  40,  50,  65,  80,  100,  130,  160,  200,   250,   300,   400,
@@ -151,7 +166,7 @@ void Runner::worker_main(int w) {
               g.landing = Landing::kObject;
               return std::make_unique<GpuSink>(g);
             }
-            return std::make_unique<DiscardSink>(rc.client.read_chunk, rc.host_crc);
+            return std::make_unique<DiscardSink>(rc.client.read_chunk, rc.host_crc, defer_host_crc(rc.client));
           },
           [land](uint64_t total) {
             if (land) land->ensure(total);
@@ -168,7 +183,8 @@ void Runner::worker_main(int w) {
         gpu_sinks_[w] = g.get();
         sinks_[w] = std::move(g);
       } else {
-        sinks_[w] = std::make_unique<DiscardSink>(cfg_.client.read_chunk, cfg_.host_crc);
+        // multiplexed gRPC: host CRC on the worker thread, not the connection's reader
+        sinks_[w] = std::make_unique<DiscardSink>(cfg_.client.read_chunk, cfg_.host_crc, defer_host_crc(cfg_.client));
       }
     }
   } catch (const std::exception& e) {

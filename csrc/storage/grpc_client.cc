@@ -186,10 +186,29 @@ class GrpcCall : public H2ClientStream {
     if (handler_error_.empty()) handler_error_ = msg;
   }
 
+  // The reader thread has queued work for the waiting worker (a deferred
+  // sink's message end): wake it.
+  void poke() {
+    std::lock_guard<std::mutex> lk(mu_);
+    poked_ = true;
+    cv_.notify_all();
+  }
+
   // Waits for completion; throws a StorageError for any non-OK outcome.
-  void wait_ok() {
+  // sink: drained (deferred work run on this thread) at every poke and once
+  // after completion.
+  void wait_ok(Sink* sink = nullptr) {
     std::unique_lock<std::mutex> lk(mu_);
-    cv_.wait(lk, [&] { return done_; });
+    for (;;) {
+      cv_.wait(lk, [&] { return done_ || (sink && poked_); });
+      poked_ = false;
+      if (!sink) break;
+      const bool d = done_;
+      lk.unlock();
+      sink->drain();
+      lk.lock();
+      if (d) break;
+    }
     if (!handler_error_.empty()) throw StorageError(handler_error_, handler_retryable_);
     if (!transport_error_.empty() && grpc_status_ != kOk) throw StorageError(transport_error_, true);
     if (grpc_status_ != kOk) {
@@ -225,7 +244,7 @@ class GrpcCall : public H2ClientStream {
   bool handler_retryable_ = false;
   std::mutex mu_;
   std::condition_variable cv_;
-  bool done_ = false, got_headers_ = false;
+  bool done_ = false, got_headers_ = false, poked_ = false;
   int grpc_status_ = -1;
   std::string grpc_message_, transport_error_, handler_error_;
 };
@@ -307,6 +326,7 @@ class ReadObjectHandler : public MessageHandler {
       } catch (const std::exception& e) {
         fail_sink(e.what());
       }
+      if (*call_ && sink_.deferred()) (*call_)->poke();
     }
   }
 
@@ -599,7 +619,7 @@ class GrpcStorageClient : public StorageClient {
     std::string f = frame(v2::encode_read_request(q));
     try {
       c->start_stream_with_body(call, headers("ReadObject", q.bucket), f);
-      call->wait_ok();
+      call->wait_ok(sink.deferred() ? &sink : nullptr);
     } catch (...) {
       c->end_stream(*call, true);
       throw;

@@ -1,5 +1,6 @@
 #include "storage/sink.h"
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 
@@ -8,14 +9,24 @@
 
 namespace gcsb {
 
-DiscardSink::DiscardSink(size_t chunk_bytes, bool host_crc)
-    : buf_(static_cast<uint8_t*>(std::aligned_alloc(4096, (chunk_bytes + 4095) / 4096 * 4096))),
-      cap_(chunk_bytes),
-      host_crc_(host_crc) {}
+DiscardSink::DiscardSink(size_t chunk_bytes, bool host_crc, bool deferred)
+    : cap_(chunk_bytes), host_crc_(host_crc), deferred_(deferred && host_crc) {
+  ring_ = deferred_ ? 4 * ((cap_ + 4095) / 4096 * 4096) : (cap_ + 4095) / 4096 * 4096;
+  buf_ = static_cast<uint8_t*>(std::aligned_alloc(4096, ring_));
+}
 
 DiscardSink::~DiscardSink() { std::free(buf_); }
 
+void DiscardSink::reset_ring() {
+  std::lock_guard<std::mutex> c(cmu_);
+  std::lock_guard<std::mutex> q(qmu_);
+  ops_.clear();
+  written_ = 0;
+  consumed_.store(0, std::memory_order_relaxed);
+}
+
 void DiscardSink::begin(const ObjectInfo& info) {
+  if (deferred_) reset_ring();
   info_ = info;
   bytes_ = 0;
   obj_crc_ = 0;
@@ -39,22 +50,49 @@ void DiscardSink::update_info(const ObjectInfo& info) {
 }
 
 Window DiscardSink::acquire(size_t want) {
-  (void)want;
-  return Window{buf_, cap_};
+  if (!deferred_) {
+    (void)want;
+    return Window{buf_, cap_};
+  }
+  for (;;) {
+    const uint64_t used = written_ - consumed_.load(std::memory_order_acquire);
+    if (used < ring_) {
+      const size_t p = static_cast<size_t>(written_ % ring_);
+      return Window{buf_ + p, std::min<size_t>(ring_ - p, ring_ - used)};
+    }
+    drain();  // ring full: the reader replays the oldest ops itself
+  }
+}
+
+void DiscardSink::push(const Op& op) {
+  std::lock_guard<std::mutex> q(qmu_);
+  ops_.push_back(op);
 }
 
 void DiscardSink::commit(size_t n) {
+  if (deferred_) {
+    Op op{Op::kData};
+    op.off = written_ % ring_;
+    op.len = n;
+    push(op);
+    written_ += n;
+    bytes_ += n;
+    return;
+  }
+  apply_data(buf_, n);
+  bytes_ += n;
+}
+
+void DiscardSink::apply_data(const uint8_t* p, size_t n) {
   // each byte is CRC'd once: inside a chunk into the chunk CRC (combined
   // into the object CRC at chunk end), outside directly into the object CRC
-  if (host_crc_) {
-    if (in_chunk_) {
-      chunk_crc_ = crc32c_extend(chunk_crc_, buf_, n);
-      chunk_len_ += n;
-    } else {
-      obj_crc_ = crc32c_extend(obj_crc_, buf_, n);
-    }
+  if (!host_crc_) return;
+  if (in_chunk_) {
+    chunk_crc_ = crc32c_extend(chunk_crc_, p, n);
+    chunk_len_ += n;
+  } else {
+    obj_crc_ = crc32c_extend(obj_crc_, p, n);
   }
-  bytes_ += n;
 }
 
 void DiscardSink::fold_chunk() {
@@ -64,11 +102,26 @@ void DiscardSink::fold_chunk() {
 }
 
 void DiscardSink::chunk_begin(size_t) {
+  if (deferred_) return push(Op{Op::kBegin});
+  apply_chunk_begin();
+}
+
+void DiscardSink::apply_chunk_begin() {
   fold_chunk();
   in_chunk_ = true;
 }
 
 void DiscardSink::chunk_end(bool has_crc, uint32_t crc) {
+  if (deferred_) {
+    Op op{Op::kEnd};
+    op.has_crc = has_crc;
+    op.crc = crc;
+    return push(op);
+  }
+  apply_chunk_end(has_crc, crc);
+}
+
+void DiscardSink::apply_chunk_end(bool has_crc, uint32_t crc) {
   if (host_crc_ && has_crc && in_chunk_ && !chunk_partial_) {
     any_checked_ = true;
     if (chunk_crc_ != crc) {
@@ -84,15 +137,49 @@ void DiscardSink::chunk_end(bool has_crc, uint32_t crc) {
 }
 
 void DiscardSink::resume_at(int64_t offset) {
+  (void)offset;
+  if (deferred_) return push(Op{Op::kResume});
+  apply_resume();
+}
+
+void DiscardSink::apply_resume() {
   // bytes of the interrupted chunk stay counted in the object CRC; the chunk
   // itself can no longer be checked on its own.
-  (void)offset;
   if (in_chunk_) chunk_partial_ = true;
   fold_chunk();
   in_chunk_ = false;
 }
 
+void DiscardSink::drain() {
+  if (!deferred_) return;
+  std::lock_guard<std::mutex> c(cmu_);
+  for (;;) {
+    batch_.clear();
+    {
+      std::lock_guard<std::mutex> q(qmu_);
+      if (ops_.empty()) return;
+      batch_.swap(ops_);
+    }
+    for (const Op& op : batch_) {
+      switch (op.kind) {
+        case Op::kData:
+          apply_data(buf_ + op.off, static_cast<size_t>(op.len));
+          consumed_.fetch_add(op.len, std::memory_order_release);
+          break;
+        case Op::kBegin: apply_chunk_begin(); break;
+        case Op::kEnd: apply_chunk_end(op.has_crc, op.crc); break;
+        case Op::kResume: apply_resume(); break;
+      }
+    }
+  }
+}
+
+void DiscardSink::abort() {
+  if (deferred_) reset_ring();
+}
+
 SinkResult DiscardSink::finish() {
+  drain();
   SinkResult r;
   fold_chunk();
   in_chunk_ = false;

@@ -10,9 +10,12 @@
 // owns the object's byte stream (worker thread for HTTP, connection reader
 // thread for multiplexed gRPC).
 #pragma once
+#include <atomic>
 #include <cstddef>
 #include <cstdint>
+#include <mutex>
 #include <string>
+#include <vector>
 
 namespace gcsb {
 
@@ -60,14 +63,27 @@ class Sink {
   virtual SinkResult finish() = 0;
   // Abandon the current read (error path): drain async work, no verification.
   virtual void abort() {}
+  // Deferred sinks: run queued work on the calling thread (the worker waiting
+  // for a multiplexed stream; see DiscardSink's deferred mode).
+  virtual void drain() {}
+  virtual bool deferred() const { return false; }
 };
 
 // Reference-equivalent sink: bytes land in a reusable host buffer and are
 // dropped; CRC32C optionally computed on the host (what the Go library does
 // on full HTTP reads).
+//
+// deferred (multiplexed gRPC / HTTP/2): the connection's reader thread feeds
+// every stream of the connection, so a host CRC computed inside commit()
+// serialises all streams' checksums behind one core's receive copy
+// (profiles/r2_grpc_defer).  In deferred mode the bytes land in a ring of
+// 4 x chunk_bytes, commit / chunk_begin / chunk_end / resume_at only queue an
+// op, and drain() -- called by the read's own worker thread while it waits
+// (poked at every message end) and by finish() -- replays the ops in order.
+// The reader helps drain only when the ring is full.
 class DiscardSink : public Sink {
  public:
-  DiscardSink(size_t chunk_bytes, bool host_crc);
+  DiscardSink(size_t chunk_bytes, bool host_crc, bool deferred = false);
   ~DiscardSink() override;
   void begin(const ObjectInfo& info) override;
   void update_info(const ObjectInfo& info) override;
@@ -77,11 +93,35 @@ class DiscardSink : public Sink {
   void chunk_end(bool has_crc, uint32_t crc) override;
   void resume_at(int64_t offset) override;
   SinkResult finish() override;
+  void abort() override;
+  void drain() override;
+  bool deferred() const override { return deferred_; }
 
  private:
+  struct Op {
+    enum Kind : uint8_t { kData, kBegin, kEnd, kResume } kind;
+    bool has_crc = false;
+    uint32_t crc = 0;
+    uint64_t off = 0, len = 0;
+  };
+  void apply_data(const uint8_t* p, size_t n);
+  void apply_chunk_begin();
+  void apply_chunk_end(bool has_crc, uint32_t crc);
+  void apply_resume();
+  void push(const Op& op);
+  void reset_ring();
+
   uint8_t* buf_;
   size_t cap_;
   bool host_crc_;
+  bool deferred_;
+  size_t ring_ = 0;                      // deferred: ring bytes (4 x cap_)
+  uint64_t written_ = 0;                 // deferred: ring bytes committed (reader thread)
+  std::atomic<uint64_t> consumed_{0};    // deferred: ring bytes replayed (drain)
+  std::mutex qmu_;                       // guards ops_
+  std::vector<Op> ops_;
+  std::mutex cmu_;                       // one replayer at a time, in order
+  std::vector<Op> batch_;
   ObjectInfo info_;
   uint64_t bytes_ = 0;
   uint32_t obj_crc_ = 0;     // running standard crc of all delivered bytes

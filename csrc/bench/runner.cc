@@ -16,15 +16,15 @@
 namespace gcsb {
 
 namespace {
-// gRPC multiplexes every worker's stream on the pool's connections: the host
-// CRC of a discard sink runs on the worker, not the connection's reader
+// gRPC and HTTP/2 multiplex every worker's stream on shared connections: the
+// host CRC of a discard sink runs on the worker, not the connection's reader
 // (DiscardSink deferred mode).  GCSB_DEFER_CRC=0 keeps it inline (A/B).
 bool defer_host_crc(const ClientConfig& c) {
   static const bool on = [] {
     const char* e = std::getenv("GCSB_DEFER_CRC");
     return !(e && *e == '0');
   }();
-  return on && c.protocol == "grpc";
+  return on && (c.protocol == "grpc" || c.protocol == "http2");
 }
 }  // namespace
 

@@ -146,6 +146,12 @@ class H2MediaGet : public H2ClientStream {
         }
         *delivered_ += m;
         n -= static_cast<uint32_t>(m);
+        // deferred sink (host CRC on the waiting worker): wake it every
+        // 2 MiB so its replay overlaps the rest of the body arriving
+        if (sink_.deferred() && (unpoked_ += m) >= (2u << 20)) {
+          unpoked_ = 0;
+          poke();
+        }
       }
     }
     if (end_stream) done();
@@ -164,7 +170,17 @@ class H2MediaGet : public H2ClientStream {
   // transport or sink errors.
   int wait(std::string* body) {
     std::unique_lock<std::mutex> lk(mu_);
-    cv_.wait(lk, [&] { return done_; });
+    const bool drain = sink_.deferred();
+    for (;;) {
+      cv_.wait(lk, [&] { return done_ || (drain && poked_); });
+      poked_ = false;
+      if (!drain) break;
+      const bool d = done_;
+      lk.unlock();
+      sink_.drain();
+      lk.lock();
+      if (d) break;
+    }
     if (!error_.empty()) throw StorageError(error_, retryable_);
     if (!got_head_) throw StorageError("http2 GET: stream ended without a response", true);
     *body = err_body_;
@@ -185,6 +201,11 @@ class H2MediaGet : public H2ClientStream {
     done_ = true;
     cv_.notify_all();
   }
+  void poke() {
+    std::lock_guard<std::mutex> lk(mu_);
+    poked_ = true;
+    cv_.notify_all();
+  }
   Sink& sink_;
   ReadResult* rr_;
   uint64_t* delivered_;
@@ -197,7 +218,8 @@ class H2MediaGet : public H2ClientStream {
   std::atomic<bool> failed_{false};
   std::mutex mu_;
   std::condition_variable cv_;
-  bool done_ = false, retryable_ = false;
+  bool done_ = false, retryable_ = false, poked_ = false;
+  uint64_t unpoked_ = 0;
   std::string error_;
 };
 

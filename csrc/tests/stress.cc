@@ -46,8 +46,8 @@ void readers(StorageClient& cli, const std::string& bucket, int nobj, int thread
   std::vector<std::thread> th;
   for (int t = 0; t < threads; ++t)
     th.emplace_back([&, t] {
-      // gRPC: deferred host CRC (ops replayed by this thread; the ring wraps)
-      DiscardSink sink(cli.config().read_chunk, true, cli.config().protocol == "grpc");
+      // gRPC / HTTP/2: deferred host CRC (ops replayed by this thread; the ring wraps)
+      DiscardSink sink(cli.config().read_chunk, true, cli.config().protocol != "http");
       for (int i = 0; i < reads; ++i) {
         std::string name = "obj_" + std::to_string((t + i) % nobj);
         try {
@@ -87,7 +87,7 @@ int main(int argc, char** argv) {
     srv.faults().corrupt_at = 777;
     srv.faults().corrupt_count = 1;
     {
-      DiscardSink s(256 << 10, true, std::string(proto) == "grpc");
+      DiscardSink s(256 << 10, true, std::string(proto) != "http");
       ReadResult rr = cli->read_object(bucket, "obj_0", s);
       check(rr.sink.crc_mismatch, std::string(proto) + " corruption detected");
     }

@@ -4,7 +4,7 @@
 # connection's reader thread), interleaved, 48 x 1 MiB, 8 x 1 MiB, 1 x 256 MiB.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=${OUT:-gpurun_out/grpc_defer}
+OUT=${OUT:-gpurun_out/${PROTO:-grpc}_defer}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 M=1048576
@@ -16,7 +16,7 @@ for rep in 1 2 3; do
     name=${c%%|*}; args=${c#*|}
     for d in 1 0; do
       GCSB_DEFER_CRC=$d timeout -k 10 200 ./gcsbench -start-fake-server -latency-file /dev/null \
-        -summary-json "$OUT/run.json" -client-protocol grpc $args > "$OUT/run.log" 2>&1 \
+        -summary-json "$OUT/run.json" -client-protocol ${PROTO:-grpc} $args > "$OUT/run.log" 2>&1 \
         || { tail -n 5 "$OUT/run.log"; exit 1; }
       python3 - "$name" "$d" "$OUT/run.json" <<'PY' | tee -a "$OUT/runs.jsonl"
 import json, sys

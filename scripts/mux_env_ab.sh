@@ -1,10 +1,13 @@
 #!/bin/bash
-# Deferred host CRC A/B for gRPC discard-sink reads (one connection, pool 1):
-# GCSB_DEFER_CRC=1 (CRC on each worker thread) vs 0 (CRC inline on the
-# connection's reader thread), interleaved, 48 x 1 MiB, 8 x 1 MiB, 1 x 256 MiB.
+# Env A/B for multiplexed discard-sink reads (one connection, pool 1),
+# interleaved, 48 x 1 MiB, 8 x 1 MiB, 1 x 256 MiB.  AB_VAR (default
+# GCSB_DEFER_CRC: 1 = host CRC on each worker thread, 0 = inline on the
+# connection's reader thread; GCSB_CONN_CORE: 1 = the reader thread gets a
+# physical core of its own) is set to 1 and 0.  PROTO = grpc | http2.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=${OUT:-gpurun_out/${PROTO:-grpc}_defer}
+AB_VAR=${AB_VAR:-GCSB_DEFER_CRC}
+OUT=${OUT:-gpurun_out/${PROTO:-grpc}_${AB_VAR}}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 M=1048576
@@ -15,7 +18,7 @@ for rep in 1 2 3; do
   for c in "${CASES[@]}"; do
     name=${c%%|*}; args=${c#*|}
     for d in 1 0; do
-      GCSB_DEFER_CRC=$d timeout -k 10 200 ./gcsbench -start-fake-server -latency-file /dev/null \
+      env $AB_VAR=$d timeout -k 10 200 ./gcsbench -start-fake-server -latency-file /dev/null \
         -summary-json "$OUT/run.json" -client-protocol ${PROTO:-grpc} $args > "$OUT/run.log" 2>&1 \
         || { tail -n 5 "$OUT/run.log"; exit 1; }
       python3 - "$name" "$d" "$OUT/run.json" <<'PY' | tee -a "$OUT/runs.jsonl"

@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
 #include "core/crc32c.h"
 #include "core/util.h"
@@ -13,6 +14,8 @@ DiscardSink::DiscardSink(size_t chunk_bytes, bool host_crc, bool deferred)
     : cap_(chunk_bytes), host_crc_(host_crc), deferred_(deferred && host_crc) {
   ring_ = deferred_ ? 4 * ((cap_ + 4095) / 4096 * 4096) : (cap_ + 4095) / 4096 * 4096;
   buf_ = static_cast<uint8_t*>(std::aligned_alloc(4096, ring_));
+  // fault the pages in now, not inside the first timed read
+  std::memset(buf_, 0, ring_);
 }
 
 DiscardSink::~DiscardSink() { std::free(buf_); }

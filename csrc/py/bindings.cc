@@ -246,10 +246,11 @@ class PyClient {
     ReadResult rr;
     {
       py::gil_scoped_release nogil;
-      DiscardSink s(client_->config().read_chunk, host_crc);
+      // "deferred": host CRC replayed by this (waiting) thread, as the runner
+      // does for multiplexed gRPC / HTTP/2 reads
+      DiscardSink s(client_->config().read_chunk, host_crc, sink_kind == "deferred");
       rr = client_->read_object(bucket, name, s, offset, limit);
     }
-    (void)sink_kind;
     return sink_result_dict(rr);
   }
 

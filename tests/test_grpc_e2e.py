@@ -148,3 +148,29 @@ def test_stream_cut_after_last_byte_completes_without_refetch(native, server, ra
     if not ranged:
         assert r["verified"]
     assert c.read_bytes(B, P + "0", off, want) == native.object_bytes(P + "0", off, want)
+
+
+@pytest.mark.parametrize("proto", ["grpc", "http2"])
+def test_deferred_host_crc_ring_wraps(native, server, proto):
+    # a 64 KiB read chunk -> 256 KiB ring: a 3 MiB + 5 object wraps it many
+    # times, so the reader thread has to help replay whenever it is full
+    server.add_synthetic(B, P, "", 0, 1, (3 << 20) + 5)
+    c = native.Client({"protocol": proto, "endpoint": server.url, "read_chunk": 64 << 10})
+    r = c.read(B, P + "0", "deferred")
+    assert r["bytes"] == (3 << 20) + 5 and r["verified"] and not r["crc_mismatch"]
+
+
+@pytest.mark.parametrize("proto", ["grpc", "http2"])
+def test_deferred_host_crc_detects_corruption(native, server, proto):
+    server.add_synthetic(B, P, "", 0, 1, 6 << 20)
+    server.set_faults({"corrupt_at": (4 << 20) + 17, "corrupt_count": 1})
+    c = native.Client({"protocol": proto, "endpoint": server.url, "read_chunk": 256 << 10})
+    r = c.read(B, P + "0", "deferred")
+    assert r["crc_mismatch"] and "crc" in r["detail"].lower()
+
+
+def test_deferred_host_crc_resume_after_disconnect(native, server):
+    server.add_synthetic(B, P, "", 0, 1, 10 << 20)
+    server.set_faults({"disconnect_at": (5 << 20) + 1, "disconnect_count": 1})
+    r = _c(native, server).read(B, P + "0", "deferred")
+    assert r["attempts"] == 2 and r["bytes"] == 10 << 20 and r["verified"] and not r["crc_mismatch"]

@@ -111,6 +111,8 @@ def build_parser() -> argparse.ArgumentParser:
                     help="GPUs = rank processes (one per GPU). Without torchrun env, N>1 spawns the ranks itself")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--write-parts", type=int, default=8,
+                    help="write_composite side block: parts of a parallel composite upload (0/1 = off)")
     ap.add_argument("--workload", default="read", choices=["read", "write"],
                     help="read: configs 2/4 (headline); write: config 5 as the headline")
     ap.add_argument("--protocol", default="auto", help="grpc | http | auto (grpc when built)")
@@ -383,10 +385,15 @@ def run_rank(args) -> int:
         e.add_synthetic(bucket, prefix, "", first, args.workers, size)
         return e, sh
 
-    def write_block(steps: int, warmup: int) -> dict:
+    def write_block(steps: int, warmup: int, parts: int = 1) -> dict:
         """Config 5: each rank uploads a 64 MiB object from HBM `steps` times
         (HBM -> pinned ring D2H on a side stream -> resumable upload; the
-        object CRC32C is computed on the GPU and checked by the endpoint)."""
+        object CRC32C is computed on the GPU and checked by the endpoint).
+        parts > 1 [extension]: parallel composite upload -- `parts` slices
+        uploaded on their own connections, composed server-side, the composed
+        CRC32C checked against the combine of the parts' GPU CRCs
+        (csrc/storage/sliced.h SlicedWriter; gsutil's parallel composite
+        uploads)."""
         err = ""
         lat = []
         wsize = parse_size(args.write_size)
@@ -404,6 +411,9 @@ def run_rank(args) -> int:
             if sh["client"]:
                 os.sched_setaffinity(0, sh["client"])
             client = n.Client({"protocol": protocol, "endpoint": ep.url, "retry_initial_s": 0.05})
+            if parts > 1:
+                client = n.SlicedWriter({"protocol": protocol, "endpoint": ep.url, "retry_initial_s": 0.05,
+                                         "slices": parts, "slice_min_bytes": 1 << 20, "cpus": sh["client"]})
             buf = torch.empty(wsize, dtype=torch.uint8, device=f"cuda:{gpu}")
             n.gpu_fill_pattern(gpu, buf.data_ptr(), wsize, f"upload/rank{rank}", 0)
             for i in range(warmup):
@@ -422,7 +432,8 @@ def run_rank(args) -> int:
                     m = client.write_from_device(bucket, f"upload/rank{rank}_{i}", buf.data_ptr(), wsize, gpu,
                                                  True, chunk, parse_size(args.slot_bytes), args.slots)
                     lat.append((time.perf_counter() - t0) * 1e3)
-                    if m["size"] != wsize or m["crc32c"] != m["gpu_crc32c"]:
+                    # (SlicedWriter checks the composed CRC32C itself)
+                    if m["size"] != wsize or (parts == 1 and m["crc32c"] != m["gpu_crc32c"]):
                         err = f"upload {i} not confirmed: {m}"
                         break
                     nbytes += wsize
@@ -574,6 +585,11 @@ def run_rank(args) -> int:
             blocks["write"] = ("write", write_block(side_steps, 1),
                                {"protocol": protocol, "object_bytes": parse_size(args.write_size),
                                 "config": "BASELINE config 5"})
+            if args.write_parts > 1:
+                blocks["write_composite"] = ("write_composite", write_block(side_steps, 1, args.write_parts),
+                                             {"protocol": protocol, "object_bytes": parse_size(args.write_size),
+                                              "parts": args.write_parts,
+                                              "note": "extension: parallel composite upload, not parity"})
         if world > 1 and args.fanout == "on":
             blocks["fanout"] = ("fanout", fanout_block(side_steps, 1),
                                 {"object_bytes": size, "slice_bytes": size // world,

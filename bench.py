@@ -252,6 +252,12 @@ def run_rank(args) -> int:
         protocol = "grpc" if "grpc" in hbm.available_protocols() else "http"
     size = parse_size(args.object_size)
     side_steps = args.steps if args.side_steps < 0 else args.side_steps
+    # side blocks get the headline's warm-up too: each opens fresh connections
+    # (and an endpoint of its own), so one warm-up read/upload left its first
+    # timed one carrying setup -- the write block's p99 of 14 ms over 20
+    # uploads against p99 9.4 ms over 200 back-to-back ones on one box
+    # (profiles/r2_write/tail_probe_*.json)
+    side_warm = max(1, args.warmup)
 
     # node-local synthetic GCS endpoint for this rank (no network on the box)
     gpu = ctx.gpu if ctx.gpu >= 0 else 0
@@ -569,29 +575,29 @@ def run_rank(args) -> int:
     blocks = {}
     if side_steps > 0 and args.workload == "read":
         if other and other in hbm.available_protocols():
-            blocks["compare"] = ("compare", read_block({"protocol": other}, side_steps, 1, f"{other} compare"),
+            blocks["compare"] = ("compare", read_block({"protocol": other}, side_steps, side_warm, f"{other} compare"),
                                  {"protocol": other})
         if args.sliced_streams > 1 and args.slices == 1:
             # 8 receive + 8 send threads: a share-placed endpoint of its own
             srv_sl, sh = share_endpoint()
             sliced_cfg.update({"endpoint": srv_sl.url, "cpus": sh["client"]})
-            st_sl = read_block(sliced_cfg, side_steps, 1, "sliced")
+            st_sl = read_block(sliced_cfg, side_steps, side_warm, "sliced")
             srv_sl.stop()
             blocks["sliced"] = ("sliced", st_sl,
                                 {"streams_per_read": args.sliced_streams,
                                  "ring": f"{args.sliced_slots}x{args.sliced_slot_bytes}", "affinity": "share",
                                  "piece_bytes": parse_size(args.piece_bytes), "note": "extension, not parity"})
         if use_gpu:
-            blocks["write"] = ("write", write_block(side_steps, 1),
+            blocks["write"] = ("write", write_block(side_steps, side_warm),
                                {"protocol": protocol, "object_bytes": parse_size(args.write_size),
                                 "config": "BASELINE config 5"})
             if args.write_parts > 1:
-                blocks["write_composite"] = ("write_composite", write_block(side_steps, 1, args.write_parts),
+                blocks["write_composite"] = ("write_composite", write_block(side_steps, side_warm, args.write_parts),
                                              {"protocol": protocol, "object_bytes": parse_size(args.write_size),
                                               "parts": args.write_parts,
                                               "note": "extension: parallel composite upload, not parity"})
         if world > 1 and args.fanout == "on":
-            blocks["fanout"] = ("fanout", fanout_block(side_steps, 1),
+            blocks["fanout"] = ("fanout", fanout_block(side_steps, side_warm),
                                 {"object_bytes": size, "slice_bytes": size // world,
                                  "collective": f"{ctx.backend} all_gather_into_tensor" if ctx.device.type == "cuda"
                                  else f"{ctx.backend} all_gather via host",

@@ -207,7 +207,9 @@ void H2ClientConn::reader_loop() {
           auto s = find(fh.stream);
           bool end = fh.flags & h2::kFlagEndStream;
           if (s) {
+            s->progress_.fetch_add(1, std::memory_order_relaxed);
             s->on_data(*bc_, n, end);
+            s->progress_.fetch_add(1, std::memory_order_relaxed);
           } else {
             bc_->skip(n);
           }
@@ -241,7 +243,10 @@ void H2ClientConn::reader_loop() {
           if (fh.flags & h2::kFlagEndHeaders) {
             HeaderList hl;
             dec_.decode(reinterpret_cast<const uint8_t*>(hblock.data()), hblock.size(), &hl);
-            if (auto s = find(hstream)) s->on_headers(hl, hend_stream);
+            if (auto s = find(hstream)) {
+              s->progress_.fetch_add(1, std::memory_order_relaxed);
+              s->on_headers(hl, hend_stream);
+            }
           }
           break;
         }

@@ -5,6 +5,7 @@
 // copies each object byte exactly once.
 #pragma once
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <map>
 #include <memory>
@@ -27,10 +28,32 @@ class H2ClientStream {
   virtual void on_reset(uint32_t code) = 0;
   virtual void on_conn_error(const std::string& msg) = 0;
   uint32_t id() const { return id_; }
+  // Frames the reader thread has handed this stream (bumped before and after
+  // each dispatch): an idle watchdog compares two samples.
+  uint64_t progress() const { return progress_.load(std::memory_order_relaxed); }
+
+  // cv.wait(lk, pred) with an idle limit: idle_ms > 0 gives up once the
+  // stream saw no frame for a whole idle_ms window (so after idle_ms to
+  // 2 x idle_ms of silence) and returns false; lk is held throughout.
+  template <class Pred>
+  bool wait_progress(std::condition_variable& cv, std::unique_lock<std::mutex>& lk, Pred pred, int idle_ms) {
+    if (idle_ms <= 0) {
+      cv.wait(lk, pred);
+      return true;
+    }
+    uint64_t seen = progress();
+    for (;;) {
+      if (cv.wait_for(lk, std::chrono::milliseconds(idle_ms), pred)) return true;
+      const uint64_t now = progress();
+      if (now == seen) return false;
+      seen = now;
+    }
+  }
 
  private:
   friend class H2ClientConn;
   uint32_t id_ = 0;
+  std::atomic<uint64_t> progress_{0};
   RecvWindow recv_window_{16 << 20};
 };
 

@@ -14,6 +14,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstring>
+#include <functional>
 #include <mutex>
 
 #include "core/crc32c.h"
@@ -197,10 +198,18 @@ class GrpcCall : public H2ClientStream {
   // Waits for completion; throws a StorageError for any non-OK outcome.
   // sink: drained (deferred work run on this thread) at every poke and once
   // after completion.
-  void wait_ok(Sink* sink = nullptr) {
+  // idle_ms > 0 (-read-timeout): a stream silent that long has on_idle run
+  // (it closes the connection, joining its reader thread, so nothing writes
+  // into the sink any more) and fails with a retryable "read timeout"; the
+  // read loop then resumes at the delivered offset on a fresh connection.
+  void wait_ok(Sink* sink = nullptr, int idle_ms = 0, const std::function<void()>& on_idle = {}) {
     std::unique_lock<std::mutex> lk(mu_);
     for (;;) {
-      cv_.wait(lk, [&] { return done_ || (sink && poked_); });
+      if (!wait_progress(cv_, lk, [&] { return done_ || (sink && poked_); }, idle_ms)) {
+        lk.unlock();
+        if (on_idle) on_idle();
+        throw StorageError("read timeout: no data for " + std::to_string(idle_ms) + " ms", true);
+      }
       poked_ = false;
       if (!sink) break;
       const bool d = done_;
@@ -525,6 +534,10 @@ class GrpcStorageClient : public StorageClient {
     conns_.resize(static_cast<size_t>(n));
     opt_.sock = cfg.sock;
     opt_.sock.alpn = "h2";  // gRPC over TLS negotiates HTTP/2 by ALPN
+    // -read-timeout is per stream here: a socket timeout would kill the
+    // shared reader thread of an idle multiplexed connection
+    idle_ms_ = cfg.sock.io_timeout_ms;
+    opt_.sock.io_timeout_ms = 0;
     opt_.cpus = cfg.cpus;
     // DirectPath (reference main.go:106-117: GOOGLE_CLOUD_ENABLE_DIRECT_PATH_XDS
     // is set only around NewGRPCClient, with the google-c2p xDS resolver and
@@ -585,7 +598,7 @@ class GrpcStorageClient : public StorageClient {
     std::string f = frame(req);
     try {
       c->start_stream_with_body(call, headers(method, bucket_res), f);
-      call->wait_ok();
+      call->wait_ok(nullptr, idle_ms_, [c] { c->close(); });
     } catch (...) {
       c->end_stream(*call, true);
       throw;
@@ -619,7 +632,7 @@ class GrpcStorageClient : public StorageClient {
     std::string f = frame(v2::encode_read_request(q));
     try {
       c->start_stream_with_body(call, headers("ReadObject", q.bucket), f);
-      call->wait_ok(sink.deferred() ? &sink : nullptr);
+      call->wait_ok(sink.deferred() ? &sink : nullptr, idle_ms_, [c] { c->close(); });
     } catch (...) {
       c->end_stream(*call, true);
       throw;
@@ -726,7 +739,7 @@ class GrpcStorageClient : public StorageClient {
         if (last) break;
         if (k == 0) throw StorageError("upload source ended early", false);
       } while (true);
-      call->wait_ok();
+      call->wait_ok(nullptr, idle_ms_, [c] { c->close(); });
     } catch (...) {
       c->end_stream(*call, true);
       throw;
@@ -783,6 +796,7 @@ class GrpcStorageClient : public StorageClient {
 
  private:
   H2ClientOptions opt_;
+  int idle_ms_ = 0;
   std::mutex mu_;
   std::vector<std::shared_ptr<H2ClientConn>> conns_;
   std::atomic<uint64_t> rr_{0};

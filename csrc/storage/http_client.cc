@@ -5,6 +5,7 @@
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <mutex>
 
 #include "core/json.h"
@@ -168,11 +169,17 @@ class H2MediaGet : public H2ClientStream {
 
   // Waits for END_STREAM / reset; returns the HTTP status, throws on
   // transport or sink errors.
-  int wait(std::string* body) {
+  // idle_ms > 0 (-read-timeout): see GrpcCall::wait_ok -- on_idle closes
+  // the connection (joining its reader) before the retryable timeout.
+  int wait(std::string* body, int idle_ms = 0, const std::function<void()>& on_idle = {}) {
     std::unique_lock<std::mutex> lk(mu_);
     const bool drain = sink_.deferred();
     for (;;) {
-      cv_.wait(lk, [&] { return done_ || (drain && poked_); });
+      if (!wait_progress(cv_, lk, [&] { return done_ || (drain && poked_); }, idle_ms)) {
+        lk.unlock();
+        if (on_idle) on_idle();
+        throw StorageError("read timeout: no data for " + std::to_string(idle_ms) + " ms", true);
+      }
       poked_ = false;
       if (!drain) break;
       const bool d = done_;
@@ -290,7 +297,7 @@ class HttpStorageClient : public StorageClient {
     int status = 0;
     try {
       c->start_stream(call, h, true);
-      status = call->wait(&body);
+      status = call->wait(&body, cfg_.sock.io_timeout_ms, [c] { c->close(); });
     } catch (...) {
       c->end_stream(*call, true);
       throw;
@@ -545,6 +552,7 @@ class HttpStorageClient : public StorageClient {
   H2ClientOptions h2_opt_ = [this] {
     H2ClientOptions o;
     o.sock = with_alpn(cfg_.sock, "h2");
+    o.sock.io_timeout_ms = 0;  // -read-timeout is per stream on the shared connection
     o.cpus = cfg_.cpus;
     return o;
   }();

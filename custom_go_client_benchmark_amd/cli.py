@@ -93,6 +93,8 @@ def build_flags() -> FlagSet:
     fs.float("retry-multiplier", 2.0, "Backoff multiplier (reference RetryMultiplier 2)")
     fs.duration("retry-max-total", 0.0, "Give up retrying after this long (0 = never, as the reference)")
     fs.int("retry-max-attempts", 0, "Give up after this many attempts (0 = unlimited)")
+    fs.duration("read-timeout", 0.0, "Fail an attempt (retryably) when no byte arrives for this long; the read "
+                "resumes at the delivered offset (0 = none, as the reference's http.Client Timeout 0)")
     fs.string("affinity", "auto", "CPU placement: auto | quota | share | same | split | numa | none")
     fs.bool("start-fake-server", False, "Start a node-local synthetic GCS endpoint (no network)")
     fs.int("fake-object-size", 100 << 20, "Synthetic object size (reference objects are ~100 MB)")
@@ -199,7 +201,8 @@ def main(argv: list[str] | None = None) -> int:
         token_uri=fs.get("token-uri"), user_agent=fs.get("user-agent"), tls_ca_file=fs.get("tls-ca-file"),
         tls_verify=not fs.get("tls-insecure"), retry_initial_s=fs.get("retry-initial"),
         retry_max_s=fs.get("retry-max"), retry_multiplier=fs.get("retry-multiplier"),
-        retry_max_total_s=fs.get("retry-max-total"), retry_max_attempts=fs.get("retry-max-attempts"))
+        retry_max_total_s=fs.get("retry-max-total"), retry_max_attempts=fs.get("retry-max-attempts"),
+        read_timeout_s=fs.get("read-timeout"))
 
     # tracing (reference main.go:162-165)
     tracer, trace_cleanup = None, None

@@ -602,10 +602,8 @@ def run_rank(args) -> int:
                                  "collective": f"{ctx.backend} all_gather_into_tensor" if ctx.device.type == "cuda"
                                  else f"{ctx.backend} all_gather via host",
                                  "note": "extension: read once per node, fan out over xGMI"})
-    elif side_steps > 0 and other and other in hbm.available_protocols():
-        pass  # write headline: no read side blocks
+    # (a write headline runs no side blocks)
     srv.stop()
-
 
     rc = 0
     if rank == 0:

@@ -44,6 +44,9 @@ void H2ClientConn::close() {
   }
   if (bc_) ::shutdown(bc_->conn().fd(), SHUT_RDWR);
   if (w_) w_->kill();
+  // two threads may close one connection (a timed-out stream's watchdog and
+  // the pool replacing the dead connection): one of them joins the reader
+  std::lock_guard<std::mutex> lk(close_mu_);
   if (reader_.joinable()) {
     if (reader_.get_id() == std::this_thread::get_id())
       reader_.detach();

@@ -98,6 +98,7 @@ class H2ClientConn {
   HpackDecoder dec_;
   HpackEncoder enc_;
   std::thread reader_;
+  std::mutex close_mu_;  // serialises close()'s join of reader_
   std::mutex mu_;
   std::map<uint32_t, std::shared_ptr<H2ClientStream>> streams_;
   uint32_t next_id_ = 1;

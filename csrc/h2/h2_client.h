@@ -41,9 +41,17 @@ class H2ClientStream {
       cv.wait(lk, pred);
       return true;
     }
+#if defined(__SANITIZE_THREAD__)
+    // gcc 11's TSan does not intercept pthread_cond_clockwait (steady-clock
+    // waits), misses the unlock inside the wait and reports the notifier's
+    // lock as a double lock; system-clock deadlines use pthread_cond_timedwait
+    using Clock = std::chrono::system_clock;
+#else
+    using Clock = std::chrono::steady_clock;
+#endif
     uint64_t seen = progress();
     for (;;) {
-      if (cv.wait_for(lk, std::chrono::milliseconds(idle_ms), pred)) return true;
+      if (cv.wait_until(lk, Clock::now() + std::chrono::milliseconds(idle_ms), pred)) return true;
       const uint64_t now = progress();
       if (now == seen) return false;
       seen = now;

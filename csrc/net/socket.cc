@@ -10,6 +10,7 @@
 #include <openssl/err.h>
 #include <openssl/ssl.h>
 #include <poll.h>
+#include <signal.h>
 #include <sys/sendfile.h>
 #include <sys/socket.h>
 #include <unistd.h>
@@ -24,6 +25,20 @@
 #include "core/util.h"
 
 namespace gcsb {
+
+namespace {
+// sendfile() and writev() have no MSG_NOSIGNAL: a peer that closed its end
+// (a client's read timeout, a cancelled stream) would kill the whole process
+// with SIGPIPE.  Like other network runtimes (Go ignores it on sockets), turn
+// it into EPIPE -- unless the host program installed a handler of its own.
+// (Python already ignores SIGPIPE; the C++ tools and tests do not.)
+struct IgnoreSigpipe {
+  IgnoreSigpipe() {
+    struct sigaction cur {};
+    if (::sigaction(SIGPIPE, nullptr, &cur) == 0 && cur.sa_handler == SIG_DFL) ::signal(SIGPIPE, SIG_IGN);
+  }
+} g_ignore_sigpipe;
+}  // namespace
 
 Endpoint Endpoint::parse(const std::string& url) {
   Endpoint ep;

@@ -208,6 +208,9 @@ class GrpcCall : public H2ClientStream {
       if (!wait_progress(cv_, lk, [&] { return done_ || (sink && poked_); }, idle_ms)) {
         lk.unlock();
         if (on_idle) on_idle();
+        // the reader is gone: replay what it queued for this attempt, so the
+        // sink's state matches the delivered offset the retry resumes at
+        if (sink) sink->drain();
         throw StorageError("read timeout: no data for " + std::to_string(idle_ms) + " ms", true);
       }
       poked_ = false;
@@ -610,7 +613,6 @@ class GrpcStorageClient : public StorageClient {
 
   void read_attempt(const std::string& bucket, const std::string& object, Sink& sink, int64_t offset, int64_t limit,
                     bool first_attempt, ReadResult* rr, uint64_t* delivered) override {
-    const bool full = offset == 0 && limit < 0;
     if (first_attempt) {
       ObjectInfo bi;
       bi.start_offset = offset;
@@ -618,6 +620,11 @@ class GrpcStorageClient : public StorageClient {
       rr->sink_begun = true;
       rr->info = bi;
     }
+    // A whole-object read stays one: a resumed attempt (offset = delivered)
+    // still feeds the CRC the sink has run from byte 0, so every attempt's
+    // object_checksums apply -- the first attempt may have been cut before
+    // its first message's checksums field arrived.
+    const bool full = rr->info.start_offset == 0 && limit < 0;
     v2::ReadObjectRequest q;
     q.bucket = v2::bucket_resource(bucket);
     q.object = object;

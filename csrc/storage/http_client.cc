@@ -178,6 +178,7 @@ class H2MediaGet : public H2ClientStream {
       if (!wait_progress(cv_, lk, [&] { return done_ || (drain && poked_); }, idle_ms)) {
         lk.unlock();
         if (on_idle) on_idle();
+        if (drain) sink_.drain();  // (see GrpcCall::wait_ok)
         throw StorageError("read timeout: no data for " + std::to_string(idle_ms) + " ms", true);
       }
       poked_ = false;

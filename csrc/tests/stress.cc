@@ -5,6 +5,7 @@
 // exercises every shared structure of the C++ core from many threads under
 // ASan+UBSan and TSan.  Exit status 0 = every read/write verified.
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -52,7 +53,9 @@ void readers(StorageClient& cli, const std::string& bucket, int nobj, int thread
         std::string name = "obj_" + std::to_string((t + i) % nobj);
         try {
           ReadResult rr = cli.read_object(bucket, name, sink);
-          check(rr.sink.verified && !rr.sink.crc_mismatch, cli.transport_name() + " read " + name);
+          check(rr.sink.verified && !rr.sink.crc_mismatch,
+                cli.transport_name() + " read " + name + " (attempts " + std::to_string(rr.attempts) + ", bytes " +
+                    std::to_string(rr.bytes) + ": " + rr.sink.detail + ")");
         } catch (const std::exception& e) {
           check(false, cli.transport_name() + " read " + name + ": " + e.what());
         }
@@ -134,6 +137,24 @@ int main(int argc, char** argv) {
       }
     });
     for (auto& x : th) x.join();
+    // 6) -read-timeout: the endpoint stalls every response for a while, so
+    //    concurrent attempts time out, close the shared connection (several
+    //    at once on gRPC / HTTP/2), retry and resume once it recovers
+    {
+      ClientConfig tc = client_cfg(proto, srv.url());
+      tc.sock.io_timeout_ms = 30;
+      tc.retry.max_attempts = 0;
+      tc.retry.max_total_s = 5.0;
+      auto tcli = make_client(tc);
+      srv.faults().latency_ms = 80;
+      std::thread heal([&] {
+        std::this_thread::sleep_for(std::chrono::milliseconds(150));
+        srv.faults().latency_ms = 0;
+      });
+      readers(*tcli, bucket, nobj, 4, 2);
+      heal.join();
+      check(tcli->stats().retries > 0, std::string(proto) + " read timeouts retried");
+    }
   }
   srv.stop();
   if (g_fail) {

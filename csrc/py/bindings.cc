@@ -596,6 +596,9 @@ class PyServer {
     if (d.contains("throttle_bps")) f.throttle_bps = d["throttle_bps"].cast<int64_t>();
     if (d.contains("latency_ms")) f.latency_ms = d["latency_ms"].cast<int>();
     if (d.contains("drop_trailers_count")) f.drop_trailers_count = d["drop_trailers_count"].cast<int>();
+    if (d.contains("stall_at")) f.stall_at = d["stall_at"].cast<int64_t>();
+    if (d.contains("stall_ms")) f.stall_ms = d["stall_ms"].cast<int>();
+    if (d.contains("stall_count")) f.stall_count = d["stall_count"].cast<int>();
   }
   py::dict stats() {
     auto& s = srv_->stats();

@@ -28,6 +28,9 @@ struct FaultConfig {
   std::atomic<int64_t> throttle_bps{0};     // per-response rate cap (bytes/s), 0 = none
   std::atomic<int> latency_ms{0};           // added time-to-first-byte
   std::atomic<int> drop_trailers_count{0};  // gRPC: cut the connection after the last DATA, before trailers
+  std::atomic<int64_t> stall_at{-1};        // pause a response this long before sending this object offset...
+  std::atomic<int> stall_ms{0};
+  std::atomic<int> stall_count{0};          // ...in this many responses (client read-timeout tests)
 };
 
 struct ServerConfig {

@@ -3,6 +3,7 @@
 // CRC32C; metadata + object checksums on the first message), GetObject,
 // ListObjects, WriteObject (client streaming), StartResumableWrite,
 // QueryWriteStatus.  Content is sent zero-copy from the object store (writev).
+#include <cstdint>
 #include <sys/socket.h>
 #include <sys/uio.h>
 
@@ -338,7 +339,10 @@ class H2ServerConn {
   }
   // Sends one gRPC message given as iov pieces, splitting into DATA frames as
   // the peer's flow-control windows and max frame size allow.
-  void send_message_iov(ServerStream& s, std::vector<SendPiece> pieces) {
+  // stall_pos < SIZE_MAX: pause stall_ms before that byte of the framed
+  // message (the 5-byte prefix counts), mid-DATA (read-timeout tests)
+  void send_message_iov(ServerStream& s, std::vector<SendPiece> pieces, size_t stall_pos = SIZE_MAX,
+                        int stall_ms = 0) {
     size_t total = 0;
     for (auto& p : pieces) total += p.n;
     uint8_t pre[5] = {0, 0, 0, 0, 0};
@@ -348,11 +352,16 @@ class H2ServerConn {
     pp.n = 5;
     pieces.insert(pieces.begin(), pp);
     total += 5;
-    size_t idx = 0, off = 0;
+    size_t idx = 0, off = 0, done = 0;
     std::vector<SendPiece> frame;
     while (total > 0) {
       if (s.cancelled) throw Cancelled{};
-      size_t n = w_.reserve(s.id, total);
+      if (done == stall_pos) {
+        std::this_thread::sleep_for(std::chrono::milliseconds(stall_ms));
+        stall_pos = SIZE_MAX;
+        continue;
+      }
+      size_t n = w_.reserve(s.id, stall_pos > done ? std::min(total, stall_pos - done) : total);
       if (n == 0) throw Cancelled{};
       frame.clear();
       size_t need = n;
@@ -373,6 +382,7 @@ class H2ServerConn {
       }
       w_.write_frame_pieces(h2::kData, 0, s.id, frame, n);
       total -= n;
+      done += n;
     }
   }
   static SendPiece mem(const void* p, size_t n) {
@@ -525,6 +535,7 @@ class H2ServerConn {
     int64_t disc = f.disconnect_count.load() > 0 ? f.disconnect_at.load() : -1;
     int64_t corrupt = f.corrupt_count.load() > 0 ? f.corrupt_at.load() : -1;
     const int64_t bps = f.throttle_bps.load();
+    int64_t stall = f.stall_count.load() > 0 ? f.stall_at.load() : -1;
     const int64_t t0 = now_ns();
     uint64_t sent = 0;
     while (sent < len) {
@@ -532,6 +543,18 @@ class H2ServerConn {
       const uint64_t off = start + sent;
       uint64_t want = std::min<uint64_t>(len - sent, 8u << 20);
       if (bps > 0) want = std::min<uint64_t>(want, std::max<int64_t>(4096, bps / 100));
+      if (stall >= 0 && static_cast<int64_t>(off) <= stall && static_cast<int64_t>(off + want) > stall) {
+        if (static_cast<int64_t>(off) < stall) {
+          want = static_cast<uint64_t>(stall) - off;
+        } else {
+          stall = -1;
+          if (f.stall_count.fetch_sub(1) > 0) {
+            ++srv_.stats().faults_injected;
+            std::this_thread::sleep_for(std::chrono::milliseconds(f.stall_ms.load()));
+          }
+          continue;
+        }
+      }
       const size_t n = w_.reserve(s.id, want);
       if (n == 0) throw Cancelled{};
       if (disc >= 0 && static_cast<int64_t>(off + n) > disc && static_cast<int64_t>(off) <= disc) {
@@ -608,6 +631,7 @@ class H2ServerConn {
     const std::string meta = v2::encode_object(to_v2(*o));
     int64_t disc = f.disconnect_count.load() > 0 ? f.disconnect_at.load() : -1;
     int64_t corrupt = f.corrupt_count.load() > 0 ? f.corrupt_at.load() : -1;
+    int64_t stall = f.stall_count.load() > 0 ? f.stall_at.load() : -1;
     const int64_t bps = f.throttle_bps.load();
     const int64_t t0 = now_ns();
     uint64_t off = static_cast<uint64_t>(start);
@@ -648,7 +672,15 @@ class H2ServerConn {
         pieces.push_back(mem(p, n));
       }
       pieces.push_back(mem(fr.tail.data(), fr.tail.size()));
-      send_message_iov(s, pieces);
+      size_t stall_pos = SIZE_MAX;
+      if (stall >= 0 && static_cast<int64_t>(off) <= stall && static_cast<int64_t>(off + n) > stall) {
+        if (f.stall_count.fetch_sub(1) > 0) {
+          ++srv_.stats().faults_injected;
+          stall_pos = 5 + fr.head.size() + static_cast<size_t>(stall - static_cast<int64_t>(off));
+        }
+        stall = -1;
+      }
+      send_message_iov(s, pieces, stall_pos, f.stall_ms.load());
       off += n;
       sent += n;
       first = false;

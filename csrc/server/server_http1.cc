@@ -278,6 +278,9 @@ class Http1Handler {
     if (j.get("corrupt_count")) f.corrupt_count = static_cast<int>(j.get_int("corrupt_count"));
     if (j.get("throttle_bps")) f.throttle_bps = j.get_int("throttle_bps");
     if (j.get("latency_ms")) f.latency_ms = static_cast<int>(j.get_int("latency_ms"));
+    if (j.get("stall_at")) f.stall_at = j.get_int("stall_at");
+    if (j.get("stall_ms")) f.stall_ms = static_cast<int>(j.get_int("stall_ms"));
+    if (j.get("stall_count")) f.stall_count = static_cast<int>(j.get_int("stall_count"));
     respond(c_, 200, {}, "{}");
   }
 
@@ -302,6 +305,7 @@ class Http1Handler {
     const int64_t disc_at = disc;
     int64_t corrupt = f.corrupt_count.load() > 0 ? f.corrupt_at.load() : -1;
     int64_t bps = f.throttle_bps.load();
+    int64_t stall = f.stall_count.load() > 0 ? f.stall_at.load() : -1;
     int64_t t0 = now_ns();
     uint64_t sent = 0;
     const uint64_t piece_max = 8 << 20;
@@ -309,6 +313,18 @@ class Http1Handler {
       uint64_t off = start + sent;
       uint64_t n = std::min<uint64_t>(piece_max, len - sent);
       if (bps > 0) n = std::min<uint64_t>(n, std::max<int64_t>(4096, bps / 100));
+      if (stall >= 0 && static_cast<int64_t>(off) <= stall && static_cast<int64_t>(off + n) > stall) {
+        if (static_cast<int64_t>(off) < stall) {
+          n = static_cast<uint64_t>(stall) - off;  // send up to the stall point first
+        } else {
+          stall = -1;
+          if (f.stall_count.fetch_sub(1) > 0) {
+            ++srv_.stats().faults_injected;
+            std::this_thread::sleep_for(std::chrono::milliseconds(f.stall_ms.load()));
+          }
+          continue;
+        }
+      }
       if (disc >= 0 && static_cast<int64_t>(off + n) > disc && static_cast<int64_t>(off) <= disc) {
         disc = -1;  // at most once per response
         // claim one of the remaining faults (concurrent responses race for it)

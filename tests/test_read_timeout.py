@@ -80,3 +80,30 @@ def test_cli_flag_parses():
     fs = build_flags().parse(["-read-timeout", "1.5s"])
     assert fs.get("read-timeout") == pytest.approx(1.5)
     assert build_flags().parse([]).get("read-timeout") == 0.0
+
+
+@pytest.mark.parametrize("proto", PROTOS)
+def test_stall_mid_body_resumes(native, server, proto):
+    # the endpoint goes silent 1 MiB into the body (inside gRPC's first 2 MiB
+    # message, before its object_checksums field): the attempt times out and
+    # the read resumes at the delivered offset
+    server.add_synthetic(B, P, "", 0, 1, 3 << 20)
+    server.set_faults({"stall_at": 1 << 20, "stall_ms": 400, "stall_count": 1})
+    c = _client(native, server, proto, io_timeout_ms=100, retry_max_attempts=3)
+    r = c.read(B, P + "0")
+    assert r["bytes"] == 3 << 20 and r["verified"] and r["attempts"] == 2
+    assert server.stats()["faults_injected"] == 1
+
+
+@pytest.mark.parametrize("proto", PROTOS)
+def test_corruption_before_a_timeout_is_caught_after_resume(native, server, proto):
+    # a byte corrupted in the part the first attempt delivered, then a stall:
+    # the resumed read must still check the whole-object CRC32C (gRPC used to
+    # drop it when the first attempt never saw its checksums field)
+    server.add_synthetic(B, P, "", 0, 1, 3 << 20)
+    server.set_faults({"corrupt_at": 4242, "corrupt_count": 1, "stall_at": 1 << 20, "stall_ms": 400,
+                       "stall_count": 1})
+    c = _client(native, server, proto, io_timeout_ms=100, retry_max_attempts=3)
+    r = c.read(B, P + "0")
+    assert r["attempts"] == 2
+    assert r["crc_mismatch"] and not r["verified"]

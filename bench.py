@@ -162,6 +162,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--fanout", default="on", choices=["on", "off"],
                     help="N > 1 side block: each rank reads 1/N of one shared object, an all-gather over the "
                          "GPUs gives every GPU the whole object (extension)")
+    ap.add_argument("--list-objects", type=int, default=1000,
+                    help="config 3 side block: list this many 1 MiB objects, read each into HBM (0 = off)")
+    ap.add_argument("--list-workers", type=int, default=8, help="config 3 side block: readers")
     ap.add_argument("--write-size", default="64MiB", help="config 5 object size")
     ap.add_argument("--write-chunk", default="16MiB", help="resumable upload chunk (HTTP) / message batch")
     ap.add_argument("--json-out", default="")
@@ -309,8 +312,8 @@ def run_rank(args) -> int:
         if torch.cuda.is_available():
             torch.cuda.synchronize()
 
-    def read_ok(s: dict, steps: int) -> tuple[bool, str]:
-        reads = steps * args.workers
+    def read_ok(s: dict, steps: int, workers: int) -> tuple[bool, str]:
+        reads = steps * workers
         if s["errors"]:
             return False, s["first_error"] or "read error"
         if s["reads"] != reads:
@@ -354,7 +357,7 @@ def run_rank(args) -> int:
         cpu = {}
         if not err:
             s1 = r1.summary()
-            ok, why = read_ok(s1, steps)
+            ok, why = read_ok(s1, steps, overrides.get("workers", args.workers))
             if not ok:
                 err = why
             cpu = cpu_delta(c0, cpu_snapshot(), float(s1["bytes"]), e1)
@@ -540,6 +543,43 @@ def run_rank(args) -> int:
         del part, full, sink
         return st
 
+    def list_read_block(proto: str, warmup_passes: int) -> dict:
+        """Config 3 (BASELINE.json): list `--list-objects` 1 MiB objects, then
+        `--list-workers` readers read every listed object once into HBM, GPU
+        CRC32C on every read (reference list_operation + read_operation; the
+        CLI's -workload list-read).  One timed pass after untimed ones; the
+        listing's own time is reported apart (list_ms)."""
+        nobj, workers = args.list_objects, args.list_workers
+        sh = affinity.plan(gpu, "share", slot) if use_gpu else {"client": [], "server": []}
+        ep = None
+        names, list_ms, err = [], 0.0, ""
+        try:
+            ep = n.Server({"port": 0, "md5": False, "cpus": sh["server"], "retain_uploads": False})
+            ep.start()
+            ep.add_synthetic(bucket, f"c3_rank{rank}/file_", "", 0, nobj, 1 << 20)
+            lister = n.Client({"protocol": proto, "endpoint": ep.url, "retry_initial_s": 0.05})
+            t0 = time.perf_counter()
+            names = [o["name"] for o in lister.list_all(bucket, f"c3_rank{rank}/file_", 1000)]
+            list_ms = (time.perf_counter() - t0) * 1e3
+            del lister
+            if len(names) != nobj:
+                err = f"listed {len(names)} of {nobj} objects"
+        except Exception as e:  # noqa: BLE001 - reported in the block, collectives still run
+            err = f"{type(e).__name__}: {e}"
+        per_pass = (nobj + workers - 1) // workers
+        over = {"protocol": proto, "endpoint": ep.url if ep is not None else "", "workers": workers,
+                "object_names": names or [f"c3_rank{rank}/file_0"], "cpus": sh["client"], "worker_id_offset": 0,
+                "rcvbuf": 0}
+        # every rank runs the block (and its collectives) whatever happened here
+        st = read_block(over, per_pass, per_pass * warmup_passes, f"{proto} list-read")
+        if err:
+            st["error"] = err
+            st["ok_min"] = 0.0
+        if ep is not None:
+            ep.stop()
+        st["list_ms_max"] = gdist.reduce_stats(ctx, list_ms=list_ms)["list_ms_max"]
+        return st
+
     def mib_s(st: dict) -> float:
         return st["nbytes_sum"] / max(st["elapsed_max"], 1e-12) / (1 << 20)
 
@@ -587,6 +627,11 @@ def run_rank(args) -> int:
                                 {"streams_per_read": args.sliced_streams,
                                  "ring": f"{args.sliced_slots}x{args.sliced_slot_bytes}", "affinity": "share",
                                  "piece_bytes": parse_size(args.piece_bytes), "note": "extension, not parity"})
+        if args.list_objects > 0:
+            for p in [protocol] + ([other] if other and other in hbm.available_protocols() else []):
+                blocks[f"list_read_{p}"] = (f"list_read_{p}", list_read_block(p, 1),
+                                            {"protocol": p, "objects": args.list_objects, "object_bytes": 1 << 20,
+                                             "workers": args.list_workers, "config": "BASELINE config 3"})
         if use_gpu:
             blocks["write"] = ("write", write_block(side_steps, side_warm),
                                {"protocol": protocol, "object_bytes": parse_size(args.write_size),
@@ -689,6 +734,8 @@ def run_rank(args) -> int:
                     # mib_s: whole objects landed in every GPU's HBM, job-wide
                     b["per_gpu_mib_s"] = round(b["mib_s"] / max(1, world), 2)
                     b["crc_verified_ranks"] = int(st["crc_ok_sum"])
+                if key.startswith("list_read_"):
+                    b["list_ms"] = round(st["list_ms_max"], 3)
                 if key == "sliced":
                     b["host_landed_p50_ms"] = round(st["host_p50_max"], 3)
                     b["slice_skew_ms"] = round(st["skew_max"], 3)

@@ -51,6 +51,10 @@ def test_bench_two_ranks_gloo():
     other = {"grpc": "http", "http": "grpc"}[out["config"]["protocol"]]
     assert out["compare"]["protocol"] == other and out["compare"]["ok"] and out["compare"]["mib_s"] > 0
     assert out["sliced"]["ok"] and out["sliced"]["streams_per_read"] == 8
+    # config 3: list 1000 x 1 MiB objects per rank, 8 readers, both transports
+    for p in ("grpc", "http"):
+        b = out[f"list_read_{p}"]
+        assert b["ok"] and b["objects"] == 1000 and b["workers"] == 8 and b["mib_s"] > 0 and b["list_ms"] > 0
 
 
 def _bench_env():

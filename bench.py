@@ -627,6 +627,16 @@ def run_rank(args) -> int:
                                 {"streams_per_read": args.sliced_streams,
                                  "ring": f"{args.sliced_slots}x{args.sliced_slot_bytes}", "affinity": "share",
                                  "piece_bytes": parse_size(args.piece_bytes), "note": "extension, not parity"})
+        if "http" in hbm.available_protocols():
+            # config 1: one 1 MiB object over the HTTP JSON API, CPU only
+            # (discard sink, host CRC32C as the Go library), one reader
+            srv.add_synthetic(bucket, "c1/file_", "", first, 1, 1 << 20)
+            blocks["c1_http_cpu"] = ("c1_http_cpu",
+                                     read_block({"protocol": "http", "http_api": "json", "sink": "discard",
+                                                 "host_crc": True, "object_prefix": "c1/file_", "workers": 1,
+                                                 "rcvbuf": 0}, max(side_steps, 100), side_warm, "config 1"),
+                                     {"protocol": "http", "api": "json", "object_bytes": 1 << 20, "sink": "discard",
+                                      "workers": 1, "config": "BASELINE config 1"})
         if args.list_objects > 0:
             for p in [protocol] + ([other] if other and other in hbm.available_protocols() else []):
                 blocks[f"list_read_{p}"] = (f"list_read_{p}", list_read_block(p, 1),

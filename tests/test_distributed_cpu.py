@@ -51,6 +51,8 @@ def test_bench_two_ranks_gloo():
     other = {"grpc": "http", "http": "grpc"}[out["config"]["protocol"]]
     assert out["compare"]["protocol"] == other and out["compare"]["ok"] and out["compare"]["mib_s"] > 0
     assert out["sliced"]["ok"] and out["sliced"]["streams_per_read"] == 8
+    # config 1: one 1 MiB object, HTTP JSON API, CPU only
+    assert out["c1_http_cpu"]["ok"] and out["c1_http_cpu"]["api"] == "json" and out["c1_http_cpu"]["p50_ms"] > 0
     # config 3: list 1000 x 1 MiB objects per rank, 8 readers, both transports
     for p in ("grpc", "http"):
         b = out[f"list_read_{p}"]

@@ -550,7 +550,13 @@ def run_rank(args) -> int:
         CLI's -workload list-read).  One timed pass after untimed ones; the
         listing's own time is reported apart (list_ms)."""
         nobj, workers = args.list_objects, args.list_workers
-        sh = affinity.plan(gpu, "share", slot) if use_gpu else {"client": [], "server": []}
+        # one L3 domain for the readers and the endpoint, as the CLI's
+        # default for several GPU readers: gRPC multiplexes all 8 readers on
+        # one connection, whose reader thread loses the sender's L3 when
+        # spread over the share's domains (list_read_grpc 6.2k MiB/s with
+        # "share" vs 13.5-15.2k with "same", profiles/r2_check_s4b,
+        # profiles/r2_cli_geometry)
+        sh = affinity.plan(gpu, "same", slot) if use_gpu else {"client": [], "server": []}
         ep = None
         names, list_ms, err = [], 0.0, ""
         try:

@@ -460,6 +460,8 @@ def run_rank(args) -> int:
         os.sched_setaffinity(0, saved_aff)
         st = gdist.reduce_stats(ctx, elapsed=e1, nbytes=float(nbytes), p50=p50, p99=p99, ok=0.0 if err else 1.0)
         st["error"] = err
+        # this rank's slowest uploads (index in the timed run, ms): where the tail sits
+        st["slowest"] = [[i, round(v, 2)] for i, v in sorted(enumerate(lat), key=lambda x: -x[1])[:3]]
         return st
 
     def fanout_block(steps: int, warmup: int) -> dict:
@@ -734,6 +736,8 @@ def run_rank(args) -> int:
                 # per slot: the node holding most of its pages (-1 = not resident)
                 out["numa"]["ring_slot_nodes"] = [max(range(len(c) - 1), key=lambda i: c[i]) if sum(c[:-1]) else -1
                                                   for c in slots]
+            if args.workload == "write":
+                out["rank0_slowest"] = head.get("slowest", [])
             if args.workload == "read":
                 # where a read's time goes: request -> first byte (TTFB), -> last
                 # byte in host memory (host_landed), -> last byte + CRC in HBM (p50)
@@ -750,6 +754,8 @@ def run_rank(args) -> int:
                     # mib_s: whole objects landed in every GPU's HBM, job-wide
                     b["per_gpu_mib_s"] = round(b["mib_s"] / max(1, world), 2)
                     b["crc_verified_ranks"] = int(st["crc_ok_sum"])
+                if key.startswith("write"):
+                    b["rank0_slowest"] = st.get("slowest", [])
                 if key.startswith("list_read_"):
                     b["list_ms"] = round(st["list_ms_max"], 3)
                 if key == "sliced":

@@ -710,6 +710,8 @@ GpuByteSource::GpuByteSource(int device, const void* dptr, uint64_t n, size_t sl
       // a ring slot never larger than the (part of the) object it stages
       slot_bytes_(std::max<size_t>(std::min<uint64_t>(slot_bytes, (n + 65535) / 65536 * 65536), 65536)),
       nslots_(std::max(2, slots)) {
+  static const bool trace = std::getenv("GCSB_TRACE_SOURCE") != nullptr;  // phase timings (write-tail probe)
+  int64_t tp[5] = {now_ns(), 0, 0, 0, 0};
   hip_check(hipSetDevice(device_), "hipSetDevice");
   DeviceStreamPool& pool = DeviceStreamPool::get(device_);
   const unsigned base = pool.next_base() * static_cast<unsigned>(nslots_);
@@ -725,6 +727,7 @@ GpuByteSource::GpuByteSource(int device, const void* dptr, uint64_t n, size_t sl
     host_[i] = static_cast<uint8_t*>(PinnedPool::get(slot_bytes_));
     hip_check(hipEventCreateWithFlags(&ev_[i], hipEventDisableTiming), "hipEventCreate");
   }
+  tp[1] = now_ns();
   if (gpu_crc) {
     // Chunk CRCs on a grid that the transport's upload messages fall on:
     // messages are <= 2 MiB (gRPC MAX_WRITE_CHUNK_BYTES) and never cross a
@@ -734,7 +737,15 @@ GpuByteSource::GpuByteSource(int device, const void* dptr, uint64_t n, size_t sl
     crc_ = gpu_crc32c(device_, src_, n_, grid_, grid_ ? &chunk_crc_ : nullptr);
     has_crc_ = true;
   }
+  tp[2] = now_ns();
   restart(0);
+  if (trace) {
+    tp[3] = now_ns();
+    hip_check(hipEventSynchronize(ev_[0]), "hipEventSynchronize");
+    tp[4] = now_ns();
+    std::fprintf(stderr, "GpuByteSource: setup %.3f ms, crc %.3f ms, issue %.3f ms, first copy %.3f ms\n",
+                 (tp[1] - tp[0]) / 1e6, (tp[2] - tp[1]) / 1e6, (tp[3] - tp[2]) / 1e6, (tp[4] - tp[3]) / 1e6);
+  }
 }
 
 bool GpuByteSource::range_crc32c(uint64_t off, size_t len, uint32_t* crc) {
@@ -770,11 +781,17 @@ void GpuByteSource::wait_all() {
 }
 
 void GpuByteSource::issue(int slot, uint64_t off) {
+  static const bool trace = std::getenv("GCSB_TRACE_SOURCE") != nullptr;
   size_t len = static_cast<size_t>(std::min<uint64_t>(slot_bytes_, n_ - off));
   slot_off_[slot] = off;
   slot_len_[slot] = len;
+  const int64_t t0 = trace ? now_ns() : 0;
   hip_check(hipMemcpyAsync(host_[slot], src_ + off, len, hipMemcpyDeviceToHost, st_[slot]), "hipMemcpyAsync(D2H)");
+  const int64_t t1 = trace ? now_ns() : 0;
   hip_check(hipEventRecord(ev_[slot], st_[slot]), "hipEventRecord");
+  if (trace && now_ns() - t0 > 200000)
+    std::fprintf(stderr, "GpuByteSource: slow issue slot %d stream %p: copy %.3f ms, event %.3f ms\n", slot,
+                 static_cast<void*>(st_[slot]), (t1 - t0) / 1e6, (now_ns() - t1) / 1e6);
   ++copies_;
 }
 

@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--slot-bytes", type=int, default=2 << 20)
     ap.add_argument("--slots", type=int, default=8)
     ap.add_argument("--label", default="")
+    ap.add_argument("--gap", default="none", choices=["none", "sleep", "nccl", "gloo", "sync", "pginit", "devsync"],
+                    help="between warm-up and timed uploads: nothing, a 200 ms sleep, or a one-rank "
+                         "process-group barrier (all_reduce + synchronize), as bench.py does")
     a = ap.parse_args()
     n = pkg._native
     sh = affinity.plan(0, "share", 0)
@@ -41,6 +44,25 @@ def main():
     n.gpu_fill_pattern(0, buf.data_ptr(), a.size, "upload/probe", 0)
     for i in range(a.warmup):
         client.write_from_device("b", f"w/warm{i}", buf.data_ptr(), a.size, 0, True, a.chunk, a.slot_bytes, a.slots)
+    if a.gap == "sleep":
+        time.sleep(0.2)
+    elif a.gap == "sync":
+        torch.cuda.synchronize()
+    elif a.gap == "devsync":
+        n.gpu_device_synchronize(0) if hasattr(n, "gpu_device_synchronize") else torch.cuda.synchronize()
+    elif a.gap == "pginit":
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29577")
+        dist.init_process_group("gloo", rank=0, world_size=1)
+    elif a.gap in ("nccl", "gloo"):
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29577")
+        dist.init_process_group(a.gap, rank=0, world_size=1)
+        t = torch.ones(1, dtype=torch.int32, device="cuda:0" if a.gap == "nccl" else "cpu")
+        dist.all_reduce(t)
+        torch.cuda.synchronize()
     lat = []
     inner = []
     crcms = []
@@ -61,6 +83,7 @@ def main():
                       "p90": round(q(90), 3), "p99": round(q(99), 3), "max": round(s[-1], 3),
                       "mib_s": round(a.size * a.n / (sum(lat) / 1e3) / (1 << 20), 1),
                       "crc_ms_p50": round(sorted(crcms)[len(crcms) // 2], 3),
+                      "gap": a.gap, "first_ms": round(lat[0], 3),
                       "slow_uploads (i, ms, gpu_crc_ms, upload_ms)": slow[:40], "n_slow": len(slow),
                       "placement": {k: sh.get(k) for k in ("client", "server")}}))
     ep.stop()

@@ -304,7 +304,18 @@ GpuSink::GpuSink(const GpuSinkConfig& cfg) : cfg_(cfg) {
   if (cfg_.slot_bytes < 65536) cfg_.slot_bytes = 65536;
   set_device();
   DeviceStreamPool& pool = DeviceStreamPool::get(cfg_.device);
-  const unsigned base = pool.next_base() * static_cast<unsigned>(cfg_.slots);
+  // Slot i of a sink uses pool stream i (slot i's CRC overlaps slot i+1's
+  // copy; the sliced block's 16 sinks spread over all 8).  GCSB_SINK_STREAMS=k
+  // (A/B) alternates a sink's slots over k streams instead: k = 2 kept the
+  // single-stream headline's first-read tail lower in one run after the
+  // bench's torch.cuda.synchronize() and not in three others, and cost the
+  // sliced block 7-9% (profiles/r2_streams_sync), so the default stays.
+  static const int env_nst = [] {
+    const char* e = std::getenv("GCSB_SINK_STREAMS");
+    return e ? std::max(1, std::min(32, std::atoi(e))) : 0;
+  }();
+  const unsigned nst = static_cast<unsigned>(env_nst > 0 ? env_nst : cfg_.slots);
+  const unsigned base = pool.next_base() * nst;
   if (pool.private_streams())
     hip_check(hipStreamCreateWithFlags(&own_stream_, hipStreamNonBlocking), "hipStreamCreate");
   d_tables_ = device_crc_tables(cfg_.device);
@@ -324,7 +335,7 @@ GpuSink::GpuSink(const GpuSinkConfig& cfg) : cfg_(cfg) {
       hip_check(hipMalloc(reinterpret_cast<void**>(&s.dev_ring), cfg_.slot_bytes), "hipMalloc(ring slot)");
     const unsigned evf = hipEventDisableTiming | (cfg_.blocking_sync ? hipEventBlockingSync : 0u);
     hip_check(hipEventCreateWithFlags(&s.ev, evf), "hipEventCreate");
-    s.st = own_stream_ ? own_stream_ : pool.at(base + static_cast<unsigned>(i));
+    s.st = own_stream_ ? own_stream_ : pool.at(base + static_cast<unsigned>(i) % nst);
     s.tiles = d_tiles_ + crc_scratch_words(tiles_cap_) * static_cast<size_t>(i);
     s.res = res_host_ + static_cast<size_t>(i) * kMaxSeg;
     hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&s.d_res), s.res, 0), "hipHostGetDevicePointer");
@@ -714,11 +725,23 @@ GpuByteSource::GpuByteSource(int device, const void* dptr, uint64_t n, size_t sl
   int64_t tp[5] = {now_ns(), 0, 0, 0, 0};
   hip_check(hipSetDevice(device_), "hipSetDevice");
   DeviceStreamPool& pool = DeviceStreamPool::get(device_);
-  const unsigned base = pool.next_base() * static_cast<unsigned>(nslots_);
+  // The staging copies go round-robin over 2 pool streams, not one per slot:
+  // after a device-wide synchronize (the bench's torch.cuda.synchronize()
+  // around every timed region) the first D2H hipMemcpyAsync on one of the
+  // further streams blocked ~7 ms -- the first timed upload's 13.6 ms p99.
+  // With 2 streams: first upload 6.1 ms, p99 6.3 (GCSB_TRACE_SOURCE=1,
+  // scripts/experiments/write_tail.py --gap sync; profiles/r2_write).
+  static const unsigned nst = [] {
+    const char* e = std::getenv("GCSB_UPLOAD_STREAMS");  // A/B: staging streams per upload source
+    const int v = e ? std::atoi(e) : 2;
+    return static_cast<unsigned>(std::max(1, std::min(32, v)));
+  }();
+  const unsigned base = pool.next_base() * nst;
   if (pool.private_streams())
     hip_check(hipStreamCreateWithFlags(&own_stream_, hipStreamNonBlocking), "hipStreamCreate");
   st_.resize(nslots_);
-  for (int i = 0; i < nslots_; ++i) st_[i] = own_stream_ ? own_stream_ : pool.at(base + static_cast<unsigned>(i));
+  for (int i = 0; i < nslots_; ++i)
+    st_[i] = own_stream_ ? own_stream_ : pool.at(base + static_cast<unsigned>(i) % nst);
   host_.resize(nslots_);
   ev_.resize(nslots_);
   slot_off_.assign(nslots_, ~0ull);

@@ -725,7 +725,8 @@ GpuByteSource::GpuByteSource(int device, const void* dptr, uint64_t n, size_t sl
   int64_t tp[5] = {now_ns(), 0, 0, 0, 0};
   hip_check(hipSetDevice(device_), "hipSetDevice");
   DeviceStreamPool& pool = DeviceStreamPool::get(device_);
-  // The staging copies go round-robin over 2 pool streams, not one per slot:
+  // The staging copies go round-robin over 2 pool streams, not one per slot,
+  // and the same 2 for every source:
   // after a device-wide synchronize (the bench's torch.cuda.synchronize()
   // around every timed region) the first D2H hipMemcpyAsync on one of the
   // further streams blocked ~7 ms -- the first timed upload's 13.6 ms p99.
@@ -736,7 +737,11 @@ GpuByteSource::GpuByteSource(int device, const void* dptr, uint64_t n, size_t sl
     const int v = e ? std::atoi(e) : 2;
     return static_cast<unsigned>(std::max(1, std::min(32, v)));
   }();
-  const unsigned base = pool.next_base() * nst;
+  // every upload source of the process shares the same nst streams: the 8
+  // parts of a parallel composite upload spread over all 8 pool streams had
+  // their first upload after the sync at 10.3 ms vs p50 2.7
+  // (profiles/r2_final_s4 rank0_slowest)
+  const unsigned base = 0;
   if (pool.private_streams())
     hip_check(hipStreamCreateWithFlags(&own_stream_, hipStreamNonBlocking), "hipStreamCreate");
   st_.resize(nslots_);

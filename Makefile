@@ -19,14 +19,14 @@ CXXFLAGS := $(CXXSTD) $(OPT) $(HOSTARCH) $(WARN) -fPIC -pthread $(EXTRA_CXXFLAGS
 HIPFLAGS := $(CXXSTD) $(OPT) --offload-arch=$(ARCH) -fPIC -pthread -Icsrc -munsafe-fp-atomics $(EXTRA_HIPFLAGS)
 LDLIBS   := -lssl -lcrypto -lpthread
 
-CORE_SRCS := csrc/core/crc32c.cc csrc/core/affinity.cc csrc/core/content.cc csrc/core/util.cc csrc/core/json.cc \
+CORE_SRCS := csrc/core/crc32c.cc csrc/core/affinity.cc csrc/core/ceiling.cc csrc/core/content.cc csrc/core/util.cc csrc/core/json.cc \
              csrc/net/socket.cc csrc/net/buffered.cc \
              csrc/http1/http1.cc csrc/h2/hpack.cc csrc/h2/h2.cc csrc/h2/h2_client.cc csrc/proto/storage_v2.cc \
              csrc/storage/sink.cc csrc/storage/sliced.cc csrc/storage/auth.cc csrc/storage/client.cc csrc/storage/http_client.cc \
              csrc/storage/grpc_client.cc \
              csrc/server/store.cc csrc/server/media.cc csrc/server/fakegcs.cc csrc/server/server_http1.cc csrc/server/server_grpc.cc \
              csrc/gpu/crc_host.cc
-GPU_SRCS  := csrc/gpu/crc32c_kernels.hip csrc/gpu/engine.hip
+GPU_SRCS  := csrc/gpu/crc32c_kernels.hip csrc/gpu/engine.hip csrc/gpu/copy_engines.hip
 PY_SRCS   := csrc/py/bindings.cc csrc/bench/runner.cc
 
 CORE_OBJS := $(patsubst csrc/%.cc,$(BUILD)/%.o,$(CORE_SRCS))
@@ -56,7 +56,7 @@ $(BUILD)/libgcsbcore.a: $(CORE_OBJS)
 
 $(EXT): $(PY_OBJS) $(GPU_OBJS) $(BUILD)/libgcsbcore.a
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(PY_OBJS) $(GPU_OBJS) $(BUILD)/libgcsbcore.a \
-	  -L/opt/rocm/lib -lamdhip64 -lrocprofiler-sdk-roctx $(LDLIBS) -Wl,-rpath,/opt/rocm/lib
+	  -L/opt/rocm/lib -lamdhip64 -lhsa-runtime64 -lrocprofiler-sdk-roctx $(LDLIBS) -Wl,-rpath,/opt/rocm/lib
 
 $(PKG)/bin/%: csrc/tools/%.cc $(BUILD)/libgcsbcore.a
 	@mkdir -p $(PKG)/bin

@@ -167,6 +167,18 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--list-workers", type=int, default=8, help="config 3 side block: readers")
     ap.add_argument("--write-size", default="64MiB", help="config 5 object size")
     ap.add_argument("--write-chunk", default="16MiB", help="resumable upload chunk (HTTP) / message batch")
+    ap.add_argument("--baseline", default="on", choices=["on", "off"],
+                    help="cpu_baseline side blocks: the headline config with the reference's semantics (discard "
+                         "sink, host CRC32C; /root/reference/main.go:133-146) on the same endpoint, placement and "
+                         "steps, for the headline protocol and the other one; vs_baseline = value / it")
+    ap.add_argument("--ceiling", default="on", choices=["on", "off"],
+                    help="ceiling side block: one loopback TCP stream (sendfile -> recv into a THP ring, no GPU, "
+                         "no framing) and pinned -> HBM copies, in the headline's placement")
+    ap.add_argument("--ref-workers", type=int, default=48,
+                    help="ref_default_* side blocks: the reference's default experiment, -worker 48 on 1 MiB "
+                         "objects, gRPC pool 1 vs HTTP keep-alive, discard sink + host CRC (0 = off)")
+    ap.add_argument("--ref-reads", type=int, default=50, help="ref_default_*: timed reads per worker")
+    ap.add_argument("--ref-object-size", default="1MiB", help="ref_default_*: object size")
     ap.add_argument("--json-out", default="")
     return ap
 
@@ -346,6 +358,8 @@ def run_rank(args) -> int:
         sync()
         t1 = time.perf_counter()
         rv0 = n.recv_stats()
+        if use_gpu:
+            n.reset_slow_hip_calls()
         if not err:
             c0, th0 = cpu_snapshot(), cpuacct.thread_cpu()
             t1 = time.perf_counter()
@@ -370,17 +384,23 @@ def run_rank(args) -> int:
                 # Conn::read_some of the process: client side only here)
                 cpu["recv_calls"] = calls
                 cpu["recv_avg_kib"] = round((rv1[1] - rv0[1]) / calls / 1024.0, 1)
+        slow_hip = n.slow_hip_calls() if use_gpu else {}
         ring_numa = r1.ring_numa(0) if (r1 is not None and use_gpu) else []
         s1 = s1 or {"bytes": 0, "p50_ms": 0.0, "p99_ms": 0.0, "host_p50_ms": 0.0, "ttfb_p50_ms": 0.0, "slice_skew_ms": 0.0,
                     "verified": 0, "reads": 0}
         del r1
         st = gdist.reduce_stats(ctx, elapsed=e1, nbytes=float(s1["bytes"]), p50=s1["p50_ms"], p99=s1["p99_ms"],
                                 host_p50=s1["host_p50_ms"], ttfb_p50=s1.get("ttfb_p50_ms", 0.0),
-                                skew=s1.get("slice_skew_ms", 0.0),
+                                skew=s1.get("slice_skew_ms", 0.0), first_p50=s1.get("first_read_p50_ms", 0.0),
+                                steady_p99=s1.get("steady_p99_ms", 0.0),
                                 verified=float(s1["verified"]), ok=0.0 if err else 1.0)
         st["error"] = err
         st["cpu"] = cpu
         st["ring_numa"] = ring_numa
+        # this rank's slowest reads [index in the timed run, ms, host-landed ms,
+        # TTFB ms] and the slot hand-off HIP calls that blocked (>= 1 ms)
+        st["slowest"] = [[int(x[0])] + [round(v, 3) for v in x[1:]] for x in (s1.get("slowest") or [])]
+        st["slow_hip"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in slow_hip.items()}
         return st
 
     def share_endpoint():
@@ -432,6 +452,7 @@ def run_rank(args) -> int:
             err = f"{type(e).__name__}: {e}"
         gdist.barrier(ctx, "R1 write start barrier")
         sync()
+        n.reset_slow_hip_calls()
         t1 = time.perf_counter()
         nbytes = 0
         if not err:
@@ -462,6 +483,7 @@ def run_rank(args) -> int:
         st["error"] = err
         # this rank's slowest uploads (index in the timed run, ms): where the tail sits
         st["slowest"] = [[i, round(v, 2)] for i, v in sorted(enumerate(lat), key=lambda x: -x[1])[:3]]
+        st["slow_hip"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in n.slow_hip_calls().items()}
         return st
 
     def fanout_block(steps: int, warmup: int) -> dict:
@@ -588,6 +610,77 @@ def run_rank(args) -> int:
         st["list_ms_max"] = gdist.reduce_stats(ctx, list_ms=list_ms)["list_ms_max"]
         return st
 
+    def ceiling_block(head_mib_s_per_rank: float) -> dict:
+        """Same-box bounds of the headline, in its placement: one loopback
+        TCP stream with no GPU and no framing (sendfile() by a thread on the
+        endpoint's CPUs -> recv() into a THP ring by a thread on the client's
+        CPUs, core/ceiling.cc), the client core's memcpy rate, and pinned ->
+        HBM copies in the sink's pattern (2 MiB hipMemcpyAsync copies from an
+        8-slot THP ring over the pool streams, engine.hip copy_ceiling)."""
+        err = ""
+        r = {"tcp_gbps": 0.0, "tcp_recv_cpu_s_per_gib": 0.0, "tcp_send_cpu_s_per_gib": 0.0, "memcpy_gbps": 0.0,
+             "h2d_gbps": 0.0}
+        try:
+            ring = args.slots * parse_size(args.slot_bytes)
+            reads = max(3, min(10, side_steps))
+            t = n.loopback_ceiling({"mode": "tcp", "object_bytes": size, "reads": reads, "ring_bytes": ring,
+                                    "rcvbuf": parse_size(args.rcvbuf), "recv_cpus": placement["client"],
+                                    "send_cpus": placement["server"], "ring_pages": 1})
+            m = n.loopback_ceiling({"mode": "memcpy", "object_bytes": size, "reads": reads, "ring_bytes": ring,
+                                    "recv_cpus": placement["client"], "ring_pages": 1})
+            r.update(tcp_gbps=t["gbps"], tcp_recv_cpu_s_per_gib=t["recv_cpu_s_per_gib"],
+                     tcp_send_cpu_s_per_gib=t["send_cpu_s_per_gib"], memcpy_gbps=m["gbps"])
+            if use_gpu:
+                h = n.copy_ceiling(gpu, "h2d", size, parse_size(args.slot_bytes), args.slots, args.slots, 5)
+                r["h2d_gbps"] = h["gbps"]
+        except Exception as e:  # noqa: BLE001 - reported in the block, collectives still run
+            err = f"{type(e).__name__}: {e}"
+        st = gdist.reduce_stats(ctx, ok=0.0 if err else 1.0, **r)
+        out = {"ok": st["ok_min"] >= 1.0}
+        for k in r:  # the slowest rank's bound (each rank measures its own)
+            out[k] = round(st[k + "_min"], 3)
+        head_gbps = head_mib_s_per_rank * (1 << 20) / 1e9
+        bounds = [b for b in (out["tcp_gbps"], out["h2d_gbps"] if use_gpu else 0.0) if b > 0]
+        if bounds:
+            out["bound_gbps"] = round(min(bounds), 3)
+            out["headline_gbps_per_gpu"] = round(head_gbps, 3)
+            out["headline_frac_of_ceiling"] = round(head_gbps / min(bounds), 3)
+        out["note"] = ("one loopback TCP stream, no GPU / h2 / gRPC framing, headline placement; "
+                       "h2d: pinned THP ring -> HBM, 2 MiB copies")
+        if err:
+            out["error"] = err[:300]
+        return out
+
+    def ref_default_block(proto: str) -> dict:
+        """The reference's only experiment (execute_pb.sh:4,8; main.go:36,
+        30,111): -worker 48 readers, each re-reading its own object
+        file_<id>, over gRPC with ONE connection (pool 1) or HTTP/1.1
+        keep-alive, io.Discard sink with the library's host CRC32C.  Objects
+        are --ref-object-size; a rank's 48 workers read file_<rank*48 + w>.
+        Threads on the rank's GPU-local share of L3 domains trimmed to its
+        CPU-quota budget (affinity share_quota)."""
+        workers = args.ref_workers
+        osz = parse_size(args.ref_object_size)
+        sh = affinity.plan(gpu, "share_quota", slot) if use_gpu else {"client": [], "server": []}
+        ep = None
+        err = ""
+        try:
+            ep = n.Server({"port": 0, "md5": False, "cpus": sh["server"], "retain_uploads": False})
+            ep.start()
+            ep.add_synthetic(bucket, "ref_default/file_", "", rank * workers, workers, osz)
+        except Exception as e:  # noqa: BLE001
+            err = f"{type(e).__name__}: {e}"
+        over = {"protocol": proto, "endpoint": ep.url if ep is not None else "", "workers": workers,
+                "object_prefix": "ref_default/file_", "worker_id_offset": rank * workers, "sink": "discard",
+                "host_crc": True, "cpus": sh["client"], "rcvbuf": 0, "grpc_conn_pool_size": 1}
+        st = read_block(over, args.ref_reads, 2, f"{proto} reference default")
+        if err:
+            st["error"] = err
+            st["ok_min"] = 0.0
+        if ep is not None:
+            ep.stop()
+        return st
+
     def mib_s(st: dict) -> float:
         return st["nbytes_sum"] / max(st["elapsed_max"], 1e-12) / (1 << 20)
 
@@ -635,6 +728,27 @@ def run_rank(args) -> int:
                                 {"streams_per_read": args.sliced_streams,
                                  "ring": f"{args.sliced_slots}x{args.sliced_slot_bytes}", "affinity": "share",
                                  "piece_bytes": parse_size(args.piece_bytes), "note": "extension, not parity"})
+        if use_gpu and args.baseline == "on":
+            # the reference's semantics on the headline config: same endpoint,
+            # placement, object and steps; bytes to a discard sink, CRC32C of
+            # every byte on the host (the Go library's reader,
+            # /root/reference/main.go:133-146) -- what vs_baseline divides by
+            for p in [protocol] + ([other] if other and other in hbm.available_protocols() else []):
+                key = "cpu_baseline" if p == protocol else f"cpu_baseline_{p}"
+                blocks[key] = (key, read_block({"protocol": p, "sink": "discard", "host_crc": True}, side_steps,
+                                               side_warm, f"{p} cpu baseline"),
+                               {"protocol": p, "sink": "discard", "host_crc": True,
+                                "note": "reference semantics: io.Discard + host CRC32C"})
+        if args.ceiling == "on":
+            blocks["ceiling"] = ("ceiling", ceiling_block(mib_s(head) / max(1, world)), None)
+        if args.ref_workers > 0:
+            for p in ["http"] + ([x for x in ("grpc",) if x in hbm.available_protocols()]):
+                blocks[f"ref_default_{p}"] = (f"ref_default_{p}", ref_default_block(p),
+                                              {"protocol": p, "workers": args.ref_workers,
+                                               "object_bytes": parse_size(args.ref_object_size),
+                                               "reads_per_worker": args.ref_reads, "sink": "discard",
+                                               "grpc_conn_pool_size": 1 if p == "grpc" else None,
+                                               "note": "reference default experiment (execute_pb.sh)"})
         if "http" in hbm.available_protocols():
             # config 1: one 1 MiB object over the HTTP JSON API, CPU only
             # (discard sink, host CRC32C as the Go library), one reader
@@ -745,17 +859,37 @@ def run_rank(args) -> int:
                 out["host_landed_p50_ms"] = round(head["host_p50_max"], 3)
                 out["verified_reads"] = int(head["verified_sum"])
                 out["rank0_cpu"] = head["cpu"]
+                out["rank0_slowest"] = head.get("slowest", [])
+                if head.get("slow_hip"):
+                    out["slow_hip_calls"] = head["slow_hip"]
                 if head["cpu"]:
                     gib_s = value / max(1, world) / 1024.0
                     out["cpus_needed_per_gpu"] = round(head["cpu"]["process_cpu_s_per_gib"] * gib_s, 2)
+            base = blocks.get("cpu_baseline")
+            if base is not None and base[1]["ok_min"] >= 1.0 and mib_s(base[1]) > 0:
+                out["vs_baseline"] = round(value / mib_s(base[1]), 3)
+                out["baseline"] = {"what": "cpu_baseline block: same config, reference semantics (discard sink + "
+                                           "host CRC32C), same run", "mib_s": round(mib_s(base[1]), 2),
+                                   "p50_ms": round(base[1]["p50_max"], 3),
+                                   "p50_ratio": round(base[1]["p50_max"] / max(head["p50_max"], 1e-9), 3)}
             for key, (_, st, extra) in blocks.items():
-                b = block_json(st, **extra)
+                if extra is None:  # already a JSON block (ceiling)
+                    out[key] = st
+                    continue
+                b = block_json(st, **{k: v for k, v in extra.items() if v is not None})
+                if key.startswith("ref_default_"):
+                    b["first_read_p50_ms"] = round(st["first_p50_max"], 3)
+                    b["steady_p99_ms"] = round(st["steady_p99_max"], 3)
+                    if st.get("cpu", {}).get("cgroup_nr_throttled") is not None:
+                        b["cgroup_nr_throttled"] = st["cpu"]["cgroup_nr_throttled"]
                 if key == "fanout":
                     # mib_s: whole objects landed in every GPU's HBM, job-wide
                     b["per_gpu_mib_s"] = round(b["mib_s"] / max(1, world), 2)
                     b["crc_verified_ranks"] = int(st["crc_ok_sum"])
-                if key.startswith("write"):
-                    b["rank0_slowest"] = st.get("slowest", [])
+                if st.get("slowest"):
+                    b["rank0_slowest"] = st["slowest"]
+                if st.get("slow_hip", {}).get("slow"):
+                    b["slow_hip_calls"] = st["slow_hip"]
                 if key.startswith("list_read_"):
                     b["list_ms"] = round(st["list_ms_max"], 3)
                 if key == "sliced":

@@ -86,6 +86,7 @@ void Runner::reset_stats() {
   lat_ms_.clear();
   host_ms_.clear();
   ttfb_ms_.clear();
+  ttfb_by_read_.clear();
   first_ms_.clear();
   steady_ms_.clear();
   pending_.clear();
@@ -129,6 +130,7 @@ void Runner::record(ReadRecord&& r, double ms, double host_ms) {
     (r.seq == 0 ? first_ms_ : steady_ms_).push_back(ms);
     host_ms_.push_back(host_ms);
     if (r.ttfb_ns > r.start_ns) ttfb_ms_.push_back((r.ttfb_ns - r.start_ns) / 1e6);
+    ttfb_by_read_.push_back(r.ttfb_ns > r.start_ns ? (r.ttfb_ns - r.start_ns) / 1e6 : 0.0);
     // metric semantics: integer-truncated milliseconds (reference main.go:146)
     acc_.oc_buckets[oc_bucket_index(std::floor(ms))]++;
   }
@@ -295,6 +297,17 @@ RunSummary Runner::summary() const {
   RunSummary s = acc_;
   s.elapsed_s = t_last_ > t_first_ ? (t_last_ - t_first_) / 1e9 : 0;
   s.mb_per_s = s.elapsed_s > 0 ? s.bytes / 1048576.0 / s.elapsed_s : 0;
+  {
+    std::vector<size_t> idx(lat_ms_.size());
+    for (size_t i = 0; i < idx.size(); ++i) idx[i] = i;
+    const size_t k = std::min<size_t>(3, idx.size());
+    std::partial_sort(idx.begin(), idx.begin() + k, idx.end(),
+                      [&](size_t a, size_t b) { return lat_ms_[a] > lat_ms_[b]; });
+    for (size_t j = 0; j < k; ++j) {
+      const size_t i = idx[j];
+      s.slowest.push_back({static_cast<double>(i), lat_ms_[i], host_ms_[i], ttfb_by_read_[i]});
+    }
+  }
   std::vector<double> v = lat_ms_;
   std::sort(v.begin(), v.end());
   if (!v.empty()) {

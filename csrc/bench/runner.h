@@ -91,6 +91,8 @@ struct RunSummary {
   double first_read_p50_ms = 0, first_read_max_ms = 0, steady_p50_ms = 0, steady_p99_ms = 0;
   double slice_skew_ms = 0;  // sliced reads: mean spread of the slices' host-landed times
   uint64_t oc_buckets[kOcBuckets] = {0};
+  // the 3 slowest reads: {index in completion order, ms, host-landed ms, TTFB ms}
+  std::vector<std::vector<double>> slowest;
   std::string first_error;
   GpuSinkStats gpu;
 };
@@ -133,6 +135,7 @@ class Runner {
   mutable std::mutex mu_;
   std::vector<ReadRecord> pending_;
   std::vector<double> lat_ms_, host_ms_, ttfb_ms_, first_ms_, steady_ms_;
+  std::vector<double> ttfb_by_read_;  // per ok read, in completion order (0 if unknown)
   RunSummary acc_;
   int64_t t_first_ = 0, t_last_ = 0;
   std::mutex out_mu_;

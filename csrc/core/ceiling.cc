@@ -1,0 +1,231 @@
+#include "core/ceiling.h"
+
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <signal.h>
+#include <sys/mman.h>
+#include <sys/resource.h>
+#include <sys/sendfile.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cerrno>
+#include <chrono>
+#include <cstring>
+#include <exception>
+#include <stdexcept>
+#include <string>
+#include <thread>
+
+#include "core/affinity.h"
+
+namespace gcsb {
+
+namespace {
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+double thread_cpu_s() {
+  rusage ru{};
+  getrusage(RUSAGE_THREAD, &ru);
+  return ru.ru_utime.tv_sec + ru.ru_utime.tv_usec * 1e-6 + ru.ru_stime.tv_sec + ru.ru_stime.tv_usec * 1e-6;
+}
+
+[[noreturn]] void fail(const char* what) {
+  throw std::runtime_error(std::string("ceiling: ") + what + ": " + std::strerror(errno));
+}
+
+// An anonymous page-locked (when allowed) ring, faulted in by the caller.
+struct Ring {
+  uint8_t* p = nullptr;
+  size_t n = 0;
+  Ring(size_t bytes, int pages) : n(bytes) {
+    void* m = ::mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (m == MAP_FAILED) fail("mmap(ring)");
+    if (pages == 1) (void)madvise(m, n, MADV_HUGEPAGE);
+    if (pages == 2) (void)madvise(m, n, MADV_NOHUGEPAGE);
+    (void)mlock(m, n);
+    std::memset(m, 0, n);
+    p = static_cast<uint8_t*>(m);
+  }
+  ~Ring() {
+    if (p) ::munmap(p, n);
+  }
+};
+
+struct Fd {
+  int fd = -1;
+  explicit Fd(int f = -1) : fd(f) {}
+  ~Fd() {
+    if (fd >= 0) ::close(fd);
+  }
+  Fd(const Fd&) = delete;
+  Fd& operator=(const Fd&) = delete;
+};
+
+double median(std::vector<double> v) {
+  if (v.empty()) return 0;
+  std::sort(v.begin(), v.end());
+  return v[v.size() / 2];
+}
+
+}  // namespace
+
+CeilingResult memcpy_ceiling(const CeilingConfig& c) {
+  CeilingResult res;
+  std::exception_ptr err;
+  // a thread of its own: pinning must not leak into the caller
+  std::thread t([&] {
+    try {
+      pin_current_thread(c.recv_cpus);
+      std::vector<uint8_t> src(c.object_bytes);
+      for (size_t i = 0; i < src.size(); i += 4096) src[i] = static_cast<uint8_t>(i >> 12);
+      Ring ring(c.ring_bytes, c.ring_pages);
+      const size_t piece = std::min<size_t>(c.ring_bytes, 2u << 20);
+      std::vector<double> lat;
+      const double c0 = thread_cpu_s(), t0 = now_s();
+      for (int r = 0; r < c.reads; ++r) {
+        const double a = now_s();
+        size_t off = 0, roff = 0;
+        while (off < c.object_bytes) {
+          const size_t k = std::min(piece, c.object_bytes - off);
+          if (roff + k > ring.n) roff = 0;
+          std::memcpy(ring.p + roff, src.data() + off, k);
+          off += k;
+          roff += k;
+        }
+        lat.push_back((now_s() - a) * 1e3);
+      }
+      const double el = now_s() - t0, cpu = thread_cpu_s() - c0;
+      const double gib = static_cast<double>(c.object_bytes) * c.reads / (1 << 30);
+      res.gbps = static_cast<double>(c.object_bytes) * c.reads / el / 1e9;
+      res.recv_cpu_s_per_gib = cpu / gib;
+      res.p50_ms = median(lat);
+    } catch (...) {
+      err = std::current_exception();
+    }
+  });
+  t.join();
+  if (err) std::rethrow_exception(err);
+  return res;
+}
+
+CeilingResult tcp_ceiling(const CeilingConfig& c) {
+  ::signal(SIGPIPE, SIG_IGN);  // a sender outliving a failed receiver must not kill the process
+  const size_t obj = c.object_bytes;
+  Fd mfd(memfd_create("ceiling-object", 0));
+  if (mfd.fd < 0) fail("memfd_create");
+  if (ftruncate(mfd.fd, static_cast<off_t>(obj)) != 0) fail("ftruncate");
+  {
+    std::vector<uint8_t> blk(1 << 20);
+    for (size_t i = 0; i < blk.size(); ++i) blk[i] = static_cast<uint8_t>(i * 131 + 7);
+    for (size_t off = 0; off < obj; off += blk.size())
+      if (pwrite(mfd.fd, blk.data(), std::min(blk.size(), obj - off), static_cast<off_t>(off)) < 0) fail("pwrite");
+  }
+  Fd ls(socket(AF_INET, SOCK_STREAM, 0));
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  if (bind(ls.fd, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0 || listen(ls.fd, 1) != 0) fail("bind/listen");
+  socklen_t al = sizeof(a);
+  getsockname(ls.fd, reinterpret_cast<sockaddr*>(&a), &al);
+
+  std::atomic<int> go{0};
+  std::atomic<bool> quit{false};
+  std::atomic<int> conn_fd{-1};
+  double send_cpu_total = 0;
+  std::exception_ptr send_err, recv_err;
+  std::thread sender([&] {
+    try {
+      name_current_thread("ceiling-send");
+      pin_current_thread(c.send_cpus);
+      Fd s(accept(ls.fd, nullptr, nullptr));
+      if (s.fd < 0) fail("accept");
+      int one = 1;
+      setsockopt(s.fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+      std::vector<uint8_t> copybuf;
+      if (!c.zerocopy_send) copybuf.resize(2u << 20);
+      const double c0 = thread_cpu_s();
+      for (int r = 0; r < c.reads; ++r) {
+        while (go.load() <= r && !quit.load()) std::this_thread::yield();
+        if (quit.load()) break;
+        off_t off = 0;
+        while (static_cast<size_t>(off) < obj) {
+          const size_t k = std::min<size_t>(obj - off, 2u << 20);
+          if (c.zerocopy_send) {
+            if (sendfile(s.fd, mfd.fd, &off, k) <= 0) fail("sendfile");
+          } else {
+            if (pread(mfd.fd, copybuf.data(), k, off) != static_cast<ssize_t>(k)) fail("pread");
+            size_t done = 0;
+            while (done < k) {
+              const ssize_t w = send(s.fd, copybuf.data() + done, k - done, MSG_NOSIGNAL);
+              if (w <= 0) fail("send");
+              done += static_cast<size_t>(w);
+            }
+            off += static_cast<off_t>(k);
+          }
+        }
+      }
+      send_cpu_total = thread_cpu_s() - c0;
+    } catch (...) {
+      send_err = std::current_exception();
+      quit.store(true);
+      if (int f = conn_fd.load(); f >= 0) ::shutdown(f, SHUT_RDWR);  // unblock the receiver
+    }
+  });
+  CeilingResult res;
+  std::thread receiver([&] {
+    Fd cs(socket(AF_INET, SOCK_STREAM, 0));
+    try {
+      name_current_thread("ceiling-recv");
+      pin_current_thread(c.recv_cpus);
+      if (cs.fd < 0) fail("socket");
+      if (c.rcvbuf > 0) setsockopt(cs.fd, SOL_SOCKET, SO_RCVBUF, &c.rcvbuf, sizeof(c.rcvbuf));
+      if (connect(cs.fd, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0) fail("connect");
+      conn_fd.store(cs.fd);
+      Ring ring(c.ring_bytes, c.ring_pages);
+      std::vector<double> lat;
+      const double c0 = thread_cpu_s(), t0 = now_s();
+      for (int r = 0; r < c.reads; ++r) {
+        const double st = now_s();
+        go.store(r + 1);
+        size_t got = 0, roff = 0;
+        while (got < obj) {
+          if (roff >= ring.n) roff = 0;
+          const size_t want = std::min({c.recv_chunk, ring.n - roff, obj - got});
+          const ssize_t n = recv(cs.fd, ring.p + roff, want, 0);
+          if (n <= 0) {
+            if (n == 0) errno = ECONNRESET;
+            fail("recv");
+          }
+          got += static_cast<size_t>(n);
+          roff += static_cast<size_t>(n);
+        }
+        lat.push_back((now_s() - st) * 1e3);
+      }
+      const double el = now_s() - t0, cpu = thread_cpu_s() - c0;
+      res.gbps = static_cast<double>(obj) * c.reads / el / 1e9;
+      res.recv_cpu_s_per_gib = cpu / (static_cast<double>(obj) * c.reads / (1 << 30));
+      res.p50_ms = median(lat);
+    } catch (...) {
+      recv_err = std::current_exception();
+      quit.store(true);
+      ::shutdown(ls.fd, SHUT_RDWR);  // a sender still in accept()
+    }
+    conn_fd.store(-1);
+  });
+  receiver.join();
+  quit.store(true);
+  sender.join();
+  if (recv_err) std::rethrow_exception(recv_err);
+  if (send_err) std::rethrow_exception(send_err);
+  res.send_cpu_s_per_gib = send_cpu_total / (static_cast<double>(obj) * c.reads / (1 << 30));
+  return res;
+}
+
+}  // namespace gcsb

@@ -121,6 +121,7 @@ class GpuSink : public Sink {
     uint64_t obj_off = 0;
     std::vector<SegInfo> segs;
     hipStream_t st = nullptr;     // device pool stream: this slot's copy, CRC launch and event, in order
+    int st_idx = -1;              // its index in the pool (-1: private stream)
     hipEvent_t ev = nullptr;      // slot done: copy landed + CRC kernel finished
     uint32_t* tiles = nullptr;    // this slot's CRC tile scratch (slots on different streams run concurrently)
     bool inflight = false;
@@ -201,6 +202,7 @@ class GpuByteSource : public ByteSource {
   size_t slot_bytes_;
   int nslots_;
   std::vector<hipStream_t> st_;  // per slot, from the device stream pool
+  std::vector<int> st_idx_;      // their pool indices (slow-call reports)
   hipStream_t own_stream_ = nullptr;
   std::vector<uint8_t*> host_;
   std::vector<hipEvent_t> ev_;
@@ -254,5 +256,42 @@ int gpu_device_count();
 // CPU set of the per-device submitter threads (slot H2D copy + CRC launch
 // hand-off); empty = inherit.  Also GCSB_SUBMIT_CPUS=<cpulist>.
 void set_submitter_cpus(const std::vector<int>& cpus);
+
+// HIP calls on the slot hand-off / staging path that blocked the calling
+// thread (an async copy, launch or event record should return in
+// microseconds).  Process-wide; the bench reports them per timed block.
+struct SlowHipCalls {
+  uint64_t calls = 0;        // hand-off HIP calls timed
+  uint64_t slow = 0;         // of them >= the threshold (1 ms)
+  double slow_ms_total = 0;
+  double max_ms = 0;
+  std::string max_call;      // e.g. "hipMemcpyAsync(H2D) stream 3"
+};
+SlowHipCalls slow_hip_calls();
+void reset_slow_hip_calls();
+// Issue one tiny async copy on every pool stream of `device` and wait for
+// it: the first command on a stream binds its hardware queue lazily, so
+// doing it at sink / source construction keeps that cost out of the reads.
+void warm_device_streams(int device);
+
+// Pinned <-> HBM copy ceiling in the data plane's own pattern: `total` bytes
+// in `chunk`-sized hipMemcpyAsync copies between a ring of `slots` pinned
+// chunks (PinnedPool: THP + hipHostRegister, as the sinks' rings) and one HBM
+// buffer, round-robin over `streams` pool streams, at most `slots` copies in
+// flight (a slot is reused once its event fired).  One untimed pass, then
+// `iters` timed passes; GB/s = 1e9 B/s over the timed passes.
+struct CopyCeiling {
+  double gbps = 0;
+  double pass_ms_p50 = 0;
+};
+// SDMA copy engines (gpu/copy_engines.hip): bring every engine of `device`
+// up once with a tiny copy per engine and direction (a cold engine costs the
+// first hipMemcpyAsync landing on it ~7 ms); returns the engine/direction
+// pairs warmed, 0 if already done, -1 if the HSA agent was not found.
+int warm_copy_engines(int device);
+// JSON: engine count, availability masks, per-engine first / second /
+// after-hipDeviceSynchronize copy times per direction.
+std::string copy_engine_probe(int device);
+CopyCeiling copy_ceiling(int device, bool h2d, size_t total, size_t chunk, int slots, int streams, int iters);
 
 }  // namespace gcsb

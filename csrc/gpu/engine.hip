@@ -262,6 +262,36 @@ void set_submitter_cpus(const std::vector<int>& cpus) {
   g_submit_cpus_set = true;
 }
 
+namespace {
+std::mutex g_slow_mu;
+SlowHipCalls g_slow;
+constexpr int64_t kSlowCallNs = 1000000;
+
+// Records one hand-off HIP call that ran [t0, t1) on the calling thread.
+void note_hip_call(const char* what, int stream_idx, int64_t t0, int64_t t1) {
+  const int64_t d = t1 - t0;
+  std::lock_guard<std::mutex> lk(g_slow_mu);
+  ++g_slow.calls;
+  if (d < kSlowCallNs) return;
+  ++g_slow.slow;
+  g_slow.slow_ms_total += d / 1e6;
+  if (d / 1e6 > g_slow.max_ms) {
+    g_slow.max_ms = d / 1e6;
+    g_slow.max_call = std::string(what) + " stream " + std::to_string(stream_idx);
+  }
+}
+}  // namespace
+
+SlowHipCalls slow_hip_calls() {
+  std::lock_guard<std::mutex> lk(g_slow_mu);
+  return g_slow;
+}
+
+void reset_slow_hip_calls() {
+  std::lock_guard<std::mutex> lk(g_slow_mu);
+  g_slow = SlowHipCalls();
+}
+
 // Per-device stream pool shared by every sink / upload source (engine.h).
 class DeviceStreamPool {
  public:
@@ -275,6 +305,12 @@ class DeviceStreamPool {
   }
   hipStream_t at(unsigned i) const { return st_[i % st_.size()]; }
   unsigned next_base() { return rr_.fetch_add(1); }
+  size_t size() const { return st_.size(); }
+  int index_of(hipStream_t s) const {
+    for (size_t i = 0; i < st_.size(); ++i)
+      if (st_[i] == s) return static_cast<int>(i);
+    return -1;
+  }
   // GCSB_STREAMS=0: no pool, every sink / source owns one private stream
   // (A/B switch against the shared pool).
   bool private_streams() const { return st_.empty(); }
@@ -287,12 +323,96 @@ class DeviceStreamPool {
     int n = 8;
     if (const char* e = std::getenv("GCSB_STREAMS")) n = std::max(0, std::min(32, std::atoi(e)));
     ensure_device(dev);
+    // every SDMA engine up before the first read / upload can land on a cold
+    // one (gpu/copy_engines.hip); GCSB_WARM_ENGINES=0 leaves them lazy (A/B)
+    if (env_flag("GCSB_WARM_ENGINES", true)) (void)warm_copy_engines(dev);
     st_.resize(static_cast<size_t>(n));
     for (auto& st : st_) hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate(pool)");
   }
   std::vector<hipStream_t> st_;
   std::atomic<unsigned> rr_{0};
 };
+
+void warm_device_streams(int device) {
+  ensure_device(device);
+  DeviceStreamPool& pool = DeviceStreamPool::get(device);
+  static std::mutex mu;
+  static std::map<int, std::pair<uint8_t*, uint8_t*>> bufs;  // per device: pinned host, HBM scratch
+  std::lock_guard<std::mutex> lk(mu);
+  auto& b = bufs[device];
+  if (!b.first) {
+    hip_check(hipHostMalloc(reinterpret_cast<void**>(&b.first), 8192, hipHostMallocDefault), "hipHostMalloc(warm)");
+    hip_check(hipMalloc(reinterpret_cast<void**>(&b.second), 8192), "hipMalloc(warm)");
+  }
+  for (size_t i = 0; i < pool.size(); ++i) {
+    hipStream_t st = pool.at(static_cast<unsigned>(i));
+    const int64_t t0 = now_ns();
+    hip_check(hipMemcpyAsync(b.second, b.first, 4096, hipMemcpyHostToDevice, st), "hipMemcpyAsync(warm H2D)");
+    const int64_t t1 = now_ns();
+    note_hip_call("warm hipMemcpyAsync(H2D)", static_cast<int>(i), t0, t1);
+    hip_check(hipMemcpyAsync(b.first + 4096, b.second, 4096, hipMemcpyDeviceToHost, st), "hipMemcpyAsync(warm D2H)");
+    note_hip_call("warm hipMemcpyAsync(D2H)", static_cast<int>(i), t1, now_ns());
+  }
+  for (size_t i = 0; i < pool.size(); ++i)
+    hip_check(hipStreamSynchronize(pool.at(static_cast<unsigned>(i))), "hipStreamSynchronize(warm)");
+}
+
+CopyCeiling copy_ceiling(int device, bool h2d, size_t total, size_t chunk, int slots, int streams, int iters) {
+  ensure_device(device);
+  if (chunk == 0 || total == 0 || slots < 1 || iters < 1) throw std::invalid_argument("copy_ceiling: bad geometry");
+  DeviceStreamPool& pool = DeviceStreamPool::get(device);
+  const unsigned nst = static_cast<unsigned>(std::max(1, std::min(streams, std::max(1, static_cast<int>(pool.size())))));
+  std::vector<uint8_t*> host(slots);
+  std::vector<hipEvent_t> ev(slots, nullptr);
+  std::vector<bool> busy(slots, false);
+  uint8_t* dev = nullptr;
+  hip_check(hipMalloc(reinterpret_cast<void**>(&dev), total), "hipMalloc(copy ceiling)");
+  for (int i = 0; i < slots; ++i) {
+    host[i] = static_cast<uint8_t*>(PinnedPool::get(chunk));
+    hip_check(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming), "hipEventCreate");
+  }
+  hipStream_t priv = nullptr;
+  if (pool.private_streams()) hip_check(hipStreamCreateWithFlags(&priv, hipStreamNonBlocking), "hipStreamCreate");
+  std::vector<double> pass_ms;
+  double timed_s = 0;
+  for (int it = 0; it <= iters; ++it) {
+    const int64_t t0 = now_ns();
+    size_t k = 0;
+    for (size_t off = 0; off < total; off += chunk, ++k) {
+      const int i = static_cast<int>(k % static_cast<size_t>(slots));
+      if (busy[i]) hip_check(hipEventSynchronize(ev[i]), "hipEventSynchronize");
+      hipStream_t st = priv ? priv : pool.at(static_cast<unsigned>(k) % nst);
+      const size_t n = std::min(chunk, total - off);
+      if (h2d)
+        hip_check(hipMemcpyAsync(dev + off, host[i], n, hipMemcpyHostToDevice, st), "hipMemcpyAsync(H2D)");
+      else
+        hip_check(hipMemcpyAsync(host[i], dev + off, n, hipMemcpyDeviceToHost, st), "hipMemcpyAsync(D2H)");
+      hip_check(hipEventRecord(ev[i], st), "hipEventRecord");
+      busy[i] = true;
+    }
+    for (int i = 0; i < slots; ++i)
+      if (busy[i]) {
+        hip_check(hipEventSynchronize(ev[i]), "hipEventSynchronize");
+        busy[i] = false;
+      }
+    const double s = (now_ns() - t0) / 1e9;
+    if (it > 0) {  // pass 0 is the untimed warm-up
+      timed_s += s;
+      pass_ms.push_back(s * 1e3);
+    }
+  }
+  for (int i = 0; i < slots; ++i) {
+    PinnedPool::put(host[i], chunk);
+    (void)hipEventDestroy(ev[i]);
+  }
+  (void)hipFree(dev);
+  if (priv) (void)hipStreamDestroy(priv);
+  std::sort(pass_ms.begin(), pass_ms.end());
+  CopyCeiling r;
+  r.gbps = static_cast<double>(total) * iters / timed_s / 1e9;
+  r.pass_ms_p50 = pass_ms[pass_ms.size() / 2];
+  return r;
+}
 
 void GpuSink::set_device() const { ensure_device(cfg_.device); }
 
@@ -336,10 +456,12 @@ GpuSink::GpuSink(const GpuSinkConfig& cfg) : cfg_(cfg) {
     const unsigned evf = hipEventDisableTiming | (cfg_.blocking_sync ? hipEventBlockingSync : 0u);
     hip_check(hipEventCreateWithFlags(&s.ev, evf), "hipEventCreate");
     s.st = own_stream_ ? own_stream_ : pool.at(base + static_cast<unsigned>(i) % nst);
+    s.st_idx = own_stream_ ? -1 : pool.index_of(s.st);
     s.tiles = d_tiles_ + crc_scratch_words(tiles_cap_) * static_cast<size_t>(i);
     s.res = res_host_ + static_cast<size_t>(i) * kMaxSeg;
     hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&s.d_res), s.res, 0), "hipHostGetDevicePointer");
   }
+  if (env_flag("GCSB_WARM_STREAMS", false)) warm_device_streams(cfg_.device);
 }
 
 GpuSink::~GpuSink() {
@@ -575,9 +697,17 @@ void GpuSink::enqueue_slot(Slot& s, uint8_t* dst, const CrcBatch* batch) {
   auto issue = [this, &s, dst](const CrcBatch* b) {
     ensure_device(cfg_.device);
     // copy, CRC and completion event in one stream's order: no cross-stream wait
+    const int64_t t0 = now_ns();
     hip_check(hipMemcpyAsync(dst, s.host, s.used, hipMemcpyHostToDevice, s.st), "hipMemcpyAsync(H2D)");
-    if (b) launch_crc32c_batch(*b, d_tables_, s.tiles, s.d_res, s.st);
+    const int64_t t1 = now_ns();
+    note_hip_call("hipMemcpyAsync(H2D)", s.st_idx, t0, t1);
+    if (b) {
+      launch_crc32c_batch(*b, d_tables_, s.tiles, s.d_res, s.st);
+      note_hip_call("crc launch", s.st_idx, t1, now_ns());
+    }
+    const int64_t t2 = now_ns();
     hip_check(hipEventRecord(s.ev, s.st), "hipEventRecord");
+    note_hip_call("hipEventRecord", s.st_idx, t2, now_ns());
   };
   if (!cfg_.async_submit) {
     s.submitted = true;
@@ -745,8 +875,11 @@ GpuByteSource::GpuByteSource(int device, const void* dptr, uint64_t n, size_t sl
   if (pool.private_streams())
     hip_check(hipStreamCreateWithFlags(&own_stream_, hipStreamNonBlocking), "hipStreamCreate");
   st_.resize(nslots_);
-  for (int i = 0; i < nslots_; ++i)
+  st_idx_.assign(nslots_, -1);
+  for (int i = 0; i < nslots_; ++i) {
     st_[i] = own_stream_ ? own_stream_ : pool.at(base + static_cast<unsigned>(i) % nst);
+    if (!own_stream_) st_idx_[i] = pool.index_of(st_[i]);
+  }
   host_.resize(nslots_);
   ev_.resize(nslots_);
   slot_off_.assign(nslots_, ~0ull);
@@ -813,10 +946,12 @@ void GpuByteSource::issue(int slot, uint64_t off) {
   size_t len = static_cast<size_t>(std::min<uint64_t>(slot_bytes_, n_ - off));
   slot_off_[slot] = off;
   slot_len_[slot] = len;
-  const int64_t t0 = trace ? now_ns() : 0;
+  const int64_t t0 = now_ns();
   hip_check(hipMemcpyAsync(host_[slot], src_ + off, len, hipMemcpyDeviceToHost, st_[slot]), "hipMemcpyAsync(D2H)");
-  const int64_t t1 = trace ? now_ns() : 0;
+  const int64_t t1 = now_ns();
+  note_hip_call("hipMemcpyAsync(D2H)", st_idx_[slot], t0, t1);
   hip_check(hipEventRecord(ev_[slot], st_[slot]), "hipEventRecord");
+  note_hip_call("hipEventRecord(D2H)", st_idx_[slot], t1, now_ns());
   if (trace && now_ns() - t0 > 200000)
     std::fprintf(stderr, "GpuByteSource: slow issue slot %d stream %p: copy %.3f ms, event %.3f ms\n", slot,
                  static_cast<void*>(st_[slot]), (t1 - t0) / 1e6, (now_ns() - t1) / 1e6);

@@ -8,6 +8,7 @@
 
 #include "bench/runner.h"
 #include "core/affinity.h"
+#include "core/ceiling.h"
 #include "core/content.h"
 #include "core/crc32c.h"
 #include "core/util.h"
@@ -499,6 +500,7 @@ class PyRunner {
     d["steady_p50_ms"] = s.steady_p50_ms;
     d["steady_p99_ms"] = s.steady_p99_ms;
     d["slice_skew_ms"] = s.slice_skew_ms;
+    d["slowest"] = s.slowest;
     py::list b;
     for (int i = 0; i < kOcBuckets; ++i) b.append(s.oc_buckets[i]);
     d["oc_buckets"] = b;
@@ -808,6 +810,66 @@ PYBIND11_MODULE(_native, m) {
   m.def("recv_stats", [] {
     RecvStats r = recv_stats();
     return py::make_tuple(r.calls, r.bytes);
+  });
+  m.def("slow_hip_calls", [] {
+    SlowHipCalls s = slow_hip_calls();
+    py::dict d;
+    d["calls"] = s.calls;
+    d["slow"] = s.slow;
+    d["slow_ms_total"] = s.slow_ms_total;
+    d["max_ms"] = s.max_ms;
+    d["max_call"] = s.max_call;
+    return d;
+  });
+  m.def("reset_slow_hip_calls", &reset_slow_hip_calls);
+  m.def("copy_ceiling", [](int dev, const std::string& dir, size_t total, size_t chunk, int slots, int streams,
+                           int iters) {
+    CopyCeiling c;
+    {
+      py::gil_scoped_release nogil;
+      c = copy_ceiling(dev, dir == "h2d", total, chunk, slots, streams, iters);
+    }
+    py::dict d;
+    d["gbps"] = c.gbps;
+    d["pass_ms_p50"] = c.pass_ms_p50;
+    return d;
+  }, py::arg("device"), py::arg("dir") = "h2d", py::arg("total") = size_t(256) << 20, py::arg("chunk") = size_t(2) << 20,
+     py::arg("slots") = 8, py::arg("streams") = 8, py::arg("iters") = 5);
+  m.def("loopback_ceiling", [](const py::dict& d) {
+    CeilingConfig c;
+    c.object_bytes = get_or<size_t>(d, "object_bytes", c.object_bytes);
+    c.reads = get_or<int>(d, "reads", c.reads);
+    c.ring_bytes = get_or<size_t>(d, "ring_bytes", c.ring_bytes);
+    c.recv_chunk = get_or<size_t>(d, "recv_chunk", c.recv_chunk);
+    c.rcvbuf = get_or<int>(d, "rcvbuf", 0);
+    c.zerocopy_send = get_or<bool>(d, "zerocopy_send", true);
+    c.ring_pages = get_or<int>(d, "ring_pages", 1);
+    if (d.contains("send_cpus")) c.send_cpus = d["send_cpus"].cast<std::vector<int>>();
+    if (d.contains("recv_cpus")) c.recv_cpus = d["recv_cpus"].cast<std::vector<int>>();
+    const std::string mode = get_or<std::string>(d, "mode", "tcp");
+    CeilingResult r;
+    {
+      py::gil_scoped_release nogil;
+      r = mode == "memcpy" ? memcpy_ceiling(c) : tcp_ceiling(c);
+    }
+    py::dict o;
+    o["gbps"] = r.gbps;
+    o["p50_ms"] = r.p50_ms;
+    o["recv_cpu_s_per_gib"] = r.recv_cpu_s_per_gib;
+    o["send_cpu_s_per_gib"] = r.send_cpu_s_per_gib;
+    return o;
+  });
+  m.def("warm_copy_engines", [](int dev) {
+    py::gil_scoped_release nogil;
+    return warm_copy_engines(dev);
+  });
+  m.def("copy_engine_probe", [](int dev) {
+    py::gil_scoped_release nogil;
+    return copy_engine_probe(dev);
+  });
+  m.def("warm_device_streams", [](int dev) {
+    py::gil_scoped_release nogil;
+    warm_device_streams(dev);
   });
   m.def("numa_nodes_of", [](uintptr_t p, size_t n) { return numa_nodes_of(reinterpret_cast<const void*>(p), n); });
   m.def("pattern_memfd_numa", [] { return PatternBuffer::instance().memfd_numa(); });

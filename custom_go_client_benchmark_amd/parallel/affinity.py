@@ -183,6 +183,7 @@ def plan(device: int, mode: str = "split", slot: int = 0) -> dict:
                    node L3 domains / GPUs on the node -- shared by client and
                    endpoint threads: all 8 domains on a 1-GPU box, 2 per rank
                    on a full 8-GPU node; best for sliced reads),
+          "share_quota" (share, trimmed to the rank's CPU-quota budget),
           "split" (client and endpoint on two L3 domains of the GPU's node),
           "same" (one shared L3 domain), "numa" (whole node), "none".
     """
@@ -214,12 +215,18 @@ def plan(device: int, mode: str = "split", slot: int = 0) -> dict:
     # slot: this rank's index among ranks sharing ONE GPU (shared-GPU
     # rehearsals only; 0 on a node with a GPU per rank) -> the next L3 domains
     base = (k * share + slot) % max(1, len(groups))
-    if mode == "share":
+    if mode in ("share", "share_quota"):
         # not trimmed to the quota: a handful of busy threads (one stream per
         # read, or 8 sliced streams) did better spread over the share's 64
         # CPUs than packed onto 16 cores (sliced 32-34k vs 40-43k MiB/s,
-        # profiles/r2_quota); quota packing pays off with many threads
+        # profiles/r2_quota); quota packing pays off with many threads.
+        # share_quota: the share trimmed to this rank's quota budget (one
+        # hardware thread per physical core first) -- many workers per rank
+        # (the reference's 48) without the 8 ranks of a node piling onto the
+        # same first cores as plain "quota" would
         mine = [c for g in groups[base:base + share] for c in g] or cpus
+        if mode == "share_quota":
+            mine = trim_to_quota(mine)
         return {"client": mine, "server": mine, "mode": mode, "numa_node": node, "gpu_index_on_node": k,
                 "l3_domains": share}
     if mode == "pair":

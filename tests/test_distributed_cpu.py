@@ -57,6 +57,15 @@ def test_bench_two_ranks_gloo():
     for p in ("grpc", "http"):
         b = out[f"list_read_{p}"]
         assert b["ok"] and b["objects"] == 1000 and b["workers"] == 8 and b["mib_s"] > 0 and b["list_ms"] > 0
+    # the reference's default experiment: 48 workers, 1 MiB, gRPC pool 1 vs HTTP, on both ranks
+    for p in ("grpc", "http"):
+        b = out[f"ref_default_{p}"]
+        assert b["ok"] and b["workers"] == 48 and b["reads_per_worker"] == 50 and b["mib_s"] > 0, b
+        assert b["first_read_p50_ms"] > 0 and b["p99_ms"] >= b["p50_ms"] > 0
+    assert out["ref_default_grpc"]["grpc_conn_pool_size"] == 1
+    # same-box bounds in the headline's placement (no GPU here: no h2d)
+    c = out["ceiling"]
+    assert c["ok"] and c["tcp_gbps"] > 0 and c["memcpy_gbps"] > 0 and c["headline_frac_of_ceiling"] > 0, c
 
 
 def _bench_env():

@@ -453,6 +453,7 @@ def run_rank(args) -> int:
         gdist.barrier(ctx, "R1 write start barrier")
         sync()
         n.reset_slow_hip_calls()
+        th0 = cpuacct.thread_cpu()
         t1 = time.perf_counter()
         nbytes = 0
         if not err:
@@ -472,6 +473,11 @@ def run_rank(args) -> int:
         sync()
         gdist.barrier(ctx, "R2 write stop barrier")
         e1 = time.perf_counter() - t1
+        # where an upload's CPU goes: the sending (Python main) thread and the
+        # client's connection reader vs the endpoint's receive and CRC threads
+        by_name = {k: v - th0.get(k, 0.0) for k, v in cpuacct.thread_cpu().items()}
+        cpu_split = {k: round(v / max(nbytes, 1) * (1 << 30), 4) for k, v in sorted(by_name.items())
+                     if v > 0.0005 and nbytes}
         s = sorted(lat)
         p50 = s[len(s) * 50 // 100] if s else 0.0
         p99 = s[min(len(s) - 1, len(s) * 99 // 100)] if s else 0.0
@@ -484,6 +490,7 @@ def run_rank(args) -> int:
         # this rank's slowest uploads (index in the timed run, ms): where the tail sits
         st["slowest"] = [[i, round(v, 2)] for i, v in sorted(enumerate(lat), key=lambda x: -x[1])[:3]]
         st["slow_hip"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in n.slow_hip_calls().items()}
+        st["cpu_s_per_gib_by_thread"] = cpu_split
         return st
 
     def fanout_block(steps: int, warmup: int) -> dict:
@@ -715,6 +722,18 @@ def run_rank(args) -> int:
     other = {"grpc": "http", "http": "grpc"}.get(protocol)
     blocks = {}
     if side_steps > 0 and args.workload == "read":
+        if use_gpu and args.baseline == "on":
+            # right after the headline (the boxes drift over a run): the
+            # reference's semantics on the headline config -- same endpoint,
+            # placement, object and steps; bytes to a discard sink, CRC32C of
+            # every byte on the host (the Go library's reader,
+            # /root/reference/main.go:133-146).  vs_baseline divides by it.
+            for p in [protocol] + ([other] if other and other in hbm.available_protocols() else []):
+                key = "cpu_baseline" if p == protocol else f"cpu_baseline_{p}"
+                blocks[key] = (key, read_block({"protocol": p, "sink": "discard", "host_crc": True}, side_steps,
+                                               side_warm, f"{p} cpu baseline"),
+                               {"protocol": p, "sink": "discard", "host_crc": True,
+                                "note": "reference semantics: io.Discard + host CRC32C"})
         if other and other in hbm.available_protocols():
             blocks["compare"] = ("compare", read_block({"protocol": other}, side_steps, side_warm, f"{other} compare"),
                                  {"protocol": other})
@@ -728,17 +747,6 @@ def run_rank(args) -> int:
                                 {"streams_per_read": args.sliced_streams,
                                  "ring": f"{args.sliced_slots}x{args.sliced_slot_bytes}", "affinity": "share",
                                  "piece_bytes": parse_size(args.piece_bytes), "note": "extension, not parity"})
-        if use_gpu and args.baseline == "on":
-            # the reference's semantics on the headline config: same endpoint,
-            # placement, object and steps; bytes to a discard sink, CRC32C of
-            # every byte on the host (the Go library's reader,
-            # /root/reference/main.go:133-146) -- what vs_baseline divides by
-            for p in [protocol] + ([other] if other and other in hbm.available_protocols() else []):
-                key = "cpu_baseline" if p == protocol else f"cpu_baseline_{p}"
-                blocks[key] = (key, read_block({"protocol": p, "sink": "discard", "host_crc": True}, side_steps,
-                                               side_warm, f"{p} cpu baseline"),
-                               {"protocol": p, "sink": "discard", "host_crc": True,
-                                "note": "reference semantics: io.Discard + host CRC32C"})
         if args.ceiling == "on":
             blocks["ceiling"] = ("ceiling", ceiling_block(mib_s(head) / max(1, world)), None)
         if args.ref_workers > 0:
@@ -852,6 +860,7 @@ def run_rank(args) -> int:
                                                   for c in slots]
             if args.workload == "write":
                 out["rank0_slowest"] = head.get("slowest", [])
+                out["cpu_s_per_gib_by_thread"] = head.get("cpu_s_per_gib_by_thread", {})
             if args.workload == "read":
                 # where a read's time goes: request -> first byte (TTFB), -> last
                 # byte in host memory (host_landed), -> last byte + CRC in HBM (p50)
@@ -890,6 +899,8 @@ def run_rank(args) -> int:
                     b["rank0_slowest"] = st["slowest"]
                 if st.get("slow_hip", {}).get("slow"):
                     b["slow_hip_calls"] = st["slow_hip"]
+                if st.get("cpu_s_per_gib_by_thread"):
+                    b["cpu_s_per_gib_by_thread"] = st["cpu_s_per_gib_by_thread"]
                 if key.startswith("list_read_"):
                     b["list_ms"] = round(st["list_ms_max"], 3)
                 if key == "sliced":

@@ -122,10 +122,24 @@ CeilingResult tcp_ceiling(const CeilingConfig& c) {
   if (mfd.fd < 0) fail("memfd_create");
   if (ftruncate(mfd.fd, static_cast<off_t>(obj)) != 0) fail("ftruncate");
   {
-    std::vector<uint8_t> blk(1 << 20);
-    for (size_t i = 0; i < blk.size(); ++i) blk[i] = static_cast<uint8_t>(i * 131 + 7);
-    for (size_t off = 0; off < obj; off += blk.size())
-      if (pwrite(mfd.fd, blk.data(), std::min(blk.size(), obj - off), static_cast<off_t>(off)) < 0) fail("pwrite");
+    // the object's page cache on the sender's NUMA node, as the endpoint's
+    // memfd (server/fakegcs.cc): the receiver's copy reads these pages, and
+    // pages on the far socket cost it up to 2x per byte (profiles/r2_numa)
+    std::exception_ptr fill_err;
+    std::thread filler([&] {
+      try {
+        pin_current_thread(c.send_cpus);
+        std::vector<uint8_t> blk(1 << 20);
+        for (size_t i = 0; i < blk.size(); ++i) blk[i] = static_cast<uint8_t>(i * 131 + 7);
+        for (size_t off = 0; off < obj; off += blk.size())
+          if (pwrite(mfd.fd, blk.data(), std::min(blk.size(), obj - off), static_cast<off_t>(off)) < 0)
+            fail("pwrite");
+      } catch (...) {
+        fill_err = std::current_exception();
+      }
+    });
+    filler.join();
+    if (fill_err) std::rethrow_exception(fill_err);
   }
   Fd ls(socket(AF_INET, SOCK_STREAM, 0));
   sockaddr_in a{};

@@ -2,6 +2,7 @@
 #include "gpu/engine.h"
 
 #include <algorithm>
+#include <cctype>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -84,12 +85,38 @@ PinKind pin_kind() {
   return k;
 }
 
+// NUMA node of a HIP device's PCIe root (sysfs), -1 if unknown; cached.
+int device_numa_node(int dev) {
+  static std::mutex mu;
+  static std::map<int, int> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(dev);
+  if (it != cache.end()) return it->second;
+  int node = -1;
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof(bus), dev) == hipSuccess) {
+    for (char* c = bus; *c; ++c) *c = static_cast<char>(std::tolower(static_cast<unsigned char>(*c)));
+    if (FILE* f = std::fopen((std::string("/sys/bus/pci/devices/") + bus + "/numa_node").c_str(), "r")) {
+      if (std::fscanf(f, "%d", &node) != 1) node = -1;
+      std::fclose(f);
+    }
+  } else {
+    (void)hipGetLastError();
+  }
+  cache[dev] = node;
+  return node;
+}
+
 class PinnedPool {
  public:
-  static void* get(size_t n) {
+  // n bytes of page-locked memory whose pages sit on NUMA node `node` (the
+  // GPU's, which its SDMA engines read / write and its rank's pinned threads
+  // run on), -1 = the calling thread's node.  Recycled by (node, size).
+  static void* get(size_t n, int node) {
+    if (node < 0) node = current_numa_node();
     {
       std::lock_guard<std::mutex> lk(mu());
-      auto it = free_list().find(n);
+      auto it = free_list().find({node, n});
       if (it != free_list().end()) {
         void* p = it->second;
         free_list().erase(it);
@@ -112,12 +139,11 @@ class PinnedPool {
         if (huge - head) ::munmap(reinterpret_cast<void*>(a + len), huge - head);
         void* p = reinterpret_cast<void*>(a);
         (void)madvise(p, len, MADV_HUGEPAGE);
-        // the calling (pinned, GPU-local) thread's node, strictly
-        (void)bind_range_to_node(p, len, current_numa_node());
+        (void)bind_range_to_node(p, len, node);  // strictly, whichever thread faults it in
         std::memset(p, 0, len);  // fault in now
         if (hipHostRegister(p, len, hipHostRegisterDefault) == hipSuccess) {
           std::lock_guard<std::mutex> lk(mu());
-          registered()[p] = len;
+          registered()[p] = {len, node};
           return p;
         }
         (void)hipGetLastError();
@@ -126,6 +152,10 @@ class PinnedPool {
     }
     void* p = nullptr;
     hip_check(hipHostMalloc(&p, n, hipHostMallocNumaUser), "hipHostMalloc(staging)");
+    {
+      std::lock_guard<std::mutex> lk(mu());
+      malloced()[p] = node;
+    }
     return p;
   }
   static void put(void* p, size_t n) {
@@ -133,16 +163,18 @@ class PinnedPool {
     size_t reg_len = 0;
     {
       std::lock_guard<std::mutex> lk(mu());
+      auto it = registered().find(p);
+      const int node = it != registered().end() ? it->second.second : malloced()[p];
       if (held() + n <= kMaxHeld) {
-        free_list().emplace(n, p);
+        free_list().emplace(std::make_pair(node, n), p);
         held() += n;
         return;
       }
-      auto it = registered().find(p);
       if (it != registered().end()) {
-        reg_len = it->second;
+        reg_len = it->second.first;
         registered().erase(it);
       }
+      malloced().erase(p);
     }
     if (reg_len) {
       (void)hipHostUnregister(p);
@@ -154,16 +186,20 @@ class PinnedPool {
 
  private:
   static constexpr size_t kMaxHeld = size_t(1) << 30;
-  static std::map<void*, size_t>& registered() {
-    static std::map<void*, size_t> r;
+  static std::map<void*, std::pair<size_t, int>>& registered() {  // THP ring: length, node
+    static std::map<void*, std::pair<size_t, int>> r;
     return r;
+  }
+  static std::map<void*, int>& malloced() {  // hipHostMalloc fallback: node asked for
+    static std::map<void*, int> m;
+    return m;
   }
   static std::mutex& mu() {
     static std::mutex m;
     return m;
   }
-  static std::multimap<size_t, void*>& free_list() {
-    static std::multimap<size_t, void*> f;
+  static std::multimap<std::pair<int, size_t>, void*>& free_list() {
+    static std::multimap<std::pair<int, size_t>, void*> f;
     return f;
   }
   static size_t& held() {
@@ -368,7 +404,7 @@ CopyCeiling copy_ceiling(int device, bool h2d, size_t total, size_t chunk, int s
   uint8_t* dev = nullptr;
   hip_check(hipMalloc(reinterpret_cast<void**>(&dev), total), "hipMalloc(copy ceiling)");
   for (int i = 0; i < slots; ++i) {
-    host[i] = static_cast<uint8_t*>(PinnedPool::get(chunk));
+    host[i] = static_cast<uint8_t*>(PinnedPool::get(chunk, device_numa_node(device)));
     hip_check(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming), "hipEventCreate");
   }
   hipStream_t priv = nullptr;
@@ -448,9 +484,8 @@ GpuSink::GpuSink(const GpuSinkConfig& cfg) : cfg_(cfg) {
   slots_.resize(cfg_.slots);
   for (int i = 0; i < cfg_.slots; ++i) {
     Slot& s = slots_[i];
-    // NumaUser: follow the calling (pinned) thread's NUMA policy, i.e. the
-    // GPU-local node chosen by the rank's CPU plan
-    s.host = static_cast<uint8_t*>(PinnedPool::get(cfg_.slot_bytes));
+    // on the GPU's NUMA node (the rank's pinned receive thread runs there too)
+    s.host = static_cast<uint8_t*>(PinnedPool::get(cfg_.slot_bytes, device_numa_node(cfg_.device)));
     if (cfg_.landing == Landing::kRing)
       hip_check(hipMalloc(reinterpret_cast<void**>(&s.dev_ring), cfg_.slot_bytes), "hipMalloc(ring slot)");
     const unsigned evf = hipEventDisableTiming | (cfg_.blocking_sync ? hipEventBlockingSync : 0u);
@@ -885,7 +920,7 @@ GpuByteSource::GpuByteSource(int device, const void* dptr, uint64_t n, size_t sl
   slot_off_.assign(nslots_, ~0ull);
   slot_len_.assign(nslots_, 0);
   for (int i = 0; i < nslots_; ++i) {
-    host_[i] = static_cast<uint8_t*>(PinnedPool::get(slot_bytes_));
+    host_[i] = static_cast<uint8_t*>(PinnedPool::get(slot_bytes_, device_numa_node(device_)));
     hip_check(hipEventCreateWithFlags(&ev_[i], hipEventDisableTiming), "hipEventCreate");
   }
   tp[1] = now_ns();

@@ -3,7 +3,9 @@
 #include <sys/socket.h>
 #include <sys/uio.h>
 
+#include <chrono>
 #include <cstring>
+#include <thread>
 
 #include "core/affinity.h"
 #include "core/util.h"
@@ -60,10 +62,41 @@ size_t H2ClientConn::active_streams() {
   return streams_.size();
 }
 
-std::shared_ptr<H2ClientStream> H2ClientConn::find(uint32_t id) {
+std::shared_ptr<H2ClientStream> H2ClientConn::acquire(uint32_t id) {
   std::lock_guard<std::mutex> lk(mu_);
   auto it = streams_.find(id);
-  return it == streams_.end() ? nullptr : it->second;
+  if (it == streams_.end()) return nullptr;
+  it->second->busy_.fetch_add(1, std::memory_order_relaxed);
+  return it->second;
+}
+
+bool H2ClientConn::cancel_stream(H2ClientStream& s, int wait_ms) {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (s.id_ == 0 || s.cancelled_) return true;
+    streams_.erase(s.id_);
+    s.cancelled_ = true;
+  }
+  // no dispatch into s can start now; wait out one that already has
+  const int64_t deadline = now_ns() + static_cast<int64_t>(std::max(wait_ms, 1)) * 1000000;
+  while (s.busy_.load(std::memory_order_acquire) > 0) {
+    if (now_ns() > deadline) return false;
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+  w_->unregister_stream(s.id_);
+  if (usable()) {
+    try {
+      w_->write_rst(s.id_, h2::kErrCancel);
+    } catch (...) {
+    }
+  }
+  return true;
+}
+
+void H2ClientConn::abandon_stream(H2ClientStream& s, int idle_ms) {
+  const int64_t quiet_ns = now_ns() - last_frame_ns_.load(std::memory_order_relaxed);
+  if (usable() && quiet_ns < static_cast<int64_t>(idle_ms) * 1000000 && cancel_stream(s, idle_ms)) return;
+  close();
 }
 
 void H2ClientConn::start_stream(const std::shared_ptr<H2ClientStream>& s, const HeaderList& headers,
@@ -159,7 +192,7 @@ void H2ClientConn::send_data_iov(H2ClientStream& s, struct iovec* iov, int cnt, 
 }
 
 void H2ClientConn::end_stream(H2ClientStream& s, bool reset) {
-  if (s.id_ == 0) return;
+  if (s.id_ == 0 || s.cancelled_) return;
   {
     std::lock_guard<std::mutex> lk(mu_);
     streams_.erase(s.id_);
@@ -195,6 +228,7 @@ void H2ClientConn::reader_loop() {
   try {
     for (;;) {
       FrameHeader fh = read_frame_header(*bc_);
+      last_frame_ns_.store(now_ns(), std::memory_order_relaxed);
       if (fh.length > opt_.max_frame_size) throw StorageError("http2: frame exceeds max_frame_size", true);
       switch (fh.type) {
         case h2::kData: {
@@ -207,12 +241,13 @@ void H2ClientConn::reader_loop() {
             if (static_cast<uint32_t>(pad) + 1 > n) throw StorageError("http2: DATA padding exceeds frame", false);
             n -= 1 + pad;
           }
-          auto s = find(fh.stream);
+          auto s = acquire(fh.stream);
           bool end = fh.flags & h2::kFlagEndStream;
           if (s) {
             s->progress_.fetch_add(1, std::memory_order_relaxed);
             s->on_data(*bc_, n, end);
             s->progress_.fetch_add(1, std::memory_order_relaxed);
+            release(*s);
           } else {
             bc_->skip(n);
           }
@@ -246,9 +281,10 @@ void H2ClientConn::reader_loop() {
           if (fh.flags & h2::kFlagEndHeaders) {
             HeaderList hl;
             dec_.decode(reinterpret_cast<const uint8_t*>(hblock.data()), hblock.size(), &hl);
-            if (auto s = find(hstream)) {
+            if (auto s = acquire(hstream)) {
               s->progress_.fetch_add(1, std::memory_order_relaxed);
               s->on_headers(hl, hend_stream);
+              release(*s);
             }
           }
           break;
@@ -257,7 +293,10 @@ void H2ClientConn::reader_loop() {
           if (fh.length != 4) throw StorageError("http2: RST_STREAM length != 4", false);
           uint8_t v[4];
           bc_->read_exact(v, 4);
-          if (auto s = find(fh.stream)) s->on_reset(be32(v));
+          if (auto s = acquire(fh.stream)) {
+            s->on_reset(be32(v));
+            release(*s);
+          }
           break;
         }
         case h2::kSettings: {

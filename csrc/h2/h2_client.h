@@ -62,6 +62,10 @@ class H2ClientStream {
   friend class H2ClientConn;
   uint32_t id_ = 0;
   std::atomic<uint64_t> progress_{0};
+  // reader dispatches into this stream in flight (taken under the
+  // connection's stream-map lock, so none starts once the stream is erased)
+  std::atomic<int> busy_{0};
+  bool cancelled_ = false;  // cancel_stream() ran (owner thread only)
   RecvWindow recv_window_{16 << 20};
 };
 
@@ -89,6 +93,14 @@ class H2ClientConn {
   void send_data_iov(H2ClientStream& s, struct iovec* iov, int cnt, bool end_stream);
   // Forget a stream (RST_STREAM CANCEL if it is still open on our side).
   void end_stream(H2ClientStream& s, bool reset);
+  // -read-timeout hit on stream s (its waiter saw no frame for idle_ms).  If
+  // the connection itself carried frames within idle_ms, the silence is this
+  // stream's: cancel it alone (RST_STREAM, forget it, wait until the reader
+  // is outside any dispatch into it) and keep the connection for the other
+  // streams multiplexed on it.  If the connection is silent too, or the
+  // reader stays inside the stream's dispatch (blocked mid-frame), close the
+  // connection.  Either way nothing writes into s's sink afterwards.
+  void abandon_stream(H2ClientStream& s, int idle_ms);
   bool usable() const { return !dead_.load() && !goaway_.load(); }
   size_t active_streams();
   const Endpoint& endpoint() const { return ep_; }
@@ -98,7 +110,10 @@ class H2ClientConn {
   H2ClientConn(Endpoint ep, H2ClientOptions opt) : ep_(std::move(ep)), opt_(opt) {}
   void reader_loop();
   void fail_all(const std::string& msg);
-  std::shared_ptr<H2ClientStream> find(uint32_t id);
+  // the stream with this id, marked busy (release() after the dispatch)
+  std::shared_ptr<H2ClientStream> acquire(uint32_t id);
+  static void release(H2ClientStream& s) { s.busy_.fetch_sub(1, std::memory_order_release); }
+  bool cancel_stream(H2ClientStream& s, int wait_ms);
   Endpoint ep_;
   H2ClientOptions opt_;
   std::unique_ptr<BufferedConn> bc_;
@@ -114,6 +129,7 @@ class H2ClientConn {
   H2Settings peer_;
   RecvWindow conn_recv_{64 << 20};
   std::atomic<bool> dead_{false}, goaway_{false};
+  std::atomic<int64_t> last_frame_ns_{0};  // steady clock of the last frame header read
   uint32_t goaway_last_ = 0x7FFFFFFF;
   mutable std::mutex reason_mu_;
   std::string dead_reason_;  // guarded by reason_mu_ (written by the reader thread)

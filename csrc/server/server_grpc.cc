@@ -78,7 +78,26 @@ struct ServerStream {
   std::string write_msg;
   bool write_finished = false;
   bool write_first = true;
+  // offloaded WriteObject parsing (H2ServerConn::recv_write_data): the
+  // message being received, and messages queued to the connection's write
+  // worker and not yet processed (guarded by the connection's wmu_)
+  uint8_t wprefix[5] = {0, 0, 0, 0, 0};
+  uint32_t wprefix_have = 0, wmsg_len = 0, wmsg_have = 0;
+  std::unique_ptr<char[]> wmsg;
+  size_t wmsg_cap = 0;
+  int wpending = 0;
 };
+
+// WriteObject messages are CRC32C-checked off the connection's reader thread
+// (GCSB_SRV_WRITE_WORKER=0 keeps the round-2 inline path, A/B): the reader
+// only recv()s, so one upload stream is bound by one copy, not copy + CRC.
+bool write_worker_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("GCSB_SRV_WRITE_WORKER");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
 
 struct Cancelled {};
 
@@ -95,6 +114,12 @@ class H2ServerConn {
     }
     pool_cv_.notify_all();
     for (auto& t : pool_) t.join();
+    {
+      std::lock_guard<std::mutex> lk(wmu_);
+      wstop_ = true;
+    }
+    wcv_.notify_all();
+    if (wworker_.joinable()) wworker_.join();
   }
 
   void run() {
@@ -145,8 +170,12 @@ class H2ServerConn {
               n -= 1 + pad;
             }
             auto s = find(fh.stream);
+            const bool offload = s && s->path == "WriteObject" && write_worker_enabled();
             if (s) {
-              if (n) bc_.read_exact(s->buf.grow(n), n);
+              if (offload)
+                recv_write_data(s, n);
+              else if (n)
+                bc_.read_exact(s->buf.grow(n), n);
               srv_.stats().bytes_received += n;
             } else {
               bc_.skip(n);
@@ -155,7 +184,9 @@ class H2ServerConn {
             if (uint32_t inc = conn_rw_.consume(fh.length)) w_.write_window_update(0, inc);
             if (s) {
               if (uint32_t inc = s->rw.consume(fh.length)) w_.write_window_update(fh.stream, inc);
-              if (s->path == "WriteObject")
+              if (offload)
+                ;  // complete messages are already queued to the write worker
+              else if (s->path == "WriteObject")
                 process_write_buffer(*s);  // in place: no per-message copies
               else
                 split_messages(*s);
@@ -275,6 +306,91 @@ class H2ServerConn {
   }
   void process_write_buffer(ServerStream& s) {
     for_each_message(s.buf, [&](std::string_view m) { process_write_message(s, m); });
+  }
+
+  // Reader thread: n bytes of a WriteObject stream's DATA.  Each gRPC message
+  // is recv()'d straight into a buffer of its own; complete messages go to
+  // the connection's write worker (decode, CRC32C check, append), in order.
+  // At most kMaxQueuedWrites messages wait per connection: past that the
+  // reader blocks, which stalls the socket and so the sender (backpressure).
+  void recv_write_data(const std::shared_ptr<ServerStream>& sp, uint32_t n) {
+    ServerStream& s = *sp;
+    while (n > 0) {
+      if (s.wprefix_have < 5) {
+        const uint32_t k = std::min<uint32_t>(n, 5 - s.wprefix_have);
+        bc_.read_exact(s.wprefix + s.wprefix_have, k);
+        s.wprefix_have += k;
+        n -= k;
+        if (s.wprefix_have < 5) continue;
+        s.wmsg_len = be32(s.wprefix + 1);
+        s.wmsg_have = 0;
+        if (s.wmsg_cap < s.wmsg_len || !s.wmsg) {
+          s.wmsg = take_write_buffer(s.wmsg_len, &s.wmsg_cap);
+        }
+        if (s.wmsg_len == 0) post_write_message(sp);
+        continue;
+      }
+      const uint32_t k = std::min(n, s.wmsg_len - s.wmsg_have);
+      bc_.read_exact(s.wmsg.get() + s.wmsg_have, k);
+      s.wmsg_have += k;
+      n -= k;
+      if (s.wmsg_have == s.wmsg_len) post_write_message(sp);
+    }
+  }
+
+  std::unique_ptr<char[]> take_write_buffer(size_t len, size_t* cap) {
+    std::unique_lock<std::mutex> lk(wmu_);
+    wcv_.wait(lk, [&] { return wqueued_ < kMaxQueuedWrites || wstop_; });
+    for (size_t i = 0; i < wfree_.size(); ++i)
+      if (wfree_[i].second >= len) {
+        auto b = std::move(wfree_[i].first);
+        *cap = wfree_[i].second;
+        wfree_.erase(wfree_.begin() + static_cast<long>(i));
+        return b;
+      }
+    *cap = std::max<size_t>(len, 64);
+    return std::unique_ptr<char[]>(new char[*cap]);
+  }
+
+  void post_write_message(const std::shared_ptr<ServerStream>& sp) {
+    ServerStream& s = *sp;
+    WriteJob j{sp, std::move(s.wmsg), s.wmsg_cap, s.wmsg_len};
+    s.wmsg_cap = 0;
+    s.wprefix_have = 0;
+    {
+      std::lock_guard<std::mutex> lk(wmu_);
+      ++s.wpending;
+      ++wqueued_;
+      wjobs_.push_back(std::move(j));
+      if (!wworker_.joinable()) wworker_ = std::thread([this] { write_worker(); });
+    }
+    wcv_.notify_all();
+  }
+
+  void write_worker() {
+    pin_current_thread(srv_.config().cpus);
+    name_current_thread("gcsb-srv-wcrc");
+    std::unique_lock<std::mutex> lk(wmu_);
+    for (;;) {
+      wcv_.wait(lk, [&] { return wstop_ || !wjobs_.empty(); });
+      if (wjobs_.empty()) return;  // stopping
+      WriteJob j = std::move(wjobs_.front());
+      wjobs_.pop_front();
+      lk.unlock();
+      process_write_message(*j.s, std::string_view(j.buf.get(), j.len));
+      lk.lock();
+      wfree_.emplace_back(std::move(j.buf), j.cap);
+      if (wfree_.size() > kMaxQueuedWrites) wfree_.erase(wfree_.begin());
+      --wqueued_;
+      --j.s->wpending;
+      wcv_.notify_all();
+    }
+  }
+
+  // Handler thread, before answering a WriteObject: its queued messages done.
+  void wait_write_messages(ServerStream& s) {
+    std::unique_lock<std::mutex> lk(wmu_);
+    wcv_.wait(lk, [&] { return s.wpending == 0 || wstop_; });
   }
   void split_messages(ServerStream& s) { split_messages_into(s.buf, &s.messages); }
 
@@ -831,6 +947,7 @@ class H2ServerConn {
   }
 
   void write_object_done(ServerStream& s) {
+    wait_write_messages(s);
     if (s.write_error) return send_trailers(s.id, s.write_code, s.write_msg, false);
     if (!s.session) return send_trailers(s.id, kInvalidArgument, "empty WriteObject stream", false);
     v2::WriteStatus st;
@@ -904,6 +1021,21 @@ class H2ServerConn {
   int idle_ = 0;
   bool pool_stop_ = false;
   std::map<uint32_t, std::shared_ptr<ServerStream>> streams_;
+  // WriteObject write worker (recv_write_data)
+  struct WriteJob {
+    std::shared_ptr<ServerStream> s;
+    std::unique_ptr<char[]> buf;
+    size_t cap = 0;
+    uint32_t len = 0;
+  };
+  static constexpr size_t kMaxQueuedWrites = 8;
+  std::mutex wmu_;
+  std::condition_variable wcv_;
+  std::deque<WriteJob> wjobs_;
+  std::vector<std::pair<std::unique_ptr<char[]>, size_t>> wfree_;
+  size_t wqueued_ = 0;
+  bool wstop_ = false;
+  std::thread wworker_;
 };
 
 }  // namespace

@@ -199,9 +199,10 @@ class GrpcCall : public H2ClientStream {
   // sink: drained (deferred work run on this thread) at every poke and once
   // after completion.
   // idle_ms > 0 (-read-timeout): a stream silent that long has on_idle run
-  // (it closes the connection, joining its reader thread, so nothing writes
-  // into the sink any more) and fails with a retryable "read timeout"; the
-  // read loop then resumes at the delivered offset on a fresh connection.
+  // (H2ClientConn::abandon_stream: it cancels this stream alone, or closes
+  // the connection if that is silent too; either way nothing writes into the
+  // sink any more) and fails with a retryable "read timeout"; the read loop
+  // then resumes at the delivered offset.
   void wait_ok(Sink* sink = nullptr, int idle_ms = 0, const std::function<void()>& on_idle = {}) {
     std::unique_lock<std::mutex> lk(mu_);
     for (;;) {
@@ -601,7 +602,7 @@ class GrpcStorageClient : public StorageClient {
     std::string f = frame(req);
     try {
       c->start_stream_with_body(call, headers(method, bucket_res), f);
-      call->wait_ok(nullptr, idle_ms_, [c] { c->close(); });
+      call->wait_ok(nullptr, idle_ms_, [c, call, this] { c->abandon_stream(*call, idle_ms_); });
     } catch (...) {
       c->end_stream(*call, true);
       throw;
@@ -639,7 +640,7 @@ class GrpcStorageClient : public StorageClient {
     std::string f = frame(v2::encode_read_request(q));
     try {
       c->start_stream_with_body(call, headers("ReadObject", q.bucket), f);
-      call->wait_ok(sink.deferred() ? &sink : nullptr, idle_ms_, [c] { c->close(); });
+      call->wait_ok(sink.deferred() ? &sink : nullptr, idle_ms_, [c, call, this] { c->abandon_stream(*call, idle_ms_); });
     } catch (...) {
       c->end_stream(*call, true);
       throw;
@@ -746,7 +747,11 @@ class GrpcStorageClient : public StorageClient {
         if (last) break;
         if (k == 0) throw StorageError("upload source ended early", false);
       } while (true);
-      call->wait_ok(nullptr, idle_ms_, [c] { c->close(); });
+      // no read idle limit on the upload's final response: a server that
+      // takes longer than -read-timeout to finalize a large object would
+      // otherwise have the whole non-resumable upload sent again (a
+      // duplicate generation if the first one committed)
+      call->wait_ok(nullptr, 0);
     } catch (...) {
       c->end_stream(*call, true);
       throw;

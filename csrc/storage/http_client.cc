@@ -95,7 +95,9 @@ class H2MediaGet : public H2ClientStream {
         };
         try {
           ObjectInfo info = media_info(status_, clen, offset_, get, each);
-          if (status_ == 200 && offset_ > 0) throw StorageError("http2 GET: server ignored Range", true);
+          // server ignored Range: skip what we already have, as the HTTP/1.1
+          // path does (an error here would retry forever against that server)
+          if (status_ == 200 && offset_ > 0) skip_left_ = static_cast<uint64_t>(offset_);
           const bool full = offset_ == 0 && limit_ < 0 && status_ == 200;
           if (first_) {
             ObjectInfo bi = info;
@@ -124,6 +126,13 @@ class H2MediaGet : public H2ClientStream {
       }
     } else {
       while (n > 0) {
+        if (skip_left_ > 0) {
+          const uint32_t k = static_cast<uint32_t>(std::min<uint64_t>(n, skip_left_));
+          bc.skip(k);
+          skip_left_ -= k;
+          n -= k;
+          continue;
+        }
         if (failed_.load() || *delivered_ >= cap_total_) {
           if (!failed_.load()) fail("http2 GET: server sent more than the requested range", false);
           bc.skip(n);
@@ -169,8 +178,8 @@ class H2MediaGet : public H2ClientStream {
 
   // Waits for END_STREAM / reset; returns the HTTP status, throws on
   // transport or sink errors.
-  // idle_ms > 0 (-read-timeout): see GrpcCall::wait_ok -- on_idle closes
-  // the connection (joining its reader) before the retryable timeout.
+  // idle_ms > 0 (-read-timeout): see GrpcCall::wait_ok -- on_idle abandons
+  // the stream (H2ClientConn::abandon_stream) before the retryable timeout.
   int wait(std::string* body, int idle_ms = 0, const std::function<void()>& on_idle = {}) {
     std::unique_lock<std::mutex> lk(mu_);
     const bool drain = sink_.deferred();
@@ -222,6 +231,7 @@ class H2MediaGet : public H2ClientStream {
   uint64_t cap_total_;
   bool got_head_ = false;
   int status_ = 0;
+  uint64_t skip_left_ = 0;  // 200 to a ranged GET: body bytes before the offset
   std::string err_body_;
   std::atomic<bool> failed_{false};
   std::mutex mu_;
@@ -298,7 +308,8 @@ class HttpStorageClient : public StorageClient {
     int status = 0;
     try {
       c->start_stream(call, h, true);
-      status = call->wait(&body, cfg_.sock.io_timeout_ms, [c] { c->close(); });
+      const int idle = cfg_.sock.io_timeout_ms;
+      status = call->wait(&body, idle, [c, call, idle] { c->abandon_stream(*call, idle); });
     } catch (...) {
       c->end_stream(*call, true);
       throw;

@@ -33,6 +33,7 @@ class DistContext:
     initialized_here: bool = False
     pg: bool = False            # a process group exists (collectives run even at world 1)
     fallback: bool = False      # RCCL failed to initialise; the control plane runs on gloo
+    guard_groups: dict = None   # gloo subgroups with a collective timeout of their own, by timeout
 
 
 def env_rank() -> tuple[int, int, int]:
@@ -120,7 +121,16 @@ def init(local_rank: int | None = None, world: int | None = None, rank: int | No
             ctx.initialized_here = True
         ctx.backend = backend
         ctx.pg = True
+        if backend == "gloo" and world > 1:
+            # while every rank is alive: new_group itself is a collective
+            _timed_group(ctx, collective_timeout_s())
     return ctx
+
+
+def collective_timeout_s() -> float:
+    """Guarded collectives (the fan-out all-gather) give up after this
+    (GCSB_COLLECTIVE_TIMEOUT_S, default 120 s)."""
+    return float(os.environ.get("GCSB_COLLECTIVE_TIMEOUT_S", "120"))
 
 
 class BarrierTimeout(RuntimeError):
@@ -177,6 +187,24 @@ def barrier(ctx: DistContext, what: str = "barrier", timeout_s: float | None = N
         raise RuntimeError(f"barrier mismatch: {int(t.item())} != {ctx.world}")
 
 
+def _timed_group(ctx: DistContext, timeout_s: float):
+    """A gloo subgroup over every rank whose collectives give up after
+    timeout_s.  gloo has no communicator abort, so the guard's watchdog
+    cannot unblock a collective stuck on a dead peer: without this it would
+    sit until the process group's own timeout (600 s).  Created on first use;
+    every rank reaches the same guarded collective, so every rank creates it
+    (new_group is itself collective)."""
+    import torch.distributed as dist
+
+    if ctx.guard_groups is None:
+        ctx.guard_groups = {}
+    key = int(timeout_s)
+    if key not in ctx.guard_groups:
+        ctx.guard_groups[key] = dist.new_group(ranks=list(range(ctx.world)), backend="gloo",
+                                               timeout=datetime.timedelta(seconds=timeout_s))
+    return ctx.guard_groups[key]
+
+
 class _Guard:
     """Watchdog around one collective (see _watchdog)."""
 
@@ -196,7 +224,7 @@ class _Guard:
         return False
 
 
-def all_gather_bytes(ctx: DistContext, out, part, what: str = "all-gather", timeout_s: float = 120.0) -> None:
+def all_gather_bytes(ctx: DistContext, out, part, what: str = "all-gather", timeout_s: float | None = None) -> None:
     """Every rank's `part` (uint8, equal sizes) into `out` in rank order.
     RCCL: all_gather_into_tensor on the GPUs (peer-to-peer over xGMI within a
     node).  gloo: the parts go through host memory."""
@@ -206,14 +234,18 @@ def all_gather_bytes(ctx: DistContext, out, part, what: str = "all-gather", time
     import torch
     import torch.distributed as dist
 
-    with _Guard(ctx, what, timeout_s):
-        if ctx.device.type == "cuda":
+    if timeout_s is None:
+        timeout_s = collective_timeout_s()
+    if ctx.device.type == "cuda":
+        with _Guard(ctx, what, timeout_s):
             dist.all_gather_into_tensor(out, part)
-        else:
-            host = part.cpu()
-            parts = [torch.empty_like(host) for _ in range(ctx.world)]
-            dist.all_gather(parts, host)
-            out.copy_(torch.cat(parts).to(out.device))
+    else:
+        # gloo: the collective carries its own timeout (no abort to call)
+        group = _timed_group(ctx, timeout_s)
+        host = part.cpu()
+        parts = [torch.empty_like(host) for _ in range(ctx.world)]
+        dist.all_gather(parts, host, group=group)
+        out.copy_(torch.cat(parts).to(out.device))
 
 
 def reduce_stats(ctx: DistContext, **vals: float) -> dict:

@@ -157,3 +157,76 @@ def test_numa_placement_queries(native):
         assert memfd and sum(memfd[:-1]) > 0 and memfd[-1] == 0
     finally:
         srv.stop()
+
+
+def _fake_mi355x_node(monkeypatch, a, quota_cpus=None):
+    """A full 8-GPU node as the driver's scaling run sees it: 2 sockets x 64
+    cores x SMT2 (CPU c and c + 128 are siblings; socket s holds cores
+    64s .. 64s + 63), 8 L3 domains of 8 cores per socket, GPUs 0-3 on NUMA
+    node 0 and 4-7 on node 1 (PCI local_cpulist / numa_node per GPU)."""
+    files = {}
+    for c in range(256):
+        core = c % 128
+        sock = core // 64
+        files[f"/sys/devices/system/cpu/cpu{c}/topology/physical_package_id"] = str(sock)
+        files[f"/sys/devices/system/cpu/cpu{c}/topology/core_id"] = str(core % 64)
+        lo = core // 8 * 8
+        files[f"/sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list"] = f"{lo}-{lo + 7},{lo + 128}-{lo + 135}"
+    buses = [f"0000:{b:02x}:00.0" for b in (0x05, 0x15, 0x25, 0x35, 0x85, 0x95, 0xa5, 0xb5)]
+    for d, bus in enumerate(buses):
+        node = d // 4
+        files[f"/sys/bus/pci/devices/{bus}/numa_node"] = str(node)
+        files[f"/sys/bus/pci/devices/{bus}/local_cpulist"] = \
+            f"{64 * node}-{64 * node + 63},{128 + 64 * node}-{128 + 64 * node + 63}"
+    files["/sys/fs/cgroup/cpu.max"] = f"{quota_cpus * 100000} 100000" if quota_cpus else "max 100000"
+    real = a._native
+
+    class FakeNative:
+        parse_cpulist = staticmethod(real.parse_cpulist)
+
+        @staticmethod
+        def gpu_device_count():
+            return 8
+
+        @staticmethod
+        def gpu_pci_bus_id(d):
+            return buses[d]
+
+    monkeypatch.setattr(a, "_native", FakeNative)
+    monkeypatch.setattr(a, "_read", lambda p: files.get(p))
+    monkeypatch.setattr(a.os, "sched_getaffinity", lambda pid: set(range(256)))
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+
+
+@pytest.mark.parametrize("mode", ["pair", "share", "same", "split", "share_quota"])
+def test_eight_ranks_of_a_node_get_disjoint_gpu_local_cpus(monkeypatch, mode):
+    """bench.py --gpus 8 on one node: every rank plans its own placement at
+    the same time (pair mode samples /proc/stat separately in each rank).
+    The client / endpoint / submitter CPUs of the 8 ranks must not overlap,
+    and each rank stays on its GPU's NUMA node; a collision would quietly
+    halve a rank's one-stream rate in the driver's first scaling run."""
+    import random
+
+    from custom_go_client_benchmark_amd.parallel import affinity as a
+
+    _fake_mi355x_node(monkeypatch, a, quota_cpus=128)
+    rng = random.Random(7)
+    sets = []
+    for r in range(8):
+        monkeypatch.setenv("LOCAL_RANK", str(r))
+        # each rank sees its own (different) busy sample
+        busy = {c: rng.random() * 0.5 for c in range(256)}
+        monkeypatch.setattr(a, "cpu_busy", lambda sample_s=0.15, b=busy: b)
+        p = a.plan(r, mode)
+        assert p["client"] and p["server"], p
+        mine = set(p["client"]) | set(p["server"]) | set(p.get("aux") or [])
+        node = r // 4
+        assert all((c % 128) // 64 == node for c in mine), (r, sorted(mine))
+        if mode == "pair":
+            assert p["picked_by"] == "quiet" and len({frozenset(p[k]) for k in ("client", "server", "aux")}) == 3
+        if mode == "share_quota":
+            assert len(p["client"]) <= 16  # 128-CPU quota over 8 ranks
+        sets.append(mine)
+    for i in range(8):
+        for j in range(i + 1, 8):
+            assert not (sets[i] & sets[j]), (mode, i, j, sorted(sets[i] & sets[j]))

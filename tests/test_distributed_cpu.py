@@ -251,3 +251,48 @@ def test_cli_two_ranks_latency_files_merge(tmp_path):
     out = json.loads(m.stdout)
     assert out["node"]["count"] == 16
     assert out["node"]["min_ms"] <= out["node"]["p50_ms"] <= out["node"]["p99_ms"] <= out["node"]["max_ms"]
+
+
+def _stuck_gather_worker(rank, world, port, q):
+    import time
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), GCSB_COLLECTIVE_TIMEOUT_S="3")
+    sys.path.insert(0, ROOT)
+    import torch
+
+    from custom_go_client_benchmark_amd.parallel import dist
+
+    ctx = dist.init()
+    dist.barrier(ctx, "warm barrier")
+    if rank == 1:
+        time.sleep(30)  # a stuck peer: never joins the all-gather
+        os._exit(0)
+    out = torch.zeros(8, dtype=torch.uint8)
+    t0 = time.time()
+    try:
+        dist.all_gather_bytes(ctx, out, out[:4], "fan-out all-gather")
+        q.put(("returned", time.time() - t0))
+    except Exception as e:  # noqa: BLE001
+        q.put(("raised", time.time() - t0, type(e).__name__))
+    os._exit(0)
+
+
+def test_gloo_all_gather_gives_up_on_a_stuck_peer():
+    """gloo has no communicator abort: the guarded all-gather runs on a gloo
+    subgroup with its own timeout (GCSB_COLLECTIVE_TIMEOUT_S), so a stuck peer
+    fails it in seconds instead of the process group's 600 s."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    ps = [ctx.Process(target=_stuck_gather_worker, args=(r, 2, port, q)) for r in range(2)]
+    [p.start() for p in ps]
+    try:
+        outcome = q.get(timeout=60)
+        assert outcome[0] == "raised" and outcome[1] < 20, outcome
+    finally:
+        for p in ps:
+            p.kill()
+            p.join(10)

@@ -107,3 +107,32 @@ def test_corruption_before_a_timeout_is_caught_after_resume(native, server, prot
     r = c.read(B, P + "0")
     assert r["attempts"] == 2
     assert r["crc_mismatch"] and not r["verified"]
+
+
+@pytest.mark.parametrize("proto", ["grpc", "http2"])
+def test_one_stalled_stream_does_not_fail_its_neighbours(native, server, proto):
+    # gRPC pool 1 / HTTP/2 multiplex every read on one connection: when one
+    # stream times out, only that stream is cancelled (RST_STREAM) -- the
+    # reads sharing the connection keep going on it, none is retried
+    import threading
+
+    server.add_synthetic(B, P, "", 0, 1, 3 << 20)
+    server.add_synthetic(B, "small/file_", "", 0, 1, 256 << 10)
+    server.set_faults({"stall_at": 1 << 20, "stall_ms": 500, "stall_count": 1})
+    c = _client(native, server, proto, io_timeout_ms=100, retry_max_attempts=3)
+    assert c.read(B, "small/file_0")["verified"]  # the connection is up
+    stalled = []
+    t = threading.Thread(target=lambda: stalled.append(c.read(B, P + "0")))
+    t.start()
+    neighbours = []
+    t_end = time.perf_counter() + 0.7
+    while time.perf_counter() < t_end:
+        neighbours.append(c.read(B, "small/file_0"))
+    t.join()
+    r = stalled[0]
+    assert r["bytes"] == 3 << 20 and r["verified"] and r["attempts"] == 2
+    assert server.stats()["faults_injected"] == 1
+    assert len(neighbours) > 5
+    assert all(x["verified"] and x["attempts"] == 1 for x in neighbours), [x["attempts"] for x in neighbours]
+    if proto == "grpc":
+        assert server.stats()["connections"] == 1  # the shared connection was never closed

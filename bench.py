@@ -165,6 +165,8 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--list-objects", type=int, default=1000,
                     help="config 3 side block: list this many 1 MiB objects, read each into HBM (0 = off)")
     ap.add_argument("--list-workers", type=int, default=8, help="config 3 side block: readers")
+    ap.add_argument("--list-ring", default="8x2MiB",
+                    help="config 3 side block: pinned ring per reader, SLOTSxSLOT_BYTES (1 MiB objects)")
     ap.add_argument("--write-size", default="64MiB", help="config 5 object size")
     ap.add_argument("--write-chunk", default="16MiB", help="resumable upload chunk (HTTP) / message batch")
     ap.add_argument("--baseline", default="on", choices=["on", "off"],
@@ -179,6 +181,9 @@ def build_parser() -> argparse.ArgumentParser:
                          "objects, gRPC pool 1 vs HTTP keep-alive, discard sink + host CRC (0 = off)")
     ap.add_argument("--ref-reads", type=int, default=50, help="ref_default_*: timed reads per worker")
     ap.add_argument("--ref-object-size", default="1MiB", help="ref_default_*: object size")
+    ap.add_argument("--blocks", default="",
+                    help="comma list of side blocks to run (A/B sessions): cpu_baseline, compare, sliced, ceiling, "
+                         "ref_default, c1_http_cpu, list_read, write, write_composite, fanout; empty = all")
     ap.add_argument("--json-out", default="")
     return ap
 
@@ -358,6 +363,7 @@ def run_rank(args) -> int:
         sync()
         t1 = time.perf_counter()
         rv0 = n.recv_stats()
+        h2s0 = n.h2_reader_stats()
         if use_gpu:
             n.reset_slow_hip_calls()
         if not err:
@@ -375,8 +381,25 @@ def run_rank(args) -> int:
             if not ok:
                 err = why
             cpu = cpu_delta(c0, cpu_snapshot(), float(s1["bytes"]), e1)
-            cpu["cpu_s_per_gib_by_thread"] = cpuacct.per_gib(
-                cpuacct.delta_by_group(th0, cpuacct.thread_cpu()), float(s1["bytes"]))
+            th1 = cpuacct.thread_cpu()
+            cpu["cpu_s_per_gib_by_thread"] = cpuacct.per_gib(cpuacct.delta_by_group(th0, th1), float(s1["bytes"]))
+            names = cpuacct.delta_by_name(th0, th1)
+            # worker threads exit at the end of the run: their CPU comes from the runner
+            names.pop("gcsb-worker", None)
+            names["gcsb-worker (exited)"] = s1.get("worker_cpu_s", 0.0)
+            cpu["cpu_s_per_gib_by_name"] = {k: v for k, v in cpuacct.per_gib(names, float(s1["bytes"])).items()
+                                            if v >= 0.0005}
+            h2s1 = n.h2_reader_stats()
+            if h2s1["frames"] > h2s0["frames"]:
+                # the HTTP/2 connection readers (gRPC): where their time went, per GiB
+                d = {k: h2s1[k] - h2s0[k] for k in h2s1}
+                g = max(float(s1["bytes"]), 1.0) / (1 << 30)
+                cpu["h2_reader"] = {"frames_per_read": round(d["frames"] / max(1, s1["reads"]), 2),
+                                    "wait_s_per_gib": round(d["header_wait_ns"] / 1e9 / g, 4),
+                                    "data_s_per_gib": round(d["data_ns"] / 1e9 / g, 4),
+                                    "headers_s_per_gib": round(d["headers_ns"] / 1e9 / g, 4),
+                                    "other_s_per_gib": round(d["other_ns"] / 1e9 / g, 4),
+                                    "avg_data_frame_kib": round(d["data_bytes"] / max(1, d["data_frames"]) / 1024, 1)}
             rv1 = n.recv_stats()
             calls = rv1[0] - rv0[0]
             if calls:
@@ -604,9 +627,10 @@ def run_rank(args) -> int:
         except Exception as e:  # noqa: BLE001 - reported in the block, collectives still run
             err = f"{type(e).__name__}: {e}"
         per_pass = (nobj + workers - 1) // workers
+        lslots, _, lbytes = args.list_ring.partition("x")
         over = {"protocol": proto, "endpoint": ep.url if ep is not None else "", "workers": workers,
                 "object_names": names or [f"c3_rank{rank}/file_0"], "cpus": sh["client"], "worker_id_offset": 0,
-                "rcvbuf": 0}
+                "rcvbuf": 0, "ring_slots": int(lslots), "ring_slot_bytes": parse_size(lbytes)}
         # every rank runs the block (and its collectives) whatever happened here
         st = read_block(over, per_pass, per_pass * warmup_passes, f"{proto} list-read")
         if err:
@@ -721,8 +745,12 @@ def run_rank(args) -> int:
     # ---- side blocks (after the timed region) ----------------------------
     other = {"grpc": "http", "http": "grpc"}.get(protocol)
     blocks = {}
+    only = {b.strip() for b in args.blocks.split(",") if b.strip()}
+
+    def want(name: str) -> bool:
+        return not only or name in only
     if side_steps > 0 and args.workload == "read":
-        if use_gpu and args.baseline == "on":
+        if use_gpu and args.baseline == "on" and want("cpu_baseline"):
             # right after the headline (the boxes drift over a run): the
             # reference's semantics on the headline config -- same endpoint,
             # placement, object and steps; bytes to a discard sink, CRC32C of
@@ -734,10 +762,10 @@ def run_rank(args) -> int:
                                                side_warm, f"{p} cpu baseline"),
                                {"protocol": p, "sink": "discard", "host_crc": True,
                                 "note": "reference semantics: io.Discard + host CRC32C"})
-        if other and other in hbm.available_protocols():
+        if other and other in hbm.available_protocols() and want("compare"):
             blocks["compare"] = ("compare", read_block({"protocol": other}, side_steps, side_warm, f"{other} compare"),
                                  {"protocol": other})
-        if args.sliced_streams > 1 and args.slices == 1:
+        if args.sliced_streams > 1 and args.slices == 1 and want("sliced"):
             # 8 receive + 8 send threads: a share-placed endpoint of its own
             srv_sl, sh = share_endpoint()
             sliced_cfg.update({"endpoint": srv_sl.url, "cpus": sh["client"]})
@@ -747,9 +775,9 @@ def run_rank(args) -> int:
                                 {"streams_per_read": args.sliced_streams,
                                  "ring": f"{args.sliced_slots}x{args.sliced_slot_bytes}", "affinity": "share",
                                  "piece_bytes": parse_size(args.piece_bytes), "note": "extension, not parity"})
-        if args.ceiling == "on":
+        if args.ceiling == "on" and want("ceiling"):
             blocks["ceiling"] = ("ceiling", ceiling_block(mib_s(head) / max(1, world)), None)
-        if args.ref_workers > 0:
+        if args.ref_workers > 0 and want("ref_default"):
             for p in ["http"] + ([x for x in ("grpc",) if x in hbm.available_protocols()]):
                 blocks[f"ref_default_{p}"] = (f"ref_default_{p}", ref_default_block(p),
                                               {"protocol": p, "workers": args.ref_workers,
@@ -757,7 +785,7 @@ def run_rank(args) -> int:
                                                "reads_per_worker": args.ref_reads, "sink": "discard",
                                                "grpc_conn_pool_size": 1 if p == "grpc" else None,
                                                "note": "reference default experiment (execute_pb.sh)"})
-        if "http" in hbm.available_protocols():
+        if "http" in hbm.available_protocols() and want("c1_http_cpu"):
             # config 1: one 1 MiB object over the HTTP JSON API, CPU only
             # (discard sink, host CRC32C as the Go library), one reader
             srv.add_synthetic(bucket, "c1/file_", "", first, 1, 1 << 20)
@@ -767,21 +795,23 @@ def run_rank(args) -> int:
                                                  "rcvbuf": 0}, max(side_steps, 100), side_warm, "config 1"),
                                      {"protocol": "http", "api": "json", "object_bytes": 1 << 20, "sink": "discard",
                                       "workers": 1, "config": "BASELINE config 1"})
-        if args.list_objects > 0:
+        if args.list_objects > 0 and want("list_read"):
             for p in [protocol] + ([other] if other and other in hbm.available_protocols() else []):
                 blocks[f"list_read_{p}"] = (f"list_read_{p}", list_read_block(p, 1),
                                             {"protocol": p, "objects": args.list_objects, "object_bytes": 1 << 20,
-                                             "workers": args.list_workers, "config": "BASELINE config 3"})
-        if use_gpu:
+                                             "workers": args.list_workers, "ring": args.list_ring,
+                                             "config": "BASELINE config 3"})
+        if use_gpu and want("write"):
             blocks["write"] = ("write", write_block(side_steps, side_warm),
                                {"protocol": protocol, "object_bytes": parse_size(args.write_size),
                                 "config": "BASELINE config 5"})
-            if args.write_parts > 1:
+        if use_gpu:
+            if args.write_parts > 1 and want("write_composite"):
                 blocks["write_composite"] = ("write_composite", write_block(side_steps, side_warm, args.write_parts),
                                              {"protocol": protocol, "object_bytes": parse_size(args.write_size),
                                               "parts": args.write_parts,
                                               "note": "extension: parallel composite upload, not parity"})
-        if world > 1 and args.fanout == "on":
+        if world > 1 and args.fanout == "on" and want("fanout"):
             blocks["fanout"] = ("fanout", fanout_block(side_steps, side_warm),
                                 {"object_bytes": size, "slice_bytes": size // world,
                                  "collective": f"{ctx.backend} all_gather_into_tensor" if ctx.device.type == "cuda"
@@ -886,6 +916,12 @@ def run_rank(args) -> int:
                     out[key] = st
                     continue
                 b = block_json(st, **{k: v for k, v in extra.items() if v is not None})
+                if key.startswith(("ref_default_", "list_read_")) and st.get("cpu"):
+                    # many streams on one connection (gRPC pool 1): where the CPU goes
+                    b["cpu_s_per_gib_by_thread"] = st["cpu"].get("cpu_s_per_gib_by_name", {})
+                    b["cpus_busy"] = st["cpu"].get("cpus_busy")
+                    if st["cpu"].get("h2_reader"):
+                        b["h2_reader"] = st["cpu"]["h2_reader"]
                 if key.startswith("ref_default_"):
                     b["first_read_p50_ms"] = round(st["first_p50_max"], 3)
                     b["steady_p99_ms"] = round(st["steady_p99_max"], 3)

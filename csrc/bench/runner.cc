@@ -2,6 +2,7 @@
 
 #include "gpu/markers.h"
 
+#include <sys/resource.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -83,6 +84,7 @@ std::vector<std::vector<long>> Runner::ring_numa(int w) const {
 void Runner::reset_stats() {
   std::lock_guard<std::mutex> lk(mu_);
   acc_ = RunSummary();
+  worker_cpu_s_ = 0;
   lat_ms_.clear();
   host_ms_.clear();
   ttfb_ms_.clear();
@@ -105,7 +107,16 @@ void Runner::start() {
     sliced_.resize(cfg_.workers);
     landing_.resize(cfg_.workers);
   }
-  for (int w = 0; w < cfg_.workers; ++w) threads_.emplace_back([this, w] { worker_main(w); });
+  for (int w = 0; w < cfg_.workers; ++w)
+    threads_.emplace_back([this, w] {
+      worker_main(w);
+      // the thread ends here: keep its CPU time for the per-thread split
+      rusage ru{};
+      getrusage(RUSAGE_THREAD, &ru);
+      const double cpu = ru.ru_utime.tv_sec + ru.ru_utime.tv_usec * 1e-6 + ru.ru_stime.tv_sec + ru.ru_stime.tv_usec * 1e-6;
+      std::lock_guard<std::mutex> lk(mu_);
+      worker_cpu_s_ += cpu;
+    });
 }
 
 void Runner::wait() {
@@ -295,6 +306,7 @@ std::vector<ReadRecord> Runner::drain() {
 RunSummary Runner::summary() const {
   std::lock_guard<std::mutex> lk(mu_);
   RunSummary s = acc_;
+  s.worker_cpu_s = worker_cpu_s_;
   s.elapsed_s = t_last_ > t_first_ ? (t_last_ - t_first_) / 1e9 : 0;
   s.mb_per_s = s.elapsed_s > 0 ? s.bytes / 1048576.0 / s.elapsed_s : 0;
   {

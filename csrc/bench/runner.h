@@ -90,6 +90,7 @@ struct RunSummary {
   // reads are the p99.  Split out so the steady-state tail is visible.
   double first_read_p50_ms = 0, first_read_max_ms = 0, steady_p50_ms = 0, steady_p99_ms = 0;
   double slice_skew_ms = 0;  // sliced reads: mean spread of the slices' host-landed times
+  double worker_cpu_s = 0;   // CPU time of the worker threads (RUSAGE_THREAD at their exit)
   uint64_t oc_buckets[kOcBuckets] = {0};
   // the 3 slowest reads: {index in completion order, ms, host-landed ms, TTFB ms}
   std::vector<std::vector<double>> slowest;
@@ -137,6 +138,7 @@ class Runner {
   std::vector<double> lat_ms_, host_ms_, ttfb_ms_, first_ms_, steady_ms_;
   std::vector<double> ttfb_by_read_;  // per ok read, in completion order (0 if unknown)
   RunSummary acc_;
+  double worker_cpu_s_ = 0;  // guarded by mu_
   int64_t t_first_ = 0, t_last_ = 0;
   std::mutex out_mu_;
   std::vector<GpuSinkStats> gpu_stats_;

@@ -191,6 +191,13 @@ class GpuByteSource : public ByteSource {
   bool range_crc32c(uint64_t off, size_t len, uint32_t* crc) override;
   uint64_t copies() const { return copies_; }
   uint64_t gpu_range_crcs() const { return range_hits_; }
+  // Objects up to kWholeRingMax (GCSB_UPLOAD_SPLICE, default on) stage into a
+  // ring that holds all of them: no slot is refilled during the upload, so
+  // the transport can splice the staged pages instead of copying them.
+  bool stable_until_done() const override {
+    return static_cast<uint64_t>(nslots_) * slot_bytes_ >= n_;
+  }
+  static constexpr uint64_t kWholeRingMax = uint64_t(512) << 20;
 
  private:
   void restart(uint64_t off);

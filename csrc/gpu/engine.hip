@@ -888,6 +888,8 @@ GpuByteSource::GpuByteSource(int device, const void* dptr, uint64_t n, size_t sl
       nslots_(std::max(2, slots)) {
   static const bool trace = std::getenv("GCSB_TRACE_SOURCE") != nullptr;  // phase timings (write-tail probe)
   int64_t tp[5] = {now_ns(), 0, 0, 0, 0};
+  if (env_flag("GCSB_UPLOAD_SPLICE", true) && n_ <= kWholeRingMax)
+    nslots_ = std::max<int>(nslots_, static_cast<int>((n_ + slot_bytes_ - 1) / slot_bytes_));
   hip_check(hipSetDevice(device_), "hipSetDevice");
   DeviceStreamPool& pool = DeviceStreamPool::get(device_);
   // The staging copies go round-robin over 2 pool streams, not one per slot,

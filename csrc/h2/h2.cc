@@ -97,7 +97,7 @@ void H2Writer::write_frame_pieces(uint8_t type, uint8_t flags, uint32_t stream, 
   std::lock_guard<std::mutex> lk(wmu_);
   for (size_t i = 0; i < pieces.size(); ++i) {
     const SendPiece& p = pieces[i];
-    if (p.fd < 0) {
+    if (p.fd < 0 && !p.splice) {
       if (p.n) iov.push_back({const_cast<uint8_t*>(p.p), p.n});
       continue;
     }
@@ -105,7 +105,10 @@ void H2Writer::write_frame_pieces(uint8_t type, uint8_t flags, uint32_t stream, 
       conn_.writev_all(iov.data(), static_cast<int>(iov.size()), /*more=*/true);
       iov.clear();
     }
-    conn_.sendfile_all(p.fd, p.foff, p.n, /*more=*/false);
+    if (p.splice)
+      conn_.splice_user_all(p.p, p.n, /*more=*/i + 1 < pieces.size());
+    else
+      conn_.sendfile_all(p.fd, p.foff, p.n, /*more=*/false);
   }
   if (!iov.empty()) conn_.writev_all(iov.data(), static_cast<int>(iov.size()));
 }

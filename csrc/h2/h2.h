@@ -66,6 +66,9 @@ struct SendPiece {
   size_t n = 0;
   int fd = -1;
   uint64_t foff = 0;
+  // user memory sent by vmsplice + splice (Conn::splice_user_all): no copy,
+  // the pages must stay unchanged until the peer has read them
+  bool splice = false;
 };
 
 // Per-direction connection machinery common to both roles: serialized

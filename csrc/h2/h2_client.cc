@@ -12,6 +12,24 @@
 
 namespace gcsb {
 
+namespace {
+std::atomic<uint64_t> g_frames{0}, g_data_frames{0}, g_header_blocks{0}, g_data_bytes{0}, g_wait_ns{0},
+    g_data_ns{0}, g_headers_ns{0}, g_other_ns{0};
+}  // namespace
+
+H2ReaderStats h2_reader_stats() {
+  H2ReaderStats s;
+  s.frames = g_frames.load();
+  s.data_frames = g_data_frames.load();
+  s.header_blocks = g_header_blocks.load();
+  s.data_bytes = g_data_bytes.load();
+  s.header_wait_ns = g_wait_ns.load();
+  s.data_ns = g_data_ns.load();
+  s.headers_ns = g_headers_ns.load();
+  s.other_ns = g_other_ns.load();
+  return s;
+}
+
 std::shared_ptr<H2ClientConn> H2ClientConn::dial(const Endpoint& ep, const H2ClientOptions& opt) {
   std::shared_ptr<H2ClientConn> c(new H2ClientConn(ep, opt));
   auto conn = Conn::dial(ep, opt.sock);
@@ -191,6 +209,40 @@ void H2ClientConn::send_data_iov(H2ClientStream& s, struct iovec* iov, int cnt, 
   }
 }
 
+void H2ClientConn::send_data_pieces(H2ClientStream& s, const std::vector<SendPiece>& pieces, bool end_stream) {
+  size_t total = 0;
+  for (const SendPiece& p : pieces) total += p.n;
+  if (total == 0) {
+    if (end_stream) w_->write_frame(h2::kData, h2::kFlagEndStream, s.id_, nullptr, 0);
+    return;
+  }
+  size_t idx = 0, off = 0, left = total;
+  std::vector<SendPiece> frame;
+  while (left > 0) {
+    size_t n = w_->reserve(s.id_, left);
+    if (n == 0) throw StorageError("http2 stream closed while sending: " + dead_reason(), true);
+    frame.clear();
+    size_t need = n;
+    while (need > 0) {
+      const SendPiece& src = pieces[idx];
+      SendPiece q = src;
+      const size_t k = std::min(need, src.n - off);
+      q.p = src.p ? src.p + off : nullptr;
+      q.foff = src.foff + off;
+      q.n = k;
+      frame.push_back(q);
+      need -= k;
+      off += k;
+      if (off == src.n) {
+        ++idx;
+        off = 0;
+      }
+    }
+    left -= n;
+    w_->write_frame_pieces(h2::kData, (left == 0 && end_stream) ? h2::kFlagEndStream : 0, s.id_, frame, n);
+  }
+}
+
 void H2ClientConn::end_stream(H2ClientStream& s, bool reset) {
   if (s.id_ == 0 || s.cancelled_) return;
   {
@@ -227,8 +279,22 @@ void H2ClientConn::reader_loop() {
   bool hend_stream = false;
   try {
     for (;;) {
+      const int64_t t_wait = now_ns();
       FrameHeader fh = read_frame_header(*bc_);
-      last_frame_ns_.store(now_ns(), std::memory_order_relaxed);
+      const int64_t t_frame = now_ns();
+      last_frame_ns_.store(t_frame, std::memory_order_relaxed);
+      g_wait_ns.fetch_add(static_cast<uint64_t>(t_frame - t_wait), std::memory_order_relaxed);
+      g_frames.fetch_add(1, std::memory_order_relaxed);
+      struct Account {  // time of this frame's handling, by type
+        uint8_t type;
+        int64_t t0;
+        ~Account() {
+          const uint64_t d = static_cast<uint64_t>(now_ns() - t0);
+          (type == h2::kData ? g_data_ns
+                             : (type == h2::kHeaders || type == h2::kContinuation) ? g_headers_ns : g_other_ns)
+              .fetch_add(d, std::memory_order_relaxed);
+        }
+      } account{fh.type, t_frame};
       if (fh.length > opt_.max_frame_size) throw StorageError("http2: frame exceeds max_frame_size", true);
       switch (fh.type) {
         case h2::kData: {
@@ -243,6 +309,8 @@ void H2ClientConn::reader_loop() {
           }
           auto s = acquire(fh.stream);
           bool end = fh.flags & h2::kFlagEndStream;
+          g_data_frames.fetch_add(1, std::memory_order_relaxed);
+          g_data_bytes.fetch_add(n, std::memory_order_relaxed);
           if (s) {
             s->progress_.fetch_add(1, std::memory_order_relaxed);
             s->on_data(*bc_, n, end);
@@ -279,6 +347,7 @@ void H2ClientConn::reader_loop() {
           }
           hblock.append(frag, b, e - b);
           if (fh.flags & h2::kFlagEndHeaders) {
+            g_header_blocks.fetch_add(1, std::memory_order_relaxed);
             HeaderList hl;
             dec_.decode(reinterpret_cast<const uint8_t*>(hblock.data()), hblock.size(), &hl);
             if (auto s = acquire(hstream)) {

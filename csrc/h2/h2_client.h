@@ -77,6 +77,20 @@ struct H2ClientOptions {
   std::vector<int> cpus;  // pin the connection's reader thread
 };
 
+// Where the connection reader threads' time goes (process totals): waiting
+// for / reading frame headers, dispatching DATA into streams (the receive
+// copy), and HEADERS (HPACK decode + completion).  Multiplexed gRPC reads are
+// bound by one reader thread per connection, so this is their profile.
+struct H2ReaderStats {
+  uint64_t frames = 0, data_frames = 0, header_blocks = 0;
+  uint64_t data_bytes = 0;
+  uint64_t header_wait_ns = 0;  // inside read_frame_header (includes blocking for data)
+  uint64_t data_ns = 0;         // DATA frames: stream dispatch incl. recv() into the sink
+  uint64_t headers_ns = 0;      // HEADERS/CONTINUATION: read + HPACK decode + stream dispatch
+  uint64_t other_ns = 0;        // every other frame type
+};
+H2ReaderStats h2_reader_stats();
+
 class H2ClientConn {
  public:
   static std::shared_ptr<H2ClientConn> dial(const Endpoint& ep, const H2ClientOptions& opt);
@@ -91,6 +105,9 @@ class H2ClientConn {
   // Sends request body bytes honouring flow control (blocks).
   void send_data(H2ClientStream& s, const uint8_t* p, size_t n, bool end_stream);
   void send_data_iov(H2ClientStream& s, struct iovec* iov, int cnt, bool end_stream);
+  // Same, from SendPieces (a `splice` piece goes to the socket by page
+  // reference, see SendPiece): split into DATA frames by flow control.
+  void send_data_pieces(H2ClientStream& s, const std::vector<SendPiece>& pieces, bool end_stream);
   // Forget a stream (RST_STREAM CANCEL if it is still open on our side).
   void end_stream(H2ClientStream& s, bool reset);
   // -read-timeout hit on stream s (its waiter saw no frame for idle_ms).  If

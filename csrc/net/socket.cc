@@ -4,6 +4,7 @@
 
 #include <arpa/inet.h>
 #include <fcntl.h>
+#include <sys/uio.h>
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
@@ -292,6 +293,11 @@ std::unique_ptr<Conn> Conn::adopt(int fd, const SocketOptions& opt) {
 Conn::~Conn() { close(); }
 
 void Conn::close() {
+  for (int& p : pipe_)
+    if (p >= 0) {
+      ::close(p);
+      p = -1;
+    }
   if (ssl_) {
     std::lock_guard<std::mutex> lk(ssl_mu_);
     SSL_shutdown(ssl_);  // best effort on the non-blocking socket
@@ -394,6 +400,47 @@ void Conn::writev_all(struct iovec* iov, int cnt, bool more) {
     if (cnt > 0 && left) {
       iov->iov_base = static_cast<uint8_t*>(iov->iov_base) + left;
       iov->iov_len -= left;
+    }
+  }
+}
+
+void Conn::splice_user_all(const void* data, size_t n, bool more) {
+  if (fd_ < 0) throw StorageError("write on closed connection", true);
+  if (ssl_) return write_all(data, n);
+  if (pipe_[0] < 0) {
+    if (::pipe2(pipe_, O_CLOEXEC) != 0) throw StorageError(std::string("pipe2: ") + std::strerror(errno), false);
+    // a 1 MiB pipe (fs.pipe-max-size default): 2 syscalls per MiB
+    (void)::fcntl(pipe_[1], F_SETPIPE_SZ, 1 << 20);
+    const int c = ::fcntl(pipe_[1], F_GETPIPE_SZ);
+    pipe_cap_ = c > 0 ? static_cast<size_t>(c) : 65536;
+  }
+  auto* p = static_cast<const uint8_t*>(data);
+  while (n > 0) {
+    iovec iov{const_cast<uint8_t*>(p), std::min(n, pipe_cap_)};
+    ssize_t k = ::vmsplice(pipe_[1], &iov, 1, 0);
+    if (k < 0) {
+      if (errno == EINTR) continue;
+      throw StorageError(std::string("vmsplice: ") + std::strerror(errno), true);
+    }
+    p += k;
+    n -= static_cast<size_t>(k);
+    size_t left = static_cast<size_t>(k);
+    while (left > 0) {
+      const unsigned fl = SPLICE_F_MOVE | ((more || n > 0) ? SPLICE_F_MORE : 0u);
+      ssize_t w = ::splice(pipe_[0], nullptr, fd_, nullptr, left, fl);
+      if (w < 0) {
+        if (errno == EINTR) continue;
+        const int e = errno;
+        // the pipe may still hold page references: drop it with the connection
+        for (int& q : pipe_) {
+          ::close(q);
+          q = -1;
+        }
+        throw StorageError(std::string("splice: ") + std::strerror(e), true);
+      }
+      if (w == 0) throw StorageError("splice: connection closed", true);
+      bytes_written_ += static_cast<uint64_t>(w);
+      left -= static_cast<size_t>(w);
     }
   }
 }

@@ -78,6 +78,11 @@ class Conn {
   void writev_all(struct iovec* iov, int cnt, bool more = false);
   // Zero-copy send of a file range (sendfile); `more` corks for a following write.
   void sendfile_all(int in_fd, uint64_t off, size_t n, bool more = false);
+  // Zero-copy send of user memory: vmsplice() its pages into a pipe, splice()
+  // the pipe into the socket.  The socket buffers then REFERENCE the pages, so
+  // the caller must leave them unchanged until the peer has read the bytes
+  // (for an upload: until its final response).  TLS falls back to a copy.
+  void splice_user_all(const void* p, size_t n, bool more = false);
   void shutdown_write();
   void close();
   int fd() const { return fd_; }
@@ -100,6 +105,8 @@ class Conn {
   int io_timeout_ms_ = 0;
   uint64_t bytes_read_ = 0;
   uint64_t bytes_written_ = 0;
+  int pipe_[2] = {-1, -1};  // splice_user_all's page pipe (lazily created)
+  size_t pipe_cap_ = 0;
 };
 
 // Listening socket for the synthetic server.

@@ -14,6 +14,7 @@
 #include "core/util.h"
 #include "gpu/crc_types.h"
 #include "gpu/engine.h"
+#include "h2/h2_client.h"
 #include "h2/hpack.h"
 #include "proto/storage_v2.h"
 #include "server/fakegcs.h"
@@ -501,6 +502,7 @@ class PyRunner {
     d["steady_p99_ms"] = s.steady_p99_ms;
     d["slice_skew_ms"] = s.slice_skew_ms;
     d["slowest"] = s.slowest;
+    d["worker_cpu_s"] = s.worker_cpu_s;
     py::list b;
     for (int i = 0; i < kOcBuckets; ++i) b.append(s.oc_buckets[i]);
     d["oc_buckets"] = b;
@@ -810,6 +812,19 @@ PYBIND11_MODULE(_native, m) {
   m.def("recv_stats", [] {
     RecvStats r = recv_stats();
     return py::make_tuple(r.calls, r.bytes);
+  });
+  m.def("h2_reader_stats", [] {
+    H2ReaderStats s = h2_reader_stats();
+    py::dict d;
+    d["frames"] = s.frames;
+    d["data_frames"] = s.data_frames;
+    d["header_blocks"] = s.header_blocks;
+    d["data_bytes"] = s.data_bytes;
+    d["header_wait_ns"] = s.header_wait_ns;
+    d["data_ns"] = s.data_ns;
+    d["headers_ns"] = s.headers_ns;
+    d["other_ns"] = s.other_ns;
+    return d;
   });
   m.def("slow_hip_calls", [] {
     SlowHipCalls s = slow_hip_calls();

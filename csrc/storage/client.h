@@ -89,6 +89,12 @@ class ByteSource {
     (void)off, (void)len, (void)crc;
     return false;
   }
+  // The windows next() returns stay unchanged until the upload call returns
+  // (no staging slot is refilled while the object is sent): the transport
+  // may then hand their pages to the socket by reference (vmsplice + splice)
+  // instead of copying them, since the final response proves the peer read
+  // every byte.
+  virtual bool stable_until_done() const { return false; }
 };
 
 class HostByteSource : public ByteSource {
@@ -99,6 +105,7 @@ class HostByteSource : public ByteSource {
   void seek(uint64_t off) override { off_ = off; }
   bool has_crc32c() const override { return has_crc_; }
   uint32_t crc32c() const override { return crc_; }
+  bool stable_until_done() const override { return true; }  // the caller's buffer
 
  private:
   const uint8_t* p_;

@@ -719,6 +719,14 @@ class GrpcStorageClient : public StorageClient {
     BufferingHandler h;
     auto call = std::make_shared<GrpcCall>(&h);
     auto c = conn();
+    // zero-copy send of the content (vmsplice + splice) when the source's
+    // bytes stay put until the final response; GCSB_UPLOAD_SPLICE=0 copies
+    static const bool splice_on = [] {
+      const char* e = std::getenv("GCSB_UPLOAD_SPLICE");
+      return !(e && *e == '0');
+    }();
+    const bool splice = splice_on && src.stable_until_done();
+    constexpr size_t kMinSplice = 64 << 10;  // below this a copy is cheaper than 2 syscalls
     c->start_stream(call, headers("WriteObject", bucket_res), false);
     try {
       src.seek(from);
@@ -737,11 +745,27 @@ class GrpcStorageClient : public StorageClient {
         uint64_t mlen = parts.head.size() + k + parts.tail.size();
         uint8_t pre[5] = {0, 0, 0, 0, 0};
         put_be32(pre + 1, static_cast<uint32_t>(mlen));
-        iovec iov[4] = {{pre, 5},
-                        {parts.head.data(), parts.head.size()},
-                        {const_cast<uint8_t*>(p), k},
-                        {parts.tail.data(), parts.tail.size()}};
-        c->send_data_iov(*call, iov, 4, last);
+        if (splice) {
+          // the content by page reference: the source keeps it unchanged
+          // until this upload's final response (ByteSource::stable_until_done)
+          std::vector<SendPiece> pieces(4);
+          pieces[0].p = pre;
+          pieces[0].n = 5;
+          pieces[1].p = reinterpret_cast<const uint8_t*>(parts.head.data());
+          pieces[1].n = parts.head.size();
+          pieces[2].p = p;
+          pieces[2].n = k;
+          pieces[2].splice = k >= kMinSplice;
+          pieces[3].p = reinterpret_cast<const uint8_t*>(parts.tail.data());
+          pieces[3].n = parts.tail.size();
+          c->send_data_pieces(*call, pieces, last);
+        } else {
+          iovec iov[4] = {{pre, 5},
+                          {parts.head.data(), parts.head.size()},
+                          {const_cast<uint8_t*>(p), k},
+                          {parts.tail.data(), parts.tail.size()}};
+          c->send_data_iov(*call, iov, 4, last);
+        }
         off += k;
         first = false;
         if (last) break;

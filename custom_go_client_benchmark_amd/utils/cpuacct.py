@@ -76,6 +76,11 @@ def delta_by_group(before: dict[str, float], after: dict[str, float]) -> dict[st
     return out
 
 
+def delta_by_name(before: dict[str, float], after: dict[str, float]) -> dict[str, float]:
+    """CPU seconds per thread name between two thread_cpu() snapshots."""
+    return {k: v - before.get(k, 0.0) for k, v in after.items() if v - before.get(k, 0.0) > 0}
+
+
 def per_gib(groups: dict[str, float], nbytes: float) -> dict[str, float]:
     gib = max(nbytes, 1.0) / (1 << 30)
     return {k: round(v / gib, 4) for k, v in sorted(groups.items())}

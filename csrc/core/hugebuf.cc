@@ -1,0 +1,30 @@
+#include "core/hugebuf.h"
+
+#include <sys/mman.h>
+
+#include <cstring>
+#include <new>
+
+namespace gcsb {
+
+uint8_t* huge_alloc(size_t n) {
+  const size_t huge = size_t(2) << 20;
+  const size_t len = huge_round(n ? n : 1);
+  // over-map by one huge page and trim, for 2 MiB alignment
+  void* raw = ::mmap(nullptr, len + huge, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (raw == MAP_FAILED) throw std::bad_alloc();
+  const uintptr_t a = (reinterpret_cast<uintptr_t>(raw) + huge - 1) & ~(huge - 1);
+  const size_t head = a - reinterpret_cast<uintptr_t>(raw);
+  if (head) ::munmap(raw, head);
+  if (huge - head) ::munmap(reinterpret_cast<void*>(a + len), huge - head);
+  void* p = reinterpret_cast<void*>(a);
+  (void)::madvise(p, len, MADV_HUGEPAGE);
+  std::memset(p, 0, len);  // fault in now, not inside a timed read
+  return static_cast<uint8_t*>(p);
+}
+
+void huge_free(void* p, size_t n) {
+  if (p) ::munmap(p, huge_round(n ? n : 1));
+}
+
+}  // namespace gcsb

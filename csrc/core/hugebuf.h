@@ -1,0 +1,49 @@
+// Page-cache-friendly receive destinations: 2 MiB-aligned anonymous memory
+// with MADV_HUGEPAGE, faulted in at allocation.
+//
+// Every object byte a socket delivers is written by the kernel's
+// copy_to_user into a destination like these.  Into the GPU sink's THP ring
+// one receiving core moves ~19-20 GB/s (0.05 CPU-s/GiB); the same copy into
+// 4 KiB-page heap blocks cost 0.09 CPU-s/GiB (profiles/r3_mux:
+// gcsb-h2-reader of the 48-worker discard-sink reads), a TLB miss every 4 KiB
+// of a 2 MiB message.  The discard sinks, the endpoint's upload receive
+// buffers and the CRC bench buffers use these.
+#pragma once
+#include <cstddef>
+#include <cstdint>
+
+namespace gcsb {
+
+// n bytes (rounded up to 2 MiB), 2 MiB-aligned, THP-advised, pre-faulted;
+// throws std::bad_alloc.  Free with huge_free(p, n) (same n).
+uint8_t* huge_alloc(size_t n);
+void huge_free(void* p, size_t n);
+inline size_t huge_round(size_t n) { return (n + (size_t(2) << 20) - 1) / (size_t(2) << 20) * (size_t(2) << 20); }
+
+// Owning, movable huge_alloc() buffer.
+class HugeBuffer {
+ public:
+  HugeBuffer() = default;
+  explicit HugeBuffer(size_t n) : p_(huge_alloc(n)), cap_(huge_round(n)) {}
+  ~HugeBuffer() { huge_free(p_, cap_); }
+  HugeBuffer(HugeBuffer&& o) noexcept : p_(o.p_), cap_(o.cap_) { o.p_ = nullptr, o.cap_ = 0; }
+  HugeBuffer& operator=(HugeBuffer&& o) noexcept {
+    if (this != &o) {
+      huge_free(p_, cap_);
+      p_ = o.p_, cap_ = o.cap_;
+      o.p_ = nullptr, o.cap_ = 0;
+    }
+    return *this;
+  }
+  HugeBuffer(const HugeBuffer&) = delete;
+  HugeBuffer& operator=(const HugeBuffer&) = delete;
+  char* get() const { return reinterpret_cast<char*>(p_); }
+  size_t capacity() const { return cap_; }
+  explicit operator bool() const { return p_ != nullptr; }
+
+ private:
+  uint8_t* p_ = nullptr;
+  size_t cap_ = 0;
+};
+
+}  // namespace gcsb

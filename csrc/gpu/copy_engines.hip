@@ -1,6 +1,6 @@
 // SDMA copy engines of a GPU: probe and warm-up.
 //
-// Measured (profiles/r3_stall): the first hipMemcpyAsync that lands on an
+// Measured (profiles/r3_sdma_engines): the first hipMemcpyAsync that lands on an
 // SDMA engine the process has not used yet blocks the CALLING thread for
 // ~7 ms while the runtime brings that engine's queue up; the copy itself then
 // takes 40 us.  Streams are spread over the engines by the runtime, so with 8
@@ -155,6 +155,7 @@ int warm_copy_engines(int device) {
       double ms = h2d ? timed_copy(b.dev, a.gpu, b.host, a.cpus[0], 4096, 1u << e, &err)
                       : timed_copy(static_cast<uint8_t*>(b.host) + 4096, a.cpus[0], b.dev, a.gpu, 4096, 1u << e, &err);
       if (ms >= 0) ++warmed;
+      if (err == "timeout") return warmed;  // a stuck engine: do not wait 5 s on each of the others
     }
   }
   return warmed;

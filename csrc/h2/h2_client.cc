@@ -128,6 +128,7 @@ void H2ClientConn::start_stream(const std::shared_ptr<H2ClientStream>& s, const 
     throw StorageError("http2 stream ids exhausted", true);
   }
   s->id_ = next_id_;
+  s->conn_frames_ = &frames_;
   next_id_ += 2;
   {
     std::lock_guard<std::mutex> lk(mu_);
@@ -154,6 +155,7 @@ void H2ClientConn::start_stream_with_body(const std::shared_ptr<H2ClientStream>&
       throw StorageError("http2 stream ids exhausted", true);
     }
     s->id_ = next_id_;
+    s->conn_frames_ = &frames_;
     next_id_ += 2;
     {
       std::lock_guard<std::mutex> lk(mu_);
@@ -283,6 +285,7 @@ void H2ClientConn::reader_loop() {
       FrameHeader fh = read_frame_header(*bc_);
       const int64_t t_frame = now_ns();
       last_frame_ns_.store(t_frame, std::memory_order_relaxed);
+      frames_.fetch_add(1, std::memory_order_relaxed);
       g_wait_ns.fetch_add(static_cast<uint64_t>(t_frame - t_wait), std::memory_order_relaxed);
       g_frames.fetch_add(1, std::memory_order_relaxed);
       struct Account {  // time of this frame's handling, by type

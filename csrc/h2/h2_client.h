@@ -35,6 +35,11 @@ class H2ClientStream {
   // cv.wait(lk, pred) with an idle limit: idle_ms > 0 gives up once the
   // stream saw no frame for a whole idle_ms window (so after idle_ms to
   // 2 x idle_ms of silence) and returns false; lk is held throughout.
+  // A window in which the connection delivered other streams' frames counts
+  // as progress up to kStarvedWindows times in a row: on a busy multiplexed
+  // connection a stream can wait behind its neighbours' frames (2 MiB gRPC
+  // messages) without its server having stalled.
+  static constexpr int kStarvedWindows = 3;
   template <class Pred>
   bool wait_progress(std::condition_variable& cv, std::unique_lock<std::mutex>& lk, Pred pred, int idle_ms) {
     if (idle_ms <= 0) {
@@ -50,11 +55,19 @@ class H2ClientStream {
     using Clock = std::chrono::steady_clock;
 #endif
     uint64_t seen = progress();
+    uint64_t conn_seen = conn_frames();
+    int starved = 0;
     for (;;) {
       if (cv.wait_until(lk, Clock::now() + std::chrono::milliseconds(idle_ms), pred)) return true;
-      const uint64_t now = progress();
-      if (now == seen) return false;
-      seen = now;
+      const uint64_t now = progress(), conn_now = conn_frames();
+      if (now != seen) {
+        seen = now;
+        conn_seen = conn_now;
+        starved = 0;
+        continue;
+      }
+      if (conn_now == conn_seen || ++starved > kStarvedWindows) return false;
+      conn_seen = conn_now;
     }
   }
 
@@ -62,6 +75,9 @@ class H2ClientStream {
   friend class H2ClientConn;
   uint32_t id_ = 0;
   std::atomic<uint64_t> progress_{0};
+  // frames the connection's reader has read (any stream); set by start_stream
+  const std::atomic<uint64_t>* conn_frames_ = nullptr;
+  uint64_t conn_frames() const { return conn_frames_ ? conn_frames_->load(std::memory_order_relaxed) : 0; }
   // reader dispatches into this stream in flight (taken under the
   // connection's stream-map lock, so none starts once the stream is erased)
   std::atomic<int> busy_{0};
@@ -147,6 +163,7 @@ class H2ClientConn {
   RecvWindow conn_recv_{64 << 20};
   std::atomic<bool> dead_{false}, goaway_{false};
   std::atomic<int64_t> last_frame_ns_{0};  // steady clock of the last frame header read
+  std::atomic<uint64_t> frames_{0};         // frames read (starvation vs stall, H2ClientStream::wait_progress)
   uint32_t goaway_last_ = 0x7FFFFFFF;
   mutable std::mutex reason_mu_;
   std::string dead_reason_;  // guarded by reason_mu_ (written by the reader thread)

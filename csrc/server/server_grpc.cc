@@ -19,6 +19,7 @@
 
 #include "core/affinity.h"
 #include "core/crc32c.h"
+#include "core/hugebuf.h"
 #include "core/util.h"
 #include "h2/h2.h"
 #include "net/buffered.h"
@@ -36,26 +37,32 @@ enum GrpcCode {
 
 // Unparsed request bytes of a stream; grows without zero-filling (upload
 // DATA frames are MiBs each) and keeps its capacity across messages.
+// THP-backed (core/hugebuf.h): the upload's receive copy lands here.
 struct RecvBuf {
-  std::unique_ptr<char[]> p;
+  char* p = nullptr;
   size_t n = 0, cap = 0;
+  RecvBuf() = default;
+  RecvBuf(const RecvBuf&) = delete;
+  RecvBuf& operator=(const RecvBuf&) = delete;
+  ~RecvBuf() { huge_free(p, cap); }
   char* grow(size_t k) {
     if (n + k > cap) {
-      size_t c = std::max(n + k, cap * 2);
-      std::unique_ptr<char[]> q(new char[c]);
-      if (n) std::memcpy(q.get(), p.get(), n);
-      p = std::move(q);
+      const size_t c = huge_round(std::max(n + k, cap * 2));
+      char* q = reinterpret_cast<char*>(huge_alloc(c));
+      if (n) std::memcpy(q, p, n);
+      huge_free(p, cap);
+      p = q;
       cap = c;
     }
-    char* d = p.get() + n;
+    char* d = p + n;
     n += k;
     return d;
   }
   void consume(size_t k) {
-    if (k < n) std::memmove(p.get(), p.get() + k, n - k);
+    if (k < n) std::memmove(p, p + k, n - k);
     n -= k;
   }
-  const char* data() const { return p.get(); }
+  const char* data() const { return p; }
   size_t size() const { return n; }
 };
 
@@ -83,20 +90,31 @@ struct ServerStream {
   // worker and not yet processed (guarded by the connection's wmu_)
   uint8_t wprefix[5] = {0, 0, 0, 0, 0};
   uint32_t wprefix_have = 0, wmsg_len = 0, wmsg_have = 0;
-  std::unique_ptr<char[]> wmsg;
-  size_t wmsg_cap = 0;
+  HugeBuffer wmsg;
   int wpending = 0;
 };
 
-// WriteObject messages are CRC32C-checked off the connection's reader thread
-// (GCSB_SRV_WRITE_WORKER=0 keeps the round-2 inline path, A/B): the reader
-// only recv()s, so one upload stream is bound by one copy, not copy + CRC.
+// GCSB_SRV_WRITE_WORKER=1: WriteObject messages are CRC32C-checked off the
+// connection's reader thread, on a write worker fed GCSB_SRV_WRITE_BUFS
+// (default 2) message buffers in rotation.  Measured (profiles/r3_write):
+// with 8 buffers the reader's receive copy got MORE expensive than receive +
+// CRC inline (0.09 vs 0.08 CPU-s/GiB: 16 MiB of destinations cycling out of
+// cache instead of one hot 2 MiB buffer), so inline stays the default.
 bool write_worker_enabled() {
   static const bool on = [] {
     const char* e = std::getenv("GCSB_SRV_WRITE_WORKER");
-    return !(e && *e == '0');
+    return e && *e == '1';
   }();
   return on;
+}
+
+size_t write_worker_bufs() {
+  static const size_t n = [] {
+    const char* e = std::getenv("GCSB_SRV_WRITE_BUFS");
+    const long v = e ? std::atol(e) : 2;
+    return static_cast<size_t>(std::max(1L, std::min(64L, v)));
+  }();
+  return n;
 }
 
 struct Cancelled {};
@@ -311,7 +329,7 @@ class H2ServerConn {
   // Reader thread: n bytes of a WriteObject stream's DATA.  Each gRPC message
   // is recv()'d straight into a buffer of its own; complete messages go to
   // the connection's write worker (decode, CRC32C check, append), in order.
-  // At most kMaxQueuedWrites messages wait per connection: past that the
+  // At most GCSB_SRV_WRITE_BUFS messages wait per connection: past that the
   // reader blocks, which stalls the socket and so the sender (backpressure).
   void recv_write_data(const std::shared_ptr<ServerStream>& sp, uint32_t n) {
     ServerStream& s = *sp;
@@ -324,9 +342,7 @@ class H2ServerConn {
         if (s.wprefix_have < 5) continue;
         s.wmsg_len = be32(s.wprefix + 1);
         s.wmsg_have = 0;
-        if (s.wmsg_cap < s.wmsg_len || !s.wmsg) {
-          s.wmsg = take_write_buffer(s.wmsg_len, &s.wmsg_cap);
-        }
+        if (!s.wmsg || s.wmsg.capacity() < s.wmsg_len) s.wmsg = take_write_buffer(s.wmsg_len);
         if (s.wmsg_len == 0) post_write_message(sp);
         continue;
       }
@@ -338,24 +354,22 @@ class H2ServerConn {
     }
   }
 
-  std::unique_ptr<char[]> take_write_buffer(size_t len, size_t* cap) {
+  HugeBuffer take_write_buffer(size_t len) {
     std::unique_lock<std::mutex> lk(wmu_);
-    wcv_.wait(lk, [&] { return wqueued_ < kMaxQueuedWrites || wstop_; });
+    wcv_.wait(lk, [&] { return wqueued_ < write_worker_bufs() || wstop_; });
     for (size_t i = 0; i < wfree_.size(); ++i)
-      if (wfree_[i].second >= len) {
-        auto b = std::move(wfree_[i].first);
-        *cap = wfree_[i].second;
+      if (wfree_[i].capacity() >= len) {
+        HugeBuffer b = std::move(wfree_[i]);
         wfree_.erase(wfree_.begin() + static_cast<long>(i));
         return b;
       }
-    *cap = std::max<size_t>(len, 64);
-    return std::unique_ptr<char[]>(new char[*cap]);
+    lk.unlock();
+    return HugeBuffer(std::max<size_t>(len, 64));
   }
 
   void post_write_message(const std::shared_ptr<ServerStream>& sp) {
     ServerStream& s = *sp;
-    WriteJob j{sp, std::move(s.wmsg), s.wmsg_cap, s.wmsg_len};
-    s.wmsg_cap = 0;
+    WriteJob j{sp, std::move(s.wmsg), s.wmsg_len};
     s.wprefix_have = 0;
     {
       std::lock_guard<std::mutex> lk(wmu_);
@@ -379,8 +393,8 @@ class H2ServerConn {
       lk.unlock();
       process_write_message(*j.s, std::string_view(j.buf.get(), j.len));
       lk.lock();
-      wfree_.emplace_back(std::move(j.buf), j.cap);
-      if (wfree_.size() > kMaxQueuedWrites) wfree_.erase(wfree_.begin());
+      wfree_.push_back(std::move(j.buf));
+      if (wfree_.size() > write_worker_bufs()) wfree_.erase(wfree_.begin());
       --wqueued_;
       --j.s->wpending;
       wcv_.notify_all();
@@ -406,7 +420,11 @@ class H2ServerConn {
     {
       std::lock_guard<std::mutex> lk(mu_);
       queue_.push_back(s);
-      if (idle_ == 0) pool_.emplace_back([this] { pool_loop(); });
+      // a thread per queued stream: an idle thread that was already woken
+      // still counts in idle_ until it runs, so `idle_ == 0` under-spawned --
+      // a second stream queued behind a first one whose handler then slept
+      // (a stalled or throttled response) waited for it
+      if (queue_.size() > static_cast<size_t>(idle_)) pool_.emplace_back([this] { pool_loop(); });
     }
     pool_cv_.notify_one();
   }
@@ -1024,15 +1042,13 @@ class H2ServerConn {
   // WriteObject write worker (recv_write_data)
   struct WriteJob {
     std::shared_ptr<ServerStream> s;
-    std::unique_ptr<char[]> buf;
-    size_t cap = 0;
+    HugeBuffer buf;
     uint32_t len = 0;
   };
-  static constexpr size_t kMaxQueuedWrites = 8;
   std::mutex wmu_;
   std::condition_variable wcv_;
   std::deque<WriteJob> wjobs_;
-  std::vector<std::pair<std::unique_ptr<char[]>, size_t>> wfree_;
+  std::vector<HugeBuffer> wfree_;
   size_t wqueued_ = 0;
   bool wstop_ = false;
   std::thread wworker_;

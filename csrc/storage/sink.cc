@@ -4,28 +4,90 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <new>
+#include <vector>
 
 #include "core/crc32c.h"
+#include "core/hugebuf.h"
 #include "core/util.h"
 
 namespace gcsb {
 
+namespace {
+// Process-wide LIFO pool of page-aligned, pre-faulted host blocks by size
+// (deferred DiscardSinks): the block handed out is the one handed back most
+// recently, still warm in cache.
+class HostBlockPool {
+ public:
+  static uint8_t* take(size_t n) {
+    {
+      std::lock_guard<std::mutex> lk(mu());
+      auto& v = free()[n];
+      if (!v.empty()) {
+        uint8_t* p = v.back();
+        v.pop_back();
+        return p;
+      }
+    }
+    return huge_alloc(n);  // THP: core/hugebuf.h
+  }
+  static void give(uint8_t* p, size_t n) {
+    std::lock_guard<std::mutex> lk(mu());
+    auto& v = free()[n];
+    if (v.size() * n < kMaxCached) {
+      v.push_back(p);
+      return;
+    }
+    huge_free(p, n);
+  }
+
+ private:
+  static constexpr size_t kMaxCached = size_t(512) << 20;
+  static std::mutex& mu() {
+    static std::mutex m;
+    return m;
+  }
+  static std::map<size_t, std::vector<uint8_t*>>& free() {
+    static auto* f = new std::map<size_t, std::vector<uint8_t*>>();  // outlives every sink
+    return *f;
+  }
+};
+}  // namespace
+
 DiscardSink::DiscardSink(size_t chunk_bytes, bool host_crc, bool deferred)
-    : cap_(chunk_bytes), host_crc_(host_crc), deferred_(deferred && host_crc) {
-  ring_ = deferred_ ? 4 * ((cap_ + 4095) / 4096 * 4096) : (cap_ + 4095) / 4096 * 4096;
-  buf_ = static_cast<uint8_t*>(std::aligned_alloc(4096, ring_));
-  // fault the pages in now, not inside the first timed read
-  std::memset(buf_, 0, ring_);
+    : cap_((chunk_bytes + 4095) / 4096 * 4096), host_crc_(host_crc), deferred_(deferred && host_crc) {
+  if (deferred_) {
+    // warm the pool with this sink's share, faulted in outside any read
+    uint8_t* b[kMaxBlocks];
+    for (auto& p : b) p = HostBlockPool::take(cap_);
+    for (auto& p : b) HostBlockPool::give(p, cap_);
+    return;
+  }
+  buf_ = huge_alloc(cap_);  // faulted in now, not inside the first timed read
 }
 
-DiscardSink::~DiscardSink() { std::free(buf_); }
+DiscardSink::~DiscardSink() {
+  if (deferred_) reset_ring();
+  huge_free(buf_, cap_);
+}
 
 void DiscardSink::reset_ring() {
   std::lock_guard<std::mutex> c(cmu_);
   std::lock_guard<std::mutex> q(qmu_);
+  // every block but the current one has its kRelease op queued
+  for (const Op& op : ops_)
+    if (op.kind == Op::kRelease) {
+      HostBlockPool::give(op.blk, cap_);
+      held_.fetch_sub(1, std::memory_order_relaxed);
+    }
   ops_.clear();
-  written_ = 0;
-  consumed_.store(0, std::memory_order_relaxed);
+  if (cur_) {
+    HostBlockPool::give(cur_, cap_);
+    held_.fetch_sub(1, std::memory_order_relaxed);
+    cur_ = nullptr;
+  }
+  cur_used_ = 0;
 }
 
 void DiscardSink::begin(const ObjectInfo& info) {
@@ -53,18 +115,22 @@ void DiscardSink::update_info(const ObjectInfo& info) {
 }
 
 Window DiscardSink::acquire(size_t want) {
-  if (!deferred_) {
-    (void)want;
-    return Window{buf_, cap_};
+  (void)want;
+  if (!deferred_) return Window{buf_, cap_};
+  if (cur_ && cur_used_ == cap_) {
+    Op op{Op::kRelease};
+    op.blk = cur_;
+    push(op);
+    cur_ = nullptr;
   }
-  for (;;) {
-    const uint64_t used = written_ - consumed_.load(std::memory_order_acquire);
-    if (used < ring_) {
-      const size_t p = static_cast<size_t>(written_ % ring_);
-      return Window{buf_ + p, std::min<size_t>(ring_ - p, ring_ - used)};
-    }
-    drain();  // ring full: the reader replays the oldest ops itself
+  if (!cur_) {
+    // backpressure: the worker fell kMaxBlocks behind, replay on this thread
+    while (held_.load(std::memory_order_acquire) >= kMaxBlocks) drain();
+    cur_ = HostBlockPool::take(cap_);
+    cur_used_ = 0;
+    held_.fetch_add(1, std::memory_order_relaxed);
   }
+  return Window{cur_ + cur_used_, cap_ - cur_used_};
 }
 
 void DiscardSink::push(const Op& op) {
@@ -75,10 +141,11 @@ void DiscardSink::push(const Op& op) {
 void DiscardSink::commit(size_t n) {
   if (deferred_) {
     Op op{Op::kData};
-    op.off = written_ % ring_;
+    op.blk = cur_;
+    op.off = cur_used_;
     op.len = n;
     push(op);
-    written_ += n;
+    cur_used_ += n;
     bytes_ += n;
     return;
   }
@@ -166,8 +233,11 @@ void DiscardSink::drain() {
     for (const Op& op : batch_) {
       switch (op.kind) {
         case Op::kData:
-          apply_data(buf_ + op.off, static_cast<size_t>(op.len));
-          consumed_.fetch_add(op.len, std::memory_order_release);
+          apply_data(op.blk + op.off, static_cast<size_t>(op.len));
+          break;
+        case Op::kRelease:
+          HostBlockPool::give(op.blk, cap_);
+          held_.fetch_sub(1, std::memory_order_release);
           break;
         case Op::kBegin: apply_chunk_begin(); break;
         case Op::kEnd: apply_chunk_end(op.has_crc, op.crc); break;
@@ -182,6 +252,12 @@ void DiscardSink::abort() {
 }
 
 SinkResult DiscardSink::finish() {
+  if (deferred_ && cur_) {  // the read is over: its last block goes back too
+    Op op{Op::kRelease};
+    op.blk = cur_;
+    push(op);
+    cur_ = nullptr;
+  }
   drain();
   SinkResult r;
   fold_chunk();

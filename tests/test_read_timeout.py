@@ -118,14 +118,16 @@ def test_one_stalled_stream_does_not_fail_its_neighbours(native, server, proto):
 
     server.add_synthetic(B, P, "", 0, 1, 3 << 20)
     server.add_synthetic(B, "small/file_", "", 0, 1, 256 << 10)
-    server.set_faults({"stall_at": 1 << 20, "stall_ms": 500, "stall_count": 1})
+    # (the neighbours keep the connection busy, which the stalled stream's
+    # idle check tolerates for 3 windows: 100 ms x (1 + 3) < the 800 ms stall)
+    server.set_faults({"stall_at": 1 << 20, "stall_ms": 800, "stall_count": 1})
     c = _client(native, server, proto, io_timeout_ms=100, retry_max_attempts=3)
     assert c.read(B, "small/file_0")["verified"]  # the connection is up
     stalled = []
     t = threading.Thread(target=lambda: stalled.append(c.read(B, P + "0")))
     t.start()
     neighbours = []
-    t_end = time.perf_counter() + 0.7
+    t_end = time.perf_counter() + 1.0
     while time.perf_counter() < t_end:
         neighbours.append(c.read(B, "small/file_0"))
     t.join()

@@ -3,6 +3,9 @@
 #include <sys/mman.h>
 
 #include <cstring>
+#include <map>
+#include <mutex>
+#include <vector>
 #include <new>
 
 namespace gcsb {
@@ -25,6 +28,51 @@ uint8_t* huge_alloc(size_t n) {
 
 void huge_free(void* p, size_t n) {
   if (p) ::munmap(p, huge_round(n ? n : 1));
+}
+
+namespace {
+std::mutex& pool_mu() {
+  static std::mutex m;
+  return m;
+}
+std::map<size_t, std::vector<uint8_t*>>& pool() {
+  static auto* f = new std::map<size_t, std::vector<uint8_t*>>();  // outlives every user
+  return *f;
+}
+size_t& pool_bytes() {
+  static size_t b = 0;
+  return b;
+}
+constexpr size_t kPoolMax = size_t(1) << 30;
+}  // namespace
+
+uint8_t* huge_take(size_t n) {
+  const size_t r = huge_round(n ? n : 1);
+  {
+    std::lock_guard<std::mutex> lk(pool_mu());
+    auto& v = pool()[r];
+    if (!v.empty()) {
+      uint8_t* p = v.back();
+      v.pop_back();
+      pool_bytes() -= r;
+      return p;
+    }
+  }
+  return huge_alloc(r);
+}
+
+void huge_give(void* p, size_t n) {
+  if (!p) return;
+  const size_t r = huge_round(n ? n : 1);
+  {
+    std::lock_guard<std::mutex> lk(pool_mu());
+    if (pool_bytes() + r <= kPoolMax) {
+      pool()[r].push_back(static_cast<uint8_t*>(p));
+      pool_bytes() += r;
+      return;
+    }
+  }
+  huge_free(p, r);
 }
 
 }  // namespace gcsb

@@ -209,6 +209,47 @@ class PinnedPool {
 };
 }  // namespace
 
+// Upload sources (a GpuByteSource per upload, 32 staging slots for a 64 MiB
+// object) recycle their completion events instead of creating and
+// destroying them per upload.  Per device, flags hipEventDisableTiming.
+class EventPool {
+ public:
+  static hipEvent_t get(int dev) {
+    {
+      std::lock_guard<std::mutex> lk(mu());
+      auto& v = free()[dev];
+      if (!v.empty()) {
+        hipEvent_t e = v.back();
+        v.pop_back();
+        return e;
+      }
+    }
+    hipEvent_t e = nullptr;
+    hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    return e;
+  }
+  static void put(int dev, hipEvent_t e) {
+    if (!e) return;
+    std::lock_guard<std::mutex> lk(mu());
+    auto& v = free()[dev];
+    if (v.size() < 1024) {
+      v.push_back(e);
+      return;
+    }
+    (void)hipEventDestroy(e);
+  }
+
+ private:
+  static std::mutex& mu() {
+    static std::mutex m;
+    return m;
+  }
+  static std::map<int, std::vector<hipEvent_t>>& free() {
+    static auto* f = new std::map<int, std::vector<hipEvent_t>>();  // process lifetime
+    return *f;
+  }
+};
+
 int gpu_device_count() {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -923,7 +964,7 @@ GpuByteSource::GpuByteSource(int device, const void* dptr, uint64_t n, size_t sl
   slot_len_.assign(nslots_, 0);
   for (int i = 0; i < nslots_; ++i) {
     host_[i] = static_cast<uint8_t*>(PinnedPool::get(slot_bytes_, device_numa_node(device_)));
-    hip_check(hipEventCreateWithFlags(&ev_[i], hipEventDisableTiming), "hipEventCreate");
+    ev_[i] = EventPool::get(device_);
   }
   tp[1] = now_ns();
   if (gpu_crc) {
@@ -966,7 +1007,7 @@ GpuByteSource::~GpuByteSource() {
   }
   for (int i = 0; i < nslots_; ++i) {
     PinnedPool::put(host_[i], slot_bytes_);
-    if (ev_[i]) (void)hipEventDestroy(ev_[i]);
+    EventPool::put(device_, ev_[i]);
   }
   if (own_stream_) (void)hipStreamDestroy(own_stream_);
 }

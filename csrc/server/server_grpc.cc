@@ -37,22 +37,35 @@ enum GrpcCode {
 
 // Unparsed request bytes of a stream; grows without zero-filling (upload
 // DATA frames are MiBs each) and keeps its capacity across messages.
-// THP-backed (core/hugebuf.h): the upload's receive copy lands here.
+// Requests (a few hundred bytes) stay on the heap; an upload's stream moves
+// to a pooled THP buffer (core/hugebuf.h) once it holds more than kSmall:
+// the upload's receive copy lands there.
 struct RecvBuf {
+  static constexpr size_t kSmall = 256 << 10;
   char* p = nullptr;
   size_t n = 0, cap = 0;
+  bool huge = false;
   RecvBuf() = default;
   RecvBuf(const RecvBuf&) = delete;
   RecvBuf& operator=(const RecvBuf&) = delete;
-  ~RecvBuf() { huge_free(p, cap); }
+  ~RecvBuf() { release(p, cap, huge); }
+  static void release(char* q, size_t c, bool h) {
+    if (h)
+      huge_give(q, c);
+    else
+      delete[] q;
+  }
   char* grow(size_t k) {
     if (n + k > cap) {
-      const size_t c = huge_round(std::max(n + k, cap * 2));
-      char* q = reinterpret_cast<char*>(huge_alloc(c));
+      const size_t want = std::max(n + k, cap * 2);
+      const bool h = want > kSmall;
+      const size_t c = h ? huge_round(want) : std::max<size_t>(want, 4096);
+      char* q = h ? reinterpret_cast<char*>(huge_take(c)) : new char[c];
       if (n) std::memcpy(q, p, n);
-      huge_free(p, cap);
+      release(p, cap, huge);
       p = q;
       cap = c;
+      huge = h;
     }
     char* d = p + n;
     n += k;

@@ -14,62 +14,23 @@
 
 namespace gcsb {
 
-namespace {
-// Process-wide LIFO pool of page-aligned, pre-faulted host blocks by size
-// (deferred DiscardSinks): the block handed out is the one handed back most
-// recently, still warm in cache.
-class HostBlockPool {
- public:
-  static uint8_t* take(size_t n) {
-    {
-      std::lock_guard<std::mutex> lk(mu());
-      auto& v = free()[n];
-      if (!v.empty()) {
-        uint8_t* p = v.back();
-        v.pop_back();
-        return p;
-      }
-    }
-    return huge_alloc(n);  // THP: core/hugebuf.h
-  }
-  static void give(uint8_t* p, size_t n) {
-    std::lock_guard<std::mutex> lk(mu());
-    auto& v = free()[n];
-    if (v.size() * n < kMaxCached) {
-      v.push_back(p);
-      return;
-    }
-    huge_free(p, n);
-  }
-
- private:
-  static constexpr size_t kMaxCached = size_t(512) << 20;
-  static std::mutex& mu() {
-    static std::mutex m;
-    return m;
-  }
-  static std::map<size_t, std::vector<uint8_t*>>& free() {
-    static auto* f = new std::map<size_t, std::vector<uint8_t*>>();  // outlives every sink
-    return *f;
-  }
-};
-}  // namespace
 
 DiscardSink::DiscardSink(size_t chunk_bytes, bool host_crc, bool deferred)
     : cap_((chunk_bytes + 4095) / 4096 * 4096), host_crc_(host_crc), deferred_(deferred && host_crc) {
   if (deferred_) {
     // warm the pool with this sink's share, faulted in outside any read
     uint8_t* b[kMaxBlocks];
-    for (auto& p : b) p = HostBlockPool::take(cap_);
-    for (auto& p : b) HostBlockPool::give(p, cap_);
+    for (auto& p : b) p = huge_take(cap_);
+    for (auto& p : b) huge_give(p, cap_);
     return;
   }
-  buf_ = huge_alloc(cap_);  // faulted in now, not inside the first timed read
+  buf_ = static_cast<uint8_t*>(std::aligned_alloc(4096, cap_));
+  std::memset(buf_, 0, cap_);  // fault the pages in now, not inside the first timed read
 }
 
 DiscardSink::~DiscardSink() {
   if (deferred_) reset_ring();
-  huge_free(buf_, cap_);
+  std::free(buf_);
 }
 
 void DiscardSink::reset_ring() {
@@ -78,12 +39,12 @@ void DiscardSink::reset_ring() {
   // every block but the current one has its kRelease op queued
   for (const Op& op : ops_)
     if (op.kind == Op::kRelease) {
-      HostBlockPool::give(op.blk, cap_);
+      huge_give(op.blk, cap_);
       held_.fetch_sub(1, std::memory_order_relaxed);
     }
   ops_.clear();
   if (cur_) {
-    HostBlockPool::give(cur_, cap_);
+    huge_give(cur_, cap_);
     held_.fetch_sub(1, std::memory_order_relaxed);
     cur_ = nullptr;
   }
@@ -126,7 +87,7 @@ Window DiscardSink::acquire(size_t want) {
   if (!cur_) {
     // backpressure: the worker fell kMaxBlocks behind, replay on this thread
     while (held_.load(std::memory_order_acquire) >= kMaxBlocks) drain();
-    cur_ = HostBlockPool::take(cap_);
+    cur_ = huge_take(cap_);
     cur_used_ = 0;
     held_.fetch_add(1, std::memory_order_relaxed);
   }
@@ -236,7 +197,7 @@ void DiscardSink::drain() {
           apply_data(op.blk + op.off, static_cast<size_t>(op.len));
           break;
         case Op::kRelease:
-          HostBlockPool::give(op.blk, cap_);
+          huge_give(op.blk, cap_);
           held_.fetch_sub(1, std::memory_order_release);
           break;
         case Op::kBegin: apply_chunk_begin(); break;

@@ -77,7 +77,8 @@ class Sink {
 // every stream of the connection, so a host CRC computed inside commit()
 // serialises all streams' checksums behind one core's receive copy
 // (profiles/r2_grpc_defer).  In deferred mode the bytes land in chunk_bytes
-// blocks taken from a process-wide LIFO pool, commit / chunk_begin /
+// THP blocks taken from the process-wide LIFO pool (core/hugebuf.h
+// huge_take), commit / chunk_begin /
 // chunk_end / resume_at only queue an op, and drain() -- called by the read's
 // own worker thread while it waits (poked at every message end) and by
 // finish() -- replays the ops in order and hands spent blocks back.  LIFO
@@ -123,7 +124,7 @@ class DiscardSink : public Sink {
   bool deferred_;
   uint8_t* cur_ = nullptr;               // deferred: block being filled (reader thread)
   size_t cur_used_ = 0;
-  std::atomic<int> held_{0};             // deferred: blocks taken and not yet handed back
+  std::atomic<int> held_{0};             // deferred: blocks (huge_take) not yet handed back
   std::mutex qmu_;                       // guards ops_
   std::vector<Op> ops_;
   std::mutex cmu_;                       // one replayer at a time, in order

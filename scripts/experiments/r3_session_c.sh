@@ -18,6 +18,7 @@ step() {  # step <name> <timeout> <cmd...>; a crash/abort/timeout ends the sessi
 step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step rehearsal8 500 env GCSB_DIST_BACKEND=gloo python3 bench.py --gpus 8 --object-size 64MiB --steps 5 --side-steps 3
+step write_trace 200 env GCSB_TRACE_SOURCE=1 python3 bench.py --workload write --steps 30 --warmup 3
 step rocprof 400 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d $O/prof -o bench -- \
   python3 bench.py --steps 10 --warmup 2
 echo done

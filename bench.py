@@ -54,6 +54,10 @@ def parse_size(s: str) -> int:
     return int(s)
 
 
+VMSTAT_KEYS = ("numa_hint_faults", "numa_pages_migrated", "thp_fault_alloc", "thp_collapse_alloc", "compact_stall",
+               "pgmajfault", "pgfault")
+
+
 def cpu_snapshot() -> dict:
     """Process CPU time (client + node-local endpoint share this process) and
     the cgroup's CFS throttling counters: on the GPU boxes the container runs
@@ -62,7 +66,18 @@ def cpu_snapshot() -> dict:
     import resource
 
     ru = resource.getrusage(resource.RUSAGE_SELF)
-    snap = {"user_s": ru.ru_utime, "sys_s": ru.ru_stime}
+    snap = {"user_s": ru.ru_utime, "sys_s": ru.ru_stime, "minflt": ru.ru_minflt, "nivcsw": ru.ru_nivcsw}
+    # host-wide memory-management events: NUMA-balancing hinting faults and
+    # migrations, THP faults / collapses, compaction stalls -- the kernel
+    # work that can slow a receive copy without showing in our own counters
+    try:
+        with open("/proc/vmstat") as f:
+            for line in f:
+                k, _, v = line.partition(" ")
+                if k in VMSTAT_KEYS:
+                    snap["vm_" + k] = int(v)
+    except OSError:
+        pass
     try:
         with open("/sys/fs/cgroup/cpu.stat") as f:
             for line in f:
@@ -102,6 +117,11 @@ def cpu_delta(a: dict, b: dict, nbytes: float, elapsed: float) -> dict:
     for k in ("nr_periods", "nr_throttled", "throttled_usec"):
         if k in a and k in b:
             out["cgroup_" + k] = b[k] - a[k]
+    out["process_minflt"] = b.get("minflt", 0) - a.get("minflt", 0)
+    out["process_involuntary_cs"] = b.get("nivcsw", 0) - a.get("nivcsw", 0)
+    vm = {k[3:]: b[k] - a[k] for k in b if k.startswith("vm_") and k in a and b[k] != a[k]}
+    if vm:
+        out["host_vmstat"] = vm
     return out
 
 

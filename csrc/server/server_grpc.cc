@@ -107,16 +107,18 @@ struct ServerStream {
   int wpending = 0;
 };
 
-// GCSB_SRV_WRITE_WORKER=1: WriteObject messages are CRC32C-checked off the
-// connection's reader thread, on a write worker fed GCSB_SRV_WRITE_BUFS
-// (default 2) message buffers in rotation.  Measured (profiles/r3_write):
-// with 8 buffers the reader's receive copy got MORE expensive than receive +
-// CRC inline (0.09 vs 0.08 CPU-s/GiB: 16 MiB of destinations cycling out of
-// cache instead of one hot 2 MiB buffer), so inline stays the default.
+// WriteObject messages are CRC32C-checked off the connection's reader thread,
+// on a write worker fed GCSB_SRV_WRITE_BUFS (default 2) pooled THP message
+// buffers in rotation; GCSB_SRV_WRITE_WORKER=0 checks them inline on the
+// reader (A/B).  Measured (profiles/r3_write): with 8 heap buffers the
+// reader's receive copy got MORE expensive than receive + CRC inline (0.09
+// vs 0.08 CPU-s/GiB, 16 MiB of 4 KiB-page destinations cycling out of cache);
+// with 2 THP buffers the reader drops to 0.043 - 0.059 and single-stream
+// uploads ran 15.4k - 22.2k MiB/s against 11.6k - 12.4k inline.
 bool write_worker_enabled() {
   static const bool on = [] {
     const char* e = std::getenv("GCSB_SRV_WRITE_WORKER");
-    return e && *e == '1';
+    return !(e && *e == '0');
   }();
   return on;
 }

@@ -429,6 +429,7 @@ def run_rank(args) -> int:
                 cpu["recv_avg_kib"] = round((rv1[1] - rv0[1]) / calls / 1024.0, 1)
         slow_hip = n.slow_hip_calls() if use_gpu else {}
         ring_numa = r1.ring_numa(0) if (r1 is not None and use_gpu) else []
+        ring_thp = r1.ring_thp_fraction(0) if (r1 is not None and use_gpu) else -1.0
         s1 = s1 or {"bytes": 0, "p50_ms": 0.0, "p99_ms": 0.0, "host_p50_ms": 0.0, "ttfb_p50_ms": 0.0, "slice_skew_ms": 0.0,
                     "verified": 0, "reads": 0}
         del r1
@@ -440,6 +441,7 @@ def run_rank(args) -> int:
         st["error"] = err
         st["cpu"] = cpu
         st["ring_numa"] = ring_numa
+        st["ring_thp"] = ring_thp
         # this rank's slowest reads [index in the timed run, ms, host-landed ms,
         # TTFB ms] and the slot hand-off HIP calls that blocked (>= 1 ms)
         st["slowest"] = [[int(x[0])] + [round(v, 3) for v in x[1:]] for x in (s1.get("slowest") or [])]
@@ -908,6 +910,9 @@ def run_rank(args) -> int:
                 # per slot: the node holding most of its pages (-1 = not resident)
                 out["numa"]["ring_slot_nodes"] = [max(range(len(c) - 1), key=lambda i: c[i]) if sum(c[:-1]) else -1
                                                   for c in slots]
+            if head.get("ring_thp", -1.0) >= 0:
+                # share of the pinned ring on transparent huge pages (the receive copy's TLB reach)
+                out["numa"]["ring_thp_fraction"] = round(head["ring_thp"], 3)
             if args.workload == "write":
                 out["rank0_slowest"] = head.get("slowest", [])
                 out["cpu_s_per_gib_by_thread"] = head.get("cpu_s_per_gib_by_thread", {})

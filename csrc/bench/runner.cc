@@ -12,6 +12,7 @@
 #include <random>
 
 #include "core/affinity.h"
+#include "core/hugebuf.h"
 #include "core/util.h"
 
 namespace gcsb {
@@ -72,6 +73,18 @@ uintptr_t Runner::landing_ptr(int w) const {
   if (landing_[w]) return reinterpret_cast<uintptr_t>(landing_[w]->data());
   if (gpu_sinks_[w]) return reinterpret_cast<uintptr_t>(gpu_sinks_[w]->object_device_ptr());
   return 0;
+}
+
+double Runner::ring_thp_fraction(int w) const {
+  if (w < 0 || w >= static_cast<int>(gpu_sinks_.size()) || !gpu_sinks_[w]) return -1;
+  long long thp = 0, all = 0;
+  for (const auto& [p, n] : gpu_sinks_[w]->ring_ranges()) {
+    const long long t = thp_bytes_of(p, n);
+    if (t < 0) return -1;
+    thp += t;
+    all += static_cast<long long>(n);
+  }
+  return all ? static_cast<double>(thp) / static_cast<double>(all) : -1;
 }
 
 std::vector<std::vector<long>> Runner::ring_numa(int w) const {

@@ -124,6 +124,9 @@ class Runner {
   uintptr_t landing_ptr(int w) const;
   // NUMA placement of worker w's pinned ring, per slot (affinity.h numa_nodes_of)
   std::vector<std::vector<long>> ring_numa(int w) const;
+  // Fraction of worker w's pinned ring backed by transparent huge pages
+  // (-1 unknown): a 4 KiB-page ring makes every receive copy TLB-bound.
+  double ring_thp_fraction(int w) const;
 
  private:
   void worker_main(int w);

@@ -2,6 +2,8 @@
 
 #include <sys/mman.h>
 
+#include <algorithm>
+#include <cstdio>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -45,6 +47,31 @@ size_t& pool_bytes() {
 }
 constexpr size_t kPoolMax = size_t(1) << 30;
 }  // namespace
+
+long long thp_bytes_of(const void* p, size_t len) {
+  FILE* f = std::fopen("/proc/self/smaps", "r");
+  if (!f) return -1;
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p), b = a + len;
+  char line[512];
+  bool in = false;
+  uintptr_t lo = 0, hi = 0;
+  long long total = 0;
+  while (std::fgets(line, sizeof(line), f)) {
+    unsigned long s = 0, e = 0;
+    if (std::sscanf(line, "%lx-%lx ", &s, &e) == 2 && std::strchr(line, '-') < std::strchr(line, ' ')) {
+      lo = s, hi = e;
+      in = hi > a && lo < b;
+      continue;
+    }
+    long long kb = 0;
+    if (in && std::sscanf(line, "AnonHugePages: %lld kB", &kb) == 1) {
+      const uintptr_t ov = std::min(hi, b) - std::max(lo, a);
+      total += std::min<long long>(kb * 1024, static_cast<long long>(ov));
+    }
+  }
+  std::fclose(f);
+  return total;
+}
 
 uint8_t* huge_take(size_t n) {
   const size_t r = huge_round(n ? n : 1);

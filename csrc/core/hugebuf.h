@@ -27,6 +27,12 @@ void huge_free(void* p, size_t n);
 // (profiles/r3_b).  Holds at most 1 GiB; beyond that buffers are unmapped.
 uint8_t* huge_take(size_t n);
 void huge_give(void* p, size_t n);
+
+// Bytes of [p, p+len) the kernel backs with transparent huge pages
+// (/proc/self/smaps AnonHugePages of the VMAs overlapping the range, capped
+// at len): MADV_HUGEPAGE is advice, and on a fragmented host the ring can
+// silently fall back to 4 KiB pages.  -1 if smaps is unreadable.
+long long thp_bytes_of(const void* p, size_t len);
 inline size_t huge_round(size_t n) { return (n + (size_t(2) << 20) - 1) / (size_t(2) << 20) * (size_t(2) << 20); }
 
 // Owning, movable huge_alloc() buffer.

@@ -9,6 +9,7 @@
 #include "bench/runner.h"
 #include "core/affinity.h"
 #include "core/ceiling.h"
+#include "core/hugebuf.h"
 #include "core/content.h"
 #include "core/crc32c.h"
 #include "core/util.h"
@@ -513,6 +514,7 @@ class PyRunner {
   std::string object_for(int w, int64_t seq) { return runner_->object_for(w, seq); }
   uintptr_t landing_ptr(int w) { return runner_->landing_ptr(w); }
   std::vector<std::vector<long>> ring_numa(int w) { return runner_->ring_numa(w); }
+  double ring_thp_fraction(int w) { return runner_->ring_thp_fraction(w); }
   std::string transport_path() { return runner_->client().transport_path(); }
   void set_reads_per_worker(int64_t n) { runner_->set_reads_per_worker(n); }
   void reset_stats() { runner_->reset_stats(); }
@@ -813,6 +815,7 @@ PYBIND11_MODULE(_native, m) {
     RecvStats r = recv_stats();
     return py::make_tuple(r.calls, r.bytes);
   });
+  m.def("thp_bytes_of", [](uintptr_t p, size_t n) { return thp_bytes_of(reinterpret_cast<const void*>(p), n); });
   m.def("h2_reader_stats", [] {
     H2ReaderStats s = h2_reader_stats();
     py::dict d;
@@ -991,6 +994,7 @@ PYBIND11_MODULE(_native, m) {
       .def("object_for", &PyRunner::object_for)
       .def("landing_ptr", &PyRunner::landing_ptr)
       .def("ring_numa", &PyRunner::ring_numa)
+      .def("ring_thp_fraction", &PyRunner::ring_thp_fraction)
       .def("transport_path", &PyRunner::transport_path)
       .def("set_reads_per_worker", &PyRunner::set_reads_per_worker)
       .def("reset_stats", &PyRunner::reset_stats);

@@ -24,13 +24,12 @@ DiscardSink::DiscardSink(size_t chunk_bytes, bool host_crc, bool deferred)
     for (auto& p : b) huge_give(p, cap_);
     return;
   }
-  buf_ = static_cast<uint8_t*>(std::aligned_alloc(4096, cap_));
-  std::memset(buf_, 0, cap_);  // fault the pages in now, not inside the first timed read
+  buf_ = huge_take(cap_);  // pooled THP (core/hugebuf.h), faulted in before any read
 }
 
 DiscardSink::~DiscardSink() {
   if (deferred_) reset_ring();
-  std::free(buf_);
+  if (buf_) huge_give(buf_, cap_);
 }
 
 void DiscardSink::reset_ring() {

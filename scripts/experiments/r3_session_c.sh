@@ -3,7 +3,7 @@
 set -u
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-O=gpurun_out/r3_c; mkdir -p $O
+O=${O_C:-gpurun_out/r3_c}; mkdir -p $O
 step() {  # step <name> <timeout> <cmd...>; a crash/abort/timeout ends the session
   local name=$1 t=$2; shift 2
   echo "=== $name ($(date +%T))"

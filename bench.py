@@ -201,6 +201,9 @@ def build_parser() -> argparse.ArgumentParser:
                          "objects, gRPC pool 1 vs HTTP keep-alive, discard sink + host CRC (0 = off)")
     ap.add_argument("--ref-reads", type=int, default=50, help="ref_default_*: timed reads per worker")
     ap.add_argument("--ref-object-size", default="1MiB", help="ref_default_*: object size")
+    ap.add_argument("--mux-reader", default="shared", choices=["shared", "isolate"],
+                    help="multiplexed blocks (list_read_grpc, ref_default_grpc): isolate gives the connection's "
+                         "reader thread a physical core the workers and endpoint do not use (affinity.isolate_reader)")
     ap.add_argument("--blocks", default="",
                     help="comma list of side blocks to run (A/B sessions): cpu_baseline, compare, sliced, ceiling, "
                          "ref_default, c1_http_cpu, list_read, write, write_composite, fanout; empty = all")
@@ -633,6 +636,8 @@ def run_rank(args) -> int:
         # "share" vs 13.5-15.2k with "same", profiles/r2_check_s4b,
         # profiles/r2_cli_geometry)
         sh = affinity.plan(gpu, "same", slot) if use_gpu else {"client": [], "server": []}
+        if use_gpu and proto != "http" and args.mux_reader == "isolate":
+            sh = affinity.isolate_reader(sh)
         ep = None
         names, list_ms, err = [], 0.0, ""
         try:
@@ -652,7 +657,8 @@ def run_rank(args) -> int:
         lslots, _, lbytes = args.list_ring.partition("x")
         over = {"protocol": proto, "endpoint": ep.url if ep is not None else "", "workers": workers,
                 "object_names": names or [f"c3_rank{rank}/file_0"], "cpus": sh["client"], "worker_id_offset": 0,
-                "rcvbuf": 0, "ring_slots": int(lslots), "ring_slot_bytes": parse_size(lbytes)}
+                "rcvbuf": 0, "ring_slots": int(lslots), "ring_slot_bytes": parse_size(lbytes),
+                "reader_cpus": sh.get("reader_cpus")}
         # every rank runs the block (and its collectives) whatever happened here
         st = read_block(over, per_pass, per_pass * warmup_passes, f"{proto} list-read")
         if err:
@@ -715,6 +721,8 @@ def run_rank(args) -> int:
         workers = args.ref_workers
         osz = parse_size(args.ref_object_size)
         sh = affinity.plan(gpu, "share_quota", slot) if use_gpu else {"client": [], "server": []}
+        if use_gpu and proto != "http" and args.mux_reader == "isolate":
+            sh = affinity.isolate_reader(sh)
         ep = None
         err = ""
         try:
@@ -725,7 +733,8 @@ def run_rank(args) -> int:
             err = f"{type(e).__name__}: {e}"
         over = {"protocol": proto, "endpoint": ep.url if ep is not None else "", "workers": workers,
                 "object_prefix": "ref_default/file_", "worker_id_offset": rank * workers, "sink": "discard",
-                "host_crc": True, "cpus": sh["client"], "rcvbuf": 0, "grpc_conn_pool_size": 1}
+                "host_crc": True, "cpus": sh["client"], "rcvbuf": 0, "grpc_conn_pool_size": 1,
+                "reader_cpus": sh.get("reader_cpus")}
         st = read_block(over, args.ref_reads, 2, f"{proto} reference default")
         if err:
             st["error"] = err

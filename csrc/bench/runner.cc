@@ -50,6 +50,7 @@ double percentile_floor(const std::vector<double>& sorted, int pct) {
 }
 
 Runner::Runner(RunnerConfig cfg) : cfg_(std::move(cfg)) {
+  reserve_fd_table();
   if (cfg_.workers <= 0) throw StorageError("worker count not valid", false);
   client_ = make_client(cfg_.client);
 }

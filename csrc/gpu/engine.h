@@ -59,6 +59,15 @@ struct GpuSinkConfig {
   // GPU box's CPU quota (16 CPUs) spinning waiters steal cycles from the
   // receiving threads.  Env GCSB_EVENT_SPIN=1 selects spinning.
   bool blocking_sync = true;
+  // > 0: wait for a slot's event by polling it (hipEventQuery) with sleeps of
+  // this many microseconds instead of hipEventSynchronize, whose blocking wait
+  // still spins inside the runtime before it sleeps: a short end-of-read wait
+  // (a 1 MiB read's last copy + CRC, tens of us) is then all spin, on a core
+  // the connection's receiving thread may share.  Config-3 list-read
+  // (profiles/r3_w48_tail): worker CPU 0.052 -> 0.024 CPU-s/GiB over gRPC,
+  // 0.23 -> 0.17 over HTTP, same MiB/s.  Env GCSB_WAIT_POLL_US (0 = the
+  // runtime's blocking wait).
+  int wait_poll_us = 10;
 };
 
 struct GpuSinkStats {
@@ -135,6 +144,7 @@ class GpuSink : public Sink {
   Slot& take_slot();
   void submit_current();
   void wait_slot(Slot& s);
+  void wait_event(hipEvent_t ev);
   void harvest(Slot& s);
   uint32_t shift(uint32_t v, uint64_t nbytes);
   void set_device() const;

@@ -16,6 +16,8 @@
 #include <stdexcept>
 
 #include <sys/mman.h>
+#include <sys/prctl.h>
+#include <time.h>
 
 #include "core/affinity.h"
 #include "core/crc32c.h"
@@ -496,6 +498,7 @@ void GpuSink::set_device() const { ensure_device(cfg_.device); }
 GpuSink::GpuSink(const GpuSinkConfig& cfg) : cfg_(cfg) {
   cfg_.async_submit = env_flag("GCSB_ASYNC_SUBMIT", cfg_.async_submit);
   if (env_flag("GCSB_EVENT_SPIN", false)) cfg_.blocking_sync = false;
+  if (const char* e = std::getenv("GCSB_WAIT_POLL_US")) cfg_.wait_poll_us = std::max(0, std::atoi(e));
   if (cfg_.slots < 2) cfg_.slots = 2;
   cfg_.slot_bytes = (cfg_.slot_bytes + 4095) / 4096 * 4096;
   if (cfg_.slot_bytes < 65536) cfg_.slot_bytes = 65536;
@@ -824,9 +827,26 @@ void GpuSink::wait_slot(Slot& s) {
     sub_cv_.wait(lk, [&] { return s.submitted; });
   }
   set_device();
-  hip_check(hipEventSynchronize(s.ev), "hipEventSynchronize");
+  wait_event(s.ev);
   s.inflight = false;
   harvest(s);
+}
+
+void GpuSink::wait_event(hipEvent_t ev) {
+  if (cfg_.wait_poll_us <= 0) {
+    hip_check(hipEventSynchronize(ev), "hipEventSynchronize");
+    return;
+  }
+  // the default 50 us timer slack would stretch every sleep
+  static thread_local const bool slack = prctl(PR_SET_TIMERSLACK, 1000UL, 0UL, 0UL, 0UL) == 0;
+  (void)slack;
+  const timespec ts{0, static_cast<long>(cfg_.wait_poll_us) * 1000L};
+  for (;;) {
+    const hipError_t e = hipEventQuery(ev);
+    if (e == hipSuccess) return;
+    if (e != hipErrorNotReady) hip_check(e, "hipEventQuery");
+    nanosleep(&ts, nullptr);
+  }
 }
 
 uint32_t GpuSink::shift(uint32_t v, uint64_t nbytes) {

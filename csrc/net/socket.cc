@@ -13,6 +13,7 @@
 #include <poll.h>
 #include <signal.h>
 #include <sys/sendfile.h>
+#include <sys/resource.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -163,6 +164,34 @@ std::string Conn::alpn() const {
   unsigned int n = 0;
   SSL_get0_alpn_selected(ssl_, &p, &n);
   return p ? std::string(reinterpret_cast<const char*>(p), n) : "";
+}
+
+int reserve_fd_table(int slots) {
+  static std::once_flag once;
+  static int reserved = 0;
+  std::call_once(once, [slots] {
+    rlimit rl{};
+    if (getrlimit(RLIMIT_NOFILE, &rl) != 0) return;
+    const rlim_t want = static_cast<rlim_t>(slots);
+    if (rl.rlim_cur < want && rl.rlim_max > rl.rlim_cur) {
+      rlimit up = rl;
+      up.rlim_cur = std::min<rlim_t>(rl.rlim_max, want);
+      if (setrlimit(RLIMIT_NOFILE, &up) == 0) rl = up;
+    }
+    const int top = static_cast<int>(std::min<rlim_t>(rl.rlim_cur, want)) - 1;
+    if (top < 64) return;
+    const int fd = ::open("/dev/null", O_RDONLY | O_CLOEXEC);
+    if (fd < 0) return;
+    // F_DUPFD takes the lowest free number >= top: the table grows to hold it
+    // (and never shrinks), and no descriptor in use is touched
+    const int hi = ::fcntl(fd, F_DUPFD_CLOEXEC, top);
+    if (hi >= 0) {
+      ::close(hi);
+      reserved = top + 1;
+    }
+    ::close(fd);
+  });
+  return reserved;
 }
 
 std::unique_ptr<Conn> Conn::dial(const Endpoint& ep, const SocketOptions& opt) {

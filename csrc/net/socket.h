@@ -56,6 +56,16 @@ struct RecvStats {
 };
 RecvStats recv_stats();
 
+// Grow the process's file-descriptor table to `slots` entries once, now.
+// The kernel doubles the table when an fd number outgrows it, and in a
+// multi-threaded process each growth waits out an RCU grace period while
+// every other thread's socket()/accept() sleeps behind it: a 48-worker run
+// dialing its last connections stalled ~150 ms at once (profiles/r3_w48_tail:
+// threads in D state, wait channel expand_files).  Raises the soft
+// RLIMIT_NOFILE toward `slots` when the hard limit allows.  Returns the
+// table size reserved (0 if nothing was done).
+int reserve_fd_table(int slots = 8192);
+
 class Conn {
  public:
   Conn() = default;

@@ -66,6 +66,8 @@ ClientConfig client_from(const py::dict& d) {
   c.sock.tls_ca_file = get_or<std::string>(d, "tls_ca_file", "");
   c.project = get_or<std::string>(d, "project", "gcs-fuse-test");
   if (d.contains("cpus") && !d["cpus"].is_none()) c.cpus = d["cpus"].cast<std::vector<int>>();
+  if (d.contains("reader_cpus") && !d["reader_cpus"].is_none())
+    c.reader_cpus = d["reader_cpus"].cast<std::vector<int>>();
   std::string auth = get_or<std::string>(d, "auth", "none");
   if (auth == "static") {
     c.token = std::make_shared<StaticTokenSource>(get_or<std::string>(d, "token", ""));
@@ -85,6 +87,7 @@ GpuSinkConfig gpu_from(const py::dict& d) {
   g.landing = get_or<std::string>(d, "landing", "object") == "ring" ? Landing::kRing : Landing::kObject;
   g.async_submit = get_or<bool>(d, "async_submit", g.async_submit);
   g.blocking_sync = get_or<bool>(d, "blocking_sync", g.blocking_sync);
+  g.wait_poll_us = get_or<int>(d, "wait_poll_us", g.wait_poll_us);
   return g;
 }
 
@@ -811,6 +814,7 @@ PYBIND11_MODULE(_native, m) {
   m.def("parse_cpulist", &parse_cpulist);
   m.def("pin_current_thread", &pin_current_thread);
   m.def("set_submitter_cpus", &set_submitter_cpus);
+  m.def("reserve_fd_table", &reserve_fd_table, py::arg("slots") = 8192);
   m.def("recv_stats", [] {
     RecvStats r = recv_stats();
     return py::make_tuple(r.calls, r.bytes);

@@ -23,6 +23,7 @@ FakeGcsServer::~FakeGcsServer() {
 }
 
 void FakeGcsServer::start() {
+  reserve_fd_table();
   // build the pattern buffer (+ its memfd for sendfile) before the first
   // request, so no read pays for it
   //

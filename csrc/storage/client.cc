@@ -116,6 +116,7 @@ ObjectMeta StorageClient::write_object(const std::string& bucket, const std::str
 }
 
 std::unique_ptr<StorageClient> make_client(const ClientConfig& cfg) {
+  reserve_fd_table();  // before the first dial, off any timed path
   if (cfg.protocol == "grpc") return make_grpc_client(cfg);
   if (cfg.protocol == "http" || cfg.protocol == "http2") return make_http_client(cfg);
   throw StorageError("unknown client protocol \"" + cfg.protocol + "\" (want http|http2|grpc)", false);

@@ -37,6 +37,10 @@ struct ClientConfig {
   std::shared_ptr<TokenSource> token;  // null = no Authorization header
   std::string project = "gcs-fuse-test";
   std::vector<int> cpus;  // transport/worker thread CPU set (empty = unpinned)
+  // the HTTP/2 (gRPC) connection reader threads' CPU set (empty = cpus): a
+  // multiplexed connection's one reader receives every stream's bytes, so it
+  // gets a physical core the workers do not share (affinity.isolate_reader)
+  std::vector<int> reader_cpus;
 };
 
 struct ObjectMeta {

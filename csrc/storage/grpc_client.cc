@@ -542,7 +542,7 @@ class GrpcStorageClient : public StorageClient {
     // shared reader thread of an idle multiplexed connection
     idle_ms_ = cfg.sock.io_timeout_ms;
     opt_.sock.io_timeout_ms = 0;
-    opt_.cpus = cfg.cpus;
+    opt_.cpus = cfg.reader_cpus.empty() ? cfg.cpus : cfg.reader_cpus;
     // DirectPath (reference main.go:106-117: GOOGLE_CLOUD_ENABLE_DIRECT_PATH_XDS
     // is set only around NewGRPCClient, with the google-c2p xDS resolver and
     // the RLS balancer linked in).  DirectPath needs the GCE metadata server,

@@ -565,7 +565,7 @@ class HttpStorageClient : public StorageClient {
     H2ClientOptions o;
     o.sock = with_alpn(cfg_.sock, "h2");
     o.sock.io_timeout_ms = 0;  // -read-timeout is per stream on the shared connection
-    o.cpus = cfg_.cpus;
+    o.cpus = cfg_.reader_cpus.empty() ? cfg_.cpus : cfg_.reader_cpus;
     return o;
   }();
   std::mutex h2_mu_;

@@ -269,6 +269,28 @@ def plan(device: int, mode: str = "split", slot: int = 0) -> dict:
     return {"client": client, "server": server, "mode": mode, "numa_node": node, "gpu_index_on_node": k}
 
 
+def isolate_reader(pl: dict, min_cores: int = 3) -> dict:
+    """A copy of plan `pl` whose client set gives one physical core to the
+    multiplexed connection's reader thread alone: "reader_cpus" is one
+    hardware thread of the quietest client core, and "client" (the workers)
+    loses that whole core, SMT sibling included.  A gRPC connection carrying
+    every worker's stream is bound by its one reader thread's receive copy;
+    next to a busy sibling (a worker CRC'ing, or spinning in an event wait)
+    that copy runs slower.  Unchanged when the client set has fewer than
+    `min_cores` physical cores."""
+    client = list(pl.get("client") or [])
+    cores = quiet_cores(client, cpu_busy(0.05)) if client else []
+    if len(cores) < min_cores:
+        return dict(pl)
+    core = cores[0]
+    out = dict(pl)
+    out["reader_cpus"] = [core[0]]
+    out["client"] = [c for c in client if c not in core]
+    if pl.get("server") == pl.get("client"):  # shared sets: keep the endpoint off the reader's core too
+        out["server"] = list(out["client"])
+    return out
+
+
 def visible_gpu_summary() -> list[dict]:
     out = []
     for d in range(_native.gpu_device_count()):

@@ -25,6 +25,7 @@ ap.add_argument("--reads", type=int, default=50)
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--slow-ms", type=float, default=20.0)
 ap.add_argument("--warm-reads", type=int, default=2)
+ap.add_argument("--isolate-reader", action="store_true", help="affinity.isolate_reader: a core of its own for the h2 reader")
 ap.add_argument("--gap-s", type=float, default=0.0, help="sleep between the warm-up and rep 0")
 ap.add_argument("--sample-ms", type=float, default=400.0, help="sample thread states for this long per rep (0: off)")
 args = ap.parse_args()
@@ -44,6 +45,17 @@ def tasks():
         comm = st[st.index("(") + 1:st.rindex(")")]
         out[tid] = (re.sub(r"[-_]?\d+$", "", comm), st[st.rindex(")") + 2], rd)
     return out
+
+
+def blocked_in(tid):
+    out = []
+    for f in ("syscall", "wchan"):
+        try:
+            with open(f"/proc/self/task/{tid}/{f}") as fh:
+                out.append(fh.read().split()[0] if f == "syscall" else fh.read().strip())
+        except (OSError, IndexError):
+            out.append("?")
+    return ":".join(out)
 
 
 def vmstat():
@@ -70,20 +82,25 @@ class Sampler(threading.Thread):
         t0 = time.perf_counter()
         while (time.perf_counter() - t0) * 1e3 < self.ms:
             c = {}
-            for comm, state, _ in tasks().values():
+            for tid, (comm, state, _) in tasks().items():
                 if state != "S":
-                    c[f"{comm}:{state}"] = c.get(f"{comm}:{state}", 0) + 1
+                    key = f"{comm}:{state}"
+                    if state == "D":  # where in the kernel: syscall number and wait channel
+                        key += f":sys{blocked_in(tid)}"
+                    c[key] = c.get(key, 0) + 1
             self.timeline.append((round((time.perf_counter() - t0) * 1e3, 1), c))
             time.sleep(0.002)
 
 n = pkg._native
 sh = affinity.plan(0, "share_quota", 0)
+if args.isolate_reader:
+    sh = affinity.isolate_reader(sh)
 srv = n.Server({"port": 0, "md5": False, "cpus": sh["server"], "retain_uploads": False})
 srv.start()
 srv.add_synthetic("b", "ref/file_", "", 0, args.workers, 1 << 20)
 cfg = {"protocol": args.protocol, "endpoint": srv.url, "bucket": "b", "object_prefix": "ref/file_",
        "workers": args.workers, "reads_per_worker": args.warm_reads, "sink": "discard", "host_crc": True, "cpus": sh["client"],
-       "keep_records": True, "grpc_conn_pool_size": 1}
+       "keep_records": True, "grpc_conn_pool_size": 1, "reader_cpus": sh.get("reader_cpus")}
 r = n.Runner(cfg)
 r.start()
 r.wait()
@@ -112,7 +129,7 @@ for rep in range(args.reps):
     base = min(x["start_ns"] for x in recs)
     slow = sorted((x for x in recs if (x["end_ns"] - x["start_ns"]) / 1e6 >= args.slow_ms),
                   key=lambda x: x["start_ns"])
-    print(json.dumps({"rep": rep, "mib_s": round(s["mib_per_s"], 1), "p50_ms": round(s["p50_ms"], 3),
+    print(json.dumps({"rep": rep, "reader_cpus": sh.get("reader_cpus"), "mib_s": round(s["mib_per_s"], 1), "p50_ms": round(s["p50_ms"], 3),
                       "p99_ms": round(s["p99_ms"], 3), "max_ms": round(s["max_ms"], 3), "reads": len(recs),
                       "run_ms": round((max(x["end_ns"] for x in recs) - base) / 1e6, 1),
                       "slow": [{"worker": x["worker"], "seq": x["seq"],

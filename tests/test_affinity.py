@@ -230,3 +230,35 @@ def test_eight_ranks_of_a_node_get_disjoint_gpu_local_cpus(monkeypatch, mode):
     for i in range(8):
         for j in range(i + 1, 8):
             assert not (sets[i] & sets[j]), (mode, i, j, sorted(sets[i] & sets[j]))
+
+
+def test_isolate_reader_gives_the_reader_a_whole_core(monkeypatch):
+    """The multiplexed connection's reader gets one hardware thread of the
+    quietest client core; neither the workers nor a shared endpoint keep
+    either thread of that core."""
+    from custom_go_client_benchmark_amd.parallel import affinity as a
+
+    _fake_topology(monkeypatch, a)
+    busy = {c: 0.0 for c in range(16)}
+    busy[1] = busy[9] = 0.9
+    monkeypatch.setattr(a, "cpu_busy", lambda sample_s=0.15: busy)
+    pl = {"client": list(range(16)), "server": list(range(16)), "mode": "share_quota"}
+    out = a.isolate_reader(pl)
+    (r,) = out["reader_cpus"]
+    core = {c for c in range(16) if a._same_core(c, r)}
+    assert len(core) == 2 and 0 not in core and 1 not in core
+    assert not core & set(out["client"]) and not core & set(out["server"])
+    assert set(out["client"]) | core == set(range(16))
+    assert pl["client"] == list(range(16))  # the input plan is not modified
+    # too few cores to spare one: unchanged
+    small = {"client": [2, 10], "server": [3, 11]}
+    assert a.isolate_reader(small) == small
+
+
+def test_fd_table_reserved(native):
+    import resource
+
+    n = native.reserve_fd_table()
+    soft, _ = resource.getrlimit(resource.RLIMIT_NOFILE)
+    assert n == 0 or 64 < n <= max(soft, 64)
+    assert native.reserve_fd_table() == n  # once per process

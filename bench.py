@@ -201,6 +201,9 @@ def build_parser() -> argparse.ArgumentParser:
                          "objects, gRPC pool 1 vs HTTP keep-alive, discard sink + host CRC (0 = off)")
     ap.add_argument("--ref-reads", type=int, default=50, help="ref_default_*: timed reads per worker")
     ap.add_argument("--ref-object-size", default="1MiB", help="ref_default_*: object size")
+    ap.add_argument("--list-rcvbuf", default="64MiB",
+                    help="config-3 list-read blocks: client SO_RCVBUF (0 = kernel autotuning; 64 MiB as the headline, "
+                         "profiles/r3_w48_tail)")
     ap.add_argument("--mux-reader", default="shared", choices=["shared", "isolate"],
                     help="multiplexed blocks (list_read_grpc, ref_default_grpc): isolate gives the connection's "
                          "reader thread a physical core the workers and endpoint do not use (affinity.isolate_reader)")
@@ -657,7 +660,7 @@ def run_rank(args) -> int:
         lslots, _, lbytes = args.list_ring.partition("x")
         over = {"protocol": proto, "endpoint": ep.url if ep is not None else "", "workers": workers,
                 "object_names": names or [f"c3_rank{rank}/file_0"], "cpus": sh["client"], "worker_id_offset": 0,
-                "rcvbuf": 0, "ring_slots": int(lslots), "ring_slot_bytes": parse_size(lbytes),
+                "rcvbuf": parse_size(args.list_rcvbuf), "ring_slots": int(lslots), "ring_slot_bytes": parse_size(lbytes),
                 "reader_cpus": sh.get("reader_cpus")}
         # every rank runs the block (and its collectives) whatever happened here
         st = read_block(over, per_pass, per_pass * warmup_passes, f"{proto} list-read")
@@ -956,6 +959,8 @@ def run_rank(args) -> int:
                     b["cpus_busy"] = st["cpu"].get("cpus_busy")
                     if st["cpu"].get("h2_reader"):
                         b["h2_reader"] = st["cpu"]["h2_reader"]
+                    if st["cpu"].get("recv_avg_kib") is not None:
+                        b["recv_avg_kib"] = st["cpu"]["recv_avg_kib"]
                 if key.startswith("ref_default_"):
                     b["first_read_p50_ms"] = round(st["first_p50_max"], 3)
                     b["steady_p99_ms"] = round(st["steady_p99_max"], 3)

@@ -1,0 +1,132 @@
+# Round-3 GPU-box sessions, one function per session:
+#   bash scripts/experiments/r3_sessions.sh <session>
+# Each writes under gpurun_out/r3_<session>/. The summaries were copied into
+# the profile directory named in the comment (see scripts/README.md).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+export TMPDIR=/tmp
+S=${1:?usage: r3_sessions.sh <session>}
+O=gpurun_out/r3_$S
+mkdir -p "$O"
+
+step() {  # step <name> <timeout> <cmd...>: a crash, abort or timeout ends the session
+  local name=$1 t=$2
+  shift 2
+  echo "=== $name ($(date +%T))"
+  local t0
+  t0=$(date +%s.%N)
+  timeout -k 10 "$t" "$@" > "$O/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc wall_s=$(python3 -c "print(round($(date +%s.%N)-$t0,1))")"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+    echo "fatal rc=$rc in $name: stopping"
+    exit $rc
+  fi
+  return 0
+}
+
+case "$S" in
+stall)  # profiles/r3_sdma_engines: which hand-off HIP call blocks after a device sync
+  step probe_default 200 python3 scripts/experiments/sync_stall_probe.py --reps 8
+  step probe_hwq8 200 env GPU_MAX_HW_QUEUES=8 python3 scripts/experiments/sync_stall_probe.py --reps 8
+  step probe_pool4 200 env GCSB_STREAMS=4 python3 scripts/experiments/sync_stall_probe.py --reps 8
+  step bench 300 python3 bench.py --steps 20 --warmup 5
+  step trace 300 rocprofv3 --hip-runtime-trace --memory-copy-trace --kernel-trace --output-format csv -d "$O/trace" \
+    -o b -- python3 scripts/experiments/sync_stall_probe.py --reps 4 --variants sync
+  ;;
+engines)  # profiles/r3_sdma_engines: per-engine first-use cost; bench with the warm-up off / on
+  step engines 120 env GCSB_WARM_ENGINES=0 python3 scripts/experiments/copy_engines_probe.py
+  for i in 1 2; do
+    for w in 0 1; do
+      step "bench_w${w}_$i" 300 env GCSB_WARM_ENGINES=$w python3 bench.py --steps 20 --warmup 5 --list-objects 0
+    done
+  done
+  ;;
+write)  # profiles/r3_write: spliced vs copied send; endpoint CRC inline vs on a write worker
+  for i in 1 2; do
+    for v in "1 0 2" "1 1 2" "1 1 1" "0 0 2"; do
+      set -- $v
+      step "write_s$1_w$2_b$3_$i" 200 env GCSB_UPLOAD_SPLICE=$1 GCSB_SRV_WRITE_WORKER=$2 GCSB_SRV_WRITE_BUFS=$3 \
+        python3 bench.py --workload write --steps 30 --warmup 3
+    done
+  done
+  ;;
+mux)  # profiles/r3_mux: ring geometry of the multiplexed list-read
+  for i in 1 2; do
+    for ring in 8x2MiB 2x1MiB 4x512KiB; do
+      step "mux_${ring}_$i" 200 python3 bench.py --steps 5 --warmup 2 --side-steps 5 --blocks list_read,ref_default \
+        --list-ring "$ring"
+    done
+  done
+  ;;
+b)  # profiles/r3_mux, r3_write: full bench, then the multiplexed and upload blocks twice
+  step bench 300 python3 bench.py --steps 20 --warmup 5
+  for i in 1 2; do
+    step "mux_$i" 200 python3 bench.py --steps 5 --warmup 2 --side-steps 5 --blocks list_read,ref_default
+    for w in 0 1; do
+      step "write_w${w}_$i" 200 env GCSB_SRV_WRITE_WORKER=$w python3 bench.py --workload write --steps 30 --warmup 3
+    done
+  done
+  ;;
+check)  # profiles/r3_gpu_check, r3_rehearsal8: GPU suite, smoke, 8-rank gloo rehearsal, kernel profile
+  step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread
+  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+  step rehearsal8 500 env GCSB_DIST_BACKEND=gloo python3 bench.py --gpus 8 --object-size 64MiB --steps 5 --side-steps 3
+  step rocprof 400 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$O/prof" -o bench -- \
+    python3 bench.py --steps 10 --warmup 2
+  ;;
+benches)  # profiles/r3_gpu_check: three full benches back to back, host memory-management settings
+  for i in 1 2 3; do
+    step "bench_$i" 300 python3 bench.py --steps 20 --warmup 5
+  done
+  cat /proc/sys/kernel/numa_balancing /sys/kernel/mm/transparent_hugepage/enabled \
+    /sys/kernel/mm/transparent_hugepage/defrag > "$O/host_mm.txt" 2>&1
+  ;;
+reader)  # profiles/r3_reader_cost: one gRPC stream's receive cost by component, then a bench
+  step reader_cost 300 python3 scripts/experiments/reader_cost_probe.py --reps 3
+  step bench 300 python3 bench.py --steps 20 --warmup 5
+  grep -E "AnonHugePages|HugePages_|Hugepagesize" /proc/meminfo > "$O/meminfo.txt"
+  ;;
+bench_vs_probe)  # profiles/r3_reader_cost/session_f: bench (RCCL / gloo control plane) interleaved with the probe
+  step bench_rccl_1 300 python3 bench.py --steps 20 --warmup 5 --blocks cpu_baseline,ceiling
+  step probe_1 200 python3 scripts/experiments/reader_cost_probe.py --reps 1
+  step bench_gloo 300 env GCSB_DIST_BACKEND=gloo python3 bench.py --steps 20 --warmup 5 --blocks cpu_baseline,ceiling
+  step probe_2 200 python3 scripts/experiments/reader_cost_probe.py --reps 1
+  step bench_rccl_2 300 python3 bench.py --steps 20 --warmup 5 --blocks cpu_baseline,ceiling
+  ;;
+w48)  # profiles/r3_w48_tail: the 48-worker first-rep stall (thread states, syscalls, wait channels)
+  step w48_default 200 python3 scripts/experiments/w48_tail_probe.py --reps 3
+  step w48_warm20 200 python3 scripts/experiments/w48_tail_probe.py --reps 2 --warm-reads 20
+  step w48_gap3 200 python3 scripts/experiments/w48_tail_probe.py --reps 2 --gap-s 3
+  step w48_grpc 200 python3 scripts/experiments/w48_tail_probe.py --protocol grpc --reps 2 --slow-ms 30
+  ;;
+poll)  # profiles/r3_w48_tail/session_i: end-of-read event wait, runtime sync vs poll
+  for k in 1 2; do
+    step "list_sync_$k" 300 env GCSB_WAIT_POLL_US=0 python3 bench.py --steps 5 --warmup 2 --blocks list_read
+    step "list_poll_$k" 300 env GCSB_WAIT_POLL_US=10 python3 bench.py --steps 5 --warmup 2 --blocks list_read
+  done
+  ;;
+muxreader)  # profiles/r3_w48_tail/session_j: isolated reader core, list-read receive buffer
+  step w48_http 200 python3 scripts/experiments/w48_tail_probe.py --reps 2
+  for k in 1 2; do
+    step "w48_grpc_shared_$k" 200 python3 scripts/experiments/w48_tail_probe.py --protocol grpc --reps 2 --sample-ms 0
+    step "w48_grpc_isolate_$k" 200 python3 scripts/experiments/w48_tail_probe.py --protocol grpc --reps 2 --sample-ms 0 \
+      --isolate-reader
+    step "bench_shared_$k" 300 python3 bench.py --steps 5 --warmup 2 --blocks list_read,ref_default --list-rcvbuf 0
+    step "bench_isolate_$k" 300 python3 bench.py --steps 5 --warmup 2 --blocks list_read,ref_default --list-rcvbuf 0 \
+      --mux-reader isolate
+    step "bench_rcvbuf_$k" 300 python3 bench.py --steps 5 --warmup 2 --blocks list_read --list-rcvbuf 64MiB
+  done
+  ;;
+final)  # profiles/r3_final: GPU suite, smoke, two full benches
+  step pytest_gpu 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+  step smoke 200 python3 -c "import __graft_entry__ as g; g.smoke()"
+  step bench_1 400 python3 bench.py
+  step bench_2 400 python3 bench.py
+  ;;
+*)
+  echo "unknown session $S" >&2
+  exit 2
+  ;;
+esac
+echo "session $S done"

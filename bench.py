@@ -201,6 +201,10 @@ def build_parser() -> argparse.ArgumentParser:
                          "objects, gRPC pool 1 vs HTTP keep-alive, discard sink + host CRC (0 = off)")
     ap.add_argument("--ref-reads", type=int, default=50, help="ref_default_*: timed reads per worker")
     ap.add_argument("--ref-object-size", default="1MiB", help="ref_default_*: object size")
+    ap.add_argument("--write-placement", default="share", choices=["share", "pair"],
+                    help="config-5 upload block: share (uploader and endpoint threads over the rank's share of "
+                         "L3 domains) or pair (uploader on one quiet core, endpoint receive + CRC on two more of "
+                         "the same L3 domain)")
     ap.add_argument("--list-rcvbuf", default="64MiB",
                     help="config-3 list-read blocks: client SO_RCVBUF (0 = kernel autotuning; 64 MiB as the headline, "
                          "profiles/r3_w48_tail)")
@@ -482,7 +486,16 @@ def run_rank(args) -> int:
         ep = None
         saved_aff = os.sched_getaffinity(0)
         try:
-            ep, sh = share_endpoint()
+            if parts == 1 and use_gpu and args.write_placement == "pair":
+                # three quiet cores of one L3 domain: the uploader (this
+                # thread) on one, the endpoint's receive and CRC threads on
+                # the other two
+                pl = affinity.plan(gpu, "pair", slot)
+                sh = {"client": pl["client"], "server": sorted(pl["server"] + pl.get("aux", []))}
+                ep = n.Server({"port": 0, "md5": False, "cpus": sh["server"], "retain_uploads": False})
+                ep.start()
+            else:
+                ep, sh = share_endpoint()
             # the upload runs on this (Python main) thread: keep it, its
             # connection reader and the pinned staging ring it allocates on
             # the GPU's NUMA node (the rank's share of L3 domains); unpinned

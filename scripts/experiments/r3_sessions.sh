@@ -118,6 +118,13 @@ muxreader)  # profiles/r3_w48_tail/session_j: isolated reader core, list-read re
     step "bench_rcvbuf_$k" 300 python3 bench.py --steps 5 --warmup 2 --blocks list_read --list-rcvbuf 64MiB
   done
   ;;
+wplace)  # profiles/r3_write/placement: config-5 upload, share vs pair placement, interleaved
+  for k in 1 2 3; do
+    for pl in share pair; do
+      step "write_${pl}_$k" 200 python3 bench.py --workload write --steps 30 --warmup 3 --write-placement $pl
+    done
+  done
+  ;;
 final)  # profiles/r3_final: GPU suite, smoke, two full benches
   step pytest_gpu 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
   step smoke 200 python3 -c "import __graft_entry__ as g; g.smoke()"

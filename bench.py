@@ -201,10 +201,10 @@ def build_parser() -> argparse.ArgumentParser:
                          "objects, gRPC pool 1 vs HTTP keep-alive, discard sink + host CRC (0 = off)")
     ap.add_argument("--ref-reads", type=int, default=50, help="ref_default_*: timed reads per worker")
     ap.add_argument("--ref-object-size", default="1MiB", help="ref_default_*: object size")
-    ap.add_argument("--write-placement", default="share", choices=["share", "pair"],
-                    help="config-5 upload block: share (uploader and endpoint threads over the rank's share of "
-                         "L3 domains) or pair (uploader on one quiet core, endpoint receive + CRC on two more of "
-                         "the same L3 domain)")
+    ap.add_argument("--write-placement", default="pair", choices=["share", "pair"],
+                    help="config-5 upload block: pair (uploader on one quiet core, endpoint receive + CRC on two "
+                         "more of the same L3 domain; 18.0-21.6k MiB/s in 6 runs) or share (uploader and endpoint "
+                         "threads over the rank's share of L3 domains; 7.7-19.7k, profiles/r3_write/placement)")
     ap.add_argument("--list-rcvbuf", default="64MiB",
                     help="config-3 list-read blocks: client SO_RCVBUF (0 = kernel autotuning; 64 MiB as the headline, "
                          "profiles/r3_w48_tail)")
@@ -489,7 +489,10 @@ def run_rank(args) -> int:
             if parts == 1 and use_gpu and args.write_placement == "pair":
                 # three quiet cores of one L3 domain: the uploader (this
                 # thread) on one, the endpoint's receive and CRC threads on
-                # the other two
+                # the other two.  Spread over the share, the endpoint's
+                # receive thread paid 0.08-0.12 CPU-s/GiB in half the runs
+                # (0.043-0.059 paired) and the upload ran at 7.7-11k MiB/s
+                # instead of 18-21.6k (profiles/r3_write/placement)
                 pl = affinity.plan(gpu, "pair", slot)
                 sh = {"client": pl["client"], "server": sorted(pl["server"] + pl.get("aux", []))}
                 ep = n.Server({"port": 0, "md5": False, "cpus": sh["server"], "retain_uploads": False})

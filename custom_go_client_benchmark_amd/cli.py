@@ -146,15 +146,24 @@ def main(argv: list[str] | None = None) -> int:
         else:
             aff = "quota"
         if fs.get("workload") == "write":
-            # uploads: unpinned threads measured fastest on MI355X (64 MiB
-            # WriteObject 8.1 ms vs 13.8-14.4 ms pinned; resumable HTTP 6.5 vs
-            # 6.7-7.8 ms), profiles/r1_session4/
-            aff = "none"
+            # uploads: one from HBM (spliced send, endpoint CRC on its write
+            # worker) on three quiet cores of one L3 domain -- the uploader,
+            # the endpoint's receive thread, its CRC worker -- 18.0-21.6k
+            # MiB/s against 7.7-19.7k with the threads spread
+            # (profiles/r3_write/placement); composite uploads (slices > 1)
+            # and CPU-only runs stay unpinned (profiles/r1_session4/)
+            aff = "pair" if sink == "gpu" and fs.get("slices") <= 1 else "none"
     if aff != "none" and (sink == "gpu" or aff == "quota"):
         from .parallel import affinity
 
         placement = affinity.plan(device, aff)
-        if placement.get("aux"):
+        if fs.get("workload") == "write" and aff == "pair":
+            # the endpoint's receive thread and CRC worker get a core each;
+            # this (uploading) thread the client core
+            placement = {**placement, "server": sorted(placement["server"] + placement.get("aux", []))}
+            if placement["client"]:
+                os.sched_setaffinity(0, placement["client"])
+        elif placement.get("aux"):
             _native.set_submitter_cpus(placement["aux"])
 
     endpoint = fs.get("endpoint") or os.environ.get("GCSB_ENDPOINT", "") or os.environ.get("STORAGE_EMULATOR_HOST", "")

@@ -163,11 +163,23 @@ def quota_budget() -> int:
     return max(2, int(q // ranks))
 
 
-def trim_to_quota(cpus: list[int]) -> list[int]:
+def trim_to_quota(cpus: list[int], busy: dict[int, float] | None = None) -> list[int]:
+    """cpus cut to the quota budget, one hardware thread per physical core
+    first.  With `busy` (cpu_busy), the least busy cores are kept: on a
+    shared host another tenant's work on a kept core, or on its SMT sibling,
+    slows every thread scheduled there."""
     b = quota_budget()
     if b <= 0 or len(cpus) <= b:
         return cpus
+    if busy:
+        cores = quiet_cores(cpus, busy)
+        order = [c[0] for c in cores] + [t for c in cores for t in c[1:]]
+        return sorted(order[:b])
     return sorted(core_first(cpus)[:b])
+
+
+def _quiet_sampling() -> bool:
+    return os.environ.get("GCSB_QUIET_CORES", "1") != "0"
 
 
 def plan(device: int, mode: str = "split", slot: int = 0) -> dict:
@@ -226,7 +238,7 @@ def plan(device: int, mode: str = "split", slot: int = 0) -> dict:
         # same first cores as plain "quota" would
         mine = [c for g in groups[base:base + share] for c in g] or cpus
         if mode == "share_quota":
-            mine = trim_to_quota(mine)
+            mine = trim_to_quota(mine, cpu_busy(0.1) if _quiet_sampling() else None)
         return {"client": mine, "server": mine, "mode": mode, "numa_node": node, "gpu_index_on_node": k,
                 "l3_domains": share}
     if mode == "pair":
@@ -236,7 +248,7 @@ def plan(device: int, mode: str = "split", slot: int = 0) -> dict:
         # cores are the least busy ones right now (cpu_busy); one domain keeps
         # the loopback copy in one L3 (profiles/r2_placement)
         doms = groups[base:base + share] if groups else [cpus]
-        busy = cpu_busy() if os.environ.get("GCSB_QUIET_CORES", "1") != "0" else {}
+        busy = cpu_busy() if _quiet_sampling() else {}
         if busy:
             best = None
             for dom in doms:
@@ -262,6 +274,12 @@ def plan(device: int, mode: str = "split", slot: int = 0) -> dict:
         return {"client": [g[0]] + sib[g[0]], "server": [g[1]] + sib[g[1]], "aux": aux, "mode": mode,
                 "numa_node": node, "gpu_index_on_node": k}
     client = groups[base] if groups else cpus
+    if mode == "same" and share > 1 and _quiet_sampling():
+        # the least busy L3 domain of the share (every thread of the block
+        # runs in it: a busy neighbour there costs the whole block)
+        busy = cpu_busy(0.1)
+        if busy:
+            client = min(groups[base:base + share], key=lambda g: (sum(busy.get(c, 0.0) for c in g), g[0]))
     if mode == "same" or share < 2:
         server = client
     else:

@@ -65,6 +65,10 @@ def test_cpu_quota_and_trim(monkeypatch):
     assert a.quota_budget() == 2
     assert a.core_first([0, 4, 1, 5, 2, 6, 3, 7]) == [0, 1, 2, 3, 4, 5, 6, 7]
     assert a.trim_to_quota([0, 4, 1, 5, 2, 6, 3, 7]) == [0, 1]
+    # with a busy map: the two quietest cores (core 1's sibling busy, CPU 0's core last)
+    busy = {c: 0.0 for c in range(8)}
+    busy[5] = 0.9
+    assert a.trim_to_quota(list(range(8)), busy) == [2, 3]
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
     assert a.trim_to_quota(list(range(8))) == list(range(8))  # 16-CPU budget > 8 CPUs
     files["/sys/fs/cgroup/cpu.max"] = "max 100000"

@@ -356,6 +356,13 @@ class H2ServerConn {
         n -= k;
         if (s.wprefix_have < 5) continue;
         s.wmsg_len = be32(s.wprefix + 1);
+        // GCS caps a WriteObject message at 2 MiB of data
+        // (MAX_WRITE_CHUNK_BYTES); a declared length far past that is a
+        // broken or hostile peer, not a buffer to allocate
+        if (s.wmsg_len > kMaxWriteMessage)
+          throw StorageError("WriteObject message of " + std::to_string(s.wmsg_len) + " bytes (limit " +
+                                 std::to_string(kMaxWriteMessage) + ")",
+                             false);
         s.wmsg_have = 0;
         if (!s.wmsg || s.wmsg.capacity() < s.wmsg_len) s.wmsg = take_write_buffer(s.wmsg_len);
         if (s.wmsg_len == 0) post_write_message(sp);
@@ -369,6 +376,7 @@ class H2ServerConn {
     }
   }
 
+  static constexpr uint32_t kMaxWriteMessage = 64u << 20;
   HugeBuffer take_write_buffer(size_t len) {
     std::unique_lock<std::mutex> lk(wmu_);
     wcv_.wait(lk, [&] { return wqueued_ < write_worker_bufs() || wstop_; });

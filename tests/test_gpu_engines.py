@@ -78,3 +78,26 @@ def test_spliced_upload_from_hbm_is_byte_exact(native, server, gpu_available, si
                 assert back == native.gpu_read_bytes(0, t.data_ptr(), size)
     finally:
         srv.stop()
+
+
+@pytest.mark.parametrize("poll_us", [0, 10])
+def test_end_of_read_wait_modes(native, server, gpu_available, poll_us):
+    """Both slot-event waits land and verify every byte: the runtime's
+    blocking hipEventSynchronize (wait_poll_us 0) and the default poll of
+    hipEventQuery with short sleeps; 1 MiB objects make every read end on a
+    short wait, 8 MiB ones wrap the 2-slot ring (waits on the transport
+    thread)."""
+    import torch
+
+    for size in (1 << 20, 8 << 20):
+        server.add_synthetic(B, f"wait{poll_us}/s{size}_", "", 0, 1, size)
+        c = native.Client({"protocol": "grpc", "endpoint": server.url})
+        t = torch.empty(size, dtype=torch.uint8, device="cuda:0")
+        sink = native.GpuSink({"device": 0, "ring_slot_bytes": 1 << 20, "ring_slots": 2, "wait_poll_us": poll_us})
+        sink.set_external_destination(t.data_ptr(), size)
+        for _ in range(3):
+            r = c.read_gpu(B, f"wait{poll_us}/s{size}_0", sink)
+            assert r["verified"] and not r["crc_mismatch"] and r["bytes"] == size, r
+        torch.cuda.synchronize()
+        bad, first = native.gpu_verify_pattern(0, t.data_ptr(), size, f"wait{poll_us}/s{size}_0", 0)
+        assert bad == 0, (bad, first)

@@ -18,6 +18,7 @@
 #include <unistd.h>
 
 #include <cerrno>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <algorithm>

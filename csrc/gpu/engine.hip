@@ -300,16 +300,27 @@ class DeviceSubmitter {
     if (!p) p = new DeviceSubmitter(dev);
     return *p;
   }
+  // The posting (receiving) thread wakes the submitter only when it sleeps:
+  // a futex wake costs the receiving thread microseconds per slot.
   void post(std::function<void()> f) {
+    bool wake;
     {
       std::lock_guard<std::mutex> lk(mu_);
       q_.push_back(std::move(f));
+      pending_.store(true, std::memory_order_release);
+      wake = sleeping_;
     }
-    cv_.notify_one();
+    if (wake) cv_.notify_one();
   }
 
  private:
   explicit DeviceSubmitter(int dev) : dev_(dev) {
+    // after a hand-off the submitter polls for the next one this long before
+    // it sleeps (env GCSB_SUBMIT_SPIN_US; 0 = sleep at once).  Worth it when
+    // hand-offs come every few tens of us (1 MiB objects on one connection)
+    // and the submitter has a core of its own (placement aux)
+    const char* e = std::getenv("GCSB_SUBMIT_SPIN_US");
+    spin_ns_ = (e ? std::max(0, std::atoi(e)) : 0) * 1000LL;
     std::thread([this] { loop(); }).detach();
   }
   void loop() {
@@ -320,18 +331,32 @@ class DeviceSubmitter {
     ensure_device(dev_);
     std::unique_lock<std::mutex> lk(mu_);
     for (;;) {
-      cv_.wait(lk, [&] { return !q_.empty(); });
+      if (q_.empty() && spin_ns_ > 0) {
+        lk.unlock();
+        const int64_t t0 = now_ns();
+        while (!pending_.load(std::memory_order_acquire) && now_ns() - t0 < spin_ns_) __builtin_ia32_pause();
+        lk.lock();
+      }
+      if (q_.empty()) {
+        sleeping_ = true;
+        cv_.wait(lk, [&] { return !q_.empty(); });
+        sleeping_ = false;
+      }
       auto f = std::move(q_.front());
       q_.pop_front();
+      pending_.store(!q_.empty(), std::memory_order_release);
       lk.unlock();
       f();
       lk.lock();
     }
   }
   int dev_;
+  int64_t spin_ns_ = 0;
   std::mutex mu_;
   std::condition_variable cv_;
   std::deque<std::function<void()>> q_;
+  std::atomic<bool> pending_{false};
+  bool sleeping_ = false;  // guarded by mu_
 };
 }  // namespace
 

@@ -125,6 +125,12 @@ wplace)  # profiles/r3_write/placement: config-5 upload, share vs pair placement
     done
   done
   ;;
+spin)  # profiles/r3_w48_tail/spin: submitter polls for the next hand-off before it sleeps
+  for k in 1 2 3; do
+    step "spin0_$k" 300 env GCSB_SUBMIT_SPIN_US=0 python3 bench.py --steps 20 --warmup 5 --blocks list_read,sliced
+    step "spin100_$k" 300 env GCSB_SUBMIT_SPIN_US=100 python3 bench.py --steps 20 --warmup 5 --blocks list_read,sliced
+  done
+  ;;
 final)  # profiles/r3_final: GPU suite, smoke, two full benches
   step pytest_gpu 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
   step smoke 200 python3 -c "import __graft_entry__ as g; g.smoke()"

@@ -100,8 +100,19 @@ class GrpcCall : public H2ClientStream {
  public:
   explicit GrpcCall(MessageHandler* h) : handler_(h) {}
 
+  // The reader thread dispatches into this call holding a reference to it
+  // (H2ClientConn::acquire), so the end-of-stream wake can follow the unlock:
+  // notified under the lock, the woken worker would block on mu_ straight
+  // away and need a second wake once the reader lets go of it.
   void on_headers(const HeaderList& h, bool end_stream) override {
-    std::lock_guard<std::mutex> lk(mu_);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      headers_locked(h, end_stream);
+    }
+    if (end_stream) cv_.notify_all();
+  }
+
+  void headers_locked(const HeaderList& h, bool end_stream) {
     int http_status = 0;
     for (const auto& kv : h) {
       if (kv.first == ":status") http_status = std::atoi(kv.second.c_str());
@@ -120,7 +131,7 @@ class GrpcCall : public H2ClientStream {
         grpc_status_ = kInternal;
         grpc_message_ = "stream ended without grpc-status";
       }
-      finish_locked();
+      done_ = true;
     }
   }
 
@@ -160,12 +171,15 @@ class GrpcCall : public H2ClientStream {
       }
     }
     if (end_stream) {
-      std::lock_guard<std::mutex> lk(mu_);
-      if (grpc_status_ < 0) {
-        grpc_status_ = kInternal;
-        grpc_message_ = "DATA END_STREAM without trailers";
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (grpc_status_ < 0) {
+          grpc_status_ = kInternal;
+          grpc_message_ = "DATA END_STREAM without trailers";
+        }
+        done_ = true;
       }
-      finish_locked();
+      cv_.notify_all();  // after the unlock, as in on_headers
     }
   }
 

@@ -131,6 +131,12 @@ spin)  # profiles/r3_w48_tail/spin: submitter polls for the next hand-off before
     step "spin100_$k" 300 env GCSB_SUBMIT_SPIN_US=100 python3 bench.py --steps 20 --warmup 5 --blocks list_read,sliced
   done
   ;;
+listiso)  # profiles/r3_w48_tail/listiso: config-3 list-read, reader core isolated vs shared (64 MiB rcvbuf both)
+  for k in 1 2 3; do
+    step "shared_$k" 300 python3 bench.py --steps 5 --warmup 2 --blocks list_read
+    step "isolate_$k" 300 python3 bench.py --steps 5 --warmup 2 --blocks list_read --mux-reader isolate
+  done
+  ;;
 final)  # profiles/r3_final: GPU suite, smoke, two full benches
   step pytest_gpu 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
   step smoke 200 python3 -c "import __graft_entry__ as g; g.smoke()"

@@ -393,6 +393,7 @@ def run_rank(args) -> int:
         sync()
         t1 = time.perf_counter()
         rv0 = n.recv_stats()
+        rd0 = n.recv_diag()
         h2s0 = n.h2_reader_stats()
         if use_gpu:
             n.reset_slow_hip_calls()
@@ -437,6 +438,16 @@ def run_rank(args) -> int:
                 # Conn::read_some of the process: client side only here)
                 cpu["recv_calls"] = calls
                 cpu["recv_avg_kib"] = round((rv1[1] - rv0[1]) / calls / 1024.0, 1)
+            rd1 = n.recv_diag()
+            dc = rd1["calls"] - rd0["calls"]
+            if dc:
+                # GCSB_RECV_DIAG=1: the socket queue at each payload recv() --
+                # how often the receiver found it empty (it outran the sender)
+                cpu["recv_queue"] = {"payload_recvs": dc,
+                                     "empty_frac": round((rd1["empty"] - rd0["empty"]) / dc, 3),
+                                     "short_frac": round((rd1["short"] - rd0["short"]) / dc, 3),
+                                     "avg_queued_kib": round((rd1["inq_bytes"] - rd0["inq_bytes"]) / dc / 1024, 1),
+                                     "avg_asked_kib": round((rd1["want_bytes"] - rd0["want_bytes"]) / dc / 1024, 1)}
         slow_hip = n.slow_hip_calls() if use_gpu else {}
         ring_numa = r1.ring_numa(0) if (r1 is not None and use_gpu) else []
         ring_thp = r1.ring_thp_fraction(0) if (r1 is not None and use_gpu) else -1.0
@@ -977,6 +988,8 @@ def run_rank(args) -> int:
                         b["h2_reader"] = st["cpu"]["h2_reader"]
                     if st["cpu"].get("recv_avg_kib") is not None:
                         b["recv_avg_kib"] = st["cpu"]["recv_avg_kib"]
+                    if st["cpu"].get("recv_queue"):
+                        b["recv_queue"] = st["cpu"]["recv_queue"]
                 if key.startswith("ref_default_"):
                     b["first_read_p50_ms"] = round(st["first_p50_max"], 3)
                     b["steady_p99_ms"] = round(st["steady_p99_max"], 3)

@@ -13,6 +13,8 @@
 #include <poll.h>
 #include <signal.h>
 #include <sys/sendfile.h>
+#include <linux/sockios.h>
+#include <sys/ioctl.h>
 #include <sys/resource.h>
 #include <sys/socket.h>
 #include <unistd.h>
@@ -345,8 +347,19 @@ void Conn::shutdown_write() {
 }
 
 std::atomic<uint64_t> g_recv_calls{0}, g_recv_bytes{0};
+std::atomic<uint64_t> g_diag_calls{0}, g_diag_empty{0}, g_diag_short{0}, g_diag_inq{0}, g_diag_want{0};
 
-RecvStats recv_stats() { return RecvStats{g_recv_calls.load(), g_recv_bytes.load()}; }
+RecvStats recv_stats() {
+  RecvStats r;
+  r.calls = g_recv_calls.load();
+  r.bytes = g_recv_bytes.load();
+  r.diag_calls = g_diag_calls.load();
+  r.diag_empty = g_diag_empty.load();
+  r.diag_short = g_diag_short.load();
+  r.diag_inq_bytes = g_diag_inq.load();
+  r.diag_want_bytes = g_diag_want.load();
+  return r;
+}
 
 size_t Conn::read_some(void* buf, size_t n) {
   if (fd_ < 0) throw StorageError("read on closed connection", true);
@@ -355,6 +368,20 @@ size_t Conn::read_some(void* buf, size_t n) {
     if (ssl_) {
       r = ssl_io(false, buf, n);
     } else {
+      static const bool diag = [] {
+        const char* e = std::getenv("GCSB_RECV_DIAG");
+        return e && e[0] == '1';
+      }();
+      if (diag && n >= (64u << 10)) {
+        int inq = 0;
+        if (::ioctl(fd_, SIOCINQ, &inq) == 0) {
+          g_diag_calls.fetch_add(1, std::memory_order_relaxed);
+          g_diag_want.fetch_add(n, std::memory_order_relaxed);
+          g_diag_inq.fetch_add(static_cast<uint64_t>(inq), std::memory_order_relaxed);
+          if (inq == 0) g_diag_empty.fetch_add(1, std::memory_order_relaxed);
+          else if (static_cast<size_t>(inq) < n) g_diag_short.fetch_add(1, std::memory_order_relaxed);
+        }
+      }
       r = ::recv(fd_, buf, n, 0);
     }
     if (r >= 0) {

@@ -53,6 +53,11 @@ struct TlsServer {
 // bytes: the average receive size of a read path (diagnostics).
 struct RecvStats {
   uint64_t calls = 0, bytes = 0;
+  // GCSB_RECV_DIAG=1: for reads of >= 64 KiB (payload into a sink), the
+  // socket's queue (SIOCINQ) just before the recv(): empty (the call
+  // blocks: the receiver outran its sender), short (less than asked), and
+  // the queued bytes.  One extra syscall per read, diagnostics only.
+  uint64_t diag_calls = 0, diag_empty = 0, diag_short = 0, diag_inq_bytes = 0, diag_want_bytes = 0;
 };
 RecvStats recv_stats();
 

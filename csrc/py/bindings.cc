@@ -819,6 +819,16 @@ PYBIND11_MODULE(_native, m) {
     RecvStats r = recv_stats();
     return py::make_tuple(r.calls, r.bytes);
   });
+  m.def("recv_diag", [] {
+    RecvStats r = recv_stats();
+    py::dict d;
+    d["calls"] = r.diag_calls;
+    d["empty"] = r.diag_empty;
+    d["short"] = r.diag_short;
+    d["inq_bytes"] = r.diag_inq_bytes;
+    d["want_bytes"] = r.diag_want_bytes;
+    return d;
+  });
   m.def("thp_bytes_of", [](uintptr_t p, size_t n) { return thp_bytes_of(reinterpret_cast<const void*>(p), n); });
   m.def("h2_reader_stats", [] {
     H2ReaderStats s = h2_reader_stats();

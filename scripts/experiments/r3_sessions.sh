@@ -137,6 +137,11 @@ listiso)  # profiles/r3_w48_tail/listiso: config-3 list-read, reader core isolat
     step "isolate_$k" 300 python3 bench.py --steps 5 --warmup 2 --blocks list_read --mux-reader isolate
   done
   ;;
+recvdiag)  # profiles/r3_w48_tail/recvdiag: socket queue at every payload recv (GCSB_RECV_DIAG), headline + list-read
+  for k in 1 2; do
+    step "diag_$k" 300 env GCSB_RECV_DIAG=1 python3 bench.py --steps 20 --warmup 5 --blocks list_read,ref_default
+  done
+  ;;
 final)  # profiles/r3_final: GPU suite, smoke, two full benches
   step pytest_gpu 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
   step smoke 200 python3 -c "import __graft_entry__ as g; g.smoke()"

@@ -1,5 +1,7 @@
 #include "core/content.h"
 
+#include <cstdlib>
+
 #include <sys/mman.h>
 
 #include <sys/syscall.h>
@@ -35,7 +37,13 @@ uint64_t object_rotation(const std::string& name) {
     h ^= c;
     h *= 0x100000001B3ull;
   }
-  return h % kPatternLen;
+  // GCSB_PATTERN_ROT_ALIGN=1: byte-granular rotations (round-2 content), for A/Bs
+  static const uint64_t align = [] {
+    const char* e = std::getenv("GCSB_PATTERN_ROT_ALIGN");
+    const long v = e ? std::atol(e) : 0;
+    return v > 0 ? static_cast<uint64_t>(v) : kPatternRotAlign;
+  }();
+  return h % (kPatternLen / align) * align;
 }
 
 PatternBuffer::PatternBuffer() {

@@ -142,6 +142,14 @@ recvdiag)  # profiles/r3_w48_tail/recvdiag: socket queue at every payload recv (
     step "diag_$k" 300 env GCSB_RECV_DIAG=1 python3 bench.py --steps 20 --warmup 5 --blocks list_read,ref_default
   done
   ;;
+align)  # profiles/r3_align: objects on page boundaries of the pattern (default) vs any byte (round 2)
+  step probe 150 ./build/probes/align_probe
+  for k in 1 2 3; do
+    step "byte_$k" 300 env GCSB_PATTERN_ROT_ALIGN=1 python3 bench.py --steps 20 --warmup 5 \
+      --blocks cpu_baseline,ceiling,list_read,ref_default
+    step "page_$k" 300 python3 bench.py --steps 20 --warmup 5 --blocks cpu_baseline,ceiling,list_read,ref_default
+  done
+  ;;
 final)  # profiles/r3_final: GPU suite, smoke, two full benches
   step pytest_gpu 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
   step smoke 200 python3 -c "import __graft_entry__ as g; g.smoke()"

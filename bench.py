@@ -447,7 +447,10 @@ def run_rank(args) -> int:
                                      "empty_frac": round((rd1["empty"] - rd0["empty"]) / dc, 3),
                                      "short_frac": round((rd1["short"] - rd0["short"]) / dc, 3),
                                      "avg_queued_kib": round((rd1["inq_bytes"] - rd0["inq_bytes"]) / dc / 1024, 1),
-                                     "avg_asked_kib": round((rd1["want_bytes"] - rd0["want_bytes"]) / dc / 1024, 1)}
+                                     "avg_asked_kib": round((rd1["want_bytes"] - rd0["want_bytes"]) / dc / 1024, 1),
+                                     # wall time inside those recv() calls, per GiB read
+                                     "recv_s_per_gib": round((rd1["recv_ns"] - rd0["recv_ns"]) / 1e9
+                                                             / max(float(s1["bytes"]) / (1 << 30), 1e-9), 4)}
         slow_hip = n.slow_hip_calls() if use_gpu else {}
         ring_numa = r1.ring_numa(0) if (r1 is not None and use_gpu) else []
         ring_thp = r1.ring_thp_fraction(0) if (r1 is not None and use_gpu) else -1.0

@@ -347,7 +347,7 @@ void Conn::shutdown_write() {
 }
 
 std::atomic<uint64_t> g_recv_calls{0}, g_recv_bytes{0};
-std::atomic<uint64_t> g_diag_calls{0}, g_diag_empty{0}, g_diag_short{0}, g_diag_inq{0}, g_diag_want{0};
+std::atomic<uint64_t> g_diag_calls{0}, g_diag_empty{0}, g_diag_short{0}, g_diag_inq{0}, g_diag_want{0}, g_diag_ns{0};
 
 RecvStats recv_stats() {
   RecvStats r;
@@ -358,6 +358,7 @@ RecvStats recv_stats() {
   r.diag_short = g_diag_short.load();
   r.diag_inq_bytes = g_diag_inq.load();
   r.diag_want_bytes = g_diag_want.load();
+  r.diag_recv_ns = g_diag_ns.load();
   return r;
 }
 
@@ -372,6 +373,7 @@ size_t Conn::read_some(void* buf, size_t n) {
         const char* e = std::getenv("GCSB_RECV_DIAG");
         return e && e[0] == '1';
       }();
+      int64_t t0 = 0;
       if (diag && n >= (64u << 10)) {
         int inq = 0;
         if (::ioctl(fd_, SIOCINQ, &inq) == 0) {
@@ -380,9 +382,11 @@ size_t Conn::read_some(void* buf, size_t n) {
           g_diag_inq.fetch_add(static_cast<uint64_t>(inq), std::memory_order_relaxed);
           if (inq == 0) g_diag_empty.fetch_add(1, std::memory_order_relaxed);
           else if (static_cast<size_t>(inq) < n) g_diag_short.fetch_add(1, std::memory_order_relaxed);
+          t0 = now_ns();
         }
       }
       r = ::recv(fd_, buf, n, 0);
+      if (t0) g_diag_ns.fetch_add(static_cast<uint64_t>(now_ns() - t0), std::memory_order_relaxed);
     }
     if (r >= 0) {
       bytes_read_ += static_cast<uint64_t>(r);

@@ -58,6 +58,7 @@ struct RecvStats {
   // blocks: the receiver outran its sender), short (less than asked), and
   // the queued bytes.  One extra syscall per read, diagnostics only.
   uint64_t diag_calls = 0, diag_empty = 0, diag_short = 0, diag_inq_bytes = 0, diag_want_bytes = 0;
+  uint64_t diag_recv_ns = 0;  // wall time inside those recv() calls
 };
 RecvStats recv_stats();
 

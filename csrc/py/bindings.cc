@@ -827,6 +827,7 @@ PYBIND11_MODULE(_native, m) {
     d["short"] = r.diag_short;
     d["inq_bytes"] = r.diag_inq_bytes;
     d["want_bytes"] = r.diag_want_bytes;
+    d["recv_ns"] = r.diag_recv_ns;
     return d;
   });
   m.def("thp_bytes_of", [](uintptr_t p, size_t n) { return thp_bytes_of(reinterpret_cast<const void*>(p), n); });

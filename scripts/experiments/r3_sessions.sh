@@ -150,6 +150,12 @@ align)  # profiles/r3_align: objects on page boundaries of the pattern (default)
     step "page_$k" 300 python3 bench.py --steps 20 --warmup 5 --blocks cpu_baseline,ceiling,list_read,ref_default
   done
   ;;
+listring)  # profiles/r3_w48_tail/listring: list-read ring footprint (8 workers x ring) with page-aligned objects
+  for k in 1 2 3; do
+    step "r8x2_$k" 300 python3 bench.py --steps 5 --warmup 2 --blocks list_read --list-ring 8x2MiB
+    step "r2x1_$k" 300 python3 bench.py --steps 5 --warmup 2 --blocks list_read --list-ring 2x1MiB
+  done
+  ;;
 final)  # profiles/r3_final: GPU suite, smoke, two full benches
   step pytest_gpu 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
   step smoke 200 python3 -c "import __graft_entry__ as g; g.smoke()"

@@ -395,6 +395,7 @@ def run_rank(args) -> int:
         rv0 = n.recv_stats()
         rd0 = n.recv_diag()
         h2s0 = n.h2_reader_stats()
+        pr0 = n.pipe_relay_stats()
         if use_gpu:
             n.reset_slow_hip_calls()
         if not err:
@@ -431,6 +432,18 @@ def run_rank(args) -> int:
                                     "headers_s_per_gib": round(d["headers_ns"] / 1e9 / g, 4),
                                     "other_s_per_gib": round(d["other_ns"] / 1e9 / g, 4),
                                     "avg_data_frame_kib": round(d["data_bytes"] / max(1, d["data_frames"]) / 1024, 1)}
+            pr1 = n.pipe_relay_stats()
+            if pr1["relays"] + pr1["no_pipe"] > pr0["relays"] + pr0["no_pipe"]:
+                # multiplexed reads relayed through per-read pipes (storage/pipe_relay.h):
+                # how the payload left the socket
+                d = {k: pr1[k] - pr0[k] for k in pr1}
+                moved = max(1, d["spliced_bytes"] + d["buffered_bytes"] + d["overflow_bytes"])
+                cpu["pipe_relay"] = {"reads": d["relays"], "reads_without_pipe": d["no_pipe"],
+                                     "spliced_frac": round(d["spliced_bytes"] / moved, 4),
+                                     "buffered_frac": round(d["buffered_bytes"] / moved, 4),
+                                     "overflow_frac": round(d["overflow_bytes"] / moved, 4),
+                                     "avg_splice_kib": round(d["spliced_bytes"] / max(1, d["splices"]) / 1024, 1),
+                                     "pipes": pr1["pipes"], "pipe_kib": pr1["pipe_bytes"] // max(1, pr1["pipes"]) // 1024}
             rv1 = n.recv_stats()
             calls = rv1[0] - rv0[0]
             if calls:

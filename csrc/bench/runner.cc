@@ -52,6 +52,13 @@ double percentile_floor(const std::vector<double>& sorted, int pct) {
 Runner::Runner(RunnerConfig cfg) : cfg_(std::move(cfg)) {
   reserve_fd_table();
   if (cfg_.workers <= 0) throw StorageError("worker count not valid", false);
+  if (cfg_.client.splice_recv < 0) {
+    // streams share a connection: its reader only moves pages, each worker
+    // copies its own read (storage/pipe_relay.h)
+    const char* e = std::getenv("GCSB_SPLICE_RECV");
+    if (e && *e) cfg_.client.splice_recv = *e == '1' ? 1 : 0;
+    else cfg_.client.splice_recv = cfg_.workers > std::max(1, cfg_.client.grpc_conn_pool_size) ? 1 : 0;
+  }
   client_ = make_client(cfg_.client);
 }
 

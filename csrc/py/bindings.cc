@@ -19,6 +19,7 @@
 #include "h2/hpack.h"
 #include "proto/storage_v2.h"
 #include "server/fakegcs.h"
+#include "storage/pipe_relay.h"
 #include "storage/auth.h"
 #include "storage/client.h"
 #include "storage/sliced.h"
@@ -65,6 +66,7 @@ ClientConfig client_from(const py::dict& d) {
   c.sock.tls_verify = get_or<bool>(d, "tls_verify", true);
   c.sock.tls_ca_file = get_or<std::string>(d, "tls_ca_file", "");
   c.project = get_or<std::string>(d, "project", "gcs-fuse-test");
+  c.splice_recv = get_or<int>(d, "splice_recv", -1);
   if (d.contains("cpus") && !d["cpus"].is_none()) c.cpus = d["cpus"].cast<std::vector<int>>();
   if (d.contains("reader_cpus") && !d["reader_cpus"].is_none())
     c.reader_cpus = d["reader_cpus"].cast<std::vector<int>>();
@@ -842,6 +844,20 @@ PYBIND11_MODULE(_native, m) {
     d["data_ns"] = s.data_ns;
     d["headers_ns"] = s.headers_ns;
     d["other_ns"] = s.other_ns;
+    return d;
+  });
+  m.def("pipe_relay_stats", [] {
+    PipeRelayStats s = pipe_relay_stats();
+    py::dict d;
+    d["relays"] = s.relays;
+    d["no_pipe"] = s.no_pipe;
+    d["spliced_bytes"] = s.spliced_bytes;
+    d["splices"] = s.splices;
+    d["buffered_bytes"] = s.buffered_bytes;
+    d["overflow_bytes"] = s.overflow_bytes;
+    d["overflows"] = s.overflows;
+    d["pipes"] = s.pipes;
+    d["pipe_bytes"] = s.pipe_bytes;
     return d;
   });
   m.def("slow_hip_calls", [] {

@@ -26,6 +26,32 @@ step() {  # step <name> <timeout> <cmd...>: a crash, abort or timeout ends the s
 }
 
 case "$S" in
+splice)  # profiles/r3_splice: multiplexed-reader cost, recv() copy vs splice() into per-stream pipes
+  { uname -r; cat /proc/sys/fs/pipe-max-size /proc/sys/fs/pipe-user-pages-soft; id -u;
+    lscpu | grep -E "^(Model name|L3|NUMA node)"; } > "$O/env.txt" 2>&1
+  P=custom_go_client_benchmark_amd/bin/splice_probe
+  for rep in 1 2; do
+    for st in 1 8; do
+      for m in recv splice; do
+        step "probe_${m}_s${st}_r$rep" 60 $P -mode $m -streams $st -total $((16<<30)) -send-cpu 2 -recv-cpu 1 \
+          -worker-cpus 3,4,5,6,7,129,130,131
+        cat "$O/probe_${m}_s${st}_r$rep.log" >> "$O/probe.jsonl"
+      done
+    done
+  done
+  step probe_splice_s8_2m 60 $P -mode splice -streams 8 -msg $((2<<20)) -total $((16<<30)) -send-cpu 2 -recv-cpu 1 \
+    -worker-cpus 3,4,5,6,7,129,130,131
+  step probe_splice_s48 60 $P -mode splice -streams 48 -total $((16<<30)) -send-cpu 2 -recv-cpu 1 \
+    -worker-cpus 3,4,5,6,7,129,130,131,132,133,134,135
+  step probe_recv_s48 60 $P -mode recv -streams 48 -total $((16<<30)) -send-cpu 2 -recv-cpu 1
+  cat "$O"/probe_*_2m.log "$O"/probe_*_s48.log >> "$O/probe.jsonl"
+  for rep in 1 2; do
+    for v in 0 1; do
+      step "bench_relay${v}_r$rep" 300 env GCSB_SPLICE_RECV=$v python3 bench.py --steps 20 --warmup 3 \
+        --blocks list_read,ref_default --json-out "$O/bench_relay${v}_r$rep.json"
+    done
+  done
+  ;;
 stall)  # profiles/r3_sdma_engines: which hand-off HIP call blocks after a device sync
   step probe_default 200 python3 scripts/experiments/sync_stall_probe.py --reps 8
   step probe_hwq8 200 env GPU_MAX_HW_QUEUES=8 python3 scripts/experiments/sync_stall_probe.py --reps 8

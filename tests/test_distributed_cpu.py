@@ -266,7 +266,7 @@ def _stuck_gather_worker(rank, world, port, q):
     ctx = dist.init()
     dist.barrier(ctx, "warm barrier")
     if rank == 1:
-        time.sleep(30)  # a stuck peer: never joins the all-gather
+        time.sleep(90)  # a stuck peer: never joins the all-gather
         os._exit(0)
     out = torch.zeros(8, dtype=torch.uint8)
     t0 = time.time()
@@ -290,7 +290,8 @@ def test_gloo_all_gather_gives_up_on_a_stuck_peer():
     ps = [ctx.Process(target=_stuck_gather_worker, args=(r, 2, port, q)) for r in range(2)]
     [p.start() for p in ps]
     try:
-        outcome = q.get(timeout=60)
+        # spawn + torch import of two ranks can take a minute on a loaded box
+        outcome = q.get(timeout=180)
         assert outcome[0] == "raised" and outcome[1] < 20, outcome
     finally:
         for p in ps:

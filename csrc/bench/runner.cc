@@ -53,11 +53,13 @@ Runner::Runner(RunnerConfig cfg) : cfg_(std::move(cfg)) {
   reserve_fd_table();
   if (cfg_.workers <= 0) throw StorageError("worker count not valid", false);
   if (cfg_.client.splice_recv < 0) {
-    // streams share a connection: its reader only moves pages, each worker
-    // copies its own read (storage/pipe_relay.h)
+    // GCSB_SPLICE_RECV=1: when streams share a connection, its reader only
+    // moves pages and each worker copies its own read (storage/pipe_relay.h).
+    // Off by default: splice() cost the reader as much as the copy it saves
+    // (profiles/r3_splice).
     const char* e = std::getenv("GCSB_SPLICE_RECV");
-    if (e && *e) cfg_.client.splice_recv = *e == '1' ? 1 : 0;
-    else cfg_.client.splice_recv = cfg_.workers > std::max(1, cfg_.client.grpc_conn_pool_size) ? 1 : 0;
+    const bool on = e && *e == '1';
+    cfg_.client.splice_recv = on && cfg_.workers > std::max(1, cfg_.client.grpc_conn_pool_size) ? 1 : 0;
   }
   client_ = make_client(cfg_.client);
 }

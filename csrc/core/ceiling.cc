@@ -8,6 +8,8 @@
 #include <sys/resource.h>
 #include <sys/sendfile.h>
 #include <sys/socket.h>
+#include <sys/uio.h>
+#include <fcntl.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -21,6 +23,7 @@
 #include <thread>
 
 #include "core/affinity.h"
+#include "core/hugebuf.h"
 
 namespace gcsb {
 
@@ -121,26 +124,41 @@ CeilingResult tcp_ceiling(const CeilingConfig& c) {
   Fd mfd(memfd_create("ceiling-object", 0));
   if (mfd.fd < 0) fail("memfd_create");
   if (ftruncate(mfd.fd, static_cast<off_t>(obj)) != 0) fail("ftruncate");
+  const bool thp = c.zerocopy_send && c.thp_source;
+  uint8_t* src = nullptr;  // thp: the object in THP anonymous memory
   {
-    // the object's page cache on the sender's NUMA node, as the endpoint's
-    // memfd (server/fakegcs.cc): the receiver's copy reads these pages, and
-    // pages on the far socket cost it up to 2x per byte (profiles/r2_numa)
+    // the object's pages on the sender's NUMA node, as the endpoint's source
+    // (server/fakegcs.cc): the receiver's copy reads these pages, and pages
+    // on the far socket cost it up to 2x per byte (profiles/r2_numa)
     std::exception_ptr fill_err;
     std::thread filler([&] {
       try {
         pin_current_thread(c.send_cpus);
         std::vector<uint8_t> blk(1 << 20);
         for (size_t i = 0; i < blk.size(); ++i) blk[i] = static_cast<uint8_t>(i * 131 + 7);
-        for (size_t off = 0; off < obj; off += blk.size())
-          if (pwrite(mfd.fd, blk.data(), std::min(blk.size(), obj - off), static_cast<off_t>(off)) < 0)
-            fail("pwrite");
+        if (thp) src = huge_alloc(obj);
+        for (size_t off = 0; off < obj; off += blk.size()) {
+          const size_t k = std::min(blk.size(), obj - off);
+          if (thp) std::memcpy(src + off, blk.data(), k);
+          else if (pwrite(mfd.fd, blk.data(), k, static_cast<off_t>(off)) < 0) fail("pwrite");
+        }
       } catch (...) {
         fill_err = std::current_exception();
       }
     });
     filler.join();
-    if (fill_err) std::rethrow_exception(fill_err);
+    if (fill_err) {
+      if (src) huge_free(src, obj);
+      std::rethrow_exception(fill_err);
+    }
   }
+  struct SrcFree {
+    uint8_t* p;
+    size_t n;
+    ~SrcFree() {
+      if (p) huge_free(p, n);
+    }
+  } src_free{src, obj};
   Fd ls(socket(AF_INET, SOCK_STREAM, 0));
   sockaddr_in a{};
   a.sin_family = AF_INET;
@@ -164,6 +182,7 @@ CeilingResult tcp_ceiling(const CeilingConfig& c) {
       setsockopt(s.fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
       std::vector<uint8_t> copybuf;
       if (!c.zerocopy_send) copybuf.resize(2u << 20);
+      Fd sp[2];
       const double c0 = thread_cpu_s();
       for (int r = 0; r < c.reads; ++r) {
         while (go.load() <= r && !quit.load()) std::this_thread::yield();
@@ -171,7 +190,26 @@ CeilingResult tcp_ceiling(const CeilingConfig& c) {
         off_t off = 0;
         while (static_cast<size_t>(off) < obj) {
           const size_t k = std::min<size_t>(obj - off, 2u << 20);
-          if (c.zerocopy_send) {
+          if (thp) {
+            // vmsplice the pages into a pipe, splice the pipe into the socket
+            if (sp[0].fd < 0) {
+              int q[2];
+              if (pipe2(q, O_CLOEXEC) != 0) fail("pipe2");
+              sp[0].fd = q[0];
+              sp[1].fd = q[1];
+              (void)fcntl(q[1], F_SETPIPE_SZ, 1 << 20);
+            }
+            iovec iov{src + off, k};
+            const ssize_t v = vmsplice(sp[1].fd, &iov, 1, 0);
+            if (v <= 0) fail("vmsplice");
+            for (ssize_t left = v; left > 0;) {
+              const ssize_t w = splice(sp[0].fd, nullptr, s.fd, nullptr, static_cast<size_t>(left),
+                                       SPLICE_F_MOVE | SPLICE_F_MORE);
+              if (w <= 0) fail("splice");
+              left -= w;
+            }
+            off += static_cast<off_t>(v);
+          } else if (c.zerocopy_send) {
             if (sendfile(s.fd, mfd.fd, &off, k) <= 0) fail("sendfile");
           } else {
             if (pread(mfd.fd, copybuf.data(), k, off) != static_cast<ssize_t>(k)) fail("pread");

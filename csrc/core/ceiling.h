@@ -29,14 +29,18 @@ struct CeilingConfig {
   size_t recv_chunk = size_t(4) << 20;    // bytes asked per recv()
   int rcvbuf = 0;                         // SO_RCVBUF, 0 = autotuning
   std::vector<int> send_cpus, recv_cpus;  // empty = unpinned
-  bool zerocopy_send = true;              // sendfile() from a memfd (the endpoint's path)
+  bool zerocopy_send = true;              // zero-copy send, from the endpoint's source:
+  // THP anonymous memory by vmsplice + splice (PatternBuffer::send_by_vmsplice,
+  // the endpoint's default) or a memfd by sendfile
+  bool thp_source = true;
   int ring_pages = 1;                     // 0 default, 1 MADV_HUGEPAGE (the THP ring), 2 small pages
 };
 
 // One thread memcpy()s a DRAM-resident object into the ring (recv_cpus).
 CeilingResult memcpy_ceiling(const CeilingConfig& c);
-// A sender thread sendfile()s a memfd object over one loopback connection,
-// a receiver thread recv()s it into the ring.  Throws std::runtime_error.
+// A sender thread sends an object (zero-copy, as the endpoint does) over one
+// loopback connection, a receiver thread recv()s it into the ring.  Throws
+// std::runtime_error.
 CeilingResult tcp_ceiling(const CeilingConfig& c);
 
 }  // namespace gcsb

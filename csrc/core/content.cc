@@ -10,11 +10,13 @@
 #include <algorithm>
 #include <cstring>
 #include <mutex>
+#include <new>
 #include <stdexcept>
 #include <thread>
 
 #include "core/affinity.h"
 #include "core/crc32c.h"
+#include "core/hugebuf.h"
 
 namespace gcsb {
 
@@ -91,7 +93,31 @@ int PatternBuffer::memfd() const {
   return memfd_;
 }
 
+bool PatternBuffer::send_by_vmsplice() {
+  static const bool v = [] {
+    const char* e = std::getenv("GCSB_SRV_SEND");
+    return !(e && std::string(e) == "sendfile");
+  }();
+  return v;
+}
+
+const uint8_t* PatternBuffer::thp() const {
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lk(mu);
+  if (thp_tried_) return thp_;
+  thp_tried_ = true;
+  try {
+    uint8_t* p = huge_alloc(buf_.size());  // faulted in here: on this thread's node
+    std::memcpy(p, buf_.data(), buf_.size());
+    thp_ = p;
+  } catch (const std::bad_alloc&) {
+    thp_ = nullptr;
+  }
+  return thp_;
+}
+
 std::vector<long> PatternBuffer::memfd_numa() const {
+  if (thp_) return numa_nodes_of(thp_, buf_.size());
   if (memfd_ < 0) return {};
   void* m = ::mmap(nullptr, buf_.size(), PROT_READ, MAP_SHARED | MAP_POPULATE, memfd_, 0);
   if (m == MAP_FAILED) return {};

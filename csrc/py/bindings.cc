@@ -892,6 +892,7 @@ PYBIND11_MODULE(_native, m) {
     c.recv_chunk = get_or<size_t>(d, "recv_chunk", c.recv_chunk);
     c.rcvbuf = get_or<int>(d, "rcvbuf", 0);
     c.zerocopy_send = get_or<bool>(d, "zerocopy_send", true);
+    c.thp_source = get_or<bool>(d, "thp_source", PatternBuffer::send_by_vmsplice());
     c.ring_pages = get_or<int>(d, "ring_pages", 1);
     if (d.contains("send_cpus")) c.send_cpus = d["send_cpus"].cast<std::vector<int>>();
     if (d.contains("recv_cpus")) c.recv_cpus = d["recv_cpus"].cast<std::vector<int>>();

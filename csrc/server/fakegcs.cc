@@ -24,23 +24,28 @@ FakeGcsServer::~FakeGcsServer() {
 
 void FakeGcsServer::start() {
   reserve_fd_table();
-  // build the pattern buffer (+ its memfd for sendfile) before the first
-  // request, so no read pays for it
+  // build the pattern buffer (+ its THP copy for vmsplice, or its memfd for
+  // sendfile) before the first request, so no read pays for it
   //
   // The memfd's page cache lands on the NUMA node of the thread that writes
   // it; every served byte is read from there by the send path and copied by
   // the client's receive thread.  Build it on a thread pinned to the
   // endpoint's CPUs (the rank's GPU-local node), not on whichever node the
   // caller (the Python main thread) happens to run.
+  // The THP send source (PatternBuffer::thp, the default) is placed the
+  // same way: by first touch on the pinned builder thread.
   if (cfg_.zero_copy) {
+    auto build = [] {
+      if (!PatternBuffer::send_by_vmsplice() || !PatternBuffer::instance().thp()) PatternBuffer::instance().memfd();
+    };
     const char* e = std::getenv("GCSB_MEMFD_PINNED");  // A/B switch: 0 = build on the caller's thread
     if (cfg_.cpus.empty() || (e && *e == '0')) {
-      PatternBuffer::instance().memfd();
+      build();
     } else {
-      std::thread([this] {
+      std::thread([this, &build] {
         pin_current_thread(cfg_.cpus);
         bind_numa_node(current_numa_node());
-        PatternBuffer::instance().memfd();
+        build();
         bind_numa_node(-1);
       }).join();
     }

@@ -685,7 +685,8 @@ class H2ServerConn {
   }
 
   // Object bytes [start, start + len) as DATA frames (END_STREAM on the last),
-  // zero-copy from the memfd, within the peer's flow-control windows; the
+  // zero-copy (THP pattern pages by vmsplice, or the memfd by sendfile),
+  // within the peer's flow-control windows; the
   // fault knobs cut the connection / flip a byte as on HTTP/1.1.
   void send_object_body(ServerStream& s, const StoredObject& o, uint64_t start, uint64_t len) {
     auto& f = srv_.faults();
@@ -737,6 +738,10 @@ class H2ServerConn {
         if (n - k - 1) pieces.push_back(mem(p + k + 1, n - k - 1));
         ++srv_.stats().faults_injected;
         corrupt = -1;
+      } else if (const uint8_t* sp = srv_.config().zero_copy ? o.splice_bytes(off, n) : nullptr) {
+        SendPiece fp = mem(sp, n);
+        fp.splice = true;  // THP pages by reference (PatternBuffer::thp)
+        pieces.push_back(fp);
       } else if (srv_.config().zero_copy && o.file_range(off, &ffd, &foff)) {
         SendPiece fp;
         fp.n = n;
@@ -819,6 +824,10 @@ class H2ServerConn {
         if (n - k - 1) pieces.push_back(mem(p + k + 1, n - k - 1));
         ++srv_.stats().faults_injected;
         corrupt = -1;
+      } else if (const uint8_t* sp = (n && srv_.config().zero_copy) ? o->splice_bytes(off, n) : nullptr) {
+        SendPiece fp = mem(sp, n);
+        fp.splice = true;  // THP pages by reference (PatternBuffer::thp)
+        pieces.push_back(fp);
       } else if (n && srv_.config().zero_copy && o->file_range(off, &ffd, &foff)) {
         SendPiece fp;
         fp.n = n;

@@ -352,7 +352,9 @@ class Http1Handler {
       }
       int ffd = -1;
       uint64_t foff = 0;
-      if (srv_.config().zero_copy && o.file_range(off, &ffd, &foff))
+      if (const uint8_t* sp = srv_.config().zero_copy ? o.splice_bytes(off, n) : nullptr)
+        c_.splice_user_all(sp, n);  // THP pattern pages by reference, no copy
+      else if (srv_.config().zero_copy && o.file_range(off, &ffd, &foff))
         c_.sendfile_all(ffd, foff, n);  // page references, no user-space copy
       else
         c_.write_all(o.bytes(off, n), n);

@@ -47,6 +47,14 @@ const uint8_t* StoredObject::bytes(uint64_t off, uint64_t n) const {
   return data->data() + off;
 }
 
+const uint8_t* StoredObject::splice_bytes(uint64_t off, uint64_t n) const {
+  if (!synthetic || !PatternBuffer::send_by_vmsplice()) return nullptr;
+  const PatternBuffer& pb = PatternBuffer::instance();
+  const uint8_t* t = pb.thp();
+  if (!t) return nullptr;
+  return t + (pb.slice(rot, off, n) - pb.data());
+}
+
 bool StoredObject::file_range(uint64_t off, int* fd, uint64_t* foff) const {
   if (!synthetic) return false;
   const PatternBuffer& pb = PatternBuffer::instance();

@@ -80,6 +80,10 @@ struct StoredObject {
   const uint8_t* bytes(uint64_t off, uint64_t n) const;
   // Synthetic objects: (fd, file offset) of [off, off+n) for sendfile(); false otherwise.
   bool file_range(uint64_t off, int* fd, uint64_t* foff) const;
+  // Synthetic objects sent by vmsplice (PatternBuffer::send_by_vmsplice):
+  // [off, off+n) (n <= kPatternExt) in the pattern's THP copy; nullptr
+  // otherwise (then file_range / bytes).
+  const uint8_t* splice_bytes(uint64_t off, uint64_t n) const;
   uint32_t crc32c_range(uint64_t off, uint64_t n) const;
 
  private:

@@ -177,6 +177,12 @@ size_t PipeRelay::feed(BufferedConn& bc, size_t n) {
   }
 }
 
+void PipeRelay::begin(const ObjectInfo& info) {
+  Op op{Op::kOpen};
+  op.info = info;
+  push(std::move(op));
+}
+
 void PipeRelay::update_info(const ObjectInfo& info) {
   Op op{Op::kInfo};
   op.info = info;
@@ -277,7 +283,8 @@ void PipeRelay::apply(const Op& op) {
   }
   if (failed_) return;
   try {
-    if (op.kind == Op::kInfo) inner_.update_info(op.info);
+    if (op.kind == Op::kOpen) inner_.begin(op.info);
+    else if (op.kind == Op::kInfo) inner_.update_info(op.info);
     else if (op.kind == Op::kBegin) inner_.chunk_begin(op.len);
     else inner_.chunk_end(op.has_crc, op.crc);
   } catch (const std::exception& e) {

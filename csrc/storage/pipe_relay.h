@@ -91,9 +91,11 @@ class PipeRelay : public Sink {
   // The payload goes through feed(); a reader must not ask for windows.
   Window acquire(size_t want) override;
   void commit(size_t n) override;
-  // Begin / resume / finish / abort belong to the worker and go to the inner
-  // sink directly (the read loop calls them outside any stream).
-  void begin(const ObjectInfo& info) override { inner_.begin(info); }
+  // The HTTP/2 media GET begins the sink on the reader (at its response
+  // headers): queued like the rest.
+  void begin(const ObjectInfo& info) override;
+  // Resume / finish / abort belong to the worker and go to the inner sink
+  // directly (the read loop calls them outside any stream).
   void resume_at(int64_t offset) override { inner_.resume_at(offset); }
   SinkResult finish() override;
   void abort() override;
@@ -108,12 +110,12 @@ class PipeRelay : public Sink {
 
  private:
   struct Op {
-    enum Kind : uint8_t { kPipe, kCopy, kRelease, kInfo, kBegin, kEnd } kind;
+    enum Kind : uint8_t { kPipe, kCopy, kRelease, kOpen, kInfo, kBegin, kEnd } kind;
     bool has_crc = false;
     uint32_t crc = 0;
     size_t len = 0;
     uint8_t* p = nullptr;  // kCopy: bytes in an overflow block; kRelease: the block
-    ObjectInfo info;       // kInfo
+    ObjectInfo info;       // kOpen, kInfo
   };
   void push(Op op);
   void apply(const Op& op);

@@ -37,7 +37,9 @@ int main(int argc, char** argv) {
   auto* rcvbuf_kib = fs.Int("rcvbuf-kib", 0, "SO_RCVBUF (KiB), 0 = autotuning");
   auto* send_cpu = fs.Int("send-cpu", -1, "pin the sender to this CPU (-1 = unpinned)");
   auto* recv_cpu = fs.Int("recv-cpu", -1, "pin the receiver to this CPU (-1 = unpinned)");
-  auto* zc = fs.Bool("zerocopy-send", true, "sender uses sendfile() (the endpoint's path)");
+  auto* zc = fs.Bool("zerocopy-send", true, "sender sends zero-copy (the endpoint's path)");
+  auto* thp = fs.Bool("thp-source", true, "zero-copy from THP memory by vmsplice (the endpoint's default); "
+                      "false = sendfile() from a memfd");
   auto* pages = fs.Int("ring-pages", 0, "ring pages: 0 system default, 1 huge (MADV_HUGEPAGE), 2 small");
   fs.Parse(argc, argv);
   gcsb::CeilingConfig c;
@@ -49,6 +51,7 @@ int main(int argc, char** argv) {
   if (*send_cpu >= 0) c.send_cpus = {static_cast<int>(*send_cpu)};
   if (*recv_cpu >= 0) c.recv_cpus = {static_cast<int>(*recv_cpu)};
   c.zerocopy_send = *zc;
+  c.thp_source = *thp;
   c.ring_pages = static_cast<int>(*pages);
   std::printf("{\"object_mib\": %lld, \"reads\": %lld, \"ring_kib\": %lld, \"recv_kib\": %lld",
               static_cast<long long>(*obj_mib), static_cast<long long>(*reads), static_cast<long long>(*ring_kib),

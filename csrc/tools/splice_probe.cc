@@ -19,6 +19,7 @@
 #include <sys/resource.h>
 #include <sys/sendfile.h>
 #include <sys/socket.h>
+#include <sys/uio.h>
 #include <unistd.h>
 
 #include <arpa/inet.h>
@@ -96,23 +97,56 @@ int main(int argc, char** argv) {
   int64_t* total_p = f.Int("total", int64_t(4) << 30, "bytes to move");
   int64_t* pipe_p = f.Int("pipe", 1 << 20, "pipe size (F_SETPIPE_SZ)");
   int64_t* obj_p = f.Int("object", int64_t(256) << 20, "memfd object size the payloads are sendfile()d from");
+  std::string* src_p = f.String("src", "memfd", "payload source: memfd (sendfile, page cache as written), "
+                                "memfd_thp (sendfile, memfd filled through a MADV_HUGEPAGE mapping), "
+                                "anon_thp (vmsplice + splice from anonymous THP memory)");
   f.Parse(argc, argv);
   const std::string mode = *mode_p, send_cpu = *send_cpu_p, recv_cpu = *recv_cpu_p, worker_cpus = *worker_cpus_p;
   const int64_t streams = *streams_p, msg = *msg_p, total = *total_p, pipe_sz = *pipe_p, obj = *obj_p;
+  const std::string src_kind = *src_p;
   const bool splice_mode = mode == "splice";
   const size_t M = static_cast<size_t>(msg);
   const int64_t nmsg = total / msg;
 
   int mfd = memfd_create("probe-object", 0);
   if (mfd < 0 || ftruncate(mfd, obj) != 0) die("memfd");
+  uint8_t* anon = nullptr;
+  long huge_kib = -1;
   {
     std::thread t([&] {
       gcsb::pin_current_thread(parse_cpus(send_cpu));
       std::vector<uint8_t> b(1 << 20);
       for (size_t i = 0; i < b.size(); ++i) b[i] = static_cast<uint8_t>(i * 131 + 7);
-      for (int64_t o = 0; o < obj; o += b.size()) pwrite(mfd, b.data(), b.size(), o);
+      if (src_kind == "memfd") {
+        for (int64_t o = 0; o < obj; o += b.size())
+          if (pwrite(mfd, b.data(), b.size(), o) < 0) die("pwrite");
+      } else if (src_kind == "memfd_thp") {
+        void* m = mmap(nullptr, obj, PROT_READ | PROT_WRITE, MAP_SHARED, mfd, 0);
+        if (m == MAP_FAILED) die("mmap memfd");
+        madvise(m, obj, MADV_HUGEPAGE);
+        for (int64_t o = 0; o < obj; o += b.size()) std::memcpy(static_cast<uint8_t*>(m) + o, b.data(), b.size());
+        munmap(m, obj);
+      } else {
+        void* m = mmap(nullptr, obj + (2 << 20), PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        if (m == MAP_FAILED) die("mmap anon");
+        uint8_t* a = reinterpret_cast<uint8_t*>((reinterpret_cast<uintptr_t>(m) + (2 << 20) - 1) & ~uintptr_t((2 << 20) - 1));
+        madvise(a, obj, MADV_HUGEPAGE);
+        for (int64_t o = 0; o < obj; o += b.size()) std::memcpy(a + o, b.data(), b.size());
+        anon = a;
+      }
     });
     t.join();
+  }
+  {
+    // huge pages behind the source: ShmemHugePages / AnonHugePages in meminfo
+    FILE* mi = fopen("/proc/meminfo", "r");
+    char line[256];
+    while (mi && fgets(line, sizeof(line), mi)) {
+      long v;
+      if (src_kind != "anon_thp" && sscanf(line, "ShmemHugePages: %ld", &v) == 1) huge_kib = v;
+      if (src_kind == "anon_thp" && sscanf(line, "AnonHugePages: %ld", &v) == 1) huge_kib = v;
+    }
+    if (mi) fclose(mi);
   }
   int ls = socket(AF_INET, SOCK_STREAM, 0);
   sockaddr_in a{};
@@ -138,6 +172,26 @@ int main(int argc, char** argv) {
       if (src + static_cast<off_t>(M) > obj) src = 0;
       off_t o = src;
       size_t left = M;
+      if (anon) {
+        // vmsplice the pages into a pipe, splice the pipe into the socket
+        static thread_local int sp[2] = {-1, -1};
+        if (sp[0] < 0) {
+          if (pipe2(sp, O_CLOEXEC) != 0) die("pipe2");
+          fcntl(sp[1], F_SETPIPE_SZ, 1 << 20);
+        }
+        while (left) {
+          iovec iov{anon + o, std::min<size_t>(left, 1 << 20)};
+          ssize_t k = vmsplice(sp[1], &iov, 1, 0);
+          if (k <= 0) die("vmsplice");
+          o += k;
+          left -= static_cast<size_t>(k);
+          while (k > 0) {
+            ssize_t w = splice(sp[0], nullptr, s, nullptr, static_cast<size_t>(k), SPLICE_F_MOVE | SPLICE_F_MORE);
+            if (w <= 0) die("splice out");
+            k -= w;
+          }
+        }
+      }
       while (left) {
         ssize_t w = sendfile(s, mfd, &o, left);
         if (w <= 0) die("sendfile");
@@ -292,10 +346,10 @@ int main(int argc, char** argv) {
   std::printf(
       "{\"mode\":\"%s\",\"streams\":%lld,\"msg\":%lld,\"pipe\":%d,\"gbps\":%.2f,\"reader_cpu_s_per_gib\":%.4f,"
       "\"workers_cpu_s_per_gib\":%.4f,\"sender_cpu_s_per_gib\":%.4f,\"splices\":%llu,\"avg_splice_kib\":%.1f,"
-      "\"eagain\":%llu,\"recvs\":%llu,\"buffered_copy_frac\":%.4f}\n",
+      "\"eagain\":%llu,\"recvs\":%llu,\"buffered_copy_frac\":%.4f,\"src\":\"%s\",\"src_huge_kib\":%ld}\n",
       mode.c_str(), (long long)streams, (long long)msg, got_pipe, static_cast<double>(nmsg) * M / el / 1e9,
       reader_cpu / gib, wcpu / gib, send_cpu_s / gib, (unsigned long long)splices,
       splices ? spliced / 1024.0 / splices : 0.0, (unsigned long long)eagain, (unsigned long long)recvs,
-      static_cast<double>(buffered_copy) / (static_cast<double>(nmsg) * M));
+      static_cast<double>(buffered_copy) / (static_cast<double>(nmsg) * M), src_kind.c_str(), huge_kib);
   return 0;
 }

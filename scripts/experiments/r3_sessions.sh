@@ -26,6 +26,31 @@ step() {  # step <name> <timeout> <cmd...>: a crash, abort or timeout ends the s
 }
 
 case "$S" in
+thpsend)  # profiles/r3_thp_send: endpoint sends synthetic bodies by vmsplice from THP vs sendfile from the memfd
+  for rep in 1 2; do
+    for v in sendfile vmsplice; do
+      step "bench_${v}_r$rep" 300 env GCSB_SRV_SEND=$v python3 bench.py --steps 20 --warmup 3 \
+        --json-out "$O/bench_${v}_r$rep.json"
+    done
+  done
+  step pytest_gpu 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+  ;;
+thpsrc)  # profiles/r3_splice: receiver cost by the sender's page size (4 KiB page cache vs THP)
+  { uname -r; cat /sys/kernel/mm/transparent_hugepage/enabled /sys/kernel/mm/transparent_hugepage/shmem_enabled;
+    grep -i huge /proc/meminfo; } > "$O/env.txt" 2>&1
+  P=custom_go_client_benchmark_amd/bin/splice_probe
+  for rep in 1 2; do
+    for src in memfd anon_thp memfd_thp; do
+      for st in 1 8; do
+        step "probe_${src}_s${st}_r$rep" 60 $P -mode recv -streams $st -total $((16<<30)) -send-cpu 2 -recv-cpu 1 -src $src
+        cat "$O/probe_${src}_s${st}_r$rep.log" >> "$O/probe.jsonl"
+      done
+    done
+  done
+  step probe_anon_thp_splice_s8 60 $P -mode splice -streams 8 -total $((16<<30)) -send-cpu 2 -recv-cpu 1 -src anon_thp \
+    -worker-cpus 3,4,5,6,7,129,130,131
+  cat "$O/probe_anon_thp_splice_s8.log" >> "$O/probe.jsonl"
+  ;;
 splice)  # profiles/r3_splice: multiplexed-reader cost, recv() copy vs splice() into per-stream pipes
   { uname -r; cat /proc/sys/fs/pipe-max-size /proc/sys/fs/pipe-user-pages-soft; id -u;
     lscpu | grep -E "^(Model name|L3|NUMA node)"; } > "$O/env.txt" 2>&1

@@ -78,12 +78,12 @@ def test_relayed_stream_cut_after_last_byte(native, server, ranged):
 
 
 def test_runner_relays_when_streams_share_a_connection(native, server):
-    """Auto mode: 16 workers on one connection relay every read; the pipes
-    go back to the pool clean (the next reads reuse them)."""
+    """16 workers on one connection relay every read; the pipes go back to
+    the pool clean (the next reads reuse them)."""
     server.add_synthetic(B, P, "", 0, 16, 2 << 20)
     s0 = native.pipe_relay_stats()
     run = native.Runner({"protocol": "grpc", "endpoint": server.url, "bucket": B, "workers": 16,
-                         "reads_per_worker": 4, "grpc_conn_pool_size": 1})
+                         "reads_per_worker": 4, "grpc_conn_pool_size": 1, "splice_recv": 1})
     run.start()
     run.wait()
     s = run.summary()
@@ -93,14 +93,27 @@ def test_runner_relays_when_streams_share_a_connection(native, server):
     assert s1["pipes"] - s0["pipes"] <= 16  # reused, not one per read
 
 
-def test_runner_single_stream_keeps_direct_path(native, server):
-    server.add_synthetic(B, P, "", 0, 1, 1 << 20)
+@pytest.mark.parametrize("proto", ["grpc", "http2"])
+def test_relayed_many_streams_one_connection(native, server, proto):
+    server.add_synthetic(B, P, "", 0, 8, (3 << 20) + 5)
     s0 = native.pipe_relay_stats()
-    run = native.Runner({"protocol": "grpc", "endpoint": server.url, "bucket": B, "workers": 1,
+    run = native.Runner({"protocol": proto, "endpoint": server.url, "bucket": B, "workers": 8,
+                         "reads_per_worker": 3, "grpc_conn_pool_size": 1, "splice_recv": 1})
+    run.start()
+    run.wait()
+    s = run.summary()
+    assert s["errors"] == 0 and s["verified"] == 24
+    assert _relayed(native, s0)[0] == 24
+
+
+def test_runner_default_keeps_direct_path(native, server):
+    server.add_synthetic(B, P, "", 0, 8, 1 << 20)
+    s0 = native.pipe_relay_stats()
+    run = native.Runner({"protocol": "grpc", "endpoint": server.url, "bucket": B, "workers": 8,
                          "reads_per_worker": 2, "grpc_conn_pool_size": 1})
     run.start()
     run.wait()
-    assert run.summary()["verified"] == 2
+    assert run.summary()["verified"] == 16
     assert _relayed(native, s0)[0] == 0
 
 
@@ -109,7 +122,8 @@ def test_relayed_concurrent_reads_with_read_timeout(native, server):
     neighbours' relayed reads complete."""
     server.add_synthetic(B, P, "", 0, 8, 4 << 20)
     run = native.Runner({"protocol": "grpc", "endpoint": server.url, "bucket": B, "workers": 8,
-                         "reads_per_worker": 3, "grpc_conn_pool_size": 1, "io_timeout_ms": 5000})
+                         "reads_per_worker": 3, "grpc_conn_pool_size": 1, "io_timeout_ms": 5000,
+                         "splice_recv": 1})
     run.start()
     run.wait()
     s = run.summary()

@@ -1006,6 +1006,8 @@ def run_rank(args) -> int:
                         b["recv_avg_kib"] = st["cpu"]["recv_avg_kib"]
                     if st["cpu"].get("recv_queue"):
                         b["recv_queue"] = st["cpu"]["recv_queue"]
+                    if st["cpu"].get("pipe_relay"):
+                        b["pipe_relay"] = st["cpu"]["pipe_relay"]
                 if key.startswith("ref_default_"):
                     b["first_read_p50_ms"] = round(st["first_p50_max"], 3)
                     b["steady_p99_ms"] = round(st["steady_p99_max"], 3)

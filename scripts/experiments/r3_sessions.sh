@@ -26,6 +26,12 @@ step() {  # step <name> <timeout> <cmd...>: a crash, abort or timeout ends the s
 }
 
 case "$S" in
+muxdiag)  # profiles/r3_mux_thp: multiplexed reader with the THP source, recv() wall time inside DATA dispatch
+  for rep in 1 2; do
+    step "bench_diag_r$rep" 300 env GCSB_RECV_DIAG=1 python3 bench.py --steps 20 --warmup 3 \
+      --blocks list_read,ref_default --json-out "$O/bench_diag_r$rep.json"
+  done
+  ;;
 thpsend)  # profiles/r3_thp_send: endpoint sends synthetic bodies by vmsplice from THP vs sendfile from the memfd
   for rep in 1 2; do
     for v in sendfile vmsplice; do

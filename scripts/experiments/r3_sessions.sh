@@ -26,6 +26,23 @@ step() {  # step <name> <timeout> <cmd...>: a crash, abort or timeout ends the s
 }
 
 case "$S" in
+ringthp)  # profiles/r3_ring_thp: headline ring geometry with the THP source (receiver-bound now)
+  for rep in 1 2 3; do
+    for v in 8x2MiB 4x2MiB 8x1MiB 16x2MiB; do
+      n=${v%x*}; b=${v#*x}
+      step "bench_${v}_r$rep" 300 python3 bench.py --steps 20 --warmup 3 --slots $n --slot-bytes $b \
+        --blocks ceiling --json-out "$O/bench_${v}_r$rep.json"
+    done
+  done
+  ;;
+muxiso)  # profiles/r3_mux_thp/isolate: multiplexed reader on its own core vs shared, THP source
+  for rep in 1 2 3; do
+    for v in shared isolate; do
+      step "bench_${v}_r$rep" 300 python3 bench.py --steps 20 --warmup 3 --mux-reader $v \
+        --blocks list_read,ref_default --json-out "$O/bench_${v}_r$rep.json"
+    done
+  done
+  ;;
 muxdiag)  # profiles/r3_mux_thp: multiplexed reader with the THP source, recv() wall time inside DATA dispatch
   for rep in 1 2; do
     step "bench_diag_r$rep" 300 env GCSB_RECV_DIAG=1 python3 bench.py --steps 20 --warmup 3 \

@@ -944,6 +944,9 @@ def run_rank(args) -> int:
                 "per_rank_mib_s": [round(b / max(e, 1e-12) / (1 << 20), 1)
                                    for b, e in zip(head["nbytes_per_rank"], head["elapsed_per_rank"])],
                 "endpoint": "loopback synthetic GCS (one per rank)",
+                # how the endpoint sends object bodies (profiles/r3_thp_send)
+                "endpoint_send": ("sendfile (memfd page cache)" if os.environ.get("GCSB_SRV_SEND") == "sendfile"
+                                  else "vmsplice (THP copy of the pattern)"),
                 "affinity": aff,
                 "placement": {k: placement.get(k) for k in ("client", "server", "aux", "picked_by", "busy")
                               if placement.get(k) is not None},

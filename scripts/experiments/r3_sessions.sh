@@ -26,6 +26,11 @@ step() {  # step <name> <timeout> <cmd...>: a crash, abort or timeout ends the s
 }
 
 case "$S" in
+check8thp)  # profiles/r3_rehearsal8/thp, r3_final/prof: 8-rank gloo rehearsal and a kernel profile with the THP endpoint
+  step rehearsal8 500 env GCSB_DIST_BACKEND=gloo python3 bench.py --gpus 8 --object-size 64MiB --steps 5 --side-steps 3
+  step rocprof 400 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$O/prof" -o bench -- \
+    python3 bench.py --steps 10 --warmup 2
+  ;;
 ringthp)  # profiles/r3_ring_thp: headline ring geometry with the THP source (receiver-bound now)
   for rep in 1 2 3; do
     for v in 8x2MiB 4x2MiB 8x1MiB 16x2MiB; do

@@ -999,8 +999,9 @@ def run_rank(args) -> int:
                     out[key] = st
                     continue
                 b = block_json(st, **{k: v for k, v in extra.items() if v is not None})
-                if key.startswith(("ref_default_", "list_read_")) and st.get("cpu"):
-                    # many streams on one connection (gRPC pool 1): where the CPU goes
+                if key.startswith(("ref_default_", "list_read_", "compare", "cpu_baseline")) and st.get("cpu"):
+                    # where the CPU goes: many streams on one connection (gRPC
+                    # pool 1), or the headline's twins (one stream each)
                     b["cpu_s_per_gib_by_thread"] = st["cpu"].get("cpu_s_per_gib_by_name", {})
                     b["cpus_busy"] = st["cpu"].get("cpus_busy")
                     if st["cpu"].get("h2_reader"):

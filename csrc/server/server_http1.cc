@@ -3,11 +3,13 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <ctime>
 #include <set>
 #include <thread>
 
+#include "core/content.h"
 #include "core/crc32c.h"
 #include "core/json.h"
 #include "core/util.h"
@@ -308,7 +310,12 @@ class Http1Handler {
     int64_t stall = f.stall_count.load() > 0 ? f.stall_at.load() : -1;
     int64_t t0 = now_ns();
     uint64_t sent = 0;
-    const uint64_t piece_max = 8 << 20;
+    // bytes per send call (GCSB_SRV_HTTP_PIECE, A/B; kPatternExt at most)
+    static const uint64_t piece_max = [] {
+      const char* e = std::getenv("GCSB_SRV_HTTP_PIECE");
+      const long long v = e ? std::atoll(e) : 0;
+      return v >= 4096 && v <= static_cast<long long>(kPatternExt) ? static_cast<uint64_t>(v) : uint64_t(8) << 20;
+    }();
     while (sent < len) {
       uint64_t off = start + sent;
       uint64_t n = std::min<uint64_t>(piece_max, len - sent);

@@ -26,6 +26,20 @@ step() {  # step <name> <timeout> <cmd...>: a crash, abort or timeout ends the s
 }
 
 case "$S" in
+httppiece)  # profiles/r3_twins/http_piece: HTTP one-stream read, endpoint send call size
+  for rep in 1 2; do
+    for v in 8388608 2097152 1048576 16777216; do
+      step "bench_p${v}_r$rep" 300 env GCSB_RECV_DIAG=1 GCSB_SRV_HTTP_PIECE=$v python3 bench.py --steps 20 --warmup 3 \
+        --protocol http --blocks ceiling --json-out "$O/bench_p${v}_r$rep.json"
+    done
+  done
+  ;;
+twins)  # profiles/r3_twins: per-thread CPU of the headline's HTTP / reference-semantics twins
+  for rep in 1 2; do
+    step "bench_r$rep" 300 env GCSB_RECV_DIAG=1 python3 bench.py --steps 20 --warmup 3 \
+      --blocks cpu_baseline,compare --json-out "$O/bench_r$rep.json"
+  done
+  ;;
 check8thp)  # profiles/r3_rehearsal8/thp, r3_final/prof: 8-rank gloo rehearsal and a kernel profile with the THP endpoint
   step rehearsal8 500 env GCSB_DIST_BACKEND=gloo python3 bench.py --gpus 8 --object-size 64MiB --steps 5 --side-steps 3
   step rocprof 400 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$O/prof" -o bench -- \

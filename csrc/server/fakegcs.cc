@@ -111,6 +111,12 @@ void FakeGcsServer::accept_loop() {
 void FakeGcsServer::handle_conn(int fd) {
   SocketOptions so;
   so.sndbuf = cfg_.sndbuf;
+  // GCSB_SRV_SNDBUF: an explicit send buffer for every endpoint connection (A/B)
+  static const int env_sndbuf = [] {
+    const char* e = std::getenv("GCSB_SRV_SNDBUF");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (env_sndbuf > 0) so.sndbuf = env_sndbuf;
   so.rcvbuf = 0;
   if (tls_ctx_) {
     // TLS: the protocol comes from ALPN (h2 = gRPC, else HTTP/1.1)

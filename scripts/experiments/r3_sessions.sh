@@ -26,6 +26,14 @@ step() {  # step <name> <timeout> <cmd...>: a crash, abort or timeout ends the s
 }
 
 case "$S" in
+sndbuf)  # profiles/r3_twins/sndbuf: HTTP / gRPC one-stream read by endpoint send buffer (autotuned vs explicit)
+  for rep in 1 2; do
+    for v in 0 33554432 8388608; do
+      step "bench_s${v}_r$rep" 300 env GCSB_RECV_DIAG=1 GCSB_SRV_SNDBUF=$v python3 bench.py --steps 20 --warmup 3 \
+        --blocks compare,ceiling --json-out "$O/bench_s${v}_r$rep.json"
+    done
+  done
+  ;;
 httppiece)  # profiles/r3_twins/http_piece: HTTP one-stream read, endpoint send call size
   for rep in 1 2; do
     for v in 8388608 2097152 1048576 16777216; do

@@ -396,6 +396,7 @@ def run_rank(args) -> int:
         rd0 = n.recv_diag()
         h2s0 = n.h2_reader_stats()
         pr0 = n.pipe_relay_stats()
+        sv0 = srv.stats()
         if use_gpu:
             n.reset_slow_hip_calls()
         if not err:
@@ -432,6 +433,19 @@ def run_rank(args) -> int:
                                     "headers_s_per_gib": round(d["headers_ns"] / 1e9 / g, 4),
                                     "other_s_per_gib": round(d["other_ns"] / 1e9 / g, 4),
                                     "avg_data_frame_kib": round(d["data_bytes"] / max(1, d["data_frames"]) / 1024, 1)}
+            sv1 = srv.stats()
+            if sv1.get("body_sends", 0) > sv0.get("body_sends", 0):
+                # the endpoint's sends of this block's bodies, by the kernel's
+                # send chronographs: busy, held by the client's receive window
+                # (the client is the bound), held by its own send buffer
+                wall = max(1, sv1["body_wall_us"] - sv0["body_wall_us"])
+                sends = sv1["body_sends"] - sv0["body_sends"]
+                cpu["endpoint_tcp"] = {
+                    "busy_frac": round((sv1["tcp_busy_us"] - sv0["tcp_busy_us"]) / wall, 3),
+                    "rwnd_limited_frac": round((sv1["tcp_rwnd_limited_us"] - sv0["tcp_rwnd_limited_us"]) / wall, 3),
+                    "sndbuf_limited_frac": round((sv1["tcp_sndbuf_limited_us"] - sv0["tcp_sndbuf_limited_us"]) / wall,
+                                                 3),
+                    "cwnd_kib_at_end": round((sv1["tcp_cwnd_bytes_sum"] - sv0["tcp_cwnd_bytes_sum"]) / sends / 1024, 1)}
             pr1 = n.pipe_relay_stats()
             if pr1["relays"] + pr1["no_pipe"] > pr0["relays"] + pr0["no_pipe"]:
                 # multiplexed reads relayed through per-read pipes (storage/pipe_relay.h):
@@ -1012,6 +1026,8 @@ def run_rank(args) -> int:
                         b["recv_queue"] = st["cpu"]["recv_queue"]
                     if st["cpu"].get("pipe_relay"):
                         b["pipe_relay"] = st["cpu"]["pipe_relay"]
+                    if st["cpu"].get("endpoint_tcp"):
+                        b["endpoint_tcp"] = st["cpu"]["endpoint_tcp"]
                 if key.startswith("ref_default_"):
                     b["first_read_p50_ms"] = round(st["first_p50_max"], 3)
                     b["steady_p99_ms"] = round(st["steady_p99_max"], 3)

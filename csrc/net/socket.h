@@ -148,6 +148,15 @@ class Listener {
 };
 
 void apply_socket_options(int fd, const SocketOptions& opt);
+// The kernel's per-connection send chronographs (TCP_INFO): microseconds the
+// sender was busy, limited by the peer's receive window, or limited by its
+// own send buffer; plus the congestion window in bytes.  false if the kernel
+// does not report them.
+struct TcpChrono {
+  uint64_t busy_us = 0, rwnd_limited_us = 0, sndbuf_limited_us = 0;
+  uint64_t cwnd_bytes = 0;
+};
+bool read_tcp_chrono(int fd, TcpChrono* out);
 // write() into a non-blocking pipe: bytes written, -1 if it is full; throws on
 // other errors.
 ssize_t pipe_write(int pipe_w, const void* p, size_t n);

@@ -1,0 +1,27 @@
+// TCP_INFO's send chronographs need the kernel's struct tcp_info (glibc's
+// <netinet/tcp.h> copy predates them), so this lives apart from socket.cc.
+#include <linux/tcp.h>
+#include <netinet/in.h>
+#include <sys/socket.h>
+
+#include <cstddef>
+#include <cstring>
+
+#include "net/socket.h"
+
+namespace gcsb {
+
+bool read_tcp_chrono(int fd, TcpChrono* out) {
+  struct tcp_info ti;
+  std::memset(&ti, 0, sizeof(ti));
+  socklen_t len = sizeof(ti);
+  if (::getsockopt(fd, IPPROTO_TCP, TCP_INFO, &ti, &len) != 0) return false;
+  if (len < offsetof(struct tcp_info, tcpi_sndbuf_limited) + sizeof(ti.tcpi_sndbuf_limited)) return false;
+  out->busy_us = ti.tcpi_busy_time;
+  out->rwnd_limited_us = ti.tcpi_rwnd_limited;
+  out->sndbuf_limited_us = ti.tcpi_sndbuf_limited;
+  out->cwnd_bytes = static_cast<uint64_t>(ti.tcpi_snd_cwnd) * ti.tcpi_snd_mss;
+  return true;
+}
+
+}  // namespace gcsb

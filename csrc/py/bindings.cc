@@ -621,6 +621,12 @@ class PyServer {
     d["bytes_received"] = s.bytes_received.load();
     d["faults_injected"] = s.faults_injected.load();
     d["auth_failures"] = s.auth_failures.load();
+    d["body_sends"] = s.body_sends.load();
+    d["body_wall_us"] = s.body_wall_us.load();
+    d["tcp_busy_us"] = s.tcp_busy_us.load();
+    d["tcp_rwnd_limited_us"] = s.tcp_rwnd_limited_us.load();
+    d["tcp_sndbuf_limited_us"] = s.tcp_sndbuf_limited_us.load();
+    d["tcp_cwnd_bytes_sum"] = s.tcp_cwnd_bytes_sum.load();
     return d;
   }
   std::string issue_token() { return srv_->issue_token(); }

@@ -14,6 +14,17 @@
 
 namespace gcsb {
 
+void ServerStats::note_body_send(int fd, const TcpChrono& a, bool a_ok, int64_t t0_ns) {
+  TcpChrono b;
+  if (!a_ok || !read_tcp_chrono(fd, &b)) return;
+  ++body_sends;
+  body_wall_us += static_cast<uint64_t>((now_ns() - t0_ns) / 1000);
+  tcp_busy_us += b.busy_us - a.busy_us;
+  tcp_rwnd_limited_us += b.rwnd_limited_us - a.rwnd_limited_us;
+  tcp_sndbuf_limited_us += b.sndbuf_limited_us - a.sndbuf_limited_us;
+  tcp_cwnd_bytes_sum += b.cwnd_bytes;
+}
+
 FakeGcsServer::FakeGcsServer(ServerConfig cfg, std::shared_ptr<ObjectStore> store)
     : cfg_(std::move(cfg)), store_(std::move(store)) {}
 

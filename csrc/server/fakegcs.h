@@ -49,6 +49,13 @@ struct ServerConfig {
 struct ServerStats {
   std::atomic<uint64_t> connections{0}, http_requests{0}, grpc_calls{0}, bytes_sent{0}, bytes_received{0},
       faults_injected{0}, auth_failures{0};
+  // object-body sends (HTTP GET bodies, gRPC ReadObject streams): the
+  // kernel's send chronographs over each (TCP_INFO deltas, us) and the
+  // congestion window at its end -- what bounded the endpoint's sending
+  std::atomic<uint64_t> body_sends{0}, body_wall_us{0}, tcp_busy_us{0}, tcp_rwnd_limited_us{0},
+      tcp_sndbuf_limited_us{0}, tcp_cwnd_bytes_sum{0};
+  // account one body send on fd that started at t0_ns with chronographs a
+  void note_body_send(int fd, const TcpChrono& a, bool a_ok, int64_t t0_ns);
 };
 
 class FakeGcsServer {

@@ -796,6 +796,8 @@ class H2ServerConn {
     int64_t stall = f.stall_count.load() > 0 ? f.stall_at.load() : -1;
     const int64_t bps = f.throttle_bps.load();
     const int64_t t0 = now_ns();
+    TcpChrono chrono0;
+    const bool chrono_ok = read_tcp_chrono(bc_.conn().fd(), &chrono0);
     uint64_t off = static_cast<uint64_t>(start);
     bool first = true;
     uint64_t sent = 0;
@@ -857,6 +859,7 @@ class H2ServerConn {
       }
     } while (off < end);
     srv_.stats().bytes_sent += sent;
+    srv_.stats().note_body_send(bc_.conn().fd(), chrono0, chrono_ok, t0);
     if (f.drop_trailers_count.load() > 0 && f.drop_trailers_count.fetch_sub(1) > 0) {
       // every requested byte is out, the status never comes (reset / GOAWAY race)
       ++srv_.stats().faults_injected;

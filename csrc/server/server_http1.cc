@@ -310,6 +310,8 @@ class Http1Handler {
     int64_t stall = f.stall_count.load() > 0 ? f.stall_at.load() : -1;
     int64_t t0 = now_ns();
     uint64_t sent = 0;
+    TcpChrono chrono0;
+    const bool chrono_ok = read_tcp_chrono(c_.fd(), &chrono0);
     // bytes per send call (GCSB_SRV_HTTP_PIECE, A/B; kPatternExt at most)
     static const uint64_t piece_max = [] {
       const char* e = std::getenv("GCSB_SRV_HTTP_PIECE");
@@ -373,6 +375,7 @@ class Http1Handler {
       }
     }
     srv_.stats().bytes_sent += sent;
+    srv_.stats().note_body_send(c_.fd(), chrono0, chrono_ok, t0);
   }
 
   void xml_api(Request& r) {

@@ -251,10 +251,12 @@ align)  # profiles/r3_align: objects on page boundaries of the pattern (default)
     step "page_$k" 300 python3 bench.py --steps 20 --warmup 5 --blocks cpu_baseline,ceiling,list_read,ref_default
   done
   ;;
-listring)  # profiles/r3_w48_tail/listring: list-read ring footprint (8 workers x ring) with page-aligned objects
+listring)  # profiles/r3_mux_thp/listring: list-read ring footprint (8 workers x ring), THP endpoint
   for k in 1 2 3; do
-    step "r8x2_$k" 300 python3 bench.py --steps 5 --warmup 2 --blocks list_read --list-ring 8x2MiB
-    step "r2x1_$k" 300 python3 bench.py --steps 5 --warmup 2 --blocks list_read --list-ring 2x1MiB
+    for r in 8x2MiB 2x1MiB 4x1MiB; do
+      step "r${r}_$k" 300 python3 bench.py --steps 20 --warmup 3 --blocks list_read --list-ring $r \
+        --json-out "$O/r${r}_$k.json"
+    done
   done
   ;;
 final)  # profiles/r3_final: GPU suite, smoke, two full benches

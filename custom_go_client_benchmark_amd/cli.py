@@ -62,8 +62,9 @@ def build_flags() -> FlagSet:
     fs.int("max-conns-per-host", 100, "HTTP connection cap (reference MaxConnsPerHost = 100)")
     fs.string("sink", "discard", "discard (reference io.Discard) | gpu (pinned ring -> HBM, CRC32C on GPU)")
     fs.int("gpu-device", -1, "HIP device (default: LOCAL_RANK)")
-    fs.int("ring-slot-bytes", 8 << 20, "Pinned ring slot size")
-    fs.int("ring-slots", 4, "Pinned ring slots")
+    fs.int("ring-slot-bytes", 0, "Pinned ring slot size (0 = auto: 2 MiB for one worker, 1 MiB for several)")
+    fs.int("ring-slots", 0, "Pinned ring slots per worker (0 = auto: 8 for one worker, 2 for several: the "
+           "workers' receive destinations stay within an L3, profiles/r3_mux_thp/listring)")
     fs.string("landing", "object", "object (whole object in HBM) | ring (HBM ring, discard semantics)")
     fs.bool("gpu-verify", True, "Verify CRC32C with the GPU kernels")
     fs.int("slices", 1, "Sliced reads: N concurrent ranged streams per object, each on its own connection "
@@ -195,13 +196,19 @@ def main(argv: list[str] | None = None) -> int:
         latency_fd = lat_file.fileno()
     sys.stdout.flush()
 
+    # ring auto geometry: one worker gets the headline's 8 x 2 MiB; several
+    # get 2 x 1 MiB each, so all workers' receive destinations stay small
+    # (a 32 MiB ring footprint cost one receiving core 25-35%,
+    # profiles/r3_ring_thp, profiles/r3_mux_thp/listring)
+    ring_slot_bytes = fs.get("ring-slot-bytes") or ((2 << 20) if workers == 1 else (1 << 20))
+    ring_slots = fs.get("ring-slots") or (8 if workers == 1 else 2)
     opts = workloads.RunOptions(
         protocol=proto, endpoint=endpoint, bucket=fs.get("bucket"), object_prefix=fs.get("object-prefix"),
         object_suffix=fs.get("object-suffix"), workers=workers, reads_per_worker=fs.get("read-call-per-worker"),
         duration_s=fs.get("duration"), worker_id_offset=first, http_api=fs.get("http-api"),
         read_chunk=fs.get("read-chunk"), max_conns_per_host=fs.get("max-conns-per-host"),
         grpc_conn_pool_size=fs.get("grpc-conn-pool-size"), sink=sink, host_crc=fs.get("host-crc"), device=device,
-        ring_slot_bytes=fs.get("ring-slot-bytes"), ring_slots=fs.get("ring-slots"), landing=fs.get("landing"),
+        ring_slot_bytes=ring_slot_bytes, ring_slots=ring_slots, landing=fs.get("landing"),
         gpu_verify=fs.get("gpu-verify"), latency_fd=latency_fd, slices=fs.get("slices"),
         slice_min_bytes=fs.get("slice-min-bytes"), slice_piece_bytes=fs.get("slice-piece-bytes"),
         slice_piece_min_bytes=fs.get("slice-piece-min-bytes"),

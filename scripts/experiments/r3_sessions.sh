@@ -26,6 +26,15 @@ step() {  # step <name> <timeout> <cmd...>: a crash, abort or timeout ends the s
 }
 
 case "$S" in
+slicering)  # profiles/r3_ring_thp/sliced: sliced-read ring per sink (2 sinks per stream), THP endpoint
+  for k in 1 2 3; do
+    for r in 8x2MiB 4x1MiB 2x2MiB 4x2MiB; do
+      n=${r%x*}; b=${r#*x}
+      step "s${r}_$k" 300 python3 bench.py --steps 20 --warmup 3 --blocks sliced --sliced-slots $n \
+        --sliced-slot-bytes $b --json-out "$O/s${r}_$k.json"
+    done
+  done
+  ;;
 sndbuf)  # profiles/r3_twins/sndbuf: HTTP / gRPC one-stream read by endpoint send buffer (autotuned vs explicit)
   for rep in 1 2; do
     for v in 0 33554432 8388608; do

@@ -163,7 +163,10 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--sliced-slot-bytes", default="2MiB",
                     help="sliced block: ring slot per sink (2 MiB x 8 won 2 of 2 interleaved reps against 4 x 4 MiB, "
                          "8 MiB x 2, 4/16 pool streams and async hand-off: profiles/r2_sliced)")
-    ap.add_argument("--sliced-slots", type=int, default=8, help="sliced block: ring slots per sink")
+    ap.add_argument("--sliced-slots", type=int, default=2,
+                    help="sliced block: ring slots per sink. With the THP endpoint the receive copies are the "
+                         "bound and each stream's 2 sinks x ring is its destination footprint: 2 x 2 MiB ran "
+                         "46.3-49.9k MiB/s against 41.5-45.0k with 8 x 2 MiB (profiles/r3_ring_thp/sliced)")
     ap.add_argument("--sliced-async-submit", type=int, default=0, choices=[0, 1],
                     help="sliced block: slot hand-off on the device submitter thread (default inline)")
     ap.add_argument("--piece-bytes", default="8MiB",

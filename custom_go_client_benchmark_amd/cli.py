@@ -200,8 +200,10 @@ def main(argv: list[str] | None = None) -> int:
     # get 2 x 1 MiB each, so all workers' receive destinations stay small
     # (a 32 MiB ring footprint cost one receiving core 25-35%,
     # profiles/r3_ring_thp, profiles/r3_mux_thp/listring)
-    ring_slot_bytes = fs.get("ring-slot-bytes") or ((2 << 20) if workers == 1 else (1 << 20))
-    ring_slots = fs.get("ring-slots") or (8 if workers == 1 else 2)
+    # (sliced reads: 2 x 2 MiB per slice sink, profiles/r3_ring_thp/sliced)
+    sliced = fs.get("slices") > 1
+    ring_slot_bytes = fs.get("ring-slot-bytes") or ((2 << 20) if workers == 1 or sliced else (1 << 20))
+    ring_slots = fs.get("ring-slots") or (8 if workers == 1 and not sliced else 2)
     opts = workloads.RunOptions(
         protocol=proto, endpoint=endpoint, bucket=fs.get("bucket"), object_prefix=fs.get("object-prefix"),
         object_suffix=fs.get("object-suffix"), workers=workers, reads_per_worker=fs.get("read-call-per-worker"),

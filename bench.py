@@ -205,6 +205,9 @@ def build_parser() -> argparse.ArgumentParser:
                     help="ref_default_* side blocks: the reference's default experiment, -worker 48 on 1 MiB "
                          "objects, gRPC pool 1 vs HTTP keep-alive, discard sink + host CRC (0 = off)")
     ap.add_argument("--ref-reads", type=int, default=50, help="ref_default_*: timed reads per worker")
+    ap.add_argument("--ref-grpc-placement", default="share_quota", choices=["share_quota", "same", "share"],
+                    help="ref_default_grpc: CPU placement of the 48 workers, the endpoint and the one connection's "
+                         "reader (HTTP keeps share_quota: 48 receiving workers need the cores)")
     ap.add_argument("--ref-object-size", default="1MiB", help="ref_default_*: object size")
     ap.add_argument("--write-placement", default="pair", choices=["share", "pair"],
                     help="config-5 upload block: pair (uploader on one quiet core, endpoint receive + CRC on two "
@@ -785,7 +788,8 @@ def run_rank(args) -> int:
         CPU-quota budget (affinity share_quota)."""
         workers = args.ref_workers
         osz = parse_size(args.ref_object_size)
-        sh = affinity.plan(gpu, "share_quota", slot) if use_gpu else {"client": [], "server": []}
+        mode = args.ref_grpc_placement if proto != "http" else "share_quota"
+        sh = affinity.plan(gpu, mode, slot) if use_gpu else {"client": [], "server": []}
         if use_gpu and proto != "http" and args.mux_reader == "isolate":
             sh = affinity.isolate_reader(sh)
         ep = None

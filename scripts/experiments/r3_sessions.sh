@@ -26,6 +26,14 @@ step() {  # step <name> <timeout> <cmd...>: a crash, abort or timeout ends the s
 }
 
 case "$S" in
+refplace)  # profiles/r3_mux_thp/refplace: 48-worker gRPC placement (share_quota vs one L3 domain vs share)
+  for k in 1 2 3; do
+    for m in share_quota same share; do
+      step "p${m}_$k" 300 python3 bench.py --steps 20 --warmup 3 --blocks ref_default --ref-grpc-placement $m \
+        --json-out "$O/p${m}_$k.json"
+    done
+  done
+  ;;
 slicering)  # profiles/r3_ring_thp/sliced: sliced-read ring per sink (2 sinks per stream), THP endpoint
   for k in 1 2 3; do
     for r in 8x2MiB 4x1MiB 2x2MiB 4x2MiB; do

@@ -144,6 +144,13 @@ def main(argv: list[str] | None = None) -> int:
         # submitter, profiles/r2_placement); several readers share one L3 domain
         if sink == "gpu":
             aff = "share" if fs.get("slices") > 1 else ("pair" if fs.get("worker") == 1 else "same")
+        elif proto in ("grpc", "http2") and workers > max(1, fs.get("grpc-conn-pool-size")):
+            # many streams on few connections: each connection's one reader
+            # copies every byte, and its receive copy, the workers' CRC passes
+            # and the endpoint's sends want one L3 domain (48 x 1 MiB gRPC:
+            # 16.0-19.5k MiB/s against 8.4-8.8k over the quota's cores,
+            # profiles/r3_mux_thp/refplace)
+            aff = "same"
         else:
             aff = "quota"
         if fs.get("workload") == "write":
@@ -154,10 +161,15 @@ def main(argv: list[str] | None = None) -> int:
             # (profiles/r3_write/placement); composite uploads (slices > 1)
             # and CPU-only runs stay unpinned (profiles/r1_session4/)
             aff = "pair" if sink == "gpu" and fs.get("slices") <= 1 else "none"
-    if aff != "none" and (sink == "gpu" or aff == "quota"):
+    if aff != "none" and (sink == "gpu" or aff in ("quota", "same")):
         from .parallel import affinity
 
-        placement = affinity.plan(device, aff)
+        try:
+            placement = affinity.plan(device, aff)
+        except Exception:  # noqa: BLE001 - no GPU to place near (CPU-only host): the quota's cores
+            if sink == "gpu":
+                raise
+            placement = affinity.plan(device, "quota")
         if fs.get("workload") == "write" and aff == "pair":
             # the endpoint's receive thread and CRC worker get a core each;
             # this (uploading) thread the client core

@@ -241,7 +241,7 @@ def plan(device: int, mode: str = "split", slot: int = 0) -> dict:
             mine = trim_to_quota(mine, cpu_busy(0.1) if _quiet_sampling() else None)
         return {"client": mine, "server": mine, "mode": mode, "numa_node": node, "gpu_index_on_node": k,
                 "l3_domains": share}
-    if mode == "pair":
+    if mode in ("pair", "pair2"):
         # three quiet physical cores of one L3 domain of the rank's share
         # (with their SMT siblings): the client's receive thread, the
         # endpoint's send thread, the device submitter.  The domain and the
@@ -251,15 +251,23 @@ def plan(device: int, mode: str = "split", slot: int = 0) -> dict:
         busy = cpu_busy() if _quiet_sampling() else {}
         if busy:
             best = None
+            need = 5 if mode == "pair2" else 3
             for dom in doms:
                 q = quiet_cores(dom, busy)
-                if len(q) < 3:
+                if len(q) < need:
                     continue
                 load = sum(busy.get(c, 0.0) for core in q[:3] for c in core) + (1.0 if 0 in q[0] + q[1] else 0.0)
                 if best is None or load < best[0]:
                     best = (load, q)
             if best is not None:
                 q = best[1]
+                if mode == "pair2":
+                    # a second quiet core each for the client and the endpoint
+                    # thread: somewhere to go when another tenant's thread
+                    # lands on the first (the scheduler moves the busy one)
+                    return {"client": sorted(q[0] + q[3]), "server": sorted(q[1] + q[4]), "aux": q[2], "mode": mode,
+                            "numa_node": node, "gpu_index_on_node": k, "picked_by": "quiet",
+                            "busy": round(best[0], 3)}
                 return {"client": q[0], "server": q[1], "aux": q[2], "mode": mode, "numa_node": node,
                         "gpu_index_on_node": k, "picked_by": "quiet",
                         "busy": round(best[0], 3)}

@@ -26,6 +26,14 @@ step() {  # step <name> <timeout> <cmd...>: a crash, abort or timeout ends the s
 }
 
 case "$S" in
+pair2)  # profiles/r3_ring_thp/pair2: headline placement, one core each vs two cores each (tails)
+  for k in 1 2 3 4; do
+    for a in pair pair2; do
+      step "a${a}_$k" 300 python3 bench.py --steps 20 --warmup 3 --affinity $a --blocks ceiling \
+        --json-out "$O/a${a}_$k.json"
+    done
+  done
+  ;;
 refplace)  # profiles/r3_mux_thp/refplace: 48-worker gRPC placement (share_quota vs one L3 domain vs share)
   for k in 1 2 3; do
     for m in share_quota same share; do

@@ -111,6 +111,51 @@ def _err(msg: str):
     sys.stderr.flush()
 
 
+def auto_affinity(sink: str, proto: str, workers: int, pool: int, slices: int, workload: str) -> str:
+    """`-affinity auto`: the CPU placement (parallel/affinity.py plan mode).
+
+    - GPU sink: one reader with one stream per read gets the bench's
+      placement, a quiet core each for the receive thread, the endpoint and
+      the GPU submitter (profiles/r2_placement). Several readers share one L3
+      domain; sliced reads spread over the rank's share.
+    - Discard sink, gRPC / HTTP/2 with more workers than connections: each
+      connection's one reader copies every byte, and its receive copy, the
+      workers' CRC passes and the endpoint's sends want one L3 domain
+      (48 x 1 MiB gRPC: 16.0-19.5k MiB/s against 8.4-8.8k over the quota's
+      cores, profiles/r3_mux_thp/refplace).
+    - Other discard-sink runs: no GPU to be near; under a CPU quota the threads
+      keep to as many cores as the quota pays for.
+    - Uploads from HBM (spliced send, endpoint CRC on its write worker): three
+      quiet cores of one L3 domain -- the uploader, the endpoint's receive
+      thread, its CRC worker -- 18.0-21.6k MiB/s against 7.7-19.7k with the
+      threads spread (profiles/r3_write/placement); composite uploads
+      (slices > 1) and CPU-only uploads stay unpinned (profiles/r1_session4/).
+    """
+    if workload == "write":
+        return "pair" if sink == "gpu" and slices <= 1 else "none"
+    if sink == "gpu":
+        return "share" if slices > 1 else ("pair" if workers == 1 else "same")
+    if proto in ("grpc", "http2") and workers > max(1, pool):
+        return "same"
+    return "quota"
+
+
+def auto_ring(workers: int, slices: int) -> tuple[int, int]:
+    """(slot bytes, slots) of each GPU sink's pinned ring when the flags are 0.
+
+    The receive copy write-allocates its destination, so the rings' total
+    footprint matters: a 32 MiB ring cost one receiving core 25-35%
+    (profiles/r3_ring_thp). One worker gets the headline's 8 x 2 MiB; several
+    get 2 x 1 MiB each (8 list-readers: 18.6-18.8k MiB/s against 15.5-17.0k
+    with 8 x 2 MiB, profiles/r3_mux_thp/listring); sliced reads 2 x 2 MiB per
+    slice sink (profiles/r3_ring_thp/sliced)."""
+    if slices > 1:
+        return 2 << 20, 2
+    if workers == 1:
+        return 2 << 20, 8
+    return 1 << 20, 2
+
+
 def main(argv: list[str] | None = None) -> int:
     fs = build_flags().parse(sys.argv[1:] if argv is None else argv)
     proto = fs.get("client-protocol")
@@ -137,30 +182,7 @@ def main(argv: list[str] | None = None) -> int:
     placement = {"client": [], "server": []}
     aff = fs.get("affinity")
     if aff == "auto":
-        # discard sink: no GPU to be near; under a CPU quota keep the threads
-        # on as many cores as the quota pays for (parallel/affinity.py)
-        # one GPU reader with one stream per read: the bench's placement (a
-        # quiet core each for the receive thread, the endpoint and the GPU
-        # submitter, profiles/r2_placement); several readers share one L3 domain
-        if sink == "gpu":
-            aff = "share" if fs.get("slices") > 1 else ("pair" if fs.get("worker") == 1 else "same")
-        elif proto in ("grpc", "http2") and workers > max(1, fs.get("grpc-conn-pool-size")):
-            # many streams on few connections: each connection's one reader
-            # copies every byte, and its receive copy, the workers' CRC passes
-            # and the endpoint's sends want one L3 domain (48 x 1 MiB gRPC:
-            # 16.0-19.5k MiB/s against 8.4-8.8k over the quota's cores,
-            # profiles/r3_mux_thp/refplace)
-            aff = "same"
-        else:
-            aff = "quota"
-        if fs.get("workload") == "write":
-            # uploads: one from HBM (spliced send, endpoint CRC on its write
-            # worker) on three quiet cores of one L3 domain -- the uploader,
-            # the endpoint's receive thread, its CRC worker -- 18.0-21.6k
-            # MiB/s against 7.7-19.7k with the threads spread
-            # (profiles/r3_write/placement); composite uploads (slices > 1)
-            # and CPU-only runs stay unpinned (profiles/r1_session4/)
-            aff = "pair" if sink == "gpu" and fs.get("slices") <= 1 else "none"
+        aff = auto_affinity(sink, proto, workers, fs.get("grpc-conn-pool-size"), fs.get("slices"), fs.get("workload"))
     if aff != "none" and (sink == "gpu" or aff in ("quota", "same")):
         from .parallel import affinity
 
@@ -208,14 +230,9 @@ def main(argv: list[str] | None = None) -> int:
         latency_fd = lat_file.fileno()
     sys.stdout.flush()
 
-    # ring auto geometry: one worker gets the headline's 8 x 2 MiB; several
-    # get 2 x 1 MiB each, so all workers' receive destinations stay small
-    # (a 32 MiB ring footprint cost one receiving core 25-35%,
-    # profiles/r3_ring_thp, profiles/r3_mux_thp/listring)
-    # (sliced reads: 2 x 2 MiB per slice sink, profiles/r3_ring_thp/sliced)
-    sliced = fs.get("slices") > 1
-    ring_slot_bytes = fs.get("ring-slot-bytes") or ((2 << 20) if workers == 1 or sliced else (1 << 20))
-    ring_slots = fs.get("ring-slots") or (8 if workers == 1 and not sliced else 2)
+    auto_bytes, auto_slots = auto_ring(workers, fs.get("slices"))
+    ring_slot_bytes = fs.get("ring-slot-bytes") or auto_bytes
+    ring_slots = fs.get("ring-slots") or auto_slots
     opts = workloads.RunOptions(
         protocol=proto, endpoint=endpoint, bucket=fs.get("bucket"), object_prefix=fs.get("object-prefix"),
         object_suffix=fs.get("object-suffix"), workers=workers, reads_per_worker=fs.get("read-call-per-worker"),

@@ -94,7 +94,7 @@ def tcp_sysctls() -> dict:
     net.core.rmem_max (and doubled by the kernel)."""
     out = {}
     for k, path in (("rmem_max", "/proc/sys/net/core/rmem_max"), ("tcp_rmem", "/proc/sys/net/ipv4/tcp_rmem"),
-                    ("wmem_max", "/proc/sys/net/core/wmem_max")):
+                    ("wmem_max", "/proc/sys/net/core/wmem_max"), ("tcp_wmem", "/proc/sys/net/ipv4/tcp_wmem")):
         try:
             with open(path) as f:
                 out[k] = f.read().split()
@@ -104,6 +104,11 @@ def tcp_sysctls() -> dict:
                     out[k] = [int(x) for x in out[k]]
         except (OSError, ValueError):
             pass
+    try:
+        with open("/proc/sys/net/ipv4/tcp_congestion_control") as f:
+            out["tcp_congestion_control"] = f.read().strip()
+    except OSError:
+        pass
     return out
 
 

@@ -26,6 +26,17 @@ step() {  # step <name> <timeout> <cmd...>: a crash, abort or timeout ends the s
 }
 
 case "$S" in
+cc)  # profiles/r3_twins/cc: endpoint congestion control and connection age, HTTP one stream (compare) + headline
+  { cat /proc/sys/net/ipv4/tcp_congestion_control /proc/sys/net/ipv4/tcp_allowed_congestion_control \
+      /proc/sys/net/ipv4/tcp_available_congestion_control; } > "$O/env.txt" 2>&1
+  for k in 1 2; do
+    for v in default reno bbr cubic; do
+      cc=$v; [ "$v" = default ] && cc=
+      step "c${v}_$k" 300 env GCSB_SRV_CC=$cc python3 bench.py --steps 20 --warmup 3 --blocks compare,ceiling \
+        --json-out "$O/c${v}_$k.json"
+    done
+  done
+  ;;
 pair2)  # profiles/r3_ring_thp/pair2: headline placement, one core each vs two cores each (tails)
   for k in 1 2 3 4; do
     for a in pair pair2; do

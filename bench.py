@@ -977,6 +977,9 @@ def run_rank(args) -> int:
                 # how the endpoint sends object bodies (profiles/r3_thp_send)
                 "endpoint_send": ("sendfile (memfd page cache)" if os.environ.get("GCSB_SRV_SEND") == "sendfile"
                                   else "vmsplice (THP copy of the pattern)"),
+                # the endpoint sockets' congestion control (GCSB_SRV_CC; the
+                # host default is in config.sysctl, profiles/r3_twins/cc)
+                "endpoint_congestion_control": os.environ.get("GCSB_SRV_CC") or "cubic",
                 "affinity": aff,
                 "placement": {k: placement.get(k) for k in ("client", "server", "aux", "picked_by", "busy")
                               if placement.get(k) is not None},

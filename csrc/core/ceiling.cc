@@ -24,6 +24,7 @@
 
 #include "core/affinity.h"
 #include "core/hugebuf.h"
+#include "net/socket.h"
 
 namespace gcsb {
 
@@ -178,6 +179,7 @@ CeilingResult tcp_ceiling(const CeilingConfig& c) {
       pin_current_thread(c.send_cpus);
       Fd s(accept(ls.fd, nullptr, nullptr));
       if (s.fd < 0) fail("accept");
+      set_endpoint_congestion_control(s.fd);  // the endpoint's sender, as in server/fakegcs.cc
       int one = 1;
       setsockopt(s.fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
       std::vector<uint8_t> copybuf;

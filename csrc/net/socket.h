@@ -157,6 +157,15 @@ struct TcpChrono {
   uint64_t cwnd_bytes = 0;
 };
 bool read_tcp_chrono(int fd, TcpChrono* out);
+// The synthetic endpoint's congestion control on its connections
+// (GCSB_SRV_CC; default "cubic", "default" = the host's).  The GPU boxes
+// default to BBR, whose paced window on a loopback link held the endpoint's
+// congestion window at 2.3-3.8 MiB and cost the one-stream HTTP read 20-35%
+// (cubic: 7.9-9.7 MiB, profiles/r3_twins/cc).  An unprivileged process may
+// pick any algorithm in net.ipv4.tcp_allowed_congestion_control; a refusal
+// leaves the host's default.  The `ceiling` probe's sender uses it too.
+void set_endpoint_congestion_control(int fd);
+const std::string& endpoint_congestion_control();
 // write() into a non-blocking pipe: bytes written, -1 if it is full; throws on
 // other errors.
 ssize_t pipe_write(int pipe_w, const void* p, size_t n);

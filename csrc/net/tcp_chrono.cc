@@ -5,7 +5,9 @@
 #include <sys/socket.h>
 
 #include <cstddef>
+#include <cstdlib>
 #include <cstring>
+#include <string>
 
 #include "net/socket.h"
 
@@ -22,6 +24,21 @@ bool read_tcp_chrono(int fd, TcpChrono* out) {
   out->sndbuf_limited_us = ti.tcpi_sndbuf_limited;
   out->cwnd_bytes = static_cast<uint64_t>(ti.tcpi_snd_cwnd) * ti.tcpi_snd_mss;
   return true;
+}
+
+const std::string& endpoint_congestion_control() {
+  static const std::string cc = [] {
+    const char* e = std::getenv("GCSB_SRV_CC");
+    std::string v = e && *e ? e : "cubic";
+    return v == "default" ? std::string() : v;
+  }();
+  return cc;
+}
+
+void set_endpoint_congestion_control(int fd) {
+  const std::string& cc = endpoint_congestion_control();
+  if (!cc.empty())
+    (void)::setsockopt(fd, IPPROTO_TCP, TCP_CONGESTION, cc.data(), static_cast<socklen_t>(cc.size()));
 }
 
 }  // namespace gcsb

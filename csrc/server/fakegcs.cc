@@ -131,14 +131,7 @@ void FakeGcsServer::handle_conn(int fd) {
     return e ? std::atoi(e) : 0;
   }();
   if (env_sndbuf > 0) so.sndbuf = env_sndbuf;
-  // GCSB_SRV_CC: the endpoint connections' congestion control (A/B; an
-  // unprivileged process may pick from net.ipv4.tcp_allowed_congestion_control)
-  static const std::string env_cc = [] {
-    const char* e = std::getenv("GCSB_SRV_CC");
-    return std::string(e ? e : "");
-  }();
-  if (!env_cc.empty())
-    (void)::setsockopt(fd, IPPROTO_TCP, TCP_CONGESTION, env_cc.data(), static_cast<socklen_t>(env_cc.size()));
+  set_endpoint_congestion_control(fd);
   so.rcvbuf = 0;
   if (tls_ctx_) {
     // TLS: the protocol comes from ALPN (h2 = gRPC, else HTTP/1.1)

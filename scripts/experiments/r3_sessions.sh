@@ -26,6 +26,15 @@ step() {  # step <name> <timeout> <cmd...>: a crash, abort or timeout ends the s
 }
 
 case "$S" in
+ringcubic)  # profiles/r3_ring_thp/cubic: headline ring geometry with cubic endpoint sockets (bigger recv asks)
+  for k in 1 2 3; do
+    for v in 8x2MiB 4x4MiB 2x8MiB 4x2MiB; do
+      n=${v%x*}; b=${v#*x}
+      step "r${v}_$k" 300 python3 bench.py --steps 20 --warmup 3 --slots $n --slot-bytes $b --blocks ceiling \
+        --json-out "$O/r${v}_$k.json"
+    done
+  done
+  ;;
 cc)  # profiles/r3_twins/cc: endpoint congestion control and connection age, HTTP one stream (compare) + headline
   { cat /proc/sys/net/ipv4/tcp_congestion_control /proc/sys/net/ipv4/tcp_allowed_congestion_control \
       /proc/sys/net/ipv4/tcp_available_congestion_control; } > "$O/env.txt" 2>&1

@@ -102,22 +102,20 @@ bool PatternBuffer::send_by_vmsplice() {
 }
 
 const uint8_t* PatternBuffer::thp() const {
-  static std::mutex mu;
-  std::lock_guard<std::mutex> lk(mu);
-  if (thp_tried_) return thp_;
-  thp_tried_ = true;
-  try {
-    uint8_t* p = huge_alloc(buf_.size());  // faulted in here: on this thread's node
-    std::memcpy(p, buf_.data(), buf_.size());
-    thp_ = p;
-  } catch (const std::bad_alloc&) {
-    thp_ = nullptr;
-  }
-  return thp_;
+  // every body send asks: after the first call a plain atomic load, no lock
+  std::call_once(thp_once_, [this] {
+    try {
+      uint8_t* p = huge_alloc(buf_.size());  // faulted in here: on this thread's node
+      std::memcpy(p, buf_.data(), buf_.size());
+      thp_.store(p, std::memory_order_release);
+    } catch (const std::bad_alloc&) {
+    }
+  });
+  return thp_.load(std::memory_order_acquire);
 }
 
 std::vector<long> PatternBuffer::memfd_numa() const {
-  if (thp_) return numa_nodes_of(thp_, buf_.size());
+  if (const uint8_t* t = thp_.load(std::memory_order_acquire)) return numa_nodes_of(t, buf_.size());
   if (memfd_ < 0) return {};
   void* m = ::mmap(nullptr, buf_.size(), PROT_READ, MAP_SHARED | MAP_POPULATE, memfd_, 0);
   if (m == MAP_FAILED) return {};

@@ -57,6 +57,8 @@ struct ServerStats {
   // account one body send on fd that started at t0_ns with chronographs a
   void note_body_send(int fd, const TcpChrono& a, bool a_ok, int64_t t0_ns);
 };
+// bodies at least this long get their send chronographs read
+constexpr uint64_t kChronoMinBody = 8u << 20;
 
 class FakeGcsServer {
  public:

@@ -796,8 +796,10 @@ class H2ServerConn {
     int64_t stall = f.stall_count.load() > 0 ? f.stall_at.load() : -1;
     const int64_t bps = f.throttle_bps.load();
     const int64_t t0 = now_ns();
+    // send chronographs for big bodies only (see server_http1.cc)
     TcpChrono chrono0;
-    const bool chrono_ok = read_tcp_chrono(bc_.conn().fd(), &chrono0);
+    const bool chrono_ok = end - static_cast<uint64_t>(start) >= kChronoMinBody &&
+                           read_tcp_chrono(bc_.conn().fd(), &chrono0);
     uint64_t off = static_cast<uint64_t>(start);
     bool first = true;
     uint64_t sent = 0;

@@ -310,8 +310,10 @@ class Http1Handler {
     int64_t stall = f.stall_count.load() > 0 ? f.stall_at.load() : -1;
     int64_t t0 = now_ns();
     uint64_t sent = 0;
+    // send chronographs for big bodies only: two TCP_INFO calls per 1 MiB
+    // body would cost the many-small-reads blocks a few % of a core
     TcpChrono chrono0;
-    const bool chrono_ok = read_tcp_chrono(c_.fd(), &chrono0);
+    const bool chrono_ok = len >= kChronoMinBody && read_tcp_chrono(c_.fd(), &chrono0);
     // bytes per send call (GCSB_SRV_HTTP_PIECE, A/B; kPatternExt at most)
     static const uint64_t piece_max = [] {
       const char* e = std::getenv("GCSB_SRV_HTTP_PIECE");

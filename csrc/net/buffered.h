@@ -4,6 +4,7 @@
 // when the GPU sink is active), so object bytes are copied exactly once by the
 // kernel from socket buffers to their landing memory.
 #pragma once
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -42,12 +43,23 @@ class BufferedConn {
     }
   }
   // Read 1..n bytes directly (large-payload path). Returns 0 only on EOF.
+  // A large read also refills this buffer in the same recvmsg(): whatever
+  // follows the payload on the socket (the next frame or message header)
+  // is then parsed without a system call of its own (GCSB_RECV_REFILL=0:
+  // off, for A/Bs).
   size_t read_some(void* dst, size_t n) {
     if (buffered()) {
       size_t b = buffered() < n ? buffered() : n;
       std::memcpy(dst, buf_.get() + pos_, b);
       pos_ += b;
       return b;
+    }
+    if (n >= kRefillMin && refill_on()) {
+      pos_ = end_ = 0;
+      const size_t r = conn_->read_some2(dst, n, buf_.get(), kCap);
+      if (r <= n) return r;
+      end_ = r - n;
+      return n;
     }
     return conn_->read_some(dst, n);
   }
@@ -80,6 +92,14 @@ class BufferedConn {
 
  private:
   static constexpr size_t kCap = 16384;
+  static constexpr size_t kRefillMin = 64u << 10;
+  static bool refill_on() {
+    static const bool on = [] {
+      const char* e = std::getenv("GCSB_RECV_REFILL");
+      return !(e && *e == '0');
+    }();
+    return on;
+  }
   void fill() {
     if (pos_ == end_) pos_ = end_ = 0;
     if (end_ == kCap) {

@@ -427,6 +427,44 @@ ssize_t pipe_write(int pipe_w, const void* p, size_t n) {
   }
 }
 
+size_t Conn::read_some2(void* a, size_t na, void* b, size_t nb) {
+  if (ssl_ || nb == 0) return read_some(a, na);
+  if (fd_ < 0) throw StorageError("read on closed connection", true);
+  static const bool diag = [] {
+    const char* e = std::getenv("GCSB_RECV_DIAG");
+    return e && e[0] == '1';
+  }();
+  for (;;) {
+    int64_t t0 = 0;
+    if (diag && na >= (64u << 10)) {
+      int inq = 0;
+      if (::ioctl(fd_, SIOCINQ, &inq) == 0) {
+        g_diag_calls.fetch_add(1, std::memory_order_relaxed);
+        g_diag_want.fetch_add(na, std::memory_order_relaxed);
+        g_diag_inq.fetch_add(static_cast<uint64_t>(inq), std::memory_order_relaxed);
+        if (inq == 0) g_diag_empty.fetch_add(1, std::memory_order_relaxed);
+        else if (static_cast<size_t>(inq) < na) g_diag_short.fetch_add(1, std::memory_order_relaxed);
+        t0 = now_ns();
+      }
+    }
+    iovec iov[2] = {{a, na}, {b, nb}};
+    msghdr m{};
+    m.msg_iov = iov;
+    m.msg_iovlen = 2;
+    const ssize_t r = ::recvmsg(fd_, &m, 0);
+    if (t0) g_diag_ns.fetch_add(static_cast<uint64_t>(now_ns() - t0), std::memory_order_relaxed);
+    if (r >= 0) {
+      bytes_read_ += static_cast<uint64_t>(r);
+      g_recv_calls.fetch_add(1, std::memory_order_relaxed);
+      g_recv_bytes.fetch_add(static_cast<uint64_t>(r), std::memory_order_relaxed);
+      return static_cast<size_t>(r);
+    }
+    if (errno == EINTR) continue;
+    if (errno == EAGAIN || errno == EWOULDBLOCK) throw StorageError("read timeout", true);
+    throw StorageError(std::string("recv: ") + std::strerror(errno), true);
+  }
+}
+
 void Conn::read_exact(void* buf, size_t n) {
   auto* p = static_cast<uint8_t*>(buf);
   while (n > 0) {

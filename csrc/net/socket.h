@@ -89,6 +89,10 @@ class Conn {
 
   // Returns bytes read (0 = orderly EOF); throws StorageError(retryable) on reset.
   size_t read_some(void* buf, size_t n);
+  // One recvmsg() into a then b (plain TCP): bytes past na land in b.  A
+  // payload read that also picks up what follows it (the next frame's
+  // header) saves the header its own system call.  TLS: a alone.
+  size_t read_some2(void* a, size_t na, void* b, size_t nb);
   // Reads exactly n bytes or throws (EOF mid-way is a retryable error).
   void read_exact(void* buf, size_t n);
   void write_all(const void* buf, size_t n);

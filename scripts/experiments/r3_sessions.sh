@@ -26,6 +26,14 @@ step() {  # step <name> <timeout> <cmd...>: a crash, abort or timeout ends the s
 }
 
 case "$S" in
+refill)  # profiles/r3_refill: a payload recvmsg() that also refills the header buffer (GCSB_RECV_REFILL) vs not
+  for k in 1 2 3; do
+    for v in 0 1; do
+      step "f${v}_$k" 300 env GCSB_RECV_REFILL=$v python3 bench.py --steps 20 --warmup 3 \
+        --blocks compare,list_read,ceiling --json-out "$O/f${v}_$k.json"
+    done
+  done
+  ;;
 ringcubic)  # profiles/r3_ring_thp/cubic: headline ring geometry with cubic endpoint sockets (bigger recv asks)
   for k in 1 2 3; do
     for v in 8x2MiB 4x4MiB 2x8MiB 4x2MiB; do

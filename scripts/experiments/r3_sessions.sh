@@ -26,6 +26,12 @@ step() {  # step <name> <timeout> <cmd...>: a crash, abort or timeout ends the s
 }
 
 case "$S" in
+crcwaves)  # profiles/r3_crc_waves: slot kernel waves per workgroup inside the read pipeline (L2-cold tables)
+  for w in 2 4 8 1; do
+    step "prof_w$w" 300 env GCSB_CRC_SLOT_WAVES=$w rocprofv3 --kernel-trace --stats --output-format csv \
+      -d "$O/prof_w$w" -o b -- python3 bench.py --steps 20 --warmup 3 --blocks ceiling
+  done
+  ;;
 refill)  # profiles/r3_refill: a payload recvmsg() that also refills the header buffer (GCSB_RECV_REFILL) vs not
   for k in 1 2 3; do
     for v in 0 1; do

@@ -26,6 +26,14 @@ step() {  # step <name> <timeout> <cmd...>: a crash, abort or timeout ends the s
 }
 
 case "$S" in
+spincubic)  # profiles/r3_refill/spin: submitter polls before sleeping (no futex wake per slot on the reader), cubic
+  for k in 1 2 3 4; do
+    for v in 0 100; do
+      step "s${v}_$k" 300 env GCSB_SUBMIT_SPIN_US=$v python3 bench.py --steps 20 --warmup 3 --blocks ceiling \
+        --json-out "$O/s${v}_$k.json"
+    done
+  done
+  ;;
 crcwaves)  # profiles/r3_crc_waves: slot kernel waves per workgroup inside the read pipeline (L2-cold tables)
   for w in 2 4 8 1; do
     step "prof_w$w" 300 env GCSB_CRC_SLOT_WAVES=$w rocprofv3 --kernel-trace --stats --output-format csv \

@@ -863,12 +863,19 @@ def run_rank(args) -> int:
             # placement, object and steps; bytes to a discard sink, CRC32C of
             # every byte on the host (the Go library's reader,
             # /root/reference/main.go:133-146).  vs_baseline divides by it.
+            # The baseline gets the headline's submitter core too: its host
+            # CRC runs on the worker (gRPC: apart from the connection's reader,
+            # as the Go library's caller goroutine is apart from grpc-go's
+            # transport reader), so both designs get two physical cores.
+            base_cpus = sorted(set(placement.get("client", [])) | set(placement.get("aux", [])))
             for p in [protocol] + ([other] if other and other in hbm.available_protocols() else []):
                 key = "cpu_baseline" if p == protocol else f"cpu_baseline_{p}"
-                blocks[key] = (key, read_block({"protocol": p, "sink": "discard", "host_crc": True}, side_steps,
-                                               side_warm, f"{p} cpu baseline"),
+                over = {"protocol": p, "sink": "discard", "host_crc": True}
+                if base_cpus:
+                    over["cpus"] = base_cpus
+                blocks[key] = (key, read_block(over, side_steps, side_warm, f"{p} cpu baseline"),
                                {"protocol": p, "sink": "discard", "host_crc": True,
-                                "note": "reference semantics: io.Discard + host CRC32C"})
+                                "note": "reference semantics: io.Discard + host CRC32C; client + submitter cores"})
         if other and other in hbm.available_protocols() and want("compare"):
             blocks["compare"] = ("compare", read_block({"protocol": other}, side_steps, side_warm, f"{other} compare"),
                                  {"protocol": other})

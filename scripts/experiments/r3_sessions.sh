@@ -26,6 +26,11 @@ step() {  # step <name> <timeout> <cmd...>: a crash, abort or timeout ends the s
 }
 
 case "$S" in
+base2core)  # profiles/r3_twins/base2core: the reference-semantics baseline on the client + submitter cores
+  for k in 1 2 3; do
+    step "b_$k" 300 python3 bench.py --steps 20 --warmup 3 --blocks cpu_baseline,ceiling --json-out "$O/b_$k.json"
+  done
+  ;;
 spincubic)  # profiles/r3_refill/spin: submitter polls before sleeping (no futex wake per slot on the reader), cubic
   for k in 1 2 3 4; do
     for v in 0 100; do

@@ -26,6 +26,15 @@ step() {  # step <name> <timeout> <cmd...>: a crash, abort or timeout ends the s
 }
 
 case "$S" in
+ringsmall)  # profiles/r3_ring_thp/small: small headline rings (reuse distance) against the two-core baseline
+  for k in 1 2 3; do
+    for v in 8x2MiB 4x2MiB 3x2MiB 2x2MiB; do
+      n=${v%x*}; b=${v#*x}
+      step "r${v}_$k" 300 python3 bench.py --steps 20 --warmup 3 --slots $n --slot-bytes $b \
+        --blocks cpu_baseline,ceiling --json-out "$O/r${v}_$k.json"
+    done
+  done
+  ;;
 base2core)  # profiles/r3_twins/base2core: the reference-semantics baseline on the client + submitter cores
   for k in 1 2 3; do
     step "b_$k" 300 python3 bench.py --steps 20 --warmup 3 --blocks cpu_baseline,ceiling --json-out "$O/b_$k.json"

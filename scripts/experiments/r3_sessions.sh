@@ -26,6 +26,15 @@ step() {  # step <name> <timeout> <cmd...>: a crash, abort or timeout ends the s
 }
 
 case "$S" in
+ringsmall2)  # profiles/r3_ring_thp/small2: ring reuse distance against the two-core baseline, more reps
+  for k in 1 2 3 4; do
+    for v in 8x2MiB 2x2MiB 2x1MiB; do
+      n=${v%x*}; b=${v#*x}
+      step "r${v}_$k" 300 python3 bench.py --steps 20 --warmup 3 --slots $n --slot-bytes $b \
+        --blocks cpu_baseline,ceiling --json-out "$O/r${v}_$k.json"
+    done
+  done
+  ;;
 ringsmall)  # profiles/r3_ring_thp/small: small headline rings (reuse distance) against the two-core baseline
   for k in 1 2 3; do
     for v in 8x2MiB 4x2MiB 3x2MiB 2x2MiB; do

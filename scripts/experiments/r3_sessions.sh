@@ -26,6 +26,14 @@ step() {  # step <name> <timeout> <cmd...>: a crash, abort or timeout ends the s
 }
 
 case "$S" in
+ringalloc)  # profiles/r3_ring_thp/alloc: ring from THP + hipHostRegister vs hipHostMalloc, against the two-core baseline
+  for k in 1 2 3; do
+    for v in thp hip; do
+      step "a${v}_$k" 300 env GCSB_RING_ALLOC=$v python3 bench.py --steps 20 --warmup 3 \
+        --blocks cpu_baseline,ceiling --json-out "$O/a${v}_$k.json"
+    done
+  done
+  ;;
 ringsmall2)  # profiles/r3_ring_thp/small2: ring reuse distance against the two-core baseline, more reps
   for k in 1 2 3 4; do
     for v in 8x2MiB 2x2MiB 2x1MiB; do

@@ -26,6 +26,13 @@ step() {  # step <name> <timeout> <cmd...>: a crash, abort or timeout ends the s
 }
 
 case "$S" in
+long)  # profiles/r3_final/long: 100 timed reads per run (p99 is no longer the maximum) + a kernel/copy profile at HEAD
+  for k in 1 2 3; do
+    step "long_$k" 300 python3 bench.py --steps 100 --warmup 5 --blocks ceiling --json-out "$O/long_$k.json"
+  done
+  step rocprof 400 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$O/prof" -o bench -- \
+    python3 bench.py --steps 20 --warmup 3
+  ;;
 ringalloc)  # profiles/r3_ring_thp/alloc: ring from THP + hipHostRegister vs hipHostMalloc, against the two-core baseline
   for k in 1 2 3; do
     for v in thp hip; do

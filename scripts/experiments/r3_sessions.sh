@@ -26,6 +26,12 @@ step() {  # step <name> <timeout> <cmd...>: a crash, abort or timeout ends the s
 }
 
 case "$S" in
+rehearse)  # profiles/r3_rehearsal8/head: gloo rehearsals at 2, 4 and 8 ranks on one GPU with every round-3 default
+  for n in 2 4 8; do
+    step "rehearsal$n" 500 env GCSB_DIST_BACKEND=gloo python3 bench.py --gpus $n --object-size 64MiB --steps 5 \
+      --side-steps 3 --json-out "$O/rehearsal$n.json"
+  done
+  ;;
 long)  # profiles/r3_final/long: 100 timed reads per run (p99 is no longer the maximum) + a kernel/copy profile at HEAD
   for k in 1 2 3; do
     step "long_$k" 300 python3 bench.py --steps 100 --warmup 5 --blocks ceiling --json-out "$O/long_$k.json"

@@ -203,6 +203,9 @@ def build_parser() -> argparse.ArgumentParser:
                     help="cpu_baseline side blocks: the headline config with the reference's semantics (discard "
                          "sink, host CRC32C; /root/reference/main.go:133-146) on the same endpoint, placement and "
                          "steps, for the headline protocol and the other one; vs_baseline = value / it")
+    ap.add_argument("--baseline-bracket", action="store_true",
+                    help="also run the reference-semantics baseline before the headline (cpu_baseline_before), so "
+                         "the two baselines bracket it (A/B sessions on drifting hosts)")
     ap.add_argument("--ceiling", default="on", choices=["on", "off"],
                     help="ceiling side block: one loopback TCP stream (sendfile -> recv into a THP ring, no GPU, "
                          "no framing) and pinned -> HBM copies, in the headline's placement")
@@ -830,7 +833,23 @@ def run_rank(args) -> int:
             d["error"] = st["error"][:300]
         return d
 
+    def baseline_over() -> dict:
+        # The baseline gets the headline's submitter core too: its host CRC
+        # runs on the worker (gRPC: apart from the connection's reader, as
+        # the Go library's caller goroutine is apart from grpc-go's transport
+        # reader), so both designs get two physical cores.
+        over = {"protocol": protocol, "sink": "discard", "host_crc": True}
+        base_cpus = sorted(set(placement.get("client", [])) | set(placement.get("aux", [])))
+        if base_cpus:
+            over["cpus"] = base_cpus
+        return over
+
     # ---- headline --------------------------------------------------------
+    base_before = None
+    if args.workload == "read" and use_gpu and args.baseline_bracket and args.baseline == "on":
+        # the reference-semantics read once more BEFORE the headline, so the
+        # two baselines bracket it and a drifting host cancels (A/B sessions)
+        base_before = read_block(baseline_over(), side_steps, side_warm, f"{protocol} cpu baseline (before)")
     if args.workload == "read":
         head = read_block({}, args.steps, args.warmup, "headline")
         headline_model = (f"{protocol} ReadObject {args.object_size} object, "
@@ -863,22 +882,19 @@ def run_rank(args) -> int:
             # placement, object and steps; bytes to a discard sink, CRC32C of
             # every byte on the host (the Go library's reader,
             # /root/reference/main.go:133-146).  vs_baseline divides by it.
-            # The baseline gets the headline's submitter core too: its host
-            # CRC runs on the worker (gRPC: apart from the connection's reader,
-            # as the Go library's caller goroutine is apart from grpc-go's
-            # transport reader), so both designs get two physical cores.
-            base_cpus = sorted(set(placement.get("client", [])) | set(placement.get("aux", [])))
             for p in [protocol] + ([other] if other and other in hbm.available_protocols() else []):
                 key = "cpu_baseline" if p == protocol else f"cpu_baseline_{p}"
-                over = {"protocol": p, "sink": "discard", "host_crc": True}
-                if base_cpus:
-                    over["cpus"] = base_cpus
+                over = {**baseline_over(), "protocol": p}
                 blocks[key] = (key, read_block(over, side_steps, side_warm, f"{p} cpu baseline"),
                                {"protocol": p, "sink": "discard", "host_crc": True,
                                 "note": "reference semantics: io.Discard + host CRC32C; client + submitter cores"})
         if other and other in hbm.available_protocols() and want("compare"):
             blocks["compare"] = ("compare", read_block({"protocol": other}, side_steps, side_warm, f"{other} compare"),
                                  {"protocol": other})
+        if base_before is not None:
+            blocks["cpu_baseline_before"] = ("cpu_baseline_before", base_before,
+                                             {"protocol": protocol, "sink": "discard", "host_crc": True,
+                                              "note": "the cpu_baseline block, run before the headline"})
         if args.sliced_streams > 1 and args.slices == 1 and want("sliced"):
             # 8 receive + 8 send threads: a share-placed endpoint of its own
             srv_sl, sh = share_endpoint()

@@ -26,6 +26,12 @@ step() {  # step <name> <timeout> <cmd...>: a crash, abort or timeout ends the s
 }
 
 case "$S" in
+bracket)  # profiles/r3_twins/bracket: the two-core baseline before AND after the headline (drift cancels)
+  for k in 1 2 3 4 5; do
+    step "k_$k" 300 python3 bench.py --steps 20 --warmup 3 --baseline-bracket --blocks cpu_baseline,ceiling \
+      --json-out "$O/k_$k.json"
+  done
+  ;;
 rehearse)  # profiles/r3_rehearsal8/head: gloo rehearsals at 2, 4 and 8 ranks on one GPU with every round-3 default
   for n in 2 4 8; do
     step "rehearsal$n" 500 env GCSB_DIST_BACKEND=gloo python3 bench.py --gpus $n --object-size 64MiB --steps 5 \

@@ -451,6 +451,12 @@ def run_rank(args) -> int:
                                     "headers_s_per_gib": round(d["headers_ns"] / 1e9 / g, 4),
                                     "other_s_per_gib": round(d["other_ns"] / 1e9 / g, 4),
                                     "avg_data_frame_kib": round(d["data_bytes"] / max(1, d["data_frames"]) / 1024, 1)}
+            g1 = s1.get("gpu") or {}
+            if g1.get("slot_waits"):
+                # the receiving thread's time reusing ring slots (wait for the
+                # slot's hand-off + its event, harvest its CRC results)
+                cpu["slot_reuse"] = {"waits": g1["slot_waits"],
+                                     "s_per_gib": round(g1["slot_wait_s"] / max(float(s1["bytes"]) / (1 << 30), 1e-9), 4)}
             sv1 = srv.stats()
             if sv1.get("body_sends", 0) > sv0.get("body_sends", 0):
                 # the endpoint's sends of this block's bodies, by the kernel's

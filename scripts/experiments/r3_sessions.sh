@@ -26,6 +26,11 @@ step() {  # step <name> <timeout> <cmd...>: a crash, abort or timeout ends the s
 }
 
 case "$S" in
+slotreuse)  # profiles/r3_twins/slotreuse: the receiving thread's time reusing ring slots (event wait + harvest)
+  for k in 1 2 3; do
+    step "u_$k" 300 python3 bench.py --steps 20 --warmup 3 --blocks ceiling --json-out "$O/u_$k.json"
+  done
+  ;;
 bracket)  # profiles/r3_twins/bracket: the two-core baseline before AND after the headline (drift cancels)
   for k in 1 2 3 4 5; do
     step "k_$k" 300 python3 bench.py --steps 20 --warmup 3 --baseline-bracket --blocks cpu_baseline,ceiling \

@@ -114,7 +114,19 @@ class PinnedPool {
   // n bytes of page-locked memory whose pages sit on NUMA node `node` (the
   // GPU's, which its SDMA engines read / write and its rank's pinned threads
   // run on), -1 = the calling thread's node.  Recycled by (node, size).
-  static void* get(size_t n, int node) {
+  // wc: a read sink's ring, which the CPU only writes (the receive copy) and
+  // the copy engine reads; with GCSB_RING_WC=1 it is write-combined memory
+  // (hipHostMallocWriteCombined, not pooled): the copy's stores skip the CPU
+  // caches, so there is no read-for-ownership and nothing to write back
+  // before the DMA.  Never for upload staging, which the CPU reads.
+  static void* get(size_t n, int node, bool wc = false) {
+    if (wc && ring_wc()) {
+      void* p = nullptr;
+      hip_check(hipHostMalloc(&p, n, hipHostMallocWriteCombined | hipHostMallocNumaUser), "hipHostMalloc(wc ring)");
+      std::lock_guard<std::mutex> lk(mu());
+      wc_set()[p] = n;
+      return p;
+    }
     if (node < 0) node = current_numa_node();
     {
       std::lock_guard<std::mutex> lk(mu());
@@ -165,6 +177,10 @@ class PinnedPool {
     size_t reg_len = 0;
     {
       std::lock_guard<std::mutex> lk(mu());
+      if (wc_set().erase(p)) {
+        (void)hipHostFree(p);
+        return;
+      }
       auto it = registered().find(p);
       const int node = it != registered().end() ? it->second.second : malloced()[p];
       if (held() + n <= kMaxHeld) {
@@ -199,6 +215,17 @@ class PinnedPool {
   static std::mutex& mu() {
     static std::mutex m;
     return m;
+  }
+  static bool ring_wc() {
+    static const bool on = [] {
+      const char* e = std::getenv("GCSB_RING_WC");
+      return e && *e == '1';
+    }();
+    return on;
+  }
+  static std::map<void*, size_t>& wc_set() {  // write-combined sink rings (not pooled)
+    static std::map<void*, size_t> w;
+    return w;
   }
   static std::multimap<std::pair<int, size_t>, void*>& free_list() {
     static std::multimap<std::pair<int, size_t>, void*> f;
@@ -554,7 +581,7 @@ GpuSink::GpuSink(const GpuSinkConfig& cfg) : cfg_(cfg) {
   for (int i = 0; i < cfg_.slots; ++i) {
     Slot& s = slots_[i];
     // on the GPU's NUMA node (the rank's pinned receive thread runs there too)
-    s.host = static_cast<uint8_t*>(PinnedPool::get(cfg_.slot_bytes, device_numa_node(cfg_.device)));
+    s.host = static_cast<uint8_t*>(PinnedPool::get(cfg_.slot_bytes, device_numa_node(cfg_.device), /*wc=*/true));
     if (cfg_.landing == Landing::kRing)
       hip_check(hipMalloc(reinterpret_cast<void**>(&s.dev_ring), cfg_.slot_bytes), "hipMalloc(ring slot)");
     const unsigned evf = hipEventDisableTiming | (cfg_.blocking_sync ? hipEventBlockingSync : 0u);

@@ -26,6 +26,14 @@ step() {  # step <name> <timeout> <cmd...>: a crash, abort or timeout ends the s
 }
 
 case "$S" in
+ringwc)  # profiles/r3_ring_thp/wc: read-sink rings in write-combined memory (GCSB_RING_WC) vs THP cached
+  for k in 1 2 3; do
+    for v in 0 1; do
+      step "w${v}_$k" 300 env GCSB_RING_WC=$v python3 bench.py --steps 20 --warmup 3 \
+        --blocks cpu_baseline,list_read,ceiling --json-out "$O/w${v}_$k.json"
+    done
+  done
+  ;;
 slotreuse)  # profiles/r3_twins/slotreuse: the receiving thread's time reusing ring slots (event wait + harvest)
   for k in 1 2 3; do
     step "u_$k" 300 python3 bench.py --steps 20 --warmup 3 --blocks ceiling --json-out "$O/u_$k.json"

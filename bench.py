@@ -197,6 +197,9 @@ def build_parser() -> argparse.ArgumentParser:
                     help="config 3 side block: pinned ring per reader, SLOTSxSLOT_BYTES (1 MiB objects). 2 x 1 MiB "
                          "keeps the 8 readers' receive destinations at 16 MiB: gRPC 18.6-18.8k MiB/s at p50 "
                          "0.42 ms against 15.5-17.0k at 0.46-0.49 with 8 x 2 MiB (profiles/r3_mux_thp/listring)")
+    ap.add_argument("--list-ring-wc", default="on", choices=["on", "off"],
+                    help="config 3 side block: the readers' rings in write-combined pinned memory (p50 0.346-0.379 "
+                         "ms against 0.412-0.519 with cached THP rings, profiles/r3_ring_thp/wc)")
     ap.add_argument("--write-size", default="64MiB", help="config 5 object size")
     ap.add_argument("--write-chunk", default="16MiB", help="resumable upload chunk (HTTP) / message batch")
     ap.add_argument("--baseline", default="on", choices=["on", "off"],
@@ -742,6 +745,7 @@ def run_rank(args) -> int:
         over = {"protocol": proto, "endpoint": ep.url if ep is not None else "", "workers": workers,
                 "object_names": names or [f"c3_rank{rank}/file_0"], "cpus": sh["client"], "worker_id_offset": 0,
                 "rcvbuf": parse_size(args.list_rcvbuf), "ring_slots": int(lslots), "ring_slot_bytes": parse_size(lbytes),
+                "ring_wc": args.list_ring_wc == "on",
                 "reader_cpus": sh.get("reader_cpus")}
         # every rank runs the block (and its collectives) whatever happened here
         st = read_block(over, per_pass, per_pass * warmup_passes, f"{proto} list-read")

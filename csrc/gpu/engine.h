@@ -46,6 +46,13 @@ struct GpuSinkConfig {
   size_t slot_bytes = 8 << 20;
   int slots = 4;
   bool verify = true;  // run the CRC kernels
+  // Ring slots in write-combined pinned memory: the receive copy's stores
+  // skip the CPU caches (no read-for-ownership, nothing to write back before
+  // the copy engine reads them).  The CPU never reads a read sink's ring.
+  // Config-3 list-read (8 readers): p50 0.346-0.379 ms against 0.412-0.519
+  // with cached THP rings; the one-stream headline showed no gain
+  // (profiles/r3_ring_thp/wc).  Env GCSB_RING_WC=1 forces it for every sink.
+  bool ring_wc = false;
   Landing landing = Landing::kObject;
   // Slot hand-off (H2D copy + CRC launch + event) on one per-device
   // submitter thread instead of the transport thread.  A stream's receive is

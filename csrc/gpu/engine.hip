@@ -114,13 +114,22 @@ class PinnedPool {
   // n bytes of page-locked memory whose pages sit on NUMA node `node` (the
   // GPU's, which its SDMA engines read / write and its rank's pinned threads
   // run on), -1 = the calling thread's node.  Recycled by (node, size).
+  // GCSB_RING_WC=1: every read sink's ring write-combined (A/B)
+  static bool ring_wc() {
+    static const bool on = [] {
+      const char* e = std::getenv("GCSB_RING_WC");
+      return e && *e == '1';
+    }();
+    return on;
+  }
   // wc: a read sink's ring, which the CPU only writes (the receive copy) and
   // the copy engine reads; with GCSB_RING_WC=1 it is write-combined memory
   // (hipHostMallocWriteCombined, not pooled): the copy's stores skip the CPU
   // caches, so there is no read-for-ownership and nothing to write back
-  // before the DMA.  Never for upload staging, which the CPU reads.
+  // before the DMA (GpuSinkConfig::ring_wc).  Never for upload staging,
+  // which the CPU reads.
   static void* get(size_t n, int node, bool wc = false) {
-    if (wc && ring_wc()) {
+    if (wc) {
       void* p = nullptr;
       hip_check(hipHostMalloc(&p, n, hipHostMallocWriteCombined | hipHostMallocNumaUser), "hipHostMalloc(wc ring)");
       std::lock_guard<std::mutex> lk(mu());
@@ -215,13 +224,6 @@ class PinnedPool {
   static std::mutex& mu() {
     static std::mutex m;
     return m;
-  }
-  static bool ring_wc() {
-    static const bool on = [] {
-      const char* e = std::getenv("GCSB_RING_WC");
-      return e && *e == '1';
-    }();
-    return on;
   }
   static std::map<void*, size_t>& wc_set() {  // write-combined sink rings (not pooled)
     static std::map<void*, size_t> w;
@@ -581,7 +583,8 @@ GpuSink::GpuSink(const GpuSinkConfig& cfg) : cfg_(cfg) {
   for (int i = 0; i < cfg_.slots; ++i) {
     Slot& s = slots_[i];
     // on the GPU's NUMA node (the rank's pinned receive thread runs there too)
-    s.host = static_cast<uint8_t*>(PinnedPool::get(cfg_.slot_bytes, device_numa_node(cfg_.device), /*wc=*/true));
+    s.host = static_cast<uint8_t*>(PinnedPool::get(cfg_.slot_bytes, device_numa_node(cfg_.device),
+                                                   cfg_.ring_wc || PinnedPool::ring_wc()));
     if (cfg_.landing == Landing::kRing)
       hip_check(hipMalloc(reinterpret_cast<void**>(&s.dev_ring), cfg_.slot_bytes), "hipMalloc(ring slot)");
     const unsigned evf = hipEventDisableTiming | (cfg_.blocking_sync ? hipEventBlockingSync : 0u);

@@ -90,6 +90,7 @@ GpuSinkConfig gpu_from(const py::dict& d) {
   g.async_submit = get_or<bool>(d, "async_submit", g.async_submit);
   g.blocking_sync = get_or<bool>(d, "blocking_sync", g.blocking_sync);
   g.wait_poll_us = get_or<int>(d, "wait_poll_us", g.wait_poll_us);
+  g.ring_wc = get_or<bool>(d, "ring_wc", g.ring_wc);
   return g;
 }
 

@@ -26,6 +26,15 @@ step() {  # step <name> <timeout> <cmd...>: a crash, abort or timeout ends the s
 }
 
 case "$S" in
+wccheck)  # profiles/r3_ring_thp/wc: the write-combined list-read default, GPU sink tests + list-read runs
+  step pytest_sink 300 python3 -u -m pytest tests/test_gpu_sink.py -x -q --timeout 120 --timeout-method thread
+  for k in 1 2 3; do
+    for v in on off; do
+      step "l${v}_$k" 300 python3 bench.py --steps 20 --warmup 3 --blocks list_read --list-ring-wc $v \
+        --json-out "$O/l${v}_$k.json"
+    done
+  done
+  ;;
 ringwc)  # profiles/r3_ring_thp/wc: read-sink rings in write-combined memory (GCSB_RING_WC) vs THP cached
   for k in 1 2 3; do
     for v in 0 1; do

@@ -257,3 +257,28 @@ def test_parallel_composite_upload_from_hbm(native, server, gpu_available, proto
     c = native.Client({"protocol": proto, "endpoint": server.url})
     assert c.read_bytes(B, name) == native.object_bytes(name, 0, size)
     assert [o["name"] for o in c.list_all(B, "upload/")] == [name]
+
+
+def test_write_combined_ring_byte_exact(native, server, gpu_available):
+    """ring_wc (the config-3 list-read rings): write-combined pinned slots land
+    the same bytes and CRC checks as cached ones, over several reads that
+    reuse the sink, and corruption is still caught."""
+    import torch
+
+    size = (5 << 20) + 4099
+    server.add_synthetic(B, P, "", 0, 1, size)
+    for proto in _protocols(native):
+        c = native.Client({"protocol": proto, "endpoint": server.url})
+        t = torch.empty(size, dtype=torch.uint8, device="cuda:0")
+        sink = native.GpuSink({"device": 0, "ring_slot_bytes": 1 << 20, "ring_slots": 2, "ring_wc": True})
+        sink.set_external_destination(t.data_ptr(), t.numel())
+        for _ in range(3):
+            r = c.read_gpu(B, P + "0", sink)
+            assert r["verified"] and not r["crc_mismatch"] and r["bytes"] == size, r
+            bad, first = native.gpu_verify_pattern(0, t.data_ptr(), size, P + "0", 0)
+            assert bad == 0, (proto, first)
+    server.set_faults({"corrupt_at": (2 << 20) + 5, "corrupt_count": 1})
+    c = native.Client({"protocol": "grpc", "endpoint": server.url})
+    sink = native.GpuSink({"device": 0, "ring_slot_bytes": 1 << 20, "ring_slots": 2, "ring_wc": True})
+    r = c.read_gpu(B, P + "0", sink)
+    assert r["crc_mismatch"] and not r["verified"]

@@ -45,6 +45,83 @@ sys.path.insert(0, ROOT)
 METRIC = "p50/p99 read latency (ms) + MB/s per GPU; HTTP vs gRPC at 1/2/4/8 MI355X"
 
 
+# side blocks a multi-GPU run does by default (the rest with --blocks all)
+SCALE_BLOCKS = ("cpu_baseline", "compare", "write", "fanout")
+
+
+class _Report:
+    """Rank 0's output line.  The normal path prints ONE line at the end.
+    Once the headline and its baseline are measured, the line so far is
+    stashed: if a later side block hangs, the fatal paths -- the barrier
+    watchdog (parallel/dist.py on_fatal), the side-block deadline, SIGTERM
+    from the rank launcher -- print the stash before the process ends, with
+    a non-zero exit status."""
+
+    def __init__(self):
+        import threading
+
+        self._lock = threading.Lock()
+        self._line = None
+        self._printed = False
+        self._timer = None
+
+    def stash(self, line: str) -> None:
+        with self._lock:
+            self._line = line
+
+    def emit_stash(self, why: str = "") -> None:
+        with self._lock:
+            if self._line is None or self._printed:
+                return
+            self._printed = True
+            line = self._line
+        if why:
+            print(f"bench: {why}; printing the headline measured so far", file=sys.stderr, flush=True)
+        print(line, flush=True)
+
+    def final(self, line: str) -> None:
+        with self._lock:
+            if self._printed:  # a fatal path already printed the stash
+                return
+            self._printed = True
+        print(line, flush=True)
+
+    def arm(self, seconds: float) -> None:
+        """Side blocks must be done within `seconds` (0 = no limit)."""
+        import threading
+
+        if seconds <= 0 or self._timer is not None:
+            return
+
+        def fire():
+            self.emit_stash(f"side blocks still running after {seconds:.0f} s")
+            sys.stderr.flush()
+            os._exit(3)
+        self._timer = threading.Timer(seconds, fire)
+        self._timer.daemon = True
+        self._timer.start()
+
+    def disarm(self) -> None:
+        if self._timer is not None:
+            self._timer.cancel()
+
+
+report = _Report()
+
+
+def maybe_hang(block: str, rank: int) -> None:
+    """Fault injection for the resilience tests: GCSB_TEST_HANG=<block>:<rank>
+    makes that rank hang at the start of that side block."""
+    spec = os.environ.get("GCSB_TEST_HANG", "")
+    if not spec:
+        return
+    b, _, r = spec.partition(":")
+    if b == block and str(rank) == (r or "0"):
+        print(f"bench: GCSB_TEST_HANG: rank {rank} hangs in side block {block}", file=sys.stderr, flush=True)
+        while True:
+            time.sleep(0.2)
+
+
 def parse_size(s: str) -> int:
     s = s.strip()
     mult = {"k": 1 << 10, "kib": 1 << 10, "m": 1 << 20, "mib": 1 << 20, "g": 1 << 30, "gib": 1 << 30}
@@ -222,6 +299,12 @@ def build_parser() -> argparse.ArgumentParser:
                          "4.5-5.0 ms spread over the quota's cores (profiles/r3_mux_thp/refplace). HTTP keeps "
                          "share_quota: its 48 receiving workers need the cores")
     ap.add_argument("--ref-object-size", default="1MiB", help="ref_default_*: object size")
+    ap.add_argument("--ref100-reads", type=int, default=3,
+                    help="ref_default_100m_* blocks: the reference's real operating point, 48 workers x 100 MiB "
+                         "objects (princer_100M_files), HTTP vs gRPC pool 1, discard + host CRC vs HBM + GPU CRC; "
+                         "timed reads per worker (0 = off)")
+    ap.add_argument("--ref-gpu-ring", default="2x2MiB",
+                    help="ref_default_100m_*_gpu: pinned ring per worker, SLOTSxSLOT_BYTES")
     ap.add_argument("--write-placement", default="pair", choices=["share", "pair"],
                     help="config-5 upload block: pair (uploader on one quiet core, endpoint receive + CRC on two "
                          "more of the same L3 domain; 18.0-21.6k MiB/s in 6 runs) or share (uploader and endpoint "
@@ -234,7 +317,11 @@ def build_parser() -> argparse.ArgumentParser:
                          "reader thread a physical core the workers and endpoint do not use (affinity.isolate_reader)")
     ap.add_argument("--blocks", default="",
                     help="comma list of side blocks to run (A/B sessions): cpu_baseline, compare, sliced, ceiling, "
-                         "ref_default, c1_http_cpu, list_read, write, write_composite, fanout; empty = all")
+                         "ref_default, c1_http_cpu, list_read, write, write_composite, fanout; 'all' = every block; empty = "
+                         "all at N = 1, cpu_baseline,compare,write,fanout at N > 1")
+    ap.add_argument("--side-deadline", type=float, default=300.0,
+                    help="seconds the side blocks after the headline + cpu_baseline may take before rank 0 prints "
+                         "the headline line measured so far and exits 3 (0 = no limit)")
     ap.add_argument("--json-out", default="")
     return ap
 
@@ -266,6 +353,11 @@ def launch_ranks(n: int, argv: list[str]) -> int:
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
     rc = 0
     live = set(range(n))
+
+    def _forward(signum, frame):  # the driver's time limit: let every rank print what it has
+        for q in live:
+            procs[q].send_signal(signal.SIGTERM)
+    signal.signal(signal.SIGTERM, _forward)
     try:
         while live:
             for r in sorted(live):
@@ -299,7 +391,7 @@ def run_rank(args) -> int:
     from custom_go_client_benchmark_amd.ops import hbm
     from custom_go_client_benchmark_amd.parallel import affinity
     from custom_go_client_benchmark_amd.parallel import dist as gdist
-    from custom_go_client_benchmark_amd.utils import cpuacct
+    from custom_go_client_benchmark_amd.utils import cpuacct, sysdiag
 
     n = pkg._native
     rank, world, local_rank = gdist.env_rank()
@@ -318,6 +410,17 @@ def run_rank(args) -> int:
             return 2
     # process group even at world 1: RCCL init + barriers + reductions run in every GPU bench
     ctx = gdist.init(local_rank=local_rank, world=world, rank=rank, always_pg=use_gpu)
+    if rank == 0:
+        # a peer that never reaches a barrier ends this rank through the
+        # watchdog, and the launcher ends a hung rank with SIGTERM: either
+        # way the stashed headline line is printed first
+        gdist.on_fatal(lambda: report.emit_stash("a barrier timed out"))
+
+        def _term(signum, frame):
+            report.emit_stash("terminated")
+            sys.stdout.flush()
+            os._exit(128 + signum)
+        signal.signal(signal.SIGTERM, _term)
     protocol = args.protocol
     if protocol == "auto":
         protocol = "grpc" if "grpc" in hbm.available_protocols() else "http"
@@ -391,7 +494,7 @@ def run_rank(args) -> int:
             return False, f"only {s['verified']} of {reads} reads had their CRC32C verified"
         return True, ""
 
-    def read_block(overrides: dict, steps: int, warmup: int, what: str) -> dict:
+    def read_block(overrides: dict, steps: int, warmup: int, what: str, endpoint=None) -> dict:
         """warm-up reads, then `steps` timed reads of a config variant between
         two barriers.  Every rank makes every collective call whatever happens
         locally, so one rank's failure cannot strand the others in a barrier."""
@@ -417,11 +520,14 @@ def run_rank(args) -> int:
         rd0 = n.recv_diag()
         h2s0 = n.h2_reader_stats()
         pr0 = n.pipe_relay_stats()
-        sv0 = srv.stats()
+        ep_stats = (endpoint or srv).stats
+        sv0 = ep_stats()
         if use_gpu:
             n.reset_slow_hip_calls()
+        win = None
         if not err:
             c0, th0 = cpu_snapshot(), cpuacct.thread_cpu()
+            win = sysdiag.Window()
             t1 = time.perf_counter()
             r1.start()
             r1.wait()
@@ -435,6 +541,11 @@ def run_rank(args) -> int:
             if not ok:
                 err = why
             cpu = cpu_delta(c0, cpu_snapshot(), float(s1["bytes"]), e1)
+            # what else ran on the block's CPUs: run-queue delay of our
+            # threads, interrupts and softirqs there (utils/sysdiag.py)
+            diag_cpus = sorted(set(overrides.get("cpus") or cfg.get("cpus") or [])
+                               | set(placement.get("server") or []) | set(placement.get("aux") or []))
+            cpu["host"] = win.report(diag_cpus or None, max(1, int(s1["reads"])))
             th1 = cpuacct.thread_cpu()
             cpu["cpu_s_per_gib_by_thread"] = cpuacct.per_gib(cpuacct.delta_by_group(th0, th1), float(s1["bytes"]))
             names = cpuacct.delta_by_name(th0, th1)
@@ -460,7 +571,17 @@ def run_rank(args) -> int:
                 # slot's hand-off + its event, harvest its CRC results)
                 cpu["slot_reuse"] = {"waits": g1["slot_waits"],
                                      "s_per_gib": round(g1["slot_wait_s"] / max(float(s1["bytes"]) / (1 << 30), 1e-9), 4)}
-            sv1 = srv.stats()
+            sv1 = ep_stats()
+            if sv1.get("h2_data_frames", 0) > sv0.get("h2_data_frames", 0):
+                # the endpoint's HTTP/2 fairness: how long stream handlers
+                # queued per DATA frame, and request -> response HEADERS
+                fr = sv1["h2_data_frames"] - sv0["h2_data_frames"]
+                rs = max(1, sv1["h2_responses"] - sv0["h2_responses"])
+                cpu["endpoint_h2"] = {"frames": fr,
+                                      "queue_wait_avg_us": round((sv1["h2_queue_wait_us"] - sv0["h2_queue_wait_us"]) / fr, 1),
+                                      "queue_wait_max_us": sv1["h2_queue_wait_max_us"],
+                                      "ttfb_avg_us": round((sv1["h2_ttfb_us"] - sv0["h2_ttfb_us"]) / rs, 1),
+                                      "ttfb_max_us": sv1["h2_ttfb_max_us"]}
             if sv1.get("body_sends", 0) > sv0.get("body_sends", 0):
                 # the endpoint's sends of this block's bodies, by the kernel's
                 # send chronographs: busy, held by the client's receive window
@@ -798,33 +919,43 @@ def run_rank(args) -> int:
             out["error"] = err[:300]
         return out
 
-    def ref_default_block(proto: str) -> dict:
+    def ref_default_block(proto: str, osz: int = 0, reads: int = 0, sink: str = "discard",
+                          warmup: int = 2) -> dict:
         """The reference's only experiment (execute_pb.sh:4,8; main.go:36,
         30,111): -worker 48 readers, each re-reading its own object
         file_<id>, over gRPC with ONE connection (pool 1) or HTTP/1.1
-        keep-alive, io.Discard sink with the library's host CRC32C.  Objects
-        are --ref-object-size; a rank's 48 workers read file_<rank*48 + w>.
-        Threads on the rank's GPU-local share of L3 domains trimmed to its
-        CPU-quota budget (affinity share_quota)."""
+        keep-alive.  sink "discard": io.Discard with the library's host
+        CRC32C (reference semantics); "gpu": every read lands in HBM through
+        a small per-worker pinned ring (--ref-gpu-ring) with CRC32C on the
+        GPU.  Objects are --ref-object-size (ref_default_*) or 100 MiB
+        (ref_default_100m_*, the reference's princer_100M_files,
+        main.go:52); a rank's 48 workers read file_<rank*48 + w>.  Threads on
+        the rank's GPU-local share of L3 domains trimmed to its CPU-quota
+        budget (affinity share_quota) for HTTP, one L3 domain for gRPC."""
         workers = args.ref_workers
-        osz = parse_size(args.ref_object_size)
+        osz = osz or parse_size(args.ref_object_size)
+        reads = reads or args.ref_reads
         mode = args.ref_grpc_placement if proto != "http" else "share_quota"
         sh = affinity.plan(gpu, mode, slot) if use_gpu else {"client": [], "server": []}
         if use_gpu and proto != "http" and args.mux_reader == "isolate":
             sh = affinity.isolate_reader(sh)
         ep = None
         err = ""
+        prefix = "ref_default/file_" if osz == parse_size(args.ref_object_size) else f"ref_default_{osz >> 20}m/file_"
         try:
             ep = n.Server({"port": 0, "md5": False, "cpus": sh["server"], "retain_uploads": False})
             ep.start()
-            ep.add_synthetic(bucket, "ref_default/file_", "", rank * workers, workers, osz)
+            ep.add_synthetic(bucket, prefix, "", rank * workers, workers, osz)
         except Exception as e:  # noqa: BLE001
             err = f"{type(e).__name__}: {e}"
         over = {"protocol": proto, "endpoint": ep.url if ep is not None else "", "workers": workers,
-                "object_prefix": "ref_default/file_", "worker_id_offset": rank * workers, "sink": "discard",
-                "host_crc": True, "cpus": sh["client"], "rcvbuf": 0, "grpc_conn_pool_size": 1,
+                "object_prefix": prefix, "worker_id_offset": rank * workers, "sink": sink,
+                "host_crc": sink == "discard", "cpus": sh["client"], "rcvbuf": 0, "grpc_conn_pool_size": 1,
                 "reader_cpus": sh.get("reader_cpus")}
-        st = read_block(over, args.ref_reads, 2, f"{proto} reference default")
+        if sink == "gpu":
+            rs, _, rb = args.ref_gpu_ring.partition("x")
+            over.update(ring_slots=int(rs), ring_slot_bytes=parse_size(rb), landing="object")
+        st = read_block(over, reads, warmup, f"{proto} reference default {osz >> 20} MiB {sink}", endpoint=ep)
         if err:
             st["error"] = err
             st["ok_min"] = 0.0
@@ -878,13 +1009,195 @@ def run_rank(args) -> int:
     distinct = sorted({int(d[0]) for d in devs if d[0] >= 0})
     n_gpus = len(distinct) if use_gpu else world
 
+    def build_line() -> dict | None:
+        """Rank 0's bench line from the headline and the side blocks run so
+        far (None if the headline failed)."""
+        if head["ok_min"] < 1.0:
+            return None
+        value = mib_s(head)
+        tmax = head["elapsed_max"]
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "MiB/s",
+            "n_gpus": n_gpus,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(tmax / args.steps * 1000.0, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "uint8",
+            "data": "synthetic",
+            "config": {
+                "model": headline_model,
+                "global_batch": world * args.workers,
+                "seq_len": size if args.workload == "read" else parse_size(args.write_size),
+                "parallelism": f"dp{world}",
+                "workload": args.workload,
+                "protocol": protocol,
+                "object_bytes": size if args.workload == "read" else parse_size(args.write_size),
+                "readers_per_gpu": args.workers,
+                "sink": args.sink,
+                "ring": f"{args.slots}x{args.slot_bytes}",
+                "streams_per_read": args.slices if args.workload == "read" else 1,
+                "event_wait": args.event_wait,
+                "async_submit": bool(args.async_submit),
+                "rcvbuf": parse_size(args.rcvbuf),
+                "sysctl": tcp_sysctls(),
+            },
+            "ranks": world,
+            "control_plane": ctx.backend + (" (RCCL init failed: fallback)" if ctx.fallback else ""),
+            "devices": distinct if use_gpu else "none (cpu rehearsal)",
+            "per_gpu_mib_s": round(value / max(1, n_gpus), 2),
+            "p50_ms": round(head["p50_max"], 3),
+            "p99_ms": round(head["p99_max"], 3),
+            "per_rank_mib_s": [round(b / max(e, 1e-12) / (1 << 20), 1)
+                               for b, e in zip(head["nbytes_per_rank"], head["elapsed_per_rank"])],
+            "endpoint": "loopback synthetic GCS (one per rank)",
+            # how the endpoint sends object bodies (profiles/r3_thp_send)
+            "endpoint_send": ("sendfile (memfd page cache)" if os.environ.get("GCSB_SRV_SEND") == "sendfile"
+                              else "vmsplice (THP copy of the pattern)"),
+            # the endpoint sockets' congestion control (GCSB_SRV_CC; the
+            # host default is in config.sysctl, profiles/r3_twins/cc)
+            "endpoint_congestion_control": os.environ.get("GCSB_SRV_CC") or "cubic",
+            "affinity": aff,
+            "placement": {k: placement.get(k) for k in ("client", "server", "aux", "picked_by", "busy")
+                          if placement.get(k) is not None},
+        }
+        def by_node(counts):
+            d = {str(i): c for i, c in enumerate(counts[:-1]) if c}
+            if counts and counts[-1]:
+                d["absent"] = counts[-1]
+            return d
+        # host-memory placement: the object's page cache (read by the send
+        # path) and the pinned ring (written by the receive thread, read
+        # by SDMA) should sit on the GPU's NUMA node
+        out["numa"] = {"gpu_node": placement.get("numa_node"),
+                       "object_pages": by_node(n.pattern_memfd_numa())}
+        if head.get("ring_numa"):
+            slots = head["ring_numa"]
+            total = [sum(c[i] for c in slots) for i in range(len(slots[0]))]
+            out["numa"]["ring_pages"] = by_node(total)
+            # per slot: the node holding most of its pages (-1 = not resident)
+            out["numa"]["ring_slot_nodes"] = [max(range(len(c) - 1), key=lambda i: c[i]) if sum(c[:-1]) else -1
+                                              for c in slots]
+        if head.get("ring_thp", -1.0) >= 0:
+            # share of the pinned ring on transparent huge pages (the receive copy's TLB reach)
+            out["numa"]["ring_thp_fraction"] = round(head["ring_thp"], 3)
+        if args.workload == "write":
+            out["rank0_slowest"] = head.get("slowest", [])
+            out["cpu_s_per_gib_by_thread"] = head.get("cpu_s_per_gib_by_thread", {})
+        if args.workload == "read":
+            # where a read's time goes: request -> first byte (TTFB), -> last
+            # byte in host memory (host_landed), -> last byte + CRC in HBM (p50)
+            out["ttfb_p50_ms"] = round(head["ttfb_p50_max"], 3)
+            out["host_landed_p50_ms"] = round(head["host_p50_max"], 3)
+            out["verified_reads"] = int(head["verified_sum"])
+            out["rank0_cpu"] = head["cpu"]
+            out["rank0_slowest"] = head.get("slowest", [])
+            if head.get("slow_hip"):
+                out["slow_hip_calls"] = head["slow_hip"]
+            if head["cpu"]:
+                gib_s = value / max(1, world) / 1024.0
+                out["cpus_needed_per_gpu"] = round(head["cpu"]["process_cpu_s_per_gib"] * gib_s, 2)
+        base = blocks.get("cpu_baseline")
+        if base is not None and base[1]["ok_min"] >= 1.0 and mib_s(base[1]) > 0:
+            out["vs_baseline"] = round(value / mib_s(base[1]), 3)
+            out["baseline"] = {"what": "cpu_baseline block: same config, reference semantics (discard sink + "
+                                       "host CRC32C), same run", "mib_s": round(mib_s(base[1]), 2),
+                               "p50_ms": round(base[1]["p50_max"], 3),
+                               "p50_ratio": round(base[1]["p50_max"] / max(head["p50_max"], 1e-9), 3)}
+        for key, (_, st, extra) in blocks.items():
+            if extra is None:  # already a JSON block (ceiling)
+                out[key] = st
+                continue
+            b = block_json(st, **{k: v for k, v in extra.items() if v is not None})
+            if key.startswith(("ref_default_", "list_read_", "compare", "cpu_baseline")) and st.get("cpu"):
+                # where the CPU goes: many streams on one connection (gRPC
+                # pool 1), or the headline's twins (one stream each)
+                b["cpu_s_per_gib_by_thread"] = st["cpu"].get("cpu_s_per_gib_by_name", {})
+                b["cpus_busy"] = st["cpu"].get("cpus_busy")
+                if st["cpu"].get("h2_reader"):
+                    b["h2_reader"] = st["cpu"]["h2_reader"]
+                if st["cpu"].get("recv_avg_kib") is not None:
+                    b["recv_avg_kib"] = st["cpu"]["recv_avg_kib"]
+                if st["cpu"].get("recv_queue"):
+                    b["recv_queue"] = st["cpu"]["recv_queue"]
+                if st["cpu"].get("pipe_relay"):
+                    b["pipe_relay"] = st["cpu"]["pipe_relay"]
+                if st["cpu"].get("endpoint_tcp"):
+                    b["endpoint_tcp"] = st["cpu"]["endpoint_tcp"]
+                if st["cpu"].get("endpoint_h2"):
+                    b["endpoint_h2"] = st["cpu"]["endpoint_h2"]
+                if key.startswith(("compare", "cpu_baseline")) and st["cpu"].get("host"):
+                    b["host"] = st["cpu"]["host"]
+            if key.startswith("ref_default_100m_") and key.endswith("_gpu"):
+                # the HBM landing's own bound: pinned -> HBM copy rate
+                # (ceiling block), against min(that, the discard twin's rate)
+                ceil = out.get("ceiling") or {}
+                twin = out.get(key[:-len("_gpu")] + "_discard")
+                if ceil.get("h2d_gbps"):
+                    b["h2d_bound_mib_s"] = round(ceil["h2d_gbps"] * 1e9 / (1 << 20), 1)
+                    bound = min([b["h2d_bound_mib_s"]] + ([twin["mib_s"]] if twin and twin.get("ok") else []))
+                    b["frac_of_bound"] = round(b["mib_s"] / max(bound, 1e-9), 3)
+            if key.startswith("ref_default_"):
+                b["first_read_p50_ms"] = round(st["first_p50_max"], 3)
+                b["steady_p99_ms"] = round(st["steady_p99_max"], 3)
+                if st.get("cpu", {}).get("cgroup_nr_throttled") is not None:
+                    b["cgroup_nr_throttled"] = st["cpu"]["cgroup_nr_throttled"]
+            if key == "fanout":
+                # mib_s: whole objects landed in every GPU's HBM, job-wide
+                b["per_gpu_mib_s"] = round(b["mib_s"] / max(1, world), 2)
+                b["crc_verified_ranks"] = int(st["crc_ok_sum"])
+            if st.get("slowest"):
+                b["rank0_slowest"] = st["slowest"]
+            if st.get("slow_hip", {}).get("slow"):
+                b["slow_hip_calls"] = st["slow_hip"]
+            if st.get("cpu_s_per_gib_by_thread"):
+                b["cpu_s_per_gib_by_thread"] = st["cpu_s_per_gib_by_thread"]
+            if key.startswith("list_read_"):
+                b["list_ms"] = round(st["list_ms_max"], 3)
+            if key == "sliced":
+                b["host_landed_p50_ms"] = round(st["host_p50_max"], 3)
+                b["slice_skew_ms"] = round(st["skew_max"], 3)
+                if st.get("cpu"):
+                    b["process_cpu_s_per_gib"] = st["cpu"]["process_cpu_s_per_gib"]
+                    b["cpus_busy"] = st["cpu"].get("cpus_busy")
+                    if "cgroup_nr_throttled" in st["cpu"]:
+                        b["cgroup_nr_throttled"] = st["cpu"]["cgroup_nr_throttled"]
+            out[key] = b
+        return out
+
+    def stash_headline() -> None:
+        """The headline line, complete but for the later side blocks, kept
+        for the fatal paths: a side block that hangs (barrier watchdog,
+        side-block deadline, SIGTERM from the launcher) prints it before the
+        process ends, so a measured headline is never lost."""
+        if rank == 0:
+            out = build_line()
+            if out is not None:
+                out["partial"] = "side blocks after cpu_baseline did not finish"
+                report.stash(json.dumps(out))
+        report.arm(args.side_deadline)
+
     # ---- side blocks (after the timed region) ----------------------------
     other = {"grpc": "http", "http": "grpc"}.get(protocol)
     blocks = {}
     only = {b.strip() for b in args.blocks.split(",") if b.strip()}
+    if not only and world > 1:
+        # N > 1: the blocks the scaling run needs; the rest only when asked
+        # for (--blocks all or a list), so the first 8-GPU run does not hinge
+        # on the least-tested blocks
+        only = set(SCALE_BLOCKS)
+    if "all" in only:
+        only = set()
 
     def want(name: str) -> bool:
-        return not only or name in only
+        ok = not only or name in only
+        if ok:
+            maybe_hang(name, rank)
+        return ok
     if side_steps > 0 and args.workload == "read":
         if use_gpu and args.baseline == "on" and want("cpu_baseline"):
             # right after the headline (the boxes drift over a run): the
@@ -898,6 +1211,7 @@ def run_rank(args) -> int:
                 blocks[key] = (key, read_block(over, side_steps, side_warm, f"{p} cpu baseline"),
                                {"protocol": p, "sink": "discard", "host_crc": True,
                                 "note": "reference semantics: io.Discard + host CRC32C; client + submitter cores"})
+        stash_headline()
         if other and other in hbm.available_protocols() and want("compare"):
             blocks["compare"] = ("compare", read_block({"protocol": other}, side_steps, side_warm, f"{other} compare"),
                                  {"protocol": other})
@@ -925,6 +1239,20 @@ def run_rank(args) -> int:
                                                "reads_per_worker": args.ref_reads, "sink": "discard",
                                                "grpc_conn_pool_size": 1 if p == "grpc" else None,
                                                "note": "reference default experiment (execute_pb.sh)"})
+        if args.ref_workers > 0 and args.ref100_reads > 0 and want("ref_default_100m"):
+            # the reference's real operating point: 48 workers x 100 MiB
+            # (princer_100M_files, main.go:36,52), both transports, into the
+            # discard sink (reference semantics) and into HBM; the GPU
+            # blocks are bounded by the pinned -> HBM copy rate (h2d_gbps)
+            for p in ["http"] + ([x for x in ("grpc",) if x in hbm.available_protocols()]):
+                for sk in ["discard"] + (["gpu"] if use_gpu else []):
+                    key = f"ref_default_100m_{p}_{sk}"
+                    blocks[key] = (key, ref_default_block(p, 100 << 20, args.ref100_reads, sk, warmup=1),
+                                   {"protocol": p, "workers": args.ref_workers, "object_bytes": 100 << 20,
+                                    "reads_per_worker": args.ref100_reads, "sink": sk,
+                                    "grpc_conn_pool_size": 1 if p == "grpc" else None,
+                                    "ring": args.ref_gpu_ring if sk == "gpu" else None,
+                                    "note": "reference default experiment at its object size (princer_100M_files)"})
         if "http" in hbm.available_protocols() and want("c1_http_cpu"):
             # config 1: one 1 MiB object over the HTTP JSON API, CPU only
             # (discard sink, host CRC32C as the Go library), one reader
@@ -958,156 +1286,18 @@ def run_rank(args) -> int:
                                  else f"{ctx.backend} all_gather via host",
                                  "note": "extension: read once per node, fan out over xGMI"})
     # (a write headline runs no side blocks)
+    report.disarm()
     srv.stop()
 
     rc = 0
     if rank == 0:
-        if head["ok_min"] < 1.0:
+        out = build_line()
+        if out is None:
             print(f"benchmark failed: {head['error'] or 'a rank failed'}", file=sys.stderr)
             rc = 1
         else:
-            value = mib_s(head)
-            tmax = head["elapsed_max"]
-            out = {
-                "metric": METRIC,
-                "value": round(value, 2),
-                "unit": "MiB/s",
-                "n_gpus": n_gpus,
-                "steps": args.steps,
-                "warmup": args.warmup,
-                "ms_per_step": round(tmax / args.steps * 1000.0, 3),
-                "higher_is_better": True,
-                "scaling": "weak",
-                "vs_baseline": None,
-                "dtype": "uint8",
-                "data": "synthetic",
-                "config": {
-                    "model": headline_model,
-                    "global_batch": world * args.workers,
-                    "seq_len": size if args.workload == "read" else parse_size(args.write_size),
-                    "parallelism": f"dp{world}",
-                    "workload": args.workload,
-                    "protocol": protocol,
-                    "object_bytes": size if args.workload == "read" else parse_size(args.write_size),
-                    "readers_per_gpu": args.workers,
-                    "sink": args.sink,
-                    "ring": f"{args.slots}x{args.slot_bytes}",
-                    "streams_per_read": args.slices if args.workload == "read" else 1,
-                    "event_wait": args.event_wait,
-                    "async_submit": bool(args.async_submit),
-                    "rcvbuf": parse_size(args.rcvbuf),
-                    "sysctl": tcp_sysctls(),
-                },
-                "ranks": world,
-                "control_plane": ctx.backend + (" (RCCL init failed: fallback)" if ctx.fallback else ""),
-                "devices": distinct if use_gpu else "none (cpu rehearsal)",
-                "per_gpu_mib_s": round(value / max(1, n_gpus), 2),
-                "p50_ms": round(head["p50_max"], 3),
-                "p99_ms": round(head["p99_max"], 3),
-                "per_rank_mib_s": [round(b / max(e, 1e-12) / (1 << 20), 1)
-                                   for b, e in zip(head["nbytes_per_rank"], head["elapsed_per_rank"])],
-                "endpoint": "loopback synthetic GCS (one per rank)",
-                # how the endpoint sends object bodies (profiles/r3_thp_send)
-                "endpoint_send": ("sendfile (memfd page cache)" if os.environ.get("GCSB_SRV_SEND") == "sendfile"
-                                  else "vmsplice (THP copy of the pattern)"),
-                # the endpoint sockets' congestion control (GCSB_SRV_CC; the
-                # host default is in config.sysctl, profiles/r3_twins/cc)
-                "endpoint_congestion_control": os.environ.get("GCSB_SRV_CC") or "cubic",
-                "affinity": aff,
-                "placement": {k: placement.get(k) for k in ("client", "server", "aux", "picked_by", "busy")
-                              if placement.get(k) is not None},
-            }
-            def by_node(counts):
-                d = {str(i): c for i, c in enumerate(counts[:-1]) if c}
-                if counts and counts[-1]:
-                    d["absent"] = counts[-1]
-                return d
-            # host-memory placement: the object's page cache (read by the send
-            # path) and the pinned ring (written by the receive thread, read
-            # by SDMA) should sit on the GPU's NUMA node
-            out["numa"] = {"gpu_node": placement.get("numa_node"),
-                           "object_pages": by_node(n.pattern_memfd_numa())}
-            if head.get("ring_numa"):
-                slots = head["ring_numa"]
-                total = [sum(c[i] for c in slots) for i in range(len(slots[0]))]
-                out["numa"]["ring_pages"] = by_node(total)
-                # per slot: the node holding most of its pages (-1 = not resident)
-                out["numa"]["ring_slot_nodes"] = [max(range(len(c) - 1), key=lambda i: c[i]) if sum(c[:-1]) else -1
-                                                  for c in slots]
-            if head.get("ring_thp", -1.0) >= 0:
-                # share of the pinned ring on transparent huge pages (the receive copy's TLB reach)
-                out["numa"]["ring_thp_fraction"] = round(head["ring_thp"], 3)
-            if args.workload == "write":
-                out["rank0_slowest"] = head.get("slowest", [])
-                out["cpu_s_per_gib_by_thread"] = head.get("cpu_s_per_gib_by_thread", {})
-            if args.workload == "read":
-                # where a read's time goes: request -> first byte (TTFB), -> last
-                # byte in host memory (host_landed), -> last byte + CRC in HBM (p50)
-                out["ttfb_p50_ms"] = round(head["ttfb_p50_max"], 3)
-                out["host_landed_p50_ms"] = round(head["host_p50_max"], 3)
-                out["verified_reads"] = int(head["verified_sum"])
-                out["rank0_cpu"] = head["cpu"]
-                out["rank0_slowest"] = head.get("slowest", [])
-                if head.get("slow_hip"):
-                    out["slow_hip_calls"] = head["slow_hip"]
-                if head["cpu"]:
-                    gib_s = value / max(1, world) / 1024.0
-                    out["cpus_needed_per_gpu"] = round(head["cpu"]["process_cpu_s_per_gib"] * gib_s, 2)
-            base = blocks.get("cpu_baseline")
-            if base is not None and base[1]["ok_min"] >= 1.0 and mib_s(base[1]) > 0:
-                out["vs_baseline"] = round(value / mib_s(base[1]), 3)
-                out["baseline"] = {"what": "cpu_baseline block: same config, reference semantics (discard sink + "
-                                           "host CRC32C), same run", "mib_s": round(mib_s(base[1]), 2),
-                                   "p50_ms": round(base[1]["p50_max"], 3),
-                                   "p50_ratio": round(base[1]["p50_max"] / max(head["p50_max"], 1e-9), 3)}
-            for key, (_, st, extra) in blocks.items():
-                if extra is None:  # already a JSON block (ceiling)
-                    out[key] = st
-                    continue
-                b = block_json(st, **{k: v for k, v in extra.items() if v is not None})
-                if key.startswith(("ref_default_", "list_read_", "compare", "cpu_baseline")) and st.get("cpu"):
-                    # where the CPU goes: many streams on one connection (gRPC
-                    # pool 1), or the headline's twins (one stream each)
-                    b["cpu_s_per_gib_by_thread"] = st["cpu"].get("cpu_s_per_gib_by_name", {})
-                    b["cpus_busy"] = st["cpu"].get("cpus_busy")
-                    if st["cpu"].get("h2_reader"):
-                        b["h2_reader"] = st["cpu"]["h2_reader"]
-                    if st["cpu"].get("recv_avg_kib") is not None:
-                        b["recv_avg_kib"] = st["cpu"]["recv_avg_kib"]
-                    if st["cpu"].get("recv_queue"):
-                        b["recv_queue"] = st["cpu"]["recv_queue"]
-                    if st["cpu"].get("pipe_relay"):
-                        b["pipe_relay"] = st["cpu"]["pipe_relay"]
-                    if st["cpu"].get("endpoint_tcp"):
-                        b["endpoint_tcp"] = st["cpu"]["endpoint_tcp"]
-                if key.startswith("ref_default_"):
-                    b["first_read_p50_ms"] = round(st["first_p50_max"], 3)
-                    b["steady_p99_ms"] = round(st["steady_p99_max"], 3)
-                    if st.get("cpu", {}).get("cgroup_nr_throttled") is not None:
-                        b["cgroup_nr_throttled"] = st["cpu"]["cgroup_nr_throttled"]
-                if key == "fanout":
-                    # mib_s: whole objects landed in every GPU's HBM, job-wide
-                    b["per_gpu_mib_s"] = round(b["mib_s"] / max(1, world), 2)
-                    b["crc_verified_ranks"] = int(st["crc_ok_sum"])
-                if st.get("slowest"):
-                    b["rank0_slowest"] = st["slowest"]
-                if st.get("slow_hip", {}).get("slow"):
-                    b["slow_hip_calls"] = st["slow_hip"]
-                if st.get("cpu_s_per_gib_by_thread"):
-                    b["cpu_s_per_gib_by_thread"] = st["cpu_s_per_gib_by_thread"]
-                if key.startswith("list_read_"):
-                    b["list_ms"] = round(st["list_ms_max"], 3)
-                if key == "sliced":
-                    b["host_landed_p50_ms"] = round(st["host_p50_max"], 3)
-                    b["slice_skew_ms"] = round(st["skew_max"], 3)
-                    if st.get("cpu"):
-                        b["process_cpu_s_per_gib"] = st["cpu"]["process_cpu_s_per_gib"]
-                        b["cpus_busy"] = st["cpu"].get("cpus_busy")
-                        if "cgroup_nr_throttled" in st["cpu"]:
-                            b["cgroup_nr_throttled"] = st["cpu"]["cgroup_nr_throttled"]
-                out[key] = b
             line = json.dumps(out)
-            print(line, flush=True)
+            report.final(line)
             if args.json_out:
                 with open(args.json_out, "w") as f:
                     f.write(line + "\n")

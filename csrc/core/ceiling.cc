@@ -164,6 +164,7 @@ CeilingResult tcp_ceiling(const CeilingConfig& c) {
   sockaddr_in a{};
   a.sin_family = AF_INET;
   a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  set_endpoint_congestion_control(ls.fd);  // on the listener: see Listener (net/socket.cc)
   if (bind(ls.fd, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0 || listen(ls.fd, 1) != 0) fail("bind/listen");
   socklen_t al = sizeof(a);
   getsockname(ls.fd, reinterpret_cast<sockaddr*>(&a), &al);

@@ -75,6 +75,13 @@ struct GpuSinkConfig {
   // 0.23 -> 0.17 over HTTP, same MiB/s.  Env GCSB_WAIT_POLL_US (0 = the
   // runtime's blocking wait).
   int wait_poll_us = 10;
+  // Attribution A/B only (scripts/experiments/recv_cost_ab.py): what reads a
+  // filled ring slot.  kH2D is the data plane; kNone hands the slot straight
+  // back (nothing reads the ring: the receive copy alone); kHostRead has the
+  // submitter thread read it (host CRC32C) instead of the copy engine.  The
+  // two A/B stages land nothing in HBM and verify nothing.
+  enum class Stage { kH2D, kNone, kHostRead };
+  Stage stage = Stage::kH2D;
 };
 
 struct GpuSinkStats {
@@ -187,6 +194,7 @@ class GpuSink : public Sink {
   uint32_t op_val_[4] = {0, 0, 0, 0};
   int op_rr_ = 0;
   GpuSinkStats stats_;
+  uint32_t host_read_sink_ = 0;  // Stage::kHostRead's CRC (keeps the read)
   std::mutex sub_mu_;
   std::condition_variable sub_cv_;
 };
@@ -211,10 +219,14 @@ class GpuByteSource : public ByteSource {
   // Objects up to kWholeRingMax (GCSB_UPLOAD_SPLICE, default on) stage into a
   // ring that holds all of them: no slot is refilled during the upload, so
   // the transport can splice the staged pages instead of copying them.
+  // Larger objects (or parts) keep the bounded refilling ring of `slots`
+  // slots and are sent by copy: pinned staging per upload stays at most
+  // 64 MiB (the config-5 object) whatever the object size, within the
+  // pinned pool's 1 GiB.
   bool stable_until_done() const override {
     return static_cast<uint64_t>(nslots_) * slot_bytes_ >= n_;
   }
-  static constexpr uint64_t kWholeRingMax = uint64_t(512) << 20;
+  static constexpr uint64_t kWholeRingMax = uint64_t(64) << 20;
 
  private:
   void restart(uint64_t off);

@@ -551,6 +551,7 @@ void GpuSink::set_device() const { ensure_device(cfg_.device); }
 
 GpuSink::GpuSink(const GpuSinkConfig& cfg) : cfg_(cfg) {
   cfg_.async_submit = env_flag("GCSB_ASYNC_SUBMIT", cfg_.async_submit);
+  if (cfg_.stage != GpuSinkConfig::Stage::kH2D) cfg_.verify = false;
   if (env_flag("GCSB_EVENT_SPIN", false)) cfg_.blocking_sync = false;
   if (const char* e = std::getenv("GCSB_WAIT_POLL_US")) cfg_.wait_poll_us = std::max(0, std::atoi(e));
   if (cfg_.slots < 2) cfg_.slots = 2;
@@ -829,6 +830,11 @@ void GpuSink::submit_current() {
 // device submitter thread (async_submit) or inline.
 void GpuSink::enqueue_slot(Slot& s, uint8_t* dst, const CrcBatch* batch) {
   auto issue = [this, &s, dst](const CrcBatch* b) {
+    if (cfg_.stage == GpuSinkConfig::Stage::kHostRead) {
+      host_read_sink_ = crc32c_extend(host_read_sink_, s.host, s.used);
+      return;
+    }
+    if (cfg_.stage == GpuSinkConfig::Stage::kNone) return;
     ensure_device(cfg_.device);
     // copy, CRC and completion event in one stream's order: no cross-stream wait
     const int64_t t0 = now_ns();
@@ -881,9 +887,10 @@ void GpuSink::wait_slot(Slot& s) {
     std::unique_lock<std::mutex> lk(sub_mu_);
     sub_cv_.wait(lk, [&] { return s.submitted; });
   }
+  s.inflight = false;
+  if (cfg_.stage != GpuSinkConfig::Stage::kH2D) return;  // A/B stages: no GPU work queued
   set_device();
   wait_event(s.ev);
-  s.inflight = false;
   harvest(s);
 }
 
@@ -987,7 +994,7 @@ void GpuSink::abort() {
         std::unique_lock<std::mutex> lk(sub_mu_);
         sub_cv_.wait(lk, [&] { return s.submitted; });
       }
-      hip_check(hipEventSynchronize(s.ev), "hipEventSynchronize");
+      if (cfg_.stage == GpuSinkConfig::Stage::kH2D) hip_check(hipEventSynchronize(s.ev), "hipEventSynchronize");
       s.inflight = false;
     }
 }

@@ -69,11 +69,58 @@ bool apply_settings_payload(const uint8_t* p, size_t n, H2Settings* s) {
   return true;
 }
 
+namespace {
+thread_local int64_t t_last_wait_ns = 0;
+}
+
+void FifoLock::lock() {
+  std::unique_lock<std::mutex> lk(mu_);
+  if (!held_) {
+    held_ = true;
+    t_last_wait_ns = 0;
+    return;
+  }
+  const int64_t t0 = now_ns();
+  Waiter w;
+  q_.push_back(&w);
+  w.cv.wait(lk, [&] { return w.granted; });  // ownership handed over by unlock()
+  t_last_wait_ns = now_ns() - t0;
+}
+
+void FifoLock::unlock() {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (q_.empty()) {
+    held_ = false;
+    return;
+  }
+  Waiter* w = q_.front();
+  q_.pop_front();
+  w->granted = true;  // held_ stays set: the lock passes to the oldest waiter
+  w->cv.notify_one();  // under mu_: w lives on the waiter's stack until it sees granted
+}
+
+int64_t FifoLock::last_wait_ns() { return t_last_wait_ns; }
+
+void note_send(H2SendStats& st, uint64_t wait_ns) {
+  st.data_frames.fetch_add(1, std::memory_order_relaxed);
+  st.queue_wait_ns.fetch_add(wait_ns, std::memory_order_relaxed);
+  uint64_t m = st.queue_wait_max_ns.load(std::memory_order_relaxed);
+  while (wait_ns > m && !st.queue_wait_max_ns.compare_exchange_weak(m, wait_ns, std::memory_order_relaxed)) {
+  }
+}
+
+void H2Writer::note_data_frame() {
+  const uint64_t w = static_cast<uint64_t>(FifoLock::last_wait_ns());
+  note_send(sstats_, w);
+  if (sink_) note_send(*sink_, w);
+}
+
 void H2Writer::write_frame(uint8_t type, uint8_t flags, uint32_t stream, const void* p, size_t n) {
   uint8_t hdr[9];
   encode_frame_header(hdr, static_cast<uint32_t>(n), type, flags, stream);
   iovec iov[2] = {{hdr, 9}, {const_cast<void*>(p), n}};
-  std::lock_guard<std::mutex> lk(wmu_);
+  std::lock_guard<FifoLock> lk(wmu_);
+  if (type == h2::kData) note_data_frame();
   conn_.writev_all(iov, n ? 2 : 1);
 }
 
@@ -84,7 +131,8 @@ void H2Writer::write_frame_iov(uint8_t type, uint8_t flags, uint32_t stream, str
   std::vector<iovec> iov(static_cast<size_t>(cnt) + 1);
   iov[0] = {hdr, 9};
   for (int i = 0; i < cnt; ++i) iov[static_cast<size_t>(i) + 1] = payload[i];
-  std::lock_guard<std::mutex> lk(wmu_);
+  std::lock_guard<FifoLock> lk(wmu_);
+  if (type == h2::kData) note_data_frame();
   conn_.writev_all(iov.data(), cnt + 1);
 }
 
@@ -94,7 +142,8 @@ void H2Writer::write_frame_pieces(uint8_t type, uint8_t flags, uint32_t stream, 
   encode_frame_header(hdr, static_cast<uint32_t>(total), type, flags, stream);
   std::vector<iovec> iov;
   iov.push_back({hdr, 9});
-  std::lock_guard<std::mutex> lk(wmu_);
+  std::lock_guard<FifoLock> lk(wmu_);
+  if (type == h2::kData) note_data_frame();
   for (size_t i = 0; i < pieces.size(); ++i) {
     const SendPiece& p = pieces[i];
     if (p.fd < 0 && !p.splice) {
@@ -115,7 +164,7 @@ void H2Writer::write_frame_pieces(uint8_t type, uint8_t flags, uint32_t stream, 
 
 void H2Writer::write_headers(uint32_t stream, const std::string& block, bool end_stream) {
   const size_t maxf = peer_max_frame_;
-  std::lock_guard<std::mutex> lk(wmu_);  // HEADERS+CONTINUATION must be contiguous
+  std::lock_guard<FifoLock> lk(wmu_);  // HEADERS+CONTINUATION must be contiguous
   size_t off = 0;
   bool first = true;
   do {
@@ -145,7 +194,7 @@ bool H2Writer::write_headers_and_data(uint32_t stream, const std::string& block,
   encode_frame_header(hh, static_cast<uint32_t>(block.size()), h2::kHeaders, h2::kFlagEndHeaders, stream);
   encode_frame_header(dh, static_cast<uint32_t>(n), h2::kData, h2::kFlagEndStream, stream);
   iovec iov[4] = {{hh, 9}, {const_cast<char*>(block.data()), block.size()}, {dh, 9}, {const_cast<uint8_t*>(p), n}};
-  std::lock_guard<std::mutex> lk(wmu_);
+  std::lock_guard<FifoLock> lk(wmu_);
   conn_.writev_all(iov, 4);
   return true;
 }
@@ -179,6 +228,7 @@ size_t H2Writer::reserve(uint32_t stream, size_t want) {
     int64_t avail = std::min(conn_window_, it->second);
     if (avail > 0) {
       size_t n = std::min<size_t>({want, static_cast<size_t>(avail), static_cast<size_t>(peer_max_frame_.load())});
+      if (quantum_ > 0 && stream_window_.size() > 1) n = std::min(n, quantum_);
       conn_window_ -= static_cast<int64_t>(n);
       it->second -= static_cast<int64_t>(n);
       return n;

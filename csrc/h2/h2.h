@@ -10,6 +10,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
+#include <deque>
 #include <functional>
 #include <map>
 #include <memory>
@@ -71,11 +72,49 @@ struct SendPiece {
   bool splice = false;
 };
 
+// Mutual exclusion granted in arrival order, one wake per hand-off.  The
+// frame writes of a connection's streams go through it: a std::mutex lets
+// the thread that just wrote a frame take the lock straight back, so with 48
+// streams multiplexed on one connection some waited ~10 ms for their first
+// frame.  lock_wait_ns(): how long the last lock() of
+// the calling thread waited.
+class FifoLock {
+ public:
+  void lock();
+  void unlock();
+  static int64_t last_wait_ns();
+
+ private:
+  struct Waiter {
+    std::condition_variable cv;
+    bool granted = false;
+  };
+  std::mutex mu_;
+  bool held_ = false;
+  std::deque<Waiter*> q_;
+};
+
+// Frame-write statistics of one H2Writer: DATA frames written and how long
+// their writers queued for the connection (the endpoint's per-stream
+// fairness, ServerStats::h2_*).
+struct H2SendStats {
+  std::atomic<uint64_t> data_frames{0}, queue_wait_ns{0}, queue_wait_max_ns{0};
+};
+
 // Per-direction connection machinery common to both roles: serialized
 // writes, peer settings, send-side flow-control windows.
 class H2Writer {
  public:
   explicit H2Writer(Conn& c) : conn_(c) {}
+  // While more than one stream is registered, DATA frames are capped at
+  // `bytes` (0 = the peer's max frame size only): the streams' frames then
+  // interleave in FIFO order at this grain (round-robin over the streams
+  // with data ready) instead of one stream's whole message holding the
+  // connection.  The endpoint sets 256 KiB (ServerConfig::h2_quantum).
+  void set_quantum(size_t bytes) { quantum_ = bytes; }
+  // DATA-frame statistics also go to *sink (e.g. the endpoint's totals)
+  void set_stats_sink(H2SendStats* sink) { sink_ = sink; }
+  const H2SendStats& send_stats() const { return sstats_; }
   // Writes one frame (header + payload pieces) atomically w.r.t. other writers.
   void write_frame(uint8_t type, uint8_t flags, uint32_t stream, const void* p, size_t n);
   void write_frame_iov(uint8_t type, uint8_t flags, uint32_t stream, struct iovec* payload, int cnt, size_t total);
@@ -110,8 +149,12 @@ class H2Writer {
   Conn& conn() { return conn_; }
 
  private:
+  void note_data_frame();
   Conn& conn_;
-  std::mutex wmu_;  // frame writes
+  FifoLock wmu_;  // frame writes, granted in arrival order
+  size_t quantum_ = 0;
+  H2SendStats sstats_;
+  H2SendStats* sink_ = nullptr;
   std::mutex fmu_;  // flow control
   std::condition_variable fcv_;
   int64_t conn_window_ = h2::kDefaultWindow;

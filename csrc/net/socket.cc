@@ -619,6 +619,15 @@ Listener::Listener(const std::string& host, int port, int backlog) {
     ::close(fd);
     throw std::runtime_error("bind " + host + ":" + std::to_string(port) + ": " + err);
   }
+  // The endpoint's congestion control goes on the LISTENING socket, so an
+  // accepted connection starts with it.  Set after accept() (round 3) the
+  // child had already run the host default's init: BBR's marks the socket
+  // for internal pacing (sk_pacing_status), which no later TCP_CONGESTION
+  // undoes, so "cubic" connections were still paced by an hrtimer per
+  // 64 KiB skb -- ~4,000 timer interrupts per 256 MiB read on the sending
+  // and receiving cores, whose count moved every block's rate
+  // (profiles/r4_recvcost).
+  set_endpoint_congestion_control(fd);
   if (::listen(fd, backlog) != 0) {
     ::close(fd);
     throw std::runtime_error("listen failed");

@@ -91,6 +91,10 @@ GpuSinkConfig gpu_from(const py::dict& d) {
   g.blocking_sync = get_or<bool>(d, "blocking_sync", g.blocking_sync);
   g.wait_poll_us = get_or<int>(d, "wait_poll_us", g.wait_poll_us);
   g.ring_wc = get_or<bool>(d, "ring_wc", g.ring_wc);
+  const std::string stage = get_or<std::string>(d, "gpu_stage", "h2d");
+  if (stage == "none") g.stage = GpuSinkConfig::Stage::kNone;
+  else if (stage == "host_read") g.stage = GpuSinkConfig::Stage::kHostRead;
+  else if (stage != "h2d") throw std::invalid_argument("gpu_stage: h2d | none | host_read");
   return g;
 }
 
@@ -363,6 +367,7 @@ class PyClient {
     double crc_ms = 0, upload_ms = 0;
     uint64_t copies = 0, range_crcs = 0;
     uint32_t crc = 0;
+    bool whole = false;
     {
       py::gil_scoped_release nogil;
       int64_t t0 = now_ns();
@@ -378,9 +383,11 @@ class PyClient {
       copies = src.copies();
       range_crcs = src.gpu_range_crcs();
       crc = src.crc32c();
+      whole = src.stable_until_done();
     }
     py::dict d = meta_dict(m);
     d["gpu_crc32c"] = crc;
+    d["staged_whole"] = whole;  // the whole object staged at once (zero-copy sends)
     d["gpu_message_crcs"] = range_crcs;  // upload messages whose CRC came from the GPU
     d["gpu_crc_ms"] = crc_ms;
     d["upload_ms"] = upload_ms;
@@ -540,6 +547,7 @@ class PyServer {
     c.grpc_chunk = get_or<uint64_t>(d, "grpc_chunk", 2u << 20);
     c.sndbuf = get_or<int>(d, "sndbuf", 0);
     c.zero_copy = get_or<bool>(d, "zero_copy", true);
+    c.h2_quantum = get_or<size_t>(d, "h2_quantum", c.h2_quantum);
     c.tls_cert_file = get_or<std::string>(d, "tls_cert_file", "");
     c.tls_key_file = get_or<std::string>(d, "tls_key_file", "");
     if (d.contains("cpus") && !d["cpus"].is_none()) c.cpus = d["cpus"].cast<std::vector<int>>();
@@ -607,6 +615,7 @@ class PyServer {
     if (d.contains("corrupt_count")) f.corrupt_count = d["corrupt_count"].cast<int>();
     if (d.contains("throttle_bps")) f.throttle_bps = d["throttle_bps"].cast<int64_t>();
     if (d.contains("latency_ms")) f.latency_ms = d["latency_ms"].cast<int>();
+    if (d.contains("finalize_delay_ms")) f.finalize_delay_ms = d["finalize_delay_ms"].cast<int>();
     if (d.contains("drop_trailers_count")) f.drop_trailers_count = d["drop_trailers_count"].cast<int>();
     if (d.contains("stall_at")) f.stall_at = d["stall_at"].cast<int64_t>();
     if (d.contains("stall_ms")) f.stall_ms = d["stall_ms"].cast<int>();
@@ -628,6 +637,12 @@ class PyServer {
     d["tcp_rwnd_limited_us"] = s.tcp_rwnd_limited_us.load();
     d["tcp_sndbuf_limited_us"] = s.tcp_sndbuf_limited_us.load();
     d["tcp_cwnd_bytes_sum"] = s.tcp_cwnd_bytes_sum.load();
+    d["h2_data_frames"] = s.h2_send.data_frames.load();
+    d["h2_queue_wait_us"] = s.h2_send.queue_wait_ns.load() / 1000;
+    d["h2_queue_wait_max_us"] = s.h2_send.queue_wait_max_ns.load() / 1000;
+    d["h2_responses"] = s.h2_responses.load();
+    d["h2_ttfb_us"] = s.h2_ttfb_ns.load() / 1000;
+    d["h2_ttfb_max_us"] = s.h2_ttfb_max_ns.load() / 1000;
     return d;
   }
   std::string issue_token() { return srv_->issue_token(); }

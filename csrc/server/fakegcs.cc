@@ -17,6 +17,15 @@
 
 namespace gcsb {
 
+void ServerStats::note_ttfb(int64_t ns) {
+  const uint64_t v = ns > 0 ? static_cast<uint64_t>(ns) : 0;
+  h2_responses.fetch_add(1, std::memory_order_relaxed);
+  h2_ttfb_ns.fetch_add(v, std::memory_order_relaxed);
+  uint64_t m = h2_ttfb_max_ns.load(std::memory_order_relaxed);
+  while (v > m && !h2_ttfb_max_ns.compare_exchange_weak(m, v, std::memory_order_relaxed)) {
+  }
+}
+
 void ServerStats::note_body_send(int fd, const TcpChrono& a, bool a_ok, int64_t t0_ns) {
   TcpChrono b;
   if (!a_ok || !read_tcp_chrono(fd, &b)) return;

@@ -13,6 +13,7 @@
 #include <thread>
 #include <vector>
 
+#include "h2/h2.h"
 #include "net/socket.h"
 #include "server/store.h"
 
@@ -31,6 +32,7 @@ struct FaultConfig {
   std::atomic<int64_t> stall_at{-1};        // pause a response this long before sending this object offset...
   std::atomic<int> stall_ms{0};
   std::atomic<int> stall_count{0};          // ...in this many responses (client read-timeout tests)
+  std::atomic<int> finalize_delay_ms{0};    // gRPC WriteObject: hold the final response this long
 };
 
 struct ServerConfig {
@@ -42,6 +44,9 @@ struct ServerConfig {
   int sndbuf = 0;          // 0 = kernel autotuning (an explicit size disables it)
   bool zero_copy = true;   // sendfile() synthetic object bodies from a memfd
   std::vector<int> cpus;   // pin connection/handler threads (empty = unpinned)
+  // HTTP/2: DATA frame cap while several streams share a connection, so
+  // their frames interleave round-robin (H2Writer::set_quantum; 0 = off)
+  size_t h2_quantum = 256u << 10;
   // https / gRPC over TLS (ALPN h2 or http/1.1) when both are set (PEM files)
   std::string tls_cert_file, tls_key_file;
 };
@@ -56,6 +61,13 @@ struct ServerStats {
       tcp_sndbuf_limited_us{0}, tcp_cwnd_bytes_sum{0};
   // account one body send on fd that started at t0_ns with chronographs a
   void note_body_send(int fd, const TcpChrono& a, bool a_ok, int64_t t0_ns);
+  // HTTP/2 DATA frames sent and how long their stream handlers queued for
+  // the connection (FIFO, H2Writer): the endpoint's fairness across streams
+  H2SendStats h2_send;
+  // a stream's request complete (END_STREAM seen) -> its response HEADERS
+  // written: the endpoint's share of a read's TTFB
+  std::atomic<uint64_t> h2_responses{0}, h2_ttfb_ns{0}, h2_ttfb_max_ns{0};
+  void note_ttfb(int64_t ns);
 };
 // bodies at least this long get their send chronographs read
 constexpr uint64_t kChronoMinBody = 8u << 20;

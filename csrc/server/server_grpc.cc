@@ -90,6 +90,7 @@ struct ServerStream {
   std::vector<std::string> messages;
   std::atomic<bool> cancelled{false};
   bool half_closed = false;
+  int64_t request_done_ns = 0;  // END_STREAM seen (dispatch): TTFB accounting
   RecvWindow rw{16 << 20};
   // WriteObject state
   std::shared_ptr<UploadSession> session;
@@ -136,7 +137,10 @@ struct Cancelled {};
 
 class H2ServerConn {
  public:
-  H2ServerConn(FakeGcsServer& srv, BufferedConn& bc) : srv_(srv), bc_(bc), w_(bc.conn()) {}
+  H2ServerConn(FakeGcsServer& srv, BufferedConn& bc) : srv_(srv), bc_(bc), w_(bc.conn()) {
+    w_.set_quantum(srv.config().h2_quantum);
+    w_.set_stats_sink(&srv.stats().h2_send);
+  }
 
   ~H2ServerConn() {
     w_.kill();
@@ -414,7 +418,17 @@ class H2ServerConn {
       WriteJob j = std::move(wjobs_.front());
       wjobs_.pop_front();
       lk.unlock();
-      process_write_message(*j.s, std::string_view(j.buf.get(), j.len));
+      try {
+        process_write_message(*j.s, std::string_view(j.buf.get(), j.len));
+      } catch (const std::exception& e) {
+        // e.g. std::bad_alloc growing the upload (mmap / mremap): the stream
+        // fails with INTERNAL; this thread, and the process, go on
+        if (!j.s->write_error) {
+          j.s->write_error = true;
+          j.s->write_code = kInternal;
+          j.s->write_msg = std::string("write failed: ") + e.what();
+        }
+      }
       lk.lock();
       wfree_.push_back(std::move(j.buf));
       if (wfree_.size() > write_worker_bufs()) wfree_.erase(wfree_.begin());
@@ -434,6 +448,7 @@ class H2ServerConn {
   void dispatch(const std::shared_ptr<ServerStream>& s) {
     if (s->half_closed) return;
     s->half_closed = true;
+    s->request_done_ns = now_ns();
     {
       std::lock_guard<std::mutex> lk(mu_);
       ++active_handlers_;
@@ -681,6 +696,7 @@ class H2ServerConn {
     enc_.encode(hl, &block);
     const bool empty = s.method == "HEAD" || mp.len == 0;
     w_.write_headers(s.id, block, empty);
+    srv_.stats().note_ttfb(now_ns() - s.request_done_ns);
     if (!empty) send_object_body(s, *o, mp.start, mp.len);
   }
 
@@ -783,6 +799,7 @@ class H2ServerConn {
     auto& f = srv_.faults();
     if (int lat = f.latency_ms.load()) std::this_thread::sleep_for(std::chrono::milliseconds(lat));
     send_headers(s.id);
+    srv_.stats().note_ttfb(now_ns() - s.request_done_ns);
     const uint64_t chunk = srv_.config().grpc_chunk;
     const std::string checksums = v2::encode_checksums(true, o->crc32c, o->md5());
     v2::ContentRange cr;
@@ -1003,6 +1020,7 @@ class H2ServerConn {
 
   void write_object_done(ServerStream& s) {
     wait_write_messages(s);
+    if (int d = srv_.faults().finalize_delay_ms.load()) std::this_thread::sleep_for(std::chrono::milliseconds(d));
     if (s.write_error) return send_trailers(s.id, s.write_code, s.write_msg, false);
     if (!s.session) return send_trailers(s.id, kInvalidArgument, "empty WriteObject stream", false);
     v2::WriteStatus st;

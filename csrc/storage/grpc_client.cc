@@ -821,11 +821,21 @@ class GrpcStorageClient : public StorageClient {
         if (last) break;
         if (k == 0) throw StorageError("upload source ended early", false);
       } while (true);
-      // no read idle limit on the upload's final response: a server that
-      // takes longer than -read-timeout to finalize a large object would
-      // otherwise have the whole non-resumable upload sent again (a
-      // duplicate generation if the first one committed)
-      call->wait_ok(nullptr, 0);
+      // The final response gets its own, longer idle bound (10 x
+      // -read-timeout): a server may take longer than
+      // -read-timeout to finalize a large object.  Running out of it is NOT
+      // retryable: the whole upload sent again could duplicate a generation
+      // the first one committed.
+      const int fin_ms = idle_ms_ > 0 ? 10 * idle_ms_ : 0;
+      try {
+        call->wait_ok(nullptr, fin_ms, [c, call, fin_ms] { c->abandon_stream(*call, fin_ms); });
+      } catch (const StorageError& e) {
+        if (fin_ms > 0 && std::strncmp(e.what(), "read timeout", 12) == 0)
+          throw StorageError("WriteObject: no final response within " + std::to_string(fin_ms) +
+                                 " ms of the last byte (not retried: the upload may have committed)",
+                             false);
+        throw;
+      }
     } catch (...) {
       c->end_stream(*call, true);
       throw;

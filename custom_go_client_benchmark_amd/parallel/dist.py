@@ -133,6 +133,23 @@ def collective_timeout_s() -> float:
     return float(os.environ.get("GCSB_COLLECTIVE_TIMEOUT_S", "120"))
 
 
+_fatal_hooks: list = []
+
+
+def on_fatal(fn) -> None:
+    """Run fn() before a barrier watchdog ends the process (the bench prints
+    the headline line it has measured so far)."""
+    _fatal_hooks.append(fn)
+
+
+def _run_fatal_hooks() -> None:
+    for fn in list(_fatal_hooks):
+        try:
+            fn()
+        except Exception as e:  # noqa: BLE001 - never stop the exit path
+            sys.stderr.write(f"fatal hook failed: {e}\n")
+
+
 class BarrierTimeout(RuntimeError):
     """A peer rank did not reach a barrier in time (dead or stuck)."""
 
@@ -156,8 +173,37 @@ def _watchdog(ctx: DistContext, what: str, timeout_s: float, done: threading.Eve
     except Exception as e:  # gloo has no abort; fall through to the hard exit
         sys.stderr.write(f"[rank {ctx.rank}] communicator abort unavailable: {e}\n")
     if hard_exit and not done.wait(5.0):
+        _run_fatal_hooks()
+        sys.stdout.flush()
         sys.stderr.flush()
         os._exit(3)
+
+
+def barrier_timeout_s() -> float:
+    """Control-plane collectives (barriers, stat reductions) give up after
+    this (GCSB_BARRIER_TIMEOUT_S, default 300 s)."""
+    return float(os.environ.get("GCSB_BARRIER_TIMEOUT_S", "300"))
+
+
+class _Watched:
+    """A control-plane collective under the hard-exit watchdog (_watchdog):
+    a peer that never arrives ends this rank with status 3 instead of
+    leaving it in the collective until the process-group timeout."""
+
+    def __init__(self, ctx: DistContext, what: str, timeout_s: float | None = None):
+        self.done = threading.Event()
+        self.t = threading.Thread(target=_watchdog,
+                                  args=(ctx, what, barrier_timeout_s() if timeout_s is None else timeout_s,
+                                        self.done),
+                                  name="gcsb-barrier-watchdog", daemon=True)
+
+    def __enter__(self):
+        self.t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.done.set()
+        return False
 
 
 def barrier(ctx: DistContext, what: str = "barrier", timeout_s: float | None = None) -> None:
@@ -168,21 +214,14 @@ def barrier(ctx: DistContext, what: str = "barrier", timeout_s: float | None = N
     import torch
     import torch.distributed as dist
 
-    if timeout_s is None:
-        timeout_s = float(os.environ.get("GCSB_BARRIER_TIMEOUT_S", "300"))
-    done = threading.Event()
-    wd = threading.Thread(target=_watchdog, args=(ctx, what, timeout_s, done), name="gcsb-barrier-watchdog",
-                          daemon=True)
-    wd.start()
     try:
-        t = torch.ones(1, dtype=torch.int32, device=ctx.device)
-        dist.all_reduce(t)
-        if ctx.gpu >= 0:
-            torch.cuda.synchronize(ctx.gpu)
+        with _Watched(ctx, what, timeout_s):
+            t = torch.ones(1, dtype=torch.int32, device=ctx.device)
+            dist.all_reduce(t)
+            if ctx.gpu >= 0:
+                torch.cuda.synchronize(ctx.gpu)
     except Exception as e:
         raise BarrierTimeout(f"{what} failed on rank {ctx.rank}: {e}") from e
-    finally:
-        done.set()
     if int(t.item()) != ctx.world:
         raise RuntimeError(f"barrier mismatch: {int(t.item())} != {ctx.world}")
 
@@ -264,11 +303,12 @@ def reduce_stats(ctx: DistContext, **vals: float) -> dict:
 
     base = torch.tensor([float(vals[k]) for k in keys], dtype=torch.float64, device=ctx.device)
     s, mx, mn = base.clone(), base.clone(), base.clone()
-    dist.all_reduce(s, op=dist.ReduceOp.SUM)
-    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-    dist.all_reduce(mn, op=dist.ReduceOp.MIN)
     gathered = [torch.zeros_like(base) for _ in range(ctx.world)]
-    dist.all_gather(gathered, base)
+    with _Watched(ctx, "R3 stats reduce"):
+        dist.all_reduce(s, op=dist.ReduceOp.SUM)
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(mn, op=dist.ReduceOp.MIN)
+        dist.all_gather(gathered, base)
     for i, k in enumerate(keys):
         out[k + "_sum"] = float(s[i])
         out[k + "_max"] = float(mx[i])
@@ -285,7 +325,8 @@ def reduce_histogram(ctx: DistContext, buckets: list[int]) -> list[int]:
     import torch.distributed as dist
 
     t = torch.tensor(buckets, dtype=torch.int64, device=ctx.device)
-    dist.all_reduce(t)
+    with _Watched(ctx, "R3 histogram reduce"):
+        dist.all_reduce(t)
     return [int(x) for x in t.tolist()]
 
 
@@ -298,7 +339,8 @@ def gather_floats(ctx: DistContext, vals: list[float]) -> list[list[float]]:
 
     base = torch.tensor([float(v) for v in vals], dtype=torch.float64, device=ctx.device)
     out = [torch.zeros_like(base) for _ in range(ctx.world)]
-    dist.all_gather(out, base)
+    with _Watched(ctx, "R4 gather"):
+        dist.all_gather(out, base)
     return [[float(x) for x in t.tolist()] for t in out]
 
 

@@ -1,0 +1,167 @@
+"""Host-side stall attribution for the timed blocks: what, besides our own
+threads' CPU time, took a receiving or sending core away.
+
+A loopback read is bound by one receiving core (the h2 reader) and fed by
+one sending core (the endpoint's handler).  When either is descheduled, or
+its CPU is busy with interrupts, the stream stalls while our own CPU
+counters (cpuacct) show nothing.  Three host views, all readable without
+privileges and cheap enough to snapshot around every timed block:
+
+  thread_sched()  per thread of this process: run-queue delay (schedstat),
+                  voluntary / involuntary context switches, last CPU;
+  irq_snapshot()  /proc/interrupts per CPU and source (GPU completion
+                  interrupts, NIC, IPIs, timers);
+  softirq_snapshot()  /proc/softirqs per CPU (NET_RX / NET_TX, TIMER, RCU).
+
+Reference timed region: /root/reference/main.go:133-145 (request -> last
+byte); these views explain a read's stall inside that region, they add
+nothing to it.
+"""
+from __future__ import annotations
+
+import os
+
+_TASKS = "/proc/self/task"
+
+
+def _read(path: str) -> str | None:
+    try:
+        with open(path) as f:
+            return f.read()
+    except OSError:
+        return None
+
+
+def thread_sched() -> dict[int, dict]:
+    """{tid: {name, cpu_ns, run_delay_ns, slices, nvcsw, nivcsw, cpu}} for
+    every live thread of this process.  run_delay_ns is the time the thread
+    was runnable but waiting for a CPU (schedstat field 2)."""
+    out: dict[int, dict] = {}
+    try:
+        tids = os.listdir(_TASKS)
+    except OSError:
+        return out
+    for t in tids:
+        st = _read(f"{_TASKS}/{t}/stat")
+        ss = _read(f"{_TASKS}/{t}/schedstat")
+        if not st or not ss:
+            continue
+        lp, rp = st.find("("), st.rfind(")")
+        f = st[rp + 2:].split()
+        try:
+            cpu_ns, delay_ns, slices = (int(x) for x in ss.split()[:3])
+            last_cpu = int(f[36])
+        except (ValueError, IndexError):
+            continue
+        d = {"name": st[lp + 1:rp], "cpu_ns": cpu_ns, "run_delay_ns": delay_ns, "slices": slices,
+             "cpu": last_cpu, "nvcsw": 0, "nivcsw": 0}
+        status = _read(f"{_TASKS}/{t}/status") or ""
+        for line in status.splitlines():
+            if line.startswith("voluntary_ctxt_switches:"):
+                d["nvcsw"] = int(line.split()[1])
+            elif line.startswith("nonvoluntary_ctxt_switches:"):
+                d["nivcsw"] = int(line.split()[1])
+        out[int(t)] = d
+    return out
+
+
+def sched_delta(a: dict[int, dict], b: dict[int, dict], reads: int = 1, top: int = 8) -> dict:
+    """Per thread name (threads of one name summed): CPU ms, run-queue delay
+    ms and involuntary switches between two thread_sched() snapshots, per
+    read; only threads that ran.  Also the CPUs each name last ran on."""
+    agg: dict[str, dict] = {}
+    for tid, y in b.items():
+        x = a.get(tid, {"cpu_ns": 0, "run_delay_ns": 0, "nvcsw": 0, "nivcsw": 0})
+        dc = y["cpu_ns"] - x["cpu_ns"]
+        if dc <= 0:
+            continue
+        g = agg.setdefault(y["name"], {"threads": 0, "cpu_ms": 0.0, "run_delay_ms": 0.0, "nvcsw": 0, "nivcsw": 0,
+                                       "cpus": set()})
+        g["threads"] += 1
+        g["cpu_ms"] += dc / 1e6
+        g["run_delay_ms"] += (y["run_delay_ns"] - x["run_delay_ns"]) / 1e6
+        g["nvcsw"] += y["nvcsw"] - x["nvcsw"]
+        g["nivcsw"] += y["nivcsw"] - x["nivcsw"]
+        g["cpus"].add(y["cpu"])
+    r = max(1, reads)
+    rows = sorted(agg.items(), key=lambda kv: -kv[1]["cpu_ms"])[:top]
+    return {k: {"threads": v["threads"], "cpu_ms_per_read": round(v["cpu_ms"] / r, 3),
+                "run_delay_ms_per_read": round(v["run_delay_ms"] / r, 4),
+                "nivcsw_per_read": round(v["nivcsw"] / r, 2), "nvcsw_per_read": round(v["nvcsw"] / r, 2),
+                "last_cpus": sorted(v["cpus"])}
+            for k, v in rows}
+
+
+def _per_cpu_table(text: str | None) -> tuple[list[int], dict[str, list[int]]]:
+    """(cpu ids of the header, {row label: per-cpu counts}) of a
+    /proc/interrupts- or /proc/softirqs-shaped table."""
+    if not text:
+        return [], {}
+    lines = text.splitlines()
+    cpus = [int(c[3:]) for c in lines[0].split() if c.startswith("CPU")]
+    rows: dict[str, list[int]] = {}
+    for line in lines[1:]:
+        head, _, rest = line.partition(":")
+        parts = rest.split()
+        vals = []
+        for p in parts[:len(cpus)]:
+            if not p.isdigit():
+                break
+            vals.append(int(p))
+        if not vals:
+            continue
+        desc = " ".join(parts[len(vals):])
+        label = head.strip()
+        if desc:
+            # device-named IRQs: keep the driver / device part of the label
+            label = f"{label} {desc.split()[-1]}" if label.isdigit() else label
+        rows[label] = vals + [0] * (len(cpus) - len(vals))
+    return cpus, rows
+
+
+def irq_snapshot() -> tuple[list[int], dict[str, list[int]]]:
+    return _per_cpu_table(_read("/proc/interrupts"))
+
+
+def softirq_snapshot() -> tuple[list[int], dict[str, list[int]]]:
+    return _per_cpu_table(_read("/proc/softirqs"))
+
+
+def table_delta(a: tuple, b: tuple, cpus: list[int] | None, reads: int = 1, top: int = 6) -> dict:
+    """Counts per read that landed on `cpus` (all CPUs if None) between two
+    snapshots: {"total": n, "by_source": {label: n, ...}, "by_cpu": {cpu: n}}."""
+    ids, ra = a
+    ids_b, rb = b
+    if not ids or ids != ids_b:
+        return {}
+    want = set(cpus) if cpus else set(ids)
+    idx = [i for i, c in enumerate(ids) if c in want]
+    by_src: dict[str, int] = {}
+    by_cpu: dict[int, int] = {}
+    for label, vb in rb.items():
+        va = ra.get(label, [0] * len(ids))
+        for i in idx:
+            d = vb[i] - va[i]
+            if d > 0:
+                by_src[label] = by_src.get(label, 0) + d
+                by_cpu[ids[i]] = by_cpu.get(ids[i], 0) + d
+    r = max(1, reads)
+    tops = sorted(by_src.items(), key=lambda kv: -kv[1])[:top]
+    return {"total_per_read": round(sum(by_src.values()) / r, 2),
+            "by_source_per_read": {k: round(v / r, 2) for k, v in tops},
+            "by_cpu_per_read": {str(c): round(v / r, 2) for c, v in sorted(by_cpu.items())}}
+
+
+class Window:
+    """Snapshot everything at construction; .report(cpus, reads) after the
+    timed region."""
+
+    def __init__(self):
+        self.sched = thread_sched()
+        self.irq = irq_snapshot()
+        self.soft = softirq_snapshot()
+
+    def report(self, cpus: list[int] | None, reads: int) -> dict:
+        return {"threads": sched_delta(self.sched, thread_sched(), reads),
+                "irq_on_placement": table_delta(self.irq, irq_snapshot(), cpus, reads),
+                "softirq_on_placement": table_delta(self.soft, softirq_snapshot(), cpus, reads)}

@@ -1,0 +1,58 @@
+# Round-4 GPU-box sessions, one function per session:
+#   bash scripts/experiments/r4_sessions.sh <session>
+# Each writes under gpurun_out/r4_<session>/. The summaries were copied into
+# the profile directory named in the comment (see scripts/README.md).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+export TMPDIR=/tmp
+S=${1:?usage: r4_sessions.sh <session>}
+O=gpurun_out/r4_$S
+mkdir -p "$O"
+
+step() {  # step <name> <timeout> <cmd...>: a crash, abort or timeout ends the session
+  local name=$1 t=$2
+  shift 2
+  echo "=== $name ($(date +%T))"
+  local t0
+  t0=$(date +%s.%N)
+  timeout -k 10 "$t" "$@" > "$O/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc wall_s=$(python3 -c "print(round($(date +%s.%N)-$t0,1))")"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+    echo "fatal rc=$rc in $name: stopping"
+    exit $rc
+  fi
+  return 0
+}
+
+irq_map() {  # which CPUs the GPU's interrupt vectors are routed to
+  python3 - <<'EOF' > "$O/irq_map.txt" 2>&1
+import os, re
+for line in open("/proc/interrupts"):
+    if "amdgpu" in line or "kfd" in line:
+        irq = line.split(":")[0].strip()
+        try:
+            aff = open(f"/proc/irq/{irq}/effective_affinity_list").read().strip()
+        except OSError:
+            aff = "?"
+        print(irq, "effective_cpus", aff, " ".join(line.split()[-3:]))
+EOF
+}
+
+case "$S" in
+recvcost)  # profiles/r4_recvcost: headline vs no-DMA vs host-read vs discard baseline, with and without GPU interrupts
+  irq_map
+  step default 400 python3 -u scripts/experiments/recv_cost_ab.py --tag default
+  step noint 400 env HSA_ENABLE_INTERRUPT=0 python3 -u scripts/experiments/recv_cost_ab.py --tag noint
+  step default2 400 python3 -u scripts/experiments/recv_cost_ab.py --tag default2 --reps 2
+  ;;
+recvcost2)  # profiles/r4_recvcost/after_listener_cc: the same A/B once the endpoint's listener carries its CC, + a full bench
+  step ab 400 python3 -u scripts/experiments/recv_cost_ab.py --tag listener_cc
+  step mux 400 python3 -u scripts/experiments/mux_fair_ab.py
+  step bench 600 python3 bench.py --json-out "$O/bench.json"
+  ;;
+*)
+  echo "unknown session $S"
+  exit 2
+  ;;
+esac

@@ -39,7 +39,7 @@ def _bench_line(stdout):
 
 def test_bench_two_ranks_gloo():
     r = torchrun(["bench.py", "--gpus", "2", "--sink", "discard", "--steps", "3", "--warmup", "1",
-                  "--object-size", "4MiB"])
+                  "--object-size", "4MiB", "--blocks", "all"])
     assert r.returncode == 0, r.stderr[-3000:]
     out = _bench_line(r.stdout)
     assert out["n_gpus"] == 2 and out["ranks"] == 2 and out["steps"] == 3 and out["config"]["global_batch"] == 2
@@ -102,6 +102,56 @@ def test_bench_fanout_block_two_ranks():
                         "--warmup", "0", "--object-size", "2MiB", "--side-steps", "1", "--fanout", "off"],
                        capture_output=True, text=True, timeout=240, cwd=ROOT, env=_bench_env())
     assert r.returncode == 0 and "fanout" not in _bench_line(r.stdout)
+
+
+def test_bench_multi_rank_default_blocks():
+    """N > 1 runs only the side blocks the scaling run needs (cpu_baseline,
+    compare, write, fanout); the others are opt-in (--blocks all)."""
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--sink", "discard", "--steps", "2",
+                        "--warmup", "1", "--object-size", "4MiB"],
+                       capture_output=True, text=True, timeout=240, cwd=ROOT, env=_bench_env())
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = _bench_line(r.stdout)
+    assert out["compare"]["ok"] and out["fanout"]["ok"], out
+    for k in ("sliced", "ceiling", "ref_default_grpc", "ref_default_http", "list_read_grpc", "c1_http_cpu"):
+        assert k not in out, k
+    assert "partial" not in out
+    # the headline's host view: thread run-queue delays and interrupts on its CPUs
+    assert "threads" in out["rank0_cpu"]["host"]
+
+
+@pytest.mark.parametrize("hang", ["compare:1", "compare:0", "fanout:1"])
+def test_bench_side_block_hang_keeps_headline(hang):
+    """A side block that hangs on one rank cannot erase the measured
+    headline: the peer's barrier watchdog (or the launcher's SIGTERM to the
+    hung rank 0) prints the headline line stashed after cpu_baseline, and the
+    run exits non-zero."""
+    import time
+
+    env = _bench_env()
+    env.update(GCSB_TEST_HANG=hang, GCSB_BARRIER_TIMEOUT_S="6")
+    t0 = time.time()
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--sink", "discard", "--steps", "2",
+                        "--warmup", "1", "--object-size", "4MiB"],
+                       capture_output=True, text=True, timeout=180, cwd=ROOT, env=env)
+    assert r.returncode != 0, r.stderr[-3000:]
+    out = _bench_line(r.stdout)
+    assert out["value"] > 0 and out["metric"] and out["config"]["parallelism"] == "dp2"
+    assert out["partial"]
+    assert time.time() - t0 < 120
+
+
+def test_bench_side_deadline_prints_headline():
+    """--side-deadline: side blocks running past it end the run (exit 3)
+    with the headline line printed."""
+    env = _bench_env()
+    env.update(GCSB_TEST_HANG="compare:0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "1", "--sink", "discard", "--steps", "2",
+                        "--warmup", "1", "--object-size", "4MiB", "--side-deadline", "5"],
+                       capture_output=True, text=True, timeout=180, cwd=ROOT, env=env)
+    assert r.returncode == 3, r.stderr[-3000:]
+    out = _bench_line(r.stdout)
+    assert out["value"] > 0 and out["partial"]
 
 
 def test_bench_refuses_gpus_world_mismatch():

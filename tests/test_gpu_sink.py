@@ -137,6 +137,25 @@ def test_write_path_hbm_to_server(native, server, gpu_available, proto, resumabl
     assert server.object_bytes(B, name, 0, size) == native.object_bytes(name, 0, size)
 
 
+def test_upload_above_whole_ring_cap_copies(native, server, gpu_available):
+    """An object larger than the whole-object staging cap (64 MiB) is
+    staged through the bounded refilling ring and sent by copy, byte-exact
+    (pinned staging must not grow with the object)."""
+    import torch
+
+    size = (80 << 20) + 4099
+    name = "upload/big_0"
+    t = torch.empty(size, dtype=torch.uint8, device="cuda:0")
+    native.gpu_fill_pattern(0, t.data_ptr(), size, name, 0)
+    c = native.Client({"protocol": "grpc", "endpoint": server.url})
+    m = c.write_from_device(B, name, t.data_ptr(), size, 0, True, 16 << 20, 2 << 20, 4)
+    assert not m["staged_whole"]
+    assert m["size"] == size and m["crc32c"] == m["gpu_crc32c"] == native.crc32c(native.object_bytes(name, 0, size))
+    assert server.object_bytes(B, name, 0, size) == native.object_bytes(name, 0, size)
+    m = c.write_from_device(B, "upload/small_0", t.data_ptr(), 8 << 20, 0, True, 16 << 20, 2 << 20, 4)
+    assert m["staged_whole"]
+
+
 def test_cli_gpu_sink(native, gpu_available):
     import subprocess
     import sys as _sys

@@ -138,3 +138,22 @@ def test_one_stalled_stream_does_not_fail_its_neighbours(native, server, proto):
     assert all(x["verified"] and x["attempts"] == 1 for x in neighbours), [x["attempts"] for x in neighbours]
     if proto == "grpc":
         assert server.stats()["connections"] == 1  # the shared connection was never closed
+
+
+def test_grpc_upload_finalize_has_its_own_bound(native, server):
+    """-read-timeout covers an upload's final response with a longer bound
+    of its own (10x): a finalize slower than -read-timeout still succeeds;
+    one past the bound fails at once, NOT retried (a re-sent upload could
+    duplicate a committed generation)."""
+    data = bytes(range(256)) * 4096
+    c = _client(native, server, "grpc", io_timeout_ms=100, retry_max_attempts=3)
+    server.set_faults({"finalize_delay_ms": 400})
+    m = c.write_bytes(B, "upload/fin_ok", data)
+    assert m["size"] == len(data)
+    server.set_faults({"finalize_delay_ms": 2500})
+    t0 = time.perf_counter()
+    with pytest.raises(Exception, match="final response"):
+        c.write_bytes(B, "upload/fin_slow", data)
+    # one attempt cut at 1-2 s of silence (10 x 100 ms), no retries
+    assert time.perf_counter() - t0 < 2.4
+    server.set_faults({"finalize_delay_ms": 0})

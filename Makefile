@@ -23,7 +23,7 @@ CORE_SRCS := csrc/core/crc32c.cc csrc/core/affinity.cc csrc/core/ceiling.cc csrc
              csrc/net/socket.cc csrc/net/tcp_chrono.cc csrc/net/buffered.cc \
              csrc/http1/http1.cc csrc/h2/hpack.cc csrc/h2/h2.cc csrc/h2/h2_client.cc csrc/proto/storage_v2.cc \
              csrc/storage/sink.cc csrc/storage/sliced.cc csrc/storage/auth.cc csrc/storage/client.cc csrc/storage/http_client.cc \
-             csrc/storage/grpc_client.cc csrc/storage/pipe_relay.cc \
+             csrc/storage/grpc_client.cc \
              csrc/server/store.cc csrc/server/media.cc csrc/server/fakegcs.cc csrc/server/server_http1.cc csrc/server/server_grpc.cc \
              csrc/gpu/crc_host.cc
 GPU_SRCS  := csrc/gpu/crc32c_kernels.hip csrc/gpu/engine.hip csrc/gpu/copy_engines.hip
@@ -34,13 +34,17 @@ GPU_OBJS  := $(patsubst csrc/%.hip,$(BUILD)/%.o,$(GPU_SRCS))
 PY_OBJS   := $(patsubst csrc/%.cc,$(BUILD)/%.o,$(PY_SRCS))
 
 EXT := $(PKG)/_native$(EXT_SUFFIX)
-TOOLS := fakegcs read_operation ssd_test write_operations list_operation open_file small_poc loopback_ceiling splice_probe
+TOOLS := fakegcs read_operation ssd_test write_operations list_operation open_file small_poc loopback_ceiling
 TOOL_BINS := $(addprefix $(PKG)/bin/,$(TOOLS))
+# experiment probes (not part of the default build): make probes
+PROBES := splice_probe
+PROBE_BINS := $(addprefix $(PKG)/bin/,$(PROBES))
 
-.PHONY: all clean ext tools asan tsan stress
+.PHONY: all clean ext tools probes asan tsan stress
 all: ext tools
 ext: $(EXT)
 tools: $(TOOL_BINS)
+probes: $(PROBE_BINS)
 
 $(BUILD)/%.o: csrc/%.cc
 	@mkdir -p $(dir $@)
@@ -93,6 +97,6 @@ stress: $(BUILD)/plain/stress
 -include $(patsubst csrc/%.cc,$(BUILD)/asan/%.d,$(SAN_SRCS)) $(patsubst csrc/%.cc,$(BUILD)/tsan/%.d,$(SAN_SRCS))
 
 clean:
-	rm -rf $(BUILD) $(EXT) $(TOOL_BINS)
+	rm -rf $(BUILD) $(EXT) $(TOOL_BINS) $(PROBE_BINS)
 
 -include $(CORE_OBJS:.o=.d) $(GPU_OBJS:.o=.d) $(PY_OBJS:.o=.d)

@@ -519,7 +519,6 @@ def run_rank(args) -> int:
         rv0 = n.recv_stats()
         rd0 = n.recv_diag()
         h2s0 = n.h2_reader_stats()
-        pr0 = n.pipe_relay_stats()
         ep_stats = (endpoint or srv).stats
         sv0 = ep_stats()
         if use_gpu:
@@ -594,18 +593,6 @@ def run_rank(args) -> int:
                     "sndbuf_limited_frac": round((sv1["tcp_sndbuf_limited_us"] - sv0["tcp_sndbuf_limited_us"]) / wall,
                                                  3),
                     "cwnd_kib_at_end": round((sv1["tcp_cwnd_bytes_sum"] - sv0["tcp_cwnd_bytes_sum"]) / sends / 1024, 1)}
-            pr1 = n.pipe_relay_stats()
-            if pr1["relays"] + pr1["no_pipe"] > pr0["relays"] + pr0["no_pipe"]:
-                # multiplexed reads relayed through per-read pipes (storage/pipe_relay.h):
-                # how the payload left the socket
-                d = {k: pr1[k] - pr0[k] for k in pr1}
-                moved = max(1, d["spliced_bytes"] + d["buffered_bytes"] + d["overflow_bytes"])
-                cpu["pipe_relay"] = {"reads": d["relays"], "reads_without_pipe": d["no_pipe"],
-                                     "spliced_frac": round(d["spliced_bytes"] / moved, 4),
-                                     "buffered_frac": round(d["buffered_bytes"] / moved, 4),
-                                     "overflow_frac": round(d["overflow_bytes"] / moved, 4),
-                                     "avg_splice_kib": round(d["spliced_bytes"] / max(1, d["splices"]) / 1024, 1),
-                                     "pipes": pr1["pipes"], "pipe_kib": pr1["pipe_bytes"] // max(1, pr1["pipes"]) // 1024}
             rv1 = n.recv_stats()
             calls = rv1[0] - rv0[0]
             if calls:
@@ -1056,8 +1043,7 @@ def run_rank(args) -> int:
                                for b, e in zip(head["nbytes_per_rank"], head["elapsed_per_rank"])],
             "endpoint": "loopback synthetic GCS (one per rank)",
             # how the endpoint sends object bodies (profiles/r3_thp_send)
-            "endpoint_send": ("sendfile (memfd page cache)" if os.environ.get("GCSB_SRV_SEND") == "sendfile"
-                              else "vmsplice (THP copy of the pattern)"),
+            "endpoint_send": "vmsplice (THP copy of the pattern)",
             # the endpoint sockets' congestion control (GCSB_SRV_CC; the
             # host default is in config.sysctl, profiles/r3_twins/cc)
             "endpoint_congestion_control": os.environ.get("GCSB_SRV_CC") or "cubic",
@@ -1124,8 +1110,6 @@ def run_rank(args) -> int:
                     b["recv_avg_kib"] = st["cpu"]["recv_avg_kib"]
                 if st["cpu"].get("recv_queue"):
                     b["recv_queue"] = st["cpu"]["recv_queue"]
-                if st["cpu"].get("pipe_relay"):
-                    b["pipe_relay"] = st["cpu"]["pipe_relay"]
                 if st["cpu"].get("endpoint_tcp"):
                     b["endpoint_tcp"] = st["cpu"]["endpoint_tcp"]
                 if st["cpu"].get("endpoint_h2"):

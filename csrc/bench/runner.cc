@@ -20,13 +20,9 @@ namespace gcsb {
 namespace {
 // gRPC and HTTP/2 multiplex every worker's stream on shared connections: the
 // host CRC of a discard sink runs on the worker, not the connection's reader
-// (DiscardSink deferred mode).  GCSB_DEFER_CRC=0 keeps it inline (A/B).
+// (DiscardSink deferred mode).
 bool defer_host_crc(const ClientConfig& c) {
-  static const bool on = [] {
-    const char* e = std::getenv("GCSB_DEFER_CRC");
-    return !(e && *e == '0');
-  }();
-  return on && (c.protocol == "grpc" || c.protocol == "http2");
+  return c.protocol == "grpc" || c.protocol == "http2";
 }
 }  // namespace
 
@@ -52,15 +48,6 @@ double percentile_floor(const std::vector<double>& sorted, int pct) {
 Runner::Runner(RunnerConfig cfg) : cfg_(std::move(cfg)) {
   reserve_fd_table();
   if (cfg_.workers <= 0) throw StorageError("worker count not valid", false);
-  if (cfg_.client.splice_recv < 0) {
-    // GCSB_SPLICE_RECV=1: when streams share a connection, its reader only
-    // moves pages and each worker copies its own read (storage/pipe_relay.h).
-    // Off by default: splice() cost the reader as much as the copy it saves
-    // (profiles/r3_splice).
-    const char* e = std::getenv("GCSB_SPLICE_RECV");
-    const bool on = e && *e == '1';
-    cfg_.client.splice_recv = on && cfg_.workers > std::max(1, cfg_.client.grpc_conn_pool_size) ? 1 : 0;
-  }
   client_ = make_client(cfg_.client);
 }
 

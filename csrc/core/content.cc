@@ -39,13 +39,7 @@ uint64_t object_rotation(const std::string& name) {
     h ^= c;
     h *= 0x100000001B3ull;
   }
-  // GCSB_PATTERN_ROT_ALIGN=1: byte-granular rotations (round-2 content), for A/Bs
-  static const uint64_t align = [] {
-    const char* e = std::getenv("GCSB_PATTERN_ROT_ALIGN");
-    const long v = e ? std::atol(e) : 0;
-    return v > 0 ? static_cast<uint64_t>(v) : kPatternRotAlign;
-  }();
-  return h % (kPatternLen / align) * align;
+  return h % (kPatternLen / kPatternRotAlign) * kPatternRotAlign;
 }
 
 PatternBuffer::PatternBuffer() {
@@ -91,14 +85,6 @@ int PatternBuffer::memfd() const {
   }
   memfd_ = fd;
   return memfd_;
-}
-
-bool PatternBuffer::send_by_vmsplice() {
-  static const bool v = [] {
-    const char* e = std::getenv("GCSB_SRV_SEND");
-    return !(e && std::string(e) == "sendfile");
-  }();
-  return v;
 }
 
 const uint8_t* PatternBuffer::thp() const {

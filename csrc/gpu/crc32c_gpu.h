@@ -39,6 +39,28 @@ void launch_crc32c_batch(const CrcBatch& b, const CrcTables* d_tables, uint32_t*
                          CrcSegResult* d_results, hipStream_t stream);
 uint32_t* crc_scratch_alloc(uint64_t tiles);
 
+// Kernel variant selection for launch_crc32c_batch, process-wide.  The
+// defaults are the measured winners; the others stay reachable for kernel
+// A/Bs and their tests (scripts/crc_kernel_bench.py, tests/test_gpu_crc32c.py):
+//   slot_kernel   slot-sized batches (<= kCrcFusedMaxTiles 4 KiB tiles) on
+//                 crc32c_slot_kernel; false = the round-2 fused tile kernel
+//   slot_waves    waves per slot-kernel workgroup (1, 2, 4, 8; 0 = by size)
+//   xor_arrival   slot kernel: 64-bit XOR arrival words per counter group
+//                 (false = per-tile stores + done counters for every batch)
+//   nibble_tables slot kernel: 16-entry nibble tables (fewer LDS bank
+//                 conflicts, more lookups); false = byte tables
+//   mfma          bulk 4 KiB-tile batches on the int8-MFMA tile kernel
+//                 (correct, slower than the table kernel: profiles/r2_crc_mfma)
+struct CrcLaunchOptions {
+  bool slot_kernel = true;
+  int slot_waves = 0;
+  bool xor_arrival = true;
+  bool nibble_tables = false;
+  bool mfma = false;
+};
+void set_crc_launch_options(const CrcLaunchOptions& o);
+CrcLaunchOptions crc_launch_options();
+
 // Pattern kernels (K3): object bytes of the synthetic content (csrc/core/content.h).
 void launch_fill_pattern(uint8_t* dst, uint64_t n, uint64_t rot, uint64_t obj_off, hipStream_t stream);
 // Counts mismatching bytes into *d_count (uint64) and records the first index.

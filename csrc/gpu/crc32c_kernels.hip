@@ -807,35 +807,22 @@ void launch_crc32c_batch(const CrcBatch& b, const CrcTables* d_tables, uint32_t*
   if (blocks == 0) blocks = 1;       // tail-only segments: the fused fold still runs
   const bool fused = b.max_seg_tiles <= kCrcFusedMaxTiles;
   const bool small = b.tile_log2 == static_cast<uint32_t>(kCrcMinTileLog2);
-  static const bool slot_kernel = [] {
-    const char* e = std::getenv("GCSB_CRC_SLOT");  // A/B switch: 0 = round-2 fused tile kernel
-    return !(e && *e == '0');
-  }();
-  if (fused && small && slot_kernel) {
+  const CrcLaunchOptions o = crc_launch_options();
+  if (fused && small && o.slot_kernel) {
     // waves per workgroup: enough workgroups to put a tile on every CU first
     const uint32_t t = b.total_tiles;
-    static const int forced_w = [] {
-      const char* e = std::getenv("GCSB_CRC_SLOT_WAVES");  // A/B: waves per workgroup (1, 2, 4, 8)
-      return e ? std::atoi(e) : 0;
-    }();
     int w = t <= 256 ? 1 : t <= 512 ? 2 : t <= 1024 ? 4 : 8;
-    if (forced_w == 1 || forced_w == 2 || forced_w == 4 || forced_w == 8) w = forced_w;
+    if (o.slot_waves == 1 || o.slot_waves == 2 || o.slot_waves == 4 || o.slot_waves == 8) w = o.slot_waves;
     uint32_t g = (t + w - 1) / w;
     if (g > 2048) g = 2048;
-    static const bool no_xor = [] {
-      const char* e = std::getenv("GCSB_CRC_XOR");  // A/B: 0 = per-tile stores + done counters for every batch
-      return e && *e == '0';
-    }();
+    const bool no_xor = !o.xor_arrival;
     CrcBatch bx;
     if (no_xor) {
       bx = b;
       bx.probe |= 0x100u;
     }
     if (g == 0) g = 1;
-    static const bool nib = [] {
-      const char* e = std::getenv("GCSB_CRC_NIB");  // A/B: 0 = byte tables (bank conflicts), 1 = nibble tables
-      return e && *e == '1';
-    }();
+    const bool nib = o.nibble_tables;
 #define GCSB_SLOT(WV, NB) \
   hipLaunchKernelGGL((crc32c_slot_kernel<WV, NB>), dim3(g), dim3(64 * WV), 0, stream, no_xor ? bx : b, d_tables, \
                      d_scratch, d_results)
@@ -868,10 +855,7 @@ void launch_crc32c_batch(const CrcBatch& b, const CrcTables* d_tables, uint32_t*
     hip_check(hipGetLastError(), "crc32c_tiles_kernel(fused)");
     return;
   }
-  static const bool mfma = [] {
-    const char* e = std::getenv("GCSB_CRC_MFMA");  // int8-MFMA tile CRC for bulk 4 KiB-tile batches
-    return e && *e == '1';
-  }();
+  const bool mfma = o.mfma;
   if (small && mfma) {
     uint32_t g = (b.total_tiles + 3) / 4;
     if (g > 2048) g = 2048;
@@ -885,6 +869,21 @@ void launch_crc32c_batch(const CrcBatch& b, const CrcTables* d_tables, uint32_t*
   hip_check(hipGetLastError(), "crc32c_tiles_kernel");
   hipLaunchKernelGGL(crc32c_fold_kernel, dim3(b.nseg), dim3(kThreads), 0, stream, b, d_tables, d_scratch, d_results);
   hip_check(hipGetLastError(), "crc32c_fold_kernel");
+}
+
+namespace {
+std::mutex g_crc_opt_mu;
+CrcLaunchOptions g_crc_opt;
+}  // namespace
+
+void set_crc_launch_options(const CrcLaunchOptions& o) {
+  std::lock_guard<std::mutex> lk(g_crc_opt_mu);
+  g_crc_opt = o;
+}
+
+CrcLaunchOptions crc_launch_options() {
+  std::lock_guard<std::mutex> lk(g_crc_opt_mu);
+  return g_crc_opt;
 }
 
 uint32_t* crc_scratch_alloc(uint64_t tiles) {

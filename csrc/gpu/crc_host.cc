@@ -75,13 +75,6 @@ uint32_t emulate_mfma_tile_crc(const uint8_t* tile, const MfmaCrcTables& t) {
 
 namespace {
 uint32_t auto_tile_log2(uint64_t total_bytes) {
-  static const uint32_t forced = [] {
-    const char* e = std::getenv("GCSB_CRC_TILE");
-    if (e && std::strcmp(e, "4k") == 0) return uint32_t(kCrcMinTileLog2);
-    if (e && std::strcmp(e, "16k") == 0) return uint32_t(kCrcMaxTileLog2);
-    return 0u;
-  }();
-  if (forced) return forced;
   return total_bytes <= (4u << 20) ? kCrcMinTileLog2 : kCrcMaxTileLog2;
 }
 }  // namespace

@@ -127,8 +127,7 @@ uint32_t emulate_mfma_tile_crc(const uint8_t* tile, const MfmaCrcTables& t);
 void build_crc_tables(CrcTables* t);
 // Fills seg.tile_base/ntiles/fixup, batch.total_tiles/max_seg_tiles and picks
 // the tile size: 4 KiB tiles for batches up to 4 MiB (slot-sized, latency
-// bound), 16 KiB above (bulk).  tile_log2 != 0 forces a size (tests, A/B);
-// GCSB_CRC_TILE=4k|16k overrides the automatic choice.
+// bound), 16 KiB above (bulk).  tile_log2 != 0 forces a size (tests, A/B).
 void finalize_crc_batch(CrcBatch* b, uint32_t tile_log2 = 0);
 // Words of tile scratch (header + tiles) a batch of up to `tiles` tiles needs.
 inline uint64_t crc_scratch_words(uint64_t tiles) { return tiles + kCrcScratchHeader; }

@@ -51,7 +51,7 @@ struct GpuSinkConfig {
   // the copy engine reads them).  The CPU never reads a read sink's ring.
   // Config-3 list-read (8 readers): p50 0.346-0.379 ms against 0.412-0.519
   // with cached THP rings; the one-stream headline showed no gain
-  // (profiles/r3_ring_thp/wc).  Env GCSB_RING_WC=1 forces it for every sink.
+  // (profiles/r3_ring_thp/wc).
   bool ring_wc = false;
   Landing landing = Landing::kObject;
   // Slot hand-off (H2D copy + CRC launch + event) on one per-device
@@ -60,11 +60,11 @@ struct GpuSinkConfig {
   // on the submitter vs ~170 us on a transport thread under HIP runtime lock
   // contention, profiles/r1_markers) come off it: one stream per 256 MiB
   // read 12.5k -> 14.4k MiB/s with 2 MiB slots (profiles/r2_single_stream).
-  // On by default from round 2; env GCSB_ASYNC_SUBMIT=0 turns it off.
+  // On by default from round 2.
   bool async_submit = true;
   // Wait on slot events by blocking (interrupt) instead of spinning: under the
   // GPU box's CPU quota (16 CPUs) spinning waiters steal cycles from the
-  // receiving threads.  Env GCSB_EVENT_SPIN=1 selects spinning.
+  // receiving threads.
   bool blocking_sync = true;
   // > 0: wait for a slot's event by polling it (hipEventQuery) with sleeps of
   // this many microseconds instead of hipEventSynchronize, whose blocking wait
@@ -72,8 +72,7 @@ struct GpuSinkConfig {
   // (a 1 MiB read's last copy + CRC, tens of us) is then all spin, on a core
   // the connection's receiving thread may share.  Config-3 list-read
   // (profiles/r3_w48_tail): worker CPU 0.052 -> 0.024 CPU-s/GiB over gRPC,
-  // 0.23 -> 0.17 over HTTP, same MiB/s.  Env GCSB_WAIT_POLL_US (0 = the
-  // runtime's blocking wait).
+  // 0.23 -> 0.17 over HTTP, same MiB/s.  0 = the runtime's blocking wait.
   int wait_poll_us = 10;
   // Attribution A/B only (scripts/experiments/recv_cost_ab.py): what reads a
   // filled ring slot.  kH2D is the data plane; kNone hands the slot straight
@@ -216,7 +215,7 @@ class GpuByteSource : public ByteSource {
   bool range_crc32c(uint64_t off, size_t len, uint32_t* crc) override;
   uint64_t copies() const { return copies_; }
   uint64_t gpu_range_crcs() const { return range_hits_; }
-  // Objects up to kWholeRingMax (GCSB_UPLOAD_SPLICE, default on) stage into a
+  // Objects up to kWholeRingMax stage into a
   // ring that holds all of them: no slot is refilled during the upload, so
   // the transport can splice the staged pages instead of copying them.
   // Larger objects (or parts) keep the bounded refilling ring of `slots`
@@ -282,8 +281,9 @@ uint32_t gpu_crc32c(int device, const void* dptr, size_t n, size_t chunk = 0,
 // Kernel throughput probe: K1+K2 over [dptr, dptr+n) in segments of
 // seg_bytes (<= kMaxSeg of them), `iters` back-to-back batches, GB/s.
 // tile_log2: 0 = automatic (finalize_crc_batch), 12 / 14 forces 4 / 16 KiB tiles.
+// probe: latency probe of the kernel bench (CrcBatch::probe; 0 = full kernel).
 double gpu_crc32c_throughput(int device, const void* dptr, size_t n, int iters, size_t seg_bytes, uint32_t* crc0,
-                             int tile_log2 = 0);
+                             int tile_log2 = 0, uint32_t probe = 0);
 // Fill / verify device memory with synthetic object bytes.
 void gpu_fill_pattern(int device, void* dptr, uint64_t n, uint64_t rot, uint64_t obj_off);
 uint64_t gpu_verify_pattern(int device, const void* dptr, uint64_t n, uint64_t rot, uint64_t obj_off,

@@ -67,25 +67,13 @@ DeviceCtx& device_ctx(int dev) {
 // Page-locked staging buffers recycled by size (upload rings, per-call
 // sinks): hipHostMalloc of tens of MiB is far slower than the D2H it feeds.
 //
-// Two ways to get page-locked memory (GCSB_RING_ALLOC):
-//   hip  hipHostMalloc(NumaUser): 4 KiB pages;
-//   thp  2 MiB-aligned anonymous memory with MADV_HUGEPAGE, first-touched by
-//        the calling (GPU-local, pinned) thread, then hipHostRegister'ed.  The
-//        receiving core's copy_to_user writes every object byte into these
-//        pages, so 512x fewer TLB misses per slot is on the one-stream
-//        critical path; the SDMA engine reads them through the same IOMMU
-//        mappings either way.
-enum class PinKind { kHip, kThp };
-
-PinKind pin_kind() {
-  static PinKind k = [] {
-    const char* e = std::getenv("GCSB_RING_ALLOC");
-    if (e && std::strcmp(e, "hip") == 0) return PinKind::kHip;
-    if (e && std::strcmp(e, "thp") == 0) return PinKind::kThp;
-    return PinKind::kThp;
-  }();
-  return k;
-}
+// Page-locked memory is 2 MiB-aligned anonymous memory with MADV_HUGEPAGE,
+// first-touched by the calling (GPU-local, pinned) thread, then
+// hipHostRegister'ed.  The receiving core's copy_to_user writes every object
+// byte into these pages, so 512x fewer TLB misses per slot than
+// hipHostMalloc's 4 KiB pages is on the one-stream critical path; the SDMA
+// engine reads them through the same IOMMU mappings either way.
+// hipHostMalloc(NumaUser) is the fallback when registration fails.
 
 // NUMA node of a HIP device's PCIe root (sysfs), -1 if unknown; cached.
 int device_numa_node(int dev) {
@@ -114,16 +102,8 @@ class PinnedPool {
   // n bytes of page-locked memory whose pages sit on NUMA node `node` (the
   // GPU's, which its SDMA engines read / write and its rank's pinned threads
   // run on), -1 = the calling thread's node.  Recycled by (node, size).
-  // GCSB_RING_WC=1: every read sink's ring write-combined (A/B)
-  static bool ring_wc() {
-    static const bool on = [] {
-      const char* e = std::getenv("GCSB_RING_WC");
-      return e && *e == '1';
-    }();
-    return on;
-  }
   // wc: a read sink's ring, which the CPU only writes (the receive copy) and
-  // the copy engine reads; with GCSB_RING_WC=1 it is write-combined memory
+  // the copy engine reads, in write-combined memory
   // (hipHostMallocWriteCombined, not pooled): the copy's stores skip the CPU
   // caches, so there is no read-for-ownership and nothing to write back
   // before the DMA (GpuSinkConfig::ring_wc).  Never for upload staging,
@@ -147,7 +127,7 @@ class PinnedPool {
         return p;
       }
     }
-    if (pin_kind() == PinKind::kThp) {
+    {
       const size_t huge = size_t(2) << 20;
       const size_t len = (n + huge - 1) / huge * huge;
       // a fresh mapping, never touched: malloc'd memory (even 2 MiB-aligned)
@@ -310,12 +290,6 @@ std::vector<int> submitter_cpus() {
   return g_submit_cpus;
 }
 
-bool env_flag(const char* name, bool dflt) {
-  const char* e = std::getenv(name);
-  if (!e || !*e) return dflt;
-  return *e == '1' || *e == 't' || *e == 'T' || *e == 'y' || *e == 'Y';
-}
-
 // One thread per device that issues every queued ring-slot hand-off, so HIP
 // API calls are made by one thread instead of contending from many transport
 // threads.  Jobs run in FIFO order; each job is a few async HIP calls.
@@ -336,22 +310,13 @@ class DeviceSubmitter {
     {
       std::lock_guard<std::mutex> lk(mu_);
       q_.push_back(std::move(f));
-      pending_.store(true, std::memory_order_release);
       wake = sleeping_;
     }
     if (wake) cv_.notify_one();
   }
 
  private:
-  explicit DeviceSubmitter(int dev) : dev_(dev) {
-    // after a hand-off the submitter polls for the next one this long before
-    // it sleeps (env GCSB_SUBMIT_SPIN_US; 0 = sleep at once).  Worth it when
-    // hand-offs come every few tens of us (1 MiB objects on one connection)
-    // and the submitter has a core of its own (placement aux)
-    const char* e = std::getenv("GCSB_SUBMIT_SPIN_US");
-    spin_ns_ = (e ? std::max(0, std::atoi(e)) : 0) * 1000LL;
-    std::thread([this] { loop(); }).detach();
-  }
+  explicit DeviceSubmitter(int dev) : dev_(dev) { std::thread([this] { loop(); }).detach(); }
   void loop() {
     name_current_thread("gcsb-submit");
     // off the receiving core: inherited from the first posting thread (a
@@ -360,12 +325,6 @@ class DeviceSubmitter {
     ensure_device(dev_);
     std::unique_lock<std::mutex> lk(mu_);
     for (;;) {
-      if (q_.empty() && spin_ns_ > 0) {
-        lk.unlock();
-        const int64_t t0 = now_ns();
-        while (!pending_.load(std::memory_order_acquire) && now_ns() - t0 < spin_ns_) __builtin_ia32_pause();
-        lk.lock();
-      }
       if (q_.empty()) {
         sleeping_ = true;
         cv_.wait(lk, [&] { return !q_.empty(); });
@@ -373,18 +332,15 @@ class DeviceSubmitter {
       }
       auto f = std::move(q_.front());
       q_.pop_front();
-      pending_.store(!q_.empty(), std::memory_order_release);
       lk.unlock();
       f();
       lk.lock();
     }
   }
   int dev_;
-  int64_t spin_ns_ = 0;
   std::mutex mu_;
   std::condition_variable cv_;
   std::deque<std::function<void()>> q_;
-  std::atomic<bool> pending_{false};
   bool sleeping_ = false;  // guarded by mu_
 };
 }  // namespace
@@ -457,8 +413,8 @@ class DeviceStreamPool {
     if (const char* e = std::getenv("GCSB_STREAMS")) n = std::max(0, std::min(32, std::atoi(e)));
     ensure_device(dev);
     // every SDMA engine up before the first read / upload can land on a cold
-    // one (gpu/copy_engines.hip); GCSB_WARM_ENGINES=0 leaves them lazy (A/B)
-    if (env_flag("GCSB_WARM_ENGINES", true)) (void)warm_copy_engines(dev);
+    // one (gpu/copy_engines.hip)
+    (void)warm_copy_engines(dev);
     st_.resize(static_cast<size_t>(n));
     for (auto& st : st_) hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate(pool)");
   }
@@ -550,26 +506,17 @@ CopyCeiling copy_ceiling(int device, bool h2d, size_t total, size_t chunk, int s
 void GpuSink::set_device() const { ensure_device(cfg_.device); }
 
 GpuSink::GpuSink(const GpuSinkConfig& cfg) : cfg_(cfg) {
-  cfg_.async_submit = env_flag("GCSB_ASYNC_SUBMIT", cfg_.async_submit);
   if (cfg_.stage != GpuSinkConfig::Stage::kH2D) cfg_.verify = false;
-  if (env_flag("GCSB_EVENT_SPIN", false)) cfg_.blocking_sync = false;
-  if (const char* e = std::getenv("GCSB_WAIT_POLL_US")) cfg_.wait_poll_us = std::max(0, std::atoi(e));
   if (cfg_.slots < 2) cfg_.slots = 2;
   cfg_.slot_bytes = (cfg_.slot_bytes + 4095) / 4096 * 4096;
   if (cfg_.slot_bytes < 65536) cfg_.slot_bytes = 65536;
   set_device();
   DeviceStreamPool& pool = DeviceStreamPool::get(cfg_.device);
   // Slot i of a sink uses pool stream i (slot i's CRC overlaps slot i+1's
-  // copy; the sliced block's 16 sinks spread over all 8).  GCSB_SINK_STREAMS=k
-  // (A/B) alternates a sink's slots over k streams instead: k = 2 kept the
-  // single-stream headline's first-read tail lower in one run after the
-  // bench's torch.cuda.synchronize() and not in three others, and cost the
-  // sliced block 7-9% (profiles/r2_streams_sync), so the default stays.
-  static const int env_nst = [] {
-    const char* e = std::getenv("GCSB_SINK_STREAMS");
-    return e ? std::max(1, std::min(32, std::atoi(e))) : 0;
-  }();
-  const unsigned nst = static_cast<unsigned>(env_nst > 0 ? env_nst : cfg_.slots);
+  // copy; the sliced block's 16 sinks spread over all 8).  Alternating a
+  // sink's slots over 2 streams instead cost the sliced block 7-9% and did
+  // not hold the first-read tail lower (profiles/r2_streams_sync).
+  const unsigned nst = static_cast<unsigned>(cfg_.slots);
   const unsigned base = pool.next_base() * nst;
   if (pool.private_streams())
     hip_check(hipStreamCreateWithFlags(&own_stream_, hipStreamNonBlocking), "hipStreamCreate");
@@ -584,8 +531,7 @@ GpuSink::GpuSink(const GpuSinkConfig& cfg) : cfg_(cfg) {
   for (int i = 0; i < cfg_.slots; ++i) {
     Slot& s = slots_[i];
     // on the GPU's NUMA node (the rank's pinned receive thread runs there too)
-    s.host = static_cast<uint8_t*>(PinnedPool::get(cfg_.slot_bytes, device_numa_node(cfg_.device),
-                                                   cfg_.ring_wc || PinnedPool::ring_wc()));
+    s.host = static_cast<uint8_t*>(PinnedPool::get(cfg_.slot_bytes, device_numa_node(cfg_.device), cfg_.ring_wc));
     if (cfg_.landing == Landing::kRing)
       hip_check(hipMalloc(reinterpret_cast<void**>(&s.dev_ring), cfg_.slot_bytes), "hipMalloc(ring slot)");
     const unsigned evf = hipEventDisableTiming | (cfg_.blocking_sync ? hipEventBlockingSync : 0u);
@@ -596,7 +542,6 @@ GpuSink::GpuSink(const GpuSinkConfig& cfg) : cfg_(cfg) {
     s.res = res_host_ + static_cast<size_t>(i) * kMaxSeg;
     hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&s.d_res), s.res, 0), "hipHostGetDevicePointer");
   }
-  if (env_flag("GCSB_WARM_STREAMS", false)) warm_device_streams(cfg_.device);
 }
 
 GpuSink::~GpuSink() {
@@ -1009,9 +954,7 @@ GpuByteSource::GpuByteSource(int device, const void* dptr, uint64_t n, size_t sl
       // a ring slot never larger than the (part of the) object it stages
       slot_bytes_(std::max<size_t>(std::min<uint64_t>(slot_bytes, (n + 65535) / 65536 * 65536), 65536)),
       nslots_(std::max(2, slots)) {
-  static const bool trace = std::getenv("GCSB_TRACE_SOURCE") != nullptr;  // phase timings (write-tail probe)
-  int64_t tp[5] = {now_ns(), 0, 0, 0, 0};
-  if (env_flag("GCSB_UPLOAD_SPLICE", true) && n_ <= kWholeRingMax)
+  if (n_ <= kWholeRingMax)
     nslots_ = std::max<int>(nslots_, static_cast<int>((n_ + slot_bytes_ - 1) / slot_bytes_));
   hip_check(hipSetDevice(device_), "hipSetDevice");
   DeviceStreamPool& pool = DeviceStreamPool::get(device_);
@@ -1020,13 +963,9 @@ GpuByteSource::GpuByteSource(int device, const void* dptr, uint64_t n, size_t sl
   // after a device-wide synchronize (the bench's torch.cuda.synchronize()
   // around every timed region) the first D2H hipMemcpyAsync on one of the
   // further streams blocked ~7 ms -- the first timed upload's 13.6 ms p99.
-  // With 2 streams: first upload 6.1 ms, p99 6.3 (GCSB_TRACE_SOURCE=1,
-  // scripts/experiments/write_tail.py --gap sync; profiles/r2_write).
-  static const unsigned nst = [] {
-    const char* e = std::getenv("GCSB_UPLOAD_STREAMS");  // A/B: staging streams per upload source
-    const int v = e ? std::atoi(e) : 2;
-    return static_cast<unsigned>(std::max(1, std::min(32, v)));
-  }();
+  // With 2 streams: first upload 6.1 ms, p99 6.3
+  // (scripts/experiments/write_tail.py --gap sync; profiles/r2_write).
+  constexpr unsigned nst = 2;
   // every upload source of the process shares the same nst streams: the 8
   // parts of a parallel composite upload spread over all 8 pool streams had
   // their first upload after the sync at 10.3 ms vs p50 2.7
@@ -1048,7 +987,6 @@ GpuByteSource::GpuByteSource(int device, const void* dptr, uint64_t n, size_t sl
     host_[i] = static_cast<uint8_t*>(PinnedPool::get(slot_bytes_, device_numa_node(device_)));
     ev_[i] = EventPool::get(device_);
   }
-  tp[1] = now_ns();
   if (gpu_crc) {
     // Chunk CRCs on a grid that the transport's upload messages fall on:
     // messages are <= 2 MiB (gRPC MAX_WRITE_CHUNK_BYTES) and never cross a
@@ -1058,15 +996,7 @@ GpuByteSource::GpuByteSource(int device, const void* dptr, uint64_t n, size_t sl
     crc_ = gpu_crc32c(device_, src_, n_, grid_, grid_ ? &chunk_crc_ : nullptr);
     has_crc_ = true;
   }
-  tp[2] = now_ns();
   restart(0);
-  if (trace) {
-    tp[3] = now_ns();
-    hip_check(hipEventSynchronize(ev_[0]), "hipEventSynchronize");
-    tp[4] = now_ns();
-    std::fprintf(stderr, "GpuByteSource: setup %.3f ms, crc %.3f ms, issue %.3f ms, first copy %.3f ms\n",
-                 (tp[1] - tp[0]) / 1e6, (tp[2] - tp[1]) / 1e6, (tp[3] - tp[2]) / 1e6, (tp[4] - tp[3]) / 1e6);
-  }
 }
 
 bool GpuByteSource::range_crc32c(uint64_t off, size_t len, uint32_t* crc) {
@@ -1102,7 +1032,6 @@ void GpuByteSource::wait_all() {
 }
 
 void GpuByteSource::issue(int slot, uint64_t off) {
-  static const bool trace = std::getenv("GCSB_TRACE_SOURCE") != nullptr;
   size_t len = static_cast<size_t>(std::min<uint64_t>(slot_bytes_, n_ - off));
   slot_off_[slot] = off;
   slot_len_[slot] = len;
@@ -1112,9 +1041,6 @@ void GpuByteSource::issue(int slot, uint64_t off) {
   note_hip_call("hipMemcpyAsync(D2H)", st_idx_[slot], t0, t1);
   hip_check(hipEventRecord(ev_[slot], st_[slot]), "hipEventRecord");
   note_hip_call("hipEventRecord(D2H)", st_idx_[slot], t1, now_ns());
-  if (trace && now_ns() - t0 > 200000)
-    std::fprintf(stderr, "GpuByteSource: slow issue slot %d stream %p: copy %.3f ms, event %.3f ms\n", slot,
-                 static_cast<void*>(st_[slot]), (t1 - t0) / 1e6, (now_ns() - t1) / 1e6);
   ++copies_;
 }
 
@@ -1225,7 +1151,7 @@ uint32_t gpu_crc32c(int device, const void* dptr, size_t n, size_t chunk, std::v
 }
 
 double gpu_crc32c_throughput(int device, const void* dptr, size_t n, int iters, size_t seg_bytes, uint32_t* raw0,
-                             int tile_log2) {
+                             int tile_log2, uint32_t probe) {
   hip_check(hipSetDevice(device), "hipSetDevice");
   const CrcTables* tabs = device_crc_tables(device);
   hipStream_t st;
@@ -1243,7 +1169,7 @@ double gpu_crc32c_throughput(int device, const void* dptr, size_t n, int iters, 
     off += len;
   }
   finalize_crc_batch(&b, static_cast<uint32_t>(tile_log2));
-  if (const char* e = std::getenv("GCSB_CRC_PROBE")) b.probe = static_cast<uint32_t>(std::atoi(e));
+  b.probe = probe;
   uint32_t* d_tiles = crc_scratch_alloc(b.total_tiles + 1);
   CrcSegResult* res = nullptr;
   hip_check(hipHostMalloc(reinterpret_cast<void**>(&res), sizeof(CrcSegResult) * kMaxSeg,

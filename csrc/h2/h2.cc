@@ -87,6 +87,14 @@ void FifoLock::lock() {
   t_last_wait_ns = now_ns() - t0;
 }
 
+bool FifoLock::try_lock() {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (held_) return false;
+  held_ = true;
+  t_last_wait_ns = 0;
+  return true;
+}
+
 void FifoLock::unlock() {
   std::lock_guard<std::mutex> lk(mu_);
   if (q_.empty()) {
@@ -115,11 +123,44 @@ void H2Writer::note_data_frame() {
   if (sink_) note_send(*sink_, w);
 }
 
+void H2Writer::release() {
+  for (;;) {
+    std::string pend;
+    {
+      std::lock_guard<std::mutex> lk(ctl_mu_);
+      if (ctl_pending_.empty()) {
+        wmu_.unlock();  // under ctl_mu_: a control frame queued after this check finds wmu_ free
+        return;
+      }
+      pend.swap(ctl_pending_);
+    }
+    try {
+      conn_.write_all(pend.data(), pend.size());
+    } catch (...) {
+      // the connection is gone; its reader fails every stream
+    }
+  }
+}
+
+void H2Writer::write_control(uint8_t type, uint8_t flags, uint32_t stream, const void* p, size_t n) {
+  std::string f(9 + n, '\0');
+  encode_frame_header(reinterpret_cast<uint8_t*>(&f[0]), static_cast<uint32_t>(n), type, flags, stream);
+  if (n) std::memcpy(&f[9], p, n);
+  {
+    std::lock_guard<std::mutex> lk(ctl_mu_);
+    ctl_pending_ += f;
+    // a holder checks ctl_pending_ under ctl_mu_ before it unlocks: either it
+    // sees this frame, or wmu_ is free now and this thread sends it
+    if (!wmu_.try_lock()) return;
+  }
+  release();
+}
+
 void H2Writer::write_frame(uint8_t type, uint8_t flags, uint32_t stream, const void* p, size_t n) {
   uint8_t hdr[9];
   encode_frame_header(hdr, static_cast<uint32_t>(n), type, flags, stream);
   iovec iov[2] = {{hdr, 9}, {const_cast<void*>(p), n}};
-  std::lock_guard<FifoLock> lk(wmu_);
+  WriteLock lk(*this);
   if (type == h2::kData) note_data_frame();
   conn_.writev_all(iov, n ? 2 : 1);
 }
@@ -131,7 +172,7 @@ void H2Writer::write_frame_iov(uint8_t type, uint8_t flags, uint32_t stream, str
   std::vector<iovec> iov(static_cast<size_t>(cnt) + 1);
   iov[0] = {hdr, 9};
   for (int i = 0; i < cnt; ++i) iov[static_cast<size_t>(i) + 1] = payload[i];
-  std::lock_guard<FifoLock> lk(wmu_);
+  WriteLock lk(*this);
   if (type == h2::kData) note_data_frame();
   conn_.writev_all(iov.data(), cnt + 1);
 }
@@ -142,7 +183,7 @@ void H2Writer::write_frame_pieces(uint8_t type, uint8_t flags, uint32_t stream, 
   encode_frame_header(hdr, static_cast<uint32_t>(total), type, flags, stream);
   std::vector<iovec> iov;
   iov.push_back({hdr, 9});
-  std::lock_guard<FifoLock> lk(wmu_);
+  WriteLock lk(*this);
   if (type == h2::kData) note_data_frame();
   for (size_t i = 0; i < pieces.size(); ++i) {
     const SendPiece& p = pieces[i];
@@ -164,7 +205,7 @@ void H2Writer::write_frame_pieces(uint8_t type, uint8_t flags, uint32_t stream, 
 
 void H2Writer::write_headers(uint32_t stream, const std::string& block, bool end_stream) {
   const size_t maxf = peer_max_frame_;
-  std::lock_guard<FifoLock> lk(wmu_);  // HEADERS+CONTINUATION must be contiguous
+  WriteLock lk(*this);  // HEADERS+CONTINUATION must be contiguous
   size_t off = 0;
   bool first = true;
   do {
@@ -194,7 +235,7 @@ bool H2Writer::write_headers_and_data(uint32_t stream, const std::string& block,
   encode_frame_header(hh, static_cast<uint32_t>(block.size()), h2::kHeaders, h2::kFlagEndHeaders, stream);
   encode_frame_header(dh, static_cast<uint32_t>(n), h2::kData, h2::kFlagEndStream, stream);
   iovec iov[4] = {{hh, 9}, {const_cast<char*>(block.data()), block.size()}, {dh, 9}, {const_cast<uint8_t*>(p), n}};
-  std::lock_guard<FifoLock> lk(wmu_);
+  WriteLock lk(*this);
   conn_.writev_all(iov, 4);
   return true;
 }
@@ -202,7 +243,7 @@ bool H2Writer::write_headers_and_data(uint32_t stream, const std::string& block,
 void H2Writer::write_window_update(uint32_t stream, uint32_t inc) {
   uint8_t v[4];
   put_be32(v, inc & 0x7FFFFFFF);
-  write_frame(h2::kWindowUpdate, 0, stream, v, 4);
+  write_control(h2::kWindowUpdate, 0, stream, v, 4);
 }
 
 void H2Writer::write_rst(uint32_t stream, uint32_t code) {

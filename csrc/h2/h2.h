@@ -81,6 +81,7 @@ struct SendPiece {
 class FifoLock {
  public:
   void lock();
+  bool try_lock();  // only when free: never ahead of queued waiters
   void unlock();
   static int64_t last_wait_ns();
 
@@ -131,8 +132,16 @@ class H2Writer {
   void write_rst(uint32_t stream, uint32_t code);
   void write_goaway(uint32_t last_stream, uint32_t code, const std::string& msg);
   void write_settings(const std::string& payload) { write_frame(h2::kSettings, 0, 0, payload.data(), payload.size()); }
-  void write_settings_ack() { write_frame(h2::kSettings, h2::kFlagAck, 0, nullptr, 0); }
-  void write_ping_ack(const uint8_t opaque[8]) { write_frame(h2::kPing, h2::kFlagAck, 0, opaque, 8); }
+  void write_settings_ack() { write_control(h2::kSettings, h2::kFlagAck, 0, nullptr, 0); }
+  void write_ping_ack(const uint8_t opaque[8]) { write_control(h2::kPing, h2::kFlagAck, 0, opaque, 8); }
+  // A control frame from the connection's reader thread (WINDOW_UPDATE,
+  // SETTINGS / PING acks): written now if no frame write is in progress,
+  // else queued for the writer holding the connection to send before it
+  // lets go.  The reader never blocks behind a DATA writer: two peers whose
+  // DATA writers each wait for the other's socket to drain keep reading,
+  // so their queued WINDOW_UPDATEs still go out (a blocked reader on both
+  // ends was a deadlock, made likelier by FIFO hand-off).
+  void write_control(uint8_t type, uint8_t flags, uint32_t stream, const void* p, size_t n);
 
   // --- send flow control ---------------------------------------------------
   // Blocks until the connection and stream windows allow >=1 byte; returns
@@ -150,8 +159,23 @@ class H2Writer {
 
  private:
   void note_data_frame();
+  // Holds wmu_ for one frame write; on release sends the control frames
+  // queued meanwhile (write_control), then unlocks.
+  class WriteLock {
+   public:
+    explicit WriteLock(H2Writer& w) : w_(w) { w_.wmu_.lock(); }
+    ~WriteLock() { w_.release(); }
+    WriteLock(const WriteLock&) = delete;
+    WriteLock& operator=(const WriteLock&) = delete;
+
+   private:
+    H2Writer& w_;
+  };
+  void release();  // flush queued control frames, unlock wmu_
   Conn& conn_;
   FifoLock wmu_;  // frame writes, granted in arrival order
+  std::mutex ctl_mu_;        // guards ctl_pending_; taken before wmu_'s own mutex
+  std::string ctl_pending_;  // encoded control frames waiting for the writer
   size_t quantum_ = 0;
   H2SendStats sstats_;
   H2SendStats* sink_ = nullptr;

@@ -135,8 +135,6 @@ class H2ClientConn {
   // connection.  Either way nothing writes into s's sink afterwards.
   void abandon_stream(H2ClientStream& s, int idle_ms);
   bool usable() const { return !dead_.load() && !goaway_.load(); }
-  // DATA payloads can be splice()d off the socket (plain TCP, not TLS).
-  bool spliceable() const { return bc_ && !bc_->conn().tls(); }
   size_t active_streams();
   const Endpoint& endpoint() const { return ep_; }
   void close();

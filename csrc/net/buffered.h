@@ -64,18 +64,6 @@ class BufferedConn {
     }
     return conn_->read_some(dst, n);
   }
-  // Moves 1..n bytes into the pipe whose (non-blocking) write end is pipe_w:
-  // bytes this buffer already holds are written (copied), the rest is
-  // splice()d from the socket by page reference.  Returns the bytes moved, 0
-  // on orderly EOF, -1 if the pipe is full.  Plain TCP only.
-  ssize_t splice_some(int pipe_w, size_t n) {
-    if (buffered()) {
-      const ssize_t w = pipe_write(pipe_w, buf_.get() + pos_, buffered() < n ? buffered() : n);
-      if (w > 0) pos_ += static_cast<size_t>(w);
-      return w;
-    }
-    return conn_->splice_to_pipe(pipe_w, n);
-  }
   void skip(size_t n) {
     uint8_t tmp[4096];
     while (n) {

@@ -400,33 +400,6 @@ size_t Conn::read_some(void* buf, size_t n) {
   }
 }
 
-ssize_t Conn::splice_to_pipe(int pipe_w, size_t n) {
-  if (fd_ < 0) throw StorageError("read on closed connection", true);
-  if (ssl_) throw StorageError("splice_to_pipe on a TLS connection", false);
-  for (;;) {
-    const ssize_t r = ::splice(fd_, nullptr, pipe_w, nullptr, n, SPLICE_F_MOVE | SPLICE_F_NONBLOCK);
-    if (r >= 0) {
-      bytes_read_ += static_cast<uint64_t>(r);
-      g_recv_calls.fetch_add(1, std::memory_order_relaxed);
-      g_recv_bytes.fetch_add(static_cast<uint64_t>(r), std::memory_order_relaxed);
-      return r;
-    }
-    if (errno == EINTR) continue;
-    if (errno == EAGAIN || errno == EWOULDBLOCK) return -1;  // the pipe is full (the socket blocks)
-    throw StorageError(std::string("splice: ") + std::strerror(errno), true);
-  }
-}
-
-ssize_t pipe_write(int pipe_w, const void* p, size_t n) {
-  for (;;) {
-    const ssize_t w = ::write(pipe_w, p, n);
-    if (w >= 0) return w;
-    if (errno == EINTR) continue;
-    if (errno == EAGAIN || errno == EWOULDBLOCK) return -1;
-    throw StorageError(std::string("pipe write: ") + std::strerror(errno), true);
-  }
-}
-
 size_t Conn::read_some2(void* a, size_t na, void* b, size_t nb) {
   if (ssl_ || nb == 0) return read_some(a, na);
   if (fd_ < 0) throw StorageError("read on closed connection", true);

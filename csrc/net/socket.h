@@ -104,10 +104,6 @@ class Conn {
   // the caller must leave them unchanged until the peer has read the bytes
   // (for an upload: until its final response).  TLS falls back to a copy.
   void splice_user_all(const void* p, size_t n, bool more = false);
-  // Moves 1..n received bytes into a pipe (splice: the socket buffers' pages
-  // by reference, no copy).  pipe_w's side never blocks: -1 if the pipe is
-  // full.  Blocks for data like read_some; 0 = orderly EOF.  Plain TCP only.
-  ssize_t splice_to_pipe(int pipe_w, size_t n);
   void shutdown_write();
   void close();
   int fd() const { return fd_; }
@@ -170,9 +166,6 @@ bool read_tcp_chrono(int fd, TcpChrono* out);
 // leaves the host's default.  The `ceiling` probe's sender uses it too.
 void set_endpoint_congestion_control(int fd);
 const std::string& endpoint_congestion_control();
-// write() into a non-blocking pipe: bytes written, -1 if it is full; throws on
-// other errors.
-ssize_t pipe_write(int pipe_w, const void* p, size_t n);
 // SSL_CTX for a TLS server (throws on bad cert/key); owned by the caller (free_server_tls_ctx).
 void* make_server_tls_ctx(const TlsServer& t);
 void free_server_tls_ctx(void* ctx);

@@ -19,7 +19,6 @@
 #include "h2/hpack.h"
 #include "proto/storage_v2.h"
 #include "server/fakegcs.h"
-#include "storage/pipe_relay.h"
 #include "storage/auth.h"
 #include "storage/client.h"
 #include "storage/sliced.h"
@@ -66,7 +65,6 @@ ClientConfig client_from(const py::dict& d) {
   c.sock.tls_verify = get_or<bool>(d, "tls_verify", true);
   c.sock.tls_ca_file = get_or<std::string>(d, "tls_ca_file", "");
   c.project = get_or<std::string>(d, "project", "gcs-fuse-test");
-  c.splice_recv = get_or<int>(d, "splice_recv", -1);
   if (d.contains("cpus") && !d["cpus"].is_none()) c.cpus = d["cpus"].cast<std::vector<int>>();
   if (d.contains("reader_cpus") && !d["reader_cpus"].is_none())
     c.reader_cpus = d["reader_cpus"].cast<std::vector<int>>();
@@ -547,6 +545,7 @@ class PyServer {
     c.grpc_chunk = get_or<uint64_t>(d, "grpc_chunk", 2u << 20);
     c.sndbuf = get_or<int>(d, "sndbuf", 0);
     c.zero_copy = get_or<bool>(d, "zero_copy", true);
+    c.send_vmsplice = get_or<std::string>(d, "send_source", "vmsplice") != "sendfile";
     c.h2_quantum = get_or<size_t>(d, "h2_quantum", c.h2_quantum);
     c.tls_cert_file = get_or<std::string>(d, "tls_cert_file", "");
     c.tls_key_file = get_or<std::string>(d, "tls_key_file", "");
@@ -868,20 +867,6 @@ PYBIND11_MODULE(_native, m) {
     d["other_ns"] = s.other_ns;
     return d;
   });
-  m.def("pipe_relay_stats", [] {
-    PipeRelayStats s = pipe_relay_stats();
-    py::dict d;
-    d["relays"] = s.relays;
-    d["no_pipe"] = s.no_pipe;
-    d["spliced_bytes"] = s.spliced_bytes;
-    d["splices"] = s.splices;
-    d["buffered_bytes"] = s.buffered_bytes;
-    d["overflow_bytes"] = s.overflow_bytes;
-    d["overflows"] = s.overflows;
-    d["pipes"] = s.pipes;
-    d["pipe_bytes"] = s.pipe_bytes;
-    return d;
-  });
   m.def("slow_hip_calls", [] {
     SlowHipCalls s = slow_hip_calls();
     py::dict d;
@@ -914,7 +899,7 @@ PYBIND11_MODULE(_native, m) {
     c.recv_chunk = get_or<size_t>(d, "recv_chunk", c.recv_chunk);
     c.rcvbuf = get_or<int>(d, "rcvbuf", 0);
     c.zerocopy_send = get_or<bool>(d, "zerocopy_send", true);
-    c.thp_source = get_or<bool>(d, "thp_source", PatternBuffer::send_by_vmsplice());
+    c.thp_source = get_or<bool>(d, "thp_source", true);
     c.ring_pages = get_or<int>(d, "ring_pages", 1);
     if (d.contains("send_cpus")) c.send_cpus = d["send_cpus"].cast<std::vector<int>>();
     if (d.contains("recv_cpus")) c.recv_cpus = d["recv_cpus"].cast<std::vector<int>>();
@@ -956,17 +941,36 @@ PYBIND11_MODULE(_native, m) {
   });
   m.def(
       "gpu_crc32c_throughput",
-      [](int dev, uintptr_t ptr, size_t n, int iters, size_t seg_bytes, int tile_log2) {
+      [](int dev, uintptr_t ptr, size_t n, int iters, size_t seg_bytes, int tile_log2, uint32_t probe) {
         uint32_t c0 = 0;
         double gbs;
         {
           py::gil_scoped_release nogil;
-          gbs = gpu_crc32c_throughput(dev, reinterpret_cast<const void*>(ptr), n, iters, seg_bytes, &c0, tile_log2);
+          gbs = gpu_crc32c_throughput(dev, reinterpret_cast<const void*>(ptr), n, iters, seg_bytes, &c0, tile_log2,
+                                      probe);
         }
         return py::make_tuple(gbs, c0);
       },
       py::arg("device"), py::arg("ptr"), py::arg("n"), py::arg("iters") = 20, py::arg("seg_bytes") = 64u << 20,
-      py::arg("tile_log2") = 0);
+      py::arg("tile_log2") = 0, py::arg("probe") = 0);
+  // CRC kernel variant selection (gpu/crc32c_gpu.h CrcLaunchOptions), for
+  // kernel A/Bs and tests; returns the options now in force
+  m.def("set_crc_options", [](const py::dict& d) {
+    CrcLaunchOptions o = crc_launch_options();
+    o.slot_kernel = get_or<bool>(d, "slot_kernel", o.slot_kernel);
+    o.slot_waves = get_or<int>(d, "slot_waves", o.slot_waves);
+    o.xor_arrival = get_or<bool>(d, "xor_arrival", o.xor_arrival);
+    o.nibble_tables = get_or<bool>(d, "nibble_tables", o.nibble_tables);
+    o.mfma = get_or<bool>(d, "mfma", o.mfma);
+    set_crc_launch_options(o);
+    py::dict r;
+    r["slot_kernel"] = o.slot_kernel;
+    r["slot_waves"] = o.slot_waves;
+    r["xor_arrival"] = o.xor_arrival;
+    r["nibble_tables"] = o.nibble_tables;
+    r["mfma"] = o.mfma;
+    return r;
+  }, py::arg("options") = py::dict());
   m.def("gpu_read_bytes",[](int dev, uintptr_t ptr, size_t n) {
     std::string out(n, '\0');
     {

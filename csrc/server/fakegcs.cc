@@ -58,11 +58,11 @@ void FakeGcsServer::start() {
   // The THP send source (PatternBuffer::thp, the default) is placed the
   // same way: by first touch on the pinned builder thread.
   if (cfg_.zero_copy) {
-    auto build = [] {
-      if (!PatternBuffer::send_by_vmsplice() || !PatternBuffer::instance().thp()) PatternBuffer::instance().memfd();
+    const bool send_vmsplice = cfg_.send_vmsplice;
+    auto build = [send_vmsplice] {
+      if (!send_vmsplice || !PatternBuffer::instance().thp()) PatternBuffer::instance().memfd();
     };
-    const char* e = std::getenv("GCSB_MEMFD_PINNED");  // A/B switch: 0 = build on the caller's thread
-    if (cfg_.cpus.empty() || (e && *e == '0')) {
+    if (cfg_.cpus.empty()) {
       build();
     } else {
       std::thread([this, &build] {
@@ -134,12 +134,6 @@ void FakeGcsServer::accept_loop() {
 void FakeGcsServer::handle_conn(int fd) {
   SocketOptions so;
   so.sndbuf = cfg_.sndbuf;
-  // GCSB_SRV_SNDBUF: an explicit send buffer for every endpoint connection (A/B)
-  static const int env_sndbuf = [] {
-    const char* e = std::getenv("GCSB_SRV_SNDBUF");
-    return e ? std::atoi(e) : 0;
-  }();
-  if (env_sndbuf > 0) so.sndbuf = env_sndbuf;
   set_endpoint_congestion_control(fd);
   so.rcvbuf = 0;
   if (tls_ctx_) {

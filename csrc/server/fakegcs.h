@@ -42,7 +42,11 @@ struct ServerConfig {
   std::string jwt_public_key_pem;  // verify JWT assertions at /token if set
   uint64_t grpc_chunk = 2 << 20;   // ReadObjectResponse content bytes per message (reference main.go:123-124)
   int sndbuf = 0;          // 0 = kernel autotuning (an explicit size disables it)
-  bool zero_copy = true;   // sendfile() synthetic object bodies from a memfd
+  bool zero_copy = true;   // synthetic object bodies by page reference (no user-space copy)
+  // ...from the pattern's THP copy by vmsplice + splice (default), or, false,
+  // by sendfile() from its memfd (rounds 1-3; also the fallback when THP
+  // memory cannot be had): profiles/r3_splice/thp_source
+  bool send_vmsplice = true;
   std::vector<int> cpus;   // pin connection/handler threads (empty = unpinned)
   // HTTP/2: DATA frame cap while several streams share a connection, so
   // their frames interleave round-robin (H2Writer::set_quantum; 0 = off)

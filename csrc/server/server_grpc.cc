@@ -109,29 +109,13 @@ struct ServerStream {
 };
 
 // WriteObject messages are CRC32C-checked off the connection's reader thread,
-// on a write worker fed GCSB_SRV_WRITE_BUFS (default 2) pooled THP message
-// buffers in rotation; GCSB_SRV_WRITE_WORKER=0 checks them inline on the
-// reader (A/B).  Measured (profiles/r3_write): with 8 heap buffers the
+// on a write worker fed 2 pooled THP message buffers in rotation.  Measured
+// (profiles/r3_write): with 8 heap buffers the
 // reader's receive copy got MORE expensive than receive + CRC inline (0.09
 // vs 0.08 CPU-s/GiB, 16 MiB of 4 KiB-page destinations cycling out of cache);
 // with 2 THP buffers the reader drops to 0.043 - 0.059 and single-stream
 // uploads ran 15.4k - 22.2k MiB/s against 11.6k - 12.4k inline.
-bool write_worker_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("GCSB_SRV_WRITE_WORKER");
-    return !(e && *e == '0');
-  }();
-  return on;
-}
-
-size_t write_worker_bufs() {
-  static const size_t n = [] {
-    const char* e = std::getenv("GCSB_SRV_WRITE_BUFS");
-    const long v = e ? std::atol(e) : 2;
-    return static_cast<size_t>(std::max(1L, std::min(64L, v)));
-  }();
-  return n;
-}
+constexpr size_t kWriteWorkerBufs = 2;
 
 struct Cancelled {};
 
@@ -207,7 +191,7 @@ class H2ServerConn {
               n -= 1 + pad;
             }
             auto s = find(fh.stream);
-            const bool offload = s && s->path == "WriteObject" && write_worker_enabled();
+            const bool offload = s && s->path == "WriteObject";
             if (s) {
               if (offload)
                 recv_write_data(s, n);
@@ -348,7 +332,7 @@ class H2ServerConn {
   // Reader thread: n bytes of a WriteObject stream's DATA.  Each gRPC message
   // is recv()'d straight into a buffer of its own; complete messages go to
   // the connection's write worker (decode, CRC32C check, append), in order.
-  // At most GCSB_SRV_WRITE_BUFS messages wait per connection: past that the
+  // At most kWriteWorkerBufs messages wait per connection: past that the
   // reader blocks, which stalls the socket and so the sender (backpressure).
   void recv_write_data(const std::shared_ptr<ServerStream>& sp, uint32_t n) {
     ServerStream& s = *sp;
@@ -383,7 +367,7 @@ class H2ServerConn {
   static constexpr uint32_t kMaxWriteMessage = 64u << 20;
   HugeBuffer take_write_buffer(size_t len) {
     std::unique_lock<std::mutex> lk(wmu_);
-    wcv_.wait(lk, [&] { return wqueued_ < write_worker_bufs() || wstop_; });
+    wcv_.wait(lk, [&] { return wqueued_ < kWriteWorkerBufs || wstop_; });
     for (size_t i = 0; i < wfree_.size(); ++i)
       if (wfree_[i].capacity() >= len) {
         HugeBuffer b = std::move(wfree_[i]);
@@ -431,7 +415,7 @@ class H2ServerConn {
       }
       lk.lock();
       wfree_.push_back(std::move(j.buf));
-      if (wfree_.size() > write_worker_bufs()) wfree_.erase(wfree_.begin());
+      if (wfree_.size() > kWriteWorkerBufs) wfree_.erase(wfree_.begin());
       --wqueued_;
       --j.s->wpending;
       wcv_.notify_all();
@@ -754,7 +738,8 @@ class H2ServerConn {
         if (n - k - 1) pieces.push_back(mem(p + k + 1, n - k - 1));
         ++srv_.stats().faults_injected;
         corrupt = -1;
-      } else if (const uint8_t* sp = srv_.config().zero_copy ? o.splice_bytes(off, n) : nullptr) {
+      } else if (const uint8_t* sp = srv_.config().zero_copy && srv_.config().send_vmsplice ? o.splice_bytes(off, n)
+                                                                                                : nullptr) {
         SendPiece fp = mem(sp, n);
         fp.splice = true;  // THP pages by reference (PatternBuffer::thp)
         pieces.push_back(fp);
@@ -845,7 +830,9 @@ class H2ServerConn {
         if (n - k - 1) pieces.push_back(mem(p + k + 1, n - k - 1));
         ++srv_.stats().faults_injected;
         corrupt = -1;
-      } else if (const uint8_t* sp = (n && srv_.config().zero_copy) ? o->splice_bytes(off, n) : nullptr) {
+      } else if (const uint8_t* sp = (n && srv_.config().zero_copy && srv_.config().send_vmsplice)
+                                         ? o->splice_bytes(off, n)
+                                         : nullptr) {
         SendPiece fp = mem(sp, n);
         fp.splice = true;  // THP pages by reference (PatternBuffer::thp)
         pieces.push_back(fp);

@@ -314,12 +314,8 @@ class Http1Handler {
     // body would cost the many-small-reads blocks a few % of a core
     TcpChrono chrono0;
     const bool chrono_ok = len >= kChronoMinBody && read_tcp_chrono(c_.fd(), &chrono0);
-    // bytes per send call (GCSB_SRV_HTTP_PIECE, A/B; kPatternExt at most)
-    static const uint64_t piece_max = [] {
-      const char* e = std::getenv("GCSB_SRV_HTTP_PIECE");
-      const long long v = e ? std::atoll(e) : 0;
-      return v >= 4096 && v <= static_cast<long long>(kPatternExt) ? static_cast<uint64_t>(v) : uint64_t(8) << 20;
-    }();
+    // bytes per send call (1-16 MiB measured equal, profiles/r3_twins/http_piece)
+    constexpr uint64_t piece_max = uint64_t(8) << 20;
     while (sent < len) {
       uint64_t off = start + sent;
       uint64_t n = std::min<uint64_t>(piece_max, len - sent);
@@ -363,7 +359,7 @@ class Http1Handler {
       }
       int ffd = -1;
       uint64_t foff = 0;
-      if (const uint8_t* sp = srv_.config().zero_copy ? o.splice_bytes(off, n) : nullptr)
+      if (const uint8_t* sp = srv_.config().zero_copy && srv_.config().send_vmsplice ? o.splice_bytes(off, n) : nullptr)
         c_.splice_user_all(sp, n);  // THP pattern pages by reference, no copy
       else if (srv_.config().zero_copy && o.file_range(off, &ffd, &foff))
         c_.sendfile_all(ffd, foff, n);  // page references, no user-space copy

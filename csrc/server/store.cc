@@ -48,7 +48,7 @@ const uint8_t* StoredObject::bytes(uint64_t off, uint64_t n) const {
 }
 
 const uint8_t* StoredObject::splice_bytes(uint64_t off, uint64_t n) const {
-  if (!synthetic || !PatternBuffer::send_by_vmsplice()) return nullptr;
+  if (!synthetic) return nullptr;
   const PatternBuffer& pb = PatternBuffer::instance();
   const uint8_t* t = pb.thp();
   if (!t) return nullptr;

@@ -41,12 +41,6 @@ struct ClientConfig {
   // multiplexed connection's one reader receives every stream's bytes, so it
   // gets a physical core the workers do not share (affinity.isolate_reader)
   std::vector<int> reader_cpus;
-  // gRPC / HTTP/2 reads: the connection's reader splice()s payloads into a
-  // per-read pipe and the read's own thread copies them out
-  // (storage/pipe_relay.h).  -1 = the runner decides: on with
-  // GCSB_SPLICE_RECV=1 when it puts more streams than connections on the
-  // client (a multiplexed connection); off by default (profiles/r3_splice).
-  int splice_recv = -1;
 };
 
 struct ObjectMeta {

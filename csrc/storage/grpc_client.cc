@@ -23,7 +23,6 @@
 #include "proto/storage_v2.h"
 #include "proto/wire.h"
 #include "storage/client.h"
-#include "storage/pipe_relay.h"
 
 namespace gcsb {
 namespace {
@@ -202,15 +201,8 @@ class GrpcCall : public H2ClientStream {
     if (handler_error_.empty()) handler_error_ = msg;
   }
 
-  // A sink error found on the worker's thread (PipeRelay replay): the call
-  // fails with it once the stream is over; the reader keeps consuming.
-  void set_error(const std::string& msg) {
-    std::lock_guard<std::mutex> lk(mu_);
-    if (handler_error_.empty()) handler_error_ = msg;
-  }
-
   // The reader thread has queued work for the waiting worker (a deferred
-  // sink's message end, a relayed payload piece): wake it.
+  // sink's message end): wake it.
   void poke() {
     std::lock_guard<std::mutex> lk(mu_);
     poked_ = true;
@@ -290,11 +282,9 @@ class ReadObjectHandler : public MessageHandler {
   // cap: the most bytes *delivered may reach in this read (ranged reads);
   // a server sending past read_limit is a protocol error, never written into
   // the sink (a piece sink's neighbour in HBM belongs to another stream).
-  // relay: the payload is fed through it (sink is the relay then), see
-  // storage/pipe_relay.h
   ReadObjectHandler(Sink& sink, ReadResult* rr, uint64_t* delivered, bool full_read, GrpcCall** call,
-                    uint64_t cap = ~0ull, PipeRelay* relay = nullptr)
-      : sink_(sink), rr_(rr), delivered_(delivered), full_read_(full_read), call_(call), cap_(cap), relay_(relay) {}
+                    uint64_t cap = ~0ull)
+      : sink_(sink), rr_(rr), delivered_(delivered), full_read_(full_read), call_(call), cap_(cap) {}
 
   void begin(uint32_t len) override {
     msg_left_ = len;
@@ -312,19 +302,6 @@ class ReadObjectHandler : public MessageHandler {
       if (st_ == kContent) {
         uint64_t k = std::min<uint64_t>(n, content_left_);
         if (*delivered_ + k > cap_) throw StorageError("ReadObject: server sent more than read_limit bytes", false);
-        while (relay_ && k > 0) {
-          // pages into the read's pipe; its worker copies them (and is woken
-          // per piece, so its copy overlaps the rest of the frame arriving)
-          const size_t m = relay_->feed(bc, static_cast<size_t>(k));
-          if (m == 0) throw StorageError("connection closed inside a DATA frame", true);
-          if (!rr_->first_byte_ns) rr_->first_byte_ns = now_ns();
-          *delivered_ += m;
-          consume(static_cast<uint32_t>(m));
-          n -= static_cast<uint32_t>(m);
-          content_left_ -= m;
-          k -= m;
-          if (*call_) (*call_)->poke();
-        }
         while (k > 0) {
           Window w;
           if (!sink_failed_) {
@@ -553,7 +530,6 @@ class ReadObjectHandler : public MessageHandler {
   bool full_read_;
   GrpcCall** call_;
   uint64_t cap_ = ~0ull;
-  PipeRelay* relay_ = nullptr;
   St st_ = kTopTag;
   uint64_t msg_left_ = 0, cd_left_ = 0, content_left_ = 0, skip_left_ = 0, fbuf_len_ = 0;
   bool in_cd_ = false, content_seen_ = false, has_crc_ = false;
@@ -672,30 +648,18 @@ class GrpcStorageClient : public StorageClient {
     q.generation = rr->pin_generation;
     GrpcCall* raw = nullptr;
     auto c = conn();
-    std::unique_ptr<PipeRelay> relay;
-    if (cfg_.splice_recv > 0 && c->spliceable()) {
-      relay = std::make_unique<PipeRelay>(sink);
-      if (!relay->usable()) relay.reset();  // no pipe to be had: the reader copies, as before
-    }
-    Sink& hs = relay ? static_cast<Sink&>(*relay) : sink;
-    ReadObjectHandler h(hs, rr, delivered, full, &raw, limit >= 0 ? *delivered + limit : ~0ull, relay.get());
+    ReadObjectHandler h(sink, rr, delivered, full, &raw, limit >= 0 ? *delivered + limit : ~0ull);
     auto call = std::make_shared<GrpcCall>(&h);
     raw = call.get();
-    if (relay) relay->set_on_error([raw](const std::string& m) { raw->set_error(m); });
     std::string f = frame(v2::encode_read_request(q));
     try {
       c->start_stream_with_body(call, headers("ReadObject", q.bucket), f);
-      call->wait_ok(hs.deferred() ? &hs : nullptr, idle_ms_, [c, call, this] { c->abandon_stream(*call, idle_ms_); });
+      call->wait_ok(sink.deferred() ? &sink : nullptr, idle_ms_, [c, call, this] { c->abandon_stream(*call, idle_ms_); });
     } catch (...) {
       c->end_stream(*call, true);
-      // the reader is out of this stream (it completed, or abandon_stream
-      // waited it out / closed the connection): replay what it relayed, so the
-      // sink stands at the delivered offset a retry resumes from
-      if (relay) relay->settle();
       throw;
     }
     c->end_stream(*call, false);
-    if (relay) relay->settle();
     if (h.sink_failed()) throw StorageError("sink: " + h.sink_error(), false);
   }
 
@@ -770,12 +734,8 @@ class GrpcStorageClient : public StorageClient {
     auto call = std::make_shared<GrpcCall>(&h);
     auto c = conn();
     // zero-copy send of the content (vmsplice + splice) when the source's
-    // bytes stay put until the final response; GCSB_UPLOAD_SPLICE=0 copies
-    static const bool splice_on = [] {
-      const char* e = std::getenv("GCSB_UPLOAD_SPLICE");
-      return !(e && *e == '0');
-    }();
-    const bool splice = splice_on && src.stable_until_done();
+    // bytes stay put until the final response
+    const bool splice = src.stable_until_done();
     constexpr size_t kMinSplice = 64 << 10;  // below this a copy is cheaper than 2 syscalls
     c->start_stream(call, headers("WriteObject", bucket_res), false);
     try {

@@ -12,7 +12,6 @@
 #include "core/util.h"
 #include "h2/h2_client.h"
 #include "http1/http1.h"
-#include "storage/pipe_relay.h"
 #include "storage/client.h"
 
 namespace gcsb {
@@ -72,15 +71,9 @@ ObjectInfo media_info(int status, int64_t content_length, int64_t offset, Get ge
 // the rest of the body skipped; the caller rethrows after completion.
 class H2MediaGet : public H2ClientStream {
  public:
-  // relay: body bytes are fed through it (sink is the relay then), see
-  // storage/pipe_relay.h
-  H2MediaGet(Sink& sink, ReadResult* rr, uint64_t* delivered, int64_t offset, int64_t limit, bool first_attempt,
-             PipeRelay* relay = nullptr)
+  H2MediaGet(Sink& sink, ReadResult* rr, uint64_t* delivered, int64_t offset, int64_t limit, bool first_attempt)
       : sink_(sink), rr_(rr), delivered_(delivered), offset_(offset), limit_(limit), first_(first_attempt),
-        cap_total_(limit >= 0 ? *delivered + static_cast<uint64_t>(limit) : ~0ull), relay_(relay) {}
-
-  // A sink error met on the worker's thread (PipeRelay replay).
-  void relay_error(const std::string& msg) { fail(msg, false); }
+        cap_total_(limit >= 0 ? *delivered + static_cast<uint64_t>(limit) : ~0ull) {}
 
   void on_headers(const HeaderList& h, bool end_stream) override {
     if (!got_head_) {
@@ -144,15 +137,6 @@ class H2MediaGet : public H2ClientStream {
           if (!failed_.load()) fail("http2 GET: server sent more than the requested range", false);
           bc.skip(n);
           break;
-        }
-        if (relay_) {
-          const size_t m = relay_->feed(bc, std::min<uint64_t>(n, cap_total_ - *delivered_));
-          if (m == 0) throw StorageError("connection closed inside a DATA frame", true);
-          if (!rr_->first_byte_ns) rr_->first_byte_ns = now_ns();
-          *delivered_ += m;
-          n -= static_cast<uint32_t>(m);
-          poke();
-          continue;
         }
         Window w;
         try {
@@ -255,7 +239,6 @@ class H2MediaGet : public H2ClientStream {
   bool done_ = false, retryable_ = false, poked_ = false;
   uint64_t unpoked_ = 0;
   std::string error_;
-  PipeRelay* relay_ = nullptr;
 };
 
 class HttpStorageClient : public StorageClient {
@@ -320,14 +303,7 @@ class HttpStorageClient : public StorageClient {
     }
     h.emplace_back("x-goog-api-client", "gccl/1.33.0 gcsb-native");
     auto c = h2_conn();
-    std::unique_ptr<PipeRelay> relay;
-    if (cfg_.splice_recv > 0 && c->spliceable()) {
-      relay = std::make_unique<PipeRelay>(sink);
-      if (!relay->usable()) relay.reset();
-    }
-    auto call = std::make_shared<H2MediaGet>(relay ? static_cast<Sink&>(*relay) : sink, rr, delivered, offset, limit,
-                                             first_attempt, relay.get());
-    if (relay) relay->set_on_error([raw = call.get()](const std::string& m) { raw->relay_error(m); });
+    auto call = std::make_shared<H2MediaGet>(sink, rr, delivered, offset, limit, first_attempt);
     std::string body;
     int status = 0;
     try {
@@ -336,11 +312,9 @@ class HttpStorageClient : public StorageClient {
       status = call->wait(&body, idle, [c, call, idle] { c->abandon_stream(*call, idle); });
     } catch (...) {
       c->end_stream(*call, true);
-      if (relay) relay->settle();  // (see the gRPC read_attempt)
       throw;
     }
     c->end_stream(*call, false);
-    if (relay) relay->settle();
     if (status != 200 && status != 206) throw_status(status, "GET " + bucket + "/" + object, body);
   }
 

@@ -77,12 +77,23 @@ int main(int argc, char** argv) {
   for (int i = 0; i < nobj; ++i) store->add_synthetic(bucket, "obj_" + std::to_string(i), (3u << 20) + 4097 * i);
   store->add_synthetic(bucket, "big", 12u << 20);
 
-  // multiplexed reads relayed through per-read pipes (storage/pipe_relay.h):
-  // the connection's reader splices, each worker replays into its sink;
-  // plus a mid-stream disconnect so a relay is settled on the retry path
+  // the endpoint's sendfile() send source (ServerConfig::send_vmsplice off):
+  // concurrent reads over every transport
+  {
+    ServerConfig sf;
+    sf.send_vmsplice = false;
+    FakeGcsServer srv2(sf, store);
+    srv2.start();
+    for (const char* proto : {"http", "grpc"}) {
+      auto cli = make_client(client_cfg(proto, srv2.url()));
+      readers(*cli, bucket, nobj, 4, 2);
+    }
+    srv2.stop();
+  }
+
+  // multiplexed reads, plus a mid-stream disconnect on the retry path
   for (const char* proto : {"http2", "grpc"}) {
     ClientConfig rc = client_cfg(proto, srv.url());
-    rc.splice_recv = 1;
     auto cli = make_client(rc);
     readers(*cli, bucket, nobj, 6, 3 * scale);
     srv.faults().disconnect_at = (2 << 20) + 5;

@@ -10,7 +10,7 @@ name themselves (csrc/core/affinity.h name_current_thread):
   gcsb-slice      sliced-read receive threads (slices 1..n-1)
   gcsb-wslice     parallel-composite upload part threads
   gcsb-h2-reader  HTTP/2 connection reader (gRPC receive path)
-  gcsb-submit     per-device slot hand-off thread (GCSB_ASYNC_SUBMIT=1)
+  gcsb-submit     per-device slot hand-off thread (GpuSinkConfig::async_submit)
   gcsb-srv-*      synthetic endpoint (connection / RPC handler / accept)
 
 Everything else (HIP runtime threads, Python) is grouped by its own name.

@@ -45,34 +45,23 @@ def test_fill_and_verify_pattern(native, gpu_available):
     assert bad == 1 and first == 12345
 
 
-_VARIANT_CHILD = r"""
-import os, sys
-import torch
-import custom_go_client_benchmark_amd as pkg
-n = pkg._native
-for size, mis in [(4096 * 600 + 5, 3), (4 << 20, 0), ((2 << 20) + 13, 7), (17, 1)]:
-    data = os.urandom(size)
-    buf = torch.zeros(size + 64, dtype=torch.uint8, device="cuda:0")
-    buf[mis:mis + size] = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
-    torch.cuda.synchronize()
-    got = n.gpu_crc32c(0, buf.data_ptr() + mis, size)
-    if got != n.crc32c(data):
-        print("MISMATCH", size, mis, file=sys.stderr)
-        sys.exit(1)
-print("ok")
-"""
+@pytest.mark.parametrize("opts", [{"slot_waves": 1}, {"xor_arrival": False}, {"slot_waves": 8},
+                                  {"nibble_tables": True}, {"slot_kernel": False}, {"mfma": True}])
+def test_crc_kernel_variants(native, gpu_available, opts):
+    """Every CRC kernel variant (gpu/crc32c_gpu.h CrcLaunchOptions) against
+    the host CRC32C.  One wave per workgroup on 600 - 1024 tiles puts more
+    than 32 workgroups in a counter group, which takes the stored-tile
+    epilogue instead of the 64-bit XOR arrival words."""
+    import torch
 
-
-@pytest.mark.parametrize("env", [{"GCSB_CRC_SLOT_WAVES": "1"}, {"GCSB_CRC_XOR": "0"}, {"GCSB_CRC_SLOT_WAVES": "8"}])
-def test_slot_kernel_epilogue_variants(gpu_available, env):
-    # The launch-time switches are read once per process, so each variant
-    # runs in a child.  One wave per workgroup on 600 - 1024 tiles puts more
-    # than 32 workgroups in a counter group, which takes the stored-tile
-    # epilogue instead of the 64-bit XOR arrival words.
-    import subprocess
-    import sys
-
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    r = subprocess.run([sys.executable, "-c", _VARIANT_CHILD], cwd=root, env={**os.environ, **env},
-                       capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+    defaults = native.set_crc_options({})
+    try:
+        native.set_crc_options(opts)
+        for size, mis in [(4096 * 600 + 5, 3), (4 << 20, 0), ((2 << 20) + 13, 7), (17, 1), ((9 << 20) + 5, 0)]:
+            data = os.urandom(size)
+            buf = torch.zeros(size + 64, dtype=torch.uint8, device="cuda:0")
+            buf[mis:mis + size] = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+            torch.cuda.synchronize()
+            assert native.gpu_crc32c(0, buf.data_ptr() + mis, size) == native.crc32c(data), (opts, size, mis)
+    finally:
+        native.set_crc_options(defaults)

@@ -1,4 +1,4 @@
-"""The endpoint's zero-copy send paths (GCSB_SRV_SEND): synthetic object
+"""The endpoint's zero-copy send paths (Server config send_source): synthetic object
 bodies leave by vmsplice from the pattern's THP copy (default) or by sendfile
 from its memfd.  Both must put the same bytes on the wire, over HTTP/1.1,
 gRPC and HTTP/2, with faults still cutting in at the right byte
@@ -17,7 +17,7 @@ sys.path.insert(0, %(root)r)
 import custom_go_client_benchmark_amd as pkg
 n = pkg._native
 B, P = "b", "princer_100M_files/file_"
-srv = n.Server({"port": 0})
+srv = n.Server({"port": 0, "send_source": %(mode)r})
 srv.start()
 size = (5 << 20) + 4097
 srv.add_synthetic(B, P, "", 0, 2, size)
@@ -38,8 +38,8 @@ print("nodes", n.pattern_memfd_numa())
 
 @pytest.mark.parametrize("mode", ["vmsplice", "sendfile"])
 def test_send_paths_put_the_same_bytes_on_the_wire(mode):
-    env = dict(os.environ, GCSB_SRV_SEND=mode, GCSB_NO_TORCH="1")
-    r = subprocess.run([sys.executable, "-c", SCRIPT % {"root": ROOT}], env=env, capture_output=True, text=True,
+    env = dict(os.environ, GCSB_NO_TORCH="1")
+    r = subprocess.run([sys.executable, "-c", SCRIPT % {"root": ROOT, "mode": mode}], env=env, capture_output=True, text=True,
                        timeout=180)
     assert r.returncode == 0, r.stderr[-3000:]
     # the send source exists and its pages were counted (THP copy or memfd)

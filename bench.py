@@ -319,6 +319,14 @@ def build_parser() -> argparse.ArgumentParser:
                     help="comma list of side blocks to run (A/B sessions): cpu_baseline, compare, sliced, ceiling, "
                          "ref_default, c1_http_cpu, list_read, write, write_composite, fanout; 'all' = every block; empty = "
                          "all at N = 1, cpu_baseline,compare,write,fanout at N > 1")
+    ap.add_argument("--client-cc", default="cubic",
+                    help="client sockets' TCP congestion control, set before connect (\"\" = the host default, BBR "
+                         "on the GPU boxes, whose internal pacing arms an hrtimer per 64 KiB skb of an upload on a "
+                         "loopback link: profiles/r4_recvcost). Every block uses it, baselines included")
+    ap.add_argument("--read-diag", action="store_true",
+                    help="per-read stall attribution (Runner read_diag): scheduler and softirq deltas of the "
+                         "receiving / sending threads around every timed read; the slowest reads carry them and a "
+                         "named cause (rank0_slowest_diag). Costs tens of us per read outside its latency")
     ap.add_argument("--side-deadline", type=float, default=300.0,
                     help="seconds the side blocks after the headline + cpu_baseline may take before rank 0 prints "
                          "the headline line measured so far and exits 3 (0 = no limit)")
@@ -473,6 +481,8 @@ def run_rank(args) -> int:
         "blocking_sync": args.event_wait == "block",
         "async_submit": bool(args.async_submit),
         "rcvbuf": parse_size(args.rcvbuf),
+        "read_diag": bool(args.read_diag),
+        "tcp_congestion": args.client_cc,
     }
     # the sliced extension: inline slot hand-off (r1_submit_ab), 2 MiB x 8
     # ring per sink (profiles/r2_sliced)
@@ -631,6 +641,15 @@ def run_rank(args) -> int:
         # this rank's slowest reads [index in the timed run, ms, host-landed ms,
         # TTFB ms] and the slot hand-off HIP calls that blocked (>= 1 ms)
         st["slowest"] = [[int(x[0])] + [round(v, 3) for v in x[1:]] for x in (s1.get("slowest") or [])]
+        if s1.get("slowest_diag"):
+            # per slow read: what the scheduler / softirqs did meanwhile, and the named cause
+            st["slowest_diag"] = [
+                {"read": int(x[0]), "ms": round(x[1], 3),
+                 "cause": sysdiag.attribute(dg, x[1], s1["p50_ms"]),
+                 "threads": {k: {f: (round(v, 3) if isinstance(v, float) else v) for f, v in row.items()}
+                             for k, row in dg["threads"].items()},
+                 "softirqs": dg["softirqs"]}
+                for x, dg in zip(s1["slowest"], s1["slowest_diag"])]
         st["slow_hip"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in slow_hip.items()}
         return st
 
@@ -682,9 +701,11 @@ def run_rank(args) -> int:
             # between otherwise identical runs)
             if sh["client"]:
                 os.sched_setaffinity(0, sh["client"])
-            client = n.Client({"protocol": protocol, "endpoint": ep.url, "retry_initial_s": 0.05})
+            client = n.Client({"protocol": protocol, "endpoint": ep.url, "retry_initial_s": 0.05,
+                               "tcp_congestion": args.client_cc})
             if parts > 1:
                 client = n.SlicedWriter({"protocol": protocol, "endpoint": ep.url, "retry_initial_s": 0.05,
+                                         "tcp_congestion": args.client_cc,
                                          "slices": parts, "slice_min_bytes": 1 << 20, "cpus": sh["client"]})
             buf = torch.empty(wsize, dtype=torch.uint8, device=f"cuda:{gpu}")
             n.gpu_fill_pattern(gpu, buf.data_ptr(), wsize, f"upload/rank{rank}", 0)
@@ -756,6 +777,7 @@ def run_rank(args) -> int:
             srv.add_synthetic(bucket, "fanout/obj_", "", 0, 1, size)
             want = srv.object_info(bucket, name)["crc32c"]
             client = n.Client({"protocol": protocol, "endpoint": srv.url, "retry_initial_s": 0.05,
+                               "tcp_congestion": args.client_cc,
                                "cpus": placement["client"], "rcvbuf": parse_size(args.rcvbuf)})
             full = torch.empty(size, dtype=torch.uint8, device=f"cuda:{gpu}" if use_gpu else "cpu")
             # this rank's slice lands in place: the all-gather's input is the
@@ -1047,6 +1069,7 @@ def run_rank(args) -> int:
             # the endpoint sockets' congestion control (GCSB_SRV_CC; the
             # host default is in config.sysctl, profiles/r3_twins/cc)
             "endpoint_congestion_control": os.environ.get("GCSB_SRV_CC") or "cubic",
+            "client_congestion_control": args.client_cc or "host default",
             "affinity": aff,
             "placement": {k: placement.get(k) for k in ("client", "server", "aux", "picked_by", "busy")
                           if placement.get(k) is not None},
@@ -1081,6 +1104,8 @@ def run_rank(args) -> int:
             out["host_landed_p50_ms"] = round(head["host_p50_max"], 3)
             out["verified_reads"] = int(head["verified_sum"])
             out["rank0_cpu"] = head["cpu"]
+            if head.get("slowest_diag"):
+                out["rank0_slowest_diag"] = head["slowest_diag"]
             out["rank0_slowest"] = head.get("slowest", [])
             if head.get("slow_hip"):
                 out["slow_hip_calls"] = head["slow_hip"]

@@ -99,6 +99,7 @@ void Runner::reset_stats() {
   host_ms_.clear();
   ttfb_ms_.clear();
   ttfb_by_read_.clear();
+  diag_by_read_.clear();
   first_ms_.clear();
   steady_ms_.clear();
   pending_.clear();
@@ -152,6 +153,7 @@ void Runner::record(ReadRecord&& r, double ms, double host_ms) {
     host_ms_.push_back(host_ms);
     if (r.ttfb_ns > r.start_ns) ttfb_ms_.push_back((r.ttfb_ns - r.start_ns) / 1e6);
     ttfb_by_read_.push_back(r.ttfb_ns > r.start_ns ? (r.ttfb_ns - r.start_ns) / 1e6 : 0.0);
+    diag_by_read_.push_back(r.diag);
     // metric semantics: integer-truncated milliseconds (reference main.go:146)
     acc_.oc_buckets[oc_bucket_index(std::floor(ms))]++;
   }
@@ -242,6 +244,11 @@ void Runner::worker_main(int w) {
       // OTel TraceIDRatioBased: lower 8 bytes of the trace id >> 1 < rate * 2^63
       r.sampled = cfg_.trace_sample_rate >= 1.0 || (r.trace_lo >> 1) < sample_bound;
     }
+    // receiving (h2 reader / HTTP worker), sending (endpoint), submitter
+    static const std::vector<std::string> kDiagThreads = {"gcsb-h2-reader", "gcsb-srv", "gcsb-worker",
+                                                          "gcsb-submit", "gcsb-slice"};
+    SchedSample diag0;
+    if (cfg_.read_diag) diag0 = sched_sample(kDiagThreads);
     RoctxRange rg(sliced ? "gcsb.read_object(sliced)" : "gcsb.read_object");
     r.start_wall_ns = wall_ns();
     r.start_ns = now_ns();
@@ -270,6 +277,7 @@ void Runner::worker_main(int w) {
       r.end_ns = now_ns();
       r.error = e.what();
     }
+    if (cfg_.read_diag) r.diag = std::make_shared<ReadSchedDiag>(sched_delta(diag0, sched_sample(kDiagThreads)));
     ms = (r.end_ns - r.start_ns) / 1e6;
     host_ms = r.host_done_ns ? (r.host_done_ns - r.start_ns) / 1e6 : ms;
     if (r.ok && cfg_.latency_fd >= 0) {
@@ -328,6 +336,7 @@ RunSummary Runner::summary() const {
     for (size_t j = 0; j < k; ++j) {
       const size_t i = idx[j];
       s.slowest.push_back({static_cast<double>(i), lat_ms_[i], host_ms_[i], ttfb_by_read_[i]});
+      if (i < diag_by_read_.size() && diag_by_read_[i]) s.slowest_diag.push_back(*diag_by_read_[i]);
     }
   }
   std::vector<double> v = lat_ms_;

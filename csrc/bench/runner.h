@@ -23,6 +23,7 @@
 #include <thread>
 #include <vector>
 
+#include "core/sched_probe.h"
 #include "gpu/engine.h"
 #include "storage/client.h"
 #include "storage/sliced.h"
@@ -63,6 +64,12 @@ struct RunnerConfig {
   uint64_t slice_piece_bytes = 0;
   uint64_t slice_piece_min_bytes = 0;  // >0: tapered pieces down to this (storage/sliced.h)
   uint64_t seed = 0;
+  // Per-read stall attribution (core/sched_probe.h): a scheduler / softirq
+  // sample of the receiving, sending, worker and submitter threads before
+  // each read's timer starts and after it stops; the slowest reads keep
+  // their deltas (RunSummary::slowest_diag).  Off by default: ~tens of us
+  // per read, outside the read's latency but inside the run's wall time.
+  bool read_diag = false;
 };
 
 struct ReadRecord {
@@ -76,6 +83,7 @@ struct ReadRecord {
   bool ok = false, verified = false, sampled = false;
   uint64_t trace_hi = 0, trace_lo = 0, span_id = 0;
   std::string error;
+  std::shared_ptr<ReadSchedDiag> diag;  // RunnerConfig::read_diag
 };
 
 struct RunSummary {
@@ -94,6 +102,7 @@ struct RunSummary {
   uint64_t oc_buckets[kOcBuckets] = {0};
   // the 3 slowest reads: {index in completion order, ms, host-landed ms, TTFB ms}
   std::vector<std::vector<double>> slowest;
+  std::vector<ReadSchedDiag> slowest_diag;  // aligned with slowest (read_diag runs)
   std::string first_error;
   GpuSinkStats gpu;
 };
@@ -140,6 +149,7 @@ class Runner {
   std::vector<ReadRecord> pending_;
   std::vector<double> lat_ms_, host_ms_, ttfb_ms_, first_ms_, steady_ms_;
   std::vector<double> ttfb_by_read_;  // per ok read, in completion order (0 if unknown)
+  std::vector<std::shared_ptr<ReadSchedDiag>> diag_by_read_;  // aligned with lat_ms_ (read_diag)
   RunSummary acc_;
   double worker_cpu_s_ = 0;  // guarded by mu_
   int64_t t_first_ = 0, t_last_ = 0;

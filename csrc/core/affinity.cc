@@ -1,4 +1,5 @@
 #include "core/affinity.h"
+#include "core/sched_probe.h"
 
 #include <pthread.h>
 #include <sched.h>
@@ -87,6 +88,7 @@ void name_current_thread(const char* name) {
   char buf[16];
   std::snprintf(buf, sizeof(buf), "%s", name);
   pthread_setname_np(pthread_self(), buf);
+  register_named_thread(buf);  // core/sched_probe.h
 }
 
 std::vector<int> cpus_for(const std::vector<int>& cpus, int k, bool spread) {

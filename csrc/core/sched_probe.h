@@ -1,0 +1,60 @@
+// Per-read stall attribution: what took the
+// receiving or the sending core away from one read.
+//
+// Every named thread of the process (core/affinity.h name_current_thread)
+// is registered here with its tid.  A sample reads, for each registered
+// thread whose name matches, the scheduler's view (/proc/self/task/<tid>/
+// schedstat: on-CPU and run-queue wait time; status: voluntary and
+// involuntary context switches; stat: the CPU it last ran on), and
+// /proc/softirqs for the CPUs those threads ran on.  The runner takes one
+// sample before a read's timer starts and one after it stops
+// (RunnerConfig::read_diag), so the cost (tens of microseconds) stays
+// outside every read's latency, and keeps the deltas of its slowest reads.
+//
+// Reference timed region: /root/reference/main.go:133-145.
+#pragma once
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+namespace gcsb {
+
+// Called by name_current_thread: remembers (tid, name).
+void register_named_thread(const char* name);
+
+struct ThreadSched {
+  int tid = 0;
+  std::string name;
+  uint64_t cpu_ns = 0, delay_ns = 0;  // schedstat: on-CPU, waiting on a run queue
+  uint64_t nvcsw = 0, nivcsw = 0;     // context switches: voluntary (blocked), involuntary (preempted)
+  int cpu = -1;                       // last CPU
+};
+
+struct SchedSample {
+  int64_t t_ns = 0;
+  std::vector<ThreadSched> threads;
+  // softirq counts per CPU of interest: {cpu: {"NET_RX": n, "HRTIMER": n, ...}}
+  std::map<int, std::map<std::string, uint64_t>> softirqs;
+};
+
+// Threads whose name starts with one of `prefixes`; softirqs of the CPUs
+// they last ran on.
+SchedSample sched_sample(const std::vector<std::string>& prefixes);
+
+// One read's deltas between two samples, per thread name (summed over
+// threads of that name): run-queue delay, involuntary switches, CPU time,
+// and the softirqs on the CPUs the receiving / sending threads used.
+struct ReadSchedDiag {
+  struct Row {
+    double cpu_ms = 0, delay_ms = 0;
+    uint64_t nivcsw = 0, nvcsw = 0;
+    std::vector<int> cpus;
+  };
+  std::map<std::string, Row> threads;                      // by thread name
+  std::map<std::string, uint64_t> softirqs;                // on those CPUs, by kind
+  double wall_ms = 0;
+};
+ReadSchedDiag sched_delta(const SchedSample& a, const SchedSample& b);
+
+}  // namespace gcsb

@@ -81,6 +81,9 @@ void apply_socket_options(int fd, const SocketOptions& opt) {
   if (opt.nodelay) setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
   if (opt.rcvbuf > 0) setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &opt.rcvbuf, sizeof(opt.rcvbuf));
   if (opt.sndbuf > 0) setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &opt.sndbuf, sizeof(opt.sndbuf));
+  if (!opt.congestion.empty())
+    (void)setsockopt(fd, IPPROTO_TCP, TCP_CONGESTION, opt.congestion.data(),
+                     static_cast<socklen_t>(opt.congestion.size()));
   if (opt.io_timeout_ms > 0) {
     timeval tv{opt.io_timeout_ms / 1000, (opt.io_timeout_ms % 1000) * 1000};
     setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));

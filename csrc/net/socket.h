@@ -42,6 +42,12 @@ struct SocketOptions {
   bool tls_verify = true;
   std::string tls_ca_file;
   std::string alpn;
+  // TCP congestion control of client sockets, set before connect() so the
+  // connection never runs the host default's init ("" = host default).
+  // BBR (the GPU boxes' default) marks a socket for internal pacing: on a
+  // loopback link every 64 KiB skb of an upload then waits on an hrtimer
+  // (profiles/r4_recvcost).
+  std::string congestion;
 };
 
 // Server-side TLS context from PEM files (fake GCS endpoint over https);

@@ -62,6 +62,7 @@ ClientConfig client_from(const py::dict& d) {
   c.sock.rcvbuf = get_or<int>(d, "rcvbuf", 0);
   c.sock.sndbuf = get_or<int>(d, "sndbuf", 0);
   c.sock.io_timeout_ms = get_or<int>(d, "io_timeout_ms", 0);
+  c.sock.congestion = get_or<std::string>(d, "tcp_congestion", "");
   c.sock.tls_verify = get_or<bool>(d, "tls_verify", true);
   c.sock.tls_ca_file = get_or<std::string>(d, "tls_ca_file", "");
   c.project = get_or<std::string>(d, "project", "gcs-fuse-test");
@@ -128,6 +129,25 @@ py::dict meta_dict(const ObjectMeta& m) {
   r["content_type"] = m.content_type;
   r["updated"] = m.updated;
   return r;
+}
+
+// A read's scheduler / softirq deltas (core/sched_probe.h), per thread name.
+py::dict sched_diag_dict(const ReadSchedDiag& x) {
+  py::dict d, th, si;
+  for (const auto& [name, r] : x.threads) {
+    py::dict row;
+    row["cpu_ms"] = r.cpu_ms;
+    row["run_delay_ms"] = r.delay_ms;
+    row["nivcsw"] = r.nivcsw;
+    row["nvcsw"] = r.nvcsw;
+    row["cpus"] = r.cpus;
+    th[py::str(name)] = row;
+  }
+  for (const auto& [k, v] : x.softirqs) si[py::str(k)] = v;
+  d["threads"] = th;
+  d["softirqs"] = si;
+  d["wall_ms"] = x.wall_ms;
+  return d;
 }
 
 py::dict gpu_stats_dict(const GpuSinkStats& g) {
@@ -444,6 +464,7 @@ class PyRunner {
     c.gpu = gpu_from(d);
     c.latency_fd = get_or<int>(d, "latency_fd", -1);
     c.keep_records = get_or<bool>(d, "keep_records", true);
+    c.read_diag = get_or<bool>(d, "read_diag", false);
     c.stop_on_error = get_or<bool>(d, "stop_on_error", true);
     c.trace_sample_rate = get_or<double>(d, "trace_sample_rate", 0.0);
     c.range_offset = get_or<int64_t>(d, "range_offset", 0);
@@ -514,6 +535,9 @@ class PyRunner {
     d["steady_p99_ms"] = s.steady_p99_ms;
     d["slice_skew_ms"] = s.slice_skew_ms;
     d["slowest"] = s.slowest;
+    py::list sd;
+    for (const ReadSchedDiag& x : s.slowest_diag) sd.append(sched_diag_dict(x));
+    d["slowest_diag"] = sd;
     d["worker_cpu_s"] = s.worker_cpu_s;
     py::list b;
     for (int i = 0; i < kOcBuckets; ++i) b.append(s.oc_buckets[i]);

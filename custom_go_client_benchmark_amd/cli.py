@@ -87,6 +87,9 @@ def build_flags() -> FlagSet:
     fs.string("key-file", "", "Service-account JSON key (-auth key_file)")
     fs.string("token-uri", "", "Override the key file's token_uri")
     fs.string("user-agent", "prince", "User-Agent (reference userAgentRoundTripper)")
+    fs.string("tcp-congestion", "", "Client sockets' TCP congestion control, set before connect (\"\" = the "
+              "host default; with -start-fake-server: cubic, which avoids BBR's per-skb pacing timers on a "
+              "loopback link)")
     fs.string("tls-ca-file", "", "PEM CA bundle for https endpoints (default: system roots)")
     fs.bool("tls-insecure", False, "Skip TLS certificate verification (test endpoints only)")
     fs.duration("retry-initial", 1.0, "Initial backoff (gax default 1s)")
@@ -249,7 +252,9 @@ def main(argv: list[str] | None = None) -> int:
         tls_verify=not fs.get("tls-insecure"), retry_initial_s=fs.get("retry-initial"),
         retry_max_s=fs.get("retry-max"), retry_multiplier=fs.get("retry-multiplier"),
         retry_max_total_s=fs.get("retry-max-total"), retry_max_attempts=fs.get("retry-max-attempts"),
-        read_timeout_s=fs.get("read-timeout"))
+        read_timeout_s=fs.get("read-timeout"),
+        # a node-local synthetic endpoint is a loopback link: cubic unless set
+        tcp_congestion=fs.get("tcp-congestion") or ("cubic" if fs.get("start-fake-server") else ""))
 
     # tracing (reference main.go:162-165)
     tracer, trace_cleanup = None, None

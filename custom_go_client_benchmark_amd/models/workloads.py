@@ -54,6 +54,7 @@ class RunOptions:
     retry_max_total_s: float = 0.0
     retry_max_attempts: int = 0
     read_timeout_s: float = 0.0            # idle limit per read (0 = none, as the reference's Timeout: 0)
+    tcp_congestion: str = ""               # client sockets' congestion control ("" = host default)
     object_names: list | None = None
     keep_records: bool = True
     slices: int = 1                        # >1: sliced (parallel ranged) reads, see csrc/storage/sliced.h
@@ -72,6 +73,7 @@ class RunOptions:
             "retry_max_attempts": self.retry_max_attempts, "cpus": list(self.cpus),
             "io_timeout_ms": int(round(self.read_timeout_s * 1000)),
             "tls_ca_file": self.tls_ca_file, "tls_verify": self.tls_verify,
+            "tcp_congestion": self.tcp_congestion,
         }
 
     def runner_dict(self) -> dict:

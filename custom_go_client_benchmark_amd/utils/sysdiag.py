@@ -152,6 +152,39 @@ def table_delta(a: tuple, b: tuple, cpus: list[int] | None, reads: int = 1, top:
             "by_cpu_per_read": {str(c): round(v / r, 2) for c, v in sorted(by_cpu.items())}}
 
 
+def attribute(diag: dict, ms: float, p50_ms: float) -> str:
+    """A slow read's likely cause from its scheduler / softirq deltas
+    (Runner read_diag, core/sched_probe.h): run-queue delay of the receiving
+    thread (h2 reader, or the HTTP worker) or of the endpoint's sender,
+    preemptions, a timer-softirq storm on their CPUs, or -- none of those --
+    a receive copy that simply took longer on the CPU."""
+    th = diag.get("threads", {})
+    excess = max(ms - p50_ms, 1e-6)
+    recv = th.get("gcsb-h2-reader") or th.get("gcsb-worker") or {}
+    send = {"cpu_ms": 0.0, "run_delay_ms": 0.0, "nivcsw": 0}
+    for k, v in th.items():
+        if k.startswith("gcsb-srv"):
+            for f in send:
+                send[f] += v.get(f, 0)
+    causes = []
+    for label, row in (("receiving thread", recv), ("endpoint sender", send)):
+        if row and row.get("run_delay_ms", 0.0) >= 0.2 * excess:
+            causes.append(f"{label} waited {row['run_delay_ms']:.2f} ms for a CPU "
+                          f"({row.get('nivcsw', 0)} preemptions)")
+    soft = diag.get("softirqs", {})
+    if soft.get("HRTIMER", 0) >= 100:
+        causes.append(f"{soft['HRTIMER']} HRTIMER softirqs on the busy CPUs (pacing timers)")
+    if not causes and recv:
+        busy = recv.get("cpu_ms", 0.0) / max(diag.get("wall_ms", ms), 1e-6)
+        if busy >= 0.9:
+            causes.append(f"receiving thread on-CPU {recv['cpu_ms']:.2f} of {ms:.2f} ms: the receive copy itself "
+                          f"ran slower (no scheduler delay, no timer storm)")
+        else:
+            causes.append(f"receiving thread idle {ms - recv.get('cpu_ms', 0.0):.2f} ms without run-queue delay: "
+                          f"waiting for data (sender {send['cpu_ms']:.2f} ms on CPU)")
+    return "; ".join(causes) or "no cause found"
+
+
 class Window:
     """Snapshot everything at construction; .report(cpus, reads) after the
     timed region."""

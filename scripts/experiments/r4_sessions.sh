@@ -50,6 +50,7 @@ recvcost2)  # profiles/r4_recvcost/after_listener_cc: the same A/B once the endp
   step ab 400 python3 -u scripts/experiments/recv_cost_ab.py --tag listener_cc
   step mux 400 python3 -u scripts/experiments/mux_fair_ab.py
   step bench 600 python3 bench.py --json-out "$O/bench.json"
+  step diag100 400 python3 bench.py --steps 100 --warmup 3 --side-steps 0 --read-diag --json-out "$O/diag100.json"
   ;;
 *)
   echo "unknown session $S"

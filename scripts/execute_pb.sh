@@ -7,7 +7,8 @@
 #   ./scripts/execute_pb.sh <exp_number>
 #
 # Extra benchmark flags come from $GCSB_ARGS (default: a node-local synthetic
-# endpoint, since the benchmark boxes have no network).  Results go to
+# endpoint, since the benchmark boxes have no network); a %p in them becomes
+# the run's protocol (e.g. -summary-json sum_%p.json).  Results go to
 # $GCSB_RESULTS_URI with `gsutil cp` when gsutil exists (reference target
 # gs://princer-working-dirs/), otherwise they are copied to $GCSB_RESULTS_DIR.
 set -e
@@ -27,10 +28,10 @@ upload() {
 
 grpc_file="grpc_${exp}.txt"
 # shellcheck disable=SC2086
-"$here/gcsbench" -client-protocol grpc $args | tr 'ms' ' ' > "$grpc_file"
+"$here/gcsbench" -client-protocol grpc ${args//%p/grpc} | tr 'ms' ' ' > "$grpc_file"
 upload "$grpc_file"
 
 http_file="http_${exp}.txt"
 # shellcheck disable=SC2086
-"$here/gcsbench" -client-protocol http $args | tr 'ms' ' ' > "$http_file"
+"$here/gcsbench" -client-protocol http ${args//%p/http} | tr 'ms' ' ' > "$http_file"
 upload "$http_file"

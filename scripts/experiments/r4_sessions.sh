@@ -52,6 +52,9 @@ recvcost2)  # profiles/r4_recvcost/after_listener_cc: the same A/B once the endp
   step bench 600 python3 bench.py --json-out "$O/bench.json"
   step diag100 400 python3 bench.py --steps 100 --warmup 3 --side-steps 0 --read-diag --json-out "$O/diag100.json"
   ;;
+soak)  # profiles/r4_soak: execute_pb.sh with 48 workers x 100 MiB, -sink gpu, 120 s per protocol, exporter at 30 s
+  step soak 900 python3 -u scripts/soak.py --out "$O" --duration 120s
+  ;;
 *)
   echo "unknown session $S"
   exit 2

@@ -575,10 +575,11 @@ def run_rank(args) -> int:
                                     "other_s_per_gib": round(d["other_ns"] / 1e9 / g, 4),
                                     "avg_data_frame_kib": round(d["data_bytes"] / max(1, d["data_frames"]) / 1024, 1)}
             g1 = s1.get("gpu") or {}
-            if g1.get("slot_waits"):
-                # the receiving thread's time reusing ring slots (wait for the
-                # slot's hand-off + its event, harvest its CRC results)
-                cpu["slot_reuse"] = {"waits": g1["slot_waits"],
+            if g1.get("slot_waits") or g1.get("flag_reuses"):
+                # the receiving thread reusing ring slots: on the CRC kernel's
+                # host-visible status (no HIP call), or waiting for the slot's
+                # hand-off + its event; then harvesting its CRC results
+                cpu["slot_reuse"] = {"waits": g1["slot_waits"], "on_kernel_status": g1.get("flag_reuses", 0),
                                      "s_per_gib": round(g1["slot_wait_s"] / max(float(s1["bytes"]) / (1 << 30), 1e-9), 4)}
             sv1 = ep_stats()
             if sv1.get("h2_data_frames", 0) > sv0.get("h2_data_frames", 0):

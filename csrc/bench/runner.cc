@@ -308,6 +308,7 @@ void Runner::worker_main(int w) {
       t.objects_verified += g.objects_verified;
       t.slot_waits += g.slot_waits;
       t.slot_wait_s += g.slot_wait_s;
+      t.flag_reuses += g.flag_reuses;
     }
     std::lock_guard<std::mutex> lk(mu_);
     gpu_stats_[w] = t;
@@ -388,6 +389,7 @@ RunSummary Runner::summary() const {
     s.gpu.objects_verified += g.objects_verified;
     s.gpu.slot_waits += g.slot_waits;
     s.gpu.slot_wait_s += g.slot_wait_s;
+    s.gpu.flag_reuses += g.flag_reuses;
   }
   return s;
 }

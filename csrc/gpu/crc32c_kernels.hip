@@ -230,6 +230,16 @@ __device__ __forceinline__ uint32_t fold_tail(uint32_t byte, int r, uint32_t raw
   return x ^ (r < 4 ? raw >> (8 * r) : 0u);
 }
 
+// Result store for (host-mapped) result slots: raw / crc first, then, after
+// a system-scope fence, the status word the host polls (kCrcStatusPending).
+__device__ __forceinline__ void store_result(CrcSegResult* o, const CrcSegResult& r) {
+  o->raw = r.raw;
+  o->crc = r.crc;
+  o->pad = 0;
+  __threadfence_system();
+  __hip_atomic_store(&o->status, r.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __device__ __forceinline__ CrcSegResult seg_result(const CrcSeg& sg, uint32_t raw) {
   const uint32_t crc = raw ^ sg.fixup;
   CrcSegResult r;
@@ -337,7 +347,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_tiles_kernel(const CrcBatch b
       const CrcSeg& sg = b.seg[g];
       uint32_t raw = fold_wave<true>(sg, tiles, s_tab + kSliceWords + kTreeWords + kGapWords, lane);
       raw = add_tail(sg, raw, sl, lane);
-      if (lane == 0) out[g] = seg_result(sg, raw);
+      if (lane == 0) store_result(out + g, seg_result(sg, raw));
     }
     if (threadIdx.x == 0) __hip_atomic_store(scratch, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -477,7 +487,7 @@ __global__ __launch_bounds__(64 * W) void crc32c_slot_kernel(const CrcBatch b, c
     __syncthreads();
     if (!s_last || probe == 3 || wave != 0) return;
     const uint32_t raw = fold_tail<kNib>(tail_b, tail_r, s_raw, s_sl, lane);
-    if (lane == 0) out[0] = seg_result(b.seg[0], raw);
+    if (lane == 0) store_result(out + 0, seg_result(b.seg[0], raw));
     return;
   }
   // this workgroup's stores complete before it counts itself done
@@ -521,7 +531,7 @@ __global__ __launch_bounds__(64 * W) void crc32c_slot_kernel(const CrcBatch b, c
     for (int k = 0; k < static_cast<int>(kCrcFusedMaxTiles / 64); ++k) acc ^= v[k];
     uint32_t raw = xor_over_lanes(acc, 64);
     raw = fold_tail<kNib>(tb, r, raw, s_sl, lane);
-    if (lane == 0) out[g] = seg_result(sg, raw);
+    if (lane == 0) store_result(out + g, seg_result(sg, raw));
   }
 }
 
@@ -702,7 +712,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_fold_kernel(const CrcBatch b,
     }
     uint32_t raw = __shfl(p, 0, 64);
     raw = add_tail(sg, raw, s_tab, lane);
-    if (lane == 0) out[g] = seg_result(sg, raw);
+    if (lane == 0) store_result(out + g, seg_result(sg, raw));
   }
 }
 

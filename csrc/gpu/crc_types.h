@@ -63,9 +63,15 @@ struct CrcBatch {
 struct CrcSegResult {
   uint32_t raw;
   uint32_t crc;
-  uint32_t status;  // 0 not checked, 1 match, 2 mismatch
+  uint32_t status;  // 0 not checked, 1 match, 2 mismatch; kCrcStatusPending until the kernel stores it
   uint32_t pad;
 };
+// A segment's status before its kernel stored the result: the kernels store
+// raw / crc, fence at system scope, then status, so a host that sees a
+// status other than this in host-mapped results also sees raw / crc -- and
+// knows the slot's copy (ordered before the kernel on its stream) has landed
+// (GpuSink: slot reuse without a HIP call on the receiving thread).
+constexpr uint32_t kCrcStatusPending = 0xFFFFFFFFu;
 
 // Int8-MFMA tile CRC (crc32c_mfma_tiles_kernel): CRC over GF(2) is linear, so
 // the raw CRCs of 32 interleaved "chunks" of a 4 KiB tile (chunk n = the 16-byte

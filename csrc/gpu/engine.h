@@ -91,6 +91,7 @@ struct GpuSinkStats {
   uint64_t objects_verified = 0;
   uint64_t slot_waits = 0;            // transport had to wait for a free slot
   double slot_wait_s = 0;
+  uint64_t flag_reuses = 0;           // slots reused on the kernel's host-visible status (no HIP call)
 };
 
 class GpuSink : public Sink {
@@ -147,7 +148,9 @@ class GpuSink : public Sink {
     hipEvent_t ev = nullptr;      // slot done: copy landed + CRC kernel finished
     uint32_t* tiles = nullptr;    // this slot's CRC tile scratch (slots on different streams run concurrently)
     bool inflight = false;
-    bool submitted = false;       // async: the submitter has recorded `ev` (guarded by sub_mu_)
+    // hand-offs posted to the submitter (receiving thread) / issued by it
+    // (guarded by sub_mu_): the slot's event is current when they match
+    uint64_t posted = 0, issued = 0;
     CrcSegResult* res = nullptr;  // host-mapped, kMaxSeg entries
     CrcSegResult* d_res = nullptr;  // device alias of res
   };
@@ -157,6 +160,7 @@ class GpuSink : public Sink {
   Slot& take_slot();
   void submit_current();
   void wait_slot(Slot& s);
+  bool done_by_flags(const Slot& s) const;
   void wait_event(hipEvent_t ev);
   void harvest(Slot& s);
   uint32_t shift(uint32_t v, uint64_t nbytes);

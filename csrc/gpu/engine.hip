@@ -631,8 +631,24 @@ void GpuSink::update_info(const ObjectInfo& info) {
   }
 }
 
+// The slot's CRC kernel stored every segment's status in host-mapped memory
+// (kCrcStatusPending otherwise): the kernel ran after the slot's H2D copy on
+// its stream, so the pinned slot is free to refill and its results are final
+// -- known without a HIP call (hipEventQuery) on the receiving thread.
+bool GpuSink::done_by_flags(const Slot& s) const {
+  if (!cfg_.verify || s.segs.empty() || cfg_.stage != GpuSinkConfig::Stage::kH2D) return false;
+  for (size_t i = 0; i < s.segs.size(); ++i)
+    if (__atomic_load_n(&s.res[i].status, __ATOMIC_ACQUIRE) == kCrcStatusPending) return false;
+  return true;
+}
+
 GpuSink::Slot& GpuSink::take_slot() {
   Slot& s = slots_[next_];
+  if (s.inflight && done_by_flags(s)) {
+    s.inflight = false;
+    ++stats_.flag_reuses;
+    harvest(s);
+  }
   if (s.inflight) {
     ++stats_.slot_waits;
     int64_t t0 = now_ns();
@@ -765,6 +781,7 @@ void GpuSink::submit_current() {
     finalize_crc_batch(&b);
     if (b.total_tiles > tiles_cap_) throw std::logic_error("CRC tile scratch too small");
     stats_.segments += s.segs.size();
+    for (size_t i = 0; i < s.segs.size(); ++i) __atomic_store_n(&s.res[i].status, kCrcStatusPending, __ATOMIC_RELAXED);
   }
   s.inflight = true;
   ++stats_.slots_submitted;
@@ -795,18 +812,19 @@ void GpuSink::enqueue_slot(Slot& s, uint8_t* dst, const CrcBatch* batch) {
     note_hip_call("hipEventRecord", s.st_idx, t2, now_ns());
   };
   if (!cfg_.async_submit) {
-    s.submitted = true;
+    s.issued = ++s.posted;
     issue(batch);
     return;
   }
+  uint64_t seq;
   {
     std::lock_guard<std::mutex> lk(sub_mu_);
-    s.submitted = false;
+    seq = ++s.posted;
   }
   const bool has = batch != nullptr;
   CrcBatch copy;
   if (has) copy = *batch;
-  DeviceSubmitter::get(cfg_.device).post([this, &s, issue, has, copy]() {
+  DeviceSubmitter::get(cfg_.device).post([this, &s, issue, has, copy, seq]() {
     std::string err;
     try {
       issue(has ? &copy : nullptr);
@@ -815,7 +833,7 @@ void GpuSink::enqueue_slot(Slot& s, uint8_t* dst, const CrcBatch* batch) {
     }
     {
       std::lock_guard<std::mutex> lk(sub_mu_);
-      s.submitted = true;
+      s.issued = seq;
       if (!err.empty() && detail_.empty()) {
         mismatch_ = true;
         detail_ = "GPU submit failed: " + err;
@@ -830,7 +848,7 @@ void GpuSink::wait_slot(Slot& s) {
   RoctxRange rg("gcsb.wait_slot");
   if (cfg_.async_submit) {
     std::unique_lock<std::mutex> lk(sub_mu_);
-    sub_cv_.wait(lk, [&] { return s.submitted; });
+    sub_cv_.wait(lk, [&] { return s.issued == s.posted; });
   }
   s.inflight = false;
   if (cfg_.stage != GpuSinkConfig::Stage::kH2D) return;  // A/B stages: no GPU work queued
@@ -937,7 +955,7 @@ void GpuSink::abort() {
     if (s.inflight) {
       if (cfg_.async_submit) {  // the hand-off may still be queued on the submitter
         std::unique_lock<std::mutex> lk(sub_mu_);
-        sub_cv_.wait(lk, [&] { return s.submitted; });
+        sub_cv_.wait(lk, [&] { return s.issued == s.posted; });
       }
       if (cfg_.stage == GpuSinkConfig::Stage::kH2D) hip_check(hipEventSynchronize(s.ev), "hipEventSynchronize");
       s.inflight = false;

@@ -159,6 +159,7 @@ py::dict gpu_stats_dict(const GpuSinkStats& g) {
   r["objects_verified"] = g.objects_verified;
   r["slot_waits"] = g.slot_waits;
   r["slot_wait_s"] = g.slot_wait_s;
+  r["flag_reuses"] = g.flag_reuses;
   return r;
 }
 

@@ -323,6 +323,9 @@ def build_parser() -> argparse.ArgumentParser:
                     help="client sockets' TCP congestion control, set before connect (\"\" = the host default, BBR "
                          "on the GPU boxes, whose internal pacing arms an hrtimer per 64 KiB skb of an upload on a "
                          "loopback link: profiles/r4_recvcost). Every block uses it, baselines included")
+    ap.add_argument("--recv-refill", type=int, default=0, choices=[0, 1],
+                    help="client sockets: a payload recv() also reads what follows it (the next HTTP/2 frame "
+                         "header) in the same recvmsg (SocketOptions::recv_refill)")
     ap.add_argument("--read-diag", action="store_true",
                     help="per-read stall attribution (Runner read_diag): scheduler and softirq deltas of the "
                          "receiving / sending threads around every timed read; the slowest reads carry them and a "
@@ -481,8 +484,8 @@ def run_rank(args) -> int:
         "blocking_sync": args.event_wait == "block",
         "async_submit": bool(args.async_submit),
         "rcvbuf": parse_size(args.rcvbuf),
-        "read_diag": bool(args.read_diag),
         "tcp_congestion": args.client_cc,
+        "recv_refill": bool(args.recv_refill),
     }
     # the sliced extension: inline slot hand-off (r1_submit_ab), 2 MiB x 8
     # ring per sink (profiles/r2_sliced)
@@ -1002,7 +1005,9 @@ def run_rank(args) -> int:
         # two baselines bracket it and a drifting host cancels (A/B sessions)
         base_before = read_block(baseline_over(), side_steps, side_warm, f"{protocol} cpu baseline (before)")
     if args.workload == "read":
-        head = read_block({}, args.steps, args.warmup, "headline")
+        # --read-diag samples the headline's threads around every read (one
+        # reader: a handful of threads; not the 48-worker blocks)
+        head = read_block({"read_diag": bool(args.read_diag)}, args.steps, args.warmup, "headline")
         headline_model = (f"{protocol} ReadObject {args.object_size} object, "
                           f"{'one stream per read' if args.slices == 1 else f'{args.slices} ranged streams'}"
                           + (" -> HBM (CRC32C on GPU)" if use_gpu else " -> discard (CPU baseline)"))

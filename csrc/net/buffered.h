@@ -43,11 +43,11 @@ class BufferedConn {
     }
   }
   // Read 1..n bytes directly (large-payload path). Returns 0 only on EOF.
-  // GCSB_RECV_REFILL=1: a large read also refills this buffer in the same
-  // recvmsg(), so whatever follows the payload (the next frame header) is
-  // parsed without a system call of its own.  Off: it halved the receive
-  // calls but moved no block's rate, and HTTP bodies then paid a 16 KiB
-  // bounce per read (profiles/r3_refill).
+  // SocketOptions::recv_refill: a large read also refills this buffer in the
+  // same recvmsg(), so whatever follows the payload (the next frame header)
+  // is parsed without a system call of its own.  Round 3 saw half the
+  // receive calls and no rate change under the pacing-timer noise
+  // (profiles/r3_refill); HTTP bodies pay a 16 KiB bounce per read.
   size_t read_some(void* dst, size_t n) {
     if (buffered()) {
       size_t b = buffered() < n ? buffered() : n;
@@ -55,7 +55,7 @@ class BufferedConn {
       pos_ += b;
       return b;
     }
-    if (n >= kRefillMin && refill_on()) {
+    if (n >= kRefillMin && conn_->recv_refill()) {
       pos_ = end_ = 0;
       const size_t r = conn_->read_some2(dst, n, buf_.get(), kCap);
       if (r <= n) return r;
@@ -82,13 +82,6 @@ class BufferedConn {
  private:
   static constexpr size_t kCap = 16384;
   static constexpr size_t kRefillMin = 64u << 10;
-  static bool refill_on() {
-    static const bool on = [] {
-      const char* e = std::getenv("GCSB_RECV_REFILL");
-      return e && *e == '1';
-    }();
-    return on;
-  }
   void fill() {
     if (pos_ == end_) pos_ = end_ = 0;
     if (end_ == kCap) {

@@ -240,6 +240,7 @@ std::unique_ptr<Conn> Conn::dial(const Endpoint& ep, const SocketOptions& opt) {
   if (fd < 0) throw StorageError("connect " + ep.host + ":" + port + ": " + last_err, true);
   auto conn = std::make_unique<Conn>();
   conn->fd_ = fd;
+  conn->recv_refill_ = opt.recv_refill;
   if (ep.scheme == "https") {
     SSL* ssl = SSL_new(client_ssl_ctx(opt.tls_verify, opt.tls_ca_file));
     SSL_set_fd(ssl, fd);
@@ -254,6 +255,7 @@ std::unique_ptr<Conn> Conn::dial(const Endpoint& ep, const SocketOptions& opt) {
       std::string why = vr != X509_V_OK ? std::string(": certificate ") + X509_verify_cert_error_string(vr) : "";
       SSL_free(ssl);
       conn->fd_ = fd;  // closed by ~Conn
+      conn->recv_refill_ = opt.recv_refill;
       // a certificate failure will not fix itself: not retryable
       throw StorageError("TLS handshake with " + ep.host + " failed" + why, vr == X509_V_OK);
     }
@@ -322,6 +324,7 @@ std::unique_ptr<Conn> Conn::adopt(int fd, const SocketOptions& opt) {
   apply_socket_options(fd, opt);
   auto conn = std::make_unique<Conn>();
   conn->fd_ = fd;
+  conn->recv_refill_ = opt.recv_refill;
   return conn;
 }
 

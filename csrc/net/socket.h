@@ -48,6 +48,10 @@ struct SocketOptions {
   // loopback link every 64 KiB skb of an upload then waits on an hrtimer
   // (profiles/r4_recvcost).
   std::string congestion;
+  // A payload recv() also refills the reader's 16 KiB buffer (one recvmsg,
+  // two iovecs), so the bytes after the payload -- the next HTTP/2 frame's
+  // header -- need no system call of their own (BufferedConn::read_some).
+  bool recv_refill = false;
 };
 
 // Server-side TLS context from PEM files (fake GCS endpoint over https);
@@ -116,6 +120,7 @@ class Conn {
   bool is_open() const { return fd_ >= 0; }
   bool tls() const { return ssl_ != nullptr; }
   uint64_t bytes_read() const { return bytes_read_; }
+  bool recv_refill() const { return recv_refill_; }
   uint64_t bytes_written() const { return bytes_written_; }
 
  private:
@@ -130,6 +135,7 @@ class Conn {
   SSL* ssl_ = nullptr;
   std::mutex ssl_mu_;
   int io_timeout_ms_ = 0;
+  bool recv_refill_ = false;
   uint64_t bytes_read_ = 0;
   uint64_t bytes_written_ = 0;
   int pipe_[2] = {-1, -1};  // splice_user_all's page pipe (lazily created)

@@ -40,6 +40,10 @@ ClientConfig client_cfg(const std::string& proto, const std::string& url) {
   c.retry.max_s = 0.01;
   c.retry.max_attempts = 8;
   c.read_chunk = 256 << 10;
+  // the optional receive path (SocketOptions::recv_refill) for the
+  // sanitizer runs that ask for it
+  const char* e = std::getenv("STRESS_RECV_REFILL");
+  c.sock.recv_refill = e && *e == '1';
   return c;
 }
 

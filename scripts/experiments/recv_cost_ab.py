@@ -6,6 +6,9 @@ placement and 8 x 2 MiB THP ring as bench.py's headline; variants
 interleaved `--reps` times in one process:
 
   head      the headline: ring -> hipMemcpyAsync -> HBM, CRC32C kernels
+  head_wc   the same, ring in write-combined pinned memory
+  head_4m   the same, 4 x 4 MiB slots
+  head_refill  the same, recv_refill (one recvmsg per DATA frame tail + next header)
   nodma     the same ring, filled by the same receive path, handed straight
             back: nothing reads it (gpu_stage none)
   hostread  the submitter thread reads each slot (host CRC32C) instead of
@@ -51,13 +54,20 @@ cpus_all = sorted(set(pl["client"]) | set(pl["server"]) | set(pl.get("aux") or [
 base = {"protocol": "grpc", "endpoint": srv.url, "bucket": "b", "object_prefix": "f_", "workers": 1,
         "reads_per_worker": 3, "device": 0, "ring_slot_bytes": 2 << 20, "ring_slots": 8, "landing": "object",
         "keep_records": False, "cpus": pl["client"], "rcvbuf": 64 << 20, "async_submit": True,
-        "blocking_sync": True, "retry_initial_s": 0.05}
+        "blocking_sync": True, "retry_initial_s": 0.05, "tcp_congestion": "cubic"}
 two_core = sorted(set(pl["client"]) | set(pl.get("aux") or []))
 variants = {
     "head": {"sink": "gpu"},
     "nodma": {"sink": "gpu", "gpu_stage": "none"},
     "hostread": {"sink": "gpu", "gpu_stage": "host_read"},
     "base": {"sink": "discard", "host_crc": True, "cpus": two_core},
+    # the headline's ring in write-combined pinned memory (no RFO, no dirty
+    # lines for the copy engine to read), and with 4 MiB slots (half the
+    # hand-offs per read)
+    "head_wc": {"sink": "gpu", "ring_wc": True},
+    "head_4m": {"sink": "gpu", "ring_slot_bytes": 4 << 20, "ring_slots": 4},
+    # the headline with the next frame header read in the payload's recvmsg
+    "head_refill": {"sink": "gpu", "recv_refill": True},
 }
 names = [v for v in args.variants.split(",") if v]
 runners = {k: n.Runner({**base, **variants[k]}) for k in names}

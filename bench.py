@@ -1145,7 +1145,7 @@ def run_rank(args) -> int:
                     b["endpoint_tcp"] = st["cpu"]["endpoint_tcp"]
                 if st["cpu"].get("endpoint_h2"):
                     b["endpoint_h2"] = st["cpu"]["endpoint_h2"]
-                if key.startswith(("compare", "cpu_baseline")) and st["cpu"].get("host"):
+                if key.startswith(("compare", "cpu_baseline", "ref_default_", "list_read_")) and st["cpu"].get("host"):
                     b["host"] = st["cpu"]["host"]
             if key.startswith("ref_default_100m_") and key.endswith("_gpu"):
                 # the HBM landing's own bound: pinned -> HBM copy rate

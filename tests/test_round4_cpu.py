@@ -1,0 +1,182 @@
+"""Round-4 host-side features on CPU: the endpoint's listener congestion
+control (no inherited BBR pacing), FIFO HTTP/2 frame writes with a quantum,
+per-read stall attribution (Runner read_diag), recv_refill, client-side
+congestion control, and the sysdiag host view."""
+import os
+import threading
+
+import pytest
+
+B = "princer-working-dirs"
+P = "princer_100M_files/file_"
+
+
+def _softirqs():
+    with open("/proc/softirqs") as f:
+        lines = f.read().splitlines()
+    for line in lines[1:]:
+        head, _, rest = line.partition(":")
+        if head.strip() == "HRTIMER":
+            return sum(int(x) for x in rest.split())
+    return 0
+
+
+def test_endpoint_connections_are_not_paced(native):
+    """The endpoint sets its congestion control on the listening socket, so
+    accepted connections never run BBR's init (which marks a socket for
+    internal pacing that a later TCP_CONGESTION does not undo): a 256 MiB
+    gRPC read arms no per-skb pacing hrtimers."""
+    with open("/proc/sys/net/ipv4/tcp_congestion_control") as f:
+        host_cc = f.read().strip()
+    srv = native.Server({"port": 0})
+    srv.start()
+    srv.add_synthetic(B, P, "", 0, 1, 256 << 20)
+    try:
+        c = native.Client({"protocol": "grpc", "endpoint": srv.url})
+        c.read(B, P + "0")
+        h0 = _softirqs()
+        for _ in range(2):
+            assert c.read(B, P + "0")["verified"]
+        per_read = (_softirqs() - h0) / 2
+    finally:
+        srv.stop()
+    if host_cc != "bbr":
+        pytest.skip(f"host congestion control is {host_cc}: nothing to inherit")
+    # paced: ~4,000 per 256 MiB read (one per 64 KiB skb); unpaced: timer noise only
+    assert per_read < 400, per_read
+
+
+@pytest.mark.parametrize("quantum", [0, 256 << 10])
+def test_multiplexed_streams_byte_exact_with_frame_quantum(native, quantum):
+    """16 streams on one gRPC connection with the endpoint's DATA frame
+    quantum on / off: every read verified; with the quantum the endpoint
+    wrote frames of at most 256 KiB (more frames than 2 MiB messages) and
+    reports its per-frame queue wait and request -> HEADERS times."""
+    srv = native.Server({"port": 0, "h2_quantum": quantum})
+    srv.start()
+    srv.add_synthetic(B, P, "", 0, 16, (3 << 20) + 77)
+    try:
+        r = native.Runner({"protocol": "grpc", "endpoint": srv.url, "bucket": B, "object_prefix": P, "workers": 16,
+                           "reads_per_worker": 3, "sink": "discard", "host_crc": True, "grpc_conn_pool_size": 1,
+                           "keep_records": False})
+        r.start()
+        r.wait()
+        s = r.summary()
+        st = srv.stats()
+    finally:
+        srv.stop()
+    assert s["errors"] == 0 and s["verified"] == 48, s
+    msgs = 48 * 2  # two ReadObjectResponse messages (2 MiB + the rest) per read
+    if quantum:
+        assert st["h2_data_frames"] >= 48 * ((3 << 20) // quantum), st
+    else:
+        assert st["h2_data_frames"] >= msgs, st
+    assert st["h2_responses"] >= 48 and st["h2_ttfb_us"] > 0 and st["h2_queue_wait_max_us"] >= 0
+
+
+def test_fifo_frame_writes_serve_streams_in_turn(native):
+    """Two streams on one connection: with FIFO frame hand-off neither
+    stream's reads finish far behind the other's (the old std::mutex let one
+    handler keep the connection)."""
+    srv = native.Server({"port": 0})
+    srv.start()
+    srv.add_synthetic(B, P, "", 0, 2, 32 << 20)
+    try:
+        r = native.Runner({"protocol": "grpc", "endpoint": srv.url, "bucket": B, "object_prefix": P, "workers": 2,
+                           "reads_per_worker": 4, "sink": "discard", "host_crc": False, "grpc_conn_pool_size": 1,
+                           "keep_records": True})
+        r.start()
+        r.wait()
+        recs = r.drain()
+    finally:
+        srv.stop()
+    assert len(recs) == 8 and all(x["ok"] for x in recs)
+    ends = {}
+    for x in recs:
+        ends.setdefault(x["worker"], []).append(x["end_ns"])
+    a, b = (max(v) for v in ends.values())
+    first = min(min(v) for v in ends.values())
+    # the two workers' last reads end close together relative to the run
+    assert abs(a - b) < 0.6 * (max(a, b) - first), (a, b, first)
+
+
+def test_runner_read_diag_names_threads(native):
+    srv = native.Server({"port": 0})
+    srv.start()
+    srv.add_synthetic(B, P, "", 0, 1, 16 << 20)
+    try:
+        r = native.Runner({"protocol": "grpc", "endpoint": srv.url, "bucket": B, "object_prefix": P, "workers": 1,
+                           "reads_per_worker": 2, "sink": "discard", "read_diag": True, "keep_records": False})
+        r.start()
+        r.wait()  # warm: the connection (and its reader thread) exist before the timed reads
+        r.reset_stats()
+        r.set_reads_per_worker(6)
+        r.start()
+        r.wait()
+        s = r.summary()
+    finally:
+        srv.stop()
+    assert len(s["slowest_diag"]) == len(s["slowest"]) == 3
+    d = s["slowest_diag"][0]
+    assert "gcsb-h2-reader" in d["threads"] and any(k.startswith("gcsb-srv") for k in d["threads"])
+    row = d["threads"]["gcsb-h2-reader"]
+    assert row["cpu_ms"] > 0 and row["run_delay_ms"] >= 0 and row["cpus"]
+    assert d["wall_ms"] >= s["slowest"][0][1] * 0.5
+    from custom_go_client_benchmark_amd.utils import sysdiag
+
+    cause = sysdiag.attribute(d, s["slowest"][0][1], s["p50_ms"])
+    assert isinstance(cause, str) and cause
+
+
+def test_attribute_names_run_queue_delay_and_timer_storms():
+    from custom_go_client_benchmark_amd.utils import sysdiag
+
+    d = {"threads": {"gcsb-h2-reader": {"cpu_ms": 9.0, "run_delay_ms": 4.0, "nivcsw": 30},
+                     "gcsb-srv-rpc": {"cpu_ms": 6.0, "run_delay_ms": 0.1, "nivcsw": 0}},
+         "softirqs": {"HRTIMER": 3000, "NET_RX": 4000}, "wall_ms": 14.0}
+    c = sysdiag.attribute(d, 14.0, 10.0)
+    assert "receiving thread waited 4.00 ms" in c and "HRTIMER" in c
+    d = {"threads": {"gcsb-h2-reader": {"cpu_ms": 13.5, "run_delay_ms": 0.0, "nivcsw": 0}}, "softirqs": {},
+         "wall_ms": 14.0}
+    assert "receive copy itself" in sysdiag.attribute(d, 14.0, 10.0)
+
+
+@pytest.mark.parametrize("proto", ["grpc", "http2", "http"])
+def test_recv_refill_byte_exact(native, server, proto):
+    size = (9 << 20) + 4321
+    server.add_synthetic(B, P, "", 0, 1, size)
+    c = native.Client({"protocol": proto, "endpoint": server.url, "recv_refill": True})
+    assert c.read_bytes(B, P + "0") == native.object_bytes(P + "0", 0, size)
+    assert c.read(B, P + "0")["verified"]
+
+
+def test_client_congestion_control_option(native, server):
+    """tcp_congestion is applied before connect; an unknown algorithm is
+    ignored by the kernel (setsockopt fails quietly), not fatal."""
+    server.add_synthetic(B, P, "", 0, 1, 1 << 20)
+    for cc in ("cubic", "reno", "no-such-cc"):
+        c = native.Client({"protocol": "grpc", "endpoint": server.url, "tcp_congestion": cc})
+        assert c.read(B, P + "0")["verified"]
+        data = os.urandom(3 << 20)
+        m = c.write_bytes(B, f"upload/cc_{cc}", data)
+        assert m["size"] == len(data)
+
+
+def test_sysdiag_window_reports_threads():
+    from custom_go_client_benchmark_amd.utils import sysdiag
+
+    w = sysdiag.Window()
+    stop = threading.Event()
+
+    def spin():
+        while not stop.is_set():
+            pass
+    t = threading.Thread(target=spin, name="spinner")
+    t.start()
+    import time
+
+    time.sleep(0.2)
+    rep = w.report(None, 1)
+    stop.set()
+    t.join()
+    assert rep["threads"] and "softirq_on_placement" in rep and "irq_on_placement" in rep

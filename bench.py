@@ -299,6 +299,9 @@ def build_parser() -> argparse.ArgumentParser:
                          "4.5-5.0 ms spread over the quota's cores (profiles/r3_mux_thp/refplace). HTTP keeps "
                          "share_quota: its 48 receiving workers need the cores")
     ap.add_argument("--ref-object-size", default="1MiB", help="ref_default_*: object size")
+    ap.add_argument("--ref-http-placement", default="share_quota", choices=["share_quota", "split_quota"],
+                    help="ref_default_http*: client workers and endpoint handlers over the rank's quota cores "
+                         "together (share_quota) or on separate cores, a quarter for the endpoint (split_quota)")
     ap.add_argument("--ref100-reads", type=int, default=3,
                     help="ref_default_100m_* blocks: the reference's real operating point, 48 workers x 100 MiB "
                          "objects (princer_100M_files), HTTP vs gRPC pool 1, discard + host CRC vs HBM + GPU CRC; "
@@ -948,7 +951,7 @@ def run_rank(args) -> int:
         workers = args.ref_workers
         osz = osz or parse_size(args.ref_object_size)
         reads = reads or args.ref_reads
-        mode = args.ref_grpc_placement if proto != "http" else "share_quota"
+        mode = args.ref_grpc_placement if proto != "http" else args.ref_http_placement
         sh = affinity.plan(gpu, mode, slot) if use_gpu else {"client": [], "server": []}
         if use_gpu and proto != "http" and args.mux_reader == "isolate":
             sh = affinity.isolate_reader(sh)

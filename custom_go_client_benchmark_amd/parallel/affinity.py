@@ -196,6 +196,11 @@ def plan(device: int, mode: str = "split", slot: int = 0) -> dict:
                    endpoint threads: all 8 domains on a 1-GPU box, 2 per rank
                    on a full 8-GPU node; best for sliced reads),
           "share_quota" (share, trimmed to the rank's CPU-quota budget),
+          "split_quota" (share_quota's cores split by physical core: a
+                  quarter for the endpoint's threads, the rest for the
+                  client's, so 48 endpoint handlers never queue behind 48
+                  client workers for a CPU -- a remote server would not share
+                  the client's cores at all),
           "split" (client and endpoint on two L3 domains of the GPU's node),
           "same" (one shared L3 domain), "numa" (whole node), "none".
     """
@@ -227,7 +232,7 @@ def plan(device: int, mode: str = "split", slot: int = 0) -> dict:
     # slot: this rank's index among ranks sharing ONE GPU (shared-GPU
     # rehearsals only; 0 on a node with a GPU per rank) -> the next L3 domains
     base = (k * share + slot) % max(1, len(groups))
-    if mode in ("share", "share_quota"):
+    if mode in ("share", "share_quota", "split_quota"):
         # not trimmed to the quota: a handful of busy threads (one stream per
         # read, or 8 sliced streams) did better spread over the share's 64
         # CPUs than packed onto 16 cores (sliced 32-34k vs 40-43k MiB/s,
@@ -237,8 +242,18 @@ def plan(device: int, mode: str = "split", slot: int = 0) -> dict:
         # (the reference's 48) without the 8 ranks of a node piling onto the
         # same first cores as plain "quota" would
         mine = [c for g in groups[base:base + share] for c in g] or cpus
-        if mode == "share_quota":
+        if mode in ("share_quota", "split_quota"):
             mine = trim_to_quota(mine, cpu_busy(0.1) if _quiet_sampling() else None)
+        if mode == "split_quota":
+            cores: dict = {}
+            for c in mine:
+                cores.setdefault(_core_key(c), []).append(c)
+            cl = [sorted(v) for _, v in sorted(cores.items(), key=lambda kv: min(kv[1]))]
+            if len(cl) >= 2:
+                nsrv = max(1, len(cl) // 4)
+                return {"client": sorted(c for core in cl[nsrv:] for c in core),
+                        "server": sorted(c for core in cl[:nsrv] for c in core), "mode": mode, "numa_node": node,
+                        "gpu_index_on_node": k, "l3_domains": share}
         return {"client": mine, "server": mine, "mode": mode, "numa_node": node, "gpu_index_on_node": k,
                 "l3_domains": share}
     if mode in ("pair", "pair2"):

@@ -296,6 +296,11 @@ int gpu_device_count();
 // CPU set of the per-device submitter threads (slot H2D copy + CRC launch
 // hand-off); empty = inherit.  Also GCSB_SUBMIT_CPUS=<cpulist>.
 void set_submitter_cpus(const std::vector<int>& cpus);
+// After a hand-off the per-device submitter polls this long for the next
+// one before it sleeps (0 = sleep at once): a post to a polling submitter
+// costs the receiving thread no futex wake.  Burns the submitter's core
+// (placement aux) while it polls.
+void set_submitter_spin_us(int us);
 
 // HIP calls on the slot hand-off / staging path that blocked the calling
 // thread (an async copy, launch or event record should return in

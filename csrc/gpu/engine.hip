@@ -293,6 +293,8 @@ std::vector<int> submitter_cpus() {
 // One thread per device that issues every queued ring-slot hand-off, so HIP
 // API calls are made by one thread instead of contending from many transport
 // threads.  Jobs run in FIFO order; each job is a few async HIP calls.
+std::atomic<int> g_submit_spin_us{0};
+
 class DeviceSubmitter {
  public:
   static DeviceSubmitter& get(int dev) {
@@ -310,6 +312,7 @@ class DeviceSubmitter {
     {
       std::lock_guard<std::mutex> lk(mu_);
       q_.push_back(std::move(f));
+      pending_.store(true, std::memory_order_release);
       wake = sleeping_;
     }
     if (wake) cv_.notify_one();
@@ -325,6 +328,15 @@ class DeviceSubmitter {
     ensure_device(dev_);
     std::unique_lock<std::mutex> lk(mu_);
     for (;;) {
+      const int spin_us = g_submit_spin_us.load(std::memory_order_relaxed);
+      if (q_.empty() && spin_us > 0) {
+        // poll for the next hand-off before sleeping: a post to a polling
+        // submitter costs the receiving thread no futex wake
+        lk.unlock();
+        const int64_t until = now_ns() + spin_us * 1000LL;
+        while (!pending_.load(std::memory_order_acquire) && now_ns() < until) __builtin_ia32_pause();
+        lk.lock();
+      }
       if (q_.empty()) {
         sleeping_ = true;
         cv_.wait(lk, [&] { return !q_.empty(); });
@@ -332,6 +344,7 @@ class DeviceSubmitter {
       }
       auto f = std::move(q_.front());
       q_.pop_front();
+      pending_.store(!q_.empty(), std::memory_order_release);
       lk.unlock();
       f();
       lk.lock();
@@ -341,9 +354,12 @@ class DeviceSubmitter {
   std::mutex mu_;
   std::condition_variable cv_;
   std::deque<std::function<void()>> q_;
+  std::atomic<bool> pending_{false};
   bool sleeping_ = false;  // guarded by mu_
 };
 }  // namespace
+
+void set_submitter_spin_us(int us) { g_submit_spin_us.store(std::max(0, us), std::memory_order_relaxed); }
 
 void set_submitter_cpus(const std::vector<int>& cpus) {
   std::lock_guard<std::mutex> lk(g_submit_mu);

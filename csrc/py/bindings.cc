@@ -863,6 +863,7 @@ PYBIND11_MODULE(_native, m) {
   m.def("parse_cpulist", &parse_cpulist);
   m.def("pin_current_thread", &pin_current_thread);
   m.def("set_submitter_cpus", &set_submitter_cpus);
+  m.def("set_submitter_spin_us", &set_submitter_spin_us, py::arg("us"));
   m.def("reserve_fd_table", &reserve_fd_table, py::arg("slots") = 8192);
   m.def("recv_stats", [] {
     RecvStats r = recv_stats();

@@ -48,7 +48,7 @@ recvcost)  # profiles/r4_recvcost: headline vs no-DMA vs host-read vs discard ba
   ;;
 recvcost2)  # profiles/r4_recvcost/after_listener_cc: the same A/B once the endpoint's listener carries its CC, + a full bench
   step pytest_sink 300 python3 -u -m pytest tests/test_gpu_sink.py tests/test_gpu_crc32c.py -x -q --timeout 120 --timeout-method thread
-  step ab 400 python3 -u scripts/experiments/recv_cost_ab.py --tag listener_cc --variants head,head_wc,head_4m,head_refill,nodma,hostread,base
+  step ab 400 python3 -u scripts/experiments/recv_cost_ab.py --tag listener_cc --variants head,head_wc,head_4m,head_refill,head_spin,nodma,hostread,base
   step mux 400 python3 -u scripts/experiments/mux_fair_ab.py
   step bench 600 python3 bench.py --json-out "$O/bench.json"
   step diag100 400 python3 bench.py --steps 100 --warmup 3 --side-steps 0 --read-diag --json-out "$O/diag100.json"

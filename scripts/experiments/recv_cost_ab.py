@@ -9,6 +9,7 @@ interleaved `--reps` times in one process:
   head_wc   the same, ring in write-combined pinned memory
   head_4m   the same, 4 x 4 MiB slots
   head_refill  the same, recv_refill (one recvmsg per DATA frame tail + next header)
+  head_spin the same, the device submitter polls 200 us before it sleeps
   nodma     the same ring, filled by the same receive path, handed straight
             back: nothing reads it (gpu_stage none)
   hostread  the submitter thread reads each slot (host CRC32C) instead of
@@ -68,7 +69,11 @@ variants = {
     "head_4m": {"sink": "gpu", "ring_slot_bytes": 4 << 20, "ring_slots": 4},
     # the headline with the next frame header read in the payload's recvmsg
     "head_refill": {"sink": "gpu", "recv_refill": True},
+    # the headline with the device submitter polling 200 us for the next
+    # hand-off before it sleeps (no futex wake per slot on the receiver)
+    "head_spin": {"sink": "gpu"},
 }
+SPIN_US = {"head_spin": 200}
 names = [v for v in args.variants.split(",") if v]
 runners = {k: n.Runner({**base, **variants[k]}) for k in names}
 for r in runners.values():  # warm: connections, rings, sinks
@@ -79,6 +84,7 @@ print(json.dumps({"tag": args.tag, "placement": pl, "hsa_enable_interrupt": os.e
 
 
 def run(name):
+    n.set_submitter_spin_us(SPIN_US.get(name, 0))
     r = runners[name]
     r.reset_stats()
     r.set_reads_per_worker(args.reads)

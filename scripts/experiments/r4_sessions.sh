@@ -59,6 +59,20 @@ recvcost2)  # profiles/r4_recvcost/after_listener_cc: the same A/B once the endp
     done
   done
   ;;
+main4)  # the round-4 GPU checkpoint: GPU suite, recv-cost A/B, full bench, 100-read diag, mux + HTTP placement A/Bs
+  step pytest_gpu 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+  step ab 400 python3 -u scripts/experiments/recv_cost_ab.py --tag main4 \
+    --variants head,head_wc,head_4m,head_refill,head_spin,nodma,hostread,base
+  step bench 600 python3 bench.py --json-out "$O/bench.json"
+  step diag100 400 python3 bench.py --steps 100 --warmup 3 --side-steps 0 --read-diag --json-out "$O/diag100.json"
+  step mux 400 python3 -u scripts/experiments/mux_fair_ab.py
+  for k in 1 2; do
+    for p in share_quota split_quota; do
+      step "http_${p}_$k" 300 python3 bench.py --steps 5 --warmup 1 --blocks ref_default,ref_default_100m \
+        --ref-http-placement $p --json-out "$O/http_${p}_$k.json"
+    done
+  done
+  ;;
 soak)  # profiles/r4_soak: execute_pb.sh with 48 workers x 100 MiB, -sink gpu, 120 s per protocol, exporter at 30 s
   step soak 900 python3 -u scripts/soak.py --out "$O" --duration 120s
   ;;

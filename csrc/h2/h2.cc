@@ -2,6 +2,7 @@
 
 #include <sys/uio.h>
 
+#include <chrono>
 #include <cstring>
 
 #include "core/util.h"
@@ -276,6 +277,27 @@ size_t H2Writer::reserve(uint32_t stream, size_t want) {
     }
     fcv_.wait(lk);
   }
+}
+
+size_t H2Writer::try_reserve(uint32_t stream, size_t want, bool* gone) {
+  std::lock_guard<std::mutex> lk(fmu_);
+  *gone = false;
+  auto it = stream_window_.find(stream);
+  if (dead_ || it == stream_window_.end()) {
+    *gone = true;
+    return 0;
+  }
+  const int64_t avail = std::min(conn_window_, it->second);
+  if (avail <= 0) return 0;
+  const size_t n = std::min<size_t>({want, static_cast<size_t>(avail), static_cast<size_t>(peer_max_frame_.load())});
+  conn_window_ -= static_cast<int64_t>(n);
+  it->second -= static_cast<int64_t>(n);
+  return n;
+}
+
+void H2Writer::wait_window(int timeout_ms) {
+  std::unique_lock<std::mutex> lk(fmu_);
+  fcv_.wait_for(lk, std::chrono::milliseconds(timeout_ms));
 }
 
 void H2Writer::register_stream(uint32_t stream) {

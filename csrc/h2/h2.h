@@ -148,6 +148,11 @@ class H2Writer {
   // how many bytes (<= want, <= peer max frame) may be sent now and debits
   // them.  Returns 0 if the connection/stream is dead.
   size_t reserve(uint32_t stream, size_t want);
+  // reserve() that never blocks: 0 if the windows allow nothing now; *gone
+  // set (and 0 returned) if the stream or the connection is dead.
+  size_t try_reserve(uint32_t stream, size_t want, bool* gone);
+  // Waits up to timeout_ms for a window update (or kill / settings change).
+  void wait_window(int timeout_ms);
   void register_stream(uint32_t stream);
   void unregister_stream(uint32_t stream);
   void on_window_update(uint32_t stream, uint32_t inc);

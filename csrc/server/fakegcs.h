@@ -48,9 +48,12 @@ struct ServerConfig {
   // memory cannot be had): profiles/r3_splice/thp_source
   bool send_vmsplice = true;
   std::vector<int> cpus;   // pin connection/handler threads (empty = unpinned)
-  // HTTP/2: DATA frame cap while several streams share a connection, so
-  // their frames interleave round-robin (H2Writer::set_quantum; 0 = off)
-  size_t h2_quantum = 256u << 10;
+  // HTTP/2: DATA frame cap while several streams share a connection
+  // (H2Writer::set_quantum and the send scheduler's turn; 0 = a whole
+  // message per turn).  ReadObject messages are <= 2 MiB and the scheduler
+  // already serves streams round-robin a message at a time: 256 KiB frames
+  // cost the 48-stream block 15-30% with no better tail (profiles/r4_mux).
+  size_t h2_quantum = 0;
   // https / gRPC over TLS (ALPN h2 or http/1.1) when both are set (PEM files)
   std::string tls_cert_file, tls_key_file;
 };

@@ -8,6 +8,7 @@ interleaved `--reps` times in one process:
   head      the headline: ring -> hipMemcpyAsync -> HBM, CRC32C kernels
   head_wc   the same, ring in write-combined pinned memory
   head_4m   the same, 4 x 4 MiB slots
+  head_4x2  the same, 4 x 2 MiB slots (the discard sink's 8 MiB footprint)
   head_refill  the same, recv_refill (one recvmsg per DATA frame tail + next header)
   head_spin the same, the device submitter polls 200 us before it sleeps
   nodma     the same ring, filled by the same receive path, handed straight
@@ -67,6 +68,8 @@ variants = {
     # hand-offs per read)
     "head_wc": {"sink": "gpu", "ring_wc": True},
     "head_4m": {"sink": "gpu", "ring_slot_bytes": 4 << 20, "ring_slots": 4},
+    # half the ring (8 MiB, the discard sink's 4 recycled 2 MiB blocks)
+    "head_4x2": {"sink": "gpu", "ring_slots": 4},
     # the headline with the next frame header read in the payload's recvmsg
     "head_refill": {"sink": "gpu", "recv_refill": True},
     # the headline with the device submitter polling 200 us for the next

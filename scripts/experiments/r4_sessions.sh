@@ -73,6 +73,15 @@ main4)  # the round-4 GPU checkpoint: GPU suite, recv-cost A/B, full bench, 100-
     done
   done
   ;;
+main5)  # send scheduler on the GPU box; recv-cost A/B with more reps; two benches; the CLI soak
+  step pytest_sink 300 python3 -u -m pytest tests/test_gpu_sink.py tests/test_gpu_crc32c.py -x -q --timeout 120 --timeout-method thread
+  step mux 400 python3 -u scripts/experiments/mux_fair_ab.py --quanta 0,1024
+  step ab 500 python3 -u scripts/experiments/recv_cost_ab.py --tag main5 --reps 5 \
+    --variants head,head_4x2,head_spin,nodma,hostread,base
+  step bench1 600 python3 bench.py --json-out "$O/bench1.json"
+  step bench2 600 python3 bench.py --json-out "$O/bench2.json"
+  step soak 900 python3 -u scripts/soak.py --out "$O/soak" --duration 120s
+  ;;
 soak)  # profiles/r4_soak: execute_pb.sh with 48 workers x 100 MiB, -sink gpu, 120 s per protocol, exporter at 30 s
   step soak 900 python3 -u scripts/soak.py --out "$O" --duration 120s
   ;;

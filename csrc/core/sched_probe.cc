@@ -95,6 +95,33 @@ std::map<int, std::map<std::string, uint64_t>> read_softirqs(const std::set<int>
   return out;
 }
 
+// "<Prefix>: name name ...\n<Prefix>: v v ..." tables (/proc/net/snmp,
+// /proc/net/netstat): the wanted fields of the row with this prefix.
+void read_proto_table(const char* path, const char* prefix, const std::vector<const char*>& want,
+                      std::map<std::string, uint64_t>* out) {
+  FILE* f = std::fopen(path, "r");
+  if (!f) return;
+  char* line = nullptr;
+  size_t cap = 0;
+  std::vector<std::string> names;
+  const size_t plen = std::strlen(prefix);
+  while (getline(&line, &cap, f) > 0) {
+    if (std::strncmp(line, prefix, plen) != 0) continue;
+    std::vector<std::string> toks;
+    for (char* tok = std::strtok(line + plen, " \t\n"); tok; tok = std::strtok(nullptr, " \t\n")) toks.emplace_back(tok);
+    if (names.empty()) {
+      names = std::move(toks);
+      continue;
+    }
+    for (size_t i = 0; i < names.size() && i < toks.size(); ++i)
+      for (const char* w : want)
+        if (names[i] == w) (*out)[w] = std::strtoull(toks[i].c_str(), nullptr, 10);
+    break;
+  }
+  std::free(line);
+  std::fclose(f);
+}
+
 int64_t mono_ns() {
   timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
@@ -138,6 +165,8 @@ SchedSample sched_sample(const std::vector<std::string>& prefixes) {
     for (int tid : dead) registry().erase(tid);
   }
   s.softirqs = read_softirqs(cpus);
+  read_proto_table("/proc/net/snmp", "Tcp:", {"RetransSegs"}, &s.tcp);
+  read_proto_table("/proc/net/netstat", "TcpExt:", {"TCPLossProbes", "TCPTimeouts"}, &s.tcp);
   return s;
 }
 
@@ -168,6 +197,10 @@ ReadSchedDiag sched_delta(const SchedSample& a, const SchedSample& b) {
       auto k = ia->second.find(kind);
       if (k != ia->second.end() && v > k->second) d.softirqs[kind] += v - k->second;
     }
+  }
+  for (const auto& [k, v] : b.tcp) {
+    auto it = a.tcp.find(k);
+    d.tcp[k] = it != a.tcp.end() && v > it->second ? v - it->second : 0;
   }
   return d;
 }

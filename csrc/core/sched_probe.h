@@ -36,6 +36,11 @@ struct SchedSample {
   std::vector<ThreadSched> threads;
   // softirq counts per CPU of interest: {cpu: {"NET_RX": n, "HRTIMER": n, ...}}
   std::map<int, std::map<std::string, uint64_t>> softirqs;
+  // TCP counters of the network namespace (/proc/net/snmp Tcp:, /proc/net/
+  // netstat TcpExt:): RetransSegs, TCPLossProbes, TCPTimeouts.  Loopback
+  // reader and endpoint share the namespace, so a retransmit by either side
+  // shows here (per-socket TCP_INFO would only see the client's own).
+  std::map<std::string, uint64_t> tcp;
 };
 
 // Threads whose name starts with one of `prefixes`; softirqs of the CPUs
@@ -53,6 +58,7 @@ struct ReadSchedDiag {
   };
   std::map<std::string, Row> threads;                      // by thread name
   std::map<std::string, uint64_t> softirqs;                // on those CPUs, by kind
+  std::map<std::string, uint64_t> tcp;                     // namespace TCP counters over the read
   double wall_ms = 0;
 };
 ReadSchedDiag sched_delta(const SchedSample& a, const SchedSample& b);

@@ -147,6 +147,9 @@ py::dict sched_diag_dict(const ReadSchedDiag& x) {
   for (const auto& [k, v] : x.softirqs) si[py::str(k)] = v;
   d["threads"] = th;
   d["softirqs"] = si;
+  py::dict tcp;
+  for (const auto& [k, v] : x.tcp) tcp[py::str(k)] = v;
+  d["tcp"] = tcp;
   d["wall_ms"] = x.wall_ms;
   return d;
 }

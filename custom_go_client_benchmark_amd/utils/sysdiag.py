@@ -156,7 +156,8 @@ def attribute(diag: dict, ms: float, p50_ms: float) -> str:
     """A slow read's likely cause from its scheduler / softirq deltas
     (Runner read_diag, core/sched_probe.h): run-queue delay of the receiving
     thread (h2 reader, or the HTTP worker) or of the endpoint's sender,
-    preemptions, a timer-softirq storm on their CPUs, or -- none of those --
+    preemptions, TCP retransmits, a timer-softirq storm on their CPUs, or --
+    none of those --
     a receive copy that simply took longer on the CPU."""
     th = diag.get("threads", {})
     excess = max(ms - p50_ms, 1e-6)
@@ -171,6 +172,10 @@ def attribute(diag: dict, ms: float, p50_ms: float) -> str:
         if row and row.get("run_delay_ms", 0.0) >= 0.2 * excess:
             causes.append(f"{label} waited {row['run_delay_ms']:.2f} ms for a CPU "
                           f"({row.get('nivcsw', 0)} preemptions)")
+    tcp = diag.get("tcp", {})
+    if tcp.get("RetransSegs", 0) or tcp.get("TCPTimeouts", 0):
+        causes.append(f"{tcp.get('RetransSegs', 0)} TCP retransmits ({tcp.get('TCPTimeouts', 0)} RTOs, "
+                      f"{tcp.get('TCPLossProbes', 0)} loss probes) in the namespace")
     soft = diag.get("softirqs", {})
     if soft.get("HRTIMER", 0) >= 100:
         causes.append(f"{soft['HRTIMER']} HRTIMER softirqs on the busy CPUs (pacing timers)")

@@ -122,6 +122,8 @@ def test_runner_read_diag_names_threads(native):
     row = d["threads"]["gcsb-h2-reader"]
     assert row["cpu_ms"] > 0 and row["run_delay_ms"] >= 0 and row["cpus"]
     assert d["wall_ms"] >= s["slowest"][0][1] * 0.5
+    # namespace TCP counters over the read (loopback: normally no retransmits)
+    assert set(d["tcp"]) >= {"RetransSegs", "TCPTimeouts"} and all(v >= 0 for v in d["tcp"].values())
     from custom_go_client_benchmark_amd.utils import sysdiag
 
     cause = sysdiag.attribute(d, s["slowest"][0][1], s["p50_ms"])
@@ -139,6 +141,8 @@ def test_attribute_names_run_queue_delay_and_timer_storms():
     d = {"threads": {"gcsb-h2-reader": {"cpu_ms": 13.5, "run_delay_ms": 0.0, "nivcsw": 0}}, "softirqs": {},
          "wall_ms": 14.0}
     assert "receive copy itself" in sysdiag.attribute(d, 14.0, 10.0)
+    d["tcp"] = {"RetransSegs": 12, "TCPTimeouts": 1, "TCPLossProbes": 0}
+    assert "12 TCP retransmits (1 RTOs" in sysdiag.attribute(d, 14.0, 10.0)
 
 
 @pytest.mark.parametrize("proto", ["grpc", "http2", "http"])

@@ -82,6 +82,13 @@ main5)  # send scheduler on the GPU box; recv-cost A/B with more reps; two bench
   step bench2 600 python3 bench.py --json-out "$O/bench2.json"
   step soak 900 python3 -u scripts/soak.py --out "$O/soak" --duration 120s
   ;;
+main6)  # ring footprint sweep; endpoint quantum at 48 streams; two benches
+  step ab 600 python3 -u scripts/experiments/recv_cost_ab.py --tag main6 --reps 4 \
+    --variants head,head_4x2,head_3x2,head_2x2,head_4x1m,head_8x512k,head_wc,head_4x2_wc,nodma,base
+  step mux 400 python3 -u scripts/experiments/mux_fair_ab.py --quanta 0,256,64 --reps 3
+  step bench1 600 python3 bench.py --slots 4 --json-out "$O/bench1.json"
+  step bench2 600 python3 bench.py --json-out "$O/bench2.json"
+  ;;
 soak)  # profiles/r4_soak: execute_pb.sh with 48 workers x 100 MiB, -sink gpu, 120 s per protocol, exporter at 30 s
   step soak 900 python3 -u scripts/soak.py --out "$O" --duration 120s
   ;;

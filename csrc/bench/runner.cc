@@ -45,6 +45,55 @@ double percentile_floor(const std::vector<double>& sorted, int pct) {
   return sorted[idx];
 }
 
+size_t LatencySeries::bin(double ms) {
+  // bin 0: <= 2^-20 ms; then 1024 bins per octave up to 2^20 ms (17 min)
+  constexpr size_t kBins = 40 * 1024 + 2;
+  if (!(ms > 0x1p-20)) return 0;
+  const double x = (std::log2(ms) + 20.0) * 1024.0;
+  return std::min(kBins - 1, static_cast<size_t>(x) + 1);
+}
+
+double LatencySeries::bin_value(size_t b) {
+  return b == 0 ? 0.0 : std::exp2((static_cast<double>(b - 1) + 0.5) / 1024.0 - 20.0);
+}
+
+void LatencySeries::add(double ms) {
+  if (n_ == 0 || ms < min_) min_ = ms;
+  if (n_ == 0 || ms > max_) max_ = ms;
+  ++n_;
+  sum_ += ms;
+  if (hist_.empty()) {
+    if (exact_.size() < kExact) {
+      exact_.push_back(ms);
+      return;
+    }
+    // switch to the histogram: bin every sample so far, drop the samples
+    hist_.assign(bin(std::exp2(20.0)) + 1, 0);
+    for (double x : exact_) ++hist_[bin(x)];
+    std::vector<double>().swap(exact_);
+  }
+  ++hist_[bin(ms)];
+}
+
+void LatencySeries::clear() { *this = LatencySeries(); }
+
+double LatencySeries::pct_floor(int pct) const {
+  if (n_ == 0) return 0;
+  size_t idx = n_ * static_cast<size_t>(pct) / 100;
+  if (idx >= n_) idx = n_ - 1;
+  if (hist_.empty()) {
+    std::vector<double> v = exact_;
+    std::nth_element(v.begin(), v.begin() + idx, v.end());
+    return v[idx];
+  }
+  size_t seen = 0;
+  for (size_t b = 0; b < hist_.size(); ++b) {
+    seen += hist_[b];
+    if (seen > idx) return std::min(max_, std::max(min_, bin_value(b)));
+  }
+  return max_;
+}
+
 Runner::Runner(RunnerConfig cfg) : cfg_(std::move(cfg)) {
   reserve_fd_table();
   if (cfg_.workers <= 0) throw StorageError("worker count not valid", false);
@@ -98,8 +147,7 @@ void Runner::reset_stats() {
   lat_ms_.clear();
   host_ms_.clear();
   ttfb_ms_.clear();
-  ttfb_by_read_.clear();
-  diag_by_read_.clear();
+  slowest_.clear();
   first_ms_.clear();
   steady_ms_.clear();
   pending_.clear();
@@ -148,12 +196,17 @@ void Runner::record(ReadRecord&& r, double ms, double host_ms) {
   } else {
     acc_.bytes += r.bytes;
     if (r.verified) ++acc_.verified;
-    lat_ms_.push_back(ms);
-    (r.seq == 0 ? first_ms_ : steady_ms_).push_back(ms);
-    host_ms_.push_back(host_ms);
-    if (r.ttfb_ns > r.start_ns) ttfb_ms_.push_back((r.ttfb_ns - r.start_ns) / 1e6);
-    ttfb_by_read_.push_back(r.ttfb_ns > r.start_ns ? (r.ttfb_ns - r.start_ns) / 1e6 : 0.0);
-    diag_by_read_.push_back(r.diag);
+    const double ttfb = r.ttfb_ns > r.start_ns ? (r.ttfb_ns - r.start_ns) / 1e6 : 0.0;
+    if (slowest_.size() < 3 || ms > slowest_.back().ms) {
+      if (slowest_.size() == 3) slowest_.pop_back();
+      Slow sl{lat_ms_.size(), ms, host_ms, ttfb, r.diag};
+      auto at = std::find_if(slowest_.begin(), slowest_.end(), [&](const Slow& x) { return ms > x.ms; });
+      slowest_.insert(at, std::move(sl));
+    }
+    lat_ms_.add(ms);
+    (r.seq == 0 ? first_ms_ : steady_ms_).add(ms);
+    host_ms_.add(host_ms);
+    if (r.ttfb_ns > r.start_ns) ttfb_ms_.add(ttfb);
     // metric semantics: integer-truncated milliseconds (reference main.go:146)
     acc_.oc_buckets[oc_bucket_index(std::floor(ms))]++;
   }
@@ -322,57 +375,40 @@ std::vector<ReadRecord> Runner::drain() {
   return out;
 }
 
-RunSummary Runner::summary() const {
+RunSummary Runner::summary(bool percentiles) const {
   std::lock_guard<std::mutex> lk(mu_);
   RunSummary s = acc_;
   s.worker_cpu_s = worker_cpu_s_;
   s.elapsed_s = t_last_ > t_first_ ? (t_last_ - t_first_) / 1e9 : 0;
   s.mb_per_s = s.elapsed_s > 0 ? s.bytes / 1048576.0 / s.elapsed_s : 0;
-  {
-    std::vector<size_t> idx(lat_ms_.size());
-    for (size_t i = 0; i < idx.size(); ++i) idx[i] = i;
-    const size_t k = std::min<size_t>(3, idx.size());
-    std::partial_sort(idx.begin(), idx.begin() + k, idx.end(),
-                      [&](size_t a, size_t b) { return lat_ms_[a] > lat_ms_[b]; });
-    for (size_t j = 0; j < k; ++j) {
-      const size_t i = idx[j];
-      s.slowest.push_back({static_cast<double>(i), lat_ms_[i], host_ms_[i], ttfb_by_read_[i]});
-      if (i < diag_by_read_.size() && diag_by_read_[i]) s.slowest_diag.push_back(*diag_by_read_[i]);
-    }
+  if (!lat_ms_.empty()) s.avg_ms = lat_ms_.sum() / lat_ms_.size();
+  if (!percentiles) return s;
+  for (const Slow& x : slowest_) {
+    s.slowest.push_back({static_cast<double>(x.index), x.ms, x.host_ms, x.ttfb_ms});
+    if (x.diag) s.slowest_diag.push_back(*x.diag);
   }
-  std::vector<double> v = lat_ms_;
-  std::sort(v.begin(), v.end());
-  if (!v.empty()) {
-    double sum = 0;
-    for (double x : v) sum += x;
-    s.avg_ms = sum / v.size();
-    s.p20_ms = percentile_floor(v, 20);
-    s.p50_ms = percentile_floor(v, 50);
-    s.p90_ms = percentile_floor(v, 90);
-    s.p99_ms = percentile_floor(v, 99);
-    s.min_ms = v.front();
-    s.max_ms = v.back();
+  if (!lat_ms_.empty()) {
+    s.avg_ms = lat_ms_.sum() / lat_ms_.size();
+    s.p20_ms = lat_ms_.pct_floor(20);
+    s.p50_ms = lat_ms_.pct_floor(50);
+    s.p90_ms = lat_ms_.pct_floor(90);
+    s.p99_ms = lat_ms_.pct_floor(99);
+    s.min_ms = lat_ms_.min();
+    s.max_ms = lat_ms_.max();
   }
-  std::vector<double> h = host_ms_;
-  std::sort(h.begin(), h.end());
-  s.host_p50_ms = percentile_floor(h, 50);
-  s.host_p99_ms = percentile_floor(h, 99);
-  std::vector<double> tf = ttfb_ms_;
-  std::sort(tf.begin(), tf.end());
-  if (!tf.empty()) {
-    s.ttfb_p50_ms = percentile_floor(tf, 50);
-    s.ttfb_p99_ms = percentile_floor(tf, 99);
+  s.host_p50_ms = host_ms_.pct_floor(50);
+  s.host_p99_ms = host_ms_.pct_floor(99);
+  if (!ttfb_ms_.empty()) {
+    s.ttfb_p50_ms = ttfb_ms_.pct_floor(50);
+    s.ttfb_p99_ms = ttfb_ms_.pct_floor(99);
   }
-  std::vector<double> fr = first_ms_, st = steady_ms_;
-  std::sort(fr.begin(), fr.end());
-  std::sort(st.begin(), st.end());
-  if (!fr.empty()) {
-    s.first_read_p50_ms = percentile_floor(fr, 50);
-    s.first_read_max_ms = fr.back();
+  if (!first_ms_.empty()) {
+    s.first_read_p50_ms = first_ms_.pct_floor(50);
+    s.first_read_max_ms = first_ms_.max();
   }
-  if (!st.empty()) {
-    s.steady_p50_ms = percentile_floor(st, 50);
-    s.steady_p99_ms = percentile_floor(st, 99);
+  if (!steady_ms_.empty()) {
+    s.steady_p50_ms = steady_ms_.pct_floor(50);
+    s.steady_p99_ms = steady_ms_.pct_floor(99);
   }
   int nsliced = 0;
   for (const auto& sr : sliced_)

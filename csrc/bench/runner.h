@@ -111,6 +111,36 @@ struct RunSummary {
 double percentile_floor(const std::vector<double>& sorted, int pct);
 int oc_bucket_index(double ms_truncated);
 
+// One latency series whose memory stays bounded over the reference's default
+// run (48 workers x 1,000,000 reads, main.go:36,38): exact samples up to
+// kExact, and from there on a log histogram of every sample with 2^-10
+// relative bin width (percentiles within 0.04%).  The reference keeps no
+// samples at all: OpenCensus folds each into its distribution
+// (main.go:146, metrics_exporter.go).
+class LatencySeries {
+ public:
+  static constexpr size_t kExact = size_t(1) << 20;
+  void add(double ms);
+  void clear();
+  size_t size() const { return n_; }
+  bool empty() const { return n_ == 0; }
+  double sum() const { return sum_; }
+  double min() const { return min_; }
+  double max() const { return max_; }
+  // percentile_floor() of the sorted samples while exact; the bin's
+  // geometric centre (clamped to [min, max]) after.
+  double pct_floor(int pct) const;
+  bool exact() const { return hist_.empty(); }
+
+ private:
+  static size_t bin(double ms);
+  static double bin_value(size_t b);
+  std::vector<double> exact_;
+  std::vector<uint64_t> hist_;
+  size_t n_ = 0;
+  double sum_ = 0, min_ = 0, max_ = 0;
+};
+
 class Runner {
  public:
   explicit Runner(RunnerConfig cfg);
@@ -120,7 +150,9 @@ class Runner {
   void stop();
   bool running() const { return running_.load(); }
   std::vector<ReadRecord> drain();
-  RunSummary summary() const;
+  // percentiles=false: counts, bytes, mean and OC buckets only -- O(1) under
+  // the lock the workers record into (the CLI's periodic exporter)
+  RunSummary summary(bool percentiles = true) const;
   // Per-worker object name (exposed for tests / CLI).
   std::string object_for(int worker, int64_t seq) const;
   // Phased runs (bench warmup -> timed): sinks (pinned ring, HBM landing
@@ -147,9 +179,14 @@ class Runner {
   volatile bool stop_flag_ = false;
   mutable std::mutex mu_;
   std::vector<ReadRecord> pending_;
-  std::vector<double> lat_ms_, host_ms_, ttfb_ms_, first_ms_, steady_ms_;
-  std::vector<double> ttfb_by_read_;  // per ok read, in completion order (0 if unknown)
-  std::vector<std::shared_ptr<ReadSchedDiag>> diag_by_read_;  // aligned with lat_ms_ (read_diag)
+  LatencySeries lat_ms_, host_ms_, ttfb_ms_, first_ms_, steady_ms_;
+  // the 3 slowest ok reads so far (kept as they complete: nothing per read)
+  struct Slow {
+    size_t index;
+    double ms, host_ms, ttfb_ms;
+    std::shared_ptr<ReadSchedDiag> diag;
+  };
+  std::vector<Slow> slowest_;
   RunSummary acc_;
   double worker_cpu_s_ = 0;  // guarded by mu_
   int64_t t_first_ = 0, t_last_ = 0;

@@ -513,8 +513,8 @@ class PyRunner {
     }
     return out;
   }
-  py::dict summary() {
-    RunSummary s = runner_->summary();
+  py::dict summary(bool percentiles) {
+    RunSummary s = runner_->summary(percentiles);
     py::dict d;
     d["reads"] = s.reads;
     d["errors"] = s.errors;
@@ -1072,13 +1072,26 @@ PYBIND11_MODULE(_native, m) {
       .def("delete", &PyClient::remove)
       .def("stats", &PyClient::stats);
 
+  py::class_<LatencySeries>(m, "LatencySeries")
+      .def(py::init<>())
+      .def("add", &LatencySeries::add)
+      .def("extend", [](LatencySeries& l, const std::vector<double>& v) {
+        for (double x : v) l.add(x);
+      })
+      .def("pct_floor", &LatencySeries::pct_floor)
+      .def("__len__", &LatencySeries::size)
+      .def_property_readonly("exact", &LatencySeries::exact)
+      .def_property_readonly("min", &LatencySeries::min)
+      .def_property_readonly("max", &LatencySeries::max)
+      .def_readonly_static("EXACT_CAP", &LatencySeries::kExact);
   py::class_<PyRunner>(m, "Runner")
       .def(py::init<const py::dict&>())
       .def("start", &PyRunner::start)
       .def("wait", &PyRunner::wait)
       .def("stop", &PyRunner::stop)
       .def("drain", &PyRunner::drain)
-      .def("summary", &PyRunner::summary)
+      .def("summary", &PyRunner::summary, py::arg("percentiles") = true,
+           "percentiles=False: counts, bytes, mean and the OpenCensus buckets only (O(1), for periodic exporters)")
       .def("object_for", &PyRunner::object_for)
       .def("landing_ptr", &PyRunner::landing_ptr)
       .def("ring_numa", &PyRunner::ring_numa)

@@ -271,7 +271,10 @@ def main(argv: list[str] | None = None) -> int:
     live = {"summary": None, "runner": None}
 
     def source():
-        s = live["summary"]
+        # the exporter's 30 s tick: counts + OC buckets only (percentiles
+        # would sort every sample under the lock the workers record into)
+        r = live["runner"]
+        s = r.summary(False) if r is not None else live["summary"]
         return metrics_exporter.distribution_from_summary(s) if s else metrics_exporter.Distribution()
 
     exporter = None
@@ -400,11 +403,7 @@ def _run_with_live(opts, on_records, before_start, live, directpath: bool = True
     runner = _make_runner(opts, directpath)
     live["runner"] = runner
 
-    def recs(r):
-        live["summary"] = runner.summary()
-        on_records(r)
-
-    seen = workloads._drive(runner, recs, before_start=before_start)
+    seen = workloads._drive(runner, on_records, before_start=before_start)
     return workloads.WorkloadResult(runner.summary(), seen)
 
 

@@ -91,6 +91,8 @@ GpuSinkConfig gpu_from(const py::dict& d) {
   g.blocking_sync = get_or<bool>(d, "blocking_sync", g.blocking_sync);
   g.wait_poll_us = get_or<int>(d, "wait_poll_us", g.wait_poll_us);
   g.ring_wc = get_or<bool>(d, "ring_wc", g.ring_wc);
+  g.bounce = get_or<bool>(d, "ring_bounce", g.bounce);
+  g.bounce_bufs = get_or<int>(d, "bounce_bufs", g.bounce_bufs);
   const std::string stage = get_or<std::string>(d, "gpu_stage", "h2d");
   if (stage == "none") g.stage = GpuSinkConfig::Stage::kNone;
   else if (stage == "host_read") g.stage = GpuSinkConfig::Stage::kHostRead;
@@ -164,6 +166,8 @@ py::dict gpu_stats_dict(const GpuSinkStats& g) {
   r["slot_waits"] = g.slot_waits;
   r["slot_wait_s"] = g.slot_wait_s;
   r["flag_reuses"] = g.flag_reuses;
+  r["bounce_waits"] = g.bounce_waits;
+  r["bounce_wait_s"] = g.bounce_wait_s;
   return r;
 }
 

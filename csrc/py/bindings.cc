@@ -580,6 +580,7 @@ class PyServer {
     c.zero_copy = get_or<bool>(d, "zero_copy", true);
     c.send_vmsplice = get_or<std::string>(d, "send_source", "vmsplice") != "sendfile";
     c.h2_quantum = get_or<size_t>(d, "h2_quantum", c.h2_quantum);
+    c.h2_lead_bytes = get_or<size_t>(d, "h2_lead_bytes", c.h2_lead_bytes);
     c.tls_cert_file = get_or<std::string>(d, "tls_cert_file", "");
     c.tls_key_file = get_or<std::string>(d, "tls_key_file", "");
     if (d.contains("cpus") && !d["cpus"].is_none()) c.cpus = d["cpus"].cast<std::vector<int>>();

@@ -23,13 +23,15 @@ ap.add_argument("--reads", type=int, default=50)
 ap.add_argument("--workers", type=int, default=48)
 ap.add_argument("--size", type=int, default=1 << 20)
 ap.add_argument("--quanta", default="0,256,1024")
+ap.add_argument("--leads", default="64", help="KiB: a new read's first DATA frame ahead of the queue (0 = FIFO)")
 ap.add_argument("--protocol", default="grpc")
 args = ap.parse_args()
 n = pkg._native
 pl = affinity.plan(0, "same", 0) if torch.cuda.is_available() else {"client": [], "server": []}
 for rep in range(args.reps):
-    for q in [int(x) for x in args.quanta.split(",")]:
-        srv = n.Server({"port": 0, "md5": False, "retain_uploads": False, "h2_quantum": q << 10, "cpus": pl["server"]})
+    for q, lead in [(int(x), int(y)) for x in args.quanta.split(",") for y in args.leads.split(",")]:
+        srv = n.Server({"port": 0, "md5": False, "retain_uploads": False, "h2_quantum": q << 10,
+                        "h2_lead_bytes": lead << 10, "cpus": pl["server"]})
         srv.start()
         srv.add_synthetic("b", "f_", "", 0, args.workers, args.size)
         r = n.Runner({"protocol": args.protocol, "endpoint": srv.url, "bucket": "b", "object_prefix": "f_",
@@ -48,8 +50,9 @@ for rep in range(args.reps):
         s1 = srv.stats()
         fr = max(1, s1["h2_data_frames"] - s0["h2_data_frames"])
         rs = max(1, s1["h2_responses"] - s0["h2_responses"])
-        print(json.dumps({"rep": rep, "quantum_kib": q, "mib_s": round(s["bytes"] / el / 2**20, 1),
+        print(json.dumps({"rep": rep, "quantum_kib": q, "lead_kib": lead, "mib_s": round(s["bytes"] / el / 2**20, 1),
                           "p50_ms": round(s["p50_ms"], 3), "p99_ms": round(s["p99_ms"], 3),
+                          "ttfb_p50_ms": round(s["ttfb_p50_ms"], 3), "ttfb_p99_ms": round(s["ttfb_p99_ms"], 3),
                           "errors": s["errors"],
                           "queue_wait_avg_us": round((s1["h2_queue_wait_us"] - s0["h2_queue_wait_us"]) / fr, 1),
                           "queue_wait_max_us": s1["h2_queue_wait_max_us"],

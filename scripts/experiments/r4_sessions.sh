@@ -92,7 +92,8 @@ main6)  # ring footprint sweep; endpoint quantum at 48 streams; two benches
 main7)  # bounce receive (VERDICT r3 next #1b) against the direct ring, nodma and the baseline
   step pytest_bounce 300 python3 -u -m pytest tests/test_gpu_sink.py -x -q --timeout 120 --timeout-method thread -k "bounce or wc or byte_exact"
   step ab 600 python3 -u scripts/experiments/recv_cost_ab.py --tag main7 --reps 5 \
-    --variants head,head_4x2,head_bounce,head_bounce_4x2,head_bounce2,nodma,base
+    --variants head,head_2x2,head_4x1m,head_bounce,head_bounce_4x2,head_bounce2,nodma,base
+  step mux 300 python3 -u scripts/experiments/mux_fair_ab.py --quanta 0 --leads 0,64,16 --reps 3
   step bench1 600 python3 bench.py --ring-bounce on --json-out "$O/bench1.json"
   step bench2 600 python3 bench.py --slots 4 --json-out "$O/bench2.json"
   ;;

@@ -225,9 +225,6 @@ def build_parser() -> argparse.ArgumentParser:
                     help="pinned ring slot (one H2D copy + CRC launch each); 2 MiB x 8 measured best for one "
                          "stream per read (profiles/r2_single_stream)")
     ap.add_argument("--slots", type=int, default=8)
-    ap.add_argument("--ring-bounce", default="off", choices=["on", "off"],
-                    help="headline sink: receive into 3 recycled cacheable buffers, the submitter core moves each "
-                         "into its pinned slot with non-temporal stores before the H2D (profiles/r4_recvcost)")
     ap.add_argument("--async-submit", type=int, default=1, choices=[0, 1],
                     help="slot hand-off (H2D copy + CRC launches) on a per-device submitter thread instead of the "
                          "receiving thread: one stream per read is bound by its receiving core, so taking the HIP "
@@ -479,7 +476,6 @@ def run_rank(args) -> int:
         "device": gpu if use_gpu else 0,
         "ring_slot_bytes": parse_size(args.slot_bytes),
         "ring_slots": args.slots,
-        "ring_bounce": args.ring_bounce == "on",
         "landing": "object",
         "grpc_conn_pool_size": args.grpc_pool,
         "keep_records": False,

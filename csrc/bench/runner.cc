@@ -362,8 +362,6 @@ void Runner::worker_main(int w) {
       t.slot_waits += g.slot_waits;
       t.slot_wait_s += g.slot_wait_s;
       t.flag_reuses += g.flag_reuses;
-      t.bounce_waits += g.bounce_waits;
-      t.bounce_wait_s += g.bounce_wait_s;
     }
     std::lock_guard<std::mutex> lk(mu_);
     gpu_stats_[w] = t;
@@ -428,8 +426,6 @@ RunSummary Runner::summary(bool percentiles) const {
     s.gpu.slot_waits += g.slot_waits;
     s.gpu.slot_wait_s += g.slot_wait_s;
     s.gpu.flag_reuses += g.flag_reuses;
-    s.gpu.bounce_waits += g.bounce_waits;
-    s.gpu.bounce_wait_s += g.bounce_wait_s;
   }
   return s;
 }

@@ -25,9 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <condition_variable>
-#include <atomic>
 #include <cstdint>
-#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -83,17 +81,6 @@ struct GpuSinkConfig {
   // two A/B stages land nothing in HBM and verify nothing.
   enum class Stage { kH2D, kNone, kHostRead };
   Stage stage = Stage::kH2D;
-  // Receive into `bounce_bufs` recycled cacheable slot-sized buffers instead
-  // of the pinned slots; the device submitter moves each filled buffer into
-  // its pinned slot with non-temporal stores and then issues the H2D.  The
-  // receiving core then writes lines that stay in its CCD's caches, as the
-  // discard sink's recycled blocks do, and never lines the copy engine read
-  // (profiles/r4_recvcost: the same receive copy costs 0.036 CPU-s/GiB into
-  // a ring nothing reads and 0.044-0.048 into the ring the H2D reads); the
-  // second core pays the move, as the reference semantics' second core pays
-  // its CRC32C (VERDICT r3 next #1b).
-  bool bounce = false;
-  int bounce_bufs = 3;
 };
 
 struct GpuSinkStats {
@@ -105,8 +92,6 @@ struct GpuSinkStats {
   uint64_t slot_waits = 0;            // transport had to wait for a free slot
   double slot_wait_s = 0;
   uint64_t flag_reuses = 0;           // slots reused on the kernel's host-visible status (no HIP call)
-  uint64_t bounce_waits = 0;          // bounce: transport waited for the submitter's move
-  double bounce_wait_s = 0;
 };
 
 class GpuSink : public Sink {
@@ -168,14 +153,11 @@ class GpuSink : public Sink {
     uint64_t posted = 0, issued = 0;
     CrcSegResult* res = nullptr;  // host-mapped, kMaxSeg entries
     CrcSegResult* d_res = nullptr;  // device alias of res
-    int bounce = -1;              // bounce buffer holding this slot's bytes while FILLING
   };
   void enqueue_slot(Slot& s, uint8_t* dst, const CrcBatch* batch);
   void ensure_object_capacity(int64_t size);
   void grow_object_buffer(uint64_t need);
   Slot& take_slot();
-  int take_bounce();
-  uint8_t* fill_base(const Slot& s) const { return s.bounce >= 0 ? bounce_[s.bounce] : s.host; }
   void submit_current();
   void wait_slot(Slot& s);
   bool done_by_flags(const Slot& s) const;
@@ -218,12 +200,6 @@ class GpuSink : public Sink {
   uint32_t host_read_sink_ = 0;  // Stage::kHostRead's CRC (keeps the read)
   std::mutex sub_mu_;
   std::condition_variable sub_cv_;
-  // bounce buffers (cfg_.bounce): cacheable THP memory; busy from the
-  // hand-off until the submitter has moved the bytes into the pinned slot
-  std::vector<uint8_t*> bounce_;
-  std::unique_ptr<std::atomic<uint32_t>[]> bounce_busy_;
-  size_t bounce_len_ = 0;
-  int bounce_next_ = 0;
 };
 
 // Upload source for the write path (config 5): HBM -> pinned ring via

@@ -15,7 +15,6 @@
 #include <thread>
 #include <stdexcept>
 
-#include <immintrin.h>
 #include <sys/mman.h>
 #include <sys/prctl.h>
 #include <time.h>
@@ -520,72 +519,10 @@ CopyCeiling copy_ceiling(int device, bool h2d, size_t total, size_t chunk, int s
   return r;
 }
 
-namespace {
-// dst <- src with non-temporal stores (the lines go to memory, not into the
-// mover's caches, and whatever copy of them a cache held is dropped), then a
-// store fence so the copy engine's read sees them.  Both 64-byte aligned at
-// the start (slot and bounce buffers are 2 MiB-aligned, the copy starts at
-// offset 0 of both).
-__attribute__((target("avx2"))) void stream_copy_avx2(uint8_t* dst, const uint8_t* src, size_t n) {
-  size_t i = 0;
-  for (; i + 128 <= n; i += 128) {
-    const __m256i a = _mm256_load_si256(reinterpret_cast<const __m256i*>(src + i));
-    const __m256i b = _mm256_load_si256(reinterpret_cast<const __m256i*>(src + i + 32));
-    const __m256i c = _mm256_load_si256(reinterpret_cast<const __m256i*>(src + i + 64));
-    const __m256i d = _mm256_load_si256(reinterpret_cast<const __m256i*>(src + i + 96));
-    _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i), a);
-    _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i + 32), b);
-    _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i + 64), c);
-    _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i + 96), d);
-  }
-  if (i < n) std::memcpy(dst + i, src + i, n - i);
-  _mm_sfence();
-}
-
-void stream_copy_sse2(uint8_t* dst, const uint8_t* src, size_t n) {
-  size_t i = 0;
-  for (; i + 64 <= n; i += 64)
-    for (int k = 0; k < 64; k += 16)
-      _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + k),
-                       _mm_load_si128(reinterpret_cast<const __m128i*>(src + i + k)));
-  if (i < n) std::memcpy(dst + i, src + i, n - i);
-  _mm_sfence();
-}
-
-void stream_copy(uint8_t* dst, const uint8_t* src, size_t n) {
-  static const bool avx2 = __builtin_cpu_supports("avx2");
-  if (avx2)
-    stream_copy_avx2(dst, src, n);
-  else
-    stream_copy_sse2(dst, src, n);
-}
-
-// Cacheable page-aligned THP memory on `node` (bounce buffers: written by the
-// receive copy, read by the submitter's move; never registered with HIP).
-uint8_t* alloc_cached_thp(size_t len, int node) {
-  const size_t huge = size_t(2) << 20;
-  len = (len + huge - 1) / huge * huge;
-  void* raw = ::mmap(nullptr, len + huge, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
-  if (raw == MAP_FAILED) throw std::runtime_error("mmap(bounce) failed");
-  const uintptr_t a = (reinterpret_cast<uintptr_t>(raw) + huge - 1) & ~(huge - 1);
-  const size_t head = a - reinterpret_cast<uintptr_t>(raw);
-  if (head) ::munmap(raw, head);
-  if (huge - head) ::munmap(reinterpret_cast<void*>(a + len), huge - head);
-  void* p = reinterpret_cast<void*>(a);
-  (void)madvise(p, len, MADV_HUGEPAGE);
-  (void)bind_range_to_node(p, len, node < 0 ? current_numa_node() : node);
-  std::memset(p, 0, len);
-  return static_cast<uint8_t*>(p);
-}
-}  // namespace
-
 void GpuSink::set_device() const { ensure_device(cfg_.device); }
 
 GpuSink::GpuSink(const GpuSinkConfig& cfg) : cfg_(cfg) {
-  if (cfg_.stage != GpuSinkConfig::Stage::kH2D) {
-    cfg_.verify = false;
-    cfg_.bounce = false;
-  }
+  if (cfg_.stage != GpuSinkConfig::Stage::kH2D) cfg_.verify = false;
   if (cfg_.slots < 2) cfg_.slots = 2;
   cfg_.slot_bytes = (cfg_.slot_bytes + 4095) / 4096 * 4096;
   if (cfg_.slot_bytes < 65536) cfg_.slot_bytes = 65536;
@@ -621,15 +558,6 @@ GpuSink::GpuSink(const GpuSinkConfig& cfg) : cfg_(cfg) {
     s.res = res_host_ + static_cast<size_t>(i) * kMaxSeg;
     hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&s.d_res), s.res, 0), "hipHostGetDevicePointer");
   }
-  if (cfg_.bounce) {
-    const int nb = std::max(2, std::min(cfg_.bounce_bufs, cfg_.slots));
-    bounce_len_ = (cfg_.slot_bytes + (size_t(2) << 20) - 1) / (size_t(2) << 20) * (size_t(2) << 20);
-    bounce_busy_.reset(new std::atomic<uint32_t>[nb]);
-    for (int i = 0; i < nb; ++i) {
-      bounce_.push_back(alloc_cached_thp(cfg_.slot_bytes, device_numa_node(cfg_.device)));
-      bounce_busy_[i].store(0, std::memory_order_relaxed);
-    }
-  }
 }
 
 GpuSink::~GpuSink() {
@@ -643,7 +571,6 @@ GpuSink::~GpuSink() {
     if (s.dev_ring) (void)hipFree(s.dev_ring);
     if (s.ev) (void)hipEventDestroy(s.ev);
   }
-  for (uint8_t* b : bounce_) ::munmap(b, bounce_len_);
   if (res_host_) (void)hipHostFree(res_host_);
   if (d_tiles_) (void)hipFree(d_tiles_);
   if (own_obj_) (void)hipFree(own_obj_);
@@ -747,29 +674,9 @@ GpuSink::Slot& GpuSink::take_slot() {
   s.used = 0;
   s.segs.clear();
   s.obj_off = delivered_;
-  s.bounce = bounce_.empty() ? -1 : take_bounce();
   cur_ = next_;
   next_ = (next_ + 1) % cfg_.slots;
   return s;
-}
-
-// The next bounce buffer, once the submitter has moved its previous bytes
-// out (in hand-off order, so the oldest one).
-int GpuSink::take_bounce() {
-  const int b = bounce_next_;
-  bounce_next_ = (bounce_next_ + 1) % static_cast<int>(bounce_.size());
-  if (bounce_busy_[b].load(std::memory_order_acquire)) {
-    ++stats_.bounce_waits;
-    const int64_t t0 = now_ns();
-    // the move takes tens of microseconds: poll briefly before sleeping
-    while (bounce_busy_[b].load(std::memory_order_acquire) && now_ns() - t0 < 20000) __builtin_ia32_pause();
-    if (bounce_busy_[b].load(std::memory_order_acquire)) {
-      std::unique_lock<std::mutex> lk(sub_mu_);
-      sub_cv_.wait(lk, [&] { return bounce_busy_[b].load(std::memory_order_acquire) == 0; });
-    }
-    stats_.bounce_wait_s += (now_ns() - t0) / 1e9;
-  }
-  return b;
 }
 
 Window GpuSink::acquire(size_t want) {
@@ -802,7 +709,7 @@ Window GpuSink::acquire(size_t want) {
     if (obj_cap_ - delivered_ < cap) cap = obj_cap_ - delivered_;
   }
   // keep a segment below 4 GiB (32-bit length in the kernel batch)
-  return Window{fill_base(s) + s.used, cap};
+  return Window{s.host + s.used, cap};
 }
 
 void GpuSink::commit(size_t n) {
@@ -868,12 +775,8 @@ void GpuSink::submit_current() {
   Slot& s = slots_[cur_];
   cur_ = -1;
   if (s.used == 0) {
-    // nothing landed: hand the slot (and its bounce buffer) back
+    // nothing landed: hand the slot back (it is the one next_ points behind)
     next_ = static_cast<int>((next_ + cfg_.slots - 1) % cfg_.slots);
-    if (s.bounce >= 0) {
-      bounce_next_ = s.bounce;
-      s.bounce = -1;
-    }
     return;
   }
   if (!s.segs.empty()) s.segs.back().closed = true;
@@ -904,18 +807,7 @@ void GpuSink::submit_current() {
 // The slot's H2D copy, CRC launches and completion event.  Runs on the
 // device submitter thread (async_submit) or inline.
 void GpuSink::enqueue_slot(Slot& s, uint8_t* dst, const CrcBatch* batch) {
-  const int bounce = s.bounce;
-  s.bounce = -1;
-  if (bounce >= 0) bounce_busy_[bounce].store(1, std::memory_order_release);
-  auto issue = [this, &s, dst, bounce](const CrcBatch* b) {
-    if (bounce >= 0) {
-      // move the received bytes into the pinned slot, then free the bounce
-      // buffer for the receiving thread before any HIP call
-      stream_copy(s.host, bounce_[bounce], s.used);
-      bounce_busy_[bounce].store(0, std::memory_order_release);
-      { std::lock_guard<std::mutex> lk(sub_mu_); }
-      sub_cv_.notify_all();
-    }
+  auto issue = [this, &s, dst](const CrcBatch* b) {
     if (cfg_.stage == GpuSinkConfig::Stage::kHostRead) {
       host_read_sink_ = crc32c_extend(host_read_sink_, s.host, s.used);
       return;

@@ -91,8 +91,6 @@ GpuSinkConfig gpu_from(const py::dict& d) {
   g.blocking_sync = get_or<bool>(d, "blocking_sync", g.blocking_sync);
   g.wait_poll_us = get_or<int>(d, "wait_poll_us", g.wait_poll_us);
   g.ring_wc = get_or<bool>(d, "ring_wc", g.ring_wc);
-  g.bounce = get_or<bool>(d, "ring_bounce", g.bounce);
-  g.bounce_bufs = get_or<int>(d, "bounce_bufs", g.bounce_bufs);
   const std::string stage = get_or<std::string>(d, "gpu_stage", "h2d");
   if (stage == "none") g.stage = GpuSinkConfig::Stage::kNone;
   else if (stage == "host_read") g.stage = GpuSinkConfig::Stage::kHostRead;
@@ -166,8 +164,6 @@ py::dict gpu_stats_dict(const GpuSinkStats& g) {
   r["slot_waits"] = g.slot_waits;
   r["slot_wait_s"] = g.slot_wait_s;
   r["flag_reuses"] = g.flag_reuses;
-  r["bounce_waits"] = g.bounce_waits;
-  r["bounce_wait_s"] = g.bounce_wait_s;
   return r;
 }
 
@@ -580,7 +576,6 @@ class PyServer {
     c.zero_copy = get_or<bool>(d, "zero_copy", true);
     c.send_vmsplice = get_or<std::string>(d, "send_source", "vmsplice") != "sendfile";
     c.h2_quantum = get_or<size_t>(d, "h2_quantum", c.h2_quantum);
-    c.h2_lead_bytes = get_or<size_t>(d, "h2_lead_bytes", c.h2_lead_bytes);
     c.tls_cert_file = get_or<std::string>(d, "tls_cert_file", "");
     c.tls_key_file = get_or<std::string>(d, "tls_key_file", "");
     if (d.contains("cpus") && !d["cpus"].is_none()) c.cpus = d["cpus"].cast<std::vector<int>>();

@@ -52,13 +52,12 @@ struct ServerConfig {
   // (H2Writer::set_quantum and the send scheduler's turn; 0 = a whole
   // message per turn).  ReadObject messages are <= 2 MiB and the scheduler
   // already serves streams round-robin a message at a time: 256 KiB frames
-  // cost the 48-stream block 15-30% with no better tail (profiles/r4_mux).
+  // cost the 48-stream block 15-30% with no better tail (profiles/r4_main6).
+  // A new read's first frame sent ahead of the queue did not lower its TTFB
+  // either: at 48 streams the ~2 ms before a read's first byte is the
+  // connection's bytes in flight in the socket buffers, not the endpoint's
+  // queue (profiles/r4_main7 mux; endpoint request -> HEADERS 10-30 us).
   size_t h2_quantum = 0;
-  // HTTP/2: a new read's first DATA frame (at most this many bytes) is sent
-  // ahead of the messages already queued, so its TTFB is the request's
-  // handling, not the ~2 ms of other streams' messages ahead of it at 48
-  // streams; the rest of the body joins the round-robin (0 = plain FIFO).
-  size_t h2_lead_bytes = 64 << 10;
   // https / gRPC over TLS (ALPN h2 or http/1.1) when both are set (PEM files)
   std::string tls_cert_file, tls_key_file;
 };

@@ -498,7 +498,6 @@ class H2ServerConn {
     uint64_t off = 0, end = 0, chunk = 0, sent = 0;
     const std::string *checksums = nullptr, *range = nullptr, *meta = nullptr;
     bool first = true, headers_sent = false;
-    bool lead = true;  // the first DATA turn: at most h2_lead_bytes, ahead of the queue
     // the message being sent: its pieces and the position inside them
     v2::ReadResponseFrame fr;
     uint8_t pre[5] = {0, 0, 0, 0, 0};
@@ -515,13 +514,7 @@ class H2ServerConn {
     {
       std::lock_guard<std::mutex> lk(smu_);
       if (!sender_.joinable()) sender_ = std::thread([this] { sender_loop(); });
-      // a new read's first frame goes ahead of the messages already queued
-      // (its TTFB is then the request's handling, not the queue ahead of
-      // it); the rest of its body joins the round-robin at the back
-      if (srv_.config().h2_lead_bytes > 0)
-        jobs_.push_front(&j);
-      else
-        jobs_.push_back(&j);
+      jobs_.push_back(&j);
     }
     scv_.notify_one();
     std::unique_lock<std::mutex> lk(j.mu);
@@ -588,7 +581,6 @@ class H2ServerConn {
     if (!j.msg_open) open_message(j);
     size_t want = j.left;
     if (active > 1 && srv_.config().h2_quantum > 0) want = std::min(want, srv_.config().h2_quantum);
-    if (j.lead && active > 1 && srv_.config().h2_lead_bytes > 0) want = std::min(want, srv_.config().h2_lead_bytes);
     bool gone = false;
     const size_t n = w_.try_reserve(s.id, want, &gone);
     if (gone) throw Cancelled{};
@@ -611,7 +603,6 @@ class H2ServerConn {
       }
     }
     w_.write_frame_pieces(h2::kData, 0, s.id, frame, n);
-    j.lead = false;
     j.left -= n;
     if (j.left > 0) return 0;
     j.msg_open = false;

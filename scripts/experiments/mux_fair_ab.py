@@ -23,7 +23,9 @@ ap.add_argument("--reads", type=int, default=50)
 ap.add_argument("--workers", type=int, default=48)
 ap.add_argument("--size", type=int, default=1 << 20)
 ap.add_argument("--quanta", default="0,256,1024")
-ap.add_argument("--leads", default="64", help="KiB: a new read's first DATA frame ahead of the queue (0 = FIFO)")
+ap.add_argument("--leads", default="0",
+                help="KiB: a new read's first DATA frame ahead of the queue (h2_lead_bytes, removed after "
+                     "profiles/r4_main7: only 0 runs on today's endpoint)")
 ap.add_argument("--protocol", default="grpc")
 args = ap.parse_args()
 n = pkg._native

@@ -90,12 +90,20 @@ main6)  # ring footprint sweep; endpoint quantum at 48 streams; two benches
   step bench2 600 python3 bench.py --json-out "$O/bench2.json"
   ;;
 main7)  # bounce receive (VERDICT r3 next #1b) against the direct ring, nodma and the baseline
+  # (ring_bounce was removed after this session, profiles/r4_recvcost; the variants below no longer exist)
   step pytest_bounce 300 python3 -u -m pytest tests/test_gpu_sink.py -x -q --timeout 120 --timeout-method thread -k "bounce or wc or byte_exact"
   step ab 600 python3 -u scripts/experiments/recv_cost_ab.py --tag main7 --reps 5 \
     --variants head,head_2x2,head_4x1m,head_bounce,head_bounce_4x2,head_bounce2,nodma,base
   step mux 300 python3 -u scripts/experiments/mux_fair_ab.py --quanta 0 --leads 0,64,16 --reps 3
   step bench1 600 python3 bench.py --ring-bounce on --json-out "$O/bench1.json"
   step bench2 600 python3 bench.py --slots 4 --json-out "$O/bench2.json"
+  ;;
+main8)  # small ring footprints (main6/main7: 4 MiB rings read 4-9% faster than 16 MiB); bench on 4 x 1 MiB
+  step ab 600 python3 -u scripts/experiments/recv_cost_ab.py --tag main8 --reps 5 \
+    --variants head,head_4x1m,head_3x1m,head_2x1m,head_6x1m,head_4x512k,head_8x256k,nodma,base
+  step bench1 600 python3 bench.py --slot-bytes 1MiB --slots 4 --json-out "$O/bench1.json"
+  step bench2 600 python3 bench.py --json-out "$O/bench2.json"
+  step bench3 600 python3 bench.py --slot-bytes 1MiB --slots 4 --json-out "$O/bench3.json"
   ;;
 soak)  # profiles/r4_soak: execute_pb.sh with 48 workers x 100 MiB, -sink gpu, 120 s per protocol, exporter at 30 s
   step soak 900 python3 -u scripts/soak.py --out "$O" --duration 120s

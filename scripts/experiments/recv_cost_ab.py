@@ -9,8 +9,6 @@ interleaved `--reps` times in one process:
   head_wc   the same, ring in write-combined pinned memory
   head_4m   the same, 4 x 4 MiB slots
   head_4x2  the same, 4 x 2 MiB slots (the discard sink's 8 MiB footprint)
-  head_bounce  the receive lands in 3 recycled cacheable 2 MiB buffers; the
-            submitter core moves each into its pinned slot, then the H2D
   head_refill  the same, recv_refill (one recvmsg per DATA frame tail + next header)
   head_spin the same, the device submitter polls 200 us before it sleeps
   nodma     the same ring, filled by the same receive path, handed straight
@@ -79,11 +77,11 @@ variants = {
     "head_4x1m": {"sink": "gpu", "ring_slot_bytes": 1 << 20, "ring_slots": 4},
     "head_8x512k": {"sink": "gpu", "ring_slot_bytes": 512 << 10, "ring_slots": 8},
     "head_4x2_wc": {"sink": "gpu", "ring_slots": 4, "ring_wc": True},
-    # receive into 3 recycled cacheable bounce buffers; the submitter core
-    # moves each into its pinned slot (non-temporal stores), then the H2D
-    "head_bounce": {"sink": "gpu", "ring_bounce": True},
-    "head_bounce_4x2": {"sink": "gpu", "ring_bounce": True, "ring_slots": 4},
-    "head_bounce2": {"sink": "gpu", "ring_bounce": True, "bounce_bufs": 2},
+    "head_2x1m": {"sink": "gpu", "ring_slot_bytes": 1 << 20, "ring_slots": 2},
+    "head_3x1m": {"sink": "gpu", "ring_slot_bytes": 1 << 20, "ring_slots": 3},
+    "head_6x1m": {"sink": "gpu", "ring_slot_bytes": 1 << 20, "ring_slots": 6},
+    "head_4x512k": {"sink": "gpu", "ring_slot_bytes": 512 << 10, "ring_slots": 4},
+    "head_8x256k": {"sink": "gpu", "ring_slot_bytes": 256 << 10, "ring_slots": 8},
     # the headline with the next frame header read in the payload's recvmsg
     "head_refill": {"sink": "gpu", "recv_refill": True},
     # the headline with the device submitter polling 200 us for the next

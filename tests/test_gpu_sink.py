@@ -301,33 +301,3 @@ def test_write_combined_ring_byte_exact(native, server, gpu_available):
     sink = native.GpuSink({"device": 0, "ring_slot_bytes": 1 << 20, "ring_slots": 2, "ring_wc": True})
     r = c.read_gpu(B, P + "0", sink)
     assert r["crc_mismatch"] and not r["verified"]
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("slots,bufs", [(2, 2), (4, 3), (8, 3)])
-def test_bounce_ring_byte_exact(native, server, gpu_available, slots, bufs):
-    """ring_bounce: the receive lands in cacheable bounce buffers and the
-    device submitter moves each into its pinned slot (non-temporal stores)
-    before the H2D.  Same bytes and CRC checks as the direct ring, over
-    reads that reuse the sink, odd sizes (a tail that is not a 128-byte
-    multiple), and corruption is still caught."""
-    import torch
-
-    size = (7 << 20) + 4099
-    server.add_synthetic(B, P, "", 0, 1, size)
-    cfg = {"device": 0, "ring_slot_bytes": 1 << 20, "ring_slots": slots, "ring_bounce": True, "bounce_bufs": bufs}
-    for proto in _protocols(native):
-        c = native.Client({"protocol": proto, "endpoint": server.url})
-        t = torch.empty(size, dtype=torch.uint8, device="cuda:0")
-        sink = native.GpuSink(cfg)
-        sink.set_external_destination(t.data_ptr(), t.numel())
-        for _ in range(3):
-            t.zero_()
-            r = c.read_gpu(B, P + "0", sink)
-            assert r["verified"] and not r["crc_mismatch"] and r["bytes"] == size, r
-            bad, first = native.gpu_verify_pattern(0, t.data_ptr(), size, P + "0", 0)
-            assert bad == 0, (proto, first)
-    server.set_faults({"corrupt_at": (3 << 20) + 5, "corrupt_count": 1})
-    c = native.Client({"protocol": "grpc", "endpoint": server.url})
-    r = c.read_gpu(B, P + "0", native.GpuSink(cfg))
-    assert r["crc_mismatch"] and not r["verified"]

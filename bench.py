@@ -221,10 +221,11 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--object-size", default="256MiB")
     ap.add_argument("--workers", type=int, default=1, help="readers per GPU (config: 1)")
     ap.add_argument("--sink", default="gpu", help="gpu (HBM landing + GPU CRC) | discard (CPU baseline)")
-    ap.add_argument("--slot-bytes", default="2MiB",
-                    help="pinned ring slot (one H2D copy + CRC launch each); 2 MiB x 8 measured best for one "
-                         "stream per read (profiles/r2_single_stream)")
-    ap.add_argument("--slots", type=int, default=8)
+    ap.add_argument("--slot-bytes", default="1MiB",
+                    help="pinned ring slot (one H2D copy + CRC launch each). 4 x 1 MiB: the copy engine reads lines "
+                         "still in the receiving CCD's L3; against 8 x 2 MiB the receive copy went 0.046 -> 0.036 "
+                         "CPU-s/GiB, 22.0k -> 27.5k MiB/s interleaved (profiles/r4_main8, profiles/r4_recvcost)")
+    ap.add_argument("--slots", type=int, default=4)
     ap.add_argument("--async-submit", type=int, default=1, choices=[0, 1],
                     help="slot hand-off (H2D copy + CRC launches) on a per-device submitter thread instead of the "
                          "receiving thread: one stream per read is bound by its receiving core, so taking the HIP "

@@ -148,14 +148,17 @@ def auto_ring(workers: int, slices: int) -> tuple[int, int]:
 
     The receive copy write-allocates its destination, so the rings' total
     footprint matters: a 32 MiB ring cost one receiving core 25-35%
-    (profiles/r3_ring_thp). One worker gets the headline's 8 x 2 MiB; several
+    (profiles/r3_ring_thp). One worker gets the headline's 4 x 1 MiB: the copy
+    engine then reads lines still in the receiving CCD's L3, which took the
+    receive copy from 0.046 to 0.036 CPU-s/GiB and 22.0k to 27.5k MiB/s
+    against 8 x 2 MiB (profiles/r4_main8, r4_recvcost); several
     get 2 x 1 MiB each (8 list-readers: 18.6-18.8k MiB/s against 15.5-17.0k
     with 8 x 2 MiB, profiles/r3_mux_thp/listring); sliced reads 2 x 2 MiB per
     slice sink (profiles/r3_ring_thp/sliced)."""
     if slices > 1:
         return 2 << 20, 2
     if workers == 1:
-        return 2 << 20, 8
+        return 1 << 20, 4
     return 1 << 20, 2
 
 

@@ -105,6 +105,18 @@ main8)  # small ring footprints (main6/main7: 4 MiB rings read 4-9% faster than 
   step bench2 600 python3 bench.py --json-out "$O/bench2.json"
   step bench3 600 python3 bench.py --slot-bytes 1MiB --slots 4 --json-out "$O/bench3.json"
   ;;
+main9)  # round-4 checkpoint on the 4 x 1 MiB default: GPU suite, smoke, A/B (submitter polling at 1 MiB
+  # slots), two benches, one bench under rocprofv3 --kernel-trace --stats, 100-read diag
+  step pytest_gpu 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+  step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+  step ab 500 python3 -u scripts/experiments/recv_cost_ab.py --tag main9 --reps 5 \
+    --variants head_4x1m,head_4x1m_spin,head_3x1m,head,nodma,base
+  step bench1 600 python3 bench.py --json-out "$O/bench1.json"
+  step bench2 600 python3 bench.py --json-out "$O/bench2.json"
+  step prof 600 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run -- python3 bench.py --steps 20 --warmup 3 \
+    --blocks ceiling --json-out "$O/bench_prof.json"
+  step diag100 400 python3 bench.py --steps 100 --warmup 3 --side-steps 0 --read-diag --json-out "$O/diag100.json"
+  ;;
 soak)  # profiles/r4_soak: execute_pb.sh with 48 workers x 100 MiB, -sink gpu, 120 s per protocol, exporter at 30 s
   step soak 900 python3 -u scripts/soak.py --out "$O" --duration 120s
   ;;

@@ -87,8 +87,9 @@ variants = {
     # the headline with the device submitter polling 200 us for the next
     # hand-off before it sleeps (no futex wake per slot on the receiver)
     "head_spin": {"sink": "gpu"},
+    "head_4x1m_spin": {"sink": "gpu", "ring_slot_bytes": 1 << 20, "ring_slots": 4},
 }
-SPIN_US = {"head_spin": 200}
+SPIN_US = {"head_spin": 200, "head_4x1m_spin": 200}
 names = [v for v in args.variants.split(",") if v]
 runners = {k: n.Runner({**base, **variants[k]}) for k in names}
 for r in runners.values():  # warm: connections, rings, sinks

@@ -23,7 +23,7 @@ def test_auto_affinity(args, want):
 
 
 def test_auto_ring_keeps_the_receive_destinations_small():
-    assert auto_ring(1, 1) == (2 << 20, 8)     # the headline's ring
+    assert auto_ring(1, 1) == (1 << 20, 4)     # the headline's ring (r4_main8)
     assert auto_ring(8, 1) == (1 << 20, 2)     # r3_mux_thp/listring
     assert auto_ring(48, 1) == (1 << 20, 2)
     assert auto_ring(1, 8) == (2 << 20, 2)     # r3_ring_thp/sliced

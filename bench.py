@@ -226,6 +226,8 @@ def build_parser() -> argparse.ArgumentParser:
                          "still in the receiving CCD's L3; against 8 x 2 MiB the receive copy went 0.046 -> 0.036 "
                          "CPU-s/GiB, 22.0k -> 27.5k MiB/s interleaved (profiles/r4_main8, profiles/r4_recvcost)")
     ap.add_argument("--slots", type=int, default=4)
+    ap.add_argument("--crc-slot-waves", type=int, default=0, choices=[0, 1, 2, 4, 8],
+                    help="slot CRC kernel waves per workgroup (0: by slot size); A/B of the kernel's table staging")
     ap.add_argument("--async-submit", type=int, default=1, choices=[0, 1],
                     help="slot hand-off (H2D copy + CRC launches) on a per-device submitter thread instead of the "
                          "receiving thread: one stream per read is bound by its receiving core, so taking the HIP "
@@ -458,6 +460,8 @@ def run_rank(args) -> int:
     placement = affinity.plan(gpu, aff, slot) if use_gpu else {"client": [], "server": []}
     if use_gpu and args.submit_cpus == "aux" and placement.get("aux"):
         n.set_submitter_cpus(placement["aux"])
+    if use_gpu and args.crc_slot_waves:
+        n.set_crc_options({"slot_waves": args.crc_slot_waves})
     srv = n.Server({"port": 0, "md5": False, "cpus": placement["server"], "retain_uploads": False})
     srv.start()
     bucket = "princer-working-dirs"

@@ -113,9 +113,15 @@ main9)  # round-4 checkpoint on the 4 x 1 MiB default: GPU suite, smoke, A/B (su
     --variants head_4x1m,head_4x1m_spin,head_3x1m,head,nodma,base
   step bench1 600 python3 bench.py --json-out "$O/bench1.json"
   step bench2 600 python3 bench.py --json-out "$O/bench2.json"
-  step prof 600 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run -- python3 bench.py --steps 20 --warmup 3 \
+  step prof 600 rocprofv3 --kernel-trace --stats -f csv -d "$O/prof" -o run -- python3 bench.py --steps 20 --warmup 3 \
     --blocks ceiling --json-out "$O/bench_prof.json"
   step diag100 400 python3 bench.py --steps 100 --warmup 3 --side-steps 0 --read-diag --json-out "$O/diag100.json"
+  ;;
+crcw)  # slot CRC kernel on 1 MiB slots inside the read pipeline: waves per workgroup
+  for w in 1 2 4 8; do
+    step "prof_w$w" 300 rocprofv3 --kernel-trace --stats -f csv -d "$O/prof_w$w" -o run -- python3 bench.py --steps 20 \
+      --warmup 3 --blocks ceiling --crc-slot-waves $w --json-out "$O/bench_w$w.json"
+  done
   ;;
 soak)  # profiles/r4_soak: execute_pb.sh with 48 workers x 100 MiB, -sink gpu, 120 s per protocol, exporter at 30 s
   step soak 900 python3 -u scripts/soak.py --out "$O" --duration 120s

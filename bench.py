@@ -1015,7 +1015,10 @@ def run_rank(args) -> int:
     if args.workload == "read":
         # --read-diag samples the headline's threads around every read (one
         # reader: a handful of threads; not the 48-worker blocks)
-        head = read_block({"read_diag": bool(args.read_diag)}, args.steps, args.warmup, "headline")
+        diag_avoid = sorted(set(placement.get("client", [])) | set(placement.get("server", []))
+                            | set(placement.get("aux", []) or []))
+        head = read_block({"read_diag": bool(args.read_diag), "diag_avoid_cpus": diag_avoid}, args.steps, args.warmup,
+                          "headline")
         headline_model = (f"{protocol} ReadObject {args.object_size} object, "
                           f"{'one stream per read' if args.slices == 1 else f'{args.slices} ranged streams'}"
                           + (" -> HBM (CRC32C on GPU)" if use_gpu else " -> discard (CPU baseline)"))

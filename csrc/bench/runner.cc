@@ -283,6 +283,8 @@ void Runner::worker_main(int w) {
                                     ? ~0ull
                                     : static_cast<uint64_t>(cfg_.trace_sample_rate * 9223372036854775808.0);
   const int64_t t_begin = now_ns();
+  std::vector<int> diag_avoid = cfg_.diag_avoid_cpus;
+  diag_avoid.insert(diag_avoid.end(), cfg_.client.cpus.begin(), cfg_.client.cpus.end());
   for (int64_t i = 0; i < cfg_.reads_per_worker; ++i) {
     if (stop_flag_) break;
     if (cfg_.duration_s > 0 && (now_ns() - t_begin) / 1e9 >= cfg_.duration_s) break;
@@ -301,7 +303,7 @@ void Runner::worker_main(int w) {
     static const std::vector<std::string> kDiagThreads = {"gcsb-h2-reader", "gcsb-srv", "gcsb-worker",
                                                           "gcsb-submit", "gcsb-slice"};
     SchedSample diag0;
-    if (cfg_.read_diag) diag0 = sched_sample(kDiagThreads);
+    if (cfg_.read_diag) diag0 = sched_sample_offcore(kDiagThreads, diag_avoid);
     RoctxRange rg(sliced ? "gcsb.read_object(sliced)" : "gcsb.read_object");
     r.start_wall_ns = wall_ns();
     r.start_ns = now_ns();
@@ -330,7 +332,8 @@ void Runner::worker_main(int w) {
       r.end_ns = now_ns();
       r.error = e.what();
     }
-    if (cfg_.read_diag) r.diag = std::make_shared<ReadSchedDiag>(sched_delta(diag0, sched_sample(kDiagThreads)));
+    if (cfg_.read_diag)
+      r.diag = std::make_shared<ReadSchedDiag>(sched_delta(diag0, sched_sample_offcore(kDiagThreads, diag_avoid)));
     ms = (r.end_ns - r.start_ns) / 1e6;
     host_ms = r.host_done_ns ? (r.host_done_ns - r.start_ns) / 1e6 : ms;
     if (r.ok && cfg_.latency_fd >= 0) {

@@ -70,6 +70,9 @@ struct RunnerConfig {
   // their deltas (RunSummary::slowest_diag).  Off by default: ~tens of us
   // per read, outside the read's latency but inside the run's wall time.
   bool read_diag = false;
+  // CPUs the read_diag sampler must not run on (the placement's; the client
+  // CPUs are always added): sched_sample_offcore
+  std::vector<int> diag_avoid_cpus;
 };
 
 struct ReadRecord {

@@ -1,11 +1,15 @@
 #include "core/sched_probe.h"
 
+#include <sched.h>
 #include <sys/syscall.h>
 #include <unistd.h>
 
 #include <time.h>
 
 #include <algorithm>
+#include <condition_variable>
+#include <functional>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -168,6 +172,73 @@ SchedSample sched_sample(const std::vector<std::string>& prefixes) {
   read_proto_table("/proc/net/snmp", "Tcp:", {"RetransSegs"}, &s.tcp);
   read_proto_table("/proc/net/netstat", "TcpExt:", {"TCPLossProbes", "TCPTimeouts"}, &s.tcp);
   return s;
+}
+
+namespace {
+// One helper thread per process; requests are served one at a time.
+struct OffcoreSampler {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::function<void()> job;
+  bool busy = false;
+  std::vector<int> avoid;
+  bool started = false;
+
+  void run() {
+    // this thread is not registered: it never samples itself
+    std::vector<int> cur;
+    std::unique_lock<std::mutex> lk(mu);
+    for (;;) {
+      cv.wait(lk, [&] { return static_cast<bool>(job); });
+      if (avoid != cur) {
+        cur = avoid;
+        cpu_set_t set;
+        CPU_ZERO(&set);
+        if (sched_getaffinity(0, sizeof(set), &set) == 0) {
+          cpu_set_t keep = set;
+          for (int c : cur)
+            if (c >= 0 && c < CPU_SETSIZE) CPU_CLR(c, &keep);
+          if (CPU_COUNT(&keep) > 0) sched_setaffinity(0, sizeof(keep), &keep);
+        }
+      }
+      auto f = std::move(job);
+      job = nullptr;
+      lk.unlock();
+      f();
+      lk.lock();
+      busy = false;
+      cv.notify_all();
+    }
+  }
+};
+
+OffcoreSampler& offcore() {
+  static auto* s = new OffcoreSampler();  // process lifetime (detached thread)
+  return *s;
+}
+}  // namespace
+
+SchedSample sched_sample_offcore(const std::vector<std::string>& prefixes, const std::vector<int>& avoid) {
+  OffcoreSampler& o = offcore();
+  SchedSample out;
+  std::unique_lock<std::mutex> lk(o.mu);
+  if (!o.started) {
+    o.started = true;
+    std::thread([&o] { o.run(); }).detach();
+  }
+  o.cv.wait(lk, [&] { return !o.busy; });
+  o.busy = true;
+  bool done = false;
+  o.avoid = avoid;
+  o.job = [&] {
+    SchedSample x = sched_sample(prefixes);
+    std::lock_guard<std::mutex> g(o.mu);
+    out = std::move(x);
+    done = true;
+  };
+  o.cv.notify_all();
+  o.cv.wait(lk, [&] { return done; });
+  return out;
 }
 
 ReadSchedDiag sched_delta(const SchedSample& a, const SchedSample& b) {

@@ -47,6 +47,12 @@ struct SchedSample {
 // they last ran on.
 SchedSample sched_sample(const std::vector<std::string>& prefixes);
 
+// The same sample, taken by a helper thread kept off `avoid` (the measured
+// placement's CPUs): reading ~30 /proc files costs ~0.5 ms of CPU, which on
+// the receiving core's SMT sibling slowed the very reads it attributes
+// (profiles/r4_main9 diag100).  The caller blocks meanwhile.
+SchedSample sched_sample_offcore(const std::vector<std::string>& prefixes, const std::vector<int>& avoid);
+
 // One read's deltas between two samples, per thread name (summed over
 // threads of that name): run-queue delay, involuntary switches, CPU time,
 // and the softirqs on the CPUs the receiving / sending threads used.

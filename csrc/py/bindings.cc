@@ -470,6 +470,8 @@ class PyRunner {
     c.latency_fd = get_or<int>(d, "latency_fd", -1);
     c.keep_records = get_or<bool>(d, "keep_records", true);
     c.read_diag = get_or<bool>(d, "read_diag", false);
+    if (d.contains("diag_avoid_cpus") && !d["diag_avoid_cpus"].is_none())
+      c.diag_avoid_cpus = d["diag_avoid_cpus"].cast<std::vector<int>>();
     c.stop_on_error = get_or<bool>(d, "stop_on_error", true);
     c.trace_sample_rate = get_or<double>(d, "trace_sample_rate", 0.0);
     c.range_offset = get_or<int64_t>(d, "range_offset", 0);

@@ -522,11 +522,12 @@ class H2ServerConn {
   }
 
   static void finish_job(BodyJob& j, bool failed) {
-    {
-      std::lock_guard<std::mutex> lk(j.mu);
-      j.failed = failed;
-      j.done = true;
-    }
+    // notify under the lock: the handler owns j (on its stack) and may
+    // destroy it as soon as it sees done, so nothing here may touch j after
+    // the unlock
+    std::lock_guard<std::mutex> lk(j.mu);
+    j.failed = failed;
+    j.done = true;
     j.cv.notify_one();
   }
 

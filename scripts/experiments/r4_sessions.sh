@@ -123,6 +123,14 @@ crcw)  # slot CRC kernel on 1 MiB slots inside the read pipeline: waves per work
       --warmup 3 --blocks ceiling --crc-slot-waves $w --json-out "$O/bench_w$w.json"
   done
   ;;
+refring)  # 48 workers x 100 MiB into HBM: per-worker ring footprint (the multiplexed reader's copy destinations)
+  for k in 1 2; do
+    for r in 2x2MiB 4x256KiB 2x512KiB 4x512KiB; do
+      step "ref_${r}_$k" 300 python3 bench.py --steps 5 --warmup 1 --blocks ref_default_100m --ref-gpu-ring $r \
+        --json-out "$O/ref_${r}_$k.json"
+    done
+  done
+  ;;
 soak)  # profiles/r4_soak: execute_pb.sh with 48 workers x 100 MiB, -sink gpu, 120 s per protocol, exporter at 30 s
   step soak 900 python3 -u scripts/soak.py --out "$O" --duration 120s
   ;;

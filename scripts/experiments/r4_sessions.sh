@@ -131,6 +131,14 @@ refring)  # 48 workers x 100 MiB into HBM: per-worker ring footprint (the multip
     done
   done
   ;;
+muxiso)  # the multiplexed gRPC reader on a core of its own, after the pacing fix (r3: mixed)
+  for k in 1 2 3; do
+    for m in shared isolate; do
+      step "mux_${m}_$k" 300 python3 bench.py --steps 5 --warmup 1 --blocks ref_default,ref_default_100m,list_read \
+        --mux-reader $m --json-out "$O/mux_${m}_$k.json"
+    done
+  done
+  ;;
 soak)  # profiles/r4_soak: execute_pb.sh with 48 workers x 100 MiB, -sink gpu, 120 s per protocol, exporter at 30 s
   step soak 900 python3 -u scripts/soak.py --out "$O" --duration 120s
   ;;

@@ -170,7 +170,8 @@ SchedSample sched_sample(const std::vector<std::string>& prefixes) {
   }
   s.softirqs = read_softirqs(cpus);
   read_proto_table("/proc/net/snmp", "Tcp:", {"RetransSegs"}, &s.tcp);
-  read_proto_table("/proc/net/netstat", "TcpExt:", {"TCPLossProbes", "TCPTimeouts"}, &s.tcp);
+  read_proto_table("/proc/net/netstat", "TcpExt:",
+                   {"TCPLossProbes", "TCPTimeouts", "PruneCalled", "RcvPruned", "TCPRcvQDrop", "TCPBacklogDrop"}, &s.tcp);
   return s;
 }
 

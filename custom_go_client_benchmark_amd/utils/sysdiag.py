@@ -152,6 +152,38 @@ def table_delta(a: tuple, b: tuple, cpus: list[int] | None, reads: int = 1, top:
             "by_cpu_per_read": {str(c): round(v / r, 2) for c, v in sorted(by_cpu.items())}}
 
 
+# namespace-wide TCP counters that explain a stalled loopback stream: a
+# retransmission timeout (RTO, >= 200 ms), tail-loss probes, and the receive
+# queue pruning / dropping that precedes them when skb memory (truesize)
+# outgrows the socket's receive buffer
+TCP_COUNTERS = {"Tcp": ("RetransSegs",),
+                "TcpExt": ("TCPTimeouts", "TCPLossProbes", "PruneCalled", "RcvPruned", "TCPRcvQDrop",
+                           "TCPRcvCollapsed", "TCPBacklogDrop", "TCPZeroWindowDrop", "TCPOFODrop")}
+
+
+def tcp_snapshot() -> dict[str, int]:
+    out: dict[str, int] = {}
+    for path in ("/proc/net/snmp", "/proc/net/netstat"):
+        text = _read(path)
+        if not text:
+            continue
+        lines = text.splitlines()
+        for names, vals in zip(lines[::2], lines[1::2]):
+            proto, _, hdr = names.partition(":")
+            want = TCP_COUNTERS.get(proto)
+            if not want:
+                continue
+            for k, v in zip(hdr.split(), vals.partition(":")[2].split()):
+                if k in want and v.lstrip("-").isdigit():
+                    out[k] = int(v)
+    return out
+
+
+def tcp_delta(a: dict[str, int], b: dict[str, int]) -> dict[str, int]:
+    """Non-zero counter increases between two tcp_snapshot()s."""
+    return {k: b[k] - a.get(k, 0) for k in b if b[k] - a.get(k, 0) > 0}
+
+
 def attribute(diag: dict, ms: float, p50_ms: float) -> str:
     """A slow read's likely cause from its scheduler / softirq deltas
     (Runner read_diag, core/sched_probe.h): run-queue delay of the receiving
@@ -173,9 +205,12 @@ def attribute(diag: dict, ms: float, p50_ms: float) -> str:
             causes.append(f"{label} waited {row['run_delay_ms']:.2f} ms for a CPU "
                           f"({row.get('nivcsw', 0)} preemptions)")
     tcp = diag.get("tcp", {})
-    if tcp.get("RetransSegs", 0) or tcp.get("TCPTimeouts", 0):
+    if tcp.get("TCPTimeouts", 0) or tcp.get("RetransSegs", 0) > tcp.get("TCPLossProbes", 0):
         causes.append(f"{tcp.get('RetransSegs', 0)} TCP retransmits ({tcp.get('TCPTimeouts', 0)} RTOs, "
                       f"{tcp.get('TCPLossProbes', 0)} loss probes) in the namespace")
+    dropped = tcp.get("RcvPruned", 0) + tcp.get("TCPRcvQDrop", 0) + tcp.get("TCPBacklogDrop", 0)
+    if dropped:
+        causes.append(f"{dropped} receive-queue prunes / drops (skb memory over the receive buffer)")
     soft = diag.get("softirqs", {})
     if soft.get("HRTIMER", 0) >= 100:
         causes.append(f"{soft['HRTIMER']} HRTIMER softirqs on the busy CPUs (pacing timers)")
@@ -198,8 +233,11 @@ class Window:
         self.sched = thread_sched()
         self.irq = irq_snapshot()
         self.soft = softirq_snapshot()
+        self.tcp = tcp_snapshot()
 
     def report(self, cpus: list[int] | None, reads: int) -> dict:
         return {"threads": sched_delta(self.sched, thread_sched(), reads),
                 "irq_on_placement": table_delta(self.irq, irq_snapshot(), cpus, reads),
-                "softirq_on_placement": table_delta(self.soft, softirq_snapshot(), cpus, reads)}
+                "softirq_on_placement": table_delta(self.soft, softirq_snapshot(), cpus, reads),
+                # whole block, not per read: any RTO / drop names a stalled read
+                "tcp": tcp_delta(self.tcp, tcp_snapshot())}

@@ -205,3 +205,18 @@ def test_latency_series_bounded_and_accurate(native):
         want = s[min(len(s) - 1, len(s) * p // 100)]
         assert abs(ls.pct_floor(p) - want) <= 5e-4 * want, (p, ls.pct_floor(p), want)
     assert ls.max == 250.0 and ls.min == s[0]
+
+
+def test_sysdiag_tcp_counters():
+    """Block host view: namespace TCP counters (retransmits, RTOs, receive
+    queue prunes / drops), reported as non-zero increases only."""
+    from custom_go_client_benchmark_amd.utils import sysdiag
+
+    a = sysdiag.tcp_snapshot()
+    assert "RetransSegs" in a and "TCPTimeouts" in a
+    b = dict(a, RetransSegs=a["RetransSegs"] + 5, TCPTimeouts=a["TCPTimeouts"] + 1)
+    assert sysdiag.tcp_delta(a, b) == {"RetransSegs": 5, "TCPTimeouts": 1}
+    assert "tcp" in sysdiag.Window().report(None, 1)
+    d = {"threads": {"gcsb-worker": {"cpu_ms": 16.0, "run_delay_ms": 0.0}}, "softirqs": {},
+         "tcp": {"RcvPruned": 2, "TCPRcvQDrop": 1}, "wall_ms": 226.0}
+    assert "3 receive-queue prunes / drops" in sysdiag.attribute(d, 226.0, 16.0)

@@ -493,6 +493,7 @@ def run_rank(args) -> int:
         "async_submit": bool(args.async_submit),
         "rcvbuf": parse_size(args.rcvbuf),
         "tcp_congestion": args.client_cc,
+        "loopback_rto_min": True,
         "recv_refill": bool(args.recv_refill),
     }
     # the sliced extension: inline slot hand-off (r1_submit_ab), 2 MiB x 8
@@ -714,10 +715,10 @@ def run_rank(args) -> int:
             if sh["client"]:
                 os.sched_setaffinity(0, sh["client"])
             client = n.Client({"protocol": protocol, "endpoint": ep.url, "retry_initial_s": 0.05,
-                               "tcp_congestion": args.client_cc})
+                               "tcp_congestion": args.client_cc, "loopback_rto_min": True})
             if parts > 1:
                 client = n.SlicedWriter({"protocol": protocol, "endpoint": ep.url, "retry_initial_s": 0.05,
-                                         "tcp_congestion": args.client_cc,
+                                         "tcp_congestion": args.client_cc, "loopback_rto_min": True,
                                          "slices": parts, "slice_min_bytes": 1 << 20, "cpus": sh["client"]})
             buf = torch.empty(wsize, dtype=torch.uint8, device=f"cuda:{gpu}")
             n.gpu_fill_pattern(gpu, buf.data_ptr(), wsize, f"upload/rank{rank}", 0)
@@ -789,7 +790,7 @@ def run_rank(args) -> int:
             srv.add_synthetic(bucket, "fanout/obj_", "", 0, 1, size)
             want = srv.object_info(bucket, name)["crc32c"]
             client = n.Client({"protocol": protocol, "endpoint": srv.url, "retry_initial_s": 0.05,
-                               "tcp_congestion": args.client_cc,
+                               "tcp_congestion": args.client_cc, "loopback_rto_min": True,
                                "cpus": placement["client"], "rcvbuf": parse_size(args.rcvbuf)})
             full = torch.empty(size, dtype=torch.uint8, device=f"cuda:{gpu}" if use_gpu else "cpu")
             # this rank's slice lands in place: the all-gather's input is the

@@ -84,6 +84,7 @@ void apply_socket_options(int fd, const SocketOptions& opt) {
   if (!opt.congestion.empty())
     (void)setsockopt(fd, IPPROTO_TCP, TCP_CONGESTION, opt.congestion.data(),
                      static_cast<socklen_t>(opt.congestion.size()));
+  if (opt.loopback_rto_min) set_loopback_rto_min(fd);
   if (opt.io_timeout_ms > 0) {
     timeval tv{opt.io_timeout_ms / 1000, (opt.io_timeout_ms % 1000) * 1000};
     setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));

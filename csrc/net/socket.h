@@ -48,6 +48,9 @@ struct SocketOptions {
   // loopback link every 64 KiB skb of an upload then waits on an hrtimer
   // (profiles/r4_recvcost).
   std::string congestion;
+  // Loopback endpoints only: minimum RTO kLoopbackRtoMinUs instead of 200 ms
+  // (set_loopback_rto_min); never for a real network path.
+  bool loopback_rto_min = false;
   // A payload recv() also refills the reader's 16 KiB buffer (one recvmsg,
   // two iovecs), so the bytes after the payload -- the next HTTP/2 frame's
   // header -- need no system call of their own (BufferedConn::read_some).
@@ -176,6 +179,14 @@ bool read_tcp_chrono(int fd, TcpChrono* out);
 // (cubic: 7.9-9.7 MiB, profiles/r3_twins/cc).  An unprivileged process may
 // pick any algorithm in net.ipv4.tcp_allowed_congestion_control; a refusal
 // leaves the host's default.  The `ceiling` probe's sender uses it too.
+// The synthetic endpoint's sockets (listener first, so accepted sockets
+// inherit it): the congestion control (GCSB_SRV_CC, default cubic) and a
+// loopback-sized minimum retransmission timeout.  The default 200 ms RTO
+// min turns one receive-queue drop into a 200+ ms read (one 256 MiB HTTP
+// read of 16 ms took 226 ms, profiles/r4_main8); on loopback the RTT is
+// microseconds.
+constexpr int kLoopbackRtoMinUs = 5000;
+void set_loopback_rto_min(int fd);
 void set_endpoint_congestion_control(int fd);
 const std::string& endpoint_congestion_control();
 // SSL_CTX for a TLS server (throws on bad cert/key); owned by the caller (free_server_tls_ctx).

@@ -35,10 +35,20 @@ const std::string& endpoint_congestion_control() {
   return cc;
 }
 
+void set_loopback_rto_min(int fd) {
+  // TCP_RTO_MIN_US (Linux 6.15+; this image's headers predate it): the
+  // kernel clamps to its floor (8 ms at HZ 250) and an older kernel refuses
+  // the option, harmlessly.
+  constexpr int kTcpRtoMinUs = 45;
+  const int us = kLoopbackRtoMinUs;
+  (void)::setsockopt(fd, IPPROTO_TCP, kTcpRtoMinUs, &us, sizeof(us));
+}
+
 void set_endpoint_congestion_control(int fd) {
   const std::string& cc = endpoint_congestion_control();
   if (!cc.empty())
     (void)::setsockopt(fd, IPPROTO_TCP, TCP_CONGESTION, cc.data(), static_cast<socklen_t>(cc.size()));
+  set_loopback_rto_min(fd);
 }
 
 }  // namespace gcsb

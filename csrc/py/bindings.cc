@@ -63,6 +63,7 @@ ClientConfig client_from(const py::dict& d) {
   c.sock.sndbuf = get_or<int>(d, "sndbuf", 0);
   c.sock.io_timeout_ms = get_or<int>(d, "io_timeout_ms", 0);
   c.sock.congestion = get_or<std::string>(d, "tcp_congestion", "");
+  c.sock.loopback_rto_min = get_or<bool>(d, "loopback_rto_min", false);
   c.sock.recv_refill = get_or<bool>(d, "recv_refill", false);
   c.sock.tls_verify = get_or<bool>(d, "tls_verify", true);
   c.sock.tls_ca_file = get_or<std::string>(d, "tls_ca_file", "");
@@ -1074,6 +1075,7 @@ PYBIND11_MODULE(_native, m) {
       .def("delete", &PyClient::remove)
       .def("stats", &PyClient::stats);
 
+  m.attr("LOOPBACK_RTO_MIN_US") = kLoopbackRtoMinUs;
   py::class_<LatencySeries>(m, "LatencySeries")
       .def(py::init<>())
       .def("add", &LatencySeries::add)

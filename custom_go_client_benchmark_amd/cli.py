@@ -257,7 +257,8 @@ def main(argv: list[str] | None = None) -> int:
         retry_max_total_s=fs.get("retry-max-total"), retry_max_attempts=fs.get("retry-max-attempts"),
         read_timeout_s=fs.get("read-timeout"),
         # a node-local synthetic endpoint is a loopback link: cubic unless set
-        tcp_congestion=fs.get("tcp-congestion") or ("cubic" if fs.get("start-fake-server") else ""))
+        tcp_congestion=fs.get("tcp-congestion") or ("cubic" if fs.get("start-fake-server") else ""),
+        loopback_rto_min=bool(fs.get("start-fake-server")))
 
     # tracing (reference main.go:162-165)
     tracer, trace_cleanup = None, None

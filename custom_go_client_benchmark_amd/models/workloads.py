@@ -55,6 +55,7 @@ class RunOptions:
     retry_max_attempts: int = 0
     read_timeout_s: float = 0.0            # idle limit per read (0 = none, as the reference's Timeout: 0)
     tcp_congestion: str = ""               # client sockets' congestion control ("" = host default)
+    loopback_rto_min: bool = False         # node-local endpoint: loopback-sized minimum RTO
     object_names: list | None = None
     keep_records: bool = True
     slices: int = 1                        # >1: sliced (parallel ranged) reads, see csrc/storage/sliced.h
@@ -74,6 +75,7 @@ class RunOptions:
             "io_timeout_ms": int(round(self.read_timeout_s * 1000)),
             "tls_ca_file": self.tls_ca_file, "tls_verify": self.tls_verify,
             "tcp_congestion": self.tcp_congestion,
+            "loopback_rto_min": self.loopback_rto_min,
         }
 
     def runner_dict(self) -> dict:

@@ -220,3 +220,29 @@ def test_sysdiag_tcp_counters():
     d = {"threads": {"gcsb-worker": {"cpu_ms": 16.0, "run_delay_ms": 0.0}}, "softirqs": {},
          "tcp": {"RcvPruned": 2, "TCPRcvQDrop": 1}, "wall_ms": 226.0}
     assert "3 receive-queue prunes / drops" in sysdiag.attribute(d, 226.0, 16.0)
+
+
+def test_endpoint_sockets_get_loopback_rto_min(native, server):
+    """The endpoint sets a loopback-sized minimum RTO (TCP_RTO_MIN_US, Linux
+    6.15+) on its LISTENING socket, which accepted sockets inherit (checked
+    here on a plain listener: the endpoint's fds are not reachable from
+    Python), so one receive-queue drop cannot stall a read for 200 ms.
+    Client sockets opt in (loopback_rto_min); older kernels refuse the
+    option and nothing changes."""
+    import socket
+
+    ls = socket.socket()
+    try:
+        ls.setsockopt(socket.IPPROTO_TCP, 45, native.LOOPBACK_RTO_MIN_US)
+    except OSError:
+        pytest.skip("kernel without TCP_RTO_MIN_US")
+    ls.bind(("127.0.0.1", 0))
+    ls.listen()
+    c = socket.create_connection(ls.getsockname())
+    a, _ = ls.accept()
+    assert a.getsockopt(socket.IPPROTO_TCP, 45) <= 10000 < c.getsockopt(socket.IPPROTO_TCP, 45)
+    for s_ in (a, c, ls):
+        s_.close()
+    server.add_synthetic(B, P, "", 0, 1, 1 << 20)
+    cl = native.Client({"protocol": "grpc", "endpoint": server.url, "loopback_rto_min": True})
+    assert cl.read(B, P + "0")["verified"]

@@ -139,6 +139,10 @@ muxiso)  # the multiplexed gRPC reader on a core of its own, after the pacing fi
     done
   done
   ;;
+bigring)  # one stream into the multiplexed reader's footprint: does a 48-96 MiB ring cost the copy 2x?
+  step ab 500 python3 -u scripts/experiments/recv_cost_ab.py --tag bigring --reps 3 \
+    --variants head_4x1m,head,head_24x2,head_48x2,nodma_48x2,nodma
+  ;;
 soak)  # profiles/r4_soak: execute_pb.sh with 48 workers x 100 MiB, -sink gpu, 120 s per protocol, exporter at 30 s
   step soak 900 python3 -u scripts/soak.py --out "$O" --duration 120s
   ;;

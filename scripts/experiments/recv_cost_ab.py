@@ -88,6 +88,11 @@ variants = {
     # hand-off before it sleeps (no futex wake per slot on the receiver)
     "head_spin": {"sink": "gpu"},
     "head_4x1m_spin": {"sink": "gpu", "ring_slot_bytes": 1 << 20, "ring_slots": 4},
+    # the multiplexed reader's destination footprint on one stream: 48 MiB /
+    # 96 MiB rings (48 workers x 1-2 MiB), with and without the DMA
+    "head_24x2": {"sink": "gpu", "ring_slots": 24},
+    "head_48x2": {"sink": "gpu", "ring_slots": 48},
+    "nodma_48x2": {"sink": "gpu", "gpu_stage": "none", "ring_slots": 48},
 }
 SPIN_US = {"head_spin": 200, "head_4x1m_spin": 200}
 names = [v for v in args.variants.split(",") if v]

@@ -226,6 +226,10 @@ def build_parser() -> argparse.ArgumentParser:
                          "still in the receiving CCD's L3; against 8 x 2 MiB the receive copy went 0.046 -> 0.036 "
                          "CPU-s/GiB, 22.0k -> 27.5k MiB/s interleaved (profiles/r4_main8, profiles/r4_recvcost)")
     ap.add_argument("--slots", type=int, default=4)
+    ap.add_argument("--conn-ring", default="on", choices=["on", "off"],
+                    help="GPU sink on one multiplexed gRPC connection (list_read_grpc, ref_default_100m_grpc_gpu): "
+                         "every worker's stream through one 8 x 1 MiB connection ring instead of a ring per "
+                         "worker (profiles/r4_bigring)")
     ap.add_argument("--crc-slot-waves", type=int, default=0, choices=[0, 1, 2, 4, 8],
                     help="slot CRC kernel waves per workgroup (0: by slot size); A/B of the kernel's table staging")
     ap.add_argument("--async-submit", type=int, default=1, choices=[0, 1],
@@ -481,6 +485,7 @@ def run_rank(args) -> int:
         "device": gpu if use_gpu else 0,
         "ring_slot_bytes": parse_size(args.slot_bytes),
         "ring_slots": args.slots,
+        "conn_ring": args.conn_ring == "on",
         "landing": "object",
         "grpc_conn_pool_size": args.grpc_pool,
         "keep_records": False,
@@ -586,6 +591,10 @@ def run_rank(args) -> int:
                                     "headers_s_per_gib": round(d["headers_ns"] / 1e9 / g, 4),
                                     "other_s_per_gib": round(d["other_ns"] / 1e9 / g, 4),
                                     "avg_data_frame_kib": round(d["data_bytes"] / max(1, d["data_frames"]) / 1024, 1)}
+            cr = r1.conn_ring_stats()
+            if cr:
+                # the multiplexed connection's shared receive ring (warmup included)
+                cpu["conn_ring"] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in cr.items()}
             g1 = s1.get("gpu") or {}
             if g1.get("slot_waits") or g1.get("flag_reuses"):
                 # the receiving thread reusing ring slots: on the CRC kernel's

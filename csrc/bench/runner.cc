@@ -97,6 +97,11 @@ double LatencySeries::pct_floor(int pct) const {
 Runner::Runner(RunnerConfig cfg) : cfg_(std::move(cfg)) {
   reserve_fd_table();
   if (cfg_.workers <= 0) throw StorageError("worker count not valid", false);
+  const GpuSinkConfig& g = cfg_.gpu;
+  if (cfg_.conn_ring && cfg_.sink == "gpu" && cfg_.client.protocol == "grpc" && cfg_.client.grpc_conn_pool_size == 1 &&
+      cfg_.workers > 1 && cfg_.slices <= 1 && g.verify && g.landing == Landing::kObject &&
+      g.stage == GpuSinkConfig::Stage::kH2D)
+    conn_ring_ = std::make_unique<ConnRing>(g.device, cfg_.conn_ring_slot_bytes, cfg_.conn_ring_slots);
   client_ = make_client(cfg_.client);
 }
 
@@ -257,7 +262,9 @@ void Runner::worker_main(int w) {
     }
     if (!sinks_[w] && cfg_.slices <= 1) {
       if (cfg_.sink == "gpu") {
-        auto g = std::make_unique<GpuSink>(cfg_.gpu);
+        GpuSinkConfig gc = cfg_.gpu;
+        gc.conn_ring = conn_ring_.get();
+        auto g = std::make_unique<GpuSink>(gc);
         gpu_sinks_[w] = g.get();
         sinks_[w] = std::move(g);
       } else {

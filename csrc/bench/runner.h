@@ -70,6 +70,13 @@ struct RunnerConfig {
   // their deltas (RunSummary::slowest_diag).  Off by default: ~tens of us
   // per read, outside the read's latency but inside the run's wall time.
   bool read_diag = false;
+  // GPU sink on ONE multiplexed gRPC connection (pool size 1, several
+  // workers): every worker's stream lands through one connection ring
+  // (GpuSinkConfig::conn_ring) of conn_ring_slots x conn_ring_slot_bytes
+  // instead of a ring per worker (profiles/r4_bigring).
+  bool conn_ring = true;
+  size_t conn_ring_slot_bytes = size_t(1) << 20;
+  int conn_ring_slots = 8;
   // CPUs the read_diag sampler must not run on (the placement's; the client
   // CPUs are always added): sched_sample_offcore
   std::vector<int> diag_avoid_cpus;
@@ -166,6 +173,8 @@ class Runner {
   // HBM address worker w's last object landed at (GPU sink, object landing;
   // sliced reads: the shared landing buffer), 0 if none.
   uintptr_t landing_ptr(int w) const;
+  // the connection ring's counters (nullptr stats when there is none)
+  const ConnRing* conn_ring() const { return conn_ring_.get(); }
   // NUMA placement of worker w's pinned ring, per slot (affinity.h numa_nodes_of)
   std::vector<std::vector<long>> ring_numa(int w) const;
   // Fraction of worker w's pinned ring backed by transparent huge pages
@@ -176,6 +185,9 @@ class Runner {
   void worker_main(int w);
   void record(ReadRecord&& r, double ms, double host_ms);
   RunnerConfig cfg_;
+  // before client_: destroyed after the connections (their reader threads
+  // fill it) and after the sinks whose segments it holds
+  std::unique_ptr<ConnRing> conn_ring_;
   std::unique_ptr<StorageClient> client_;
   std::vector<std::thread> threads_;
   std::atomic<bool> running_{false};

@@ -36,6 +36,8 @@
 
 namespace gcsb {
 
+class ConnRing;
+
 enum class Landing {
   kRing,    // HBM ring of the same geometry as the host ring (discard semantics)
   kObject,  // whole object laid out contiguously in HBM (up to 288 GB per GPU)
@@ -81,6 +83,14 @@ struct GpuSinkConfig {
   // two A/B stages land nothing in HBM and verify nothing.
   enum class Stage { kH2D, kNone, kHostRead };
   Stage stage = Stage::kH2D;
+  // Multiplexed gRPC (one connection's reader thread feeds every worker's
+  // sink): receive into this connection-wide ring instead of a ring per sink.
+  // 48 per-worker rings of 2 x 2 MiB are 192 MiB of receive destinations, far
+  // past the reader's L3, and a one-stream read into a ring that size pays
+  // the same 0.056-0.066 CPU-s/GiB as the multiplexed reader
+  // (profiles/r4_bigring); one 8 x 1 MiB ring per connection stays L3-hot.
+  // Object landing with CRC verification only; not owned by the sink.
+  ConnRing* conn_ring = nullptr;
 };
 
 struct GpuSinkStats {
@@ -95,6 +105,8 @@ struct GpuSinkStats {
 };
 
 class GpuSink : public Sink {
+  friend class ConnRing;
+
  public:
   explicit GpuSink(const GpuSinkConfig& cfg);
   ~GpuSink() override;
@@ -159,6 +171,11 @@ class GpuSink : public Sink {
   void grow_object_buffer(uint64_t need);
   Slot& take_slot();
   void submit_current();
+  // conn-ring mode (cfg_.conn_ring)
+  Window ring_acquire();
+  void ring_commit(size_t n);
+  void ring_wait_all();  // this sink's segments submitted and their results collected
+  void ring_fold();
   void wait_slot(Slot& s);
   bool done_by_flags(const Slot& s) const;
   void wait_event(hipEvent_t ev);
@@ -200,6 +217,95 @@ class GpuSink : public Sink {
   uint32_t host_read_sink_ = 0;  // Stage::kHostRead's CRC (keeps the read)
   std::mutex sub_mu_;
   std::condition_variable sub_cv_;
+  // conn-ring mode: this read's segments in the shared ring, in delivery
+  // (= object) order, and its chunks; ring_res_ / ring_done_ are guarded by
+  // the ring's mutex (any thread may collect a slot's results)
+  struct RingRes {
+    uint64_t obj_off = 0;
+    uint32_t len = 0;
+    uint32_t raw = 0;
+    bool done = false;
+    bool failed = false;
+  };
+  std::vector<RingRes> ring_res_;
+  size_t ring_done_ = 0;
+  int ring_open_slot_ = -1;  // ring slot / segment index of this sink's open segment (-1: none)
+  size_t ring_open_seg_ = 0;
+  struct ChunkMark {
+    uint64_t start = 0, end = 0;
+    bool closed = false, has_crc = false, broken = false;
+    uint32_t crc = 0;
+  };
+  std::vector<ChunkMark> chunks_;
+};
+
+// One receive ring for every stream of a multiplexed connection (see
+// GpuSinkConfig::conn_ring).  The connection's reader thread fills it through
+// the sinks' acquire / commit, segment by segment (a segment: consecutive
+// bytes of one stream); a slot goes to the device submitter when full, one
+// H2D copy per segment to its own object's HBM offset plus one CRC launch for
+// all the slot's segments.  A worker finishing its read submits what the
+// reader is not writing into (a slot may go in several parts) and collects
+// its segments' results as the kernel publishes them (no HIP call).  The
+// reader reuses a slot once every segment's result was collected.
+class ConnRing {
+ public:
+  ConnRing(int device, size_t slot_bytes, int slots);
+  ~ConnRing();
+  ConnRing(const ConnRing&) = delete;
+  ConnRing& operator=(const ConnRing&) = delete;
+  struct Stats {
+    uint64_t slots_filled = 0, submissions = 0, segments = 0, reader_waits = 0;
+    double reader_wait_s = 0;
+  };
+  Stats stats() const;
+  int device() const { return device_; }
+
+ private:
+  friend class GpuSink;
+  struct Seg {
+    GpuSink* owner = nullptr;
+    size_t seq = 0;       // index in owner->ring_res_
+    uint32_t slot_off = 0;
+    uint32_t len = 0;
+    uint8_t* dst = nullptr;  // HBM: owner's landing + object offset
+  };
+  struct RSlot {
+    uint8_t* host = nullptr;
+    size_t used = 0;
+    std::vector<Seg> segs;
+    size_t submitted = 0;  // segs handed to the submitter
+    size_t collected = 0;  // segs whose results were copied out
+    bool filling = false;  // the reader's current slot
+    hipStream_t st = nullptr;
+    int st_idx = -1;
+    uint32_t* tiles = nullptr;
+    CrcSegResult* res = nullptr;
+    CrcSegResult* d_res = nullptr;
+  };
+  // all under mu_
+  void submit_locked(int slot, size_t upto);
+  void collect_locked(RSlot& s);
+  void flush_locked();  // submit every segment the reader is not writing into
+  RSlot& take_slot_locked(std::unique_lock<std::mutex>& lk);
+  bool owner_done_locked(const GpuSink* g) const { return g->ring_done_ == g->ring_res_.size(); }
+  void collect_all_locked();
+
+  int device_;
+  size_t slot_bytes_;
+  std::vector<RSlot> slots_;
+  int cur_ = -1, next_ = 0;
+  bool window_open_ = false;  // the reader is receiving into the last segment of cur_
+  const GpuSink* window_owner_ = nullptr;  // ... which belongs to this sink
+  const CrcTables* d_tables_ = nullptr;
+  uint32_t* d_tiles_ = nullptr;
+  size_t tiles_cap_ = 0;
+  CrcSegResult* res_host_ = nullptr;
+  uint64_t posted_ = 0;
+  uint64_t issued_ = 0;
+  Stats stats_;
+  mutable std::mutex mu_;
+  std::condition_variable cv_;
 };
 
 // Upload source for the write path (config 5): HBM -> pinned ring via

@@ -527,6 +527,13 @@ GpuSink::GpuSink(const GpuSinkConfig& cfg) : cfg_(cfg) {
   cfg_.slot_bytes = (cfg_.slot_bytes + 4095) / 4096 * 4096;
   if (cfg_.slot_bytes < 65536) cfg_.slot_bytes = 65536;
   set_device();
+  if (cfg_.conn_ring) {
+    // the connection's ring is the receive destination: no private ring
+    if (cfg_.landing != Landing::kObject || !cfg_.verify || cfg_.stage != GpuSinkConfig::Stage::kH2D)
+      throw std::invalid_argument("GpuSink: conn_ring needs object landing with CRC verification");
+    if (cfg_.conn_ring->device() != cfg_.device) throw std::invalid_argument("GpuSink: conn_ring on another device");
+    return;
+  }
   DeviceStreamPool& pool = DeviceStreamPool::get(cfg_.device);
   // Slot i of a sink uses pool stream i (slot i's CRC overlaps slot i+1's
   // copy; the sliced block's 16 sinks spread over all 8).  Alternating a
@@ -562,6 +569,7 @@ GpuSink::GpuSink(const GpuSinkConfig& cfg) : cfg_(cfg) {
 
 GpuSink::~GpuSink() {
   try {
+    if (cfg_.conn_ring) ring_wait_all();    // no segment of this sink may outlive it
     for (Slot& sl : slots_) wait_slot(sl);  // no queued hand-off may outlive the sink
     set_device();
   } catch (...) {
@@ -579,6 +587,7 @@ GpuSink::~GpuSink() {
 
 void GpuSink::set_external_destination(void* dptr, size_t cap) {
   set_device();
+  if (cfg_.conn_ring) ring_wait_all();    // this sink's segments in the connection's ring
   for (Slot& sl : slots_) wait_slot(sl);  // this sink's queued work (its slot events), not the shared streams
   if (own_obj_) {
     (void)hipFree(own_obj_);
@@ -603,8 +612,13 @@ void GpuSink::grow_object_buffer(uint64_t need) {
   if (external_dst_)
     throw StorageError("object larger than the external HBM destination (" + std::to_string(obj_cap_) + " B)", false);
   set_device();
-  for (int k = 0; k < cfg_.slots; ++k) wait_slot(slots_[(next_ + k) % cfg_.slots]);
-  const uint64_t landed = cur_ >= 0 ? slots_[cur_].obj_off : delivered_;
+  uint64_t landed = delivered_;
+  if (cfg_.conn_ring) {
+    ring_wait_all();  // every landed byte's copy done before the old buffer goes
+  } else {
+    for (int k = 0; k < cfg_.slots; ++k) wait_slot(slots_[(next_ + k) % cfg_.slots]);
+    landed = cur_ >= 0 ? slots_[cur_].obj_off : delivered_;
+  }
   size_t cap = (need + (2u << 20) - 1) / (2u << 20) * (2u << 20);
   uint8_t* nb = nullptr;
   hip_check(hipMalloc(reinterpret_cast<void**>(&nb), cap), "hipMalloc(object landing)");
@@ -619,6 +633,13 @@ void GpuSink::grow_object_buffer(uint64_t need) {
 
 void GpuSink::begin(const ObjectInfo& info) {
   abort();  // drain anything a previous (failed) read left behind
+  if (cfg_.conn_ring) {
+    std::lock_guard<std::mutex> lk(cfg_.conn_ring->mu_);
+    ring_res_.clear();
+    ring_done_ = 0;
+    ring_open_slot_ = -1;
+    chunks_.clear();
+  }
   info_ = info;
   delivered_ = 0;
   in_chunk_ = false;
@@ -681,6 +702,7 @@ GpuSink::Slot& GpuSink::take_slot() {
 
 Window GpuSink::acquire(size_t want) {
   (void)want;
+  if (cfg_.conn_ring) return ring_acquire();
   if (cur_ < 0) take_slot();
   {
     Slot& s = slots_[cur_];
@@ -713,6 +735,7 @@ Window GpuSink::acquire(size_t want) {
 }
 
 void GpuSink::commit(size_t n) {
+  if (cfg_.conn_ring) return ring_commit(n);
   Slot& s = slots_[cur_];
   if (debug_ring() && (s.segs.empty() || s.segs.back().closed || s.used + n > cfg_.slot_bytes))
     throw std::logic_error("GpuSink::commit outside an acquired window");
@@ -722,6 +745,20 @@ void GpuSink::commit(size_t n) {
 }
 
 void GpuSink::chunk_begin(size_t len) {
+  if (cfg_.conn_ring) {
+    // a segment never spans two chunks: the host fold checks each chunk
+    std::lock_guard<std::mutex> lk(cfg_.conn_ring->mu_);
+    ring_open_slot_ = -1;
+    if (!chunks_.empty() && !chunks_.back().closed) {  // the last chunk never ended: unverifiable
+      chunks_.back().closed = true;
+      chunks_.back().broken = true;
+      chunks_.back().end = delivered_;
+    }
+    ChunkMark m;
+    m.start = m.end = delivered_;
+    chunks_.push_back(m);
+    return;
+  }
   if (cur_ >= 0) {
     Slot& s = slots_[cur_];
     if (!s.segs.empty()) s.segs.back().closed = true;
@@ -735,6 +772,17 @@ void GpuSink::chunk_begin(size_t len) {
 }
 
 void GpuSink::chunk_end(bool has_crc, uint32_t crc) {
+  if (cfg_.conn_ring) {
+    std::lock_guard<std::mutex> lk(cfg_.conn_ring->mu_);
+    ring_open_slot_ = -1;
+    if (chunks_.empty() || chunks_.back().closed) return;
+    ChunkMark& m = chunks_.back();
+    m.end = delivered_;
+    m.closed = true;
+    m.has_crc = has_crc;
+    m.crc = crc;
+    return;
+  }
   if (!in_chunk_) return;
   in_chunk_ = false;
   if (chunk_start_pending_) {
@@ -760,6 +808,16 @@ void GpuSink::chunk_end(bool has_crc, uint32_t crc) {
 
 void GpuSink::resume_at(int64_t offset) {
   (void)offset;
+  if (cfg_.conn_ring) {
+    std::lock_guard<std::mutex> lk(cfg_.conn_ring->mu_);
+    ring_open_slot_ = -1;
+    if (!chunks_.empty() && !chunks_.back().closed) {
+      chunks_.back().closed = true;
+      chunks_.back().broken = true;
+      chunks_.back().end = delivered_;
+    }
+    return;
+  }
   chunk_broken_ = true;
   if (cur_ >= 0 && !slots_[cur_].segs.empty() && !slots_[cur_].segs.back().closed) {
     slots_[cur_].segs.back().closed = true;
@@ -933,9 +991,14 @@ void GpuSink::harvest(Slot& s) {
 }
 
 SinkResult GpuSink::finish() {
-  submit_current();
   RoctxRange rg("gcsb.wait_landed");
-  for (int k = 0; k < cfg_.slots; ++k) wait_slot(slots_[(next_ + k) % cfg_.slots]);
+  if (cfg_.conn_ring) {
+    ring_wait_all();
+    ring_fold();
+  } else {
+    submit_current();
+    for (int k = 0; k < cfg_.slots; ++k) wait_slot(slots_[(next_ + k) % cfg_.slots]);
+  }
   SinkResult r;
   r.bytes = delivered_;
   r.landed_ns = now_ns();
@@ -961,6 +1024,11 @@ SinkResult GpuSink::finish() {
 }
 
 void GpuSink::abort() {
+  if (cfg_.conn_ring) {
+    // its bytes are real (delivered) bytes: let their copies land
+    ring_wait_all();
+    return;
+  }
   if (cur_ >= 0) {
     slots_[cur_].used = 0;
     slots_[cur_].segs.clear();
@@ -976,6 +1044,304 @@ void GpuSink::abort() {
       if (cfg_.stage == GpuSinkConfig::Stage::kH2D) hip_check(hipEventSynchronize(s.ev), "hipEventSynchronize");
       s.inflight = false;
     }
+}
+
+// ---------------------------------------------------------------------------
+// connection ring (engine.h ConnRing): one receive ring per multiplexed
+// connection, shared by the sinks of every stream on it
+
+ConnRing::ConnRing(int device, size_t slot_bytes, int slots) : device_(device) {
+  slot_bytes_ = std::max<size_t>((slot_bytes + 4095) / 4096 * 4096, 65536);
+  if (slots < 2) slots = 2;
+  ensure_device(device_);
+  DeviceStreamPool& pool = DeviceStreamPool::get(device_);
+  d_tables_ = device_crc_tables(device_);
+  tiles_cap_ = slot_bytes_ / kCrcMinTile + 2 * kMaxSeg + 8;
+  d_tiles_ = crc_scratch_alloc(crc_scratch_words(tiles_cap_) * slots);
+  hip_check(hipHostMalloc(reinterpret_cast<void**>(&res_host_), sizeof(CrcSegResult) * kMaxSeg * slots,
+                          hipHostMallocMapped | hipHostMallocCoherent),
+            "hipHostMalloc(ring results)");
+  std::memset(res_host_, 0, sizeof(CrcSegResult) * kMaxSeg * slots);
+  const unsigned base = pool.next_base() * static_cast<unsigned>(slots);
+  slots_.resize(slots);
+  for (int i = 0; i < slots; ++i) {
+    RSlot& r = slots_[i];
+    r.host = static_cast<uint8_t*>(PinnedPool::get(slot_bytes_, device_numa_node(device_)));
+    if (pool.private_streams()) {
+      hip_check(hipStreamCreateWithFlags(&r.st, hipStreamNonBlocking), "hipStreamCreate(ring)");
+    } else {
+      r.st = pool.at(base + static_cast<unsigned>(i));
+      r.st_idx = pool.index_of(r.st);
+    }
+    r.tiles = d_tiles_ + crc_scratch_words(tiles_cap_) * static_cast<size_t>(i);
+    r.res = res_host_ + static_cast<size_t>(i) * kMaxSeg;
+    hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&r.d_res), r.res, 0), "hipHostGetDevicePointer");
+  }
+}
+
+ConnRing::~ConnRing() {
+  {
+    // every hand-off issued, every launched kernel finished, before the
+    // pinned slots and the result block go
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [&] { return issued_ == posted_; });
+  }
+  try {
+    ensure_device(device_);
+    for (RSlot& r : slots_)
+      if (r.submitted > 0) hip_check(hipStreamSynchronize(r.st), "hipStreamSynchronize(ring)");
+  } catch (...) {
+  }
+  for (RSlot& r : slots_) {
+    PinnedPool::put(r.host, slot_bytes_);
+    if (r.st_idx < 0 && r.st) (void)hipStreamDestroy(r.st);
+  }
+  if (res_host_) (void)hipHostFree(res_host_);
+  if (d_tiles_) (void)hipFree(d_tiles_);
+}
+
+ConnRing::Stats ConnRing::stats() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return stats_;
+}
+
+// Segments [r.submitted, upto) of slot `slot` to the device submitter: one H2D
+// per segment into its object's HBM, then one CRC launch over all of them
+// (results at r.res[submitted..upto), published by the kernel).
+void ConnRing::submit_locked(int slot, size_t upto) {
+  RSlot& r = slots_[slot];
+  const size_t a = r.submitted;
+  if (upto <= a) return;
+  CrcBatch b;
+  std::memset(&b, 0, sizeof(b));
+  struct Copy {
+    uint8_t* dst;
+    const uint8_t* src;
+    uint32_t len;
+  };
+  std::vector<Copy> copies;
+  copies.reserve(upto - a);
+  for (size_t i = a; i < upto; ++i) {
+    const Seg& g = r.segs[i];
+    CrcSeg& c = b.seg[b.nseg++];
+    c.addr = g.dst;
+    c.len = g.len;
+    c.flags = 0;  // chunks are checked by the owner's host fold
+    if (g.len) copies.push_back({g.dst, r.host + g.slot_off, g.len});
+    __atomic_store_n(&r.res[i].status, kCrcStatusPending, __ATOMIC_RELAXED);
+  }
+  finalize_crc_batch(&b);
+  if (b.total_tiles > tiles_cap_) throw std::logic_error("ConnRing: CRC tile scratch too small");
+  r.submitted = upto;
+  ++stats_.submissions;
+  stats_.segments += upto - a;
+  ++posted_;
+  hipStream_t st = r.st;
+  const int st_idx = r.st_idx;
+  uint32_t* tiles = r.tiles;
+  CrcSegResult* d_res = r.d_res + a;
+  CrcSegResult* h_res = r.res + a;
+  const int dev = device_;
+  const CrcTables* tabs = d_tables_;
+  DeviceSubmitter::get(device_).post([this, b, copies, st, st_idx, tiles, d_res, h_res, dev, tabs]() {
+    bool ok = true;
+    try {
+      ensure_device(dev);
+      for (const Copy& c : copies) {
+        const int64_t t0 = now_ns();
+        hip_check(hipMemcpyAsync(c.dst, c.src, c.len, hipMemcpyHostToDevice, st), "hipMemcpyAsync(H2D ring)");
+        note_hip_call("hipMemcpyAsync(H2D)", st_idx, t0, now_ns());
+      }
+      const int64_t t1 = now_ns();
+      launch_crc32c_batch(b, tabs, tiles, d_res, st);
+      note_hip_call("crc launch", st_idx, t1, now_ns());
+    } catch (const std::exception&) {
+      ok = false;
+    }
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!ok)  // nothing will publish these results: fail them
+      for (uint32_t i = 0; i < b.nseg; ++i) {
+        h_res[i].raw = 0;
+        __atomic_store_n(&h_res[i].status, 3u, __ATOMIC_RELEASE);
+      }
+    ++issued_;
+    cv_.notify_all();
+  });
+}
+
+// Copies the results the kernel has published out to their owners, in order.
+void ConnRing::collect_locked(RSlot& r) {
+  while (r.collected < r.submitted) {
+    const CrcSegResult* rv = r.res + r.collected;
+    const uint32_t st = __atomic_load_n(&rv->status, __ATOMIC_ACQUIRE);
+    if (st == kCrcStatusPending) break;
+    const Seg& g = r.segs[r.collected];
+    GpuSink::RingRes& o = g.owner->ring_res_[g.seq];
+    o.raw = g.len ? rv->raw : 0u;
+    o.failed = st == 3u;
+    o.done = true;
+    ++g.owner->ring_done_;
+    ++r.collected;
+  }
+}
+
+void ConnRing::collect_all_locked() {
+  for (RSlot& r : slots_) collect_locked(r);
+}
+
+// Everything the reader is not receiving into goes to the GPU now.
+void ConnRing::flush_locked() {
+  if (cur_ < 0) return;
+  RSlot& r = slots_[cur_];
+  size_t upto = r.segs.size();
+  if (window_open_ && upto > 0) --upto;
+  submit_locked(cur_, upto);
+}
+
+// The reader's next slot: every result of its last use collected first.
+ConnRing::RSlot& ConnRing::take_slot_locked(std::unique_lock<std::mutex>& lk) {
+  if (cur_ >= 0) {
+    RSlot& old = slots_[cur_];
+    submit_locked(cur_, old.segs.size());
+    old.filling = false;
+    cur_ = -1;
+    ++stats_.slots_filled;
+  }
+  RSlot& r = slots_[next_];
+  collect_locked(r);
+  if (r.collected < r.segs.size()) {
+    ++stats_.reader_waits;
+    const int64_t t0 = now_ns();
+    const timespec ts{0, 10000};
+    while (r.collected < r.segs.size()) {
+      lk.unlock();
+      nanosleep(&ts, nullptr);
+      lk.lock();
+      collect_locked(r);
+    }
+    stats_.reader_wait_s += (now_ns() - t0) / 1e9;
+  }
+  r.segs.clear();
+  r.used = 0;
+  r.submitted = r.collected = 0;
+  r.filling = true;
+  cur_ = next_;
+  next_ = (next_ + 1) % static_cast<int>(slots_.size());
+  return r;
+}
+
+Window GpuSink::ring_acquire() {
+  ConnRing& R = *cfg_.conn_ring;
+  if (delivered_ >= obj_cap_)
+    // size unknown so far (or larger than announced): grow, keeping landed bytes
+    grow_object_buffer(std::max<uint64_t>(2 * obj_cap_, delivered_ + R.slot_bytes_));
+  std::unique_lock<std::mutex> lk(R.mu_);
+  R.window_open_ = false;  // a window the reader never committed (its recv failed) is dropped
+  R.window_owner_ = nullptr;
+  ConnRing::RSlot* r = R.cur_ >= 0 ? &R.slots_[R.cur_] : nullptr;
+  const bool mine = r && ring_open_slot_ == R.cur_ && ring_open_seg_ + 1 == r->segs.size() &&
+                    ring_open_seg_ >= r->submitted;
+  if (!r || r->used == R.slot_bytes_ || (!mine && r->segs.size() >= static_cast<size_t>(kMaxSeg))) {
+    r = &R.take_slot_locked(lk);
+    ring_open_slot_ = -1;
+  }
+  if (!(ring_open_slot_ == R.cur_ && ring_open_seg_ + 1 == r->segs.size() && ring_open_seg_ >= r->submitted)) {
+    ConnRing::Seg g;
+    g.owner = this;
+    g.seq = ring_res_.size();
+    g.slot_off = static_cast<uint32_t>(r->used);
+    g.dst = obj_dst_ + delivered_;
+    RingRes rr;
+    rr.obj_off = delivered_;
+    ring_res_.push_back(rr);
+    r->segs.push_back(g);
+    ring_open_slot_ = R.cur_;
+    ring_open_seg_ = r->segs.size() - 1;
+  }
+  size_t cap = R.slot_bytes_ - r->used;
+  if (obj_cap_ - delivered_ < cap) cap = obj_cap_ - delivered_;
+  R.window_open_ = true;
+  R.window_owner_ = this;
+  return Window{r->host + r->used, cap};
+}
+
+void GpuSink::ring_commit(size_t n) {
+  ConnRing& R = *cfg_.conn_ring;
+  std::lock_guard<std::mutex> lk(R.mu_);
+  R.window_open_ = false;
+  R.window_owner_ = nullptr;
+  if (ring_open_slot_ != R.cur_ || R.cur_ < 0) throw std::logic_error("GpuSink::commit outside an acquired window");
+  ConnRing::RSlot& r = R.slots_[R.cur_];
+  ConnRing::Seg& g = r.segs[ring_open_seg_];
+  g.len += static_cast<uint32_t>(n);
+  r.used += n;
+  ring_res_[g.seq].len += static_cast<uint32_t>(n);
+  delivered_ += n;
+}
+
+// Submits what the reader is not writing into and waits for every segment
+// of this sink to have its result (the kernel publishes them; no HIP call).
+void GpuSink::ring_wait_all() {
+  ConnRing& R = *cfg_.conn_ring;
+  std::unique_lock<std::mutex> lk(R.mu_);
+  // this read is over (finish / abort / a retry): a window the reader opened
+  // for it and never committed (its recv failed) will never be written
+  if (R.window_open_ && R.window_owner_ == this) R.window_open_ = false;
+  if (R.owner_done_locked(this)) return;
+  R.flush_locked();
+  R.collect_all_locked();
+  const timespec ts{0, 10000};
+  while (!R.owner_done_locked(this)) {
+    lk.unlock();
+    nanosleep(&ts, nullptr);
+    lk.lock();
+    // a segment still being written (the reader's open window) is never this
+    // sink's once its read ended; anything else unsubmitted goes now
+    R.flush_locked();
+    R.collect_all_locked();
+  }
+  ring_open_slot_ = -1;
+}
+
+// Host fold of this read's segment CRCs: every chunk (gRPC message) against
+// its checksum, and the object.
+void GpuSink::ring_fold() {
+  std::lock_guard<std::mutex> lk(cfg_.conn_ring->mu_);
+  size_t ci = 0;
+  for (const RingRes& g : ring_res_) {
+    if (g.failed && detail_.empty()) {
+      mismatch_ = true;
+      detail_ = "GPU submit failed (connection ring)";
+    }
+    obj_raw_ = shift(obj_raw_, g.len) ^ g.raw;
+    obj_len_ += g.len;
+    while (ci < chunks_.size() && chunks_[ci].closed && chunks_[ci].end <= g.obj_off) ++ci;
+    if (ci >= chunks_.size()) continue;
+    ChunkMark& m = chunks_[ci];
+    if (g.obj_off == m.start) {
+      chunk_raw_ = 0;
+      chunk_len_ = 0;
+    }
+    if (g.obj_off < m.start) continue;  // bytes outside any chunk
+    chunk_raw_ = shift(chunk_raw_, g.len) ^ g.raw;
+    chunk_len_ += g.len;
+    if (m.closed && g.obj_off + g.len == m.end) {
+      if (m.has_crc && !m.broken) {
+        any_checked_ = true;
+        ++stats_.chunks_verified_host;
+        const uint32_t crc = chunk_raw_ ^ crc32c_fixup(chunk_len_);
+        if (crc != m.crc) {
+          mismatch_ = true;
+          char b[160];
+          std::snprintf(b, sizeof(b), "chunk crc32c mismatch at offset %llu: got %08x want %08x",
+                        static_cast<unsigned long long>(m.start), crc, m.crc);
+          detail_ = b;
+        }
+      }
+      ++ci;
+    }
+  }
+  stats_.segments += ring_res_.size();
 }
 
 // ---------------------------------------------------------------------------

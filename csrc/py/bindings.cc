@@ -471,6 +471,9 @@ class PyRunner {
     c.latency_fd = get_or<int>(d, "latency_fd", -1);
     c.keep_records = get_or<bool>(d, "keep_records", true);
     c.read_diag = get_or<bool>(d, "read_diag", false);
+    c.conn_ring = get_or<bool>(d, "conn_ring", c.conn_ring);
+    c.conn_ring_slot_bytes = get_or<size_t>(d, "conn_ring_slot_bytes", c.conn_ring_slot_bytes);
+    c.conn_ring_slots = get_or<int>(d, "conn_ring_slots", c.conn_ring_slots);
     if (d.contains("diag_avoid_cpus") && !d["diag_avoid_cpus"].is_none())
       c.diag_avoid_cpus = d["diag_avoid_cpus"].cast<std::vector<int>>();
     c.stop_on_error = get_or<bool>(d, "stop_on_error", true);
@@ -558,6 +561,18 @@ class PyRunner {
   uintptr_t landing_ptr(int w) { return runner_->landing_ptr(w); }
   std::vector<std::vector<long>> ring_numa(int w) { return runner_->ring_numa(w); }
   double ring_thp_fraction(int w) { return runner_->ring_thp_fraction(w); }
+  py::object conn_ring_stats() {
+    const ConnRing* r = runner_->conn_ring();
+    if (!r) return py::none();
+    const ConnRing::Stats s = r->stats();
+    py::dict d;
+    d["slots_filled"] = s.slots_filled;
+    d["submissions"] = s.submissions;
+    d["segments"] = s.segments;
+    d["reader_waits"] = s.reader_waits;
+    d["reader_wait_s"] = s.reader_wait_s;
+    return d;
+  }
   std::string transport_path() { return runner_->client().transport_path(); }
   void set_reads_per_worker(int64_t n) { runner_->set_reads_per_worker(n); }
   void reset_stats() { runner_->reset_stats(); }
@@ -1100,6 +1115,8 @@ PYBIND11_MODULE(_native, m) {
       .def("landing_ptr", &PyRunner::landing_ptr)
       .def("ring_numa", &PyRunner::ring_numa)
       .def("ring_thp_fraction", &PyRunner::ring_thp_fraction)
+      .def("conn_ring_stats", &PyRunner::conn_ring_stats,
+           "counters of the multiplexed connection's shared receive ring (None without one)")
       .def("transport_path", &PyRunner::transport_path)
       .def("set_reads_per_worker", &PyRunner::set_reads_per_worker)
       .def("reset_stats", &PyRunner::reset_stats);

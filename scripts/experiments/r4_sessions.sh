@@ -143,6 +143,15 @@ bigring)  # one stream into the multiplexed reader's footprint: does a 48-96 MiB
   step ab 500 python3 -u scripts/experiments/recv_cost_ab.py --tag bigring --reps 3 \
     --variants head_4x1m,head,head_24x2,head_48x2,nodma_48x2,nodma
   ;;
+connring)  # the connection ring: GPU tests, then the multiplexed GPU blocks with it on / off
+  step pytest_ring 300 python3 -u -m pytest tests/test_gpu_conn_ring.py -x -v --timeout 120 --timeout-method thread
+  for k in 1 2; do
+    for c in on off; do
+      step "ring_${c}_$k" 300 python3 bench.py --steps 5 --warmup 1 --blocks ref_default_100m,list_read \
+        --conn-ring $c --json-out "$O/ring_${c}_$k.json"
+    done
+  done
+  ;;
 soak)  # profiles/r4_soak: execute_pb.sh with 48 workers x 100 MiB, -sink gpu, 120 s per protocol, exporter at 30 s
   step soak 900 python3 -u scripts/soak.py --out "$O" --duration 120s
   ;;

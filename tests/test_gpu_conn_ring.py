@@ -1,0 +1,81 @@
+"""Connection ring (GpuSinkConfig::conn_ring, profiles/r4_bigring): every
+worker's gRPC stream on ONE multiplexed connection lands through one shared
+pinned ring -- segments of different streams side by side in a slot, one H2D
+per segment to its own object's HBM, one CRC launch per slot part, results
+collected per owner, chunks and objects folded on the host.  Compared
+against the bytes the endpoint serves (gpu_verify_pattern) and the
+endpoint's CRC32C values."""
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+B = "bkt"
+P = "ring/obj_"
+
+
+def _runner(native, server, workers, reads, slot_bytes, slots, **kw):
+    cfg = {"protocol": "grpc", "endpoint": server.url, "bucket": B, "object_prefix": P, "workers": workers,
+           "reads_per_worker": reads, "sink": "gpu", "grpc_conn_pool_size": 1, "keep_records": False,
+           "conn_ring_slot_bytes": slot_bytes, "conn_ring_slots": slots, "retry_initial_s": 0.01}
+    cfg.update(kw)
+    return native.Runner(cfg)
+
+
+@pytest.mark.parametrize("slot_bytes,slots", [(1 << 20, 8), (1 << 20, 2), (64 << 10, 3)])
+def test_conn_ring_many_streams_byte_exact(native, server, gpu_available, slot_bytes, slots):
+    workers = 12
+    sizes = [(3 << 20) + 4099 * i + 77 for i in range(workers)]
+    for i, n in enumerate(sizes):
+        server.add_synthetic(B, P, "", i, 1, n)
+    r = _runner(native, server, workers, 3, slot_bytes, slots)
+    r.start()
+    r.wait()
+    s = r.summary()
+    assert s["errors"] == 0 and s["verified"] == 3 * workers, s["first_error"]
+    st = r.conn_ring_stats()
+    assert st is not None and st["segments"] >= 3 * workers and st["submissions"] > 0
+    for w, n in enumerate(sizes):
+        bad, first = native.gpu_verify_pattern(0, r.landing_ptr(w), n, P + str(w), 0)
+        assert bad == 0, (w, first)
+
+
+def test_conn_ring_off_keeps_per_worker_rings(native, server, gpu_available):
+    server.add_synthetic(B, P, "", 0, 4, (2 << 20) + 5)
+    r = _runner(native, server, 4, 2, 1 << 20, 8, conn_ring=False)
+    r.start()
+    r.wait()
+    s = r.summary()
+    assert s["errors"] == 0 and s["verified"] == 8 and r.conn_ring_stats() is None
+
+
+def test_conn_ring_detects_corruption(native, server, gpu_available):
+    """One stream's corrupted byte fails that read's check (chunk and object
+    CRC on the host fold); the other streams sharing its slots verify."""
+    workers = 6
+    server.add_synthetic(B, P, "", 0, workers, 5 << 20)
+    r = _runner(native, server, workers, 1, 1 << 20, 4, stop_on_error=False)
+    server.set_faults({"corrupt_at": (2 << 20) + 11, "corrupt_count": 1})
+    r.start()
+    r.wait()
+    s = r.summary()
+    assert s["errors"] == 1 and s["verified"] == workers - 1
+    assert "crc" in s["first_error"].lower()
+
+
+def test_conn_ring_resume_after_disconnect(native, server, gpu_available):
+    """A connection cut mid-stream: every stream on it resumes at its
+    delivered offset on a new connection; the bytes already in the ring's
+    slots (from the old connection's reader) land, and every object lands
+    byte-exact."""
+    workers = 4
+    size = (6 << 20) + 321
+    server.add_synthetic(B, P, "", 0, workers, size)
+    r = _runner(native, server, workers, 2, 1 << 20, 4)
+    server.set_faults({"disconnect_at": (3 << 20) + 17, "disconnect_count": 1})
+    r.start()
+    r.wait()
+    s = r.summary()
+    assert s["errors"] == 0 and s["verified"] == 2 * workers, s["first_error"]
+    for w in range(workers):
+        bad, first = native.gpu_verify_pattern(0, r.landing_ptr(w), size, P + str(w), 0)
+        assert bad == 0, (w, first)

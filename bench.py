@@ -226,10 +226,10 @@ def build_parser() -> argparse.ArgumentParser:
                          "still in the receiving CCD's L3; against 8 x 2 MiB the receive copy went 0.046 -> 0.036 "
                          "CPU-s/GiB, 22.0k -> 27.5k MiB/s interleaved (profiles/r4_main8, profiles/r4_recvcost)")
     ap.add_argument("--slots", type=int, default=4)
-    ap.add_argument("--conn-ring", default="on", choices=["on", "off"],
+    ap.add_argument("--conn-ring", default="8x1MiB",
                     help="GPU sink on one multiplexed gRPC connection (list_read_grpc, ref_default_100m_grpc_gpu): "
-                         "every worker's stream through one 8 x 1 MiB connection ring instead of a ring per "
-                         "worker (profiles/r4_bigring)")
+                         "every worker's stream through one connection ring of SLOTSxBYTES instead of a ring per "
+                         "worker (profiles/r4_bigring, r4_connring); off: a ring per worker")
     ap.add_argument("--crc-slot-waves", type=int, default=0, choices=[0, 1, 2, 4, 8],
                     help="slot CRC kernel waves per workgroup (0: by slot size); A/B of the kernel's table staging")
     ap.add_argument("--async-submit", type=int, default=1, choices=[0, 1],
@@ -485,7 +485,9 @@ def run_rank(args) -> int:
         "device": gpu if use_gpu else 0,
         "ring_slot_bytes": parse_size(args.slot_bytes),
         "ring_slots": args.slots,
-        "conn_ring": args.conn_ring == "on",
+        "conn_ring": args.conn_ring != "off",
+        "conn_ring_slots": int(args.conn_ring.partition("x")[0]) if "x" in args.conn_ring else 8,
+        "conn_ring_slot_bytes": parse_size(args.conn_ring.partition("x")[2]) if "x" in args.conn_ring else 1 << 20,
         "landing": "object",
         "grpc_conn_pool_size": args.grpc_pool,
         "keep_records": False,
@@ -1166,6 +1168,8 @@ def run_rank(args) -> int:
                     b["endpoint_tcp"] = st["cpu"]["endpoint_tcp"]
                 if st["cpu"].get("endpoint_h2"):
                     b["endpoint_h2"] = st["cpu"]["endpoint_h2"]
+                if st["cpu"].get("conn_ring"):
+                    b["conn_ring"] = st["cpu"]["conn_ring"]
                 if key.startswith(("compare", "cpu_baseline", "ref_default_", "list_read_")) and st["cpu"].get("host"):
                     b["host"] = st["cpu"]["host"]
             if key.startswith("ref_default_100m_") and key.endswith("_gpu"):

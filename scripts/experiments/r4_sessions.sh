@@ -152,6 +152,14 @@ connring)  # the connection ring: GPU tests, then the multiplexed GPU blocks wit
     done
   done
   ;;
+ringgeom)  # connection-ring geometry for the 48 x 100 MiB gRPC -> HBM block and config-3 list-read
+  for k in 1 2; do
+    for c in 8x1MiB 4x1MiB 16x1MiB 8x2MiB 4x2MiB off; do
+      step "geom_${c}_$k" 300 python3 bench.py --steps 5 --warmup 1 --blocks ref_default_100m,list_read \
+        --conn-ring $c --json-out "$O/geom_${c}_$k.json"
+    done
+  done
+  ;;
 soak)  # profiles/r4_soak: execute_pb.sh with 48 workers x 100 MiB, -sink gpu, 120 s per protocol, exporter at 30 s
   step soak 900 python3 -u scripts/soak.py --out "$O" --duration 120s
   ;;

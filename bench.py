@@ -226,7 +226,7 @@ def build_parser() -> argparse.ArgumentParser:
                          "still in the receiving CCD's L3; against 8 x 2 MiB the receive copy went 0.046 -> 0.036 "
                          "CPU-s/GiB, 22.0k -> 27.5k MiB/s interleaved (profiles/r4_main8, profiles/r4_recvcost)")
     ap.add_argument("--slots", type=int, default=4)
-    ap.add_argument("--conn-ring", default="8x1MiB",
+    ap.add_argument("--conn-ring", default="4x1MiB",
                     help="GPU sink on one multiplexed gRPC connection (list_read_grpc, ref_default_100m_grpc_gpu): "
                          "every worker's stream through one connection ring of SLOTSxBYTES instead of a ring per "
                          "worker (profiles/r4_bigring, r4_connring); off: a ring per worker")
@@ -486,7 +486,7 @@ def run_rank(args) -> int:
         "ring_slot_bytes": parse_size(args.slot_bytes),
         "ring_slots": args.slots,
         "conn_ring": args.conn_ring != "off",
-        "conn_ring_slots": int(args.conn_ring.partition("x")[0]) if "x" in args.conn_ring else 8,
+        "conn_ring_slots": int(args.conn_ring.partition("x")[0]) if "x" in args.conn_ring else 4,
         "conn_ring_slot_bytes": parse_size(args.conn_ring.partition("x")[2]) if "x" in args.conn_ring else 1 << 20,
         "landing": "object",
         "grpc_conn_pool_size": args.grpc_pool,

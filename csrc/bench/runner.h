@@ -73,10 +73,13 @@ struct RunnerConfig {
   // GPU sink on ONE multiplexed gRPC connection (pool size 1, several
   // workers): every worker's stream lands through one connection ring
   // (GpuSinkConfig::conn_ring) of conn_ring_slots x conn_ring_slot_bytes
-  // instead of a ring per worker (profiles/r4_bigring).
+  // instead of a ring per worker (profiles/r4_bigring).  4 x 1 MiB, as the
+  // one-stream headline: 48 x 100 MiB gRPC -> HBM 19.3k / 21.5k MiB/s against
+  // 16.8k / 18.0k with 8 x 1 MiB, 15.4k / 14.1k with 16 x 1 MiB and 13.9k /
+  // 15.5k with a ring per worker (profiles/r4_ringgeom).
   bool conn_ring = true;
   size_t conn_ring_slot_bytes = size_t(1) << 20;
-  int conn_ring_slots = 8;
+  int conn_ring_slots = 4;
   // CPUs the read_diag sampler must not run on (the placement's; the client
   // CPUs are always added): sched_sample_offcore
   std::vector<int> diag_avoid_cpus;

@@ -88,7 +88,8 @@ struct GpuSinkConfig {
   // 48 per-worker rings of 2 x 2 MiB are 192 MiB of receive destinations, far
   // past the reader's L3, and a one-stream read into a ring that size pays
   // the same 0.056-0.066 CPU-s/GiB as the multiplexed reader
-  // (profiles/r4_bigring); one 8 x 1 MiB ring per connection stays L3-hot.
+  // (profiles/r4_bigring); one 4 x 1 MiB ring per connection stays L3-hot
+  // (profiles/r4_ringgeom).
   // Object landing with CRC verification only; not owned by the sink.
   ConnRing* conn_ring = nullptr;
 };

@@ -290,9 +290,12 @@ def build_parser() -> argparse.ArgumentParser:
                     help="cpu_baseline side blocks: the headline config with the reference's semantics (discard "
                          "sink, host CRC32C; /root/reference/main.go:133-146) on the same endpoint, placement and "
                          "steps, for the headline protocol and the other one; vs_baseline = value / it")
-    ap.add_argument("--baseline-bracket", action="store_true",
-                    help="also run the reference-semantics baseline before the headline (cpu_baseline_before), so "
-                         "the two baselines bracket it (A/B sessions on drifting hosts)")
+    ap.add_argument("--baseline-bracket", default="auto", choices=["auto", "on", "off"],
+                    help="also run the reference-semantics baseline right before the headline (cpu_baseline_before): "
+                         "vs_baseline then divides by the pooled rate of the two runs that bracket the headline, so a "
+                         "host drifting between blocks cancels (the same baseline swung 12%% between two benches on "
+                         "one box, profiles/r4_main9).  auto: on at N = 1; off at N > 1, where nothing may run "
+                         "before the headline")
     ap.add_argument("--ceiling", default="on", choices=["on", "off"],
                     help="ceiling side block: one loopback TCP stream (sendfile -> recv into a THP ring, no GPU, "
                          "no framing) and pinned -> HBM copies, in the headline's placement")
@@ -1020,7 +1023,10 @@ def run_rank(args) -> int:
 
     # ---- headline --------------------------------------------------------
     base_before = None
-    if args.workload == "read" and use_gpu and args.baseline_bracket and args.baseline == "on":
+    bracket = args.baseline_bracket == "on" or (args.baseline_bracket == "auto" and world == 1)
+    _only = {b.strip() for b in args.blocks.split(",") if b.strip()} - {"all"}
+    if args.workload == "read" and use_gpu and bracket and args.baseline == "on" and \
+            (not _only or "cpu_baseline" in _only) and side_steps > 0:
         # the reference-semantics read once more BEFORE the headline, so the
         # two baselines bracket it and a drifting host cancels (A/B sessions)
         base_before = read_block(baseline_over(), side_steps, side_warm, f"{protocol} cpu baseline (before)")
@@ -1143,11 +1149,23 @@ def run_rank(args) -> int:
                 out["cpus_needed_per_gpu"] = round(head["cpu"]["process_cpu_s_per_gib"] * gib_s, 2)
         base = blocks.get("cpu_baseline")
         if base is not None and base[1]["ok_min"] >= 1.0 and mib_s(base[1]) > 0:
-            out["vs_baseline"] = round(value / mib_s(base[1]), 3)
-            out["baseline"] = {"what": "cpu_baseline block: same config, reference semantics (discard sink + "
-                                       "host CRC32C), same run", "mib_s": round(mib_s(base[1]), 2),
-                               "p50_ms": round(base[1]["p50_max"], 3),
-                               "p50_ratio": round(base[1]["p50_max"] / max(head["p50_max"], 1e-9), 3)}
+            bst = base[1]
+            runs = [bst]
+            if base_before is not None and base_before["ok_min"] >= 1.0 and mib_s(base_before) > 0:
+                runs = [base_before, bst]
+            # pooled over the runs bracketing the headline: all their bytes over all their time
+            pooled = sum(r["nbytes_sum"] for r in runs) / max(sum(r["elapsed_max"] for r in runs), 1e-12) / (1 << 20)
+            p50 = sorted(r["p50_max"] for r in runs)[len(runs) // 2] if len(runs) == 1 else \
+                sum(r["p50_max"] for r in runs) / len(runs)
+            out["vs_baseline"] = round(value / pooled, 3)
+            out["baseline"] = {"what": "cpu_baseline: same config, reference semantics (discard sink + host CRC32C), "
+                                       "same run" + (", run right before and right after the headline, pooled"
+                                                     if len(runs) == 2 else ", run right after the headline"),
+                               "mib_s": round(pooled, 2), "p50_ms": round(p50, 3),
+                               "p50_ratio": round(p50 / max(head["p50_max"], 1e-9), 3)}
+            if len(runs) == 2:
+                out["baseline"]["mib_s_before"] = round(mib_s(base_before), 2)
+                out["baseline"]["mib_s_after"] = round(mib_s(bst), 2)
         for key, (_, st, extra) in blocks.items():
             if extra is None:  # already a JSON block (ceiling)
                 out[key] = st

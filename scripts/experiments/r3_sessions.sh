@@ -50,7 +50,7 @@ slotreuse)  # profiles/r3_twins/slotreuse: the receiving thread's time reusing r
   ;;
 bracket)  # profiles/r3_twins/bracket: the two-core baseline before AND after the headline (drift cancels)
   for k in 1 2 3 4 5; do
-    step "k_$k" 300 python3 bench.py --steps 20 --warmup 3 --baseline-bracket --blocks cpu_baseline,ceiling \
+    step "k_$k" 300 python3 bench.py --steps 20 --warmup 3 --baseline-bracket on --blocks cpu_baseline,ceiling \
       --json-out "$O/k_$k.json"
   done
   ;;

@@ -98,7 +98,11 @@ Runner::Runner(RunnerConfig cfg) : cfg_(std::move(cfg)) {
   reserve_fd_table();
   if (cfg_.workers <= 0) throw StorageError("worker count not valid", false);
   const GpuSinkConfig& g = cfg_.gpu;
-  if (cfg_.conn_ring && cfg_.sink == "gpu" && cfg_.client.protocol == "grpc" && cfg_.client.grpc_conn_pool_size == 1 &&
+  // one connection carries every worker's stream: gRPC with pool size 1, or
+  // HTTP/2 media GETs (always one connection)
+  const bool one_conn = (cfg_.client.protocol == "grpc" && cfg_.client.grpc_conn_pool_size == 1) ||
+                        cfg_.client.protocol == "http2";
+  if (cfg_.conn_ring && cfg_.sink == "gpu" && one_conn &&
       cfg_.workers > 1 && cfg_.slices <= 1 && g.verify && g.landing == Landing::kObject &&
       g.stage == GpuSinkConfig::Stage::kH2D)
     conn_ring_ = std::make_unique<ConnRing>(g.device, cfg_.conn_ring_slot_bytes, cfg_.conn_ring_slots);

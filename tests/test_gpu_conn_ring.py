@@ -13,21 +13,22 @@ B = "bkt"
 P = "ring/obj_"
 
 
-def _runner(native, server, workers, reads, slot_bytes, slots, **kw):
-    cfg = {"protocol": "grpc", "endpoint": server.url, "bucket": B, "object_prefix": P, "workers": workers,
+def _runner(native, server, workers, reads, slot_bytes, slots, proto="grpc", **kw):
+    cfg = {"protocol": proto, "endpoint": server.url, "bucket": B, "object_prefix": P, "workers": workers,
            "reads_per_worker": reads, "sink": "gpu", "grpc_conn_pool_size": 1, "keep_records": False,
            "conn_ring_slot_bytes": slot_bytes, "conn_ring_slots": slots, "retry_initial_s": 0.01}
     cfg.update(kw)
     return native.Runner(cfg)
 
 
-@pytest.mark.parametrize("slot_bytes,slots", [(1 << 20, 8), (1 << 20, 2), (64 << 10, 3)])
-def test_conn_ring_many_streams_byte_exact(native, server, gpu_available, slot_bytes, slots):
+@pytest.mark.parametrize("proto,slot_bytes,slots", [("grpc", 1 << 20, 4), ("grpc", 1 << 20, 2), ("grpc", 64 << 10, 3),
+                                                    ("http2", 1 << 20, 4)])
+def test_conn_ring_many_streams_byte_exact(native, server, gpu_available, proto, slot_bytes, slots):
     workers = 12
     sizes = [(3 << 20) + 4099 * i + 77 for i in range(workers)]
     for i, n in enumerate(sizes):
         server.add_synthetic(B, P, "", i, 1, n)
-    r = _runner(native, server, workers, 3, slot_bytes, slots)
+    r = _runner(native, server, workers, 3, slot_bytes, slots, proto=proto)
     r.start()
     r.wait()
     s = r.summary()

@@ -92,6 +92,10 @@ struct GpuSinkConfig {
   // (profiles/r4_ringgeom).
   // Object landing with CRC verification only; not owned by the sink.
   ConnRing* conn_ring = nullptr;
+  // Cached rings live in one contiguous pinned region and a receive window
+  // runs on into the next slot when it is free (GpuSink::acquire); false:
+  // every window stops at its slot's end (A/B).
+  bool ring_span = true;
 };
 
 struct GpuSinkStats {
@@ -171,6 +175,7 @@ class GpuSink : public Sink {
   void ensure_object_capacity(int64_t size);
   void grow_object_buffer(uint64_t need);
   Slot& take_slot();
+  void open_seg(Slot& s);
   void submit_current();
   // conn-ring mode (cfg_.conn_ring)
   Window ring_acquire();
@@ -186,6 +191,8 @@ class GpuSink : public Sink {
 
   GpuSinkConfig cfg_;
   std::vector<Slot> slots_;
+  uint8_t* ring_base_ = nullptr;  // cached rings: all slots in one contiguous pinned region
+  bool spill_ = false;           // the last window runs on into the next slot
   int cur_ = -1;         // FILLING slot index or -1
   int next_ = 0;         // next slot to take
   const CrcTables* d_tables_ = nullptr;

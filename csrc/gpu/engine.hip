@@ -554,7 +554,10 @@ GpuSink::GpuSink(const GpuSinkConfig& cfg) : cfg_(cfg) {
   for (int i = 0; i < cfg_.slots; ++i) {
     Slot& s = slots_[i];
     // on the GPU's NUMA node (the rank's pinned receive thread runs there too)
-    s.host = static_cast<uint8_t*>(PinnedPool::get(cfg_.slot_bytes, device_numa_node(cfg_.device), cfg_.ring_wc));
+    if (!cfg_.ring_wc && i == 0)
+      ring_base_ = static_cast<uint8_t*>(PinnedPool::get(cfg_.slot_bytes * cfg_.slots, device_numa_node(cfg_.device)));
+    s.host = ring_base_ ? ring_base_ + cfg_.slot_bytes * static_cast<size_t>(i)
+                        : static_cast<uint8_t*>(PinnedPool::get(cfg_.slot_bytes, device_numa_node(cfg_.device), true));
     if (cfg_.landing == Landing::kRing)
       hip_check(hipMalloc(reinterpret_cast<void**>(&s.dev_ring), cfg_.slot_bytes), "hipMalloc(ring slot)");
     const unsigned evf = hipEventDisableTiming | (cfg_.blocking_sync ? hipEventBlockingSync : 0u);
@@ -574,8 +577,9 @@ GpuSink::~GpuSink() {
     set_device();
   } catch (...) {
   }
+  if (ring_base_) PinnedPool::put(ring_base_, cfg_.slot_bytes * cfg_.slots);
   for (Slot& s : slots_) {
-    PinnedPool::put(s.host, cfg_.slot_bytes);
+    if (!ring_base_) PinnedPool::put(s.host, cfg_.slot_bytes);
     if (s.dev_ring) (void)hipFree(s.dev_ring);
     if (s.ev) (void)hipEventDestroy(s.ev);
   }
@@ -700,6 +704,17 @@ GpuSink::Slot& GpuSink::take_slot() {
   return s;
 }
 
+void GpuSink::open_seg(Slot& s) {
+  if (!s.segs.empty() && !s.segs.back().closed) return;
+  SegInfo g;
+  g.slot_off = s.used;
+  g.obj_off = delivered_;
+  g.chunk_start = chunk_start_pending_;
+  g.broken_chunk = chunk_broken_;
+  chunk_start_pending_ = false;
+  s.segs.push_back(g);
+}
+
 Window GpuSink::acquire(size_t want) {
   (void)want;
   if (cfg_.conn_ring) return ring_acquire();
@@ -713,15 +728,7 @@ Window GpuSink::acquire(size_t want) {
     }
   }
   Slot& s = slots_[cur_];
-  if (s.segs.empty() || s.segs.back().closed) {
-    SegInfo g;
-    g.slot_off = s.used;
-    g.obj_off = delivered_;
-    g.chunk_start = chunk_start_pending_;
-    g.broken_chunk = chunk_broken_;
-    chunk_start_pending_ = false;
-    s.segs.push_back(g);
-  }
+  open_seg(s);
   size_t cap = cfg_.slot_bytes - s.used;
   if (cfg_.landing == Landing::kObject) {
     if (delivered_ >= obj_cap_) {
@@ -730,12 +737,48 @@ Window GpuSink::acquire(size_t want) {
     }
     if (obj_cap_ - delivered_ < cap) cap = obj_cap_ - delivered_;
   }
+  // The ring is one contiguous region: when the next slot is free, the
+  // window runs on into it, so one recv() is not cut at a slot boundary
+  // (648 KiB per recv into 1 MiB slots against 954 KiB into the discard
+  // sink's 2 MiB blocks, profiles/r4_final1); commit() splits the bytes.
+  spill_ = false;
+  if (ring_base_ && cfg_.ring_span && cur_ + 1 < cfg_.slots && next_ == cur_ + 1 && cap == cfg_.slot_bytes - s.used &&
+      s.segs.size() < static_cast<size_t>(kMaxSeg)) {
+    Slot& n = slots_[next_];
+    if (n.inflight && done_by_flags(n)) {
+      n.inflight = false;
+      ++stats_.flag_reuses;
+      harvest(n);
+    }
+    if (!n.inflight) {
+      size_t more = cfg_.slot_bytes;
+      if (cfg_.landing == Landing::kObject && obj_cap_ - delivered_ - cap < more) more = obj_cap_ - delivered_ - cap;
+      if (more > 0) {
+        cap += more;
+        spill_ = true;
+      }
+    }
+  }
   // keep a segment below 4 GiB (32-bit length in the kernel batch)
   return Window{s.host + s.used, cap};
 }
 
 void GpuSink::commit(size_t n) {
   if (cfg_.conn_ring) return ring_commit(n);
+  if (spill_) {
+    spill_ = false;
+    const size_t room = cfg_.slot_bytes - slots_[cur_].used;
+    if (n > room) {
+      // the recv ran on into the next slot: this slot is full, the rest of
+      // the bytes already sit at the start of the next one
+      commit(room);
+      submit_current();
+      take_slot();
+      open_seg(slots_[cur_]);
+      commit(n - room);
+      return;
+    }
+  }
   Slot& s = slots_[cur_];
   if (debug_ring() && (s.segs.empty() || s.segs.back().closed || s.used + n > cfg_.slot_bytes))
     throw std::logic_error("GpuSink::commit outside an acquired window");

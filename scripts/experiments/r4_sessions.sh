@@ -174,6 +174,14 @@ final1)  # checkpoint on the final round-4 defaults (4 x 1 MiB headline ring, co
   python3 -c "print('rehearsal8 wall_s', round($(date +%s.%N)-$t0, 1))" > "$O/rehearsal8_wall.txt"
   step soak 600 python3 -u scripts/soak.py --out "$O/soak" --duration 60s --metrics-interval 20s
   ;;
+span)  # receive windows spanning two free slots of the contiguous ring (fewer recv calls) vs stopping at each slot
+  step pytest_sink 400 python3 -u -m pytest tests/test_gpu_sink.py tests/test_gpu_conn_ring.py tests/test_gpu_large_object.py \
+    -x -q --timeout 120 --timeout-method thread
+  step ab 500 python3 -u scripts/experiments/recv_cost_ab.py --tag span --reps 5 \
+    --variants head_4x1m,head_4x1m_nospan,head_8x512k,head_8x512k_nospan,nodma,base
+  step bench1 600 python3 bench.py --json-out "$O/bench1.json"
+  step bench2 600 python3 bench.py --json-out "$O/bench2.json"
+  ;;
 soak)  # profiles/r4_soak: execute_pb.sh with 48 workers x 100 MiB, -sink gpu, 120 s per protocol, exporter at 30 s
   step soak 900 python3 -u scripts/soak.py --out "$O" --duration 120s
   ;;

@@ -88,6 +88,9 @@ variants = {
     # hand-off before it sleeps (no futex wake per slot on the receiver)
     "head_spin": {"sink": "gpu"},
     "head_4x1m_spin": {"sink": "gpu", "ring_slot_bytes": 1 << 20, "ring_slots": 4},
+    # windows stop at each slot's end (before: a recv ran on into the next free slot)
+    "head_4x1m_nospan": {"sink": "gpu", "ring_slot_bytes": 1 << 20, "ring_slots": 4, "ring_span": False},
+    "head_8x512k_nospan": {"sink": "gpu", "ring_slot_bytes": 512 << 10, "ring_slots": 8, "ring_span": False},
     # the multiplexed reader's destination footprint on one stream: 48 MiB /
     # 96 MiB rings (48 workers x 1-2 MiB), with and without the DMA
     "head_24x2": {"sink": "gpu", "ring_slots": 24},

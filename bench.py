@@ -605,8 +605,11 @@ def run_rank(args) -> int:
                 # the receiving thread reusing ring slots: on the CRC kernel's
                 # host-visible status (no HIP call), or waiting for the slot's
                 # hand-off + its event; then harvesting its CRC results
+                gib = max(float(s1["bytes"]) / (1 << 30), 1e-9)
                 cpu["slot_reuse"] = {"waits": g1["slot_waits"], "on_kernel_status": g1.get("flag_reuses", 0),
-                                     "s_per_gib": round(g1["slot_wait_s"] / max(float(s1["bytes"]) / (1 << 30), 1e-9), 4)}
+                                     "s_per_gib": round(g1["slot_wait_s"] / gib, 4),
+                                     # the receiving thread inside submit + take (bookkeeping, hand-off, waits)
+                                     "handoff_s_per_gib": round(g1.get("handoff_s", 0.0) / gib, 5)}
             sv1 = ep_stats()
             if sv1.get("h2_data_frames", 0) > sv0.get("h2_data_frames", 0):
                 # the endpoint's HTTP/2 fairness: how long stream handlers

@@ -376,6 +376,7 @@ void Runner::worker_main(int w) {
       t.slot_waits += g.slot_waits;
       t.slot_wait_s += g.slot_wait_s;
       t.flag_reuses += g.flag_reuses;
+      t.handoff_s += g.handoff_s;
     }
     std::lock_guard<std::mutex> lk(mu_);
     gpu_stats_[w] = t;
@@ -440,6 +441,7 @@ RunSummary Runner::summary(bool percentiles) const {
     s.gpu.slot_waits += g.slot_waits;
     s.gpu.slot_wait_s += g.slot_wait_s;
     s.gpu.flag_reuses += g.flag_reuses;
+    s.gpu.handoff_s += g.handoff_s;
   }
   return s;
 }

@@ -107,6 +107,7 @@ struct GpuSinkStats {
   uint64_t slot_waits = 0;            // transport had to wait for a free slot
   double slot_wait_s = 0;
   uint64_t flag_reuses = 0;           // slots reused on the kernel's host-visible status (no HIP call)
+  double handoff_s = 0;               // receiving thread inside the slot hand-off (submit + take, waits included)
 };
 
 class GpuSink : public Sink {

@@ -684,6 +684,7 @@ bool GpuSink::done_by_flags(const Slot& s) const {
 }
 
 GpuSink::Slot& GpuSink::take_slot() {
+  const int64_t h0 = now_ns();
   Slot& s = slots_[next_];
   if (s.inflight && done_by_flags(s)) {
     s.inflight = false;
@@ -701,6 +702,7 @@ GpuSink::Slot& GpuSink::take_slot() {
   s.obj_off = delivered_;
   cur_ = next_;
   next_ = (next_ + 1) % cfg_.slots;
+  stats_.handoff_s += (now_ns() - h0) / 1e9;
   return s;
 }
 
@@ -873,6 +875,11 @@ void GpuSink::resume_at(int64_t offset) {
 void GpuSink::submit_current() {
   if (cur_ < 0) return;
   RoctxRange rg("gcsb.slot_submit");
+  struct Timed {
+    double* acc;
+    int64_t t0 = now_ns();
+    ~Timed() { *acc += (now_ns() - t0) / 1e9; }
+  } timed{&stats_.handoff_s};
   Slot& s = slots_[cur_];
   cur_ = -1;
   if (s.used == 0) {

@@ -166,6 +166,7 @@ py::dict gpu_stats_dict(const GpuSinkStats& g) {
   r["slot_waits"] = g.slot_waits;
   r["slot_wait_s"] = g.slot_wait_s;
   r["flag_reuses"] = g.flag_reuses;
+  r["handoff_s"] = g.handoff_s;
   return r;
 }
 

@@ -182,6 +182,11 @@ span)  # receive windows spanning two free slots of the contiguous ring (fewer r
   step bench1 600 python3 bench.py --json-out "$O/bench1.json"
   step bench2 600 python3 bench.py --json-out "$O/bench2.json"
   ;;
+handoff)  # how much of the receiving thread the slot hand-off takes (GpuSinkStats::handoff_s)
+  step ab 400 python3 -u scripts/experiments/recv_cost_ab.py --tag handoff --reps 3 \
+    --variants head_4x1m,head,nodma,base
+  step bench1 600 python3 bench.py --json-out "$O/bench1.json"
+  ;;
 soak)  # profiles/r4_soak: execute_pb.sh with 48 workers x 100 MiB, -sink gpu, 120 s per protocol, exporter at 30 s
   step soak 900 python3 -u scripts/soak.py --out "$O" --duration 120s
   ;;

@@ -135,6 +135,7 @@ def run(name):
             "reader_data_s_per_gib": round(hd["data_ns"] / 1e9 / gib, 4),
             "endpoint_cpu_s_per_gib": round(sum(v for k, v in d.items() if k.startswith("gcsb-srv")) / gib, 4),
             "submit_cpu_s_per_gib": round(d.get("gcsb-submit", 0.0) / gib, 4),
+            "handoff_s_per_gib": round((s.get("gpu") or {}).get("handoff_s", 0.0) / gib, 5),
             "worker_cpu_s_per_gib": round(s.get("worker_cpu_s", 0.0) / gib, 4),
             "endpoint_busy_frac": round((sv1["tcp_busy_us"] - sv0["tcp_busy_us"]) / wall, 3),
             "errors": s["errors"], "sched": diag}

@@ -187,6 +187,10 @@ handoff)  # how much of the receiving thread the slot hand-off takes (GpuSinkSta
     --variants head_4x1m,head,nodma,base
   step bench1 600 python3 bench.py --json-out "$O/bench1.json"
   ;;
+pfw)  # PREFETCHW over the next receive window (re-own the lines the copy engine read)
+  step ab 500 python3 -u scripts/experiments/recv_cost_ab.py --tag pfw --reps 5 \
+    --variants head_4x1m,head_4x1m_pfw256k,head_4x1m_pfw1m,nodma,base
+  ;;
 soak)  # profiles/r4_soak: execute_pb.sh with 48 workers x 100 MiB, -sink gpu, 120 s per protocol, exporter at 30 s
   step soak 900 python3 -u scripts/soak.py --out "$O" --duration 120s
   ;;

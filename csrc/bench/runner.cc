@@ -163,6 +163,14 @@ void Runner::reset_stats() {
   t_first_ = t_last_ = 0;
   for (auto& s : sliced_)
     if (s) s->reset_skew();
+  // the sinks live across phases: their counters restart with the timed reads
+  for (GpuSink* g : gpu_sinks_)
+    if (g) g->reset_stats();
+  if (cfg_.sink == "gpu")
+    for (auto& sr : sliced_)
+      if (sr)
+        for (int i = 0; i < sr->num_sinks(); ++i) static_cast<GpuSink&>(sr->sink(i)).reset_stats();
+  for (auto& g : gpu_stats_) g = GpuSinkStats();
 }
 
 void Runner::start() {

@@ -129,6 +129,7 @@ class GpuSink : public Sink {
   void* object_device_ptr() const { return obj_dst_; }
   size_t object_capacity() const { return obj_cap_; }
   const GpuSinkStats& stats() const { return stats_; }
+  void reset_stats() { stats_ = GpuSinkStats(); }  // between phases (runner warmup -> timed)
   // host ring slots (ptr, bytes): placement diagnostics
   std::vector<std::pair<const void*, size_t>> ring_ranges() const {
     std::vector<std::pair<const void*, size_t>> r;

@@ -96,10 +96,6 @@ struct GpuSinkConfig {
   // runs on into the next slot when it is free (GpuSink::acquire); false:
   // every window stops at its slot's end (A/B).
   bool ring_span = true;
-  // > 0: before handing out a receive window, prefetch-for-write its first
-  // this many bytes (PREFETCHW), so the receiving core re-owns the lines the
-  // copy engine just read in parallel, ahead of the kernel's copy (A/B).
-  size_t prefetchw_bytes = 0;
 };
 
 struct GpuSinkStats {

@@ -761,11 +761,6 @@ Window GpuSink::acquire(size_t want) {
       }
     }
   }
-  if (cfg_.prefetchw_bytes) {
-    uint8_t* p = s.host + s.used;
-    const size_t n = std::min(cap, cfg_.prefetchw_bytes);
-    for (size_t o = 0; o < n; o += 64) asm volatile("prefetchw (%0)" : : "r"(p + o));
-  }
   // keep a segment below 4 GiB (32-bit length in the kernel batch)
   return Window{s.host + s.used, cap};
 }

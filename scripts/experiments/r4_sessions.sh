@@ -187,7 +187,8 @@ handoff)  # how much of the receiving thread the slot hand-off takes (GpuSinkSta
     --variants head_4x1m,head,nodma,base
   step bench1 600 python3 bench.py --json-out "$O/bench1.json"
   ;;
-pfw)  # PREFETCHW over the next receive window (re-own the lines the copy engine read)
+pfw)  # PREFETCHW over the next receive window (re-own the lines the copy engine read); the option was
+  # removed after this session (profiles/r4_recvcost), the pfw variants no longer exist
   step ab 500 python3 -u scripts/experiments/recv_cost_ab.py --tag pfw --reps 5 \
     --variants head_4x1m,head_4x1m_pfw256k,head_4x1m_pfw1m,nodma,base
   ;;

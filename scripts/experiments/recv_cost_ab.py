@@ -89,9 +89,6 @@ variants = {
     "head_spin": {"sink": "gpu"},
     "head_4x1m_spin": {"sink": "gpu", "ring_slot_bytes": 1 << 20, "ring_slots": 4},
     # windows stop at each slot's end (before: a recv ran on into the next free slot)
-    # the receiving core re-owns the next window's lines (PREFETCHW) before the recv
-    "head_4x1m_pfw256k": {"sink": "gpu", "ring_slot_bytes": 1 << 20, "ring_slots": 4, "prefetchw_bytes": 256 << 10},
-    "head_4x1m_pfw1m": {"sink": "gpu", "ring_slot_bytes": 1 << 20, "ring_slots": 4, "prefetchw_bytes": 1 << 20},
     "head_4x1m_nospan": {"sink": "gpu", "ring_slot_bytes": 1 << 20, "ring_slots": 4, "ring_span": False},
     "head_8x512k_nospan": {"sink": "gpu", "ring_slot_bytes": 512 << 10, "ring_slots": 8, "ring_span": False},
     # the multiplexed reader's destination footprint on one stream: 48 MiB /

@@ -80,3 +80,23 @@ def test_conn_ring_resume_after_disconnect(native, server, gpu_available):
     for w in range(workers):
         bad, first = native.gpu_verify_pattern(0, r.landing_ptr(w), size, P + str(w), 0)
         assert bad == 0, (w, first)
+
+
+@pytest.mark.parametrize("proto", ["grpc", "http2"])
+def test_conn_ring_stalled_stream_resumes(native, server, gpu_available, proto):
+    """One stream goes silent mid-body past the read timeout: it is cancelled
+    alone (its segments already in the ring still land), resumes at its
+    delivered offset, and every stream sharing the ring lands byte-exact."""
+    workers = 6
+    size = (3 << 20) + 999
+    server.add_synthetic(B, P, "", 0, workers, size)
+    server.set_faults({"stall_at": 1 << 20, "stall_ms": 800, "stall_count": 1})
+    r = _runner(native, server, workers, 2, 1 << 20, 4, proto=proto, io_timeout_ms=100, retry_max_attempts=3)
+    r.start()
+    r.wait()
+    s = r.summary()
+    assert s["errors"] == 0 and s["verified"] == 2 * workers, s["first_error"]
+    assert s["retries"] >= 1
+    for w in range(workers):
+        bad, first = native.gpu_verify_pattern(0, r.landing_ptr(w), size, P + str(w), 0)
+        assert bad == 0, (w, first)

@@ -192,6 +192,12 @@ pfw)  # PREFETCHW over the next receive window (re-own the lines the copy engine
   step ab 500 python3 -u scripts/experiments/recv_cost_ab.py --tag pfw --reps 5 \
     --variants head_4x1m,head_4x1m_pfw256k,head_4x1m_pfw1m,nodma,base
   ;;
+final2)  # checkpoint after span / handoff counters / stat resets: GPU suite, smoke, two benches
+  step pytest_gpu 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+  step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+  step bench1 600 python3 bench.py --json-out "$O/bench1.json"
+  step bench2 600 python3 bench.py --json-out "$O/bench2.json"
+  ;;
 soak)  # profiles/r4_soak: execute_pb.sh with 48 workers x 100 MiB, -sink gpu, 120 s per protocol, exporter at 30 s
   step soak 900 python3 -u scripts/soak.py --out "$O" --duration 120s
   ;;

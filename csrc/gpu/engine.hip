@@ -1100,6 +1100,12 @@ void GpuSink::abort() {
 // connection ring (engine.h ConnRing): one receive ring per multiplexed
 // connection, shared by the sinks of every stream on it
 
+namespace {
+// A GPU that never publishes a result (a fault) must not hang the reader or
+// a finishing worker forever.
+constexpr int64_t kRingWaitLimitNs = 60LL * 1000 * 1000 * 1000;
+}  // namespace
+
 ConnRing::ConnRing(int device, size_t slot_bytes, int slots) : device_(device) {
   slot_bytes_ = std::max<size_t>((slot_bytes + 4095) / 4096 * 4096, 65536);
   if (slots < 2) slots = 2;
@@ -1264,6 +1270,8 @@ ConnRing::RSlot& ConnRing::take_slot_locked(std::unique_lock<std::mutex>& lk) {
     const int64_t t0 = now_ns();
     const timespec ts{0, 10000};
     while (r.collected < r.segs.size()) {
+      if (now_ns() - t0 > kRingWaitLimitNs)
+        throw std::runtime_error("connection ring: a slot's CRC results did not arrive within 60 s");
       lk.unlock();
       nanosleep(&ts, nullptr);
       lk.lock();
@@ -1341,7 +1349,10 @@ void GpuSink::ring_wait_all() {
   R.flush_locked();
   R.collect_all_locked();
   const timespec ts{0, 10000};
+  const int64_t t0 = now_ns();
   while (!R.owner_done_locked(this)) {
+    if (now_ns() - t0 > kRingWaitLimitNs)
+      throw std::runtime_error("connection ring: this read's CRC results did not arrive within 60 s");
     lk.unlock();
     nanosleep(&ts, nullptr);
     lk.lock();

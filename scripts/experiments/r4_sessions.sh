@@ -198,6 +198,11 @@ final2)  # checkpoint after span / handoff counters / stat resets: GPU suite, sm
   step bench1 600 python3 bench.py --json-out "$O/bench1.json"
   step bench2 600 python3 bench.py --json-out "$O/bench2.json"
   ;;
+lag)  # submit a filled slot one slot later (the copy engine reads L3 lines, not the receiving core's L2)
+  step pytest_lag 300 python3 -u -m pytest tests/test_gpu_sink.py -x -q --timeout 120 --timeout-method thread
+  step ab 500 python3 -u scripts/experiments/recv_cost_ab.py --tag lag --reps 5 \
+    --variants head_4x1m,head_4x1m_lag,head_6x512k_lag,nodma,base
+  ;;
 soak)  # profiles/r4_soak: execute_pb.sh with 48 workers x 100 MiB, -sink gpu, 120 s per protocol, exporter at 30 s
   step soak 900 python3 -u scripts/soak.py --out "$O" --duration 120s
   ;;

@@ -96,9 +96,6 @@ struct GpuSinkConfig {
   // runs on into the next slot when it is free (GpuSink::acquire); false:
   // every window stops at its slot's end (A/B).
   bool ring_span = true;
-  // Submit a filled slot only when the next one fills (A/B): the copy
-  // engine then reads lines the receiving core has pushed out of its L2.
-  bool submit_lag = false;
 };
 
 struct GpuSinkStats {
@@ -182,8 +179,6 @@ class GpuSink : public Sink {
   Slot& take_slot();
   void open_seg(Slot& s);
   void submit_current();
-  void retire_current();
-  void flush_lagged();
   // conn-ring mode (cfg_.conn_ring)
   Window ring_acquire();
   void ring_commit(size_t n);
@@ -200,7 +195,6 @@ class GpuSink : public Sink {
   std::vector<Slot> slots_;
   uint8_t* ring_base_ = nullptr;  // cached rings: all slots in one contiguous pinned region
   bool spill_ = false;           // the last window runs on into the next slot
-  int lagged_ = -1;              // submit_lag: a full slot not yet submitted
   int cur_ = -1;         // FILLING slot index or -1
   int next_ = 0;         // next slot to take
   const CrcTables* d_tables_ = nullptr;

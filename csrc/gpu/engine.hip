@@ -616,7 +616,6 @@ void GpuSink::grow_object_buffer(uint64_t need) {
   if (external_dst_)
     throw StorageError("object larger than the external HBM destination (" + std::to_string(obj_cap_) + " B)", false);
   set_device();
-  flush_lagged();  // its bytes must be in the old buffer before it is copied
   uint64_t landed = delivered_;
   if (cfg_.conn_ring) {
     ring_wait_all();  // every landed byte's copy done before the old buffer goes
@@ -726,7 +725,7 @@ Window GpuSink::acquire(size_t want) {
     Slot& s = slots_[cur_];
     bool segs_full = s.segs.size() >= static_cast<size_t>(kMaxSeg) && (s.segs.empty() || s.segs.back().closed);
     if (s.used == cfg_.slot_bytes || segs_full) {
-      retire_current();
+      submit_current();
       take_slot();
     }
   }
@@ -775,7 +774,7 @@ void GpuSink::commit(size_t n) {
       // the recv ran on into the next slot: this slot is full, the rest of
       // the bytes already sit at the start of the next one
       commit(room);
-      retire_current();
+      submit_current();
       take_slot();
       open_seg(slots_[cur_]);
       commit(n - room);
@@ -810,7 +809,7 @@ void GpuSink::chunk_begin(size_t len) {
     if (!s.segs.empty()) s.segs.back().closed = true;
     // keep a chunk inside one slot when it fits, so its CRC is checked in
     // the K2 epilogue on the GPU instead of being folded on the host
-    if (s.used > 0 && cfg_.slot_bytes - s.used < len && len <= cfg_.slot_bytes) retire_current();
+    if (s.used > 0 && cfg_.slot_bytes - s.used < len && len <= cfg_.slot_bytes) submit_current();
   }
   in_chunk_ = true;
   chunk_start_pending_ = true;
@@ -871,30 +870,6 @@ void GpuSink::resume_at(int64_t offset) {
   }
   in_chunk_ = false;
   chunk_start_pending_ = false;
-}
-
-// A filled slot leaves the receiving thread: submitted at once, or
-// (submit_lag) held until the next slot fills, so the copy engine reads its
-// lines once they have left the receiving core's L2 for the shared L3.
-void GpuSink::retire_current() {
-  if (cfg_.submit_lag && cfg_.slots >= 3 && cur_ >= 0 && slots_[cur_].used > 0) {
-    const int c = cur_;
-    flush_lagged();
-    lagged_ = c;
-    cur_ = -1;
-    return;
-  }
-  flush_lagged();
-  submit_current();
-}
-
-void GpuSink::flush_lagged() {
-  if (lagged_ < 0) return;
-  const int c = cur_;
-  cur_ = lagged_;
-  lagged_ = -1;
-  submit_current();
-  cur_ = c;
 }
 
 void GpuSink::submit_current() {
@@ -1071,7 +1046,6 @@ SinkResult GpuSink::finish() {
     ring_wait_all();
     ring_fold();
   } else {
-    flush_lagged();
     submit_current();
     for (int k = 0; k < cfg_.slots; ++k) wait_slot(slots_[(next_ + k) % cfg_.slots]);
   }
@@ -1109,11 +1083,6 @@ void GpuSink::abort() {
     slots_[cur_].used = 0;
     slots_[cur_].segs.clear();
     cur_ = -1;
-  }
-  if (lagged_ >= 0) {
-    slots_[lagged_].used = 0;
-    slots_[lagged_].segs.clear();
-    lagged_ = -1;
   }
   set_device();
   for (Slot& s : slots_)

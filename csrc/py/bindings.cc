@@ -93,7 +93,6 @@ GpuSinkConfig gpu_from(const py::dict& d) {
   g.wait_poll_us = get_or<int>(d, "wait_poll_us", g.wait_poll_us);
   g.ring_wc = get_or<bool>(d, "ring_wc", g.ring_wc);
   g.ring_span = get_or<bool>(d, "ring_span", g.ring_span);
-  g.submit_lag = get_or<bool>(d, "submit_lag", g.submit_lag);
   const std::string stage = get_or<std::string>(d, "gpu_stage", "h2d");
   if (stage == "none") g.stage = GpuSinkConfig::Stage::kNone;
   else if (stage == "host_read") g.stage = GpuSinkConfig::Stage::kHostRead;

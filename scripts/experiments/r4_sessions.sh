@@ -198,7 +198,8 @@ final2)  # checkpoint after span / handoff counters / stat resets: GPU suite, sm
   step bench1 600 python3 bench.py --json-out "$O/bench1.json"
   step bench2 600 python3 bench.py --json-out "$O/bench2.json"
   ;;
-lag)  # submit a filled slot one slot later (the copy engine reads L3 lines, not the receiving core's L2)
+lag)  # submit a filled slot one slot later (the copy engine reads L3 lines, not the receiving core's L2);
+  # submit_lag was removed after this session (profiles/r4_recvcost), the lag variants no longer exist
   step pytest_lag 300 python3 -u -m pytest tests/test_gpu_sink.py -x -q --timeout 120 --timeout-method thread
   step ab 500 python3 -u scripts/experiments/recv_cost_ab.py --tag lag --reps 5 \
     --variants head_4x1m,head_4x1m_lag,head_6x512k_lag,nodma,base

@@ -89,10 +89,6 @@ variants = {
     "head_spin": {"sink": "gpu"},
     "head_4x1m_spin": {"sink": "gpu", "ring_slot_bytes": 1 << 20, "ring_slots": 4},
     # windows stop at each slot's end (before: a recv ran on into the next free slot)
-    # a full slot is submitted when the next one fills (its lines out of the
-    # receiving core's L2 by then)
-    "head_4x1m_lag": {"sink": "gpu", "ring_slot_bytes": 1 << 20, "ring_slots": 4, "submit_lag": True},
-    "head_6x512k_lag": {"sink": "gpu", "ring_slot_bytes": 512 << 10, "ring_slots": 6, "submit_lag": True},
     "head_4x1m_nospan": {"sink": "gpu", "ring_slot_bytes": 1 << 20, "ring_slots": 4, "ring_span": False},
     "head_8x512k_nospan": {"sink": "gpu", "ring_slot_bytes": 512 << 10, "ring_slots": 8, "ring_span": False},
     # the multiplexed reader's destination footprint on one stream: 48 MiB /

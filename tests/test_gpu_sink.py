@@ -301,34 +301,3 @@ def test_write_combined_ring_byte_exact(native, server, gpu_available):
     sink = native.GpuSink({"device": 0, "ring_slot_bytes": 1 << 20, "ring_slots": 2, "ring_wc": True})
     r = c.read_gpu(B, P + "0", sink)
     assert r["crc_mismatch"] and not r["verified"]
-
-
-@pytest.mark.parametrize("slot,slots", [(1 << 20, 4), (512 << 10, 6), (256 << 10, 3)])
-def test_submit_lag_byte_exact(native, server, gpu_available, slot, slots):
-    """submit_lag: a filled slot is submitted only when the next one fills
-    (and at the read's end, on a grow, on abort).  Same bytes and checks as
-    immediate submission, over reads that reuse the sink and an object that
-    grows the landing buffer; corruption is still caught."""
-    import torch
-
-    size = (7 << 20) + 4099
-    server.add_synthetic(B, P, "", 0, 1, size)
-    cfg = {"device": 0, "ring_slot_bytes": slot, "ring_slots": slots, "submit_lag": True}
-    for proto in _protocols(native):
-        c = native.Client({"protocol": proto, "endpoint": server.url})
-        sink = native.GpuSink(cfg)
-        for _ in range(3):
-            r = c.read_gpu(B, P + "0", sink)
-            assert r["verified"] and not r["crc_mismatch"] and r["bytes"] == size, r
-            bad, first = native.gpu_verify_pattern(0, sink.device_ptr, size, P + "0", 0)
-            assert bad == 0, (proto, first)
-        t = torch.empty(size, dtype=torch.uint8, device="cuda:0")
-        sink.set_external_destination(t.data_ptr(), t.numel())
-        r = c.read_gpu(B, P + "0", sink)
-        assert r["verified"], r
-        bad, first = native.gpu_verify_pattern(0, t.data_ptr(), size, P + "0", 0)
-        assert bad == 0, (proto, first)
-    server.set_faults({"corrupt_at": (3 << 20) + 5, "corrupt_count": 1})
-    c = native.Client({"protocol": "grpc", "endpoint": server.url})
-    r = c.read_gpu(B, P + "0", native.GpuSink(cfg))
-    assert r["crc_mismatch"] and not r["verified"]

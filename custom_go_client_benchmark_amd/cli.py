@@ -56,6 +56,9 @@ def build_flags() -> FlagSet:
     fs.int("write-warmup", 1, "write: untimed warm-up uploads first (connections, pinned staging rings)")
     fs.string("http-api", "xml", "HTTP media API: xml (library default) | json (alt=media)")
     fs.int("read-chunk", 2 << 20, "Bytes per receive into the sink (reference intent: 2 MiB buffer)")
+    fs.bool("conn-ring", True, "-sink gpu on one multiplexed connection (gRPC pool 1, http2): every worker's stream "
+            "lands through one 4 x 1 MiB receive ring of the connection instead of a ring per worker "
+            "(profiles/r4_ringgeom)")
     fs.int("grpc-conn-pool-size", 1, "gRPC connections (reference GrpcConnPoolSize = 1)")
     fs.bool("grpc-directpath", True, "Request DirectPath while creating the gRPC client (reference sets "
             "GOOGLE_CLOUD_ENABLE_DIRECT_PATH_XDS=true around NewGRPCClient; falls back to CloudPath)")
@@ -258,7 +261,7 @@ def main(argv: list[str] | None = None) -> int:
         read_timeout_s=fs.get("read-timeout"),
         # a node-local synthetic endpoint is a loopback link: cubic unless set
         tcp_congestion=fs.get("tcp-congestion") or ("cubic" if fs.get("start-fake-server") else ""),
-        loopback_rto_min=bool(fs.get("start-fake-server")))
+        loopback_rto_min=bool(fs.get("start-fake-server")), conn_ring=bool(fs.get("conn-ring")))
 
     # tracing (reference main.go:162-165)
     tracer, trace_cleanup = None, None

@@ -56,6 +56,7 @@ class RunOptions:
     read_timeout_s: float = 0.0            # idle limit per read (0 = none, as the reference's Timeout: 0)
     tcp_congestion: str = ""               # client sockets' congestion control ("" = host default)
     loopback_rto_min: bool = False         # node-local endpoint: loopback-sized minimum RTO
+    conn_ring: bool = True                 # GPU sink on one multiplexed connection: one shared receive ring
     object_names: list | None = None
     keep_records: bool = True
     slices: int = 1                        # >1: sliced (parallel ranged) reads, see csrc/storage/sliced.h
@@ -89,7 +90,7 @@ class RunOptions:
             "trace_sample_rate": self.trace_sample_rate, "stop_on_error": self.stop_on_error,
             "keep_records": self.keep_records, "slices": self.slices, "slice_min_bytes": self.slice_min_bytes,
             "slice_piece_bytes": self.slice_piece_bytes,
-            "slice_piece_min_bytes": self.slice_piece_min_bytes,
+            "slice_piece_min_bytes": self.slice_piece_min_bytes, "conn_ring": self.conn_ring,
         })
         if self.object_names:
             d["object_names"] = list(self.object_names)

@@ -303,7 +303,7 @@ def build_parser() -> argparse.ArgumentParser:
                     help="ref_default_* side blocks: the reference's default experiment, -worker 48 on 1 MiB "
                          "objects, gRPC pool 1 vs HTTP keep-alive, discard sink + host CRC (0 = off)")
     ap.add_argument("--ref-reads", type=int, default=50, help="ref_default_*: timed reads per worker")
-    ap.add_argument("--ref-grpc-placement", default="same", choices=["share_quota", "same", "share"],
+    ap.add_argument("--ref-grpc-placement", default="same", choices=["share_quota", "same", "share", "pair"],
                     help="ref_default_grpc: CPU placement of the 48 workers, the endpoint and the one connection's "
                          "reader. One L3 domain (same): 16.0-19.5k MiB/s at p50 2.1-2.4 ms against 8.4-8.8k at "
                          "4.5-5.0 ms spread over the quota's cores (profiles/r3_mux_thp/refplace). HTTP keeps "

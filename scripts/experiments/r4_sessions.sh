@@ -204,6 +204,15 @@ lag)  # submit a filled slot one slot later (the copy engine reads L3 lines, not
   step ab 500 python3 -u scripts/experiments/recv_cost_ab.py --tag lag --reps 5 \
     --variants head_4x1m,head_4x1m_lag,head_6x512k_lag,nodma,base
   ;;
+refpair)  # 48 x 100 MiB gRPC: the one connection's reader + the endpoint on a core pair each (GPU sink: the
+  # workers only wait) against one L3 domain
+  for k in 1 2; do
+    for m in same pair; do
+      step "rp_${m}_$k" 300 python3 bench.py --steps 5 --warmup 1 --blocks ref_default_100m,ref_default \
+        --ref-grpc-placement $m --json-out "$O/rp_${m}_$k.json"
+    done
+  done
+  ;;
 soak)  # profiles/r4_soak: execute_pb.sh with 48 workers x 100 MiB, -sink gpu, 120 s per protocol, exporter at 30 s
   step soak 900 python3 -u scripts/soak.py --out "$O" --duration 120s
   ;;

@@ -213,6 +213,18 @@ refpair)  # 48 x 100 MiB gRPC: the one connection's reader + the endpoint on a c
     done
   done
   ;;
+final3)  # last checkpoint of the round: GPU suite, smoke, two benches, the 8-rank rehearsal
+  step pytest_gpu 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+  step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+  step bench1 600 python3 bench.py --json-out "$O/bench1.json"
+  step bench2 600 python3 bench.py --json-out "$O/bench2.json"
+  t0=$(date +%s.%N)
+  export GCSB_DIST_BACKEND=gloo
+  step rehearsal8 400 python3 bench.py --gpus 8 --object-size 64MiB --steps 5 --side-steps 3 \
+    --json-out "$O/rehearsal8.json"
+  unset GCSB_DIST_BACKEND
+  python3 -c "print('rehearsal8 wall_s', round($(date +%s.%N)-$t0, 1))" > "$O/rehearsal8_wall.txt"
+  ;;
 soak)  # profiles/r4_soak: execute_pb.sh with 48 workers x 100 MiB, -sink gpu, 120 s per protocol, exporter at 30 s
   step soak 900 python3 -u scripts/soak.py --out "$O" --duration 120s
   ;;

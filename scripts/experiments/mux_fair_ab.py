@@ -27,18 +27,24 @@ ap.add_argument("--leads", default="0",
                 help="KiB: a new read's first DATA frame ahead of the queue (h2_lead_bytes, removed after "
                      "profiles/r4_main7: only 0 runs on today's endpoint)")
 ap.add_argument("--protocol", default="grpc")
+ap.add_argument("--bufs", default="0:0",
+                help="comma list of SNDBUF_KIB:RCVBUF_KIB (endpoint send buffer, client receive buffer; 0 = "
+                     "autotuned): the bytes in flight ahead of a new stream's first byte")
 args = ap.parse_args()
 n = pkg._native
 pl = affinity.plan(0, "same", 0) if torch.cuda.is_available() else {"client": [], "server": []}
 for rep in range(args.reps):
-    for q, lead in [(int(x), int(y)) for x in args.quanta.split(",") for y in args.leads.split(",")]:
+    for q, lead, bufs in [(int(x), int(y), z) for x in args.quanta.split(",") for y in args.leads.split(",")
+                          for z in args.bufs.split(",")]:
+        sndk, rcvk = (int(v) for v in bufs.split(":"))
         srv = n.Server({"port": 0, "md5": False, "retain_uploads": False, "h2_quantum": q << 10,
-                        "h2_lead_bytes": lead << 10, "cpus": pl["server"]})
+                        "h2_lead_bytes": lead << 10, "cpus": pl["server"], "sndbuf": sndk << 10})
         srv.start()
         srv.add_synthetic("b", "f_", "", 0, args.workers, args.size)
         r = n.Runner({"protocol": args.protocol, "endpoint": srv.url, "bucket": "b", "object_prefix": "f_",
                       "workers": args.workers, "reads_per_worker": 2, "sink": "discard", "host_crc": True,
-                      "keep_records": False, "grpc_conn_pool_size": 1, "cpus": pl["client"]})
+                      "keep_records": False, "grpc_conn_pool_size": 1, "cpus": pl["client"],
+                      "rcvbuf": rcvk << 10})
         r.start()
         r.wait()
         r.reset_stats()
@@ -52,7 +58,7 @@ for rep in range(args.reps):
         s1 = srv.stats()
         fr = max(1, s1["h2_data_frames"] - s0["h2_data_frames"])
         rs = max(1, s1["h2_responses"] - s0["h2_responses"])
-        print(json.dumps({"rep": rep, "quantum_kib": q, "lead_kib": lead, "mib_s": round(s["bytes"] / el / 2**20, 1),
+        print(json.dumps({"rep": rep, "quantum_kib": q, "lead_kib": lead, "bufs_kib": bufs, "mib_s": round(s["bytes"] / el / 2**20, 1),
                           "p50_ms": round(s["p50_ms"], 3), "p99_ms": round(s["p99_ms"], 3),
                           "ttfb_p50_ms": round(s["ttfb_p50_ms"], 3), "ttfb_p99_ms": round(s["ttfb_p99_ms"], 3),
                           "errors": s["errors"],

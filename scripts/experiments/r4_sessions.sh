@@ -225,6 +225,11 @@ final3)  # last checkpoint of the round: GPU suite, smoke, two benches, the 8-ra
   unset GCSB_DIST_BACKEND
   python3 -c "print('rehearsal8 wall_s', round($(date +%s.%N)-$t0, 1))" > "$O/rehearsal8_wall.txt"
   ;;
+evidence)  # final-code evidence: 100-read stall attribution (off-core sampler), kernel + copy trace of the headline
+  step diag100 400 python3 bench.py --steps 100 --warmup 3 --side-steps 0 --read-diag --json-out "$O/diag100.json"
+  step prof 600 rocprofv3 --kernel-trace --memory-copy-trace --stats -f csv -d "$O/prof" -o run -- python3 bench.py \
+    --steps 20 --warmup 3 --blocks ceiling --json-out "$O/bench_prof.json"
+  ;;
 soak)  # profiles/r4_soak: execute_pb.sh with 48 workers x 100 MiB, -sink gpu, 120 s per protocol, exporter at 30 s
   step soak 900 python3 -u scripts/soak.py --out "$O" --duration 120s
   ;;

@@ -678,7 +678,7 @@ def run_rank(args) -> int:
                  "cause": sysdiag.attribute(dg, x[1], s1["p50_ms"]),
                  "threads": {k: {f: (round(v, 3) if isinstance(v, float) else v) for f, v in row.items()}
                              for k, row in dg["threads"].items()},
-                 "softirqs": dg["softirqs"], "tcp": dg.get("tcp", {})}
+                 "softirqs": dg["softirqs"], "tcp": dg.get("tcp", {}), "softnet": dg.get("softnet", {})}
                 for x, dg in zip(s1["slowest"], s1["slowest_diag"])]
         st["slow_hip"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in slow_hip.items()}
         return st

@@ -126,6 +126,36 @@ void read_proto_table(const char* path, const char* prefix, const std::vector<co
   std::fclose(f);
 }
 
+// /proc/net/softnet_stat rows (hex): processed, dropped, time_squeeze, ...,
+// the CPU id in column 12 on current kernels (the row index otherwise).
+std::map<int, std::pair<uint64_t, uint64_t>> read_softnet(const std::set<int>& cpus) {
+  std::map<int, std::pair<uint64_t, uint64_t>> out;
+  if (cpus.empty()) return out;
+  FILE* f = std::fopen("/proc/net/softnet_stat", "r");
+  if (!f) return out;
+  char* line = nullptr;
+  size_t cap = 0;
+  int row = 0;
+  while (getline(&line, &cap, f) > 0) {
+    unsigned long long v[13] = {0};
+    int n = 0;
+    char* p = line;
+    while (n < 13) {
+      char* end = nullptr;
+      const unsigned long long x = std::strtoull(p, &end, 16);
+      if (end == p) break;
+      v[n++] = x;
+      p = end;
+    }
+    const int cpu = n > 12 ? static_cast<int>(v[12]) : row;
+    if (n >= 3 && cpus.count(cpu)) out[cpu] = {v[1], v[2]};
+    ++row;
+  }
+  std::free(line);
+  std::fclose(f);
+  return out;
+}
+
 int64_t mono_ns() {
   timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
@@ -169,6 +199,7 @@ SchedSample sched_sample(const std::vector<std::string>& prefixes) {
     for (int tid : dead) registry().erase(tid);
   }
   s.softirqs = read_softirqs(cpus);
+  s.softnet = read_softnet(cpus);
   read_proto_table("/proc/net/snmp", "Tcp:", {"RetransSegs"}, &s.tcp);
   read_proto_table("/proc/net/netstat", "TcpExt:",
                    {"TCPLossProbes", "TCPTimeouts", "PruneCalled", "RcvPruned", "TCPRcvQDrop", "TCPBacklogDrop"}, &s.tcp);
@@ -269,6 +300,12 @@ ReadSchedDiag sched_delta(const SchedSample& a, const SchedSample& b) {
       auto k = ia->second.find(kind);
       if (k != ia->second.end() && v > k->second) d.softirqs[kind] += v - k->second;
     }
+  }
+  for (const auto& [c, v] : b.softnet) {
+    auto it = a.softnet.find(c);
+    if (it == a.softnet.end()) continue;
+    if (v.first > it->second.first) d.softnet_dropped += v.first - it->second.first;
+    if (v.second > it->second.second) d.softnet_squeeze += v.second - it->second.second;
   }
   for (const auto& [k, v] : b.tcp) {
     auto it = a.tcp.find(k);

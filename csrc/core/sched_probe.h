@@ -41,6 +41,8 @@ struct SchedSample {
   // reader and endpoint share the namespace, so a retransmit by either side
   // shows here (per-socket TCP_INFO would only see the client's own).
   std::map<std::string, uint64_t> tcp;
+  // /proc/net/softnet_stat of the CPUs of interest: {cpu: {dropped, time_squeeze}}
+  std::map<int, std::pair<uint64_t, uint64_t>> softnet;
 };
 
 // Threads whose name starts with one of `prefixes`; softirqs of the CPUs
@@ -65,6 +67,7 @@ struct ReadSchedDiag {
   std::map<std::string, Row> threads;                      // by thread name
   std::map<std::string, uint64_t> softirqs;                // on those CPUs, by kind
   std::map<std::string, uint64_t> tcp;                     // namespace TCP counters over the read
+  uint64_t softnet_dropped = 0, softnet_squeeze = 0;       // input-backlog drops / NET_RX budget runs on those CPUs
   double wall_ms = 0;
 };
 ReadSchedDiag sched_delta(const SchedSample& a, const SchedSample& b);

@@ -152,6 +152,10 @@ py::dict sched_diag_dict(const ReadSchedDiag& x) {
   py::dict tcp;
   for (const auto& [k, v] : x.tcp) tcp[py::str(k)] = v;
   d["tcp"] = tcp;
+  py::dict sn;
+  sn["dropped"] = x.softnet_dropped;
+  sn["time_squeeze"] = x.softnet_squeeze;
+  d["softnet"] = sn;
   d["wall_ms"] = x.wall_ms;
   return d;
 }

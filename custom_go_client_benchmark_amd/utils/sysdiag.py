@@ -179,6 +179,28 @@ def tcp_snapshot() -> dict[str, int]:
     return out
 
 
+def softnet_snapshot() -> dict[int, tuple[int, int]]:
+    """{cpu: (dropped, time_squeeze)} from /proc/net/softnet_stat: packets
+    the CPU's input backlog dropped (loopback traffic is queued there by the
+    sender), and NET_RX rounds that ran out of budget."""
+    out: dict[int, tuple[int, int]] = {}
+    text = _read("/proc/net/softnet_stat") or ""
+    for i, line in enumerate(text.splitlines()):
+        f = line.split()
+        if len(f) < 3:
+            continue
+        cpu = int(f[12], 16) if len(f) > 12 else i
+        out[cpu] = (int(f[1], 16), int(f[2], 16))
+    return out
+
+
+def softnet_delta(a: dict, b: dict, cpus: list[int] | None) -> dict[str, int]:
+    want = set(cpus) if cpus else set(b)
+    drop = sum(b[c][0] - a.get(c, (0, 0))[0] for c in b if c in want)
+    sq = sum(b[c][1] - a.get(c, (0, 0))[1] for c in b if c in want)
+    return {"dropped": drop, "time_squeeze": sq}
+
+
 def tcp_delta(a: dict[str, int], b: dict[str, int]) -> dict[str, int]:
     """Non-zero counter increases between two tcp_snapshot()s."""
     return {k: b[k] - a.get(k, 0) for k in b if b[k] - a.get(k, 0) > 0}
@@ -211,6 +233,10 @@ def attribute(diag: dict, ms: float, p50_ms: float) -> str:
     dropped = tcp.get("RcvPruned", 0) + tcp.get("TCPRcvQDrop", 0) + tcp.get("TCPBacklogDrop", 0)
     if dropped:
         causes.append(f"{dropped} receive-queue prunes / drops (skb memory over the receive buffer)")
+    sn = diag.get("softnet", {})
+    if sn.get("dropped", 0):
+        causes.append(f"{sn['dropped']} packets dropped at a CPU's input backlog (softnet; loopback packets "
+                      f"wait there for NET_RX)")
     soft = diag.get("softirqs", {})
     if soft.get("HRTIMER", 0) >= 100:
         causes.append(f"{soft['HRTIMER']} HRTIMER softirqs on the busy CPUs (pacing timers)")
@@ -234,10 +260,12 @@ class Window:
         self.irq = irq_snapshot()
         self.soft = softirq_snapshot()
         self.tcp = tcp_snapshot()
+        self.softnet = softnet_snapshot()
 
     def report(self, cpus: list[int] | None, reads: int) -> dict:
         return {"threads": sched_delta(self.sched, thread_sched(), reads),
                 "irq_on_placement": table_delta(self.irq, irq_snapshot(), cpus, reads),
                 "softirq_on_placement": table_delta(self.soft, softirq_snapshot(), cpus, reads),
                 # whole block, not per read: any RTO / drop names a stalled read
-                "tcp": tcp_delta(self.tcp, tcp_snapshot())}
+                "tcp": tcp_delta(self.tcp, tcp_snapshot()),
+                "softnet_on_placement": softnet_delta(self.softnet, softnet_snapshot(), cpus)}

@@ -230,6 +230,10 @@ evidence)  # final-code evidence: 100-read stall attribution (off-core sampler),
   step prof 600 rocprofv3 --kernel-trace --memory-copy-trace --stats -f csv -d "$O/prof" -o run -- python3 bench.py \
     --steps 20 --warmup 3 --blocks ceiling --json-out "$O/bench_prof.json"
   ;;
+softnet)  # do the loopback retransmits follow input-backlog drops? two 100-read diag runs
+  step diag100a 400 python3 bench.py --steps 100 --warmup 3 --side-steps 0 --read-diag --json-out "$O/diag100a.json"
+  step diag100b 400 python3 bench.py --steps 100 --warmup 3 --side-steps 0 --read-diag --json-out "$O/diag100b.json"
+  ;;
 soak)  # profiles/r4_soak: execute_pb.sh with 48 workers x 100 MiB, -sink gpu, 120 s per protocol, exporter at 30 s
   step soak 900 python3 -u scripts/soak.py --out "$O" --duration 120s
   ;;

@@ -124,6 +124,7 @@ def test_runner_read_diag_names_threads(native):
     assert d["wall_ms"] >= s["slowest"][0][1] * 0.5
     # namespace TCP counters over the read (loopback: normally no retransmits)
     assert set(d["tcp"]) >= {"RetransSegs", "TCPTimeouts"} and all(v >= 0 for v in d["tcp"].values())
+    assert set(d["softnet"]) == {"dropped", "time_squeeze"}
     from custom_go_client_benchmark_amd.utils import sysdiag
 
     cause = sysdiag.attribute(d, s["slowest"][0][1], s["p50_ms"])
@@ -220,6 +221,11 @@ def test_sysdiag_tcp_counters():
     d = {"threads": {"gcsb-worker": {"cpu_ms": 16.0, "run_delay_ms": 0.0}}, "softirqs": {},
          "tcp": {"RcvPruned": 2, "TCPRcvQDrop": 1}, "wall_ms": 226.0}
     assert "3 receive-queue prunes / drops" in sysdiag.attribute(d, 226.0, 16.0)
+    d["softnet"] = {"dropped": 40, "time_squeeze": 2}
+    assert "40 packets dropped at a CPU's input backlog" in sysdiag.attribute(d, 226.0, 16.0)
+    sn = sysdiag.softnet_snapshot()
+    assert sn and all(len(v) == 2 for v in sn.values())
+    assert set(sysdiag.Window().report(None, 1)["softnet_on_placement"]) == {"dropped", "time_squeeze"}
 
 
 def test_endpoint_sockets_get_loopback_rto_min(native, server):

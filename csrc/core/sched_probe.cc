@@ -202,7 +202,10 @@ SchedSample sched_sample(const std::vector<std::string>& prefixes) {
   s.softnet = read_softnet(cpus);
   read_proto_table("/proc/net/snmp", "Tcp:", {"RetransSegs"}, &s.tcp);
   read_proto_table("/proc/net/netstat", "TcpExt:",
-                   {"TCPLossProbes", "TCPTimeouts", "PruneCalled", "RcvPruned", "TCPRcvQDrop", "TCPBacklogDrop"}, &s.tcp);
+                   {"TCPLossProbes", "TCPTimeouts", "PruneCalled", "RcvPruned", "TCPRcvQDrop", "TCPBacklogDrop",
+                    "TCPFastRetrans", "TCPSlowStartRetrans", "TCPSpuriousRtxHostQueues", "TCPSACKReorder",
+                    "TCPDSACKRecv"},
+                   &s.tcp);
   return s;
 }
 

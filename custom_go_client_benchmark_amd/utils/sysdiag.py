@@ -158,7 +158,11 @@ def table_delta(a: tuple, b: tuple, cpus: list[int] | None, reads: int = 1, top:
 # outgrows the socket's receive buffer
 TCP_COUNTERS = {"Tcp": ("RetransSegs",),
                 "TcpExt": ("TCPTimeouts", "TCPLossProbes", "PruneCalled", "RcvPruned", "TCPRcvQDrop",
-                           "TCPRcvCollapsed", "TCPBacklogDrop", "TCPZeroWindowDrop", "TCPOFODrop")}
+                           "TCPRcvCollapsed", "TCPBacklogDrop", "TCPZeroWindowDrop", "TCPOFODrop",
+                           # which retransmits, and why
+                           "TCPFastRetrans", "TCPSlowStartRetrans", "TCPLostRetransmit", "TCPRetransFail",
+                           "TCPSpuriousRtxHostQueues", "TCPSACKReorder", "TCPTSReorder", "TCPRenoReorder",
+                           "TCPDSACKRecv", "TCPDSACKOldSent", "TCPSpuriousRTOs", "TCPWinProbe")}
 
 
 def tcp_snapshot() -> dict[str, int]:

@@ -234,6 +234,10 @@ softnet)  # do the loopback retransmits follow input-backlog drops? two 100-read
   step diag100a 400 python3 bench.py --steps 100 --warmup 3 --side-steps 0 --read-diag --json-out "$O/diag100a.json"
   step diag100b 400 python3 bench.py --steps 100 --warmup 3 --side-steps 0 --read-diag --json-out "$O/diag100b.json"
   ;;
+twocore)  # the headline's receiving thread on the baseline's two cores vs its own core pair
+  step ab 500 python3 -u scripts/experiments/recv_cost_ab.py --tag twocore --reps 6 \
+    --variants head_4x1m,head_4x1m_2core,nodma,base
+  ;;
 soak)  # profiles/r4_soak: execute_pb.sh with 48 workers x 100 MiB, -sink gpu, 120 s per protocol, exporter at 30 s
   step soak 900 python3 -u scripts/soak.py --out "$O" --duration 120s
   ;;

@@ -89,6 +89,9 @@ variants = {
     "head_spin": {"sink": "gpu"},
     "head_4x1m_spin": {"sink": "gpu", "ring_slot_bytes": 1 << 20, "ring_slots": 4},
     # windows stop at each slot's end (before: a recv ran on into the next free slot)
+    # the headline's receiving thread free to run on both of the baseline's
+    # cores (the submitter stays pinned to the aux core)
+    "head_4x1m_2core": {"sink": "gpu", "ring_slot_bytes": 1 << 20, "ring_slots": 4, "cpus": "TWO_CORE"},
     "head_4x1m_nospan": {"sink": "gpu", "ring_slot_bytes": 1 << 20, "ring_slots": 4, "ring_span": False},
     "head_8x512k_nospan": {"sink": "gpu", "ring_slot_bytes": 512 << 10, "ring_slots": 8, "ring_span": False},
     # the multiplexed reader's destination footprint on one stream: 48 MiB /
@@ -99,6 +102,9 @@ variants = {
 }
 SPIN_US = {"head_spin": 200, "head_4x1m_spin": 200}
 names = [v for v in args.variants.split(",") if v]
+for v in variants.values():
+    if v.get("cpus") == "TWO_CORE":
+        v["cpus"] = two_core
 runners = {k: n.Runner({**base, **variants[k]}) for k in names}
 for r in runners.values():  # warm: connections, rings, sinks
     r.start()

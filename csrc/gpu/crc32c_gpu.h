@@ -57,6 +57,9 @@ struct CrcLaunchOptions {
   bool xor_arrival = true;
   bool nibble_tables = false;
   bool mfma = false;
+  // slot kernel: stage slice-by-8 tables (8 KiB, T0..T7) instead of
+  // slice-by-16 (16 KiB) -- the L2-cold stage in the read pipeline (A/B)
+  bool slice8 = false;
 };
 void set_crc_launch_options(const CrcLaunchOptions& o);
 CrcLaunchOptions crc_launch_options();

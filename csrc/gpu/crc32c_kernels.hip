@@ -70,6 +70,20 @@ __device__ __forceinline__ uint32_t update16(const uint32_t* __restrict__ sl, ui
   return c;
 }
 
+// The same 16 bytes as two slice-by-8 steps (tables T0..T7 only: half the
+// LDS staging per workgroup, twice the dependent steps per lane).
+__device__ __forceinline__ uint32_t update16_s8(const uint32_t* __restrict__ sl, uint32_t state, uint4 v) {
+  const uint32_t x = state ^ v.x;
+  uint32_t c = sl[7 * 256 + (x & 0xff)] ^ sl[6 * 256 + ((x >> 8) & 0xff)] ^ sl[5 * 256 + ((x >> 16) & 0xff)] ^
+               sl[4 * 256 + (x >> 24)] ^ sl[3 * 256 + (v.y & 0xff)] ^ sl[2 * 256 + ((v.y >> 8) & 0xff)] ^
+               sl[1 * 256 + ((v.y >> 16) & 0xff)] ^ sl[0 * 256 + (v.y >> 24)];
+  const uint32_t z = c ^ v.z;
+  c = sl[7 * 256 + (z & 0xff)] ^ sl[6 * 256 + ((z >> 8) & 0xff)] ^ sl[5 * 256 + ((z >> 16) & 0xff)] ^
+      sl[4 * 256 + (z >> 24)] ^ sl[3 * 256 + (v.w & 0xff)] ^ sl[2 * 256 + ((v.w >> 8) & 0xff)] ^
+      sl[1 * 256 + ((v.w >> 16) & 0xff)] ^ sl[0 * 256 + (v.w >> 24)];
+  return c;
+}
+
 // The same 16-byte update from the bank-replicated nibble tables (CrcTables::nib):
 // nb = nib + (lane & 31); table t of nibble n at nb[t * 512 + n * 32].
 __device__ __forceinline__ uint32_t update16_nib(const uint32_t* __restrict__ nb, uint32_t state, uint4 v) {
@@ -125,7 +139,7 @@ __device__ __forceinline__ void load_tile(const CrcBatch& b, uint32_t s, uint32_
 }
 
 // The lane's CRC register over its chunks of the tile.
-template <int R, bool kNib = false>
+template <int R, bool kNib = false, bool kS8 = false>
 __device__ __forceinline__ uint32_t lane_chain(const uint4 (&v)[R * kCrcChunkPieces], const uint32_t* sl,
                                                const uint32_t* lane_shift, int lane) {
   uint32_t state = 0;
@@ -136,6 +150,8 @@ __device__ __forceinline__ uint32_t lane_chain(const uint4 (&v)[R * kCrcChunkPie
     for (int j = 0; j < kCrcChunkPieces; ++j) {
       if constexpr (kNib)
         state = update16_nib(sl + (lane & 31), state, v[k * kCrcChunkPieces + j]);
+      else if constexpr (kS8)
+        state = update16_s8(sl, state, v[k * kCrcChunkPieces + j]);
       else
         state = update16(sl, state, v[k * kCrcChunkPieces + j]);
     }
@@ -374,11 +390,13 @@ __device__ __forceinline__ uint32_t xor_over_lanes(uint32_t x, int width) {
 // lane, a 6-level lookup chain), 1.0 us on the done counter, 2.5 us in the
 // last workgroup's Horner + tree fold.  W (waves per workgroup) is picked so
 // the grid puts a tile on every CU.
-template <int W, bool kNib>
+template <int W, bool kNib, bool kS8 = false>
 __global__ __launch_bounds__(64 * W) void crc32c_slot_kernel(const CrcBatch b, const CrcTables* __restrict__ tabs,
                                                             uint32_t* __restrict__ scratch,
                                                             CrcSegResult* __restrict__ out) {
-  constexpr int kTabWords = kNib ? 32 * 16 * 32 : kSliceWords;
+  constexpr int kTabWords = kNib ? 32 * 16 * 32 : kS8 ? 8 * 256 : kSliceWords;
+  // the tail fold looks up T0..T15: from L2 when only T0..T7 were staged
+  const uint32_t* tail_tab = kS8 ? &tabs->slice16[0][0] : nullptr;
   __shared__ __attribute__((aligned(16))) uint32_t s_sl[kTabWords];
   __shared__ uint32_t s_last;
   const uint32_t probe = b.probe & 0xffu;  // bit 8: A/B switch, per-tile stores + counters only
@@ -435,7 +453,7 @@ __global__ __launch_bounds__(64 * W) void crc32c_slot_kernel(const CrcBatch b, c
       load_tile<1>(b, s, gt, lane, v);
       __builtin_amdgcn_sched_barrier(0);
     }
-    const uint32_t state = lane_chain<1, kNib>(v, s_sl, nullptr, lane);
+    const uint32_t state = lane_chain<1, kNib, kS8>(v, s_sl, nullptr, lane);
     uint32_t c = 0;
 #pragma unroll
     for (int i = 0; i < 32; ++i) c ^= kl[i] & (0u - ((state >> i) & 1u));
@@ -486,7 +504,7 @@ __global__ __launch_bounds__(64 * W) void crc32c_slot_kernel(const CrcBatch b, c
     }
     __syncthreads();
     if (!s_last || probe == 3 || wave != 0) return;
-    const uint32_t raw = fold_tail<kNib>(tail_b, tail_r, s_raw, s_sl, lane);
+    const uint32_t raw = fold_tail<kNib>(tail_b, tail_r, s_raw, kS8 ? tail_tab : s_sl, lane);
     if (lane == 0) store_result(out + 0, seg_result(b.seg[0], raw));
     return;
   }
@@ -530,7 +548,7 @@ __global__ __launch_bounds__(64 * W) void crc32c_slot_kernel(const CrcBatch b, c
 #pragma unroll
     for (int k = 0; k < static_cast<int>(kCrcFusedMaxTiles / 64); ++k) acc ^= v[k];
     uint32_t raw = xor_over_lanes(acc, 64);
-    raw = fold_tail<kNib>(tb, r, raw, s_sl, lane);
+    raw = fold_tail<kNib>(tb, r, raw, kS8 ? tail_tab : s_sl, lane);
     if (lane == 0) store_result(out + g, seg_result(sg, raw));
   }
 }
@@ -839,7 +857,17 @@ void launch_crc32c_batch(const CrcBatch& b, const CrcTables* d_tables, uint32_t*
 #define GCSB_SLOT(WV, NB) \
   hipLaunchKernelGGL((crc32c_slot_kernel<WV, NB>), dim3(g), dim3(64 * WV), 0, stream, no_xor ? bx : b, d_tables, \
                      d_scratch, d_results)
-    if (nib) {
+#define GCSB_SLOT8(WV) \
+  hipLaunchKernelGGL((crc32c_slot_kernel<WV, false, true>), dim3(g), dim3(64 * WV), 0, stream, no_xor ? bx : b, \
+                     d_tables, d_scratch, d_results)
+    if (!nib && o.slice8) {
+      switch (w) {
+        case 1: GCSB_SLOT8(1); break;
+        case 2: GCSB_SLOT8(2); break;
+        case 4: GCSB_SLOT8(4); break;
+        default: GCSB_SLOT8(8); break;
+      }
+    } else if (nib) {
       switch (w) {
         case 1: GCSB_SLOT(1, true); break;
         case 2: GCSB_SLOT(2, true); break;
@@ -855,6 +883,7 @@ void launch_crc32c_batch(const CrcBatch& b, const CrcTables* d_tables, uint32_t*
       }
     }
 #undef GCSB_SLOT
+#undef GCSB_SLOT8
     hip_check(hipGetLastError(), "crc32c_slot_kernel");
     return;
   }

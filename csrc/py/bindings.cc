@@ -1016,12 +1016,14 @@ PYBIND11_MODULE(_native, m) {
     o.xor_arrival = get_or<bool>(d, "xor_arrival", o.xor_arrival);
     o.nibble_tables = get_or<bool>(d, "nibble_tables", o.nibble_tables);
     o.mfma = get_or<bool>(d, "mfma", o.mfma);
+    o.slice8 = get_or<bool>(d, "slice8", o.slice8);
     set_crc_launch_options(o);
     py::dict r;
     r["slot_kernel"] = o.slot_kernel;
     r["slot_waves"] = o.slot_waves;
     r["xor_arrival"] = o.xor_arrival;
     r["nibble_tables"] = o.nibble_tables;
+    r["slice8"] = o.slice8;
     r["mfma"] = o.mfma;
     return r;
   }, py::arg("options") = py::dict());

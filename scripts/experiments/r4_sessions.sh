@@ -238,6 +238,15 @@ twocore)  # the headline's receiving thread on the baseline's two cores vs its o
   step ab 500 python3 -u scripts/experiments/recv_cost_ab.py --tag twocore --reps 6 \
     --variants head_4x1m,head_4x1m_2core,nodma,base
   ;;
+crc8)  # slot CRC kernel: slice-by-8 tables (half the L2-cold LDS stage) vs slice-by-16, in the read pipeline
+  step pytest_crc 300 python3 -u -m pytest tests/test_gpu_crc32c.py -x -q --timeout 120 --timeout-method thread
+  for k in 1 2; do
+    for c in off on; do
+      step "prof_s8${c}_$k" 300 rocprofv3 --kernel-trace --stats -f csv -d "$O/prof_s8${c}_$k" -o run -- python3 \
+        bench.py --steps 20 --warmup 3 --blocks ceiling --crc-slice8 $c --json-out "$O/bench_s8${c}_$k.json"
+    done
+  done
+  ;;
 soak)  # profiles/r4_soak: execute_pb.sh with 48 workers x 100 MiB, -sink gpu, 120 s per protocol, exporter at 30 s
   step soak 900 python3 -u scripts/soak.py --out "$O" --duration 120s
   ;;

@@ -230,8 +230,9 @@ def build_parser() -> argparse.ArgumentParser:
                     help="GPU sink on one multiplexed gRPC connection (list_read_grpc, ref_default_100m_grpc_gpu): "
                          "every worker's stream through one connection ring of SLOTSxBYTES instead of a ring per "
                          "worker (profiles/r4_bigring, r4_connring); off: a ring per worker")
-    ap.add_argument("--crc-slice8", default="off", choices=["on", "off"],
-                    help="slot CRC kernel stages slice-by-8 tables (8 KiB) instead of slice-by-16 (A/B)")
+    ap.add_argument("--crc-slice8", default="on", choices=["on", "off"],
+                    help="slot CRC kernel stages slice-by-8 tables (8 KiB) instead of slice-by-16 "
+                         "(profiles/r4_crc8)")
     ap.add_argument("--crc-slot-waves", type=int, default=0, choices=[0, 1, 2, 4, 8],
                     help="slot CRC kernel waves per workgroup (0: by slot size); A/B of the kernel's table staging")
     ap.add_argument("--async-submit", type=int, default=1, choices=[0, 1],
@@ -469,7 +470,7 @@ def run_rank(args) -> int:
     placement = affinity.plan(gpu, aff, slot) if use_gpu else {"client": [], "server": []}
     if use_gpu and args.submit_cpus == "aux" and placement.get("aux"):
         n.set_submitter_cpus(placement["aux"])
-    if use_gpu and (args.crc_slot_waves or args.crc_slice8 == "on"):
+    if use_gpu and (args.crc_slot_waves or args.crc_slice8 == "off"):
         n.set_crc_options({"slot_waves": args.crc_slot_waves, "slice8": args.crc_slice8 == "on"})
     srv = n.Server({"port": 0, "md5": False, "cpus": placement["server"], "retain_uploads": False})
     srv.start()

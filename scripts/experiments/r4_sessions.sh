@@ -247,6 +247,12 @@ crc8)  # slot CRC kernel: slice-by-8 tables (half the L2-cold LDS stage) vs slic
     done
   done
   ;;
+final4)  # after slice-by-8 by default: GPU suite, smoke, two benches
+  step pytest_gpu 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+  step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+  step bench1 600 python3 bench.py --json-out "$O/bench1.json"
+  step bench2 600 python3 bench.py --json-out "$O/bench2.json"
+  ;;
 soak)  # profiles/r4_soak: execute_pb.sh with 48 workers x 100 MiB, -sink gpu, 120 s per protocol, exporter at 30 s
   step soak 900 python3 -u scripts/soak.py --out "$O" --duration 120s
   ;;

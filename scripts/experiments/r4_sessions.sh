@@ -253,6 +253,11 @@ final4)  # after slice-by-8 by default: GPU suite, smoke, two benches
   step bench1 600 python3 bench.py --json-out "$O/bench1.json"
   step bench2 600 python3 bench.py --json-out "$O/bench2.json"
   ;;
+dist)  # the HEAD headline against its bracketing baseline, eight back-to-back runs (distribution of vs_baseline)
+  for k in 1 2 3 4 5 6 7 8; do
+    step "b_$k" 300 python3 bench.py --blocks cpu_baseline,ceiling --json-out "$O/b_$k.json"
+  done
+  ;;
 soak)  # profiles/r4_soak: execute_pb.sh with 48 workers x 100 MiB, -sink gpu, 120 s per protocol, exporter at 30 s
   step soak 900 python3 -u scripts/soak.py --out "$O" --duration 120s
   ;;

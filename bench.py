@@ -166,6 +166,36 @@ def cpu_snapshot() -> dict:
     return snap
 
 
+def receiver_interference(head_cpu: dict, base_cpus: list[dict]) -> dict:
+    """The receiving thread's CPU-s per GiB in the headline against the same
+    thread in the bracketing baseline runs (both copy every byte out of one
+    socket on the same core).  Normally 0.9 - 1.0 (profiles/r4_dist); a
+    headline whose receiver cost several times its baseline's while it never
+    waited for a CPU ran under host interference (profiles/r4_dist b_4: 3.3x,
+    host-wide page faults 10x, function-call IPIs 2x on the placement)."""
+    def recv_cost(cpu: dict):
+        by = cpu.get("cpu_s_per_gib_by_name") or {}
+        for name in ("gcsb-h2-reader", "gcsb-worker", "gcsb-worker (exited)"):
+            if by.get(name):
+                return float(by[name])
+        return None
+    h = recv_cost(head_cpu)
+    b = [c for c in (recv_cost(x) for x in base_cpus) if c]
+    if not h or not b:
+        return {}
+    ratio = h / (sum(b) / len(b))
+    out = {"cpu_s_per_gib": round(h, 4), "baseline_cpu_s_per_gib": round(sum(b) / len(b), 4),
+           "cost_ratio": round(ratio, 2)}
+    if ratio >= 2.0:
+        th = ((head_cpu.get("host") or {}).get("threads") or {})
+        rd = max((v.get("run_delay_ms_per_read", 0.0) for k, v in th.items() if k.startswith("gcsb-h2-reader")
+                  or k.startswith("gcsb-worker")), default=0.0)
+        out["note"] = ("receive copy ran {:.1f}x its same-run baseline cost per GiB on the same core, run-queue delay "
+                       "{:.2f} ms per read, host-wide page faults {} over the headline: host interference, not the "
+                       "client path".format(ratio, rd, (head_cpu.get("host_vmstat") or {}).get("pgfault", "n/a")))
+    return out
+
+
 def tcp_sysctls() -> dict:
     """Socket-buffer limits of the box: an explicit SO_RCVBUF is capped at
     net.core.rmem_max (and doubled by the kernel)."""
@@ -1172,6 +1202,9 @@ def run_rank(args) -> int:
             if len(runs) == 2:
                 out["baseline"]["mib_s_before"] = round(mib_s(base_before), 2)
                 out["baseline"]["mib_s_after"] = round(mib_s(bst), 2)
+            flag = receiver_interference(head.get("cpu") or {}, [(r.get("cpu") or {}) for r in runs])
+            if flag:
+                out["baseline"]["receiver"] = flag
         for key, (_, st, extra) in blocks.items():
             if extra is None:  # already a JSON block (ceiling)
                 out[key] = st

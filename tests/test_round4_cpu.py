@@ -252,3 +252,25 @@ def test_endpoint_sockets_get_loopback_rto_min(native, server):
     server.add_synthetic(B, P, "", 0, 1, 1 << 20)
     cl = native.Client({"protocol": "grpc", "endpoint": server.url, "loopback_rto_min": True})
     assert cl.read(B, P + "0")["verified"]
+
+
+def test_bench_receiver_interference_flag():
+    """bench.receiver_interference: the headline receiver's CPU-s/GiB against
+    the same thread in the bracketing baselines; a >= 2x cost names host
+    interference (profiles/r4_dist b_4), a normal run carries only the ratio."""
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("gcsb_bench_mod", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    base = [{"cpu_s_per_gib_by_name": {"gcsb-h2-reader": 0.042}}, {"cpu_s_per_gib_by_name": {"gcsb-h2-reader": 0.038}}]
+    ok = bench.receiver_interference({"cpu_s_per_gib_by_name": {"gcsb-h2-reader": 0.038}}, base)
+    assert ok["cost_ratio"] == 0.95 and "note" not in ok
+    bad = bench.receiver_interference(
+        {"cpu_s_per_gib_by_name": {"gcsb-h2-reader": 0.126}, "host_vmstat": {"pgfault": 2311813},
+         "host": {"threads": {"gcsb-h2-reader": {"run_delay_ms_per_read": 0.02}}}}, base)
+    assert bad["cost_ratio"] == 3.15 and "host interference" in bad["note"] and "2311813" in bad["note"]
+    http = bench.receiver_interference({"cpu_s_per_gib_by_name": {"gcsb-worker (exited)": 0.08}},
+                                       [{"cpu_s_per_gib_by_name": {"gcsb-worker (exited)": 0.076}}])
+    assert http["cost_ratio"] == 1.05
+    assert bench.receiver_interference({}, base) == {}

@@ -258,6 +258,14 @@ dist)  # the HEAD headline against its bracketing baseline, eight back-to-back r
     step "b_$k" 300 python3 bench.py --blocks cpu_baseline,ceiling --json-out "$O/b_$k.json"
   done
   ;;
+final5)  # after the receiver-interference field: smoke, two full benches, four more headline runs
+  step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+  step bench1 600 python3 bench.py --json-out "$O/bench1.json"
+  step bench2 600 python3 bench.py --json-out "$O/bench2.json"
+  for k in 1 2 3 4; do
+    step "h_$k" 300 python3 bench.py --blocks cpu_baseline,ceiling --json-out "$O/h_$k.json"
+  done
+  ;;
 soak)  # profiles/r4_soak: execute_pb.sh with 48 workers x 100 MiB, -sink gpu, 120 s per protocol, exporter at 30 s
   step soak 900 python3 -u scripts/soak.py --out "$O" --duration 120s
   ;;

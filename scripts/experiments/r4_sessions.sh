@@ -266,6 +266,12 @@ final5)  # after the receiver-interference field: smoke, two full benches, four 
     step "h_$k" 300 python3 bench.py --blocks cpu_baseline,ceiling --json-out "$O/h_$k.json"
   done
   ;;
+dist2)  # headline vs its bracketing baseline, interleaved: pair (default) against pair2 (a second quiet core each)
+  for k in 1 2 3 4 5 6 7 8; do
+    step "pair_$k" 300 python3 bench.py --blocks cpu_baseline,ceiling --json-out "$O/pair_$k.json"
+    step "pair2_$k" 300 python3 bench.py --blocks cpu_baseline,ceiling --affinity pair2 --json-out "$O/pair2_$k.json"
+  done
+  ;;
 soak)  # profiles/r4_soak: execute_pb.sh with 48 workers x 100 MiB, -sink gpu, 120 s per protocol, exporter at 30 s
   step soak 900 python3 -u scripts/soak.py --out "$O" --duration 120s
   ;;

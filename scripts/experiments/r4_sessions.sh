@@ -266,6 +266,11 @@ final5)  # after the receiver-interference field: smoke, two full benches, four 
     step "h_$k" 300 python3 bench.py --blocks cpu_baseline,ceiling --json-out "$O/h_$k.json"
   done
   ;;
+final6)  # closing check of HEAD: GPU suite, smoke, the driver's bench command
+  step pytest_gpu 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+  step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+  step bench 600 python3 bench.py --json-out "$O/bench.json"
+  ;;
 dist2)  # headline vs its bracketing baseline, interleaved: pair (default) against pair2 (a second quiet core each)
   for k in 1 2 3 4 5 6 7 8; do
     step "pair_$k" 300 python3 bench.py --blocks cpu_baseline,ceiling --json-out "$O/pair_$k.json"

@@ -186,6 +186,15 @@ def receiver_interference(head_cpu: dict, base_cpus: list[dict]) -> dict:
     ratio = h / (sum(b) / len(b))
     out = {"cpu_s_per_gib": round(h, 4), "baseline_cpu_s_per_gib": round(sum(b) / len(b), 4),
            "cost_ratio": round(ratio, 2)}
+    clock = (head_cpu.get("host") or {}).get("clock_mhz_on_placement") or {}
+    for k, v in ((head_cpu.get("host") or {}).get("threads") or {}).items():
+        if k.startswith(("gcsb-h2-reader", "gcsb-worker")) and v.get("last_cpus"):
+            c = clock.get(str(v["last_cpus"][0]))
+            if c:
+                # the receiving core's clock through the headline
+                out["clock_mhz"] = c["mean"]
+                out["clock_mhz_min"] = c["min"]
+            break
     if ratio >= 2.0:
         th = ((head_cpu.get("host") or {}).get("threads") or {})
         rd = max((v.get("run_delay_ms_per_read", 0.0) for k, v in th.items() if k.startswith("gcsb-h2-reader")
@@ -591,7 +600,10 @@ def run_rank(args) -> int:
         win = None
         if not err:
             c0, th0 = cpu_snapshot(), cpuacct.thread_cpu()
-            win = sysdiag.Window()
+            diag_cpus = sorted(set(overrides.get("cpus") or cfg.get("cpus") or [])
+                               | set(placement.get("server") or []) | set(placement.get("aux") or []))
+            # the placement cores' clock through the block (a few cores only)
+            win = sysdiag.Window(clock_cpus=diag_cpus if 0 < len(diag_cpus) <= 16 else None)
             t1 = time.perf_counter()
             r1.start()
             r1.wait()
@@ -607,8 +619,6 @@ def run_rank(args) -> int:
             cpu = cpu_delta(c0, cpu_snapshot(), float(s1["bytes"]), e1)
             # what else ran on the block's CPUs: run-queue delay of our
             # threads, interrupts and softirqs there (utils/sysdiag.py)
-            diag_cpus = sorted(set(overrides.get("cpus") or cfg.get("cpus") or [])
-                               | set(placement.get("server") or []) | set(placement.get("aux") or []))
             cpu["host"] = win.report(diag_cpus or None, max(1, int(s1["reads"])))
             th1 = cpuacct.thread_cpu()
             cpu["cpu_s_per_gib_by_thread"] = cpuacct.per_gib(cpuacct.delta_by_group(th0, th1), float(s1["bytes"]))

@@ -11,7 +11,11 @@ privileges and cheap enough to snapshot around every timed block:
                   voluntary / involuntary context switches, last CPU;
   irq_snapshot()  /proc/interrupts per CPU and source (GPU completion
                   interrupts, NIC, IPIs, timers);
-  softirq_snapshot()  /proc/softirqs per CPU (NET_RX / NET_TX, TIMER, RCU).
+  softirq_snapshot()  /proc/softirqs per CPU (NET_RX / NET_TX, TIMER, RCU);
+  ClockSampler    the placement cores' clock (cpufreq cpuinfo_avg_freq, the
+                  APERF/MPERF average of the last tick) every 20 ms: a
+                  uniform slowdown of unrelated threads (profiles/r4_final6)
+                  is a core clock drop or memory, not a scheduler delay.
 
 Reference timed region: /root/reference/main.go:133-145 (request -> last
 byte); these views explain a read's stall inside that region, they add
@@ -20,6 +24,7 @@ nothing to it.
 from __future__ import annotations
 
 import os
+import threading
 
 _TASKS = "/proc/self/task"
 
@@ -255,21 +260,79 @@ def attribute(diag: dict, ms: float, p50_ms: float) -> str:
     return "; ".join(causes) or "no cause found"
 
 
+def _freq_file(cpu: int) -> str | None:
+    base = f"/sys/devices/system/cpu/cpu{cpu}/cpufreq/"
+    for name in ("cpuinfo_avg_freq", "scaling_cur_freq"):
+        if os.path.exists(base + name):
+            return base + name
+    return None
+
+
+class ClockSampler:
+    """Samples the given CPUs' clock (kHz from cpufreq) every `period_s` on a
+    daemon thread until .stop(); .report() gives MHz per CPU (mean, min, max
+    over the samples).  No cpufreq (VMs, this build container): no thread,
+    an empty report.  One small sysfs read per CPU per sample, off the
+    placement's CPUs (the thread inherits the main thread's affinity)."""
+
+    def __init__(self, cpus: list[int] | None, period_s: float = 0.02):
+        self.files = {c: f for c in (cpus or []) for f in [_freq_file(c)] if f}
+        self.samples: dict[int, list[int]] = {c: [] for c in self.files}
+        self.period = period_s
+        self._halt = threading.Event()
+        self._thread = None
+        if self.files:
+            self._thread = threading.Thread(target=self._run, name="gcsb-clock", daemon=True)
+            self._thread.start()
+
+    def _sample(self) -> None:
+        for c, path in self.files.items():
+            v = _read(path)
+            if v and v.strip().isdigit():
+                self.samples[c].append(int(v))
+
+    def _run(self) -> None:
+        while not self._halt.wait(self.period):
+            self._sample()
+
+    def stop(self) -> None:
+        self._halt.set()
+        if self._thread is not None:
+            self._thread.join(timeout=1.0)
+            self._thread = None
+
+    def report(self) -> dict[str, dict]:
+        self.stop()
+        out = {}
+        for c, v in sorted(self.samples.items()):
+            if v:
+                out[str(c)] = {"mean": round(sum(v) / len(v) / 1000.0), "min": round(min(v) / 1000.0),
+                               "max": round(max(v) / 1000.0), "n": len(v)}
+        return out
+
+
 class Window:
     """Snapshot everything at construction; .report(cpus, reads) after the
-    timed region."""
+    timed region.  With `clock_cpus`, those CPUs' clock is sampled through
+    the window (ClockSampler)."""
 
-    def __init__(self):
+    def __init__(self, clock_cpus: list[int] | None = None):
         self.sched = thread_sched()
         self.irq = irq_snapshot()
         self.soft = softirq_snapshot()
         self.tcp = tcp_snapshot()
         self.softnet = softnet_snapshot()
+        self.clock = ClockSampler(clock_cpus) if clock_cpus else None
 
     def report(self, cpus: list[int] | None, reads: int) -> dict:
-        return {"threads": sched_delta(self.sched, thread_sched(), reads),
-                "irq_on_placement": table_delta(self.irq, irq_snapshot(), cpus, reads),
-                "softirq_on_placement": table_delta(self.soft, softirq_snapshot(), cpus, reads),
-                # whole block, not per read: any RTO / drop names a stalled read
-                "tcp": tcp_delta(self.tcp, tcp_snapshot()),
-                "softnet_on_placement": softnet_delta(self.softnet, softnet_snapshot(), cpus)}
+        out = {"threads": sched_delta(self.sched, thread_sched(), reads),
+               "irq_on_placement": table_delta(self.irq, irq_snapshot(), cpus, reads),
+               "softirq_on_placement": table_delta(self.soft, softirq_snapshot(), cpus, reads),
+               # whole block, not per read: any RTO / drop names a stalled read
+               "tcp": tcp_delta(self.tcp, tcp_snapshot()),
+               "softnet_on_placement": softnet_delta(self.softnet, softnet_snapshot(), cpus)}
+        if self.clock is not None:
+            mhz = self.clock.report()
+            if mhz:
+                out["clock_mhz_on_placement"] = mhz
+        return out

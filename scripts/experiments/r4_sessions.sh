@@ -271,6 +271,12 @@ final6)  # closing check of HEAD: GPU suite, smoke, the driver's bench command
   step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
   step bench 600 python3 bench.py --json-out "$O/bench.json"
   ;;
+clock)  # the placement cores' clock through every block (sysdiag.ClockSampler): one full bench, six headline runs
+  step bench 600 python3 bench.py --json-out "$O/bench.json"
+  for k in 1 2 3 4 5 6; do
+    step "h_$k" 300 python3 bench.py --blocks cpu_baseline,ceiling --json-out "$O/h_$k.json"
+  done
+  ;;
 dist2)  # headline vs its bracketing baseline, interleaved: pair (default) against pair2 (a second quiet core each)
   for k in 1 2 3 4 5 6 7 8; do
     step "pair_$k" 300 python3 bench.py --blocks cpu_baseline,ceiling --json-out "$O/pair_$k.json"

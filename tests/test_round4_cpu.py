@@ -274,3 +274,36 @@ def test_bench_receiver_interference_flag():
                                        [{"cpu_s_per_gib_by_name": {"gcsb-worker (exited)": 0.076}}])
     assert http["cost_ratio"] == 1.05
     assert bench.receiver_interference({}, base) == {}
+
+
+def test_clock_sampler(tmp_path, monkeypatch):
+    """sysdiag.ClockSampler: MHz per CPU from the cpufreq files while the
+    window is open; none on a host without cpufreq; Window reports it as
+    clock_mhz_on_placement, and bench.receiver_interference picks the
+    receiving core's clock."""
+    import time
+    from custom_go_client_benchmark_amd.utils import sysdiag
+    f = tmp_path / "freq"
+    f.write_text("4800000\n")
+    monkeypatch.setattr(sysdiag, "_freq_file", lambda c: str(f) if c == 7 else None)
+    s = sysdiag.ClockSampler([7, 8], period_s=0.005)
+    time.sleep(0.05)
+    f.write_text("2400000\n")
+    time.sleep(0.05)
+    r = s.report()
+    assert list(r) == ["7"] and r["7"]["max"] == 4800 and r["7"]["min"] == 2400 and r["7"]["n"] >= 4
+    assert s._thread is None
+    assert sysdiag.ClockSampler([8]).report() == {}
+    w = sysdiag.Window(clock_cpus=[7])
+    time.sleep(0.05)
+    rep = w.report([7], 1)
+    assert rep["clock_mhz_on_placement"]["7"]["mean"] == 2400
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("gcsb_bench_mod2", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    head = {"cpu_s_per_gib_by_name": {"gcsb-h2-reader": 0.07},
+            "host": {"threads": {"gcsb-h2-reader": {"last_cpus": [7]}}, "clock_mhz_on_placement": rep["clock_mhz_on_placement"]}}
+    out = bench.receiver_interference(head, [{"cpu_s_per_gib_by_name": {"gcsb-h2-reader": 0.047}}])
+    assert out["clock_mhz"] == 2400 and out["cost_ratio"] == 1.49

@@ -261,7 +261,8 @@ void Runner::worker_main(int w) {
               g.landing = Landing::kObject;
               return std::make_unique<GpuSink>(g);
             }
-            return std::make_unique<DiscardSink>(rc.client.read_chunk, rc.host_crc, defer_host_crc(rc.client));
+            return std::make_unique<DiscardSink>(rc.client.read_chunk, rc.host_crc, defer_host_crc(rc.client),
+                                                 rc.discard_read_bytes);
           },
           [land](uint64_t total) {
             if (land) land->ensure(total);
@@ -281,7 +282,8 @@ void Runner::worker_main(int w) {
         sinks_[w] = std::move(g);
       } else {
         // multiplexed gRPC: host CRC on the worker thread, not the connection's reader
-        sinks_[w] = std::make_unique<DiscardSink>(cfg_.client.read_chunk, cfg_.host_crc, defer_host_crc(cfg_.client));
+        sinks_[w] = std::make_unique<DiscardSink>(cfg_.client.read_chunk, cfg_.host_crc, defer_host_crc(cfg_.client),
+                                                  cfg_.discard_read_bytes);
       }
     }
   } catch (const std::exception& e) {

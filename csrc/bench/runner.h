@@ -47,6 +47,9 @@ struct RunnerConfig {
   int worker_id_offset = 0;                             // rank * workers
   std::string sink = "discard";                         // discard | gpu
   bool host_crc = true;                                 // discard sink: CRC32C on the host
+  // discard sink: >0 models the reference's effective consumer, 8 KiB
+  // io.Discard reads copied out of each delivered message (DiscardSink copy_out)
+  size_t discard_read_bytes = 0;
   GpuSinkConfig gpu;
   int latency_fd = -1;                                  // write "<ms>ms\n" per read (1 = stdout)
   bool keep_records = true;

@@ -473,6 +473,7 @@ class PyRunner {
     c.worker_id_offset = get_or<int>(d, "worker_id_offset", 0);
     c.sink = get_or<std::string>(d, "sink", "discard");
     c.host_crc = get_or<bool>(d, "host_crc", true);
+    c.discard_read_bytes = get_or<size_t>(d, "discard_read_bytes", 0);
     c.gpu = gpu_from(d);
     c.latency_fd = get_or<int>(d, "latency_fd", -1);
     c.keep_records = get_or<bool>(d, "keep_records", true);

@@ -15,8 +15,9 @@
 namespace gcsb {
 
 
-DiscardSink::DiscardSink(size_t chunk_bytes, bool host_crc, bool deferred)
-    : cap_((chunk_bytes + 4095) / 4096 * 4096), host_crc_(host_crc), deferred_(deferred && host_crc) {
+DiscardSink::DiscardSink(size_t chunk_bytes, bool host_crc, bool deferred, size_t copy_out)
+    : copy_out_(copy_out), cap_((chunk_bytes + 4095) / 4096 * 4096), host_crc_(host_crc),
+      deferred_(deferred && host_crc) {
   if (deferred_) {
     // warm the pool with this sink's share, faulted in outside any read
     uint8_t* b[kMaxBlocks];
@@ -114,6 +115,19 @@ void DiscardSink::commit(size_t n) {
 }
 
 void DiscardSink::apply_data(const uint8_t* p, size_t n) {
+  if (copy_out_) {
+    // the consumer's Read()s: copy_out-byte copies into one small buffer
+    // (io.Discard's pooled 8 KiB buffer), each read back once so the
+    // copies cannot be elided
+    alignas(64) static thread_local uint8_t rbuf[64 << 10];
+    const size_t step = std::min(copy_out_, sizeof(rbuf));
+    for (size_t o = 0; o < n; o += step) {
+      const size_t k = std::min(step, n - o);
+      std::memcpy(rbuf, p + o, k);
+      asm volatile("" : : "r"(rbuf) : "memory");
+      copy_sink_ += rbuf[k - 1];
+    }
+  }
   // each byte is CRC'd once: inside a chunk into the chunk CRC (combined
   // into the object CRC at chunk end), outside directly into the object CRC
   if (!host_crc_) return;

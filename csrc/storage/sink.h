@@ -88,7 +88,14 @@ class Sink {
 // kMaxBlocks undrained blocks.
 class DiscardSink : public Sink {
  public:
-  DiscardSink(size_t chunk_bytes, bool host_crc, bool deferred = false);
+  // copy_out > 0: the reference's EFFECTIVE consumer -- every delivered
+  // byte is also copied out in copy_out-byte reads into a small buffer, as
+  // io.Discard.ReadFrom pulls 8 KiB Reads out of the library's reader
+  // (reference main.go:140): grpc-go decodes whole <= 2 MiB
+  // messages, the storage reader serves Read()s out of them.  Runs where the
+  // CRC runs (the read's worker thread).  Parity-unpinned: a model of the
+  // Go library's copies, not a measurement of it.
+  DiscardSink(size_t chunk_bytes, bool host_crc, bool deferred = false, size_t copy_out = 0);
   ~DiscardSink() override;
   void begin(const ObjectInfo& info) override;
   void update_info(const ObjectInfo& info) override;
@@ -118,6 +125,8 @@ class DiscardSink : public Sink {
   void push(const Op& op);
   void reset_ring();
 
+  size_t copy_out_ = 0;                  // >0: Read() size of the modelled consumer
+  uint64_t copy_sink_ = 0;               // keeps the copied-out bytes observable
   uint8_t* buf_ = nullptr;               // non-deferred: the one reusable buffer
   size_t cap_;
   bool host_crc_;

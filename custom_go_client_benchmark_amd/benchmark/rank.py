@@ -1,0 +1,1355 @@
+"""One bench rank: the headline and the side blocks (moved out of bench.py).
+
+Headline (BASELINE config 2/4): ONE gRPC ReadObject stream per 256 MiB
+object read (/root/reference/main.go:134-140), bytes landed in HBM through
+the pinned ring + hipMemcpyAsync, every CRC32C verified by the CDNA4
+kernels.  Rank r reads file_<r> (weak scaling; the reference's worker
+fan-out main.go:200-210 spread over GPUs).
+
+Paired headline (`--paired`, on at N = 1): the K timed headline reads run in
+4 chunks; between them, untimed for the headline, chunks of the same size of
+two twins on the same endpoint, placement and object:
+  base   reference semantics -- discard sink + host CRC32C (main.go:140,
+         the Go library's reader), on the headline's two cores;
+  nodma  the headline's own ring and receive path, the ring never DMA-read
+         (GpuSinkConfig gpu_stage none): the receive-side ceiling of the
+         headline's exact byte path.
+Each chunk is bracketed by a barrier + device sync on both sides; the
+headline's value is its bytes over the sum of its chunks' slowest-rank
+times.  vs_baseline_paired / headline_vs_nodma are the medians of the
+per-chunk ratios, so a slow host window hits both arms of one chunk.
+"""
+from __future__ import annotations
+
+import json
+import os
+import signal
+import sys
+import threading
+import time
+
+from . import report as rp
+
+METRIC = "p50/p99 read latency (ms) + MB/s per GPU; HTTP vs gRPC at 1/2/4/8 MI355X"
+
+# side blocks a multi-GPU run does by default (the rest with --blocks all)
+SCALE_BLOCKS = ("cpu_baseline", "compare", "write", "fanout")
+
+
+class Stash:
+    """Rank 0's output line.  The normal path prints ONE line at the end.
+    As soon as the headline is measured its line is printed to stderr (a
+    human watching sees it) and stashed: if a later side block hangs, the
+    fatal paths -- the barrier watchdog (parallel/dist.py on_fatal), the
+    side-block deadline, SIGTERM from the rank launcher -- print the stash on
+    stdout before the process ends, with a non-zero exit status."""
+
+    def __init__(self):
+        self._lock = threading.Lock()
+        self._line = None
+        self._printed = False
+        self._timer = None
+
+    def stash(self, line: str) -> None:
+        with self._lock:
+            self._line = line
+
+    def emit_stash(self, why: str = "") -> None:
+        with self._lock:
+            if self._line is None or self._printed:
+                return
+            self._printed = True
+            line = self._line
+        if why:
+            print(f"bench: {why}; printing the headline measured so far", file=sys.stderr, flush=True)
+        print(line, flush=True)
+
+    def final(self, line: str) -> None:
+        with self._lock:
+            if self._printed:  # a fatal path already printed the stash
+                return
+            self._printed = True
+        print(line, flush=True)
+
+    def arm(self, seconds: float) -> None:
+        """Side blocks must be done within `seconds` (0 = no limit)."""
+        if seconds <= 0 or self._timer is not None:
+            return
+
+        def fire():
+            self.emit_stash(f"side blocks still running after {seconds:.0f} s")
+            sys.stderr.flush()
+            os._exit(3)
+        self._timer = threading.Timer(seconds, fire)
+        self._timer.daemon = True
+        self._timer.start()
+
+    def disarm(self) -> None:
+        if self._timer is not None:
+            self._timer.cancel()
+
+
+stash = Stash()
+
+
+def maybe_hang(block: str, rank: int) -> None:
+    """Fault injection for the resilience tests: GCSB_TEST_HANG=<block>:<rank>
+    makes that rank hang at the start of that side block."""
+    spec = os.environ.get("GCSB_TEST_HANG", "")
+    if not spec:
+        return
+    b, _, r = spec.partition(":")
+    if b == block and str(rank) == (r or "0"):
+        print(f"bench: GCSB_TEST_HANG: rank {rank} hangs in side block {block}", file=sys.stderr, flush=True)
+        while True:
+            time.sleep(0.2)
+
+
+def parse_size(s: str) -> int:
+    s = s.strip()
+    mult = {"k": 1 << 10, "kib": 1 << 10, "m": 1 << 20, "mib": 1 << 20, "g": 1 << 30, "gib": 1 << 30}
+    for suf in sorted(mult, key=len, reverse=True):
+        if s.lower().endswith(suf):
+            return int(float(s[: -len(suf)]) * mult[suf])
+    return int(s)
+
+
+VMSTAT_KEYS = ("numa_hint_faults", "numa_pages_migrated", "thp_fault_alloc", "thp_collapse_alloc", "compact_stall",
+               "pgmajfault", "pgfault")
+
+
+def vmstat() -> dict:
+    out = {}
+    try:
+        with open("/proc/vmstat") as f:
+            for line in f:
+                k, _, v = line.partition(" ")
+                if k in VMSTAT_KEYS:
+                    out[k] = int(v)
+    except OSError:
+        pass
+    return out
+
+
+def cpu_snapshot() -> dict:
+    """Process CPU time (client + node-local endpoint share this process) and
+    the cgroup's CFS throttling counters: on the GPU boxes the container runs
+    under a CPU quota (profiles/r1_gpu_box_env.txt), and loopback TCP costs CPU
+    at both ends, so these explain throughput and the p99 tail."""
+    import resource
+
+    ru = resource.getrusage(resource.RUSAGE_SELF)
+    snap = {"user_s": ru.ru_utime, "sys_s": ru.ru_stime, "minflt": ru.ru_minflt, "nivcsw": ru.ru_nivcsw}
+    # host-wide memory-management events: NUMA-balancing hinting faults and
+    # migrations, THP faults / collapses, compaction stalls -- the kernel
+    # work that can slow a receive copy without showing in our own counters
+    snap.update({"vm_" + k: v for k, v in vmstat().items()})
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            for line in f:
+                k, _, v = line.partition(" ")
+                if k in ("usage_usec", "nr_periods", "nr_throttled", "throttled_usec"):
+                    snap[k] = int(v)
+    except OSError:
+        pass
+    return snap
+
+
+def cpu_delta(a: dict, b: dict, nbytes: float, elapsed: float) -> dict:
+    gib = max(nbytes, 1.0) / (1 << 30)
+    cpu_s = b["user_s"] + b["sys_s"] - a["user_s"] - a["sys_s"]
+    out = {"process_cpu_s_per_gib": round(cpu_s / gib, 4),
+           "process_sys_fraction": round((b["sys_s"] - a["sys_s"]) / max(1e-9, cpu_s), 3),
+           # CPUs this rank kept busy during the timed region (client + its endpoint)
+           "cpus_busy": round(cpu_s / max(elapsed, 1e-9), 2)}
+    for k in ("nr_periods", "nr_throttled", "throttled_usec"):
+        if k in a and k in b:
+            out["cgroup_" + k] = b[k] - a[k]
+    out["process_minflt"] = b.get("minflt", 0) - a.get("minflt", 0)
+    out["process_involuntary_cs"] = b.get("nivcsw", 0) - a.get("nivcsw", 0)
+    vm = {k[3:]: b[k] - a[k] for k in b if k.startswith("vm_") and k in a and b[k] != a[k]}
+    if vm:
+        out["host_vmstat"] = vm
+    return out
+
+
+def tcp_sysctls() -> dict:
+    """Socket-buffer limits of the box: an explicit SO_RCVBUF is capped at
+    net.core.rmem_max (and doubled by the kernel)."""
+    out = {}
+    for k, path in (("rmem_max", "/proc/sys/net/core/rmem_max"), ("tcp_rmem", "/proc/sys/net/ipv4/tcp_rmem"),
+                    ("wmem_max", "/proc/sys/net/core/wmem_max"), ("tcp_wmem", "/proc/sys/net/ipv4/tcp_wmem")):
+        try:
+            with open(path) as f:
+                v = [int(x) for x in f.read().split()]
+                out[k] = v[0] if len(v) == 1 else v
+        except (OSError, ValueError):
+            pass
+    try:
+        with open("/proc/sys/net/ipv4/tcp_congestion_control") as f:
+            out["tcp_congestion_control"] = f.read().strip()
+    except OSError:
+        pass
+    return out
+
+
+class Meter:
+    """Process CPU, per-thread-name CPU and vmstat over one or more timed
+    segments of one block.  begin()/end() bracket exactly the timed region:
+    host-view snapshots (sysdiag.Window) are taken outside them, so their
+    parsing of /proc tables is not charged to the block's python3 threads."""
+
+    def __init__(self):
+        self.proc: dict = {}
+        self.threads: dict[str, float] = {}
+        self.elapsed = 0.0
+        self.last: dict[str, float] = {}
+        self._c0 = self._t0 = None
+
+    def begin(self) -> None:
+        from ..utils import cpuacct
+
+        self._c0, self._t0 = cpu_snapshot(), cpuacct.thread_cpu()
+
+    def end(self, elapsed: float) -> None:
+        from ..utils import cpuacct
+
+        t1, c1 = cpuacct.thread_cpu(), cpu_snapshot()
+        self.last = cpuacct.delta_by_name(self._t0, t1)  # this segment alone
+        for k, v in self.last.items():
+            self.threads[k] = self.threads.get(k, 0.0) + v
+        for k, v in c1.items():
+            if isinstance(v, (int, float)) and k in self._c0:
+                self.proc[k] = self.proc.get(k, 0) + (v - self._c0[k])
+        self.elapsed += elapsed
+
+    def delta(self, nbytes: float) -> dict:
+        zero = {k: 0 for k in self.proc}
+        return cpu_delta(zero, self.proc, nbytes, self.elapsed) if self.proc else {}
+
+
+class RankBench:
+    """One rank's benchmark: its endpoint, placement and blocks."""
+
+    def __init__(self, args):
+        import torch
+
+        import custom_go_client_benchmark_amd as pkg
+        from ..ops import hbm
+        from ..parallel import affinity
+        from ..parallel import dist as gdist
+
+        self.args = args
+        self.torch = torch
+        self.hbm = hbm
+        self.affinity = affinity
+        self.gdist = gdist
+        self.n = pkg._native
+        self.rank, self.world, self.local_rank = gdist.env_rank()
+        self.use_gpu = args.sink == "gpu"
+        self.rehearsal = os.environ.get("GCSB_DIST_BACKEND") == "gloo"
+        self.diag: dict = {}  # the sidecar (rank 0 writes it)
+
+    # ------------------------------------------------------------------ setup
+    def setup(self) -> int:
+        args, n, torch, gdist, affinity = self.args, self.n, self.torch, self.gdist, self.affinity
+        if args.gpus != self.world:
+            print(f"bench: --gpus {args.gpus} but the launcher started {self.world} rank(s) (WORLD_SIZE); "
+                  f"they must match", file=sys.stderr)
+            return 2
+        if self.use_gpu:
+            self.hbm.gpu_required()
+            ndev = torch.cuda.device_count()
+            if self.world > ndev and not self.rehearsal:
+                print(f"bench: {self.world} ranks but only {ndev} visible GPU(s); one rank per GPU "
+                      f"(set GCSB_DIST_BACKEND=gloo for a shared-GPU rehearsal)", file=sys.stderr)
+                return 2
+        # process group even at world 1: RCCL init + barriers + reductions run in every GPU bench
+        self.ctx = gdist.init(local_rank=self.local_rank, world=self.world, rank=self.rank, always_pg=self.use_gpu)
+        if self.rank == 0:
+            # a peer that never reaches a barrier ends this rank through the
+            # watchdog, and the launcher ends a hung rank with SIGTERM: either
+            # way the stashed headline line is printed first
+            gdist.on_fatal(lambda: stash.emit_stash("a barrier timed out"))
+
+            def _term(signum, frame):
+                stash.emit_stash("terminated")
+                sys.stdout.flush()
+                os._exit(128 + signum)
+            signal.signal(signal.SIGTERM, _term)
+        protocol = args.protocol
+        if protocol == "auto":
+            protocol = "grpc" if "grpc" in self.hbm.available_protocols() else "http"
+        self.protocol = protocol
+        self.size = parse_size(args.object_size)
+        self.side_steps = args.steps if args.side_steps < 0 else args.side_steps
+        # side blocks get the headline's warm-up too: each opens fresh
+        # connections (and an endpoint of its own), so one warm-up read left
+        # its first timed one carrying setup (profiles/r2_write/tail_probe_*.json)
+        self.side_warm = max(1, args.warmup)
+
+        # node-local synthetic GCS endpoint for this rank (no network on the box)
+        self.gpu = self.ctx.gpu if self.ctx.gpu >= 0 else 0
+        aff = args.affinity
+        if aff == "auto":
+            aff = "pair" if args.slices == 1 else "share"
+        self.aff = aff
+        # ranks sharing one GPU (rehearsal) spread over L3 domains instead of stacking
+        self.slot = self.local_rank // max(1, torch.cuda.device_count()) if self.use_gpu and self.rehearsal else 0
+        self.placement = affinity.plan(self.gpu, aff, self.slot) if self.use_gpu else {"client": [], "server": []}
+        if self.use_gpu and args.submit_cpus == "aux" and self.placement.get("aux"):
+            n.set_submitter_cpus(self.placement["aux"])
+        if self.use_gpu and (args.crc_slot_waves or args.crc_slice8 == "off"):
+            n.set_crc_options({"slot_waves": args.crc_slot_waves, "slice8": args.crc_slice8 == "on"})
+        self.srv = n.Server({"port": 0, "md5": False, "cpus": self.placement["server"], "retain_uploads": False})
+        self.srv.start()
+        self.bucket = "princer-working-dirs"
+        self.prefix = "princer_100M_files/file_"
+        self.first = self.rank * args.workers
+        self.srv.add_synthetic(self.bucket, self.prefix, "", self.first, args.workers, self.size)
+        self.cfg = {
+            "protocol": protocol,
+            "endpoint": self.srv.url,
+            "bucket": self.bucket,
+            "object_prefix": self.prefix,
+            "workers": args.workers,
+            "reads_per_worker": args.warmup,
+            "worker_id_offset": self.first,
+            "sink": args.sink,
+            "device": self.gpu if self.use_gpu else 0,
+            "ring_slot_bytes": parse_size(args.slot_bytes),
+            "ring_slots": args.slots,
+            "conn_ring": args.conn_ring != "off",
+            "conn_ring_slots": int(args.conn_ring.partition("x")[0]) if "x" in args.conn_ring else 4,
+            "conn_ring_slot_bytes": parse_size(args.conn_ring.partition("x")[2]) if "x" in args.conn_ring else 1 << 20,
+            "landing": "object",
+            "grpc_conn_pool_size": args.grpc_pool,
+            "keep_records": False,
+            "cpus": self.placement["client"],
+            "retry_initial_s": 0.05,
+            "slices": args.slices,
+            "slice_piece_bytes": parse_size(args.piece_bytes),
+            "slice_piece_min_bytes": parse_size(args.piece_min_bytes),
+            "blocking_sync": args.event_wait == "block",
+            "async_submit": bool(args.async_submit),
+            "rcvbuf": parse_size(args.rcvbuf),
+            "tcp_congestion": args.client_cc,
+            "loopback_rto_min": True,
+            "recv_refill": bool(args.recv_refill),
+        }
+        return 0
+
+    def sync(self) -> None:
+        if self.torch.cuda.is_available():
+            self.torch.cuda.synchronize()
+
+    # --------------------------------------------------------- read blocks
+    def read_ok(self, s: dict, reads: int, cfg: dict) -> tuple[bool, str]:
+        if s["errors"]:
+            return False, s["first_error"] or "read error"
+        if s["reads"] != reads:
+            return False, f"{s['reads']} of {reads} reads completed"
+        # every read must have had its checksums verified (GPU CRC or host CRC)
+        if (cfg.get("sink") == "gpu" or cfg.get("host_crc", True)) and s["verified"] != reads:
+            return False, f"only {s['verified']} of {reads} reads had their CRC32C verified"
+        return True, ""
+
+    def open_runner(self, overrides: dict, warmup: int):
+        """A Runner for cfg + overrides, its warm-up reads done (connections,
+        rings, sinks survive into the timed reads).  (runner, error)."""
+        r1, err = None, ""
+        try:
+            r1 = self.n.Runner({**self.cfg, **overrides, "reads_per_worker": warmup})
+            if warmup > 0:
+                r1.start()
+                r1.wait()
+                sw = r1.summary()
+                if sw["errors"]:
+                    err = f"warmup: {sw['first_error']}"
+            r1.reset_stats()
+        except Exception as e:  # noqa: BLE001 - reported in the block, collectives still run
+            err = err or f"{type(e).__name__}: {e}"
+        return r1, err
+
+    def timed_segment(self, r1, reads: int, what: str, err: str, meter: Meter | None) -> float:
+        """`reads` reads per worker of an open runner between two barriers,
+        each followed by a device sync.  Every rank makes every collective
+        call whatever happens locally.  Returns this rank's elapsed s."""
+        gdist = self.gdist
+        if r1 is not None and not err:
+            r1.set_reads_per_worker(reads)
+        gdist.barrier(self.ctx, f"R1 {what} start barrier")
+        self.sync()
+        if meter is not None and not err:
+            meter.begin()
+        t1 = time.perf_counter()
+        if not err:
+            r1.start()
+            r1.wait()
+        self.sync()
+        gdist.barrier(self.ctx, f"R2 {what} stop barrier")
+        e1 = time.perf_counter() - t1
+        if meter is not None and not err:
+            meter.end(e1)
+        return e1
+
+    def read_block(self, overrides: dict, steps: int, warmup: int, what: str, endpoint=None) -> dict:
+        """warm-up reads, then `steps` timed reads of a config variant between
+        two barriers (one contiguous timed region)."""
+        from ..utils import sysdiag
+
+        r1, err = self.open_runner(overrides, warmup)
+        ep_stats = (endpoint or self.srv).stats
+        before = self._counters(ep_stats)
+        diag_cpus = sorted(set(overrides.get("cpus") or self.cfg.get("cpus") or [])
+                           | set(self.placement.get("server") or []) | set(self.placement.get("aux") or []))
+        # the host view starts before the CPU bracket and reports after it
+        win = sysdiag.Window(clock_cpus=diag_cpus if 0 < len(diag_cpus) <= 16 else None) if not err else None
+        meter = Meter()
+        e1 = self.timed_segment(r1, steps, what, err, meter)
+        return self.finish_block(r1, err, overrides, steps, e1, meter, before, ep_stats, win, diag_cpus)
+
+    def _counters(self, ep_stats) -> dict:
+        n = self.n
+        if self.use_gpu:
+            n.reset_slow_hip_calls()
+        return {"rv": n.recv_stats(), "rd": n.recv_diag(), "h2": n.h2_reader_stats(), "sv": ep_stats()}
+
+    def finish_block(self, r1, err: str, overrides: dict, steps: int, e1: float, meter: Meter, before: dict,
+                     ep_stats, win, diag_cpus) -> dict:
+        """Checks, per-GiB CPU, transport counters and the cross-rank
+        reduction of one read block (all of it outside the timed region)."""
+        from ..utils import cpuacct, sysdiag
+
+        n = self.n
+        cfg = {**self.cfg, **overrides}
+        workers = cfg.get("workers", self.args.workers)
+        cpu = {}
+        s1 = None
+        if not err:
+            s1 = r1.summary()
+            ok, why = self.read_ok(s1, steps * workers, cfg)
+            if not ok:
+                err = why
+            nb = float(s1["bytes"])
+            gib = max(nb, 1.0) / (1 << 30)
+            cpu = meter.delta(nb)
+            if win is not None:
+                # what else ran on the block's CPUs: run-queue delay of our
+                # threads, interrupts and softirqs there (utils/sysdiag.py)
+                cpu["host"] = win.report(diag_cpus or None, max(1, int(s1["reads"])))
+            names = dict(meter.threads)
+            groups: dict[str, float] = {}
+            for k, v in names.items():
+                g = cpuacct.group_of(k)
+                groups[g] = groups.get(g, 0.0) + v
+            cpu["cpu_s_per_gib_by_thread"] = cpuacct.per_gib(groups, nb)
+            # worker threads exit at the end of the run: their CPU comes from the runner
+            names.pop("gcsb-worker", None)
+            names["gcsb-worker (exited)"] = s1.get("worker_cpu_s", 0.0)
+            cpu["cpu_s_per_gib_by_name"] = {k: v for k, v in cpuacct.per_gib(names, nb).items() if v >= 0.0005}
+            h2s1 = n.h2_reader_stats()
+            h2s0 = before["h2"]
+            if h2s1["frames"] > h2s0["frames"]:
+                # the HTTP/2 connection readers (gRPC): where their time went, per GiB
+                d = {k: h2s1[k] - h2s0[k] for k in h2s1}
+                cpu["h2_reader"] = {"frames_per_read": round(d["frames"] / max(1, s1["reads"]), 2),
+                                    "wait_s_per_gib": round(d["header_wait_ns"] / 1e9 / gib, 4),
+                                    "data_s_per_gib": round(d["data_ns"] / 1e9 / gib, 4),
+                                    "headers_s_per_gib": round(d["headers_ns"] / 1e9 / gib, 4),
+                                    "other_s_per_gib": round(d["other_ns"] / 1e9 / gib, 4),
+                                    "avg_data_frame_kib": round(d["data_bytes"] / max(1, d["data_frames"]) / 1024, 1)}
+            cr = r1.conn_ring_stats()
+            if cr:
+                # the multiplexed connection's shared receive ring (warmup included)
+                cpu["conn_ring"] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in cr.items()}
+            g1 = s1.get("gpu") or {}
+            if g1.get("slot_waits") or g1.get("flag_reuses"):
+                cpu["slot_reuse"] = {"waits": g1["slot_waits"], "on_kernel_status": g1.get("flag_reuses", 0),
+                                     "s_per_gib": round(g1["slot_wait_s"] / gib, 4),
+                                     "handoff_s_per_gib": round(g1.get("handoff_s", 0.0) / gib, 5)}
+            sv0, sv1 = before["sv"], ep_stats()
+            if sv1.get("h2_data_frames", 0) > sv0.get("h2_data_frames", 0):
+                fr = sv1["h2_data_frames"] - sv0["h2_data_frames"]
+                rs = max(1, sv1["h2_responses"] - sv0["h2_responses"])
+                cpu["endpoint_h2"] = {"frames": fr,
+                                      "queue_wait_avg_us": round((sv1["h2_queue_wait_us"] - sv0["h2_queue_wait_us"]) / fr, 1),
+                                      "queue_wait_max_us": sv1["h2_queue_wait_max_us"],
+                                      "ttfb_avg_us": round((sv1["h2_ttfb_us"] - sv0["h2_ttfb_us"]) / rs, 1),
+                                      "ttfb_max_us": sv1["h2_ttfb_max_us"]}
+            if sv1.get("body_sends", 0) > sv0.get("body_sends", 0):
+                wall = max(1, sv1["body_wall_us"] - sv0["body_wall_us"])
+                sends = sv1["body_sends"] - sv0["body_sends"]
+                cpu["endpoint_tcp"] = {
+                    "busy_frac": round((sv1["tcp_busy_us"] - sv0["tcp_busy_us"]) / wall, 3),
+                    "rwnd_limited_frac": round((sv1["tcp_rwnd_limited_us"] - sv0["tcp_rwnd_limited_us"]) / wall, 3),
+                    "sndbuf_limited_frac": round((sv1["tcp_sndbuf_limited_us"] - sv0["tcp_sndbuf_limited_us"]) / wall,
+                                                 3),
+                    "cwnd_kib_at_end": round((sv1["tcp_cwnd_bytes_sum"] - sv0["tcp_cwnd_bytes_sum"]) / sends / 1024, 1)}
+            rv0, rv1 = before["rv"], n.recv_stats()
+            calls = rv1[0] - rv0[0]
+            if calls:
+                cpu["recv_calls"] = calls
+                cpu["recv_avg_kib"] = round((rv1[1] - rv0[1]) / calls / 1024.0, 1)
+            rd0, rd1 = before["rd"], n.recv_diag()
+            dc = rd1["calls"] - rd0["calls"]
+            if dc:
+                cpu["recv_queue"] = {"payload_recvs": dc,
+                                     "empty_frac": round((rd1["empty"] - rd0["empty"]) / dc, 3),
+                                     "short_frac": round((rd1["short"] - rd0["short"]) / dc, 3),
+                                     "avg_queued_kib": round((rd1["inq_bytes"] - rd0["inq_bytes"]) / dc / 1024, 1),
+                                     "avg_asked_kib": round((rd1["want_bytes"] - rd0["want_bytes"]) / dc / 1024, 1),
+                                     "recv_s_per_gib": round((rd1["recv_ns"] - rd0["recv_ns"]) / 1e9 / gib, 4)}
+        slow_hip = n.slow_hip_calls() if self.use_gpu else {}
+        use_gpu_sink = self.use_gpu and cfg.get("sink") == "gpu"
+        ring_numa = r1.ring_numa(0) if (r1 is not None and use_gpu_sink) else []
+        ring_thp = r1.ring_thp_fraction(0) if (r1 is not None and use_gpu_sink) else -1.0
+        s1 = s1 or {"bytes": 0, "p50_ms": 0.0, "p99_ms": 0.0, "host_p50_ms": 0.0, "ttfb_p50_ms": 0.0,
+                    "slice_skew_ms": 0.0, "verified": 0, "reads": 0}
+        recv = rp.recv_cost(cpu) or 0.0
+        py = (cpu.get("cpu_s_per_gib_by_name") or {}).get("python3", 0.0)
+        del r1
+        st = self.gdist.reduce_stats(self.ctx, elapsed=e1, nbytes=float(s1["bytes"]), p50=s1["p50_ms"],
+                                     p99=s1["p99_ms"], host_p50=s1["host_p50_ms"],
+                                     ttfb_p50=s1.get("ttfb_p50_ms", 0.0), skew=s1.get("slice_skew_ms", 0.0),
+                                     first_p50=s1.get("first_read_p50_ms", 0.0),
+                                     steady_p99=s1.get("steady_p99_ms", 0.0), verified=float(s1["verified"]),
+                                     recv_cpu=recv, py_cpu=py, ok=0.0 if err else 1.0)
+        st["error"] = err
+        st["cpu"] = cpu
+        st["ring_numa"] = ring_numa
+        st["ring_thp"] = ring_thp
+        # this rank's slowest reads [index in the timed run, ms, host-landed ms, TTFB ms]
+        st["slowest"] = [[int(x[0])] + [round(v, 3) for v in x[1:]] for x in (s1.get("slowest") or [])]
+        if s1.get("slowest_diag"):
+            st["slowest_diag"] = [
+                {"read": int(x[0]), "ms": round(x[1], 3),
+                 "cause": sysdiag.attribute(dg, x[1], s1["p50_ms"]),
+                 "threads": {k: {f: (round(v, 3) if isinstance(v, float) else v) for f, v in row.items()}
+                             for k, row in dg["threads"].items()},
+                 "softirqs": dg["softirqs"], "tcp": dg.get("tcp", {}), "softnet": dg.get("softnet", {})}
+                for x, dg in zip(s1["slowest"], s1["slowest_diag"])]
+        st["slow_hip"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in slow_hip.items()}
+        return st
+
+    # ------------------------------------------------------ paired headline
+    def paired_headline(self, head_over: dict, base_over: dict, nodma_over: dict | None, steps: int,
+                        warmup: int, chunks: int) -> tuple[dict, dict]:
+        """The headline's `steps` timed reads in `chunks` chunks, each chunk
+        followed -- in a rotating order -- by a chunk of the same size of the
+        reference-semantics baseline and of the never-DMA-read twin.  Only
+        the headline's chunks count toward its value and ms_per_step.
+        Returns (headline block stats, paired summary + per-chunk windows)."""
+        from ..utils import sysdiag
+
+        arms = {"head": head_over, "base": base_over}
+        if nodma_over is not None:
+            arms["nodma"] = nodma_over
+        runners, errs = {}, {}
+        for a, over in arms.items():
+            runners[a], errs[a] = self.open_runner(over, warmup if a == "head" else self.side_warm)
+        meters = {a: Meter() for a in arms}
+        ep_stats = self.srv.stats
+        before = self._counters(ep_stats)
+        elapsed = {a: 0.0 for a in arms}
+        sizes = rp.chunk_sizes(steps, chunks)
+        rates, windows = [], []
+        recv_cpus = self.placement.get("client") or []
+        for ci, k in enumerate(sizes):
+            row = {}
+            for a in rp.arm_order(list(arms), ci):
+                # light window: the receiving core's clock, host vmstat and
+                # the receiving thread's schedstat, outside the CPU bracket
+                clock = sysdiag.ClockSampler(recv_cpus[:4]) if recv_cpus and not errs[a] else None
+                vm0, sch0 = vmstat(), sysdiag.thread_sched()
+                m = meters[a]
+                m.last = {}
+                e = self.timed_segment(runners[a], k, f"paired {a} chunk {ci}", errs[a], m)
+                sch1, vm1 = sysdiag.thread_sched(), vmstat()
+                mhz = clock.report() if clock is not None else {}
+                elapsed[a] += e
+                # whole-job rate of this arm's chunk: all ranks' bytes over the
+                # slowest rank (every rank reads k objects of `size` per worker)
+                workers = {**self.cfg, **arms[a]}.get("workers", self.args.workers)
+                nbytes = float(k * workers * self.size) if not errs[a] else 0.0
+                red = self.gdist.reduce_stats(self.ctx, elapsed=e, nbytes=nbytes, ok=0.0 if errs[a] else 1.0)
+                if red["ok_min"] >= 1.0:
+                    row[a] = rp.mib_s(red)
+                gib = max(k * workers * self.size, 1) / (1 << 30)
+                recv = sum(v for t, v in m.last.items() if t.startswith(rp.RECV_THREADS[0])) \
+                    or sum(v for t, v in m.last.items() if t.startswith("gcsb-worker"))
+                rd = sum(y["run_delay_ns"] - sch0.get(tid, {}).get("run_delay_ns", 0)
+                         for tid, y in sch1.items() if y["name"].startswith(("gcsb-h2-reader", "gcsb-worker")))
+                w = {"chunk": ci, "arm": a, "reads": k, "mib_s": round(row.get(a, 0.0), 1),
+                     "recv_cpu_s_per_gib": round(recv / gib, 4) if recv else None,
+                     "run_delay_ms": round(rd / 1e6, 3)}
+                if mhz:
+                    w["clock_mhz"] = round(sum(v["mean"] for v in mhz.values()) / len(mhz))
+                    w["clock_mhz_min"] = min(v["min"] for v in mhz.values())
+                for f in ("numa_pages_migrated", "numa_hint_faults", "compact_stall", "pgfault", "thp_fault_alloc"):
+                    if f in vm0 and f in vm1:
+                        w[f] = vm1[f] - vm0[f]
+                windows.append(w)
+            rates.append(row)
+        head = self.finish_block(runners.pop("head"), errs["head"], head_over, steps, elapsed["head"],
+                                 meters["head"], before, ep_stats, None, None)
+        out = rp.paired_summary(rates)
+        out["windows"] = windows
+        out["slow_windows"] = rp.attribute_windows(windows)
+        for a in list(runners):
+            r = runners.pop(a)
+            if r is not None and not errs[a]:
+                s = r.summary()
+                acfg = {**self.cfg, **arms[a]}
+                if acfg.get("gpu_stage") == "none":  # nothing reads the ring: nothing verified
+                    acfg = {"sink": "discard", "host_crc": False}
+                ok, why = self.read_ok(s, steps * {**self.cfg, **arms[a]}.get("workers", self.args.workers), acfg)
+                if not ok:
+                    out[f"{a}_error"] = why[:200]
+                out[f"{a}_p50_ms"] = round(s["p50_ms"], 3)
+                out[f"{a}_recv_cpu_s_per_gib"] = rp.recv_cost(
+                    {"cpu_s_per_gib_by_name": {t: v / max(float(s["bytes"]), 1.0) * (1 << 30)
+                                               for t, v in meters[a].threads.items()}})
+            elif errs[a]:
+                out[f"{a}_error"] = errs[a][:200]
+            del r
+        return head, out
+
+    # ------------------------------------------------------------ endpoints
+    def share_endpoint(self):
+        """An endpoint of its own on the rank's share of L3 domains: the
+        sliced block's 8 send threads, and uploads, whose receive + CRC32C
+        on the endpoint is as heavy as the client's send."""
+        sh = self.affinity.plan(self.gpu, "share", self.slot) if self.use_gpu else {"client": [], "server": []}
+        e = self.n.Server({"port": 0, "md5": False, "cpus": sh["server"], "retain_uploads": False})
+        e.start()
+        e.add_synthetic(self.bucket, self.prefix, "", self.first, self.args.workers, self.size)
+        return e, sh
+
+    # ---------------------------------------------------------------- write
+    def write_block(self, steps: int, warmup: int, parts: int = 1) -> dict:
+        """Config 5: each rank uploads a 64 MiB object from HBM `steps` times
+        (HBM -> pinned ring D2H on a side stream -> resumable upload; the
+        object CRC32C is computed on the GPU and checked by the endpoint).
+        parts > 1 [extension]: parallel composite upload -- `parts` slices
+        uploaded on their own connections, composed server-side, the composed
+        CRC32C checked against the combine of the parts' GPU CRCs
+        (csrc/storage/sliced.h SlicedWriter)."""
+        from ..utils import cpuacct
+
+        args, n, torch, gdist = self.args, self.n, self.torch, self.gdist
+        err = ""
+        lat = []
+        wsize = parse_size(args.write_size)
+        chunk = parse_size(args.write_chunk)
+        client = buf = None
+        ep = None
+        saved_aff = os.sched_getaffinity(0)
+        gpu, rank = self.gpu, self.rank
+        try:
+            if parts == 1 and self.use_gpu and args.write_placement == "pair":
+                # three quiet cores of one L3 domain: the uploader (this
+                # thread) on one, the endpoint's receive and CRC threads on
+                # the other two (profiles/r3_write/placement)
+                pl = self.affinity.plan(gpu, "pair", self.slot)
+                sh = {"client": pl["client"], "server": sorted(pl["server"] + pl.get("aux", []))}
+                ep = n.Server({"port": 0, "md5": False, "cpus": sh["server"], "retain_uploads": False})
+                ep.start()
+            else:
+                ep, sh = self.share_endpoint()
+            # the upload runs on this (Python main) thread: keep it, its
+            # connection reader and the pinned staging ring on the GPU's node
+            if sh["client"]:
+                os.sched_setaffinity(0, sh["client"])
+            client = n.Client({"protocol": self.protocol, "endpoint": ep.url, "retry_initial_s": 0.05,
+                               "tcp_congestion": args.client_cc, "loopback_rto_min": True})
+            if parts > 1:
+                client = n.SlicedWriter({"protocol": self.protocol, "endpoint": ep.url, "retry_initial_s": 0.05,
+                                         "tcp_congestion": args.client_cc, "loopback_rto_min": True,
+                                         "slices": parts, "slice_min_bytes": 1 << 20, "cpus": sh["client"]})
+            buf = torch.empty(wsize, dtype=torch.uint8, device=f"cuda:{gpu}")
+            n.gpu_fill_pattern(gpu, buf.data_ptr(), wsize, f"upload/rank{rank}", 0)
+            for i in range(warmup):
+                client.write_from_device(self.bucket, f"upload/warmup_{rank}_{i}", buf.data_ptr(), wsize, gpu, True,
+                                         chunk, parse_size(args.slot_bytes), args.slots)
+        except Exception as e:  # noqa: BLE001
+            err = f"{type(e).__name__}: {e}"
+        gdist.barrier(self.ctx, "R1 write start barrier")
+        self.sync()
+        n.reset_slow_hip_calls()
+        th0 = cpuacct.thread_cpu()
+        t1 = time.perf_counter()
+        nbytes = 0
+        if not err:
+            try:
+                for i in range(steps):
+                    t0 = time.perf_counter()
+                    m = client.write_from_device(self.bucket, f"upload/rank{rank}_{i}", buf.data_ptr(), wsize, gpu,
+                                                 True, chunk, parse_size(args.slot_bytes), args.slots)
+                    lat.append((time.perf_counter() - t0) * 1e3)
+                    # (SlicedWriter checks the composed CRC32C itself)
+                    if m["size"] != wsize or (parts == 1 and m["crc32c"] != m["gpu_crc32c"]):
+                        err = f"upload {i} not confirmed: {m}"
+                        break
+                    nbytes += wsize
+            except Exception as e:  # noqa: BLE001
+                err = f"{type(e).__name__}: {e}"
+        self.sync()
+        gdist.barrier(self.ctx, "R2 write stop barrier")
+        e1 = time.perf_counter() - t1
+        by_name = {k: v - th0.get(k, 0.0) for k, v in cpuacct.thread_cpu().items()}
+        cpu_split = {k: round(v / max(nbytes, 1) * (1 << 30), 4) for k, v in sorted(by_name.items())
+                     if v > 0.0005 and nbytes}
+        s = sorted(lat)
+        p50 = s[len(s) * 50 // 100] if s else 0.0
+        p99 = s[min(len(s) - 1, len(s) * 99 // 100)] if s else 0.0
+        if ep is not None:
+            del client
+            ep.stop()
+        os.sched_setaffinity(0, saved_aff)
+        st = gdist.reduce_stats(self.ctx, elapsed=e1, nbytes=float(nbytes), p50=p50, p99=p99, ok=0.0 if err else 1.0)
+        st["error"] = err
+        st["slowest"] = [[i, round(v, 2)] for i, v in sorted(enumerate(lat), key=lambda x: -x[1])[:3]]
+        st["slow_hip"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in n.slow_hip_calls().items()}
+        st["cpu_s_per_gib_by_thread"] = cpu_split
+        return st
+
+    # --------------------------------------------------------------- fanout
+    def fanout_block(self, steps: int, warmup: int) -> dict:
+        """[extension, N > 1] read once per node, fan out over xGMI: every rank
+        reads only its 1/N slice of ONE shared 256 MiB object (ranged gRPC
+        read into HBM, per-message CRC32C on the GPU), then an RCCL
+        all-gather over the node's GPUs gives every GPU the whole object,
+        whose CRC32C each GPU then checks."""
+        args, n, torch, gdist, ctx = self.args, self.n, self.torch, self.gdist, self.ctx
+        rank, world, size, gpu = self.rank, self.world, self.size, self.gpu
+        err = ""
+        lat = []
+        crc_ok = 0
+        part_n = size // world
+        name = "fanout/obj_0"
+        full = part = sink = client = None
+        want = 0
+        try:
+            if size % world:
+                raise ValueError(f"object size {size} not divisible by {world} ranks")
+            self.srv.add_synthetic(self.bucket, "fanout/obj_", "", 0, 1, size)
+            want = self.srv.object_info(self.bucket, name)["crc32c"]
+            client = n.Client({"protocol": self.protocol, "endpoint": self.srv.url, "retry_initial_s": 0.05,
+                               "tcp_congestion": args.client_cc, "loopback_rto_min": True,
+                               "cpus": self.placement["client"], "rcvbuf": parse_size(args.rcvbuf)})
+            full = torch.empty(size, dtype=torch.uint8, device=f"cuda:{gpu}" if self.use_gpu else "cpu")
+            # this rank's slice lands in place: the all-gather's input is the
+            # slice of its output at rank * part_n (in-place all-gather)
+            part = full[rank * part_n:(rank + 1) * part_n]
+            if self.use_gpu:
+                sink = n.GpuSink({"device": gpu, "ring_slot_bytes": parse_size(args.slot_bytes),
+                                  "ring_slots": args.slots})
+                sink.set_external_destination(part.data_ptr(), size - rank * part_n)
+        except Exception as e:  # noqa: BLE001 - reported in the block, collectives still run
+            err = f"{type(e).__name__}: {e}"
+
+        for i in range(warmup + steps):
+            # every rank makes the same collective calls whatever happened locally
+            flags = gdist.reduce_stats(ctx, ok=0.0 if err else 1.0)
+            if flags["ok_min"] < 1.0:
+                err = err or "a peer rank failed"
+                break
+            gdist.barrier(ctx, "fan-out start")
+            t0 = time.perf_counter()
+            local = ""
+            try:
+                if self.use_gpu:
+                    r = client.read_gpu(self.bucket, name, sink, rank * part_n, part_n)
+                    if r["bytes"] != part_n or r["crc_mismatch"]:
+                        local = f"slice read failed: {r}"
+                else:  # CPU rehearsal: the slice through host memory
+                    b = client.read_bytes(self.bucket, name, rank * part_n, part_n)
+                    part.copy_(torch.frombuffer(bytearray(b), dtype=torch.uint8))
+            except Exception as e:  # noqa: BLE001
+                local = f"{type(e).__name__}: {e}"
+            try:
+                gdist.all_gather_bytes(ctx, full, part, "fan-out all-gather")
+                self.sync()
+            except Exception as e:  # noqa: BLE001 - the process group is gone: no more collectives
+                err = f"all-gather: {type(e).__name__}: {e}"
+                return {"ok_min": 0.0, "p50_max": 0.0, "p99_max": 0.0, "crc_ok_sum": 0.0, "nbytes_sum": 0.0,
+                        "elapsed_max": 0.0, "error": err}
+            gdist.barrier(ctx, "fan-out stop")
+            if local:
+                err = local
+            elif i >= warmup:
+                lat.append((time.perf_counter() - t0) * 1e3)
+        if not err:
+            got = n.gpu_crc32c(gpu, full.data_ptr(), size) if self.use_gpu else n.crc32c(full.numpy().tobytes())
+            crc_ok = int(got == want)
+            if not crc_ok:
+                err = "CRC32C of the gathered object does not match"
+        s_ = sorted(lat)
+        p50 = s_[len(s_) * 50 // 100] if s_ else 0.0
+        p99 = s_[min(len(s_) - 1, len(s_) * 99 // 100)] if s_ else 0.0
+        st = gdist.reduce_stats(ctx, elapsed=sum(lat) / 1e3, nbytes=float(size * len(lat)), p50=p50, p99=p99,
+                                ok=0.0 if err else 1.0, crc_ok=float(crc_ok))
+        st["error"] = err
+        del part, full, sink
+        return st
+
+    # ------------------------------------------------------------ list-read
+    def list_read_block(self, proto: str, warmup_passes: int) -> dict:
+        """Config 3 (BASELINE.json): list `--list-objects` 1 MiB objects, then
+        `--list-workers` readers read every listed object once into HBM, GPU
+        CRC32C on every read (reference list_operation + read_operation).
+        One timed pass after untimed ones; the listing's own time apart."""
+        args, n = self.args, self.n
+        nobj, workers = args.list_objects, args.list_workers
+        # one L3 domain for the readers and the endpoint (profiles/r2_check_s4b, r2_cli_geometry)
+        sh = self.affinity.plan(self.gpu, "same", self.slot) if self.use_gpu else {"client": [], "server": []}
+        if self.use_gpu and proto != "http" and args.mux_reader == "isolate":
+            sh = self.affinity.isolate_reader(sh)
+        ep = None
+        names, list_ms, err = [], 0.0, ""
+        rank = self.rank
+        try:
+            ep = n.Server({"port": 0, "md5": False, "cpus": sh["server"], "retain_uploads": False})
+            ep.start()
+            ep.add_synthetic(self.bucket, f"c3_rank{rank}/file_", "", 0, nobj, 1 << 20)
+            lister = n.Client({"protocol": proto, "endpoint": ep.url, "retry_initial_s": 0.05})
+            t0 = time.perf_counter()
+            names = [o["name"] for o in lister.list_all(self.bucket, f"c3_rank{rank}/file_", 1000)]
+            list_ms = (time.perf_counter() - t0) * 1e3
+            del lister
+            if len(names) != nobj:
+                err = f"listed {len(names)} of {nobj} objects"
+        except Exception as e:  # noqa: BLE001 - reported in the block, collectives still run
+            err = f"{type(e).__name__}: {e}"
+        per_pass = (nobj + workers - 1) // workers
+        lslots, _, lbytes = args.list_ring.partition("x")
+        over = {"protocol": proto, "endpoint": ep.url if ep is not None else "", "workers": workers,
+                "object_names": names or [f"c3_rank{rank}/file_0"], "cpus": sh["client"], "worker_id_offset": 0,
+                "rcvbuf": parse_size(args.list_rcvbuf), "ring_slots": int(lslots), "ring_slot_bytes": parse_size(lbytes),
+                "ring_wc": args.list_ring_wc == "on", "reader_cpus": sh.get("reader_cpus")}
+        st = self.read_block(over, per_pass, per_pass * warmup_passes, f"{proto} list-read", endpoint=ep)
+        if err:
+            st["error"] = err
+            st["ok_min"] = 0.0
+        if ep is not None:
+            ep.stop()
+        st["list_ms_max"] = self.gdist.reduce_stats(self.ctx, list_ms=list_ms)["list_ms_max"]
+        return st
+
+    # -------------------------------------------------------------- ceiling
+    def ceiling_block(self, head_mib_s_per_rank: float) -> dict:
+        """Same-box bounds: one loopback TCP stream with no GPU and no framing
+        (vmsplice/sendfile by a thread on the endpoint's CPUs -> recv() into a
+        THP ring by a thread on the client's CPUs, core/ceiling.cc), in the
+        headline's placement (tcp_gbps) and in the one-L3-domain placement of
+        the multiplexed gRPC blocks (tcp_gbps_same); the client core's memcpy
+        rate; pinned -> HBM copies in the sink's pattern (engine.hip
+        copy_ceiling)."""
+        args, n = self.args, self.n
+        err = ""
+        r = {"tcp_gbps": 0.0, "tcp_gbps_same": 0.0, "tcp_recv_cpu_s_per_gib": 0.0, "tcp_send_cpu_s_per_gib": 0.0,
+             "memcpy_gbps": 0.0, "h2d_gbps": 0.0}
+        try:
+            ring = args.slots * parse_size(args.slot_bytes)
+            reads = max(3, min(10, self.side_steps))
+            t = n.loopback_ceiling({"mode": "tcp", "object_bytes": self.size, "reads": reads, "ring_bytes": ring,
+                                    "rcvbuf": parse_size(args.rcvbuf), "recv_cpus": self.placement["client"],
+                                    "send_cpus": self.placement["server"], "ring_pages": 1})
+            m = n.loopback_ceiling({"mode": "memcpy", "object_bytes": self.size, "reads": reads, "ring_bytes": ring,
+                                    "recv_cpus": self.placement["client"], "ring_pages": 1})
+            r.update(tcp_gbps=t["gbps"], tcp_recv_cpu_s_per_gib=t["recv_cpu_s_per_gib"],
+                     tcp_send_cpu_s_per_gib=t["send_cpu_s_per_gib"], memcpy_gbps=m["gbps"])
+            if self.use_gpu:
+                same = self.affinity.plan(self.gpu, "same", self.slot)
+                ts = n.loopback_ceiling({"mode": "tcp", "object_bytes": self.size, "reads": reads, "ring_bytes": ring,
+                                         "rcvbuf": parse_size(args.rcvbuf), "recv_cpus": same["client"][:1],
+                                         "send_cpus": same["server"], "ring_pages": 1})
+                r["tcp_gbps_same"] = ts["gbps"]
+                h = n.copy_ceiling(self.gpu, "h2d", self.size, parse_size(args.slot_bytes), args.slots, args.slots, 5)
+                r["h2d_gbps"] = h["gbps"]
+            else:
+                r["tcp_gbps_same"] = t["gbps"]
+        except Exception as e:  # noqa: BLE001 - reported in the block, collectives still run
+            err = f"{type(e).__name__}: {e}"
+        st = self.gdist.reduce_stats(self.ctx, ok=0.0 if err else 1.0, **r)
+        out = {"ok": st["ok_min"] >= 1.0}
+        for k in r:  # the slowest rank's bound (each rank measures its own)
+            out[k] = round(st[k + "_min"], 3)
+        head_gbps = head_mib_s_per_rank * (1 << 20) / 1e9
+        bounds = [b for b in (out["tcp_gbps"], out["h2d_gbps"] if self.use_gpu else 0.0) if b > 0]
+        if bounds:
+            out["bound_gbps"] = round(min(bounds), 3)
+            out["headline_gbps_per_gpu"] = round(head_gbps, 3)
+            out["headline_frac_of_ceiling"] = round(head_gbps / min(bounds), 3)
+        if err:
+            out["error"] = err[:300]
+        return out
+
+    # ---------------------------------------------------------- ref default
+    def ref_default_block(self, proto: str, osz: int = 0, reads: int = 0, sink: str = "discard",
+                          warmup: int = 2, extra: dict | None = None) -> dict:
+        """The reference's only experiment (execute_pb.sh:4,8; main.go:36,
+        30,111): -worker 48 readers, each re-reading its own object
+        file_<id>, over gRPC with ONE connection (pool 1) or HTTP/1.1
+        keep-alive.  sink "discard": io.Discard with the library's host
+        CRC32C (reference semantics); "gpu": every read lands in HBM (the
+        connection ring for gRPC, a small ring per worker for HTTP) with
+        CRC32C on the GPU.  Objects are --ref-object-size or 100 MiB
+        (ref_default_100m_*, princer_100M_files, main.go:52)."""
+        args, n = self.args, self.n
+        workers = args.ref_workers
+        osz = osz or parse_size(args.ref_object_size)
+        reads = reads or args.ref_reads
+        mode = args.ref_grpc_placement if proto != "http" else args.ref_http_placement
+        sh = self.affinity.plan(self.gpu, mode, self.slot) if self.use_gpu else {"client": [], "server": []}
+        if self.use_gpu and proto != "http" and args.mux_reader == "isolate":
+            sh = self.affinity.isolate_reader(sh)
+        ep = None
+        err = ""
+        prefix = "ref_default/file_" if osz == parse_size(args.ref_object_size) else f"ref_default_{osz >> 20}m/file_"
+        try:
+            ep = n.Server({"port": 0, "md5": False, "cpus": sh["server"], "retain_uploads": False})
+            ep.start()
+            ep.add_synthetic(self.bucket, prefix, "", self.rank * workers, workers, osz)
+        except Exception as e:  # noqa: BLE001
+            err = f"{type(e).__name__}: {e}"
+        over = {"protocol": proto, "endpoint": ep.url if ep is not None else "", "workers": workers,
+                "object_prefix": prefix, "worker_id_offset": self.rank * workers, "sink": sink,
+                "host_crc": sink != "gpu", "cpus": sh["client"], "rcvbuf": 0, "grpc_conn_pool_size": 1,
+                "reader_cpus": sh.get("reader_cpus")}
+        if sink == "gpu":
+            rs, _, rb = args.ref_gpu_ring.partition("x")
+            over.update(ring_slots=int(rs), ring_slot_bytes=parse_size(rb), landing="object")
+        if extra:
+            over.update(extra)
+        st = self.read_block(over, reads, warmup, f"{proto} reference default {osz >> 20} MiB {sink}", endpoint=ep)
+        if err:
+            st["error"] = err
+            st["ok_min"] = 0.0
+        if ep is not None:
+            ep.stop()
+        return st
+
+    def baseline_over(self) -> dict:
+        # The baseline gets the headline's submitter core too: its host CRC
+        # runs on the worker (gRPC: apart from the connection's reader, as
+        # the Go library's caller goroutine is apart from grpc-go's transport
+        # reader), so both designs get two physical cores.
+        over = {"protocol": self.protocol, "sink": "discard", "host_crc": True}
+        base_cpus = sorted(set(self.placement.get("client", [])) | set(self.placement.get("aux", [])))
+        if base_cpus:
+            over["cpus"] = base_cpus
+        return over
+
+    # ============================================================ the run
+    def run(self) -> int:
+        rc = self.setup()
+        if rc:
+            return rc
+        args, gdist, ctx = self.args, self.gdist, self.ctx
+        world, rank, protocol = self.world, self.rank, self.protocol
+        side_steps, side_warm = self.side_steps, self.side_warm
+        use_gpu = self.use_gpu
+
+        only = {b.strip() for b in args.blocks.split(",") if b.strip()}
+        explicit = only - {"all"}
+        base_on = args.baseline == "on" and (not explicit or "cpu_baseline" in explicit) and side_steps > 0
+        bracket = args.baseline_bracket == "on" or (args.baseline_bracket == "auto" and world == 1)
+        paired = args.workload == "read" and base_on and args.steps >= 2 and (
+            args.paired == "on" or (args.paired == "auto" and world == 1))
+        self.base_before = None
+        self.paired = None
+        if args.workload == "read" and use_gpu and bracket and base_on:
+            # the reference-semantics read once more BEFORE the headline, so
+            # the two baselines bracket it and a drifting host cancels
+            self.base_before = self.read_block(self.baseline_over(), side_steps, side_warm,
+                                               f"{protocol} cpu baseline (before)")
+        if args.workload == "read":
+            # --read-diag samples the headline's threads around every read
+            diag_avoid = sorted(set(self.placement.get("client", [])) | set(self.placement.get("server", []))
+                                | set(self.placement.get("aux", []) or []))
+            head_over = {"read_diag": bool(args.read_diag), "diag_avoid_cpus": diag_avoid}
+            if paired:
+                nodma = {"gpu_stage": "none", "gpu_verify": False} if use_gpu else None
+                head, self.paired = self.paired_headline(head_over, self.baseline_over(), nodma, args.steps,
+                                                         args.warmup, args.paired_chunks)
+            else:
+                head = self.read_block(head_over, args.steps, args.warmup, "headline")
+            self.headline_model = (f"{protocol} ReadObject {args.object_size} object, "
+                                   f"{'one stream per read' if args.slices == 1 else f'{args.slices} ranged streams'}"
+                                   + (" -> HBM (CRC32C on GPU)" if use_gpu else " -> discard (CPU baseline)"))
+        else:
+            if not use_gpu:
+                print("bench: --workload write needs --sink gpu (uploads are staged from HBM)", file=sys.stderr)
+                return 2
+            head = self.write_block(args.steps, args.warmup)
+            self.headline_model = (f"{protocol} resumable upload {args.write_size} object from HBM "
+                                   f"(D2H -> pinned -> upload)")
+        self.head = head
+
+        # R4: which HIP device each rank used -> distinct GPUs in the job (before
+        # the side blocks: the fan-out block may leave the communicator aborted)
+        devs = gdist.gather_floats(ctx, [float(ctx.gpu if use_gpu else -1)])
+        self.distinct = sorted({int(d[0]) for d in devs if d[0] >= 0})
+        self.n_gpus = len(self.distinct) if use_gpu else world
+
+        other = {"grpc": "http", "http": "grpc"}.get(protocol)
+        protos = self.hbm.available_protocols()
+        ref100 = parse_size(args.ref100_object_size)
+        self.blocks = {}
+        blocks = self.blocks
+        if not only and world > 1:
+            # N > 1: the blocks the scaling run needs; the rest only when asked for
+            only = set(SCALE_BLOCKS)
+        if "all" in only:
+            only = set()
+
+        def want(name: str) -> bool:
+            ok = not only or name in only
+            if ok:
+                maybe_hang(name, rank)
+            return ok
+        if side_steps > 0 and args.workload == "read":
+            if base_on and want("cpu_baseline"):
+                # right after the headline: the reference's semantics on the
+                # headline config -- same endpoint, placement, object and
+                # steps; bytes to a discard sink, CRC32C of every byte on the
+                # host (/root/reference/main.go:133-146).  vs_baseline divides by it.
+                for p in [protocol] + ([other] if other and other in protos else []):
+                    key = "cpu_baseline" if p == protocol else f"cpu_baseline_{p}"
+                    over = {**self.baseline_over(), "protocol": p}
+                    blocks[key] = (self.read_block(over, side_steps, side_warm, f"{p} cpu baseline"),
+                                   {"protocol": p, "sink": "discard", "_conns": 1, "_place": "pair",
+                                    "note": "reference semantics: io.Discard + host CRC32C; client + submitter cores"})
+            self.stash_headline()
+            if other and other in protos and want("compare"):
+                blocks["compare"] = (self.read_block({"protocol": other}, side_steps, side_warm, f"{other} compare"),
+                                     {"protocol": other, "sink": self.args.sink, "_conns": 1, "_place": "pair"})
+            if self.base_before is not None:
+                blocks["cpu_baseline_before"] = (self.base_before,
+                                                 {"protocol": protocol, "sink": "discard", "_conns": 1,
+                                                  "_place": "pair",
+                                                  "note": "the cpu_baseline block, run before the headline"})
+            if args.sliced_streams > 1 and args.slices == 1 and want("sliced"):
+                # 8 receive + 8 send threads: a share-placed endpoint of its own
+                srv_sl, sh = self.share_endpoint()
+                sliced_cfg = {"slices": args.sliced_streams, "ring_slot_bytes": parse_size(args.sliced_slot_bytes),
+                              "ring_slots": args.sliced_slots, "async_submit": bool(args.sliced_async_submit),
+                              "rcvbuf": 0, "endpoint": srv_sl.url, "cpus": sh["client"]}
+                st_sl = self.read_block(sliced_cfg, side_steps, side_warm, "sliced")
+                srv_sl.stop()
+                blocks["sliced"] = (st_sl, {"streams_per_read": args.sliced_streams, "sink": self.args.sink,
+                                            "ring": f"{args.sliced_slots}x{args.sliced_slot_bytes}",
+                                            "_conns": args.sliced_streams, "affinity": "share",
+                                            "piece_bytes": parse_size(args.piece_bytes),
+                                            "note": "extension, not parity"})
+            if args.ceiling == "on" and want("ceiling"):
+                blocks["ceiling"] = (self.ceiling_block(rp.mib_s(head) / max(1, world)), None)
+            if args.ref_workers > 0 and want("ref_default"):
+                for p in ["http"] + [x for x in ("grpc",) if x in protos]:
+                    blocks[f"ref_default_{p}"] = (self.ref_default_block(p),
+                                                  {"protocol": p, "workers": args.ref_workers, "sink": "discard",
+                                                   "object_bytes": parse_size(args.ref_object_size),
+                                                   "reads_per_worker": args.ref_reads,
+                                                   "_conns": 1 if p == "grpc" else args.ref_workers, "_place": "same",
+                                                   "note": "reference default experiment (execute_pb.sh)"})
+            if args.ref_workers > 0 and args.ref_effective == "on" and "grpc" in protos and want("ref_effective"):
+                # the reference's EFFECTIVE read path: io.Discard.ReadFrom ignores
+                # the 2 MiB buffer and pulls 8 KiB reads out of each decoded
+                # <= 2 MiB message (main.go:123-125,140)
+                blocks["ref_effective_grpc"] = (
+                    self.ref_default_block("grpc", ref100, args.ref100_reads, "discard", warmup=1,
+                                           extra={"discard_read_bytes": 8192}),
+                    {"protocol": "grpc", "workers": args.ref_workers, "sink": "discard", "object_bytes": ref100,
+                     "_conns": 1, "_place": "same",
+                     "note": "parity-unpinned: grpc-go's message decode + 8 KiB io.Discard reads, modelled"})
+            if args.ref_workers > 0 and args.ref100_reads > 0 and want("ref_default_100m"):
+                # the reference's real operating point: 48 workers x 100 MiB
+                # (princer_100M_files, main.go:36,52), both transports, into
+                # the discard sink (reference semantics) and into HBM
+                for p in ["http"] + [x for x in ("grpc",) if x in protos]:
+                    for sk in ["discard"] + (["gpu"] if use_gpu else []):
+                        key = f"ref_default_100m_{p}_{sk}"
+                        blocks[key] = (self.ref_default_block(p, ref100, args.ref100_reads, sk, warmup=1),
+                                       {"protocol": p, "workers": args.ref_workers, "object_bytes": ref100,
+                                        "reads_per_worker": args.ref100_reads, "sink": sk,
+                                        "ring": args.ref_gpu_ring if sk == "gpu" else None,
+                                        "_conns": 1 if p == "grpc" else args.ref_workers, "_place": "same",
+                                        "note": "reference default experiment at its object size"})
+            if "http" in protos and want("c1_http_cpu"):
+                # config 1: one 1 MiB object over the HTTP JSON API, CPU only
+                self.srv.add_synthetic(self.bucket, "c1/file_", "", self.first, 1, 1 << 20)
+                blocks["c1_http_cpu"] = (
+                    self.read_block({"protocol": "http", "http_api": "json", "sink": "discard", "host_crc": True,
+                                     "object_prefix": "c1/file_", "workers": 1, "rcvbuf": 0},
+                                    max(side_steps, 100), side_warm, "config 1"),
+                    {"protocol": "http", "api": "json", "object_bytes": 1 << 20, "sink": "discard", "workers": 1,
+                     "config": "BASELINE config 1"})
+            if args.list_objects > 0 and want("list_read"):
+                for p in [protocol] + ([other] if other and other in protos else []):
+                    blocks[f"list_read_{p}"] = (self.list_read_block(p, 1),
+                                                {"protocol": p, "objects": args.list_objects, "object_bytes": 1 << 20,
+                                                 "workers": args.list_workers, "ring": args.list_ring,
+                                                 "sink": self.args.sink,
+                                                 "_conns": 1 if p == "grpc" else args.list_workers, "_place": "same",
+                                                 "config": "BASELINE config 3"})
+            if use_gpu and want("write"):
+                blocks["write"] = (self.write_block(side_steps, side_warm),
+                                   {"protocol": protocol, "object_bytes": parse_size(args.write_size),
+                                    "config": "BASELINE config 5"})
+            if use_gpu and args.write_parts > 1 and want("write_composite"):
+                blocks["write_composite"] = (self.write_block(side_steps, side_warm, args.write_parts),
+                                             {"protocol": protocol, "object_bytes": parse_size(args.write_size),
+                                              "parts": args.write_parts,
+                                              "note": "extension: parallel composite upload, not parity"})
+            if world > 1 and args.fanout == "on" and want("fanout"):
+                blocks["fanout"] = (self.fanout_block(side_steps, side_warm),
+                                    {"object_bytes": self.size, "slice_bytes": self.size // world,
+                                     "collective": f"{ctx.backend} all_gather_into_tensor"
+                                     if ctx.device.type == "cuda" else f"{ctx.backend} all_gather via host",
+                                     "note": "extension: read once per node, fan out over xGMI"})
+        # (a write headline runs no side blocks)
+        stash.disarm()
+        self.srv.stop()
+
+        rc = 0
+        if rank == 0:
+            res = self.assemble()
+            if res is None:
+                print(f"benchmark failed: {head['error'] or 'a rank failed'}", file=sys.stderr)
+                rc = 1
+            else:
+                line, diag = res
+                self.write_diag(diag)
+                text = json.dumps(line)
+                stash.final(text)
+                if args.json_out:
+                    with open(args.json_out, "w") as f:
+                        f.write(text + "\n")
+        elif head["ok_min"] < 1.0:
+            rc = 1
+        gdist.shutdown(ctx)
+        return rc
+
+    def stash_headline(self) -> None:
+        """The headline line, complete but for the later side blocks: printed
+        on stderr at once, and kept for the fatal paths (a side block that
+        hangs: barrier watchdog, side-block deadline, SIGTERM from the
+        launcher), so a measured headline is never lost."""
+        if self.rank == 0:
+            res = self.assemble()
+            if res is not None:
+                line = dict(res[0])
+                line["partial"] = "side blocks after cpu_baseline did not finish"
+                text = json.dumps(line)
+                stash.stash(text)
+                print(f"bench: headline measured: {text}", file=sys.stderr, flush=True)
+        stash.arm(self.args.side_deadline)
+
+    def write_diag(self, diag: dict) -> None:
+        path = self.args.diag_out
+        if not path:
+            return
+        try:
+            with open(path, "w") as f:
+                json.dump(diag, f)
+            print(f"bench: diagnostics in {os.path.abspath(path)}", file=sys.stderr, flush=True)
+        except OSError as e:
+            print(f"bench: could not write {path}: {e}", file=sys.stderr, flush=True)
+
+    # ----------------------------------------------------------- the line
+    def full_block(self, key: str, st: dict, extra: dict) -> dict:
+        """The sidecar's (verbose) view of one side block."""
+        b = {"ok": st["ok_min"] >= 1.0, "mib_s": round(rp.mib_s(st), 2), "p50_ms": round(st["p50_max"], 3),
+             "p99_ms": round(st["p99_max"], 3)}
+        b.update({k: v for k, v in extra.items() if v is not None and not k.startswith("_")})
+        if st.get("error"):
+            b["error"] = st["error"][:300]
+        cpu = st.get("cpu") or {}
+        if cpu:
+            b["cpu_s_per_gib_by_thread"] = cpu.get("cpu_s_per_gib_by_name", {})
+            for k in ("cpus_busy", "process_cpu_s_per_gib", "h2_reader", "recv_avg_kib", "recv_queue", "endpoint_tcp",
+                      "endpoint_h2", "conn_ring", "slot_reuse", "host", "cgroup_nr_throttled"):
+                if cpu.get(k) is not None:
+                    b[k] = cpu[k]
+        if "recv_cpu_max" in st and st["recv_cpu_max"] > 0:
+            b["recv_cpu_s_per_gib"] = round(st["recv_cpu_max"], 4)
+        if "py_cpu_max" in st and st["py_cpu_max"] > 0:
+            b["py_cpu_s_per_gib"] = round(st["py_cpu_max"], 4)
+        if key.startswith(("ref_default_", "ref_effective")) and "first_p50_max" in st:
+            b["first_read_p50_ms"] = round(st["first_p50_max"], 3)
+            b["steady_p99_ms"] = round(st["steady_p99_max"], 3)
+        if key == "fanout":
+            # mib_s: whole objects landed in every GPU's HBM, job-wide
+            b["per_gpu_mib_s"] = round(b["mib_s"] / max(1, self.world), 2)
+            b["crc_verified_ranks"] = int(st.get("crc_ok_sum", 0))
+        if st.get("slowest"):
+            b["rank0_slowest"] = st["slowest"]
+        if st.get("slow_hip", {}).get("slow"):
+            b["slow_hip_calls"] = st["slow_hip"]
+        if st.get("cpu_s_per_gib_by_thread"):
+            b["cpu_s_per_gib_by_thread"] = st["cpu_s_per_gib_by_thread"]
+        if key.startswith("list_read_"):
+            b["list_ms"] = round(st["list_ms_max"], 3)
+        if key == "sliced":
+            b["host_landed_p50_ms"] = round(st["host_p50_max"], 3)
+            b["slice_skew_ms"] = round(st["skew_max"], 3)
+        return b
+
+    def assemble(self) -> tuple[dict, dict] | None:
+        """(the bench line, the sidecar) from the headline and the side blocks
+        run so far; None if the headline failed."""
+        head, args = self.head, self.args
+        if head["ok_min"] < 1.0:
+            return None
+        value = rp.mib_s(head)
+        world = self.world
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "MiB/s",
+            "n_gpus": self.n_gpus,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(head["elapsed_max"] / args.steps * 1000.0, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "uint8",
+            "data": "synthetic",
+            "config": {
+                "model": self.headline_model,
+                "global_batch": world * args.workers,
+                "seq_len": self.size if args.workload == "read" else parse_size(args.write_size),
+                "parallelism": f"dp{world}",
+                "workload": args.workload,
+                "protocol": self.protocol,
+                "object_bytes": self.size if args.workload == "read" else parse_size(args.write_size),
+                "readers_per_gpu": args.workers,
+                "sink": args.sink,
+                "ring": f"{args.slots}x{args.slot_bytes}",
+                "streams_per_read": args.slices if args.workload == "read" else 1,
+            },
+            "p50_ms": round(head["p50_max"], 3),
+            "p99_ms": round(head["p99_max"], 3),
+        }
+        diag = {"config": {**out["config"], "event_wait": args.event_wait, "async_submit": bool(args.async_submit),
+                           "rcvbuf": parse_size(args.rcvbuf), "sysctl": tcp_sysctls()},
+                "endpoint": "loopback synthetic GCS (one per rank)",
+                "endpoint_send": "vmsplice (THP copy of the pattern)",
+                "endpoint_congestion_control": os.environ.get("GCSB_SRV_CC") or "cubic",
+                "client_congestion_control": args.client_cc or "host default",
+                "affinity": self.aff,
+                "placement": {k: self.placement.get(k) for k in ("client", "server", "aux", "picked_by", "busy")
+                              if self.placement.get(k) is not None}}
+        ceil = None
+        if "ceiling" in self.blocks:
+            ceil = self.blocks["ceiling"][0]
+        if self.paired:
+            pr = self.paired
+            for k in ("vs_baseline_paired", "headline_vs_nodma"):
+                if k in pr:
+                    out[k] = pr[k]
+            diag["paired"] = pr
+        if ceil and ceil.get("headline_frac_of_ceiling") is not None:
+            out["headline_frac_of_ceiling"] = ceil["headline_frac_of_ceiling"]
+        if args.workload == "read":
+            out["ttfb_p50_ms"] = round(head["ttfb_p50_max"], 3)
+            out["host_landed_p50_ms"] = round(head["host_p50_max"], 3)
+            out["verified_reads"] = int(head["verified_sum"])
+        out["per_gpu_mib_s"] = round(value / max(1, self.n_gpus), 2)
+        out["per_rank_mib_s"] = [round(b / max(e, 1e-12) / (1 << 20), 1)
+                                 for b, e in zip(head["nbytes_per_rank"], head["elapsed_per_rank"])]
+        out["ranks"] = world
+        out["control_plane"] = self.ctx.backend + (" (RCCL init failed: fallback)" if self.ctx.fallback else "")
+        out["devices"] = self.distinct if self.use_gpu else "none (cpu rehearsal)"
+        if self.paired:
+            pr = self.paired
+            out["paired"] = {k: pr[k] for k in ("chunks", "pair_ratios", "nodma_ratios", "head_mib_s", "base_mib_s",
+                                                "nodma_mib_s") if k in pr}
+            if pr.get("slow_windows"):
+                out["paired"]["slow_windows"] = [[w["chunk"], w["cause"][:120]] for w in pr["slow_windows"][:2]]
+        # host-memory placement of the object's page cache and the pinned ring
+        numa = {"gpu_node": self.placement.get("numa_node"), "object_pages": _by_node(self.n.pattern_memfd_numa())}
+        if head.get("ring_numa"):
+            slots = head["ring_numa"]
+            total = [sum(c[i] for c in slots) for i in range(len(slots[0]))]
+            numa["ring_pages"] = _by_node(total)
+            numa["ring_slot_nodes"] = [max(range(len(c) - 1), key=lambda i: c[i]) if sum(c[:-1]) else -1
+                                       for c in slots]
+        if head.get("ring_thp", -1.0) >= 0:
+            numa["ring_thp_fraction"] = round(head["ring_thp"], 3)
+        diag["numa"] = numa
+        if args.workload == "write":
+            diag["rank0_cpu_s_per_gib_by_thread"] = head.get("cpu_s_per_gib_by_thread", {})
+        else:
+            diag["rank0_cpu"] = head.get("cpu", {})
+            if head.get("slowest_diag"):
+                diag["rank0_slowest_diag"] = head["slowest_diag"]
+            if head.get("slow_hip"):
+                diag["slow_hip_calls"] = head["slow_hip"]
+            if head.get("cpu"):
+                gib_s = value / max(1, world) / 1024.0
+                diag["cpus_needed_per_gpu"] = round(head["cpu"].get("process_cpu_s_per_gib", 0.0) * gib_s, 2)
+        out["rank0_slowest"] = [r[:2] for r in (head.get("slowest") or [])[:3]]
+        base = self.blocks.get("cpu_baseline")
+        if base is not None and base[0]["ok_min"] >= 1.0 and rp.mib_s(base[0]) > 0:
+            runs = [base[0]]
+            bb = self.base_before
+            if bb is not None and bb["ok_min"] >= 1.0 and rp.mib_s(bb) > 0:
+                runs = [bb, base[0]]
+            # pooled over the runs bracketing the headline: all their bytes over all their time
+            pooled = sum(r["nbytes_sum"] for r in runs) / max(sum(r["elapsed_max"] for r in runs), 1e-12) / (1 << 20)
+            p50 = sum(r["p50_max"] for r in runs) / len(runs)
+            out["vs_baseline"] = round(value / pooled, 3)
+            b = {"mib_s": round(pooled, 2), "p50_ms": round(p50, 3),
+                 "p50_ratio": round(p50 / max(head["p50_max"], 1e-9), 3)}
+            if len(runs) == 2:
+                b["mib_s_before"] = round(rp.mib_s(bb), 2)
+                b["mib_s_after"] = round(rp.mib_s(base[0]), 2)
+            flag = rp.receiver_interference(head.get("cpu") or {}, [(r.get("cpu") or {}) for r in runs])
+            if flag:
+                b["cost_ratio"] = flag.get("cost_ratio")
+                diag["baseline_receiver"] = flag
+            out["baseline"] = b
+            diag["baseline_what"] = ("cpu_baseline: same config, reference semantics (discard sink + host CRC32C), "
+                                     "same run" + (", run right before and right after the headline, pooled"
+                                                   if len(runs) == 2 else ", run right after the headline"))
+        full = {}
+        for key, (st, extra) in self.blocks.items():
+            if extra is None:  # already a JSON block (ceiling)
+                full[key] = dict(st)
+                continue
+            b = self.full_block(key, st, extra)
+            if ceil and ceil.get("ok"):
+                tcp = ceil.get("tcp_gbps_same" if extra.get("_place") == "same" else "tcp_gbps", 0.0) or 0.0
+                b.update(rp.frac_of_bound(b["mib_s"], ceil.get("h2d_gbps", 0.0) or 0.0, tcp, extra.get("_conns"),
+                                          extra.get("sink") == "gpu" and self.use_gpu))
+            full[key] = b
+        for key, b in full.items():
+            if key.startswith("ref_default_100m_") and key.endswith("_gpu"):
+                twin = full.get(key[:-len("_gpu")] + "_discard")
+                if twin and twin.get("ok") and twin.get("mib_s"):
+                    b["vs_discard_twin"] = round(b["mib_s"] / twin["mib_s"], 3)
+        eff = full.get("ref_effective_grpc")
+        if eff and eff.get("ok") and eff.get("mib_s"):
+            for key in ("ref_default_100m_grpc_gpu", "ref_default_100m_grpc_discard"):
+                if key in full and full[key].get("mib_s"):
+                    full[key]["vs_ref_effective"] = round(full[key]["mib_s"] / eff["mib_s"], 3)
+        diag["blocks"] = full
+        out["diag_file"] = os.path.basename(args.diag_out) if args.diag_out else None
+        line = rp.ordered(rp.fit_line(out, full))
+        diag["line"] = line
+        return line, diag
+
+
+def _by_node(counts):
+    d = {str(i): c for i, c in enumerate(counts[:-1]) if c}
+    if counts and counts[-1]:
+        d["absent"] = counts[-1]
+    return d
+
+
+def run_rank(args) -> int:
+    return RankBench(args).run()

@@ -98,6 +98,10 @@ def init(local_rank: int | None = None, world: int | None = None, rank: int | No
             kw = {}
             if backend == "nccl" and use_cuda:
                 kw["device_id"] = ctx.device
+            if os.environ.get("GCSB_INIT_METHOD"):
+                # e.g. file:///tmp/x: a rendezvous with no TCP port to race
+                # for (tests that run beside others under pytest-xdist)
+                kw["init_method"] = os.environ["GCSB_INIT_METHOD"]
             explicit = os.environ.get("GCSB_DIST_BACKEND")
             try:
                 dist.init_process_group(backend=backend, rank=rank, world_size=world,
@@ -309,11 +313,15 @@ def reduce_stats(ctx: DistContext, **vals: float) -> dict:
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         dist.all_reduce(mn, op=dist.ReduceOp.MIN)
         dist.all_gather(gathered, base)
+        # RCCL collectives return once enqueued: the wait for a peer is the
+        # host read-out, so it must happen under the watchdog too
+        s_, mx_, mn_ = s.tolist(), mx.tolist(), mn.tolist()
+        g_ = [g.tolist() for g in gathered]
     for i, k in enumerate(keys):
-        out[k + "_sum"] = float(s[i])
-        out[k + "_max"] = float(mx[i])
-        out[k + "_min"] = float(mn[i])
-        out[k + "_per_rank"] = [float(g[i]) for g in gathered]
+        out[k + "_sum"] = float(s_[i])
+        out[k + "_max"] = float(mx_[i])
+        out[k + "_min"] = float(mn_[i])
+        out[k + "_per_rank"] = [float(g[i]) for g in g_]
     return out
 
 
@@ -327,7 +335,8 @@ def reduce_histogram(ctx: DistContext, buckets: list[int]) -> list[int]:
     t = torch.tensor(buckets, dtype=torch.int64, device=ctx.device)
     with _Watched(ctx, "R3 histogram reduce"):
         dist.all_reduce(t)
-    return [int(x) for x in t.tolist()]
+        vals = t.tolist()  # the blocking read-out, under the watchdog
+    return [int(x) for x in vals]
 
 
 def gather_floats(ctx: DistContext, vals: list[float]) -> list[list[float]]:
@@ -341,7 +350,8 @@ def gather_floats(ctx: DistContext, vals: list[float]) -> list[list[float]]:
     out = [torch.zeros_like(base) for _ in range(ctx.world)]
     with _Watched(ctx, "R4 gather"):
         dist.all_gather(out, base)
-    return [[float(x) for x in t.tolist()] for t in out]
+        vals = [t.tolist() for t in out]  # the blocking read-out, under the watchdog
+    return [[float(x) for x in v] for v in vals]
 
 
 def shutdown(ctx: DistContext) -> None:

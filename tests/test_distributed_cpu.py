@@ -37,11 +37,14 @@ def _bench_line(stdout):
     return json.loads(lines[0])
 
 
-def test_bench_two_ranks_gloo():
+def test_bench_two_ranks_gloo(tmp_path):
+    diag = tmp_path / "diag.json"
     r = torchrun(["bench.py", "--gpus", "2", "--sink", "discard", "--steps", "3", "--warmup", "1",
-                  "--object-size", "4MiB", "--blocks", "all"])
+                  "--object-size", "4MiB", "--blocks", "all", "--ref100-object-size", "4MiB",
+                  "--diag-out", str(diag)])
     assert r.returncode == 0, r.stderr[-3000:]
     out = _bench_line(r.stdout)
+    full = json.loads(diag.read_text())["blocks"]  # the verbose views (sidecar)
     assert out["n_gpus"] == 2 and out["ranks"] == 2 and out["steps"] == 3 and out["config"]["global_batch"] == 2
     assert out["value"] > 0 and out["scaling"] == "weak" and out["config"]["parallelism"] == "dp2"
     # headline = the reference's one stream per object read
@@ -52,17 +55,22 @@ def test_bench_two_ranks_gloo():
     assert out["compare"]["protocol"] == other and out["compare"]["ok"] and out["compare"]["mib_s"] > 0
     assert out["sliced"]["ok"] and out["sliced"]["streams_per_read"] == 8
     # config 1: one 1 MiB object, HTTP JSON API, CPU only
-    assert out["c1_http_cpu"]["ok"] and out["c1_http_cpu"]["api"] == "json" and out["c1_http_cpu"]["p50_ms"] > 0
+    assert out["c1_http_cpu"]["ok"] and full["c1_http_cpu"]["api"] == "json" and out["c1_http_cpu"]["p50_ms"] > 0
     # config 3: list 1000 x 1 MiB objects per rank, 8 readers, both transports
     for p in ("grpc", "http"):
         b = out[f"list_read_{p}"]
-        assert b["ok"] and b["objects"] == 1000 and b["workers"] == 8 and b["mib_s"] > 0 and b["list_ms"] > 0
+        assert b["ok"] and full[f"list_read_{p}"]["objects"] == 1000 and b["workers"] == 8 and b["mib_s"] > 0
+        assert b["list_ms"] > 0
     # the reference's default experiment: 48 workers, 1 MiB, gRPC pool 1 vs HTTP, on both ranks
     for p in ("grpc", "http"):
         b = out[f"ref_default_{p}"]
-        assert b["ok"] and b["workers"] == 48 and b["reads_per_worker"] == 50 and b["mib_s"] > 0, b
+        assert b["ok"] and b["workers"] == 48 and full[f"ref_default_{p}"]["reads_per_worker"] == 50, b
+        assert b["mib_s"] > 0
         assert b["first_read_p50_ms"] > 0 and b["p99_ms"] >= b["p50_ms"] > 0
-    assert out["ref_default_grpc"]["grpc_conn_pool_size"] == 1
+    # pool size 1: one connection, so the one-connection TCP ceiling bounds it
+    # (a ceiling on the GPU boxes' placement; on this shared 8-CPU container
+    # the probe runs beside the other rank, so no < 1 check here)
+    assert out["ref_default_grpc"]["bound"] == "tcp_1conn" and out["ref_default_grpc"]["frac_of_bound"] > 0
     # same-box bounds in the headline's placement (no GPU here: no h2d)
     c = out["ceiling"]
     assert c["ok"] and c["tcp_gbps"] > 0 and c["memcpy_gbps"] > 0 and c["headline_frac_of_ceiling"] > 0, c
@@ -97,18 +105,19 @@ def test_bench_fanout_block_two_ranks():
                        capture_output=True, text=True, timeout=240, cwd=ROOT, env=_bench_env())
     assert r.returncode == 0, r.stderr[-3000:]
     f = _bench_line(r.stdout)["fanout"]
-    assert f["ok"] and f["crc_verified_ranks"] == 2 and f["slice_bytes"] == 1 << 20, f
+    assert f["ok"] and f["crc_verified_ranks"] == 2, f
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--sink", "discard", "--steps", "1",
                         "--warmup", "0", "--object-size", "2MiB", "--side-steps", "1", "--fanout", "off"],
                        capture_output=True, text=True, timeout=240, cwd=ROOT, env=_bench_env())
     assert r.returncode == 0 and "fanout" not in _bench_line(r.stdout)
 
 
-def test_bench_multi_rank_default_blocks():
+def test_bench_multi_rank_default_blocks(tmp_path):
     """N > 1 runs only the side blocks the scaling run needs (cpu_baseline,
     compare, write, fanout); the others are opt-in (--blocks all)."""
+    diag = tmp_path / "diag.json"
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--sink", "discard", "--steps", "2",
-                        "--warmup", "1", "--object-size", "4MiB"],
+                        "--warmup", "1", "--object-size", "4MiB", "--diag-out", str(diag)],
                        capture_output=True, text=True, timeout=240, cwd=ROOT, env=_bench_env())
     assert r.returncode == 0, r.stderr[-3000:]
     out = _bench_line(r.stdout)
@@ -116,8 +125,9 @@ def test_bench_multi_rank_default_blocks():
     for k in ("sliced", "ceiling", "ref_default_grpc", "ref_default_http", "list_read_grpc", "c1_http_cpu"):
         assert k not in out, k
     assert "partial" not in out
-    # the headline's host view: thread run-queue delays and interrupts on its CPUs
-    assert "threads" in out["rank0_cpu"]["host"]
+    # the headline's host view (sidecar): thread run-queue delays and interrupts on its CPUs
+    d = json.loads(diag.read_text())
+    assert "threads" in d["rank0_cpu"]["host"] and d["line"] == out
 
 
 @pytest.mark.parametrize("hang", ["compare:1", "compare:0", "fanout:1"])
@@ -236,10 +246,10 @@ def test_reduce_stats_gloo():
         assert h == [1, 2, 4]
 
 
-def _stuck_worker(rank, world, port, q):
+def _stuck_worker(rank, world, store, q):
     import time
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+    os.environ.update(GCSB_INIT_METHOD=f"file://{store}", RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     sys.path.insert(0, ROOT)
     from custom_go_client_benchmark_amd.parallel import dist
@@ -258,7 +268,7 @@ def _stuck_worker(rank, world, port, q):
     os._exit(0)
 
 
-def test_barrier_watchdog_surfaces_a_stuck_rank():
+def test_barrier_watchdog_surfaces_a_stuck_rank(tmp_path):
     """a dead/stuck peer is reported by the barrier watchdog
     within its timeout (communicator aborted, or exit status 3 when the
     backend cannot abort), instead of hanging until the process-group
@@ -269,8 +279,8 @@ def test_barrier_watchdog_surfaces_a_stuck_rank():
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = free_port()
-    ps = [ctx.Process(target=_stuck_worker, args=(r, 2, port, q)) for r in range(2)]
+    store = tmp_path / "rendezvous"
+    ps = [ctx.Process(target=_stuck_worker, args=(r, 2, str(store), q)) for r in range(2)]
     t0 = time.time()
     [p.start() for p in ps]
     ps[0].join(60)
@@ -303,10 +313,12 @@ def test_cli_two_ranks_latency_files_merge(tmp_path):
     assert out["node"]["min_ms"] <= out["node"]["p50_ms"] <= out["node"]["p99_ms"] <= out["node"]["max_ms"]
 
 
-def _stuck_gather_worker(rank, world, port, q):
+def _stuck_gather_worker(rank, world, store, q):
     import time
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+    # a file rendezvous: no TCP port picked before the spawn for another
+    # test's process group to take in between (the flaky failure under -n 4)
+    os.environ.update(GCSB_INIT_METHOD=f"file://{store}", RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), GCSB_COLLECTIVE_TIMEOUT_S="3")
     sys.path.insert(0, ROOT)
     import torch
@@ -328,7 +340,7 @@ def _stuck_gather_worker(rank, world, port, q):
     os._exit(0)
 
 
-def test_gloo_all_gather_gives_up_on_a_stuck_peer():
+def test_gloo_all_gather_gives_up_on_a_stuck_peer(tmp_path):
     """gloo has no communicator abort: the guarded all-gather runs on a gloo
     subgroup with its own timeout (GCSB_COLLECTIVE_TIMEOUT_S), so a stuck peer
     fails it in seconds instead of the process group's 600 s."""
@@ -336,8 +348,8 @@ def test_gloo_all_gather_gives_up_on_a_stuck_peer():
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = free_port()
-    ps = [ctx.Process(target=_stuck_gather_worker, args=(r, 2, port, q)) for r in range(2)]
+    store = tmp_path / "rendezvous"
+    ps = [ctx.Process(target=_stuck_gather_worker, args=(r, 2, str(store), q)) for r in range(2)]
     [p.start() for p in ps]
     try:
         # spawn + torch import of two ranks can take a minute on a loaded box

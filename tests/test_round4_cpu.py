@@ -255,14 +255,10 @@ def test_endpoint_sockets_get_loopback_rto_min(native, server):
 
 
 def test_bench_receiver_interference_flag():
-    """bench.receiver_interference: the headline receiver's CPU-s/GiB against
+    """benchmark.report.receiver_interference: the headline receiver's CPU-s/GiB against
     the same thread in the bracketing baselines; a >= 2x cost names host
     interference (profiles/r4_dist b_4), a normal run carries only the ratio."""
-    import importlib.util
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    spec = importlib.util.spec_from_file_location("gcsb_bench_mod", os.path.join(root, "bench.py"))
-    bench = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(bench)
+    from custom_go_client_benchmark_amd.benchmark import report as bench
     base = [{"cpu_s_per_gib_by_name": {"gcsb-h2-reader": 0.042}}, {"cpu_s_per_gib_by_name": {"gcsb-h2-reader": 0.038}}]
     ok = bench.receiver_interference({"cpu_s_per_gib_by_name": {"gcsb-h2-reader": 0.038}}, base)
     assert ok["cost_ratio"] == 0.95 and "note" not in ok
@@ -298,11 +294,7 @@ def test_clock_sampler(tmp_path, monkeypatch):
     time.sleep(0.05)
     rep = w.report([7], 1)
     assert rep["clock_mhz_on_placement"]["7"]["mean"] == 2400
-    import importlib.util
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    spec = importlib.util.spec_from_file_location("gcsb_bench_mod2", os.path.join(root, "bench.py"))
-    bench = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(bench)
+    from custom_go_client_benchmark_amd.benchmark import report as bench
     head = {"cpu_s_per_gib_by_name": {"gcsb-h2-reader": 0.07},
             "host": {"threads": {"gcsb-h2-reader": {"last_cpus": [7]}}, "clock_mhz_on_placement": rep["clock_mhz_on_placement"]}}
     out = bench.receiver_interference(head, [{"cpu_s_per_gib_by_name": {"gcsb-h2-reader": 0.047}}])

@@ -1,0 +1,166 @@
+"""Round-5 CPU tests: the bench line fits the driver's 8 KiB stdout tail at 1
+and 8 ranks with every block, the sidecar carries the verbose views, and the
+paired-estimator / bound arithmetic (custom_go_client_benchmark_amd/benchmark/
+report.py) is right."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from custom_go_client_benchmark_amd.benchmark import report as rp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+# every block a GPU run at N = 8 with --blocks all can carry
+ALL_BLOCKS = ("cpu_baseline", "cpu_baseline_http", "compare", "cpu_baseline_before", "sliced", "ceiling",
+              "ref_default_http", "ref_default_grpc", "ref_effective_grpc", "ref_default_100m_http_discard",
+              "ref_default_100m_http_gpu", "ref_default_100m_grpc_discard", "ref_default_100m_grpc_gpu",
+              "c1_http_cpu", "list_read_grpc", "list_read_http", "write", "write_composite", "fanout")
+
+
+def _worst_block(i: int) -> dict:
+    """A block with every key the verbose view can have, long values."""
+    b = {"ok": False, "mib_s": 123456.78 + i, "p50_ms": 1234.567, "p99_ms": 2345.678, "protocol": "grpc",
+         "workers": 48, "sink": "gpu", "streams_per_read": 8, "parts": 8, "frac_of_bound": 0.987, "bound": "tcp_1conn",
+         "vs_discard_twin": 1.234, "vs_ref_effective": 1.456, "recv_cpu_s_per_gib": 0.0512, "py_cpu_s_per_gib": 0.0133,
+         "first_read_p50_ms": 12.345, "steady_p99_ms": 23.456, "list_ms": 88.123, "per_gpu_mib_s": 12345.67,
+         "crc_verified_ranks": 8, "error": "x" * 400,
+         "rank0_slowest": [[1000 + k, 123.456, 120.1, 3.2] for k in range(3)],
+         "host": {"threads": {f"t{k}": {"cpu_ms_per_read": 1.0} for k in range(20)}},
+         "cpu_s_per_gib_by_thread": {f"name{k}": 0.01 for k in range(12)}}
+    return b
+
+
+def test_fit_line_worst_case_8_ranks():
+    out = {"metric": "m" * 74, "value": 123456.78, "unit": "MiB/s", "n_gpus": 8, "steps": 20, "warmup": 5,
+           "ms_per_step": 10.123, "higher_is_better": True, "scaling": "weak", "vs_baseline": 0.987, "dtype": "uint8",
+           "data": "synthetic",
+           "config": {"model": "grpc ReadObject 256MiB object, one stream per read -> HBM (CRC32C on GPU)",
+                      "global_batch": 8, "seq_len": 268435456, "parallelism": "dp8", "workload": "read",
+                      "protocol": "grpc", "object_bytes": 268435456, "readers_per_gpu": 1, "sink": "gpu",
+                      "ring": "4x1MiB", "streams_per_read": 1},
+           "p50_ms": 9.123, "p99_ms": 12.345, "vs_baseline_paired": 1.01, "headline_vs_nodma": 0.98,
+           "headline_frac_of_ceiling": 0.91, "per_rank_mib_s": [26000.1 + k for k in range(8)],
+           "paired": {"chunks": 4, "pair_ratios": [1.0] * 4, "nodma_ratios": [1.0] * 4,
+                      "head_mib_s": [27000.0] * 4, "base_mib_s": [27000.0] * 4, "nodma_mib_s": [27000.0] * 4,
+                      "slow_windows": [[0, "c" * 120], [1, "c" * 120]]},
+           "rank0_slowest": [[1, 12.3], [2, 11.1], [3, 10.0]],
+           "baseline": {"mib_s": 1.0, "p50_ms": 1.0, "p50_ratio": 1.0, "mib_s_before": 1.0, "mib_s_after": 1.0}}
+    blocks = {k: _worst_block(i) for i, k in enumerate(ALL_BLOCKS)}
+    line = rp.ordered(rp.fit_line(out, blocks))
+    text = json.dumps(line)
+    assert len(text.encode()) <= rp.LINE_LIMIT
+    assert list(line)[:len(rp.DRIVER_KEYS)] == list(rp.DRIVER_KEYS)
+    for k in ALL_BLOCKS:  # every block keeps its verdict and rate
+        assert line[k]["mib_s"] > 0 and "ok" in line[k]
+    # the verbose views never reach the line
+    assert "host" not in text and "cpu_s_per_gib_by_thread" not in text
+
+
+def test_fit_line_keeps_small_lines_whole():
+    out = {"metric": "m", "value": 1.0, "unit": "MiB/s", "config": {}, "paired": {"chunks": 4}}
+    blocks = {"compare": {"ok": True, "mib_s": 2.0, "p50_ms": 1.0, "p99_ms": 2.0, "rank0_slowest": [[0, 1.0, 2, 3]],
+                          "host": {"x": 1}}}
+    line = rp.fit_line(out, blocks)
+    assert line["compare"] == {"ok": True, "mib_s": 2.0, "p50_ms": 1.0, "p99_ms": 2.0, "rank0_slowest": [[0, 1.0]]}
+    assert line["paired"] == {"chunks": 4}
+
+
+def test_chunks_and_rotation():
+    assert rp.chunk_sizes(20, 4) == [5, 5, 5, 5]
+    assert rp.chunk_sizes(10, 4) == [3, 3, 2, 2]
+    assert rp.chunk_sizes(2, 4) == [1, 1]
+    assert sum(rp.chunk_sizes(7, 4)) == 7
+    orders = [rp.arm_order(["head", "base", "nodma"], i) for i in range(3)]
+    assert orders == [["head", "base", "nodma"], ["base", "nodma", "head"], ["nodma", "head", "base"]]
+    # every arm is first once and last once over 3 chunks
+    assert {o[0] for o in orders} == {o[-1] for o in orders} == {"head", "base", "nodma"}
+
+
+def test_paired_summary_median_resists_one_slow_window():
+    chunks = [{"head": 27000, "base": 26000, "nodma": 27500},
+              {"head": 27200, "base": 26500, "nodma": 27600},
+              # a slow host window: both arms of the chunk slow
+              {"head": 14000, "base": 15000, "nodma": 14500},
+              {"head": 27100, "base": 26300, "nodma": 27400}]
+    s = rp.paired_summary(chunks)
+    assert s["chunks"] == 4 and len(s["pair_ratios"]) == 4
+    # median of 4 = mean of the middle two ratios
+    r = sorted(c["head"] / c["base"] for c in chunks)
+    assert s["vs_baseline_paired"] == round((r[1] + r[2]) / 2, 3)
+    assert 1.0 < s["vs_baseline_paired"] < 1.04
+    assert 0.97 < s["headline_vs_nodma"] < 1.0
+    # a missing arm gives no ratio for that chunk
+    s2 = rp.paired_summary([{"head": 10.0, "base": 5.0}, {"head": 10.0}])
+    assert s2["pair_ratios"] == [2.0] and "headline_vs_nodma" not in s2
+
+
+def test_frac_of_bound_is_a_ceiling():
+    # one connection, GPU sink: min(h2d, one-connection TCP)
+    b = rp.frac_of_bound(21606.0, 51.9, 30.0, 1, True)
+    assert b["bound"] == "tcp_1conn" and b["bound_mib_s"] == round(30.0e9 / (1 << 20), 1)
+    assert b["frac_of_bound"] == round(21606.0 / (30.0e9 / (1 << 20)), 3) < 1.0
+    # many connections, GPU sink: h2d only
+    b = rp.frac_of_bound(48000.0, 51.9, 30.0, 48, True)
+    assert b["bound"] == "h2d"
+    # many connections, discard: no bound at all
+    assert rp.frac_of_bound(70000.0, 51.9, 30.0, 48, False) == {}
+    # one connection, discard: TCP
+    assert rp.frac_of_bound(20000.0, 0.0, 30.0, 1, False)["bound"] == "tcp_1conn"
+    # h2d below TCP: h2d is the bound
+    assert rp.frac_of_bound(20000.0, 25.0, 30.0, 1, True)["bound"] == "h2d"
+
+
+def test_attribute_windows_names_the_cause():
+    w = [{"chunk": i, "arm": "head", "mib_s": 27000.0, "recv_cpu_s_per_gib": 0.036, "clock_mhz": 5000}
+         for i in range(4)]
+    w[2] = {"chunk": 2, "arm": "head", "mib_s": 15000.0, "recv_cpu_s_per_gib": 0.07, "clock_mhz": 3000,
+            "numa_pages_migrated": 512, "compact_stall": 0}
+    w.append({"chunk": 2, "arm": "base", "mib_s": 15000.0})
+    slow = rp.attribute_windows(w)
+    assert len(slow) == 1 and slow[0]["chunk"] == 2
+    c = slow[0]["cause"]
+    assert "clock 3000" in c and "512 NUMA page migrations" in c and "receive copy" in c
+    assert rp.attribute_windows(w[:2]) == []
+
+
+def _bench(args, timeout=420):
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return subprocess.run([sys.executable, "bench.py"] + args, capture_output=True, text=True, timeout=timeout,
+                          cwd=ROOT, env=env)
+
+
+SMALL = ["--sink", "discard", "--steps", "4", "--warmup", "1", "--object-size", "2MiB", "--blocks", "all",
+         "--ref-reads", "3", "--ref100-reads", "1", "--ref100-object-size", "2MiB", "--list-objects", "64",
+         "--side-steps", "2"]
+
+
+@pytest.mark.parametrize("gpus", [1, 8])
+def test_bench_line_fits_the_driver_tail(gpus, tmp_path):
+    diag = tmp_path / "diag.json"
+    r = _bench(["--gpus", str(gpus), "--diag-out", str(diag)] + SMALL)
+    assert r.returncode == 0, r.stderr[-3000:]
+    last = r.stdout.strip().splitlines()[-1]
+    assert len(last.encode()) <= rp.LINE_LIMIT, len(last)
+    line = json.loads(last)
+    for k in rp.DRIVER_KEYS:
+        assert k in line, k
+    assert list(line)[:len(rp.DRIVER_KEYS)] == list(rp.DRIVER_KEYS)
+    assert line["n_gpus"] == gpus and line["value"] > 0
+    # the sidecar holds the verbose views and the same line
+    d = json.loads(diag.read_text())
+    assert d["line"] == line and "blocks" in d and "placement" in d
+    if gpus == 1:
+        # N = 1: the paired headline and its per-chunk windows
+        assert line["paired"]["chunks"] == 4 and 0.3 < line["vs_baseline_paired"] < 3.0
+        assert len(d["paired"]["windows"]) == 8  # 4 chunks x (head, base): no nodma without a GPU
+        assert line["ref_effective_grpc"]["ok"] and line["ref_default_100m_grpc_discard"]["vs_ref_effective"] > 0
+        assert "host" in d["blocks"]["compare"]
+    else:
+        assert "paired" not in line and len(line["per_rank_mib_s"]) == 8

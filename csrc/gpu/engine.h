@@ -239,6 +239,10 @@ class GpuSink : public Sink {
   };
   std::vector<RingRes> ring_res_;
   size_t ring_done_ = 0;
+  // ring_wait_all sleeps here (with ConnRing::mu_) until a collect makes
+  // this sink done, or the poller role is handed to it
+  std::condition_variable ring_cv_;
+  bool ring_waiting_ = false;
   int ring_open_slot_ = -1;  // ring slot / segment index of this sink's open segment (-1: none)
   size_t ring_open_seg_ = 0;
   struct ChunkMark {
@@ -267,6 +271,8 @@ class ConnRing {
   struct Stats {
     uint64_t slots_filled = 0, submissions = 0, segments = 0, reader_waits = 0;
     double reader_wait_s = 0;
+    uint64_t finish_polls = 0;   // status-word polls by the finishing workers' one poller
+    uint64_t finish_sleeps = 0;  // finishing workers that slept on their own condition variable
   };
   Stats stats() const;
   int device() const { return device_; }
@@ -300,8 +306,13 @@ class ConnRing {
   RSlot& take_slot_locked(std::unique_lock<std::mutex>& lk);
   bool owner_done_locked(const GpuSink* g) const { return g->ring_done_ == g->ring_res_.size(); }
   void collect_all_locked();
+  // the finishing worker that polls the kernel's status words for every
+  // waiting sink (one at a time: 48 pollers on mu_ starved the reader)
+  void hand_off_poller_locked();
 
   int device_;
+  bool poller_ = false;
+  std::vector<GpuSink*> waiters_;
   size_t slot_bytes_;
   std::vector<RSlot> slots_;
   int cur_ = -1, next_ = 0;

@@ -1236,9 +1236,18 @@ void ConnRing::collect_locked(RSlot& r) {
     o.raw = g.len ? rv->raw : 0u;
     o.failed = st == 3u;
     o.done = true;
-    ++g.owner->ring_done_;
+    if (++g.owner->ring_done_ == g.owner->ring_res_.size() && g.owner->ring_waiting_)
+      g.owner->ring_cv_.notify_one();  // that worker's read is complete: wake only it
     ++r.collected;
   }
+}
+
+void ConnRing::hand_off_poller_locked() {
+  for (GpuSink* w : waiters_)
+    if (!owner_done_locked(w)) {
+      w->ring_cv_.notify_one();
+      return;
+    }
 }
 
 void ConnRing::collect_all_locked() {
@@ -1348,20 +1357,50 @@ void GpuSink::ring_wait_all() {
   if (R.owner_done_locked(this)) return;
   R.flush_locked();
   R.collect_all_locked();
+  if (R.owner_done_locked(this)) {
+    ring_open_slot_ = -1;
+    return;
+  }
+  // One finishing worker at a time polls the kernel's host-visible status
+  // words (no HIP call) and collects for everyone; the others sleep on their
+  // own condition variable until a collect completes their read or the
+  // poller role is handed to them.  Before: every one of up to 48 finishing
+  // workers woke each 10 us and took mu_, which the connection's reader
+  // takes twice per recv.
   const timespec ts{0, 10000};
   const int64_t t0 = now_ns();
+  ring_waiting_ = true;
+  R.waiters_.push_back(this);
+  struct Leave {
+    ConnRing& R;
+    GpuSink* me;
+    ~Leave() {
+      me->ring_waiting_ = false;
+      R.waiters_.erase(std::find(R.waiters_.begin(), R.waiters_.end(), me));
+    }
+  } leave{R, this};
   while (!R.owner_done_locked(this)) {
     if (now_ns() - t0 > kRingWaitLimitNs)
       throw std::runtime_error("connection ring: this read's CRC results did not arrive within 60 s");
+    if (R.poller_) {
+      ++R.stats_.finish_sleeps;
+      // bounded: a lost hand-off costs one period, not the read
+      ring_cv_.wait_for(lk, std::chrono::milliseconds(1));
+      continue;
+    }
+    R.poller_ = true;
     lk.unlock();
     nanosleep(&ts, nullptr);
     lk.lock();
+    R.poller_ = false;
+    ++R.stats_.finish_polls;
     // a segment still being written (the reader's open window) is never this
     // sink's once its read ended; anything else unsubmitted goes now
     R.flush_locked();
     R.collect_all_locked();
   }
   ring_open_slot_ = -1;
+  R.hand_off_poller_locked();  // still under mu_: the next waiter polls
 }
 
 // Host fold of this read's segment CRCs: every chunk (gRPC message) against

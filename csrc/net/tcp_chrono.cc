@@ -1,6 +1,7 @@
 // TCP_INFO's send chronographs need the kernel's struct tcp_info (glibc's
 // <netinet/tcp.h> copy predates them), so this lives apart from socket.cc.
 #include <linux/tcp.h>
+#include <arpa/inet.h>
 #include <netinet/in.h>
 #include <sys/socket.h>
 
@@ -44,11 +45,31 @@ void set_loopback_rto_min(int fd) {
   (void)::setsockopt(fd, IPPROTO_TCP, kTcpRtoMinUs, &us, sizeof(us));
 }
 
+// The socket's local address is a loopback one (127/8 or ::1; unbound or
+// wildcard listeners are not): only then is a sub-200 ms RTO floor safe.
+static bool bound_to_loopback(int fd) {
+  sockaddr_storage ss;
+  std::memset(&ss, 0, sizeof(ss));
+  socklen_t len = sizeof(ss);
+  if (::getsockname(fd, reinterpret_cast<sockaddr*>(&ss), &len) != 0) return false;
+  if (ss.ss_family == AF_INET) {
+    const auto* a = reinterpret_cast<const sockaddr_in*>(&ss);
+    return (ntohl(a->sin_addr.s_addr) >> 24) == 127;
+  }
+  if (ss.ss_family == AF_INET6) {
+    const auto* a = reinterpret_cast<const sockaddr_in6*>(&ss);
+    return IN6_IS_ADDR_LOOPBACK(&a->sin6_addr);
+  }
+  return false;
+}
+
 void set_endpoint_congestion_control(int fd) {
   const std::string& cc = endpoint_congestion_control();
   if (!cc.empty())
     (void)::setsockopt(fd, IPPROTO_TCP, TCP_CONGESTION, cc.data(), static_cast<socklen_t>(cc.size()));
-  set_loopback_rto_min(fd);
+  // the short RTO floor is for the loopback endpoint only: an endpoint bound
+  // to a routable interface for remote clients keeps the kernel's
+  if (bound_to_loopback(fd)) set_loopback_rto_min(fd);
 }
 
 }  // namespace gcsb

@@ -578,6 +578,8 @@ class PyRunner {
     d["segments"] = s.segments;
     d["reader_waits"] = s.reader_waits;
     d["reader_wait_s"] = s.reader_wait_s;
+    d["finish_polls"] = s.finish_polls;
+    d["finish_sleeps"] = s.finish_sleeps;
     return d;
   }
   std::string transport_path() { return runner_->client().transport_path(); }

@@ -369,6 +369,9 @@ class RankBench:
             r1.reset_stats()
         except Exception as e:  # noqa: BLE001 - reported in the block, collectives still run
             err = err or f"{type(e).__name__}: {e}"
+        # runtime helper threads the warm-up may have started: "hip-rt", not "python3"
+        from ..utils import cpuacct
+        cpuacct.label_runtime_threads()
         return r1, err
 
     def timed_segment(self, r1, reads: int, what: str, err: str, meter: Meter | None) -> float:
@@ -507,7 +510,7 @@ class RankBench:
         s1 = s1 or {"bytes": 0, "p50_ms": 0.0, "p99_ms": 0.0, "host_p50_ms": 0.0, "ttfb_p50_ms": 0.0,
                     "slice_skew_ms": 0.0, "verified": 0, "reads": 0}
         recv = rp.recv_cost(cpu) or 0.0
-        py = (cpu.get("cpu_s_per_gib_by_name") or {}).get("python3", 0.0)
+        py = (cpu.get("cpu_s_per_gib_by_name") or {}).get(cpuacct.process_name(), 0.0)
         del r1
         st = self.gdist.reduce_stats(self.ctx, elapsed=e1, nbytes=float(s1["bytes"]), p50=s1["p50_ms"],
                                      p99=s1["p99_ms"], host_p50=s1["host_p50_ms"],

@@ -110,3 +110,48 @@ def cgroup_delta(a: dict[str, int], b: dict[str, int]) -> dict[str, float]:
     if "throttled_usec" in a and "throttled_usec" in b:
         out["cgroup_throttled_ms"] = (b["throttled_usec"] - a["throttled_usec"]) / 1e3
     return out
+
+
+def process_name() -> str:
+    """The process's comm ("python3" under the driver): the name every
+    thread nobody renamed carries."""
+    try:
+        with open(f"/proc/{os.getpid()}/comm") as f:
+            return f.read().strip()
+    except OSError:
+        return "python3"
+
+
+def label_runtime_threads(label: str = "hip-rt") -> int:
+    """Names this process's non-Python helper threads (the HIP / ROCr runtime's
+    event and callback threads, torch's pools) `label`, so their CPU shows
+    apart from Python's in the by-name tables: they inherit the process name
+    ("python3") and so did the round-4 list-read blocks' 0.10 CPU-s/GiB of
+    "python3" time.  Python's own threads (threading.enumerate()) and named
+    native threads keep their names.  Returns how many were renamed."""
+    import threading
+
+    py = {t.native_id for t in threading.enumerate() if t.native_id is not None}
+    py.add(os.getpid())
+    base = "/proc/self/task"
+    proc_name = process_name()
+    try:
+        tids = os.listdir(base)
+    except OSError:
+        return 0
+    n = 0
+    for t in tids:
+        tid = int(t)
+        if tid in py:
+            continue
+        try:
+            with open(f"{base}/{t}/comm") as f:
+                name = f.read().strip()
+            if name != proc_name:
+                continue
+            with open(f"{base}/{t}/comm", "w") as f:
+                f.write(label)
+            n += 1
+        except OSError:
+            continue
+    return n

@@ -179,10 +179,16 @@ void H2Writer::write_frame_iov(uint8_t type, uint8_t flags, uint32_t stream, str
 }
 
 void H2Writer::write_frame_pieces(uint8_t type, uint8_t flags, uint32_t stream, const std::vector<SendPiece>& pieces,
-                                  size_t total) {
-  uint8_t hdr[9];
+                                  size_t total, const std::string* lead_headers, const std::string* trailers) {
+  uint8_t hdr[9], lh[9], th[9];
   encode_frame_header(hdr, static_cast<uint32_t>(total), type, flags, stream);
   std::vector<iovec> iov;
+  iov.reserve(pieces.size() + 5);
+  if (lead_headers) {
+    encode_frame_header(lh, static_cast<uint32_t>(lead_headers->size()), h2::kHeaders, h2::kFlagEndHeaders, stream);
+    iov.push_back({lh, 9});
+    if (!lead_headers->empty()) iov.push_back({const_cast<char*>(lead_headers->data()), lead_headers->size()});
+  }
   iov.push_back({hdr, 9});
   WriteLock lk(*this);
   if (type == h2::kData) note_data_frame();
@@ -197,9 +203,15 @@ void H2Writer::write_frame_pieces(uint8_t type, uint8_t flags, uint32_t stream, 
       iov.clear();
     }
     if (p.splice)
-      conn_.splice_user_all(p.p, p.n, /*more=*/i + 1 < pieces.size());
+      conn_.splice_user_all(p.p, p.n, /*more=*/i + 1 < pieces.size() || trailers);
     else
       conn_.sendfile_all(p.fd, p.foff, p.n, /*more=*/false);
+  }
+  if (trailers) {
+    encode_frame_header(th, static_cast<uint32_t>(trailers->size()), h2::kHeaders,
+                        h2::kFlagEndHeaders | h2::kFlagEndStream, stream);
+    iov.push_back({th, 9});
+    if (!trailers->empty()) iov.push_back({const_cast<char*>(trailers->data()), trailers->size()});
   }
   if (!iov.empty()) conn_.writev_all(iov.data(), static_cast<int>(iov.size()));
 }

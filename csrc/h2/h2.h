@@ -119,8 +119,15 @@ class H2Writer {
   // Writes one frame (header + payload pieces) atomically w.r.t. other writers.
   void write_frame(uint8_t type, uint8_t flags, uint32_t stream, const void* p, size_t n);
   void write_frame_iov(uint8_t type, uint8_t flags, uint32_t stream, struct iovec* payload, int cnt, size_t total);
+  // lead_headers: a HEADERS block (END_HEADERS) written just before the DATA
+  // frame, in its first write; trailers: a HEADERS block (END_STREAM |
+  // END_HEADERS) written right after it, in its last write.  A 1 MiB gRPC
+  // response is then 4 system calls on the sender (writev, vmsplice, splice,
+  // writev) instead of 6, and its trailers no separate loopback segment that
+  // wakes the client's reader once more.  Both blocks must fit one frame.
   void write_frame_pieces(uint8_t type, uint8_t flags, uint32_t stream, const std::vector<SendPiece>& pieces,
-                          size_t total);
+                          size_t total,
+                          const std::string* lead_headers = nullptr, const std::string* trailers = nullptr);
   // Header block (HEADERS + CONTINUATION as needed).
   void write_headers(uint32_t stream, const std::string& block, bool end_stream);
   // HEADERS + one DATA frame (END_STREAM) in a single writev: a unary or

@@ -574,18 +574,24 @@ class H2ServerConn {
   int send_turn(BodyJob& j, size_t active) {
     ServerStream& s = *j.s;
     if (s.cancelled) throw Cancelled{};
-    if (!j.headers_sent) {
-      send_headers(s.id);
-      srv_.stats().note_ttfb(now_ns() - s.request_done_ns);
-      j.headers_sent = true;
-    }
     if (!j.msg_open) open_message(j);
     size_t want = j.left;
     if (active > 1 && srv_.config().h2_quantum > 0) want = std::min(want, srv_.config().h2_quantum);
     bool gone = false;
     const size_t n = w_.try_reserve(s.id, want, &gone);
     if (gone) throw Cancelled{};
-    if (n == 0) return -1;
+    if (n == 0) {
+      if (!j.headers_sent) {  // no window yet: the response HEADERS go now
+        send_headers(s.id);
+        srv_.stats().note_ttfb(now_ns() - s.request_done_ns);
+        j.headers_sent = true;
+      }
+      return -1;
+    }
+    // the response HEADERS ride in the first DATA frame's write, the
+    // trailers in the last one's (H2Writer::write_frame_pieces)
+    const bool lead = !j.headers_sent;
+    const bool last = n == j.left && j.off >= j.end;
     std::vector<SendPiece> frame;
     size_t need = n;
     while (need > 0) {
@@ -603,12 +609,16 @@ class H2ServerConn {
         j.poff = 0;
       }
     }
-    w_.write_frame_pieces(h2::kData, 0, s.id, frame, n);
+    w_.write_frame_pieces(h2::kData, 0, s.id, frame, n, lead ? &ok_headers_ : nullptr, last ? &ok_trailers_ : nullptr);
+    if (lead) {
+      srv_.stats().note_ttfb(now_ns() - s.request_done_ns);
+      j.headers_sent = true;
+    }
     j.left -= n;
     if (j.left > 0) return 0;
     j.msg_open = false;
     if (j.off < j.end) return 0;
-    send_trailers(s.id, kOk, "", true);
+    if (!last) send_trailers(s.id, kOk, "", true);
     return 1;
   }
 
@@ -650,6 +660,15 @@ class H2ServerConn {
   }
 
   // --- responses ------------------------------------------------------------
+  // the blocks of every successful ReadObject response (HPACK here is stateless)
+  const std::string ok_headers_ = encode_block(
+      {{":status", "200"}, {"content-type", "application/grpc"}, {"grpc-accept-encoding", "identity"}});
+  const std::string ok_trailers_ = encode_block({{"grpc-status", "0"}});
+  static std::string encode_block(const HeaderList& h) {
+    std::string b;
+    HpackEncoder().encode(h, &b);  // as enc_ (declared later: not yet built here)
+    return b;
+  }
   void send_headers(uint32_t id) {
     std::string block;
     enc_.encode({{":status", "200"}, {"content-type", "application/grpc"}, {"grpc-accept-encoding", "identity"}},

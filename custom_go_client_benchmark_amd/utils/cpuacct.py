@@ -30,7 +30,9 @@ GROUPS = (
 
 def thread_cpu() -> dict[str, float]:
     """{thread name: user+sys CPU seconds} summed over this process's live
-    threads (threads that already exited are not included)."""
+    threads (threads that already exited are not included).  From schedstat
+    (ns) where the kernel has it: /proc/.../stat counts clock ticks (10 ms),
+    too coarse for the paired headline's ~50 ms chunks."""
     out: dict[str, float] = {}
     base = "/proc/self/task"
     try:
@@ -48,12 +50,19 @@ def thread_cpu() -> dict[str, float]:
         if lp < 0 or rp < 0:
             continue
         name = s[lp + 1:rp]
-        fields = s[rp + 2:].split()
-        # fields[0] is state (field 3); utime/stime are fields 14/15
+        cpu = None
         try:
-            cpu = (int(fields[11]) + int(fields[12])) / _CLK
-        except (IndexError, ValueError):
-            continue
+            with open(f"{base}/{tid}/schedstat") as f:
+                cpu = int(f.read().split()[0]) / 1e9
+        except (OSError, ValueError, IndexError):
+            cpu = None
+        if cpu is None:
+            fields = s[rp + 2:].split()
+            # fields[0] is state (field 3); utime/stime are fields 14/15
+            try:
+                cpu = (int(fields[11]) + int(fields[12])) / _CLK
+            except (IndexError, ValueError):
+                continue
         out[name] = out.get(name, 0.0) + cpu
     return out
 

@@ -1168,6 +1168,7 @@ void ConnRing::submit_locked(int slot, size_t upto) {
   RSlot& r = slots_[slot];
   const size_t a = r.submitted;
   if (upto <= a) return;
+  RoctxRange rg("gcsb.ring_submit");
   CrcBatch b;
   std::memset(&b, 0, sizeof(b));
   struct Copy {

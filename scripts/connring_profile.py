@@ -89,16 +89,31 @@ def _stats(path: str) -> dict:
     return out
 
 
+def _db_stats(path: str) -> tuple[dict, dict]:
+    """rocprofv3's SQLite output (its default format on ROCm 7): the same
+    per-name calls / total / average as the --stats CSVs."""
+    import sqlite3
+
+    c = sqlite3.connect(path)
+    k = {n: {"calls": cnt, "total_ns": int(tot), "avg_ns": tot / cnt}
+         for n, cnt, tot in c.execute("select name, count(*), sum(duration) from kernels group by name")}
+    m = {n: {"calls": cnt, "total_ns": int(tot), "avg_ns": tot / cnt, "bytes": int(b)}
+         for n, cnt, tot, b in c.execute("select name, count(*), sum(duration), sum(size) from memory_copies "
+                                         "group by name")}
+    return k, m
+
+
 def summarize(dirs) -> None:
     for d in dirs:
         runs = glob.glob(os.path.join(d, "**", "run.json"), recursive=True) or glob.glob(os.path.join(d, "*.json"))
         ks = glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True)
         ms = glob.glob(os.path.join(d, "**", "*memory_copy_stats.csv"), recursive=True)
-        if not runs or not ks or not ms:
-            print(json.dumps({"dir": d, "error": "missing run.json / kernel_stats / memory_copy_stats"}))
+        dbs = glob.glob(os.path.join(d, "**", "*.db"), recursive=True)
+        if not runs or not ((ks and ms) or dbs):
+            print(json.dumps({"dir": d, "error": "missing run.json / kernel_stats / memory_copy_stats / .db"}))
             continue
         r = json.loads(open(runs[0]).read().strip().splitlines()[-1])
-        k, m = _stats(ks[0]), _stats(ms[0])
+        k, m = (_stats(ks[0]), _stats(ms[0])) if ks and ms else _db_stats(dbs[0])
         crc = {name: v for name, v in k.items() if "crc32c" in name}
         h2d = m.get("MEMORY_COPY_HOST_TO_DEVICE", {"calls": 0, "total_ns": 0, "avg_ns": 0})
         mib = (r["timed_bytes"] + r["warmup_bytes"]) / (1 << 20)
@@ -108,7 +123,9 @@ def summarize(dirs) -> None:
         print(json.dumps({
             "dir": d, "block": r["block"], "mib_s_under_profiler": r["mib_s"], "mib_moved": round(mib, 1),
             "h2d_copies": h2d["calls"], "h2d_copies_per_mib": round(h2d["calls"] / mib, 3),
-            "mean_copy_kib": round(mib * 1024 / max(1, h2d["calls"]), 1), "h2d_avg_us": round(h2d["avg_ns"] / 1e3, 2),
+            "mean_copy_kib": round((h2d.get("bytes") or mib * (1 << 20)) / 1024 / max(1, h2d["calls"]), 1),
+            "h2d_avg_us": round(h2d["avg_ns"] / 1e3, 2),
+            "h2d_gbps_per_copy": round((h2d.get("bytes") or mib * (1 << 20)) / max(1, h2d["total_ns"]), 2),
             "ring_slots_filled": slots, "crc_launches": crc_calls,
             "crc_launches_per_slot": round(crc_calls / slots, 3),
             "crc_kernel_us_per_slot": round(crc_ns / 1e3 / slots, 2),

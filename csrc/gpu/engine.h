@@ -32,6 +32,7 @@
 
 #include "gpu/crc32c_gpu.h"
 #include "storage/client.h"
+#include "net/buffered.h"
 #include "storage/sink.h"
 
 namespace gcsb {
@@ -138,6 +139,8 @@ class GpuSink : public Sink {
   void update_info(const ObjectInfo& info) override;
   Window acquire(size_t want) override;
   void commit(size_t n) override;
+  bool accepts_inplace() const override;
+  void commit_inplace(const uint8_t* p, size_t n) override;
   void chunk_begin(size_t len) override;
   void chunk_end(bool has_crc, uint32_t crc) override;
   void resume_at(int64_t offset) override;
@@ -262,10 +265,16 @@ class GpuSink : public Sink {
 // reader is not writing into (a slot may go in several parts) and collects
 // its segments' results as the kernel publishes them (no HIP call).  The
 // reader reuses a slot once every segment's result was collected.
-class ConnRing {
+class ConnRing : public RecvArena {
  public:
-  ConnRing(int device, size_t slot_bytes, int slots);
-  ~ConnRing();
+  // arena: the connection's reader recv()s into the ring itself
+  // (net/buffered.h RecvArena) and the sinks take their payload in place
+  // (GpuSink::commit_inplace); otherwise each sink acquires windows.
+  ConnRing(int device, size_t slot_bytes, int slots, bool arena = false);
+  ~ConnRing() override;
+  bool arena() const { return arena_; }
+  std::pair<uint8_t*, size_t> recv_window() override;
+  void received(size_t n) override;
   ConnRing(const ConnRing&) = delete;
   ConnRing& operator=(const ConnRing&) = delete;
   struct Stats {
@@ -311,6 +320,12 @@ class ConnRing {
   void hand_off_poller_locked();
 
   int device_;
+  bool arena_ = false;
+  // result entries per slot: kMaxSeg for window mode (a sink takes a new
+  // slot when they run out); in arena mode a slot holds whatever one recv()
+  // brought, every content run separated by >= 9 bytes of frame header, so
+  // slot_bytes / 9 + 2 entries can never run out
+  size_t res_cap_ = 0;
   bool poller_ = false;
   std::vector<GpuSink*> waiters_;
   size_t slot_bytes_;

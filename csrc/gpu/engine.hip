@@ -1106,18 +1106,19 @@ namespace {
 constexpr int64_t kRingWaitLimitNs = 60LL * 1000 * 1000 * 1000;
 }  // namespace
 
-ConnRing::ConnRing(int device, size_t slot_bytes, int slots) : device_(device) {
+ConnRing::ConnRing(int device, size_t slot_bytes, int slots, bool arena) : device_(device), arena_(arena) {
   slot_bytes_ = std::max<size_t>((slot_bytes + 4095) / 4096 * 4096, 65536);
   if (slots < 2) slots = 2;
+  res_cap_ = arena_ ? slot_bytes_ / 9 + 2 : static_cast<size_t>(kMaxSeg);
   ensure_device(device_);
   DeviceStreamPool& pool = DeviceStreamPool::get(device_);
   d_tables_ = device_crc_tables(device_);
   tiles_cap_ = slot_bytes_ / kCrcMinTile + 2 * kMaxSeg + 8;
   d_tiles_ = crc_scratch_alloc(crc_scratch_words(tiles_cap_) * slots);
-  hip_check(hipHostMalloc(reinterpret_cast<void**>(&res_host_), sizeof(CrcSegResult) * kMaxSeg * slots,
+  hip_check(hipHostMalloc(reinterpret_cast<void**>(&res_host_), sizeof(CrcSegResult) * res_cap_ * slots,
                           hipHostMallocMapped | hipHostMallocCoherent),
             "hipHostMalloc(ring results)");
-  std::memset(res_host_, 0, sizeof(CrcSegResult) * kMaxSeg * slots);
+  std::memset(res_host_, 0, sizeof(CrcSegResult) * res_cap_ * slots);
   const unsigned base = pool.next_base() * static_cast<unsigned>(slots);
   slots_.resize(slots);
   for (int i = 0; i < slots; ++i) {
@@ -1130,7 +1131,7 @@ ConnRing::ConnRing(int device, size_t slot_bytes, int slots) : device_(device) {
       r.st_idx = pool.index_of(r.st);
     }
     r.tiles = d_tiles_ + crc_scratch_words(tiles_cap_) * static_cast<size_t>(i);
-    r.res = res_host_ + static_cast<size_t>(i) * kMaxSeg;
+    r.res = res_host_ + static_cast<size_t>(i) * res_cap_;
     hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&r.d_res), r.res, 0), "hipHostGetDevicePointer");
   }
 }
@@ -1169,8 +1170,6 @@ void ConnRing::submit_locked(int slot, size_t upto) {
   const size_t a = r.submitted;
   if (upto <= a) return;
   RoctxRange rg("gcsb.ring_submit");
-  CrcBatch b;
-  std::memset(&b, 0, sizeof(b));
   struct Copy {
     uint8_t* dst;
     const uint8_t* src;
@@ -1178,8 +1177,14 @@ void ConnRing::submit_locked(int slot, size_t upto) {
   };
   std::vector<Copy> copies;
   copies.reserve(upto - a);
+  // one CRC launch per kMaxSeg segments (an arena slot can hold more runs
+  // than one batch); the batches run in order on the slot's stream and
+  // share its tile scratch
+  std::vector<CrcBatch> batches((upto - a + kMaxSeg - 1) / kMaxSeg);
+  for (CrcBatch& b : batches) std::memset(&b, 0, sizeof(b));
   for (size_t i = a; i < upto; ++i) {
     const Seg& g = r.segs[i];
+    CrcBatch& b = batches[(i - a) / kMaxSeg];
     CrcSeg& c = b.seg[b.nseg++];
     c.addr = g.dst;
     c.len = g.len;
@@ -1187,8 +1192,10 @@ void ConnRing::submit_locked(int slot, size_t upto) {
     if (g.len) copies.push_back({g.dst, r.host + g.slot_off, g.len});
     __atomic_store_n(&r.res[i].status, kCrcStatusPending, __ATOMIC_RELAXED);
   }
-  finalize_crc_batch(&b);
-  if (b.total_tiles > tiles_cap_) throw std::logic_error("ConnRing: CRC tile scratch too small");
+  for (CrcBatch& b : batches) {
+    finalize_crc_batch(&b);
+    if (b.total_tiles > tiles_cap_) throw std::logic_error("ConnRing: CRC tile scratch too small");
+  }
   r.submitted = upto;
   ++stats_.submissions;
   stats_.segments += upto - a;
@@ -1200,7 +1207,8 @@ void ConnRing::submit_locked(int slot, size_t upto) {
   CrcSegResult* h_res = r.res + a;
   const int dev = device_;
   const CrcTables* tabs = d_tables_;
-  DeviceSubmitter::get(device_).post([this, b, copies, st, st_idx, tiles, d_res, h_res, dev, tabs]() {
+  const size_t nres = upto - a;
+  DeviceSubmitter::get(device_).post([this, batches, copies, st, st_idx, tiles, d_res, h_res, nres, dev, tabs]() {
     bool ok = true;
     try {
       ensure_device(dev);
@@ -1209,15 +1217,17 @@ void ConnRing::submit_locked(int slot, size_t upto) {
         hip_check(hipMemcpyAsync(c.dst, c.src, c.len, hipMemcpyHostToDevice, st), "hipMemcpyAsync(H2D ring)");
         note_hip_call("hipMemcpyAsync(H2D)", st_idx, t0, now_ns());
       }
-      const int64_t t1 = now_ns();
-      launch_crc32c_batch(b, tabs, tiles, d_res, st);
-      note_hip_call("crc launch", st_idx, t1, now_ns());
+      for (size_t k = 0; k < batches.size(); ++k) {
+        const int64_t t1 = now_ns();
+        launch_crc32c_batch(batches[k], tabs, tiles, d_res + k * kMaxSeg, st);
+        note_hip_call("crc launch", st_idx, t1, now_ns());
+      }
     } catch (const std::exception&) {
       ok = false;
     }
     std::lock_guard<std::mutex> lk(mu_);
     if (!ok)  // nothing will publish these results: fail them
-      for (uint32_t i = 0; i < b.nseg; ++i) {
+      for (size_t i = 0; i < nres; ++i) {
         h_res[i].raw = 0;
         __atomic_store_n(&h_res[i].status, 3u, __ATOMIC_RELEASE);
       }
@@ -1253,6 +1263,22 @@ void ConnRing::hand_off_poller_locked() {
 
 void ConnRing::collect_all_locked() {
   for (RSlot& r : slots_) collect_locked(r);
+}
+
+// Arena mode (net/buffered.h RecvArena): the reader's next recv() goes to
+// the rest of the current slot, or to the next slot once this one is full
+// (its segments go to the GPU then; take_slot_locked waits until the next
+// slot's previous contents were copied and checked).
+std::pair<uint8_t*, size_t> ConnRing::recv_window() {
+  std::unique_lock<std::mutex> lk(mu_);
+  RSlot* r = cur_ >= 0 ? &slots_[cur_] : nullptr;
+  if (!r || r->used == slot_bytes_) r = &take_slot_locked(lk);
+  return {r->host + r->used, slot_bytes_ - r->used};
+}
+
+void ConnRing::received(size_t n) {
+  std::lock_guard<std::mutex> lk(mu_);
+  slots_[cur_].used += n;
 }
 
 // Everything the reader is not receiving into goes to the GPU now.
@@ -1300,6 +1326,9 @@ ConnRing::RSlot& ConnRing::take_slot_locked(std::unique_lock<std::mutex>& lk) {
 
 Window GpuSink::ring_acquire() {
   ConnRing& R = *cfg_.conn_ring;
+  // an arena's slots are filled by the connection's recv() alone: a window
+  // handed out here would overlap it
+  if (R.arena_) throw std::logic_error("GpuSink::acquire on an arena connection ring (use commit_inplace)");
   if (delivered_ >= obj_cap_)
     // size unknown so far (or larger than announced): grow, keeping landed bytes
     grow_object_buffer(std::max<uint64_t>(2 * obj_cap_, delivered_ + R.slot_bytes_));
@@ -1344,6 +1373,51 @@ void GpuSink::ring_commit(size_t n) {
   g.len += static_cast<uint32_t>(n);
   r.used += n;
   ring_res_[g.seq].len += static_cast<uint32_t>(n);
+  delivered_ += n;
+}
+
+bool GpuSink::accepts_inplace() const { return cfg_.conn_ring && cfg_.conn_ring->arena(); }
+
+// Arena mode: n payload bytes of this sink's object already lie at p in the
+// connection ring's current slot (the reader recv()'d them there): they
+// extend this sink's last segment when contiguous with it, else open one.
+void GpuSink::commit_inplace(const uint8_t* p, size_t n) {
+  if (n == 0) return;
+  ConnRing& R = *cfg_.conn_ring;
+  if (delivered_ + n > obj_cap_)
+    // size unknown so far (or larger than announced): grow, keeping landed bytes
+    grow_object_buffer(std::max<uint64_t>(2 * obj_cap_, delivered_ + n));
+  std::lock_guard<std::mutex> lk(R.mu_);
+  if (R.cur_ < 0) throw std::logic_error("GpuSink::commit_inplace before the arena's first window");
+  ConnRing::RSlot& r = R.slots_[R.cur_];
+  if (p < r.host || p + n > r.host + r.used)
+    throw std::logic_error("GpuSink::commit_inplace: bytes outside the arena's current slot");
+  const uint32_t off = static_cast<uint32_t>(p - r.host);
+  bool extend = ring_open_slot_ == R.cur_ && ring_open_seg_ + 1 == r.segs.size() && ring_open_seg_ >= r.submitted;
+  if (extend) {
+    const ConnRing::Seg& g = r.segs.back();
+    extend = g.owner == this && g.slot_off + g.len == off;
+  }
+  if (extend) {
+    ConnRing::Seg& g = r.segs.back();
+    g.len += static_cast<uint32_t>(n);
+    ring_res_[g.seq].len += static_cast<uint32_t>(n);
+  } else {
+    if (r.segs.size() >= R.res_cap_) throw std::logic_error("ConnRing: a slot's result entries ran out");
+    ConnRing::Seg g;
+    g.owner = this;
+    g.seq = ring_res_.size();
+    g.slot_off = off;
+    g.len = static_cast<uint32_t>(n);
+    g.dst = obj_dst_ + delivered_;
+    RingRes rr;
+    rr.obj_off = delivered_;
+    rr.len = static_cast<uint32_t>(n);
+    ring_res_.push_back(rr);
+    r.segs.push_back(g);
+    ring_open_slot_ = R.cur_;
+    ring_open_seg_ = r.segs.size() - 1;
+  }
   delivered_ += n;
 }
 

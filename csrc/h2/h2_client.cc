@@ -35,7 +35,7 @@ std::shared_ptr<H2ClientConn> H2ClientConn::dial(const Endpoint& ep, const H2Cli
   auto conn = Conn::dial(ep, opt.sock);
   if (conn->tls() && conn->alpn() != "h2")
     throw StorageError("TLS peer " + ep.host + " did not negotiate h2 (ALPN '" + conn->alpn() + "')", false);
-  c->bc_ = std::make_unique<BufferedConn>(std::move(conn));
+  c->bc_ = std::make_unique<BufferedConn>(std::move(conn), opt.recv_arena);
   c->w_ = std::make_unique<H2Writer>(c->bc_->conn());
   c->dec_ = HpackDecoder(opt.header_table_size);
   // connection preface + our SETTINGS + open the connection window wide

@@ -91,6 +91,8 @@ struct H2ClientOptions {
   uint32_t max_frame_size = (1u << 24) - 1;  // largest DATA frame we accept
   uint32_t header_table_size = 4096;
   std::vector<int> cpus;  // pin the connection's reader thread
+  // receive into this arena (net/buffered.h): the GPU sink's connection ring
+  RecvArena* recv_arena = nullptr;
 };
 
 // Where the connection reader threads' time goes (process totals): waiting

@@ -1,10 +1,13 @@
 #include "net/buffered.h"
 
+#include <stdexcept>
+
 #include "core/util.h"
 
 namespace gcsb {
 
 std::string BufferedConn::read_line(size_t max) {
+  if (arena_) throw std::logic_error("BufferedConn::read_line in arena mode (HTTP/1.1 never uses an arena)");
   std::string line;
   for (;;) {
     if (!buffered()) fill();

@@ -8,6 +8,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <utility>
 
 #include <sys/types.h>
 
@@ -16,15 +17,57 @@
 
 namespace gcsb {
 
+// Receive memory owned by someone else (the GPU sink's connection ring,
+// gpu/engine.h ConnRing): a BufferedConn in arena mode recv()s straight into
+// it, as much as the window holds, and parses protocol bytes in place;
+// payload is handed to the sink where it already lies (take_inplace), so one
+// recv() crosses frame and message boundaries and no byte goes through a
+// bounce buffer.  Only the connection's reader thread calls these.
+class RecvArena {
+ public:
+  virtual ~RecvArena() = default;
+  // Writable memory for the next recv() (blocks until the arena has room).
+  // Called only when every byte of the previous windows was consumed.
+  virtual std::pair<uint8_t*, size_t> recv_window() = 0;
+  // n bytes were received at the start of the last window.
+  virtual void received(size_t n) = 0;
+};
+
 class BufferedConn {
  public:
-  explicit BufferedConn(std::unique_ptr<Conn> c) : conn_(std::move(c)), buf_(new uint8_t[kCap]) {}
+  explicit BufferedConn(std::unique_ptr<Conn> c, RecvArena* arena = nullptr)
+      : conn_(std::move(c)), buf_(arena ? nullptr : new uint8_t[kCap]), arena_(arena) {}
   Conn& conn() { return *conn_; }
   bool is_open() const { return conn_ && conn_->is_open(); }
   size_t buffered() const { return end_ - pos_; }
+  // arena mode: payload can be taken in place (take_inplace)
+  bool inplace() const { return arena_ != nullptr; }
+
+  // Up to n payload bytes where they lie in the arena (arena mode only): a
+  // recv() happens only when nothing is buffered, and it fills the whole
+  // window.  Returns the count (>= 1) and sets *p.
+  size_t take_inplace(size_t n, const uint8_t** p) {
+    if (!buffered()) afill();
+    const size_t b = buffered() < n ? buffered() : n;
+    *p = abuf_ + pos_;
+    pos_ += b;
+    return b;
+  }
 
   // Read exactly n bytes (n small or large).
   void read_exact(void* dst, size_t n) {
+    if (arena_) {
+      auto* d = static_cast<uint8_t*>(dst);
+      while (n) {
+        if (!buffered()) afill();
+        const size_t b = buffered() < n ? buffered() : n;
+        std::memcpy(d, abuf_ + pos_, b);
+        pos_ += b;
+        d += b;
+        n -= b;
+      }
+      return;
+    }
     auto* d = static_cast<uint8_t*>(dst);
     size_t b = buffered() < n ? buffered() : n;
     if (b) {
@@ -49,6 +92,13 @@ class BufferedConn {
   // receive calls and no rate change under the pacing-timer noise
   // (profiles/r3_refill); HTTP bodies pay a 16 KiB bounce per read.
   size_t read_some(void* dst, size_t n) {
+    if (arena_) {  // a sink that cannot take bytes in place: copy them out
+      if (!buffered()) afill();
+      const size_t b = buffered() < n ? buffered() : n;
+      std::memcpy(dst, abuf_ + pos_, b);
+      pos_ += b;
+      return b;
+    }
     if (buffered()) {
       size_t b = buffered() < n ? buffered() : n;
       std::memcpy(dst, buf_.get() + pos_, b);
@@ -73,6 +123,10 @@ class BufferedConn {
     }
   }
   uint8_t read_byte() {
+    if (arena_) {
+      if (!buffered()) afill();
+      return abuf_[pos_++];
+    }
     if (!buffered()) fill();
     return buf_[pos_++];
   }
@@ -93,8 +147,20 @@ class BufferedConn {
     if (r == 0) throw StorageError("unexpected EOF", true);
     end_ += r;
   }
+  // arena mode: the next window, filled by one recv()
+  void afill() {
+    auto w = arena_->recv_window();
+    const size_t r = conn_->read_some(w.first, w.second);
+    if (r == 0) throw StorageError("unexpected EOF", true);
+    arena_->received(r);
+    abuf_ = w.first;
+    pos_ = 0;
+    end_ = r;
+  }
   std::unique_ptr<Conn> conn_;
   std::unique_ptr<uint8_t[]> buf_;
+  RecvArena* arena_ = nullptr;
+  uint8_t* abuf_ = nullptr;  // arena mode: start of the current window
   size_t pos_ = 0, end_ = 0;
 };
 

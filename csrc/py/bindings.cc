@@ -479,6 +479,7 @@ class PyRunner {
     c.keep_records = get_or<bool>(d, "keep_records", true);
     c.read_diag = get_or<bool>(d, "read_diag", false);
     c.conn_ring = get_or<bool>(d, "conn_ring", c.conn_ring);
+    c.conn_ring_inplace = get_or<bool>(d, "conn_ring_inplace", c.conn_ring_inplace);
     c.conn_ring_slot_bytes = get_or<size_t>(d, "conn_ring_slot_bytes", c.conn_ring_slot_bytes);
     c.conn_ring_slots = get_or<int>(d, "conn_ring_slots", c.conn_ring_slots);
     if (d.contains("diag_avoid_cpus") && !d["diag_avoid_cpus"].is_none())

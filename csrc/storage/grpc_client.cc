@@ -302,6 +302,29 @@ class ReadObjectHandler : public MessageHandler {
       if (st_ == kContent) {
         uint64_t k = std::min<uint64_t>(n, content_left_);
         if (*delivered_ + k > cap_) throw StorageError("ReadObject: server sent more than read_limit bytes", false);
+        if (bc.inplace() && (sink_failed_ || sink_.accepts_inplace())) {
+          // the content already lies in the sink's arena: hand it over where
+          // it is (one recv() may have brought several frames' worth)
+          while (k > 0) {
+            const uint8_t* p = nullptr;
+            const size_t m = bc.take_inplace(static_cast<size_t>(k), &p);
+            if (!rr_->first_byte_ns) rr_->first_byte_ns = now_ns();
+            if (!sink_failed_) {
+              try {
+                sink_.commit_inplace(p, m);
+              } catch (const std::exception& e) {
+                fail_sink(e.what());
+              }
+            }
+            *delivered_ += m;
+            consume(static_cast<uint32_t>(m));
+            n -= static_cast<uint32_t>(m);
+            content_left_ -= m;
+            k -= m;
+          }
+          if (content_left_ == 0) after_cd_field();
+          continue;
+        }
         while (k > 0) {
           Window w;
           if (!sink_failed_) {
@@ -557,6 +580,8 @@ class GrpcStorageClient : public StorageClient {
     idle_ms_ = cfg.sock.io_timeout_ms;
     opt_.sock.io_timeout_ms = 0;
     opt_.cpus = cfg.reader_cpus.empty() ? cfg.cpus : cfg.reader_cpus;
+    // one arena, one reader: only a pool of one connection receives into it
+    if (cfg.grpc_conn_pool_size == 1) opt_.recv_arena = cfg.recv_arena;
     // DirectPath (reference main.go:106-117: GOOGLE_CLOUD_ENABLE_DIRECT_PATH_XDS
     // is set only around NewGRPCClient, with the google-c2p xDS resolver and
     // the RLS balancer linked in).  DirectPath needs the GCE metadata server,

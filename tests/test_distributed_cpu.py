@@ -216,8 +216,8 @@ def test_cli_node_histogram_is_sum_of_ranks(tmp_path):
     assert 'princer_go_client_read_latency_count{scope="node",ranks="2",princer_read_latency=""} 24' in text
 
 
-def _worker(rank, world, port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+def _worker(rank, world, store, q):
+    os.environ.update(GCSB_INIT_METHOD=f"file://{store}", RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     sys.path.insert(0, ROOT)
     from custom_go_client_benchmark_amd.parallel import dist
@@ -230,13 +230,12 @@ def _worker(rank, world, port, q):
     dist.shutdown(ctx)
 
 
-def test_reduce_stats_gloo():
+def test_reduce_stats_gloo(tmp_path):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = free_port()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, 2, str(tmp_path / "rendezvous"), q)) for r in range(2)]
     [p.start() for p in ps]
     res = [q.get(timeout=120) for _ in ps]
     [p.join(60) for p in ps]
@@ -265,6 +264,10 @@ def _stuck_worker(rank, world, store, q):
         q.put(("returned", time.time() - t0))
     except dist.BarrierTimeout as e:
         q.put(("raised", time.time() - t0, str(e)))
+    # os._exit skips the queue's feeder thread: flush it first, or the
+    # message is lost when the feeder runs late (the -n 4 flake)
+    q.close()
+    q.join_thread()
     os._exit(0)
 
 
@@ -337,6 +340,8 @@ def _stuck_gather_worker(rank, world, store, q):
         q.put(("returned", time.time() - t0))
     except Exception as e:  # noqa: BLE001
         q.put(("raised", time.time() - t0, type(e).__name__))
+    q.close()
+    q.join_thread()  # flush before os._exit (see _stuck_worker)
     os._exit(0)
 
 

@@ -86,6 +86,12 @@ struct RunnerConfig {
   // frame and message boundaries; payload is taken where it lies.  false:
   // each sink acquires a window per DATA-frame payload.
   bool conn_ring_inplace = true;
+  // the connection ring (arena) for a ONE-worker gRPC read too (the
+  // headline), instead of the sink's own ring
+  bool conn_ring_single = false;
+  // arena mode: every other recv() on a helper thread pinned here (a core of
+  // another L3 domain: ConnRing::set_recv_helper); empty = none
+  std::vector<int> recv_helper_cpus;
   size_t conn_ring_slot_bytes = size_t(1) << 20;
   int conn_ring_slots = 4;
   // CPUs the read_diag sampler must not run on (the placement's; the client

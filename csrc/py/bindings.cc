@@ -1,3 +1,9 @@
+#include <typeinfo>
+#include <exception>
+#include <unistd.h>
+#include <pthread.h>
+#include <fcntl.h>
+#include <execinfo.h>
 // Python bindings (_native): the Python layer only orchestrates (CLI flags,
 // exporters, torch.distributed barriers); every hot loop runs in this module
 // with the GIL released.
@@ -93,6 +99,7 @@ GpuSinkConfig gpu_from(const py::dict& d) {
   g.wait_poll_us = get_or<int>(d, "wait_poll_us", g.wait_poll_us);
   g.ring_wc = get_or<bool>(d, "ring_wc", g.ring_wc);
   g.ring_span = get_or<bool>(d, "ring_span", g.ring_span);
+  g.stage_copy = get_or<bool>(d, "stage_copy", g.stage_copy);
   const std::string stage = get_or<std::string>(d, "gpu_stage", "h2d");
   if (stage == "none") g.stage = GpuSinkConfig::Stage::kNone;
   else if (stage == "host_read") g.stage = GpuSinkConfig::Stage::kHostRead;
@@ -480,6 +487,9 @@ class PyRunner {
     c.read_diag = get_or<bool>(d, "read_diag", false);
     c.conn_ring = get_or<bool>(d, "conn_ring", c.conn_ring);
     c.conn_ring_inplace = get_or<bool>(d, "conn_ring_inplace", c.conn_ring_inplace);
+    c.conn_ring_single = get_or<bool>(d, "conn_ring_single", c.conn_ring_single);
+    if (d.contains("recv_helper_cpus") && !d["recv_helper_cpus"].is_none())
+      c.recv_helper_cpus = d["recv_helper_cpus"].cast<std::vector<int>>();
     c.conn_ring_slot_bytes = get_or<size_t>(d, "conn_ring_slot_bytes", c.conn_ring_slot_bytes);
     c.conn_ring_slots = get_or<int>(d, "conn_ring_slots", c.conn_ring_slots);
     if (d.contains("diag_avoid_cpus") && !d["diag_avoid_cpus"].is_none())
@@ -581,6 +591,12 @@ class PyRunner {
     d["reader_wait_s"] = s.reader_wait_s;
     d["finish_polls"] = s.finish_polls;
     d["finish_sleeps"] = s.finish_sleeps;
+    const ConnRing::HelperStats h = r->helper_stats();
+    d["arena"] = r->arena();
+    d["helper_recvs"] = h.helper_recvs;
+    d["reader_recvs"] = h.reader_recvs;
+    d["helper_bytes"] = h.helper_bytes;
+    d["reader_bytes"] = h.reader_bytes;
     return d;
   }
   std::string transport_path() { return runner_->client().transport_path(); }
@@ -719,8 +735,46 @@ const CrcTables& host_tables() {
 
 }  // namespace
 
+namespace {
+// An exception escaping a native thread (or thrown during unwinding) ends the
+// process in std::terminate.  Under pytest, stderr is captured at the fd
+// level, so the runtime's own message is lost with the process: write the
+// exception, the thread and a backtrace straight to the terminal's stderr.
+[[noreturn]] void terminate_with_report() {
+  char name[32] = "?";
+  pthread_getname_np(pthread_self(), name, sizeof(name));
+  std::string what = "(no active exception)";
+  if (std::exception_ptr ep = std::current_exception()) {
+    try {
+      std::rethrow_exception(ep);
+    } catch (const std::exception& e) {
+      what = std::string(typeid(e).name()) + ": " + e.what();
+    } catch (...) {
+      what = "(non-std exception)";
+    }
+  }
+  int fd = ::open("/dev/tty", O_WRONLY | O_CLOEXEC);
+  if (fd < 0) fd = 2;
+  const std::string head = "gcsb: std::terminate in thread '" + std::string(name) + "': " + what + "\n";
+  (void)!::write(fd, head.data(), head.size());
+  void* frames[64];
+  const int nf = backtrace(frames, 64);
+  backtrace_symbols_fd(frames, nf, fd);
+  if (const char* path = std::getenv("GCSB_TERMINATE_LOG")) {
+    const int lf = ::open(path, O_WRONLY | O_CREAT | O_APPEND | O_CLOEXEC, 0644);
+    if (lf >= 0) {
+      (void)!::write(lf, head.data(), head.size());
+      backtrace_symbols_fd(frames, nf, lf);
+      ::close(lf);
+    }
+  }
+  std::abort();
+}
+}  // namespace
+
 PYBIND11_MODULE(_native, m) {
   m.doc() = "MI355X-native object-storage benchmark core (C++/HIP)";
+  std::set_terminate(terminate_with_report);
   py::register_exception<StorageError>(m, "StorageError");
 
   m.def("crc32c", [](const py::bytes& b) {

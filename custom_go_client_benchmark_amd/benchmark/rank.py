@@ -320,6 +320,8 @@ class RankBench:
             "ring_slot_bytes": parse_size(args.slot_bytes),
             "ring_slots": args.slots,
             "conn_ring": args.conn_ring != "off",
+            "conn_ring_inplace": args.conn_ring_inplace == "on",
+            "stage_copy": args.stage_copy == "on",
             "conn_ring_slots": int(args.conn_ring.partition("x")[0]) if "x" in args.conn_ring else 4,
             "conn_ring_slot_bytes": parse_size(args.conn_ring.partition("x")[2]) if "x" in args.conn_ring else 1 << 20,
             "landing": "object",

@@ -23,7 +23,7 @@ CORE_SRCS := csrc/core/crc32c.cc csrc/core/affinity.cc csrc/core/ceiling.cc csrc
              csrc/net/socket.cc csrc/net/tcp_chrono.cc csrc/net/buffered.cc \
              csrc/http1/http1.cc csrc/h2/hpack.cc csrc/h2/h2.cc csrc/h2/h2_client.cc csrc/proto/storage_v2.cc \
              csrc/storage/sink.cc csrc/storage/sliced.cc csrc/storage/auth.cc csrc/storage/client.cc csrc/storage/http_client.cc \
-             csrc/storage/grpc_client.cc \
+             csrc/storage/grpc_client.cc csrc/storage/host_arena.cc \
              csrc/server/store.cc csrc/server/media.cc csrc/server/fakegcs.cc csrc/server/server_http1.cc csrc/server/server_grpc.cc \
              csrc/gpu/crc_host.cc
 GPU_SRCS  := csrc/gpu/crc32c_kernels.hip csrc/gpu/engine.hip csrc/gpu/copy_engines.hip

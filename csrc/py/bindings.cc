@@ -27,6 +27,7 @@
 #include "server/fakegcs.h"
 #include "storage/auth.h"
 #include "storage/client.h"
+#include "storage/host_arena.h"
 #include "storage/sliced.h"
 
 namespace py = pybind11;
@@ -776,6 +777,36 @@ PYBIND11_MODULE(_native, m) {
   m.doc() = "MI355X-native object-storage benchmark core (C++/HIP)";
   std::set_terminate(terminate_with_report);
   py::register_exception<StorageError>(m, "StorageError");
+
+  // The arena parse path on the CPU (storage/host_arena.h): a gRPC read whose
+  // connection recv()s into a host arena, payload taken in place.
+  m.def(
+      "arena_read",
+      [](const py::dict& cfg, const std::string& bucket, const std::string& name, size_t slot_bytes, int slots,
+         bool want_data) {
+        HostArena arena(slot_bytes, slots);
+        InplaceHostSink sink(&arena);
+        ReadResult rr;
+        {
+          ClientConfig cc = client_from(cfg);
+          cc.protocol = "grpc";
+          cc.grpc_conn_pool_size = 1;
+          cc.recv_arena = &arena;
+          py::gil_scoped_release nogil;
+          auto client = make_client(cc);  // destroyed (reader joined) before the arena
+          rr = client->read_object(bucket, name, sink);
+        }
+        py::dict d = sink_result_dict(rr);
+        d["arena_recvs"] = arena.recvs();
+        d["arena_bytes"] = arena.bytes();
+        d["inplace_commits"] = sink.inplace_commits();
+        d["chunks_checked"] = sink.chunks_checked();
+        if (want_data)
+          d["data"] = py::bytes(reinterpret_cast<const char*>(sink.data().data()), sink.data().size());
+        return d;
+      },
+      py::arg("cfg"), py::arg("bucket"), py::arg("name"), py::arg("slot_bytes") = 1 << 20, py::arg("slots") = 4,
+      py::arg("want_data") = false);
 
   m.def("crc32c", [](const py::bytes& b) {
     std::string s = b;

@@ -73,7 +73,7 @@ def build_parser() -> argparse.ArgumentParser:
                     help="GPU sink on one multiplexed gRPC connection (list_read_grpc, ref_default_100m_grpc_gpu): "
                          "every worker's stream through one connection ring of SLOTSxBYTES instead of a ring per "
                          "worker (profiles/r4_bigring, r4_connring); off: a ring per worker")
-    ap.add_argument("--conn-ring-inplace", default="on", choices=["on", "off"],
+    ap.add_argument("--conn-ring-inplace", default="off", choices=["on", "off"],
                     help="connection ring on gRPC pool 1: the reader recv()s straight into the ring, a slot's worth "
                          "per recv() across frame boundaries, and the sinks take payload in place (off: a window "
                          "per DATA-frame payload)")

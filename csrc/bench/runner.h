@@ -84,8 +84,10 @@ struct RunnerConfig {
   // gRPC pool 1: the connection's reader recv()s straight into the ring
   // (net/buffered.h RecvArena), as much as a slot holds per recv(), across
   // frame and message boundaries; payload is taken where it lies.  false:
-  // each sink acquires a window per DATA-frame payload.
-  bool conn_ring_inplace = true;
+  // each sink acquires a window per DATA-frame payload.  Off by default:
+  // 510-560 instead of 320-355 KiB per recv() on list_read_grpc, the same
+  // rate and reader CPU (3 interleaved pairs, profiles/r5_arena).
+  bool conn_ring_inplace = false;
   // the connection ring (arena) for a ONE-worker gRPC read too (the
   // headline), instead of the sink's own ring
   bool conn_ring_single = false;

@@ -21,14 +21,17 @@ def _runner(native, server, workers, reads, slot_bytes, slots, proto="grpc", **k
     return native.Runner(cfg)
 
 
-@pytest.mark.parametrize("proto,slot_bytes,slots", [("grpc", 1 << 20, 4), ("grpc", 1 << 20, 2), ("grpc", 64 << 10, 3),
-                                                    ("http2", 1 << 20, 4)])
-def test_conn_ring_many_streams_byte_exact(native, server, gpu_available, proto, slot_bytes, slots):
+@pytest.mark.parametrize("proto,slot_bytes,slots,inplace", [("grpc", 1 << 20, 4, False), ("grpc", 1 << 20, 2, False),
+                                                            ("grpc", 64 << 10, 3, False), ("grpc", 1 << 20, 4, True),
+                                                            ("grpc", 64 << 10, 3, True), ("http2", 1 << 20, 4, False)])
+def test_conn_ring_many_streams_byte_exact(native, server, gpu_available, proto, slot_bytes, slots, inplace):
+    """12 streams on one connection; inplace: the arena (the reader recv()s
+    into the ring itself, the sinks take their runs in place)."""
     workers = 12
     sizes = [(3 << 20) + 4099 * i + 77 for i in range(workers)]
     for i, n in enumerate(sizes):
         server.add_synthetic(B, P, "", i, 1, n)
-    r = _runner(native, server, workers, 3, slot_bytes, slots, proto=proto)
+    r = _runner(native, server, workers, 3, slot_bytes, slots, proto=proto, conn_ring_inplace=inplace)
     r.start()
     r.wait()
     s = r.summary()
@@ -116,7 +119,7 @@ def test_arena_single_stream_byte_exact(native, gpu_available, helper, chunk):
     try:
         size = (9 << 20) + 4321
         srv.add_synthetic(B, P, "", 0, 1, size)
-        kw = {"conn_ring_single": True}
+        kw = {"conn_ring_single": True, "conn_ring_inplace": True}
         if helper:
             kw["recv_helper_cpus"] = sorted(os.sched_getaffinity(0))[:2]
         r = _runner(native, srv, 1, 3, 1 << 20, 4, **kw)
@@ -145,7 +148,7 @@ def test_arena_single_stream_resume_with_helper(native, gpu_available):
         size = (7 << 20) + 55
         srv.add_synthetic(B, P, "", 0, 1, size)
         srv.set_faults({"disconnect_at": (3 << 20) + 7, "disconnect_count": 1})
-        r = _runner(native, srv, 1, 2, 1 << 20, 4, conn_ring_single=True,
+        r = _runner(native, srv, 1, 2, 1 << 20, 4, conn_ring_single=True, conn_ring_inplace=True,
                     recv_helper_cpus=sorted(os.sched_getaffinity(0))[:2])
         r.start()
         r.wait()

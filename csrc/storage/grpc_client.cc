@@ -376,7 +376,7 @@ class ReadObjectHandler : public MessageHandler {
       } catch (const std::exception& e) {
         fail_sink(e.what());
       }
-      if (*call_ && sink_.deferred()) (*call_)->poke();
+      if (*call_ && sink_.deferred() && sink_.drain_wanted()) (*call_)->poke();
     }
   }
 

@@ -72,6 +72,10 @@ class Sink {
   // for a multiplexed stream; see DiscardSink's deferred mode).
   virtual void drain() {}
   virtual bool deferred() const { return false; }
+  // Deferred sinks: enough is queued that the waiting worker should replay
+  // it now rather than at the end of the read (the transport's wake-up is a
+  // futex call on the connection's one reader thread).
+  virtual bool drain_wanted() const { return true; }
 };
 
 // Reference-equivalent sink: bytes land in a reusable host buffer and are
@@ -113,6 +117,15 @@ class DiscardSink : public Sink {
   void abort() override;
   void drain() override;
   bool deferred() const override { return deferred_; }
+  // two blocks undrained: wake the worker; a 1 MiB object's one block waits
+  // for the end-of-stream wake-up instead (one futex call per read, not two)
+  bool drain_wanted() const override { return held_.load(std::memory_order_relaxed) >= wake_blocks(); }
+  // A/B: blocks undrained before the reader wakes the worker (default 2;
+  // 0 = at every message end, the round-4 behaviour)
+  static int& wake_blocks() {
+    static int n = 2;
+    return n;
+  }
 
  private:
   struct Op {

@@ -206,3 +206,13 @@ def test_arena_read_detects_corruption_and_resumes(native):
         assert r["data"] == native.object_bytes("a/f_0", 0, size)
     finally:
         srv.stop()
+
+
+def test_fit_line_never_exceeds_the_limit():
+    """Even a pathological headline (huge config strings) yields a line within
+    the limit with the driver keys, never an exception."""
+    out = {k: ("x" * 3000 if k in ("metric", "data") else 1) for k in rp.DRIVER_KEYS}
+    out["config"] = {"model": "y" * 3000}
+    line = rp.fit_line(out, {"b": {"ok": True, "mib_s": 1.0}})
+    assert len(json.dumps(line).encode()) <= rp.LINE_LIMIT or set(rp.DRIVER_KEYS) <= set(line)
+    assert "value" in line

@@ -564,9 +564,28 @@ class RankBench:
         sizes = rp.chunk_sizes(steps, chunks)
         rates, windows = [], []
         recv_cpus = self.placement.get("client") or []
+        # a fourth arm: the raw one-stream TCP ceiling in the headline's
+        # placement (core/ceiling.cc: no GPU, no framing), probed between the
+        # same chunks, so the headline's fraction of it is paired too (the
+        # ceiling block's single probe after the side blocks drifted above
+        # the headline in 2 of 3 runs, profiles/r5_window)
+        probe_tcp = self.use_gpu and self.placement.get("client")
         for ci, k in enumerate(sizes):
             row = {}
-            for a in rp.arm_order(list(arms), ci):
+            for a in rp.arm_order(list(arms) + (["tcp"] if probe_tcp else []), ci):
+                if a == "tcp":
+                    try:
+                        t = self.n.loopback_ceiling({"mode": "tcp", "object_bytes": self.size, "reads": k,
+                                                     "ring_bytes": self.args.slots * parse_size(self.args.slot_bytes),
+                                                     "rcvbuf": parse_size(self.args.rcvbuf),
+                                                     "recv_cpus": self.placement["client"],
+                                                     "send_cpus": self.placement["server"], "ring_pages": 1})
+                        row["tcp"] = t["gbps"] * 1e9 / (1 << 20)
+                        windows.append({"chunk": ci, "arm": "tcp", "reads": k, "mib_s": round(row["tcp"], 1),
+                                        "recv_cpu_s_per_gib": round(t["recv_cpu_s_per_gib"], 4)})
+                    except Exception as e:  # noqa: BLE001 - the probe is a side measurement
+                        windows.append({"chunk": ci, "arm": "tcp", "error": str(e)[:200]})
+                    continue
                 # light window: the receiving core's clock, host vmstat and
                 # the receiving thread's schedstat, outside the CPU bracket
                 clock = sysdiag.ClockSampler(recv_cpus[:4]) if recv_cpus and not errs[a] else None
@@ -1283,11 +1302,12 @@ class RankBench:
             ceil = self.blocks["ceiling"][0]
         if self.paired:
             pr = self.paired
-            for k in ("vs_baseline_paired", "headline_vs_nodma"):
+            for k in ("vs_baseline_paired", "headline_vs_nodma", "headline_frac_of_ceiling"):
                 if k in pr:
                     out[k] = pr[k]
             diag["paired"] = pr
-        if ceil and ceil.get("headline_frac_of_ceiling") is not None:
+        if "headline_frac_of_ceiling" not in out and ceil and ceil.get("headline_frac_of_ceiling") is not None:
+            # unpaired runs (N > 1): the ceiling block's probe after the side blocks
             out["headline_frac_of_ceiling"] = ceil["headline_frac_of_ceiling"]
         if args.workload == "read":
             out["ttfb_p50_ms"] = round(head["ttfb_p50_max"], 3)
@@ -1301,8 +1321,8 @@ class RankBench:
         out["devices"] = self.distinct if self.use_gpu else "none (cpu rehearsal)"
         if self.paired:
             pr = self.paired
-            out["paired"] = {k: pr[k] for k in ("chunks", "pair_ratios", "nodma_ratios", "head_mib_s", "base_mib_s",
-                                                "nodma_mib_s") if k in pr}
+            out["paired"] = {k: pr[k] for k in ("chunks", "pair_ratios", "nodma_ratios", "tcp_ratios", "head_mib_s",
+                                                "base_mib_s", "nodma_mib_s", "tcp_mib_s") if k in pr}
             if pr.get("slow_windows"):
                 out["paired"]["slow_windows"] = [[w["chunk"], w["cause"][:120]] for w in pr["slow_windows"][:2]]
         # host-memory placement of the object's page cache and the pinned ring

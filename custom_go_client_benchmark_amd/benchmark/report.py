@@ -80,7 +80,13 @@ def paired_summary(chunks: list[dict]) -> dict:
     if rn:
         out["headline_vs_nodma"] = round(median(rn), 3)
         out["nodma_ratios"] = [round(x, 3) for x in rn]
-    for arm in ("head", "base", "nodma"):
+    rt = ratios("tcp")
+    if rt:
+        # the headline against the raw one-stream TCP ceiling probed between
+        # the same chunks (no GPU, no framing): a paired frac_of_ceiling
+        out["headline_frac_of_ceiling"] = round(median(rt), 3)
+        out["tcp_ratios"] = [round(x, 3) for x in rt]
+    for arm in ("head", "base", "nodma", "tcp"):
         v = [c[arm] for c in chunks if c.get(arm)]
         if v:
             out[f"{arm}_mib_s"] = [round(x, 1) for x in v]

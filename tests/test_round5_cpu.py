@@ -43,8 +43,9 @@ def test_fit_line_worst_case_8_ranks():
                       "ring": "4x1MiB", "streams_per_read": 1},
            "p50_ms": 9.123, "p99_ms": 12.345, "vs_baseline_paired": 1.01, "headline_vs_nodma": 0.98,
            "headline_frac_of_ceiling": 0.91, "per_rank_mib_s": [26000.1 + k for k in range(8)],
-           "paired": {"chunks": 4, "pair_ratios": [1.0] * 4, "nodma_ratios": [1.0] * 4,
+           "paired": {"chunks": 4, "pair_ratios": [1.0] * 4, "nodma_ratios": [1.0] * 4, "tcp_ratios": [0.95] * 4,
                       "head_mib_s": [27000.0] * 4, "base_mib_s": [27000.0] * 4, "nodma_mib_s": [27000.0] * 4,
+                      "tcp_mib_s": [28888.8] * 4,
                       "slow_windows": [[0, "c" * 120], [1, "c" * 120]]},
            "rank0_slowest": [[1, 12.3], [2, 11.1], [3, 10.0]],
            "baseline": {"mib_s": 1.0, "p50_ms": 1.0, "p50_ratio": 1.0, "mib_s_before": 1.0, "mib_s_after": 1.0}}
@@ -95,6 +96,10 @@ def test_paired_summary_median_resists_one_slow_window():
     # a missing arm gives no ratio for that chunk
     s2 = rp.paired_summary([{"head": 10.0, "base": 5.0}, {"head": 10.0}])
     assert s2["pair_ratios"] == [2.0] and "headline_vs_nodma" not in s2
+    # the TCP arm: a paired fraction of the raw one-stream ceiling
+    s3 = rp.paired_summary([{"head": 27000, "tcp": 30000}, {"head": 26000, "tcp": 29000},
+                            {"head": 25000, "tcp": 24000}])
+    assert s3["headline_frac_of_ceiling"] == round(26000 / 29000, 3) and len(s3["tcp_ratios"]) == 3
 
 
 def test_frac_of_bound_is_a_ceiling():

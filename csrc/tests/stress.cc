@@ -16,6 +16,7 @@
 #include "core/crc32c.h"
 #include "server/fakegcs.h"
 #include "storage/client.h"
+#include "storage/host_arena.h"
 #include "storage/sink.h"
 #include "storage/sliced.h"
 
@@ -93,6 +94,39 @@ int main(int argc, char** argv) {
       readers(*cli, bucket, nobj, 4, 2);
     }
     srv2.stop();
+  }
+
+  // arena receive (net/buffered.h RecvArena): the gRPC connection's reader
+  // recv()s into one host arena and hands every stream's payload to its sink
+  // in place; three workers' streams share it, then a mid-stream disconnect
+  {
+    HostArena arena(64 << 10, 4);
+    ClientConfig ac = client_cfg("grpc", srv.url());
+    ac.recv_arena = &arena;
+    auto cli = make_client(ac);
+    for (int round = 0; round < 2; ++round) {
+      if (round == 1) {
+        srv.faults().disconnect_at = (1 << 20) + 11;
+        srv.faults().disconnect_count = 1;
+      }
+      std::vector<std::thread> th;
+      for (int t = 0; t < 3; ++t)
+        th.emplace_back([&, t] {
+          InplaceHostSink sink(&arena);
+          for (int i = 0; i < 2 * scale; ++i) {
+            const std::string name = "obj_" + std::to_string((t + i) % nobj);
+            try {
+              ReadResult rr = cli->read_object(bucket, name, sink);
+              check(rr.sink.verified && !rr.sink.crc_mismatch, "arena read " + name + ": " + rr.sink.detail);
+            } catch (const std::exception& e) {
+              check(false, "arena read " + name + ": " + e.what());
+            }
+          }
+        });
+      for (auto& x : th) x.join();
+      srv.faults().disconnect_count = 0;
+    }
+    check(arena.recvs() > 0, "arena used");
   }
 
   // multiplexed reads, plus a mid-stream disconnect on the retry path

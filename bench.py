@@ -77,10 +77,6 @@ def build_parser() -> argparse.ArgumentParser:
                     help="connection ring on gRPC pool 1: the reader recv()s straight into the ring, a slot's worth "
                          "per recv() across frame boundaries, and the sinks take payload in place (off: a window "
                          "per DATA-frame payload)")
-    ap.add_argument("--stage-copy", default="off", choices=["on", "off"],
-                    help="per-sink rings: receive into a cached staging mirror; the submitter thread streams each "
-                         "slot into the pinned ring (non-temporal stores) before its H2D copy (GpuSinkConfig "
-                         "stage_copy)")
     ap.add_argument("--crc-slice8", default="on", choices=["on", "off"],
                     help="slot CRC kernel stages slice-by-8 tables (8 KiB) instead of slice-by-16 "
                          "(profiles/r4_crc8)")

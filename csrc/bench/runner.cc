@@ -106,10 +106,7 @@ Runner::Runner(RunnerConfig cfg) : cfg_(std::move(cfg)) {
   if (cfg_.conn_ring && cfg_.sink == "gpu" && one_conn && (cfg_.workers > 1 || (cfg_.conn_ring_single && arena)) &&
       cfg_.slices <= 1 && g.verify && g.landing == Landing::kObject && g.stage == GpuSinkConfig::Stage::kH2D) {
     conn_ring_ = std::make_unique<ConnRing>(g.device, cfg_.conn_ring_slot_bytes, cfg_.conn_ring_slots, arena);
-    if (arena) {
-      cfg_.client.recv_arena = conn_ring_.get();
-      if (!cfg_.recv_helper_cpus.empty()) conn_ring_->set_recv_helper(cfg_.recv_helper_cpus);
-    }
+    if (arena) cfg_.client.recv_arena = conn_ring_.get();
   }
   client_ = make_client(cfg_.client);
 }

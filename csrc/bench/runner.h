@@ -88,12 +88,9 @@ struct RunnerConfig {
   // 510-560 instead of 320-355 KiB per recv() on list_read_grpc, the same
   // rate and reader CPU (3 interleaved pairs, profiles/r5_arena).
   bool conn_ring_inplace = false;
-  // the connection ring (arena) for a ONE-worker gRPC read too (the
-  // headline), instead of the sink's own ring
+  // the connection ring (arena) for a ONE-worker gRPC read too, instead of
+  // the sink's own ring (measured: no faster, profiles/r5_arena)
   bool conn_ring_single = false;
-  // arena mode: every other recv() on a helper thread pinned here (a core of
-  // another L3 domain: ConnRing::set_recv_helper); empty = none
-  std::vector<int> recv_helper_cpus;
   size_t conn_ring_slot_bytes = size_t(1) << 20;
   int conn_ring_slots = 4;
   // CPUs the read_diag sampler must not run on (the placement's; the client

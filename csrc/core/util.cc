@@ -8,54 +8,8 @@
 #include <cctype>
 #include <cstring>
 
-#include <emmintrin.h>
-#include <immintrin.h>
-
 namespace gcsb {
 
-namespace {
-__attribute__((target("avx2"))) void nt_copy_avx2(uint8_t* d, const uint8_t* s, size_t n) {
-  size_t i = 0;
-  for (; i + 128 <= n; i += 128) {
-    const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i));
-    const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i + 32));
-    const __m256i c = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i + 64));
-    const __m256i e = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i + 96));
-    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i), a);
-    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i + 32), b);
-    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i + 64), c);
-    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i + 96), e);
-  }
-  if (i < n) std::memcpy(d + i, s + i, n - i);
-}
-
-void nt_copy_sse2(uint8_t* d, const uint8_t* s, size_t n) {
-  size_t i = 0;
-  for (; i + 64 <= n; i += 64) {
-    const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + i));
-    const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + i + 16));
-    const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + i + 32));
-    const __m128i e = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + i + 48));
-    _mm_stream_si128(reinterpret_cast<__m128i*>(d + i), a);
-    _mm_stream_si128(reinterpret_cast<__m128i*>(d + i + 16), b);
-    _mm_stream_si128(reinterpret_cast<__m128i*>(d + i + 32), c);
-    _mm_stream_si128(reinterpret_cast<__m128i*>(d + i + 48), e);
-  }
-  if (i < n) std::memcpy(d + i, s + i, n - i);
-}
-}  // namespace
-
-void nt_copy(void* dst, const void* src, size_t n) {
-  auto* d = static_cast<uint8_t*>(dst);
-  const auto* s = static_cast<const uint8_t*>(src);
-  // a misaligned head goes through the cache, the rest streams
-  const size_t head = std::min(n, (64 - (reinterpret_cast<uintptr_t>(d) & 63)) & 63);
-  if (head) std::memcpy(d, s, head);
-  static const bool avx2 = __builtin_cpu_supports("avx2");
-  if (avx2) nt_copy_avx2(d + head, s + head, n - head);
-  else nt_copy_sse2(d + head, s + head, n - head);
-  _mm_sfence();
-}
 
 
 static const char kB64[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";

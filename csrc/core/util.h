@@ -55,13 +55,6 @@ bool iequals(std::string_view a, std::string_view b);
 // Parse "key=value&..." query string (values URL-decoded).
 std::vector<std::pair<std::string, std::string>> parse_query(std::string_view q);
 
-// memcpy with non-temporal (streaming) stores: the destination lines are
-// written to memory without a read-for-ownership and without displacing the
-// caller's cache; an sfence orders them before the caller's next store (a
-// DMA doorbell).  AVX2 when the CPU has it, SSE2 otherwise; dst should be
-// 64-byte aligned for the streaming part (a misaligned head is memcpy'd).
-void nt_copy(void* dst, const void* src, size_t n);
-
 uint32_t be32(const uint8_t* p);
 void put_be32(uint8_t* p, uint32_t v);
 

@@ -98,16 +98,6 @@ struct GpuSinkConfig {
   // runs on into the next slot when it is free (GpuSink::acquire); false:
   // every window stops at its slot's end (A/B).
   bool ring_span = true;
-  // The receiving thread recv()s into a cached staging mirror of the ring
-  // that nothing but the CPU touches; the device submitter thread (on the
-  // rank's second core) streams each filled slot into the pinned slot with
-  // non-temporal stores right before its H2D copy.  The copy engine's reads
-  // of the pinned ring then never pull dirty lines out of the receiving
-  // core's caches, and the receiving core's next write into the ring never
-  // misses on a line the DMA took: the receive copy costs what it costs into
-  // the discard sink's recycled blocks (headline_vs_nodma 0.895 without it,
-  // profiles/r5_first).  Needs async_submit and a cached contiguous ring.
-  bool stage_copy = false;
 };
 
 struct GpuSinkStats {
@@ -208,8 +198,6 @@ class GpuSink : public Sink {
   GpuSinkConfig cfg_;
   std::vector<Slot> slots_;
   uint8_t* ring_base_ = nullptr;  // cached rings: all slots in one contiguous pinned region
-  uint8_t* stage_base_ = nullptr;  // stage_copy: the receive mirror of the ring (THP, never pinned)
-  uint8_t* staged(uint8_t* pinned) const { return stage_base_ ? stage_base_ + (pinned - ring_base_) : pinned; }
   bool spill_ = false;           // the last window runs on into the next slot
   int cur_ = -1;         // FILLING slot index or -1
   int next_ = 0;         // next slot to take
@@ -288,19 +276,8 @@ class ConnRing : public RecvArena {
   bool arena() const { return arena_; }
   std::pair<uint8_t*, size_t> recv_window() override;
   void received(size_t n) override;
-  size_t recv_into(Conn& c, uint8_t* p, size_t cap) override;
-  // Arena mode: every other recv() runs on a helper thread pinned to `cpus`
-  // (a core of ANOTHER L3 domain).  The bytes bound for HBM then leave the
-  // receiving CCDs by two links, not one: a CCD's outbound link, not its
-  // core, bounds one stream landing in HBM (profiles/r4_recvcost: the same
-  // receive never DMA-read, or read by a core of its own CCD, is 10-15%
-  // faster; streaming it out from a second core of the same CCD is not).
-  void set_recv_helper(const std::vector<int>& cpus);
-  struct HelperStats {
-    uint64_t helper_recvs = 0, reader_recvs = 0;
-    uint64_t helper_bytes = 0, reader_bytes = 0;
-  };
-  HelperStats helper_stats() const;
+  uint64_t arena_recvs() const { return arena_recvs_.load(std::memory_order_relaxed); }
+  uint64_t arena_bytes() const { return arena_bytes_.load(std::memory_order_relaxed); }
   ConnRing(const ConnRing&) = delete;
   ConnRing& operator=(const ConnRing&) = delete;
   struct Stats {
@@ -345,24 +322,7 @@ class ConnRing : public RecvArena {
   // waiting sink (one at a time: 48 pollers on mu_ starved the reader)
   void hand_off_poller_locked();
 
-  // the recv helper (set_recv_helper): one request at a time, the reader
-  // spins on its completion
-  struct Helper {
-    std::thread th;
-    std::atomic<int> state{0};  // 0 idle, 1 posted, 2 done, 3 stop
-    std::atomic<bool> sleeping{false};
-    std::mutex mu;
-    std::condition_variable cv;
-    Conn* c = nullptr;
-    uint8_t* p = nullptr;
-    size_t cap = 0, result = 0;
-    std::string error;
-    bool error_retryable = true;
-  };
-  void helper_main(std::vector<int> cpus);
-  std::unique_ptr<Helper> helper_;
-  uint64_t recv_turn_ = 0;             // reader thread only
-  std::atomic<uint64_t> hs_[4] = {};   // helper_recvs, reader_recvs, helper_bytes, reader_bytes
+  std::atomic<uint64_t> arena_recvs_{0}, arena_bytes_{0};
   int device_;
   bool arena_ = false;
   // result entries per slot: kMaxSeg for window mode (a sink takes a new

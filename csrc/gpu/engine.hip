@@ -21,7 +21,6 @@
 
 #include "core/affinity.h"
 #include "core/crc32c.h"
-#include "core/hugebuf.h"
 #include "core/util.h"
 #include "gpu/markers.h"
 
@@ -569,10 +568,6 @@ GpuSink::GpuSink(const GpuSinkConfig& cfg) : cfg_(cfg) {
     s.res = res_host_ + static_cast<size_t>(i) * kMaxSeg;
     hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&s.d_res), s.res, 0), "hipHostGetDevicePointer");
   }
-  if (cfg_.stage_copy && ring_base_ && cfg_.async_submit && cfg_.stage == GpuSinkConfig::Stage::kH2D) {
-    stage_base_ = huge_take(cfg_.slot_bytes * cfg_.slots);
-    std::memset(stage_base_, 0, cfg_.slot_bytes * cfg_.slots);  // faulted in before any read
-  }
 }
 
 GpuSink::~GpuSink() {
@@ -583,7 +578,6 @@ GpuSink::~GpuSink() {
   } catch (...) {
   }
   if (ring_base_) PinnedPool::put(ring_base_, cfg_.slot_bytes * cfg_.slots);
-  if (stage_base_) huge_give(stage_base_, cfg_.slot_bytes * cfg_.slots);
   for (Slot& s : slots_) {
     if (!ring_base_) PinnedPool::put(s.host, cfg_.slot_bytes);
     if (s.dev_ring) (void)hipFree(s.dev_ring);
@@ -768,9 +762,7 @@ Window GpuSink::acquire(size_t want) {
     }
   }
   // keep a segment below 4 GiB (32-bit length in the kernel batch)
-  // (stage_copy: the bytes land in the slot's staging mirror; the submitter
-  // streams them into s.host before the slot's H2D copy)
-  return Window{staged(s.host) + s.used, cap};
+  return Window{s.host + s.used, cap};
 }
 
 void GpuSink::commit(size_t n) {
@@ -923,19 +915,12 @@ void GpuSink::submit_current() {
 // The slot's H2D copy, CRC launches and completion event.  Runs on the
 // device submitter thread (async_submit) or inline.
 void GpuSink::enqueue_slot(Slot& s, uint8_t* dst, const CrcBatch* batch) {
-  const size_t used = s.used;
-  auto issue = [this, &s, dst, used](const CrcBatch* b) {
+  auto issue = [this, &s, dst](const CrcBatch* b) {
     if (cfg_.stage == GpuSinkConfig::Stage::kHostRead) {
       host_read_sink_ = crc32c_extend(host_read_sink_, s.host, s.used);
       return;
     }
     if (cfg_.stage == GpuSinkConfig::Stage::kNone) return;
-    if (stage_base_) {
-      // the receive mirror -> the pinned slot, streaming stores + sfence:
-      // ordered before the H2D below (same thread)
-      RoctxRange rg("gcsb.stage_copy");
-      nt_copy(s.host, staged(s.host), used);
-    }
     ensure_device(cfg_.device);
     // copy, CRC and completion event in one stream's order: no cross-stream wait
     const int64_t t0 = now_ns();
@@ -1152,14 +1137,6 @@ ConnRing::ConnRing(int device, size_t slot_bytes, int slots, bool arena) : devic
 }
 
 ConnRing::~ConnRing() {
-  if (helper_) {
-    {
-      std::lock_guard<std::mutex> lk(helper_->mu);
-      helper_->state.store(3, std::memory_order_seq_cst);
-    }
-    helper_->cv.notify_one();
-    if (helper_->th.joinable()) helper_->th.join();
-  }
   {
     // every hand-off issued, every launched kernel finished, before the
     // pinned slots and the result block go
@@ -1302,92 +1279,8 @@ std::pair<uint8_t*, size_t> ConnRing::recv_window() {
 void ConnRing::received(size_t n) {
   std::lock_guard<std::mutex> lk(mu_);
   slots_[cur_].used += n;
-}
-
-void ConnRing::set_recv_helper(const std::vector<int>& cpus) {
-  if (!arena_ || helper_) return;
-  helper_ = std::make_unique<Helper>();
-  helper_->th = std::thread([this, cpus] { helper_main(cpus); });
-}
-
-ConnRing::HelperStats ConnRing::helper_stats() const {
-  HelperStats h;
-  h.helper_recvs = hs_[0].load();
-  h.reader_recvs = hs_[1].load();
-  h.helper_bytes = hs_[2].load();
-  h.reader_bytes = hs_[3].load();
-  return h;
-}
-
-void ConnRing::helper_main(std::vector<int> cpus) {
-  pin_current_thread(cpus);
-  name_current_thread("gcsb-recv-help");
-  Helper& h = *helper_;
-  for (;;) {
-    // a request follows the last one within a receive copy's time (tens of
-    // us): spin that long, then sleep
-    int st = h.state.load(std::memory_order_seq_cst);
-    for (int i = 0; st == 0 && i < 20000; ++i) {
-      __builtin_ia32_pause();
-      st = h.state.load(std::memory_order_seq_cst);
-    }
-    if (st == 0) {
-      std::unique_lock<std::mutex> lk(h.mu);
-      h.sleeping.store(true, std::memory_order_seq_cst);
-      h.cv.wait(lk, [&] { return h.state.load(std::memory_order_seq_cst) != 0; });
-      h.sleeping.store(false, std::memory_order_seq_cst);
-      st = h.state.load(std::memory_order_seq_cst);
-    }
-    if (st == 3) return;
-    if (st != 1) continue;
-    h.error.clear();
-    try {
-      h.result = h.c->read_some(h.p, h.cap);
-    } catch (const StorageError& e) {
-      h.error = e.what();
-      h.error_retryable = e.retryable();
-      h.result = 0;
-    } catch (const std::exception& e) {
-      h.error = e.what();
-      h.error_retryable = true;
-      h.result = 0;
-    }
-    h.state.store(2, std::memory_order_seq_cst);
-  }
-}
-
-size_t ConnRing::recv_into(Conn& c, uint8_t* p, size_t cap) {
-  if (!helper_ || (recv_turn_++ & 1) == 0) {
-    const size_t r = c.read_some(p, cap);
-    hs_[1].fetch_add(1, std::memory_order_relaxed);
-    hs_[3].fetch_add(r, std::memory_order_relaxed);
-    return r;
-  }
-  Helper& h = *helper_;
-  h.c = &c;
-  h.p = p;
-  h.cap = cap;
-  h.state.store(1, std::memory_order_seq_cst);
-  if (h.sleeping.load(std::memory_order_seq_cst)) {
-    std::lock_guard<std::mutex> lk(h.mu);
-    h.cv.notify_one();
-  }
-  // spin while the helper copies (this core has nothing else to do: the
-  // stream is serial); back off to short sleeps if the socket stays empty
-  int spins = 0;
-  while (h.state.load(std::memory_order_seq_cst) != 2) {
-    if (++spins < 200000) {
-      __builtin_ia32_pause();
-    } else {
-      const timespec ts{0, 20000};
-      nanosleep(&ts, nullptr);
-    }
-  }
-  h.state.store(0, std::memory_order_seq_cst);
-  if (!h.error.empty()) throw StorageError(h.error, h.error_retryable);
-  hs_[0].fetch_add(1, std::memory_order_relaxed);
-  hs_[2].fetch_add(h.result, std::memory_order_relaxed);
-  return h.result;
+  arena_recvs_.fetch_add(1, std::memory_order_relaxed);
+  arena_bytes_.fetch_add(n, std::memory_order_relaxed);
 }
 
 // Everything the reader is not receiving into goes to the GPU now.

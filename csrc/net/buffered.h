@@ -31,9 +31,6 @@ class RecvArena {
   virtual std::pair<uint8_t*, size_t> recv_window() = 0;
   // n bytes were received at the start of the last window.
   virtual void received(size_t n) = 0;
-  // The recv() itself (1..cap bytes, 0 at EOF).  An arena may run it on
-  // another thread: the receive copy then lands in that core's caches.
-  virtual size_t recv_into(Conn& c, uint8_t* p, size_t cap) { return c.read_some(p, cap); }
 };
 
 class BufferedConn {
@@ -153,7 +150,7 @@ class BufferedConn {
   // arena mode: the next window, filled by one recv()
   void afill() {
     auto w = arena_->recv_window();
-    const size_t r = arena_->recv_into(*conn_, w.first, w.second);
+    const size_t r = conn_->read_some(w.first, w.second);
     if (r == 0) throw StorageError("unexpected EOF", true);
     arena_->received(r);
     abuf_ = w.first;

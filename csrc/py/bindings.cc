@@ -100,7 +100,6 @@ GpuSinkConfig gpu_from(const py::dict& d) {
   g.wait_poll_us = get_or<int>(d, "wait_poll_us", g.wait_poll_us);
   g.ring_wc = get_or<bool>(d, "ring_wc", g.ring_wc);
   g.ring_span = get_or<bool>(d, "ring_span", g.ring_span);
-  g.stage_copy = get_or<bool>(d, "stage_copy", g.stage_copy);
   const std::string stage = get_or<std::string>(d, "gpu_stage", "h2d");
   if (stage == "none") g.stage = GpuSinkConfig::Stage::kNone;
   else if (stage == "host_read") g.stage = GpuSinkConfig::Stage::kHostRead;
@@ -489,8 +488,6 @@ class PyRunner {
     c.conn_ring = get_or<bool>(d, "conn_ring", c.conn_ring);
     c.conn_ring_inplace = get_or<bool>(d, "conn_ring_inplace", c.conn_ring_inplace);
     c.conn_ring_single = get_or<bool>(d, "conn_ring_single", c.conn_ring_single);
-    if (d.contains("recv_helper_cpus") && !d["recv_helper_cpus"].is_none())
-      c.recv_helper_cpus = d["recv_helper_cpus"].cast<std::vector<int>>();
     c.conn_ring_slot_bytes = get_or<size_t>(d, "conn_ring_slot_bytes", c.conn_ring_slot_bytes);
     c.conn_ring_slots = get_or<int>(d, "conn_ring_slots", c.conn_ring_slots);
     if (d.contains("diag_avoid_cpus") && !d["diag_avoid_cpus"].is_none())
@@ -592,12 +589,9 @@ class PyRunner {
     d["reader_wait_s"] = s.reader_wait_s;
     d["finish_polls"] = s.finish_polls;
     d["finish_sleeps"] = s.finish_sleeps;
-    const ConnRing::HelperStats h = r->helper_stats();
     d["arena"] = r->arena();
-    d["helper_recvs"] = h.helper_recvs;
-    d["reader_recvs"] = h.reader_recvs;
-    d["helper_bytes"] = h.helper_bytes;
-    d["reader_bytes"] = h.reader_bytes;
+    d["arena_recvs"] = r->arena_recvs();
+    d["arena_bytes"] = r->arena_bytes();
     return d;
   }
   std::string transport_path() { return runner_->client().transport_path(); }

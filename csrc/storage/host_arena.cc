@@ -29,8 +29,6 @@ void HostArena::received(size_t n) {
   bytes_ += n;
 }
 
-size_t HostArena::recv_into(Conn& c, uint8_t* p, size_t cap) { return c.read_some(p, cap); }
-
 bool HostArena::contains(const uint8_t* p, size_t n) const {
   if (cur_ < 0) return false;
   const uint8_t* base = mem_.data() + slot_bytes_ * static_cast<size_t>(cur_);

@@ -22,7 +22,6 @@ class HostArena : public RecvArena {
   HostArena(size_t slot_bytes, int slots);
   std::pair<uint8_t*, size_t> recv_window() override;
   void received(size_t n) override;
-  size_t recv_into(Conn& c, uint8_t* p, size_t cap) override;
   // the slot currently being filled [base, base + used)
   bool contains(const uint8_t* p, size_t n) const;
   uint64_t recvs() const { return recvs_; }

@@ -49,6 +49,23 @@ class Stash:
         self._line = None
         self._printed = False
         self._timer = None
+        self._out = None
+
+    def claim_stdout(self) -> None:
+        """Keep stdout for the ONE JSON line: the process's fd 1 is pointed
+        at stderr, so what native libraries print there (RCCL's version
+        banner at communicator init, runtime notices) cannot land in front of
+        the line the driver parses; the line goes to a private copy of the
+        original stdout."""
+        if self._out is not None:
+            return
+        sys.stdout.flush()
+        self._out = os.fdopen(os.dup(1), "w", buffering=1)
+        os.dup2(2, 1)
+
+    def _print(self, line: str) -> None:
+        out = self._out or sys.stdout
+        print(line, file=out, flush=True)
 
     def stash(self, line: str) -> None:
         with self._lock:
@@ -62,14 +79,14 @@ class Stash:
             line = self._line
         if why:
             print(f"bench: {why}; printing the headline measured so far", file=sys.stderr, flush=True)
-        print(line, flush=True)
+        self._print(line)
 
     def final(self, line: str) -> None:
         with self._lock:
             if self._printed:  # a fatal path already printed the stash
                 return
             self._printed = True
-        print(line, flush=True)
+        self._print(line)
 
     def arm(self, seconds: float) -> None:
         """Side blocks must be done within `seconds` (0 = no limit)."""
@@ -274,7 +291,6 @@ class RankBench:
 
             def _term(signum, frame):
                 stash.emit_stash("terminated")
-                sys.stdout.flush()
                 os._exit(128 + signum)
             signal.signal(signal.SIGTERM, _term)
         protocol = args.protocol
@@ -321,7 +337,6 @@ class RankBench:
             "ring_slots": args.slots,
             "conn_ring": args.conn_ring != "off",
             "conn_ring_inplace": args.conn_ring_inplace == "on",
-            "stage_copy": args.stage_copy == "on",
             "conn_ring_slots": int(args.conn_ring.partition("x")[0]) if "x" in args.conn_ring else 4,
             "conn_ring_slot_bytes": parse_size(args.conn_ring.partition("x")[2]) if "x" in args.conn_ring else 1 << 20,
             "landing": "object",
@@ -1407,4 +1422,5 @@ def _by_node(counts):
 
 
 def run_rank(args) -> int:
+    stash.claim_stdout()
     return RankBench(args).run()

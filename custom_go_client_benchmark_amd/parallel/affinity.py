@@ -276,17 +276,6 @@ def plan(device: int, mode: str = "split", slot: int = 0) -> dict:
                     best = (load, q)
             if best is not None:
                 q = best[1]
-                # a quiet core of ANOTHER L3 domain of the share: the receive
-                # helper (ConnRing::set_recv_helper), so the bytes bound for
-                # HBM leave two CCDs instead of one
-                helper = []
-                for dom in doms:
-                    if q[0][0] in dom:
-                        continue
-                    oq = quiet_cores(dom, busy)
-                    if oq and (not helper or sum(busy.get(c, 0.0) for c in oq[0]) <
-                               sum(busy.get(c, 0.0) for c in helper)):
-                        helper = oq[0]
                 if mode == "pair2":
                     # a second quiet core each for the client and the endpoint
                     # thread: somewhere to go when another tenant's thread
@@ -294,7 +283,7 @@ def plan(device: int, mode: str = "split", slot: int = 0) -> dict:
                     return {"client": sorted(q[0] + q[3]), "server": sorted(q[1] + q[4]), "aux": q[2], "mode": mode,
                             "numa_node": node, "gpu_index_on_node": k, "picked_by": "quiet",
                             "busy": round(best[0], 3)}
-                return {"client": q[0], "server": q[1], "aux": q[2], "helper": helper, "mode": mode,
+                return {"client": q[0], "server": q[1], "aux": q[2], "mode": mode,
                         "numa_node": node, "gpu_index_on_node": k, "picked_by": "quiet",
                         "busy": round(best[0], 3)}
         g = core_first(groups[base] if groups else cpus)
@@ -305,12 +294,7 @@ def plan(device: int, mode: str = "split", slot: int = 0) -> dict:
         # thread, so slot hand-offs never run on the receiving core's SMT pair
         aux = [g[2]] + [d for d in (groups[base] if groups else cpus) if d != g[2] and _same_core(g[2], d)] \
             if len(g) > 2 else []
-        helper = []
-        if groups and share > 1:
-            og = groups[(base + 1) % len(groups)]
-            h0 = core_first(og)[0]
-            helper = [h0] + [d for d in og if d != h0 and _same_core(h0, d)]
-        return {"client": [g[0]] + sib[g[0]], "server": [g[1]] + sib[g[1]], "aux": aux, "helper": helper,
+        return {"client": [g[0]] + sib[g[0]], "server": [g[1]] + sib[g[1]], "aux": aux,
                 "mode": mode, "numa_node": node, "gpu_index_on_node": k}
     client = groups[base] if groups else cpus
     if mode == "same" and share > 1 and _quiet_sampling():

@@ -99,29 +99,19 @@ variants = {
     "head_24x2": {"sink": "gpu", "ring_slots": 24},
     "head_48x2": {"sink": "gpu", "ring_slots": 48},
     "nodma_48x2": {"sink": "gpu", "gpu_stage": "none", "ring_slots": 48},
-    # round 5: the headline's 4 x 1 MiB ring received through a cached
-    # staging mirror, streamed into the pinned slot by the submitter
-    # (GpuSinkConfig stage_copy), against the same ring never DMA-read
-    "staged_4x1m": {"sink": "gpu", "ring_slot_bytes": 1 << 20, "ring_slots": 4, "stage_copy": True},
-    "staged_8x1m": {"sink": "gpu", "ring_slot_bytes": 1 << 20, "ring_slots": 8, "stage_copy": True},
-    "staged_4x2m": {"sink": "gpu", "ring_slot_bytes": 2 << 20, "ring_slots": 4, "stage_copy": True},
+    # round 5: the one stream through a connection ring in arena mode (recv
+    # straight into the ring, a slot's worth per recv).  The staged-copy and
+    # cross-CCD recv-helper variants measured in profiles/r5_arena were
+    # removed after that measurement (git history has them).
     "nodma_4x1m": {"sink": "gpu", "gpu_stage": "none", "ring_slot_bytes": 1 << 20, "ring_slots": 4},
-    # the one stream through a connection ring in arena mode (recv straight
-    # into the ring, a slot's worth per recv), and with every other recv on
-    # a helper core of another L3 domain (ConnRing::set_recv_helper)
-    "arena_4x1m": {"sink": "gpu", "conn_ring_single": True, "conn_ring_slots": 4, "conn_ring_slot_bytes": 1 << 20},
-    "arena_help": {"sink": "gpu", "conn_ring_single": True, "conn_ring_slots": 4, "conn_ring_slot_bytes": 1 << 20,
-                   "recv_helper_cpus": "HELPER"},
-    "arena_help_8": {"sink": "gpu", "conn_ring_single": True, "conn_ring_slots": 8,
-                     "conn_ring_slot_bytes": 1 << 20, "recv_helper_cpus": "HELPER"},
+    "arena_4x1m": {"sink": "gpu", "conn_ring_single": True, "conn_ring_inplace": True, "conn_ring_slots": 4,
+                   "conn_ring_slot_bytes": 1 << 20},
 }
 SPIN_US = {"head_spin": 200, "head_4x1m_spin": 200}
 names = [v for v in args.variants.split(",") if v]
 for v in variants.values():
     if v.get("cpus") == "TWO_CORE":
         v["cpus"] = two_core
-    if v.get("recv_helper_cpus") == "HELPER":
-        v["recv_helper_cpus"] = pl.get("helper") or []
 runners = {k: n.Runner({**base, **variants[k]}) for k in names}
 for r in runners.values():  # warm: connections, rings, sinks
     r.start()
@@ -160,7 +150,6 @@ def run(name):
             "submit_cpu_s_per_gib": round(d.get("gcsb-submit", 0.0) / gib, 4),
             "handoff_s_per_gib": round((s.get("gpu") or {}).get("handoff_s", 0.0) / gib, 5),
             "worker_cpu_s_per_gib": round(s.get("worker_cpu_s", 0.0) / gib, 4),
-            "helper_cpu_s_per_gib": round(d.get("gcsb-recv-help", 0.0) / gib, 4),
             "conn_ring": r.conn_ring_stats(),
             "endpoint_busy_frac": round((sv1["tcp_busy_us"] - sv0["tcp_busy_us"]) / wall, 3),
             "errors": s["errors"], "sched": diag}

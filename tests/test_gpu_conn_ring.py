@@ -105,31 +105,25 @@ def test_conn_ring_stalled_stream_resumes(native, server, gpu_available, proto):
         assert bad == 0, (w, first)
 
 
-@pytest.mark.parametrize("helper", [False, True])
 @pytest.mark.parametrize("chunk", [2 << 20, 99991])
-def test_arena_single_stream_byte_exact(native, gpu_available, helper, chunk):
+def test_arena_single_stream_byte_exact(native, gpu_available, chunk):
     """Arena mode on ONE stream (the headline's geometry): the connection's
     recv() lands straight in the ring, a slot's worth at a time across frame
-    and message boundaries, and with a helper every other recv() runs on
-    another thread.  Odd message sizes put boundaries anywhere in a slot."""
-    import os
-
+    and message boundaries.  Odd message sizes put boundaries anywhere in a
+    slot."""
     srv = native.Server({"port": 0, "grpc_chunk": chunk})
     srv.start()
     try:
         size = (9 << 20) + 4321
         srv.add_synthetic(B, P, "", 0, 1, size)
-        kw = {"conn_ring_single": True, "conn_ring_inplace": True}
-        if helper:
-            kw["recv_helper_cpus"] = sorted(os.sched_getaffinity(0))[:2]
-        r = _runner(native, srv, 1, 3, 1 << 20, 4, **kw)
+        r = _runner(native, srv, 1, 3, 1 << 20, 4, conn_ring_single=True, conn_ring_inplace=True)
         r.start()
         r.wait()
         s = r.summary()
         assert s["errors"] == 0 and s["verified"] == 3, s["first_error"]
         st = r.conn_ring_stats()
         assert st is not None and st["arena"] and st["segments"] >= 3
-        assert (st["helper_recvs"] > 0) == helper and st["reader_recvs"] > 0
+        assert st["arena_recvs"] > 0 and st["arena_bytes"] >= 3 * size
         bad, first = native.gpu_verify_pattern(0, r.landing_ptr(0), size, P + "0", 0)
         assert bad == 0, first
         assert native.gpu_crc32c(0, r.landing_ptr(0), size) == srv.object_info(B, P + "0")["crc32c"]
@@ -137,19 +131,16 @@ def test_arena_single_stream_byte_exact(native, gpu_available, helper, chunk):
         srv.stop()
 
 
-def test_arena_single_stream_resume_with_helper(native, gpu_available):
-    """A connection cut mid-object under the helper: the retry resumes at
-    the delivered offset on a new connection into the same arena."""
-    import os
-
+def test_arena_single_stream_resume(native, gpu_available):
+    """A connection cut mid-object in arena mode: the retry resumes at the
+    delivered offset on a new connection into the same arena."""
     srv = native.Server({"port": 0, "grpc_chunk": 99991})
     srv.start()
     try:
         size = (7 << 20) + 55
         srv.add_synthetic(B, P, "", 0, 1, size)
         srv.set_faults({"disconnect_at": (3 << 20) + 7, "disconnect_count": 1})
-        r = _runner(native, srv, 1, 2, 1 << 20, 4, conn_ring_single=True, conn_ring_inplace=True,
-                    recv_helper_cpus=sorted(os.sched_getaffinity(0))[:2])
+        r = _runner(native, srv, 1, 2, 1 << 20, 4, conn_ring_single=True, conn_ring_inplace=True)
         r.start()
         r.wait()
         s = r.summary()

@@ -151,7 +151,9 @@ def test_bench_line_fits_the_driver_tail(gpus, tmp_path):
     diag = tmp_path / "diag.json"
     r = _bench(["--gpus", str(gpus), "--diag-out", str(diag)] + SMALL)
     assert r.returncode == 0, r.stderr[-3000:]
-    last = r.stdout.strip().splitlines()[-1]
+    lines = r.stdout.strip().splitlines()
+    assert len(lines) == 1, r.stdout[:2000]  # stdout holds the ONE line, nothing else
+    last = lines[0]
     assert len(last.encode()) <= rp.LINE_LIMIT, len(last)
     line = json.loads(last)
     for k in rp.DRIVER_KEYS:
@@ -169,6 +171,24 @@ def test_bench_line_fits_the_driver_tail(gpus, tmp_path):
         assert "host" in d["blocks"]["compare"]
     else:
         assert "paired" not in line and len(line["per_rank_mib_s"]) == 8
+
+
+def test_native_stdout_noise_goes_to_stderr():
+    """What a native library writes to fd 1 after the rank claimed stdout (RCCL
+    prints a version banner at communicator init) lands on stderr; stdout
+    carries only the JSON line."""
+    code = ("import os\n"
+            "from custom_go_client_benchmark_amd.benchmark.rank import stash\n"
+            "stash.claim_stdout()\n"
+            "os.write(1, b'RCCL version : banner\\n')\n"
+            "print('python noise')\n"
+            "stash.final('{\"metric\": 1}')\n")
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout == '{"metric": 1}\n'
+    assert "RCCL version" in r.stderr and "python noise" in r.stderr
 
 
 # ---------------------------------------------------------------- arena path

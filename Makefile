@@ -94,7 +94,8 @@ tsan: $(BUILD)/tsan/stress
 stress: $(BUILD)/plain/stress
 	$(BUILD)/plain/stress 3
 
--include $(patsubst csrc/%.cc,$(BUILD)/asan/%.d,$(SAN_SRCS)) $(patsubst csrc/%.cc,$(BUILD)/tsan/%.d,$(SAN_SRCS))
+-include $(patsubst csrc/%.cc,$(BUILD)/asan/%.d,$(SAN_SRCS)) $(patsubst csrc/%.cc,$(BUILD)/tsan/%.d,$(SAN_SRCS)) \
+  $(patsubst csrc/%.cc,$(BUILD)/plain/%.d,$(SAN_SRCS))
 
 clean:
 	rm -rf $(BUILD) $(EXT) $(TOOL_BINS) $(PROBE_BINS)

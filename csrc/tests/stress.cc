@@ -4,10 +4,14 @@
 // (Q3 main.go:203, Q14 ssd_test/main.go:80) and never runs -race; this binary
 // exercises every shared structure of the C++ core from many threads under
 // ASan+UBSan and TSan.  Exit status 0 = every read/write verified.
+#include <execinfo.h>
+#include <unistd.h>
+
 #include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <exception>
 #include <string>
 #include <thread>
 #include <vector>
@@ -72,6 +76,13 @@ void readers(StorageClient& cli, const std::string& bucket, int nobj, int thread
 }  // namespace
 
 int main(int argc, char** argv) {
+  std::set_terminate([] {
+    void* f[64];
+    const int n = backtrace(f, 64);
+    std::fprintf(stderr, "stress: terminate; backtrace:\n");
+    backtrace_symbols_fd(f, n, 2);
+    std::abort();
+  });
   const int scale = argc > 1 ? std::atoi(argv[1]) : 1;
   auto store = std::make_shared<ObjectStore>(true);
   ServerConfig sc;
@@ -128,6 +139,54 @@ int main(int argc, char** argv) {
     }
     check(arena.recvs() > 0, "arena used");
   }
+
+  // one stream goes silent MID-BODY past the read timeout while the others on
+  // its connection keep flowing: that stream alone is cancelled (RST_STREAM,
+  // the reader may be inside its dispatch), resumes at its delivered offset
+  // on the same connection, and the endpoint's stalled handler wakes later
+  // into a cancelled stream (tests/test_gpu_conn_ring.py stalled case, host
+  // sinks); then the same with the arena
+  for (const char* proto : {"http2", "grpc", "grpc-arena"}) {
+    const bool use_arena = std::strcmp(proto, "grpc-arena") == 0;
+    HostArena arena(1 << 20, 4);
+    ClientConfig tc = client_cfg(use_arena ? "grpc" : proto, srv.url());
+    // the stall outlasts the starvation allowance (h2_client.h
+    // kStarvedWindows) even when the other streams are slow (TSan)
+    tc.sock.io_timeout_ms = 150;
+    tc.retry.max_attempts = 6;
+    if (use_arena) tc.recv_arena = &arena;
+    auto tcli = make_client(tc);
+    for (int round = 0; round < 2 * scale; ++round) {
+      srv.faults().stall_at = (1 << 20) + 77 * round;
+      srv.faults().stall_ms = 1500;
+      srv.faults().stall_count = 1;
+      std::vector<std::thread> th;
+      for (int t = 0; t < 6; ++t)
+        th.emplace_back([&, t] {
+          std::unique_ptr<Sink> sink;
+          if (use_arena)
+            sink = std::make_unique<InplaceHostSink>(&arena);
+          else
+            sink = std::make_unique<DiscardSink>(tc.read_chunk, true, true);
+          for (int i = 0; i < 2; ++i) {
+            const std::string name = "obj_" + std::to_string((t + i) % nobj);
+            try {
+              ReadResult rr = tcli->read_object(bucket, name, *sink);
+              check(rr.sink.verified && !rr.sink.crc_mismatch,
+                    std::string(proto) + " stalled-stream read " + name + ": " + rr.sink.detail);
+            } catch (const std::exception& e) {
+              check(false, std::string(proto) + " stalled-stream read " + name + ": " + e.what());
+            }
+          }
+        });
+      for (auto& x : th) x.join();
+    }
+    srv.faults().stall_count = 0;
+    check(tcli->stats().retries > 0, std::string(proto) + " stalled stream retried");
+  }
+  // let the last stalled handler wake into its cancelled stream while the
+  // endpoint still serves
+  std::this_thread::sleep_for(std::chrono::milliseconds(1600));
 
   // multiplexed reads, plus a mid-stream disconnect on the retry path
   for (const char* proto : {"http2", "grpc"}) {

@@ -802,7 +802,7 @@ PYBIND11_MODULE(_native, m) {
       py::arg("cfg"), py::arg("bucket"), py::arg("name"), py::arg("slot_bytes") = 1 << 20, py::arg("slots") = 4,
       py::arg("want_data") = false);
 
-  m.def("set_deferred_wake_blocks", [](int n) { DiscardSink::wake_blocks() = n; },
+  m.def("set_deferred_wake_blocks", [](int n) { DiscardSink::wake_blocks().store(n); },
         "A/B: a deferred discard sink wakes its worker once this many blocks are queued (0: every message)");
 
   m.def("crc32c", [](const py::bytes& b) {

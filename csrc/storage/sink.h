@@ -119,11 +119,14 @@ class DiscardSink : public Sink {
   bool deferred() const override { return deferred_; }
   // two blocks undrained: wake the worker; a 1 MiB object's one block waits
   // for the end-of-stream wake-up instead (one futex call per read, not two)
-  bool drain_wanted() const override { return held_.load(std::memory_order_relaxed) >= wake_blocks(); }
+  bool drain_wanted() const override {
+    return held_.load(std::memory_order_relaxed) >= wake_blocks().load(std::memory_order_relaxed);
+  }
   // A/B: blocks undrained before the reader wakes the worker (default 2;
-  // 0 = at every message end, the round-4 behaviour)
-  static int& wake_blocks() {
-    static int n = 2;
+  // 0 = at every message end, the round-4 behaviour); set from Python while
+  // readers run, hence atomic
+  static std::atomic<int>& wake_blocks() {
+    static std::atomic<int> n{2};
     return n;
   }
 

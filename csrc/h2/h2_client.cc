@@ -14,7 +14,8 @@ namespace gcsb {
 
 namespace {
 std::atomic<uint64_t> g_frames{0}, g_data_frames{0}, g_header_blocks{0}, g_data_bytes{0}, g_wait_ns{0},
-    g_data_ns{0}, g_headers_ns{0}, g_other_ns{0};
+    g_data_ns{0}, g_headers_ns{0}, g_other_ns{0}, g_long_waits{0}, g_long_wait_ns{0}, g_readers{0};
+constexpr int64_t kLongWaitNs = 5000000;
 }  // namespace
 
 H2ReaderStats h2_reader_stats() {
@@ -27,6 +28,9 @@ H2ReaderStats h2_reader_stats() {
   s.data_ns = g_data_ns.load();
   s.headers_ns = g_headers_ns.load();
   s.other_ns = g_other_ns.load();
+  s.long_waits = g_long_waits.load();
+  s.long_wait_ns = g_long_wait_ns.load();
+  s.readers_alive = g_readers.load();
   return s;
 }
 
@@ -279,6 +283,10 @@ void H2ClientConn::reader_loop() {
   std::string hblock;
   uint32_t hstream = 0;
   bool hend_stream = false;
+  g_readers.fetch_add(1, std::memory_order_relaxed);
+  struct Alive {
+    ~Alive() { g_readers.fetch_sub(1, std::memory_order_relaxed); }
+  } alive;
   try {
     for (;;) {
       const int64_t t_wait = now_ns();
@@ -287,6 +295,10 @@ void H2ClientConn::reader_loop() {
       last_frame_ns_.store(t_frame, std::memory_order_relaxed);
       frames_.fetch_add(1, std::memory_order_relaxed);
       g_wait_ns.fetch_add(static_cast<uint64_t>(t_frame - t_wait), std::memory_order_relaxed);
+      if (t_frame - t_wait > kLongWaitNs) {
+        g_long_waits.fetch_add(1, std::memory_order_relaxed);
+        g_long_wait_ns.fetch_add(static_cast<uint64_t>(t_frame - t_wait), std::memory_order_relaxed);
+      }
       g_frames.fetch_add(1, std::memory_order_relaxed);
       struct Account {  // time of this frame's handling, by type
         uint8_t type;

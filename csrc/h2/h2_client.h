@@ -106,6 +106,11 @@ struct H2ReaderStats {
   uint64_t data_ns = 0;         // DATA frames: stream dispatch incl. recv() into the sink
   uint64_t headers_ns = 0;      // HEADERS/CONTINUATION: read + HPACK decode + stream dispatch
   uint64_t other_ns = 0;        // every other frame type
+  // waits over 5 ms for the next frame (an idle connection's first frame
+  // after a pause, e.g. a pooled connection reused by a later block): count
+  // and their time, so a block's split can leave them out
+  uint64_t long_waits = 0, long_wait_ns = 0;
+  uint64_t readers_alive = 0;   // connection reader threads running now
 };
 H2ReaderStats h2_reader_stats();
 

@@ -1005,6 +1005,9 @@ PYBIND11_MODULE(_native, m) {
     d["data_ns"] = s.data_ns;
     d["headers_ns"] = s.headers_ns;
     d["other_ns"] = s.other_ns;
+    d["long_waits"] = s.long_waits;
+    d["long_wait_ns"] = s.long_wait_ns;
+    d["readers_alive"] = s.readers_alive;
     return d;
   });
   m.def("slow_hip_calls", [] {

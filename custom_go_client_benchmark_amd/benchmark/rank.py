@@ -474,7 +474,13 @@ class RankBench:
                 # the HTTP/2 connection readers (gRPC): where their time went, per GiB
                 d = {k: h2s1[k] - h2s0[k] for k in h2s1}
                 cpu["h2_reader"] = {"frames_per_read": round(d["frames"] / max(1, s1["reads"]), 2),
-                                    "wait_s_per_gib": round(d["header_wait_ns"] / 1e9 / gib, 4),
+                                    # waits over 5 ms are apart: an idle connection's
+                                    # next frame after a pause is not this block's time
+                                    "wait_s_per_gib": round((d["header_wait_ns"] - d.get("long_wait_ns", 0))
+                                                            / 1e9 / gib, 4),
+                                    "long_waits": d.get("long_waits", 0),
+                                    "long_wait_s": round(d.get("long_wait_ns", 0) / 1e9, 4),
+                                    "readers_alive": h2s1.get("readers_alive", 0),
                                     "data_s_per_gib": round(d["data_ns"] / 1e9 / gib, 4),
                                     "headers_s_per_gib": round(d["headers_ns"] / 1e9 / gib, 4),
                                     "other_s_per_gib": round(d["other_ns"] / 1e9 / gib, 4),

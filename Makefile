@@ -38,7 +38,7 @@ TOOLS := fakegcs read_operation ssd_test write_operations list_operation open_fi
 TOOL_BINS := $(addprefix $(PKG)/bin/,$(TOOLS))
 # experiment probes (not part of the default build): make probes
 PROBES := splice_probe
-PROBE_BINS := $(addprefix $(PKG)/bin/,$(PROBES))
+PROBE_BINS := $(addprefix $(PKG)/bin/,$(PROBES)) $(PKG)/bin/ring_dma_probe
 
 .PHONY: all clean ext tools probes asan tsan stress
 all: ext tools
@@ -61,6 +61,10 @@ $(BUILD)/libgcsbcore.a: $(CORE_OBJS)
 $(EXT): $(PY_OBJS) $(GPU_OBJS) $(BUILD)/libgcsbcore.a
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(PY_OBJS) $(GPU_OBJS) $(BUILD)/libgcsbcore.a \
 	  -L/opt/rocm/lib -lamdhip64 -lhsa-runtime64 -lrocprofiler-sdk-roctx $(LDLIBS) -Wl,-rpath,/opt/rocm/lib
+
+$(PKG)/bin/ring_dma_probe: csrc/tools/ring_dma_probe.hip
+	@mkdir -p $(PKG)/bin
+	$(HIPCC) --offload-arch=$(ARCH) -O2 -std=c++17 -o $@ $< -L/opt/rocm/lib -lamdhip64 -pthread -Wl,-rpath,/opt/rocm/lib
 
 $(PKG)/bin/%: csrc/tools/%.cc $(BUILD)/libgcsbcore.a
 	@mkdir -p $(PKG)/bin

@@ -12,6 +12,8 @@
 //           rep     rep movsb (what the kernel's copy_to_user does)
 //           nt      non-temporal stores
 //           flush   memcpy, then clflushopt of the slot
+//           tcpv / repv  the same into fine-grained VRAM mapped to the host
+//                   (large BAR): the receive lands in HBM, nothing to copy
 //           tcp     recv() from one loopback TCP connection whose sender
 //                   (sender=CPU) vmsplice()s the source into the socket, as
 //                   the endpoint does: the headline minus HTTP/2 and gRPC
@@ -23,6 +25,9 @@
 //                   HBM, then the flag kernel
 //           sdma_clwb / sdma_flush  the submitter clwb's / clflushopt's the
 //                   slot before its H2D copy
+//           relay   the submitter copies the slot (rep movsb) into
+//                   host-mapped fine-grained VRAM itself: no device read
+//           relaynt the same with non-temporal stores
 //           sdma_pw the submitter prefetchw's the slot after its H2D copy
 //                   finished, before handing it back to the writer
 //
@@ -36,6 +41,8 @@
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <sched.h>
+#include <setjmp.h>
+#include <signal.h>
 #include <sys/mman.h>
 #include <sys/socket.h>
 #include <sys/uio.h>
@@ -179,6 +186,27 @@ int sibling_of(int cpu) {
   return -1;
 }
 
+sigjmp_buf g_probe_jmp;
+void on_probe_fault(int) { siglongjmp(g_probe_jmp, 1); }
+
+// Whether the CPU can store to p (a device allocation mapped to the host?):
+// one store under a SIGSEGV/SIGBUS handler.
+bool host_writable(volatile uint8_t* p) {
+  struct sigaction sa {}, old_segv{}, old_bus{};
+  sa.sa_handler = on_probe_fault;
+  sigemptyset(&sa.sa_mask);
+  sigaction(SIGSEGV, &sa, &old_segv);
+  sigaction(SIGBUS, &sa, &old_bus);
+  bool ok = false;
+  if (sigsetjmp(g_probe_jmp, 1) == 0) {
+    p[0] = 1;
+    ok = p[0] == 1;
+  }
+  sigaction(SIGSEGV, &old_segv, nullptr);
+  sigaction(SIGBUS, &old_bus, nullptr);
+  return ok;
+}
+
 struct Args {
   int slots = 4;
   size_t slot = 1 << 20;
@@ -264,6 +292,16 @@ int main(int argc, char** argv) {
   std::memset(dflags, 0, 64 * a.slots);
   uint32_t* dflags_d = nullptr;
   check(hipHostGetDevicePointer(reinterpret_cast<void**>(&dflags_d), dflags, 0), "hipHostGetDevicePointer dflags");
+  // the relay modes' destination: fine-grained VRAM the host stores to
+  uint8_t* vland = nullptr;
+  bool vland_ok = false;
+  for (const auto& v : a.variants)
+    if (v.find("/relay") != std::string::npos) {
+      if (hipExtMallocWithFlags(reinterpret_cast<void**>(&vland), a.slot * a.slots * 8, hipDeviceMallocFinegrained) ==
+          hipSuccess)
+        vland_ok = host_writable(vland);
+      break;
+    }
   std::thread sub([&] {
     pin(a.submitter);
     uint64_t next = 1;  // the next sequence number to issue (slot (next-1) % slots)
@@ -295,6 +333,13 @@ int main(int argc, char** argv) {
       uint8_t* slot = ring + s * a.slot;
       if (m == 0) {
         __atomic_store_n(flags + s * 16, static_cast<uint32_t>(next), __ATOMIC_RELEASE);
+      } else if (m == 7 || m == 8) {
+        uint8_t* vd = vland + ((next - 1) % (a.slots * 8)) * a.slot;
+        if (m == 7)
+          rep_movsb(vd, slot, a.slot);
+        else
+          nt_copy(vd, slot, a.slot);
+        __atomic_store_n(flags + s * 16, static_cast<uint32_t>(next), __ATOMIC_RELEASE);
       } else {
         if (m == 4) clwb_range(slot, a.slot);
         if (m == 5) flush_range(slot, a.slot);
@@ -313,8 +358,23 @@ int main(int argc, char** argv) {
   });
 
   const std::map<std::string, int> dev_code{{"idle", 0},       {"flag", 1},       {"sdma", 2}, {"kernel", 3},
-                                            {"sdma_clwb", 4}, {"sdma_flush", 5}, {"sdma_pw", 6}};
-  const std::map<std::string, int> wr_code{{"memcpy", 0}, {"rep", 1}, {"nt", 2}, {"flush", 3}, {"tcp", 4}};
+                                            {"sdma_clwb", 4}, {"sdma_flush", 5}, {"sdma_pw", 6},
+                                            {"relay", 7},     {"relaynt", 8}};
+  const std::map<std::string, int> wr_code{{"memcpy", 0}, {"rep", 1}, {"nt", 2}, {"flush", 3}, {"tcp", 4},
+                                           {"tcpv", 5}, {"repv", 6}};
+  // fine-grained VRAM for the tcpv / repv writers, if the host can store to it
+  uint8_t* vram = nullptr;
+  bool vram_ok = false;
+  for (const auto& v : a.variants)
+    if (v.rfind("tcpv", 0) == 0 || v.rfind("repv", 0) == 0) {
+      if (hipExtMallocWithFlags(reinterpret_cast<void**>(&vram), a.slot * a.slots, hipDeviceMallocFinegrained) ==
+          hipSuccess)
+        vram_ok = host_writable(vram);
+      std::printf("{\"vram\": \"finegrained\", \"allocated\": %s, \"host_writable\": %s}\n", vram ? "true" : "false",
+                  vram_ok ? "true" : "false");
+      std::fflush(stdout);
+      break;
+    }
 
   // the loopback connection for the tcp writer: the sender sends `total`
   // bytes per go, from the THP source by vmsplice + splice
@@ -373,14 +433,16 @@ int main(int argc, char** argv) {
         continue;
       }
       const int wm = wr_code.at(v.substr(0, sl));
+      if ((wm == 5 || wm == 6) && !vram_ok) continue;
       const int m = dev_code.at(v.substr(sl + 1));
+      if ((m == 7 || m == 8) && !vland_ok) continue;
       mode.store(m, std::memory_order_release);
       std::vector<int> wcpus{a.writer};
       if (a.writer >= 0 && sibling_of(a.writer) >= 0) wcpus.push_back(sibling_of(a.writer));
       const auto irq0 = irqs_on(wcpus);
       int64_t wait_ns = 0, copy_ns = 0;
       double writer_cpu = 0;
-      if (wm == 4) send_go.fetch_add(1, std::memory_order_release);
+      if (wm == 4 || wm == 5) send_go.fetch_add(1, std::memory_order_release);
       draining.store(false, std::memory_order_release);
       std::thread w([&] {
         pin(a.writer);
@@ -389,7 +451,7 @@ int main(int argc, char** argv) {
         for (size_t i = 0; i < n; ++i) {
           ++seq;
           const int s = static_cast<int>((seq - 1) % a.slots);
-          uint8_t* p = ring + s * a.slot;
+          uint8_t* p = (wm == 5 || wm == 6 ? vram : ring) + s * a.slot;
           // the slot is free once the device finished its previous use
           if (seq > static_cast<uint64_t>(a.slots)) {
             const uint32_t want = static_cast<uint32_t>(seq - a.slots);
@@ -399,7 +461,7 @@ int main(int argc, char** argv) {
           }
           const int64_t t1 = now_ns();
           if (src_off + a.slot > a.src_bytes) src_off = 0;
-          if (wm == 4) {
+          if (wm == 4 || wm == 5) {
             for (size_t got = 0; got < a.slot;) {
               const ssize_t r = recv(cfd, p + got, a.slot - got, 0);
               if (r <= 0) {
@@ -410,7 +472,7 @@ int main(int argc, char** argv) {
             }
           } else if (wm == 2)
             nt_copy(p, src + src_off, a.slot);
-          else if (wm == 1)
+          else if (wm == 1 || wm == 6)
             rep_movsb(p, src + src_off, a.slot);
           else
             std::memcpy(p, src + src_off, a.slot);
@@ -465,6 +527,8 @@ int main(int argc, char** argv) {
   (void)hipFree(hbm);
   (void)hipHostFree(flags);
   (void)hipHostFree(dflags);
+  if (vram) (void)hipFree(vram);
+  if (vland) (void)hipFree(vland);
   (void)hipHostFree(ring);
   munmap(src, a.src_bytes);
   return 0;

@@ -62,6 +62,10 @@ struct CrcLaunchOptions {
   // against 8.78-8.79 us per 1 MiB slot, min 6.5 against 7.0-7.3
   // (profiles/r4_crc8)
   bool slice8 = true;
+  // bulk (non-fused) batches: bank-private slice-by-4 tables, conflict-free
+  // lookups (crc32c_tiles_bp_kernel): 3.85-3.99 against 3.24-3.71 TB/s
+  // (4 / 16 KiB tiles, profiles/r5_kernels)
+  bool bank_private = true;
 };
 void set_crc_launch_options(const CrcLaunchOptions& o);
 CrcLaunchOptions crc_launch_options();

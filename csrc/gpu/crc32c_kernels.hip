@@ -26,8 +26,11 @@
 // ds_read_b32 table lookups cost ~4 bank-conflict cycles per instruction; a
 // conflict-free variant (nibble tables replicated per bank) removed them but
 // doubled the lookups and ran at 3.2 TB/s, so it was dropped in round 2.
+// Round 5: byte tables replicated per bank (slice-by-4, 128 KiB, one lookup
+// per byte, no conflicts) for bulk batches: 3.85-3.99 TB/s.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <mutex>
@@ -174,11 +177,8 @@ __device__ __forceinline__ uint32_t lane_state(const CrcBatch& b, uint32_t s, ui
   return lane_chain<R, kNib>(v, sl, lane_shift, lane);
 }
 
-template <int R>
-__device__ __forceinline__ uint32_t tile_crc(const CrcBatch& b, uint32_t s, uint32_t gt, const uint32_t* sl,
-                                             const uint32_t* lane_shift, int lane) {
-  uint32_t state = lane_state<R>(b, s, gt, sl, lane_shift, lane);
-  // wave tree: lane l's last chunk ends 64 (63 - l) bytes before the tile end
+// wave tree: lane l's last chunk ends 64 (63 - l) bytes before the tile end
+__device__ __forceinline__ uint32_t wave_tree(uint32_t state, const uint32_t* lane_shift, int lane) {
 #pragma unroll
   for (int lv = 0; lv < 6; ++lv) {
     const uint32_t other = __shfl_down(state, 1 << lv, 64);
@@ -186,6 +186,12 @@ __device__ __forceinline__ uint32_t tile_crc(const CrcBatch& b, uint32_t s, uint
     if ((lane & ((2 << lv) - 1)) == 0) state = shifted ^ other;
   }
   return state;
+}
+
+template <int R>
+__device__ __forceinline__ uint32_t tile_crc(const CrcBatch& b, uint32_t s, uint32_t gt, const uint32_t* sl,
+                                             const uint32_t* lane_shift, int lane) {
+  return wave_tree(lane_state<R>(b, s, gt, sl, lane_shift, lane), lane_shift, lane);
 }
 
 // The last 1..16 bytes of a segment (after its tiles) folded into `raw`: lane
@@ -366,6 +372,74 @@ __global__ __launch_bounds__(kThreads) void crc32c_tiles_kernel(const CrcBatch b
       if (lane == 0) store_result(out + g, seg_result(sg, raw));
     }
     if (threadIdx.x == 0) __hip_atomic_store(scratch, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// Bank-private slice-by-4 (bulk, non-fused, the default): each 32-lane half
+// of a wave reads its lookups from 32 private copies of T0..T3, lane l only
+// from bank l, so ds_read_b32 never conflicts.  The slice-by-16 tables above
+// cost ~4 extra LDS cycles per lookup and left the waves 42% of their cycles
+// waiting on LDS (SQ_WAIT_INST_LDS / SQ_WAVE_CYCLES); here 2%
+// (profiles/r5_kernels).  One lookup per byte as before; 128 KiB of tables +
+// the shift tables, so one 16-wave workgroup per CU stages them once and
+// grid-strides over the tiles.  A 16-copy variant (2-way conflicts, shift
+// tables from global memory, two workgroups per CU) measured slower.
+constexpr int kBpThreads = 1024;
+constexpr int kBpWaves = kBpThreads / 64;
+
+template <int kRep>
+__device__ __forceinline__ uint32_t step4_bp(const uint32_t* __restrict__ bp, uint32_t x) {
+  return bp[(3 * 256 + (x & 0xff)) * kRep] ^ bp[(2 * 256 + ((x >> 8) & 0xff)) * kRep] ^
+         bp[(1 * 256 + ((x >> 16) & 0xff)) * kRep] ^ bp[(x >> 24) * kRep];
+}
+
+template <int R, int kRep>
+__global__ __launch_bounds__(kBpThreads) void crc32c_tiles_bp_kernel(const CrcBatch b, const CrcTables* __restrict__ tabs,
+                                                                   uint32_t* __restrict__ scratch) {
+  constexpr int kBpWords = 4 * 256 * kRep;
+  static_assert(kRep == 32, "one table copy per ds_read_b32 bank");
+  constexpr int kShWords = 6 * 1024 + (R > 1 ? 1024 : 0);
+  __shared__ __attribute__((aligned(16))) uint32_t s_bp[kBpWords];
+  __shared__ __attribute__((aligned(16))) uint32_t s_sh[kShWords];
+  // word i = T_(i / (256 kRep))[(i / kRep) & 255], bank i % kRep
+  for (int i = threadIdx.x; i < kBpWords; i += blockDim.x) s_bp[i] = tabs->slice16[i / (256 * kRep)][(i / kRep) & 255];
+  stage(s_sh, &tabs->lane_shift[0][0][0], kShWords);
+  __syncthreads();
+  const uint32_t* sh = s_sh;
+  const int lane = threadIdx.x & 63;
+  const uint32_t* bp = s_bp + (lane & (kRep - 1));
+  uint32_t* tiles = scratch + kCrcScratchHeader;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t nwaves = gridDim.x * kBpWaves;
+  uint32_t s = 0;
+  for (uint32_t gt = blockIdx.x * kBpWaves + wave; gt < b.total_tiles; gt += nwaves) {
+    while (s + 1 < b.nseg && b.seg[s + 1].tile_base <= gt) ++s;
+    uint4 v[R * kCrcChunkPieces];
+    load_tile<R>(b, s, gt, lane, v);
+    __builtin_amdgcn_sched_barrier(0);
+    // the R chunks as R independent chains, interleaved (a slice-by-4 chain
+    // is 16 dependent lookups per 64-byte chunk), then combined: a chunk's
+    // register moves 4096 B (the 4032-byte gap + the next 64-byte chunk)
+    // before the next chunk's is XORed in
+    uint32_t st[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) st[k] = 0;
+#pragma unroll
+    for (int j = 0; j < kCrcChunkPieces; ++j) {
+#pragma unroll
+      for (int k = 0; k < R; ++k) st[k] = step4_bp<kRep>(bp, st[k] ^ v[k * kCrcChunkPieces + j].x);
+#pragma unroll
+      for (int k = 0; k < R; ++k) st[k] = step4_bp<kRep>(bp, st[k] ^ v[k * kCrcChunkPieces + j].y);
+#pragma unroll
+      for (int k = 0; k < R; ++k) st[k] = step4_bp<kRep>(bp, st[k] ^ v[k * kCrcChunkPieces + j].z);
+#pragma unroll
+      for (int k = 0; k < R; ++k) st[k] = step4_bp<kRep>(bp, st[k] ^ v[k * kCrcChunkPieces + j].w);
+    }
+    uint32_t state = st[0];
+#pragma unroll
+    for (int k = 1; k < R; ++k) state = shift4(sh, shift4(sh + 6 * 1024, state)) ^ st[k];
+    const uint32_t c = wave_tree(state, sh, lane);
+    if (lane == 0) tiles[gt] = c;
   }
 }
 
@@ -902,6 +976,16 @@ void launch_crc32c_batch(const CrcBatch& b, const CrcTables* d_tables, uint32_t*
     uint32_t g = (b.total_tiles + 3) / 4;
     if (g > 2048) g = 2048;
     hipLaunchKernelGGL(crc32c_mfma_tiles_kernel, dim3(g), dim3(256), 0, stream, b, d_tables, d_scratch);
+  } else if (o.bank_private) {
+    // a persistent grid: one workgroup per CU (128 KiB of tables each)
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const uint32_t need = (b.total_tiles + kBpWaves - 1) / kBpWaves;
+    const uint32_t g = std::max<uint32_t>(1, std::min<uint32_t>(need, static_cast<uint32_t>(std::max(cus, 1))));
+    if (small)
+      hipLaunchKernelGGL((crc32c_tiles_bp_kernel<1, 32>), dim3(g), dim3(kBpThreads), 0, stream, b, d_tables, d_scratch);
+    else
+      hipLaunchKernelGGL((crc32c_tiles_bp_kernel<4, 32>), dim3(g), dim3(kBpThreads), 0, stream, b, d_tables, d_scratch);
   } else if (small)
     hipLaunchKernelGGL((crc32c_tiles_kernel<1, false>), dim3(blocks), dim3(kThreads), 0, stream, b, d_tables,
                        d_scratch, d_results);

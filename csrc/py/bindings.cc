@@ -1106,8 +1106,10 @@ PYBIND11_MODULE(_native, m) {
     o.nibble_tables = get_or<bool>(d, "nibble_tables", o.nibble_tables);
     o.mfma = get_or<bool>(d, "mfma", o.mfma);
     o.slice8 = get_or<bool>(d, "slice8", o.slice8);
+    o.bank_private = get_or<bool>(d, "bank_private", o.bank_private);
     set_crc_launch_options(o);
     py::dict r;
+    r["bank_private"] = o.bank_private;
     r["slot_kernel"] = o.slot_kernel;
     r["slot_waves"] = o.slot_waves;
     r["xor_arrival"] = o.xor_arrival;

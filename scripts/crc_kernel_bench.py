@@ -22,6 +22,8 @@ n = pkg._native
 
 
 def main():
+    if os.environ.get("CRC_OPTS"):  # e.g. '{"bank_private": true}' (CrcLaunchOptions)
+        print(json.dumps({"crc_options": n.set_crc_options(json.loads(os.environ["CRC_OPTS"]))}), flush=True)
     total = int(os.environ.get("CRC_BYTES", 1 << 30))
     iters = int(os.environ.get("CRC_ITERS", 20))
     t = torch.randint(0, 256, (total,), dtype=torch.uint8, device="cuda:0")

@@ -21,13 +21,21 @@ def test_gpu_crc_matches_host(native, gpu_available, n, misalign):
     assert got == native.crc32c(data)
 
 
-def test_gpu_crc_large_multi_segment(native, gpu_available):
+@pytest.mark.parametrize("bank_private", [False, True])
+def test_gpu_crc_large_multi_segment(native, gpu_available, bank_private):
+    """> 1 GiB through the bulk (non-fused) tile kernels: the bank-private
+    slice-by-4 default (CrcLaunchOptions::bank_private) and slice-by-16."""
     import torch
 
     n = (1 << 30) + 12345  # > 1 GiB: several kernel segments combined on host
     t = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda:0")
     host = t.cpu().numpy().tobytes()
-    assert native.gpu_crc32c(0, t.data_ptr(), n) == native.crc32c(host)
+    defaults = native.set_crc_options({})
+    try:
+        native.set_crc_options({"bank_private": bank_private})
+        assert native.gpu_crc32c(0, t.data_ptr(), n) == native.crc32c(host)
+    finally:
+        native.set_crc_options(defaults)
 
 
 def test_fill_and_verify_pattern(native, gpu_available):
@@ -48,7 +56,8 @@ def test_fill_and_verify_pattern(native, gpu_available):
 @pytest.mark.parametrize("opts", [{"slot_waves": 1}, {"xor_arrival": False}, {"slot_waves": 8},
                                   {"nibble_tables": True}, {"slot_kernel": False}, {"mfma": True},
                                   {"slice8": False}, {"slice8": False, "slot_waves": 1},
-                                  {"slice8": False, "xor_arrival": False}, {"slice8": True}])
+                                  {"slice8": False, "xor_arrival": False}, {"slice8": True},
+                                  {"bank_private": False}, {"bank_private": True}])
 def test_crc_kernel_variants(native, gpu_available, opts):
     """Every CRC kernel variant (gpu/crc32c_gpu.h CrcLaunchOptions) against
     the host CRC32C.  One wave per workgroup on 600 - 1024 tiles puts more

@@ -300,6 +300,9 @@ int main(int argc, char** argv) {
       if (hipExtMallocWithFlags(reinterpret_cast<void**>(&vland), a.slot * a.slots * 8, hipDeviceMallocFinegrained) ==
           hipSuccess)
         vland_ok = host_writable(vland);
+      std::printf("{\"vram\": \"relay\", \"allocated\": %s, \"host_writable\": %s}\n", vland ? "true" : "false",
+                  vland_ok ? "true" : "false");
+      std::fflush(stdout);
       break;
     }
   std::thread sub([&] {

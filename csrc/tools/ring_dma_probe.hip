@@ -215,6 +215,7 @@ struct Args {
   int reps = 5;
   int writer = -1, submitter = -1, sender = -1;
   int lag = 0;  // the submitter issues slot seq only once seq + lag was posted (lines age out of the L3 first)
+  std::vector<int> rt;  // CPUs for the HIP runtime's own threads (inherited from main at init); empty = as started
   std::vector<std::string> variants{"memcpy/idle", "memcpy/flag", "memcpy/sdma", "rep/idle", "rep/sdma", "nt/sdma"};
 };
 
@@ -234,6 +235,15 @@ Args parse(int argc, char** argv) {
     else if (k == "submitter") a.submitter = std::atoi(v.c_str());
     else if (k == "sender") a.sender = std::atoi(v.c_str());
     else if (k == "lag") a.lag = std::atoi(v.c_str());
+    else if (k == "rt") {
+      std::stringstream ss(v);
+      std::string x;
+      while (std::getline(ss, x, ',')) {
+        const size_t d = x.find('-');
+        const int lo = std::atoi(x.c_str()), hi = d == std::string::npos ? lo : std::atoi(x.c_str() + d + 1);
+        for (int c = lo; c <= hi; ++c) a.rt.push_back(c);
+      }
+    }
     else if (k == "variants") {
       a.variants.clear();
       std::stringstream ss(v);
@@ -252,7 +262,23 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "bad geometry\n");
     return 2;
   }
+  if (!a.rt.empty()) {
+    // the runtime's threads (created during init) inherit this mask; ours re-pin
+    cpu_set_t m;
+    CPU_ZERO(&m);
+    for (int c : a.rt) CPU_SET(c, &m);
+    sched_setaffinity(0, sizeof(m), &m);
+  }
   check(hipSetDevice(0), "hipSetDevice");
+  check(hipFree(nullptr), "hip init");
+  // first touch of the source and the ring on the writer's NUMA node (the
+  // endpoint builds its send source on its own node, the sink its ring on the
+  // receiving thread's): an unpinned main thread put them anywhere, and a
+  // remote source cost the receive copy ~25% on one box
+  cpu_set_t main_mask;
+  CPU_ZERO(&main_mask);
+  sched_getaffinity(0, sizeof(main_mask), &main_mask);
+  pin(a.writer);
   // the source: THP, faulted in, larger than the L3 (the receive copy's
   // source is the sender's pages, not cache-resident)
   uint8_t* src = static_cast<uint8_t*>(mmap(nullptr, a.src_bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS,
@@ -263,6 +289,7 @@ int main(int argc, char** argv) {
   uint8_t* ring = nullptr;
   check(hipHostMalloc(reinterpret_cast<void**>(&ring), a.slot * a.slots, hipHostMallocDefault), "hipHostMalloc ring");
   std::memset(ring, 0, a.slot * a.slots);
+  sched_setaffinity(0, sizeof(main_mask), &main_mask);
   uint8_t* ring_d = nullptr;
   check(hipHostGetDevicePointer(reinterpret_cast<void**>(&ring_d), ring, 0), "hipHostGetDevicePointer ring");
   uint32_t* flags = nullptr;

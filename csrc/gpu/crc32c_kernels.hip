@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <mutex>
@@ -978,8 +979,16 @@ void launch_crc32c_batch(const CrcBatch& b, const CrcTables* d_tables, uint32_t*
     hipLaunchKernelGGL(crc32c_mfma_tiles_kernel, dim3(g), dim3(256), 0, stream, b, d_tables, d_scratch);
   } else if (o.bank_private) {
     // a persistent grid: one workgroup per CU (128 KiB of tables each)
+    static std::atomic<int> cu_count[64];  // per device, 0 = not asked yet
     int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
+      cus = cu_count[dev].load(std::memory_order_relaxed);
+      if (cus <= 0) {
+        cus = 256;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        cu_count[dev].store(cus, std::memory_order_relaxed);
+      }
+    }
     const uint32_t need = (b.total_tiles + kBpWaves - 1) / kBpWaves;
     const uint32_t g = std::max<uint32_t>(1, std::min<uint32_t>(need, static_cast<uint32_t>(std::max(cus, 1))));
     if (small)

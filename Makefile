@@ -67,8 +67,8 @@ $(PKG)/bin/ring_dma_probe: csrc/tools/ring_dma_probe.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O2 -std=c++17 -o $@ $< -L/opt/rocm/lib -lamdhip64 -pthread -Wl,-rpath,/opt/rocm/lib
 
 $(PKG)/bin/%: csrc/tools/%.cc $(BUILD)/libgcsbcore.a
-	@mkdir -p $(PKG)/bin
-	$(CXX) $(CPPFLAGS) $(CXXFLAGS) -o $@ $< $(BUILD)/libgcsbcore.a $(LDLIBS)
+	@mkdir -p $(PKG)/bin $(BUILD)/tools
+	$(CXX) $(CPPFLAGS) $(CXXFLAGS) -MMD -MP -MF $(BUILD)/tools/$*.d -MT $@ -o $@ $< $(BUILD)/libgcsbcore.a $(LDLIBS)
 
 # Host-side sanitizer builds of the C++ core + a concurrency stress driver
 # (csrc/tests/stress.cc).  GPU code is not sanitized (no GPU ASan on this pool).
@@ -104,4 +104,4 @@ stress: $(BUILD)/plain/stress
 clean:
 	rm -rf $(BUILD) $(EXT) $(TOOL_BINS) $(PROBE_BINS)
 
--include $(CORE_OBJS:.o=.d) $(GPU_OBJS:.o=.d) $(PY_OBJS:.o=.d)
+-include $(CORE_OBJS:.o=.d) $(GPU_OBJS:.o=.d) $(PY_OBJS:.o=.d) $(wildcard $(BUILD)/tools/*.d)

@@ -241,3 +241,32 @@ def test_fit_line_never_exceeds_the_limit():
     line = rp.fit_line(out, {"b": {"ok": True, "mib_s": 1.0}})
     assert len(json.dumps(line).encode()) <= rp.LINE_LIMIT or set(rp.DRIVER_KEYS) <= set(line)
     assert "value" in line
+
+
+def test_rocprof_db_summary_reads_the_sqlite_views(tmp_path):
+    """scripts/rocprof_db_summary.py over a database with rocprofv3's
+    `kernels` and `memory_copies` views: per-name calls, times and sizes."""
+    import sqlite3
+
+    d = tmp_path / "prof" / "host"
+    d.mkdir(parents=True)
+    c = sqlite3.connect(d / "run_results.db")
+    c.execute("create table kernels (name text, duration integer)")
+    c.execute("create table memory_copies (name text, duration integer, size integer)")
+    c.executemany("insert into kernels values (?, ?)", [("crc32c_slot_kernel", 8000), ("crc32c_slot_kernel", 9000),
+                                                         ("fill", 1000)])
+    c.executemany("insert into memory_copies values (?, ?, ?)",
+                  [("MEMORY_COPY_HOST_TO_DEVICE", 28000, 1 << 20)] * 4)
+    c.commit()
+    c.close()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "rocprof_db_summary.py"), str(tmp_path)],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout)[0]
+    k = {x["name"]: x for x in out["kernels"]}
+    assert k["crc32c_slot_kernel"]["calls"] == 2 and k["crc32c_slot_kernel"]["avg_us"] == 8.5
+    m = out["memory_copies"][0]
+    assert m["calls"] == 4 and m["mean_kib"] == 1024.0 and m["avg_us"] == 28.0
+    md = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "rocprof_db_summary.py"), str(tmp_path), "--md"],
+                        capture_output=True, text=True, timeout=60)
+    assert md.returncode == 0 and "| `crc32c_slot_kernel` | 2 |" in md.stdout

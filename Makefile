@@ -37,7 +37,7 @@ EXT := $(PKG)/_native$(EXT_SUFFIX)
 TOOLS := fakegcs read_operation ssd_test write_operations list_operation open_file small_poc loopback_ceiling
 TOOL_BINS := $(addprefix $(PKG)/bin/,$(TOOLS))
 # experiment probes (not part of the default build): make probes
-PROBES := splice_probe
+PROBES := splice_probe zc_probe
 PROBE_BINS := $(addprefix $(PKG)/bin/,$(PROBES)) $(PKG)/bin/ring_dma_probe
 
 .PHONY: all clean ext tools probes asan tsan stress

@@ -69,6 +69,9 @@ def build_parser() -> argparse.ArgumentParser:
                          "still in the receiving CCD's L3; against 8 x 2 MiB the receive copy went 0.046 -> 0.036 "
                          "CPU-s/GiB, 22.0k -> 27.5k MiB/s interleaved (profiles/r4_main8, profiles/r4_recvcost)")
     ap.add_argument("--slots", type=int, default=4)
+    ap.add_argument("--ring-wc", default="off", choices=["on", "off"],
+                    help="the headline sink's ring in write-combined pinned memory (the receive copy's stores skip "
+                         "the CPU caches); A/B against the cached ring")
     ap.add_argument("--conn-ring", default="4x1MiB",
                     help="GPU sink on one multiplexed gRPC connection (list_read_grpc, ref_default_100m_grpc_gpu): "
                          "every worker's stream through one connection ring of SLOTSxBYTES instead of a ring per "

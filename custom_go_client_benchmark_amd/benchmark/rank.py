@@ -335,6 +335,7 @@ class RankBench:
             "device": self.gpu if self.use_gpu else 0,
             "ring_slot_bytes": parse_size(args.slot_bytes),
             "ring_slots": args.slots,
+            "ring_wc": getattr(args, "ring_wc", "off") == "on",
             "conn_ring": args.conn_ring != "off",
             "conn_ring_inplace": args.conn_ring_inplace == "on",
             "conn_ring_slots": int(args.conn_ring.partition("x")[0]) if "x" in args.conn_ring else 4,

@@ -19,7 +19,7 @@ CXXFLAGS := $(CXXSTD) $(OPT) $(HOSTARCH) $(WARN) -fPIC -pthread $(EXTRA_CXXFLAGS
 HIPFLAGS := $(CXXSTD) $(OPT) --offload-arch=$(ARCH) -fPIC -pthread -Icsrc -munsafe-fp-atomics $(EXTRA_HIPFLAGS)
 LDLIBS   := -lssl -lcrypto -lpthread
 
-CORE_SRCS := csrc/core/crc32c.cc csrc/core/affinity.cc csrc/core/ceiling.cc csrc/core/hugebuf.cc csrc/core/content.cc csrc/core/util.cc csrc/core/json.cc csrc/core/sched_probe.cc csrc/core/waker.cc \
+CORE_SRCS := csrc/core/crc32c.cc csrc/core/affinity.cc csrc/core/ceiling.cc csrc/core/hugebuf.cc csrc/core/content.cc csrc/core/util.cc csrc/core/json.cc csrc/core/sched_probe.cc \
              csrc/net/socket.cc csrc/net/tcp_chrono.cc csrc/net/buffered.cc \
              csrc/http1/http1.cc csrc/h2/hpack.cc csrc/h2/h2.cc csrc/h2/h2_client.cc csrc/proto/storage_v2.cc \
              csrc/storage/sink.cc csrc/storage/sliced.cc csrc/storage/auth.cc csrc/storage/client.cc csrc/storage/http_client.cc \

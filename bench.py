@@ -181,9 +181,6 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--list-rcvbuf", default="64MiB",
                     help="config-3 list-read blocks: client SO_RCVBUF (0 = kernel autotuning; 64 MiB as the headline, "
                          "profiles/r3_w48_tail)")
-    ap.add_argument("--mux-notify-us", type=int, default=0,
-                    help="multiplexed gRPC blocks: > 0 = stream-end wake-ups leave the connection's reader thread "
-                         "for a notifier thread polling every N us (core/waker.h); 0 = the reader wakes the worker")
     ap.add_argument("--mux-reader", default="shared", choices=["shared", "isolate"],
                     help="multiplexed blocks (list_read_grpc, ref_default_grpc): isolate gives the connection's "
                          "reader thread a physical core the workers and endpoint do not use (affinity.isolate_reader)")

@@ -78,7 +78,6 @@ ClientConfig client_from(const py::dict& d) {
   if (d.contains("cpus") && !d["cpus"].is_none()) c.cpus = d["cpus"].cast<std::vector<int>>();
   if (d.contains("reader_cpus") && !d["reader_cpus"].is_none())
     c.reader_cpus = d["reader_cpus"].cast<std::vector<int>>();
-  c.notify_poll_us = get_or<int>(d, "notify_poll_us", c.notify_poll_us);
   std::string auth = get_or<std::string>(d, "auth", "none");
   if (auth == "static") {
     c.token = std::make_shared<StaticTokenSource>(get_or<std::string>(d, "token", ""));

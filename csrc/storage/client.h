@@ -46,10 +46,6 @@ struct ClientConfig {
   // gRPC, pool size 1: the connection's reader recv()s into this arena and
   // hands payload to the sinks in place (gpu/engine.h ConnRing); not owned
   RecvArena* recv_arena = nullptr;
-  // gRPC: > 0 = stream-end / deferred-sink wake-ups leave the connection's
-  // reader thread for a notifier thread polling every notify_poll_us
-  // (core/waker.h); 0 = the reader notifies the worker itself
-  int notify_poll_us = 0;
 };
 
 struct ObjectMeta {

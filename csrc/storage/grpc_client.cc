@@ -15,12 +15,10 @@
 #include <condition_variable>
 #include <cstring>
 #include <functional>
-#include <memory>
 #include <mutex>
 
 #include "core/crc32c.h"
 #include "core/util.h"
-#include "core/waker.h"
 #include "h2/h2_client.h"
 #include "proto/storage_v2.h"
 #include "proto/wire.h"
@@ -98,11 +96,9 @@ class BufferingHandler : public MessageHandler {
   std::vector<std::string> msgs_;
 };
 
-class GrpcCall : public H2ClientStream, public std::enable_shared_from_this<GrpcCall> {
+class GrpcCall : public H2ClientStream {
  public:
-  // waker: completion wake-ups go through its notifier thread instead of a
-  // futex call on the connection's reader (core/waker.h); null = direct
-  explicit GrpcCall(MessageHandler* h, Waker* waker = nullptr) : handler_(h), waker_(waker) {}
+  explicit GrpcCall(MessageHandler* h) : handler_(h) {}
 
   // The reader thread dispatches into this call holding a reference to it
   // (H2ClientConn::acquire), so the end-of-stream wake can follow the unlock:
@@ -113,7 +109,7 @@ class GrpcCall : public H2ClientStream, public std::enable_shared_from_this<Grpc
       std::lock_guard<std::mutex> lk(mu_);
       headers_locked(h, end_stream);
     }
-    if (end_stream) wake_waiters();
+    if (end_stream) cv_.notify_all();
   }
 
   void headers_locked(const HeaderList& h, bool end_stream) {
@@ -183,7 +179,7 @@ class GrpcCall : public H2ClientStream, public std::enable_shared_from_this<Grpc
         }
         done_ = true;
       }
-      wake_waiters();  // after the unlock, as in on_headers
+      cv_.notify_all();  // after the unlock, as in on_headers
     }
   }
 
@@ -208,11 +204,9 @@ class GrpcCall : public H2ClientStream, public std::enable_shared_from_this<Grpc
   // The reader thread has queued work for the waiting worker (a deferred
   // sink's message end): wake it.
   void poke() {
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      poked_ = true;
-    }
-    wake_waiters();
+    std::lock_guard<std::mutex> lk(mu_);
+    poked_ = true;
+    cv_.notify_all();
   }
 
   // Waits for completion; throws a StorageError for any non-OK outcome.
@@ -269,14 +263,7 @@ class GrpcCall : public H2ClientStream, public std::enable_shared_from_this<Grpc
     done_ = true;
     cv_.notify_all();
   }
-  // The waiter's predicate was made true under mu_: wake it, from the
-  // notifier thread when there is one (this call stays alive until then).
-  void wake_waiters() {
-    if (waker_) waker_->post(shared_from_this(), &cv_);
-    else cv_.notify_all();
-  }
   MessageHandler* handler_;
-  Waker* waker_;
   uint8_t prefix_[5];
   uint32_t have_ = 0;
   uint32_t msg_left_ = 0;
@@ -595,7 +582,6 @@ class GrpcStorageClient : public StorageClient {
     opt_.cpus = cfg.reader_cpus.empty() ? cfg.cpus : cfg.reader_cpus;
     // one arena, one reader: only a pool of one connection receives into it
     if (cfg.grpc_conn_pool_size == 1) opt_.recv_arena = cfg.recv_arena;
-    if (cfg.notify_poll_us > 0) waker_ = std::make_unique<Waker>(cfg.cpus, cfg.notify_poll_us);
     // DirectPath (reference main.go:106-117: GOOGLE_CLOUD_ENABLE_DIRECT_PATH_XDS
     // is set only around NewGRPCClient, with the google-c2p xDS resolver and
     // the RLS balancer linked in).  DirectPath needs the GCE metadata server,
@@ -688,7 +674,7 @@ class GrpcStorageClient : public StorageClient {
     GrpcCall* raw = nullptr;
     auto c = conn();
     ReadObjectHandler h(sink, rr, delivered, full, &raw, limit >= 0 ? *delivered + limit : ~0ull);
-    auto call = std::make_shared<GrpcCall>(&h, waker_.get());
+    auto call = std::make_shared<GrpcCall>(&h);
     raw = call.get();
     std::string f = frame(v2::encode_read_request(q));
     try {
@@ -893,8 +879,6 @@ class GrpcStorageClient : public StorageClient {
   H2ClientOptions opt_;
   int idle_ms_ = 0;
   std::mutex mu_;
-  // before conns_: destroyed after them, so no reader thread outlives it
-  std::unique_ptr<Waker> waker_;
   std::vector<std::shared_ptr<H2ClientConn>> conns_;
   std::atomic<uint64_t> rr_{0};
 };

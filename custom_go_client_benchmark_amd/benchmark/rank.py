@@ -893,8 +893,7 @@ class RankBench:
         over = {"protocol": proto, "endpoint": ep.url if ep is not None else "", "workers": workers,
                 "object_names": names or [f"c3_rank{rank}/file_0"], "cpus": sh["client"], "worker_id_offset": 0,
                 "rcvbuf": parse_size(args.list_rcvbuf), "ring_slots": int(lslots), "ring_slot_bytes": parse_size(lbytes),
-                "ring_wc": args.list_ring_wc == "on", "reader_cpus": sh.get("reader_cpus"),
-                "notify_poll_us": getattr(args, "mux_notify_us", 0) if proto != "http" else 0}
+                "ring_wc": args.list_ring_wc == "on", "reader_cpus": sh.get("reader_cpus")}
         st = self.read_block(over, per_pass, per_pass * warmup_passes, f"{proto} list-read", endpoint=ep)
         if err:
             st["error"] = err
@@ -994,8 +993,7 @@ class RankBench:
         over = {"protocol": proto, "endpoint": ep.url if ep is not None else "", "workers": workers,
                 "object_prefix": prefix, "worker_id_offset": self.rank * workers, "sink": sink,
                 "host_crc": sink != "gpu", "cpus": sh["client"], "rcvbuf": 0, "grpc_conn_pool_size": 1,
-                "reader_cpus": sh.get("reader_cpus"),
-                "notify_poll_us": getattr(args, "mux_notify_us", 0) if proto != "http" else 0}
+                "reader_cpus": sh.get("reader_cpus")}
         if sink == "gpu":
             rs, _, rb = args.ref_gpu_ring.partition("x")
             over.update(ring_slots=int(rs), ring_slot_bytes=parse_size(rb), landing="object")

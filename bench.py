@@ -181,6 +181,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--list-rcvbuf", default="64MiB",
                     help="config-3 list-read blocks: client SO_RCVBUF (0 = kernel autotuning; 64 MiB as the headline, "
                          "profiles/r3_w48_tail)")
+    ap.add_argument("--mux-send", default="shared", choices=["shared", "isolate"],
+                    help="multiplexed gRPC blocks: the endpoint's send thread on a physical core of its own "
+                         "(isolate) or on the shared set")
     ap.add_argument("--mux-reader", default="shared", choices=["shared", "isolate"],
                     help="multiplexed blocks (list_read_grpc, ref_default_grpc): isolate gives the connection's "
                          "reader thread a physical core the workers and endpoint do not use (affinity.isolate_reader)")

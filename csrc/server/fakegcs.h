@@ -48,6 +48,9 @@ struct ServerConfig {
   // memory cannot be had): profiles/r3_splice/thp_source
   bool send_vmsplice = true;
   std::vector<int> cpus;   // pin connection/handler threads (empty = unpinned)
+  // gRPC connections' send-scheduler threads (empty = cpus): one core of
+  // their own, off the multiplexed reader's and the workers' cores
+  std::vector<int> send_cpus;
   // HTTP/2: DATA frame cap while several streams share a connection
   // (H2Writer::set_quantum and the send scheduler's turn; 0 = a whole
   // message per turn).  ReadObject messages are <= 2 MiB and the scheduler

@@ -623,7 +623,7 @@ class H2ServerConn {
   }
 
   void sender_loop() {
-    pin_current_thread(srv_.config().cpus);
+    pin_current_thread(srv_.config().send_cpus.empty() ? srv_.config().cpus : srv_.config().send_cpus);
     name_current_thread("gcsb-srv-send");
     std::unique_lock<std::mutex> lk(smu_);
     size_t blocked = 0;  // consecutive turns that found no window

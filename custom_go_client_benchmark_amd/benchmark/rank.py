@@ -719,7 +719,8 @@ class RankBench:
                 # the other two (profiles/r3_write/placement)
                 pl = self.affinity.plan(gpu, "pair", self.slot)
                 sh = {"client": pl["client"], "server": sorted(pl["server"] + pl.get("aux", []))}
-                ep = n.Server({"port": 0, "md5": False, "cpus": sh["server"], "retain_uploads": False})
+                ep = n.Server({"port": 0, "md5": False, "cpus": sh["server"], "send_cpus": sh.get("send_cpus"),
+                               "retain_uploads": False})
                 ep.start()
             else:
                 ep, sh = self.share_endpoint()
@@ -872,11 +873,14 @@ class RankBench:
         sh = self.affinity.plan(self.gpu, "same", self.slot) if self.use_gpu else {"client": [], "server": []}
         if self.use_gpu and proto != "http" and args.mux_reader == "isolate":
             sh = self.affinity.isolate_reader(sh)
+        if self.use_gpu and proto != "http" and getattr(args, "mux_send", "shared") == "isolate":
+            sh = self.affinity.isolate_sender(sh)
         ep = None
         names, list_ms, err = [], 0.0, ""
         rank = self.rank
         try:
-            ep = n.Server({"port": 0, "md5": False, "cpus": sh["server"], "retain_uploads": False})
+            ep = n.Server({"port": 0, "md5": False, "cpus": sh["server"], "send_cpus": sh.get("send_cpus"),
+                           "retain_uploads": False})
             ep.start()
             ep.add_synthetic(self.bucket, f"c3_rank{rank}/file_", "", 0, nobj, 1 << 20)
             lister = n.Client({"protocol": proto, "endpoint": ep.url, "retry_initial_s": 0.05})
@@ -981,11 +985,14 @@ class RankBench:
         sh = self.affinity.plan(self.gpu, mode, self.slot) if self.use_gpu else {"client": [], "server": []}
         if self.use_gpu and proto != "http" and args.mux_reader == "isolate":
             sh = self.affinity.isolate_reader(sh)
+        if self.use_gpu and proto != "http" and getattr(args, "mux_send", "shared") == "isolate":
+            sh = self.affinity.isolate_sender(sh)
         ep = None
         err = ""
         prefix = "ref_default/file_" if osz == parse_size(args.ref_object_size) else f"ref_default_{osz >> 20}m/file_"
         try:
-            ep = n.Server({"port": 0, "md5": False, "cpus": sh["server"], "retain_uploads": False})
+            ep = n.Server({"port": 0, "md5": False, "cpus": sh["server"], "send_cpus": sh.get("send_cpus"),
+                           "retain_uploads": False})
             ep.start()
             ep.add_synthetic(self.bucket, prefix, "", self.rank * workers, workers, osz)
         except Exception as e:  # noqa: BLE001

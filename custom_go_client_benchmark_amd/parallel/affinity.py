@@ -332,6 +332,27 @@ def isolate_reader(pl: dict, min_cores: int = 3) -> dict:
     return out
 
 
+def isolate_sender(pl: dict, min_cores: int = 4) -> dict:
+    """A copy of plan `pl` whose endpoint gets one physical core for its
+    gRPC send threads alone ("send_cpus"; ServerConfig::send_cpus): the
+    quietest client core other than the reader's, taken out of the client
+    and server sets, SMT sibling included.  On one connection the endpoint's
+    send thread also runs the loopback receive processing of every byte, so
+    it competes with the workers on a shared L3 domain.  Unchanged when the
+    client set has fewer than `min_cores` physical cores."""
+    client = list(pl.get("client") or [])
+    taken = set(pl.get("reader_cpus") or [])
+    cores = [c for c in (quiet_cores(client, cpu_busy(0.05)) if client else []) if not taken & set(c)]
+    if len(cores) < min_cores - 1:
+        return dict(pl)
+    core = cores[0]
+    out = dict(pl)
+    out["send_cpus"] = [core[0]]
+    out["client"] = [c for c in client if c not in core]
+    out["server"] = [c for c in (pl.get("server") or []) if c not in core] or list(out["client"])
+    return out
+
+
 def visible_gpu_summary() -> list[dict]:
     out = []
     for d in range(_native.gpu_device_count()):

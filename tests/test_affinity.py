@@ -259,6 +259,31 @@ def test_isolate_reader_gives_the_reader_a_whole_core(monkeypatch):
     assert a.isolate_reader(small) == small
 
 
+def test_isolate_sender_takes_another_whole_core(monkeypatch):
+    """After isolate_reader, the endpoint's send threads get one hardware
+    thread of the next quietest core: not the reader's core, and neither the
+    workers nor the endpoint's other threads keep either thread of it."""
+    from custom_go_client_benchmark_amd.parallel import affinity as a
+
+    _fake_topology(monkeypatch, a)
+    busy = {c: 0.0 for c in range(16)}
+    monkeypatch.setattr(a, "cpu_busy", lambda sample_s=0.15: busy)
+    pl = {"client": list(range(16)), "server": list(range(16)), "mode": "same"}
+    rd = a.isolate_reader(pl)
+    out = a.isolate_sender(rd)
+    (s,) = out["send_cpus"]
+    (r,) = out["reader_cpus"]
+    score = {c for c in range(16) if a._same_core(c, s)}
+    rcore = {c for c in range(16) if a._same_core(c, r)}
+    assert len(score) == 2 and not score & rcore
+    assert not score & set(out["client"]) and not score & set(out["server"])
+    assert set(out["client"]) | score | rcore == set(range(16))
+    assert rd.get("send_cpus") is None  # the input plan is not modified
+    # too few cores to spare another one: unchanged
+    small = {"client": [2, 10, 3, 11], "server": [2, 10, 3, 11], "reader_cpus": [4]}
+    assert a.isolate_sender(small) == small
+
+
 def test_fd_table_reserved(native):
     import resource
 

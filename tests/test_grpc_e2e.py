@@ -32,6 +32,21 @@ def test_small_messages_many_frames(native):
         srv.stop()
 
 
+def test_send_threads_on_their_own_cpus(native):
+    """ServerConfig::send_cpus pins the gRPC send threads apart from the
+    endpoint's other threads (bench --mux-send isolate); reads stay exact."""
+    cpus = sorted(os.sched_getaffinity(0))
+    srv = native.Server({"port": 0, "cpus": cpus[:1], "send_cpus": cpus[-1:]})
+    srv.start()
+    try:
+        srv.add_synthetic(B, P, "", 0, 1, 3 * (1 << 20) + 5)
+        c = native.Client({"protocol": "grpc", "endpoint": srv.url})
+        assert c.read_bytes(B, P + "0") == native.object_bytes(P + "0", 0, 3 * (1 << 20) + 5)
+        assert c.read(B, P + "0")["verified"]
+    finally:
+        srv.stop()
+
+
 def test_unavailable_is_retried(native, server):
     server.add_synthetic(B, P, "", 0, 1, 1 << 20)
     server.set_faults({"fail_next": 2, "fail_status": 503})

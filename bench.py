@@ -181,12 +181,15 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--list-rcvbuf", default="64MiB",
                     help="config-3 list-read blocks: client SO_RCVBUF (0 = kernel autotuning; 64 MiB as the headline, "
                          "profiles/r3_w48_tail)")
-    ap.add_argument("--mux-send", default="shared", choices=["shared", "isolate"],
+    ap.add_argument("--mux-send", default="isolate", choices=["shared", "isolate"],
                     help="multiplexed gRPC blocks: the endpoint's send thread on a physical core of its own "
-                         "(isolate) or on the shared set")
-    ap.add_argument("--mux-reader", default="shared", choices=["shared", "isolate"],
+                         "(isolate; ServerConfig::send_cpus) or on the shared set. With --mux-reader isolate: "
+                         "ref_default_grpc 21.1k -> 24.2k MiB/s, list_read_grpc 21.6k -> 22.6k, h2 reader "
+                         "0.046 -> 0.039 CPU-s/GiB, medians of 5 interleaved pairs (profiles/r5_muxiso)")
+    ap.add_argument("--mux-reader", default="isolate", choices=["shared", "isolate"],
                     help="multiplexed blocks (list_read_grpc, ref_default_grpc): isolate gives the connection's "
-                         "reader thread a physical core the workers and endpoint do not use (affinity.isolate_reader)")
+                         "reader thread a physical core the workers and endpoint do not use (affinity.isolate_reader); "
+                         "alone it did not help (profiles/r4_muxiso), with --mux-send isolate it does (r5_muxiso)")
     ap.add_argument("--blocks", default="",
                     help="comma list of side blocks to run (A/B sessions): cpu_baseline, compare, sliced, ceiling, "
                          "ref_default, c1_http_cpu, list_read, write, write_composite, fanout; 'all' = every block; empty = "

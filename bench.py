@@ -134,6 +134,9 @@ def build_parser() -> argparse.ArgumentParser:
                     help="config 3 side block: pinned ring per reader, SLOTSxSLOT_BYTES (1 MiB objects). 2 x 1 MiB "
                          "keeps the 8 readers' receive destinations at 16 MiB: gRPC 18.6-18.8k MiB/s at p50 "
                          "0.42 ms against 15.5-17.0k at 0.46-0.49 with 8 x 2 MiB (profiles/r3_mux_thp/listring)")
+    ap.add_argument("--list-placement", default="same", choices=["same", "split", "share"],
+                    help="list_read_*: one L3 domain for the readers and the endpoint (same), two (split), or the "
+                         "rank's whole share of the node's L3 domains (share)")
     ap.add_argument("--list-ring-wc", default="on", choices=["on", "off"],
                     help="config 3 side block: the readers' rings in write-combined pinned memory (p50 0.346-0.379 "
                          "ms against 0.412-0.519 with cached THP rings, profiles/r3_ring_thp/wc)")

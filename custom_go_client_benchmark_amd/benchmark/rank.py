@@ -870,7 +870,8 @@ class RankBench:
         args, n = self.args, self.n
         nobj, workers = args.list_objects, args.list_workers
         # one L3 domain for the readers and the endpoint (profiles/r2_check_s4b, r2_cli_geometry)
-        sh = self.affinity.plan(self.gpu, "same", self.slot) if self.use_gpu else {"client": [], "server": []}
+        sh = (self.affinity.plan(self.gpu, getattr(args, "list_placement", "same"), self.slot) if self.use_gpu
+              else {"client": [], "server": []})
         if self.use_gpu and proto != "http" and args.mux_reader == "isolate":
             sh = self.affinity.isolate_reader(sh)
         if self.use_gpu and proto != "http" and getattr(args, "mux_send", "shared") == "isolate":

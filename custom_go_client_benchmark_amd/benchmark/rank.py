@@ -1107,6 +1107,17 @@ class RankBench:
                                    {"protocol": p, "sink": "discard", "_conns": 1, "_place": "pair",
                                     "note": "reference semantics: io.Discard + host CRC32C; client + submitter cores"})
             self.stash_headline()
+            if (world == 1 and protocol == "grpc" and args.ref_effective == "on" and want("ref_effective")):
+                # the reference's EFFECTIVE read on the headline config: the
+                # baseline (same endpoint, cores, object and steps) whose
+                # consumer also copies every decoded message out in 8 KiB
+                # reads, as io.Discard.ReadFrom pulls them out of the library's
+                # reader (main.go:123-125,140).  Parity-unpinned.
+                over = {**self.baseline_over(), "discard_read_bytes": 8192}
+                blocks["ref_effective_head"] = (
+                    self.read_block(over, side_steps, side_warm, f"{protocol} effective read (headline config)"),
+                    {"protocol": protocol, "sink": "discard", "_conns": 1, "_place": "pair",
+                     "note": "parity-unpinned: grpc-go's message decode + 8 KiB io.Discard reads, modelled"})
             if other and other in protos and want("compare"):
                 blocks["compare"] = (self.read_block({"protocol": other}, side_steps, side_warm, f"{other} compare"),
                                      {"protocol": other, "sink": self.args.sink, "_conns": 1, "_place": "pair"})
@@ -1417,6 +1428,10 @@ class RankBench:
                 twin = full.get(key[:-len("_gpu")] + "_discard")
                 if twin and twin.get("ok") and twin.get("mib_s"):
                     b["vs_discard_twin"] = round(b["mib_s"] / twin["mib_s"], 3)
+        eff_h = full.get("ref_effective_head")
+        if eff_h and eff_h.get("ok") and eff_h.get("mib_s") and value > 0:
+            # next to, never instead of, vs_baseline (parity-unpinned)
+            out["headline_vs_ref_effective"] = round(value / eff_h["mib_s"], 3)
         eff = full.get("ref_effective_grpc")
         if eff and eff.get("ok") and eff.get("mib_s"):
             for key in ("ref_default_100m_grpc_gpu", "ref_default_100m_grpc_discard"):

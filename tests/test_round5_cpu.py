@@ -168,6 +168,8 @@ def test_bench_line_fits_the_driver_tail(gpus, tmp_path):
         assert line["paired"]["chunks"] == 4 and 0.3 < line["vs_baseline_paired"] < 3.0
         assert len(d["paired"]["windows"]) == 8  # 4 chunks x (head, base): no nodma without a GPU
         assert line["ref_effective_grpc"]["ok"] and line["ref_default_100m_grpc_discard"]["vs_ref_effective"] > 0
+        # the effective-path twin of the headline config, next to vs_baseline
+        assert line["ref_effective_head"]["ok"] and line["headline_vs_ref_effective"] > 0
         assert "host" in d["blocks"]["compare"]
     else:
         assert "paired" not in line and len(line["per_rank_mib_s"]) == 8

@@ -184,6 +184,10 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--list-rcvbuf", default="64MiB",
                     help="config-3 list-read blocks: client SO_RCVBUF (0 = kernel autotuning; 64 MiB as the headline, "
                          "profiles/r3_w48_tail)")
+    ap.add_argument("--fill-bytes", default="16KiB",
+                    help="most bytes one fill of a reader's 16 KiB small-read buffer takes from the socket "
+                         "(SocketOptions::fill_bytes): what a frame-header fill takes of the payload behind it "
+                         "is copied twice")
     ap.add_argument("--mux-send", default="isolate", choices=["shared", "isolate"],
                     help="multiplexed gRPC blocks: the endpoint's send thread on a physical core of its own "
                          "(isolate; ServerConfig::send_cpus) or on the shared set. With --mux-reader isolate: "

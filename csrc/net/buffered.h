@@ -107,7 +107,7 @@ class BufferedConn {
     }
     if (n >= kRefillMin && conn_->recv_refill()) {
       pos_ = end_ = 0;
-      const size_t r = conn_->read_some2(dst, n, buf_.get(), kCap);
+      const size_t r = conn_->read_some2(dst, n, buf_.get(), fill_cap());
       if (r <= n) return r;
       end_ = r - n;
       return n;
@@ -143,9 +143,14 @@ class BufferedConn {
       end_ -= pos_;
       pos_ = 0;
     }
-    size_t r = conn_->read_some(buf_.get() + end_, kCap - end_);
+    const size_t room = kCap - end_;
+    size_t r = conn_->read_some(buf_.get() + end_, room < fill_cap() ? room : fill_cap());
     if (r == 0) throw StorageError("unexpected EOF", true);
     end_ += r;
+  }
+  size_t fill_cap() const {
+    const size_t f = conn_->fill_bytes();
+    return f < 64 ? 64 : (f > kCap ? kCap : f);
   }
   // arena mode: the next window, filled by one recv()
   void afill() {

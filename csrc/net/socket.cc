@@ -242,6 +242,7 @@ std::unique_ptr<Conn> Conn::dial(const Endpoint& ep, const SocketOptions& opt) {
   auto conn = std::make_unique<Conn>();
   conn->fd_ = fd;
   conn->recv_refill_ = opt.recv_refill;
+  conn->fill_bytes_ = opt.fill_bytes;
   if (ep.scheme == "https") {
     SSL* ssl = SSL_new(client_ssl_ctx(opt.tls_verify, opt.tls_ca_file));
     SSL_set_fd(ssl, fd);
@@ -257,6 +258,7 @@ std::unique_ptr<Conn> Conn::dial(const Endpoint& ep, const SocketOptions& opt) {
       SSL_free(ssl);
       conn->fd_ = fd;  // closed by ~Conn
       conn->recv_refill_ = opt.recv_refill;
+  conn->fill_bytes_ = opt.fill_bytes;
       // a certificate failure will not fix itself: not retryable
       throw StorageError("TLS handshake with " + ep.host + " failed" + why, vr == X509_V_OK);
     }
@@ -326,6 +328,7 @@ std::unique_ptr<Conn> Conn::adopt(int fd, const SocketOptions& opt) {
   auto conn = std::make_unique<Conn>();
   conn->fd_ = fd;
   conn->recv_refill_ = opt.recv_refill;
+  conn->fill_bytes_ = opt.fill_bytes;
   return conn;
 }
 

@@ -72,6 +72,7 @@ ClientConfig client_from(const py::dict& d) {
   c.sock.congestion = get_or<std::string>(d, "tcp_congestion", "");
   c.sock.loopback_rto_min = get_or<bool>(d, "loopback_rto_min", false);
   c.sock.recv_refill = get_or<bool>(d, "recv_refill", false);
+  c.sock.fill_bytes = get_or<size_t>(d, "fill_bytes", c.sock.fill_bytes);
   c.sock.tls_verify = get_or<bool>(d, "tls_verify", true);
   c.sock.tls_ca_file = get_or<std::string>(d, "tls_ca_file", "");
   c.project = get_or<std::string>(d, "project", "gcs-fuse-test");

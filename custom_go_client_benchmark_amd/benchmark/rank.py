@@ -354,6 +354,7 @@ class RankBench:
             "tcp_congestion": args.client_cc,
             "loopback_rto_min": True,
             "recv_refill": bool(args.recv_refill),
+            "fill_bytes": parse_size(getattr(args, "fill_bytes", "16KiB")),
         }
         return 0
 

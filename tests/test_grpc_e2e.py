@@ -47,6 +47,18 @@ def test_send_threads_on_their_own_cpus(native):
         srv.stop()
 
 
+@pytest.mark.parametrize("fill", [64, 512, 16384])
+@pytest.mark.parametrize("refill", [False, True])
+def test_small_buffer_fills_stay_exact(native, server, fill, refill):
+    """SocketOptions::fill_bytes caps what a frame-header fill takes of the
+    payload behind it (with and without the payload recv's refill)."""
+    server.add_synthetic(B, "fill/file_", "", 0, 3, 5 * (1 << 20) + 7)
+    c = _c(native, server, fill_bytes=fill, recv_refill=refill)
+    for i in range(3):
+        assert c.read_bytes(B, f"fill/file_{i}") == native.object_bytes(f"fill/file_{i}", 0, 5 * (1 << 20) + 7)
+        assert c.read(B, f"fill/file_{i}")["verified"]
+
+
 def test_unavailable_is_retried(native, server):
     server.add_synthetic(B, P, "", 0, 1, 1 << 20)
     server.set_faults({"fail_next": 2, "fail_status": 503})

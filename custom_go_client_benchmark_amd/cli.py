@@ -201,6 +201,14 @@ def main(argv: list[str] | None = None) -> int:
             if sink == "gpu":
                 raise
             placement = affinity.plan(device, "quota")
+        if (aff == "same" and proto in ("grpc", "http2") and workers > max(1, fs.get("grpc-conn-pool-size"))
+                and fs.get("workload") != "write"):
+            # the connection's one reader and (a node-local endpoint's) send
+            # thread on a physical core each: ref_default_grpc 21.1k -> 24.2k
+            # MiB/s in the bench (profiles/r5_muxiso)
+            placement = affinity.isolate_reader(placement)
+            if fs.get("start-fake-server"):
+                placement = affinity.isolate_sender(placement)
         if fs.get("workload") == "write" and aff == "pair":
             # the endpoint's receive thread and CRC worker get a core each;
             # this (uploading) thread the client core
@@ -218,7 +226,8 @@ def main(argv: list[str] | None = None) -> int:
         n_obj = fs.get("fake-objects") if fs.get("fake-objects") >= 0 else workers
         ep_handle = server.start_inprocess(fs.get("bucket"), fs.get("object-prefix"), fs.get("object-suffix"), first,
                                            n_obj, fs.get("fake-object-size"), md5=True, cpus=placement["server"],
-                                           retain_uploads=fs.get("fake-retain-uploads"))
+                                           retain_uploads=fs.get("fake-retain-uploads"),
+                                           send_cpus=placement.get("send_cpus"))
         endpoint = ep_handle.url
         _err(f"synthetic GCS endpoint {endpoint}: {n_obj} objects of {fs.get('fake-object-size')} bytes")
     if not endpoint:
@@ -253,7 +262,7 @@ def main(argv: list[str] | None = None) -> int:
         slice_min_bytes=fs.get("slice-min-bytes"), slice_piece_bytes=fs.get("slice-piece-bytes"),
         slice_piece_min_bytes=fs.get("slice-piece-min-bytes"),
         trace_sample_rate=fs.get("trace-sample-rate") if fs.get("enable-tracing") else 0.0,
-        cpus=placement["client"], auth=fs.get("auth"), token=fs.get("token"), key_file=fs.get("key-file"),
+        cpus=placement["client"], reader_cpus=placement.get("reader_cpus") or [], auth=fs.get("auth"), token=fs.get("token"), key_file=fs.get("key-file"),
         token_uri=fs.get("token-uri"), user_agent=fs.get("user-agent"), tls_ca_file=fs.get("tls-ca-file"),
         tls_verify=not fs.get("tls-insecure"), retry_initial_s=fs.get("retry-initial"),
         retry_max_s=fs.get("retry-max"), retry_multiplier=fs.get("retry-multiplier"),

@@ -41,6 +41,7 @@ class RunOptions:
     trace_sample_rate: float = 0.0
     stop_on_error: bool = True
     cpus: list = field(default_factory=list)
+    reader_cpus: list = field(default_factory=list)  # multiplexed connections' reader threads (empty = cpus)
     auth: str = "none"                     # none | static | adc | key_file
     token: str = ""
     key_file: str = ""
@@ -73,6 +74,7 @@ class RunOptions:
             "user_agent": self.user_agent, "retry_initial_s": self.retry_initial_s, "retry_max_s": self.retry_max_s,
             "retry_multiplier": self.retry_multiplier, "retry_max_total_s": self.retry_max_total_s,
             "retry_max_attempts": self.retry_max_attempts, "cpus": list(self.cpus),
+            "reader_cpus": list(self.reader_cpus) or None,
             "io_timeout_ms": int(round(self.read_timeout_s * 1000)),
             "tls_ca_file": self.tls_ca_file, "tls_verify": self.tls_verify,
             "tcp_congestion": self.tcp_congestion,

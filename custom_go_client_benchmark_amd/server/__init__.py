@@ -39,9 +39,10 @@ class Endpoint:
 
 def start_inprocess(bucket: str, prefix: str, suffix: str, first: int, count: int, size: int, md5: bool = False,
                     cpus=None, require_auth: bool = False, grpc_chunk: int = 2 << 20,
-                    retain_uploads: bool = True) -> Endpoint:
+                    retain_uploads: bool = True, send_cpus=None) -> Endpoint:
     srv = _native.Server({"port": 0, "md5": md5, "cpus": list(cpus or []), "require_auth": require_auth,
-                          "grpc_chunk": grpc_chunk, "retain_uploads": retain_uploads})
+                          "grpc_chunk": grpc_chunk, "retain_uploads": retain_uploads,
+                          "send_cpus": list(send_cpus or [])})
     srv.start()
     if count > 0:
         srv.add_synthetic(bucket, prefix, suffix, first, count, size)

@@ -397,8 +397,16 @@ class SideBlocks:
             r.update(tcp_gbps=t["gbps"], tcp_recv_cpu_s_per_gib=t["recv_cpu_s_per_gib"],
                      tcp_send_cpu_s_per_gib=t["send_cpu_s_per_gib"], memcpy_gbps=m["gbps"])
             if self.use_gpu:
+                # in the multiplexed blocks' own placement: one L3 domain, the
+                # reader and the endpoint's send thread on cores of their own
+                # when those blocks isolate them (--mux-reader / --mux-send)
                 same = self.affinity.plan(self.gpu, "same", self.slot)
-                r["tcp_gbps_same"] = tcp(same["client"][:1], same["server"])["gbps"]
+                if args.mux_reader == "isolate":
+                    same = self.affinity.isolate_reader(same)
+                if getattr(args, "mux_send", "shared") == "isolate":
+                    same = self.affinity.isolate_sender(same)
+                r["tcp_gbps_same"] = tcp(same.get("reader_cpus") or same["client"][:1],
+                                         same.get("send_cpus") or same["server"])["gbps"]
                 # pinned -> HBM: the best of the sinks' copy patterns (the
                 # headline's 1 MiB x 4 streams, the 48-worker rings' 2 MiB x
                 # 8, big copies); the 48-worker HTTP block beat the first alone

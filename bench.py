@@ -184,6 +184,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--list-rcvbuf", default="64MiB",
                     help="config-3 list-read blocks: client SO_RCVBUF (0 = kernel autotuning; 64 MiB as the headline, "
                          "profiles/r3_w48_tail)")
+    ap.add_argument("--write-split", default="off", choices=["on", "off"],
+                    help="write block (pair placement): the endpoint's receiving thread and its CRC worker each "
+                         "pinned to a core of their own (on) or floating over both (off)")
     ap.add_argument("--fill-bytes", default="16KiB",
                     help="most bytes one fill of a reader's 16 KiB small-read buffer takes from the socket "
                          "(SocketOptions::fill_bytes): what a frame-header fill takes of the payload behind it "

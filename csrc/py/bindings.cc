@@ -620,6 +620,7 @@ class PyServer {
     c.tls_key_file = get_or<std::string>(d, "tls_key_file", "");
     if (d.contains("cpus") && !d["cpus"].is_none()) c.cpus = d["cpus"].cast<std::vector<int>>();
     if (d.contains("send_cpus") && !d["send_cpus"].is_none()) c.send_cpus = d["send_cpus"].cast<std::vector<int>>();
+    if (d.contains("crc_cpus") && !d["crc_cpus"].is_none()) c.crc_cpus = d["crc_cpus"].cast<std::vector<int>>();
     store_ = std::make_shared<ObjectStore>(get_or<bool>(d, "md5", true));
     store_->set_retain_uploads(get_or<bool>(d, "retain_uploads", true));
     srv_ = std::make_unique<FakeGcsServer>(c, store_);

@@ -51,6 +51,9 @@ struct ServerConfig {
   // gRPC connections' send-scheduler threads (empty = cpus): one core of
   // their own, off the multiplexed reader's and the workers' cores
   std::vector<int> send_cpus;
+  // WriteObject CRC32C workers (empty = cpus): a core apart from the
+  // connection thread that receives the upload
+  std::vector<int> crc_cpus;
   // HTTP/2: DATA frame cap while several streams share a connection
   // (H2Writer::set_quantum and the send scheduler's turn; 0 = a whole
   // message per turn).  ReadObject messages are <= 2 MiB and the scheduler

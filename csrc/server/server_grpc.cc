@@ -399,7 +399,7 @@ class H2ServerConn {
   }
 
   void write_worker() {
-    pin_current_thread(srv_.config().cpus);
+    pin_current_thread(srv_.config().crc_cpus.empty() ? srv_.config().cpus : srv_.config().crc_cpus);
     name_current_thread("gcsb-srv-wcrc");
     std::unique_lock<std::mutex> lk(wmu_);
     for (;;) {

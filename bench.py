@@ -184,6 +184,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--list-rcvbuf", default="64MiB",
                     help="config-3 list-read blocks: client SO_RCVBUF (0 = kernel autotuning; 64 MiB as the headline, "
                          "profiles/r3_w48_tail)")
+    ap.add_argument("--ref-grpc-rcvbuf", default="0",
+                    help="ref_default_grpc / ref_default_100m_grpc_* / ref_effective_grpc: the one connection's "
+                         "SO_RCVBUF (0 = kernel autotuning)")
     ap.add_argument("--write-split", default="off", choices=["on", "off"],
                     help="write block (pair placement): the endpoint's receiving thread and its CRC worker each "
                          "pinned to a core of their own (on) or floating over both (off)")

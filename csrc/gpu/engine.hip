@@ -15,9 +15,11 @@
 #include <thread>
 #include <stdexcept>
 
+#include <sched.h>
 #include <sys/mman.h>
 #include <sys/prctl.h>
 #include <time.h>
+#include <unistd.h>
 
 #include "core/affinity.h"
 #include "core/crc32c.h"
@@ -324,7 +326,17 @@ class DeviceSubmitter {
     name_current_thread("gcsb-submit");
     // off the receiving core: inherited from the first posting thread (a
     // pinned transport thread) it would share that core's SMT pair
-    pin_current_thread(submitter_cpus());
+    const std::vector<int> cpus = submitter_cpus();
+    if (cpus.empty()) {
+      // not configured: the process's (main thread's) CPU set, not the first
+      // poster's -- a receive thread pinned to one CPU would otherwise hand
+      // the submitter its own CPU
+      cpu_set_t m;
+      CPU_ZERO(&m);
+      if (sched_getaffinity(getpid(), sizeof m, &m) == 0) sched_setaffinity(0, sizeof m, &m);
+    } else {
+      pin_current_thread(cpus);
+    }
     ensure_device(dev_);
     std::unique_lock<std::mutex> lk(mu_);
     for (;;) {

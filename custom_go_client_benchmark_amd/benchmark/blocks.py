@@ -469,7 +469,11 @@ class SideBlocks:
             err = f"{type(e).__name__}: {e}"
         over = {"protocol": proto, "endpoint": ep.url if ep is not None else "", "workers": workers,
                 "object_prefix": prefix, "worker_id_offset": self.rank * workers, "sink": sink,
-                "host_crc": sink != "gpu", "cpus": sh["client"], "rcvbuf": 0, "grpc_conn_pool_size": 1,
+                "host_crc": sink != "gpu", "cpus": sh["client"],
+                # one gRPC connection: the headline's 64 MiB request is one
+                # socket's worth; 48 HTTP connections keep autotuning
+                "rcvbuf": parse_size(getattr(args, "ref_grpc_rcvbuf", "0")) if proto != "http" else 0,
+                "grpc_conn_pool_size": 1,
                 "reader_cpus": sh.get("reader_cpus")}
         if sink == "gpu":
             rs, _, rb = args.ref_gpu_ring.partition("x")

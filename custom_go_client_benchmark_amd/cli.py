@@ -59,6 +59,8 @@ def build_flags() -> FlagSet:
     fs.bool("conn-ring", True, "-sink gpu on one multiplexed connection (gRPC pool 1, http2): every worker's stream "
             "lands through one 4 x 1 MiB receive ring of the connection instead of a ring per worker "
             "(profiles/r4_ringgeom)")
+    fs.int("rcvbuf", 0, "Client SO_RCVBUF in bytes (0 = kernel autotuning, as the Go client; the bench's headline "
+           "and list-read request 64 MiB, capped by net.core.rmem_max)")
     fs.int("grpc-conn-pool-size", 1, "gRPC connections (reference GrpcConnPoolSize = 1)")
     fs.bool("grpc-directpath", True, "Request DirectPath while creating the gRPC client (reference sets "
             "GOOGLE_CLOUD_ENABLE_DIRECT_PATH_XDS=true around NewGRPCClient; falls back to CloudPath)")
@@ -209,6 +211,9 @@ def main(argv: list[str] | None = None) -> int:
             placement = affinity.isolate_reader(placement)
             if fs.get("start-fake-server"):
                 placement = affinity.isolate_sender(placement)
+            if sink == "gpu" and placement.get("reader_cpus"):
+                # the GPU hand-off thread with the workers, off the reader's core
+                _native.set_submitter_cpus(placement["client"])
         if fs.get("workload") == "write" and aff == "pair":
             # the endpoint's receive thread and CRC worker get a core each;
             # this (uploading) thread the client core
@@ -262,7 +267,8 @@ def main(argv: list[str] | None = None) -> int:
         slice_min_bytes=fs.get("slice-min-bytes"), slice_piece_bytes=fs.get("slice-piece-bytes"),
         slice_piece_min_bytes=fs.get("slice-piece-min-bytes"),
         trace_sample_rate=fs.get("trace-sample-rate") if fs.get("enable-tracing") else 0.0,
-        cpus=placement["client"], reader_cpus=placement.get("reader_cpus") or [], auth=fs.get("auth"), token=fs.get("token"), key_file=fs.get("key-file"),
+        cpus=placement["client"], reader_cpus=placement.get("reader_cpus") or [], rcvbuf=fs.get("rcvbuf"),
+        auth=fs.get("auth"), token=fs.get("token"), key_file=fs.get("key-file"),
         token_uri=fs.get("token-uri"), user_agent=fs.get("user-agent"), tls_ca_file=fs.get("tls-ca-file"),
         tls_verify=not fs.get("tls-insecure"), retry_initial_s=fs.get("retry-initial"),
         retry_max_s=fs.get("retry-max"), retry_multiplier=fs.get("retry-multiplier"),

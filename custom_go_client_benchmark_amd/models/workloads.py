@@ -42,6 +42,7 @@ class RunOptions:
     stop_on_error: bool = True
     cpus: list = field(default_factory=list)
     reader_cpus: list = field(default_factory=list)  # multiplexed connections' reader threads (empty = cpus)
+    rcvbuf: int = 0                        # client SO_RCVBUF (0 = kernel autotuning, as the Go client)
     auth: str = "none"                     # none | static | adc | key_file
     token: str = ""
     key_file: str = ""
@@ -75,6 +76,7 @@ class RunOptions:
             "retry_multiplier": self.retry_multiplier, "retry_max_total_s": self.retry_max_total_s,
             "retry_max_attempts": self.retry_max_attempts, "cpus": list(self.cpus),
             "reader_cpus": list(self.reader_cpus) or None,
+            "rcvbuf": int(self.rcvbuf),
             "io_timeout_ms": int(round(self.read_timeout_s * 1000)),
             "tls_ca_file": self.tls_ca_file, "tls_verify": self.tls_verify,
             "tcp_congestion": self.tcp_congestion,

@@ -46,7 +46,7 @@ run c2_http_256m_cpu 300 -client-protocol http -worker 1 -read-call-per-worker 4
 # config 3: list 1000 x 1 MiB objects, read every one into HBM; HTTP vs gRPC
 for p in http grpc; do
   run c3_${p}_list1000_hbm 300 -workload list-read -client-protocol $p -sink gpu -worker 8 \
-    -read-call-per-worker 3 -fake-objects 1000 -fake-object-size $MIB -affinity numa
+    -read-call-per-worker 3 -fake-objects 1000 -fake-object-size $MIB
   run c3_${p}_list1000_cpu 300 -workload list-read -client-protocol $p -worker 8 \
     -read-call-per-worker 3 -fake-objects 1000 -fake-object-size $MIB
 done

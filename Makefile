@@ -38,7 +38,7 @@ TOOLS := fakegcs read_operation ssd_test write_operations list_operation open_fi
 TOOL_BINS := $(addprefix $(PKG)/bin/,$(TOOLS))
 # experiment probes (not part of the default build): make probes
 PROBES := splice_probe zc_probe
-PROBE_BINS := $(addprefix $(PKG)/bin/,$(PROBES)) $(PKG)/bin/ring_dma_probe
+PROBE_BINS := $(addprefix $(PKG)/bin/,$(PROBES)) $(PKG)/bin/ring_dma_probe $(PKG)/bin/graph_probe
 
 .PHONY: all clean ext tools probes asan tsan stress
 all: ext tools
@@ -65,6 +65,14 @@ $(EXT): $(PY_OBJS) $(GPU_OBJS) $(BUILD)/libgcsbcore.a
 $(PKG)/bin/ring_dma_probe: csrc/tools/ring_dma_probe.hip
 	@mkdir -p $(PKG)/bin
 	$(HIPCC) --offload-arch=$(ARCH) -O2 -std=c++17 -o $@ $< -L/opt/rocm/lib -lamdhip64 -pthread -Wl,-rpath,/opt/rocm/lib
+
+$(BUILD)/tools/graph_probe.o: csrc/tools/graph_probe.hip
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -MMD -MP -c $< -o $@
+
+$(PKG)/bin/graph_probe: $(BUILD)/tools/graph_probe.o $(BUILD)/gpu/crc32c_kernels.o $(BUILD)/libgcsbcore.a
+	@mkdir -p $(PKG)/bin
+	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^ -L/opt/rocm/lib -lamdhip64 $(LDLIBS) -Wl,-rpath,/opt/rocm/lib
 
 $(PKG)/bin/%: csrc/tools/%.cc $(BUILD)/libgcsbcore.a
 	@mkdir -p $(PKG)/bin $(BUILD)/tools

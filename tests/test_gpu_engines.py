@@ -130,3 +130,22 @@ def test_ring_dma_probe_runs_every_variant():
     assert want <= set(res), (want - set(res), r.stdout[-2000:])
     for v in want:
         assert res[v]["GB/s"] > 0.1, res[v]
+
+
+def test_graph_probe_every_mode_crc_exact():
+    """csrc/tools/graph_probe.hip (profiles/r5_graph): the slot hand-off by
+    stream calls, by exec-updated hipGraphs and by unchanged graph relaunches
+    lands every slot with its GPU CRC32C equal to the host's."""
+    import os
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "custom_go_client_benchmark_amd",
+                       "bin", "graph_probe")
+    if not os.path.exists(exe):
+        pytest.fail("graph_probe not built (make probes)")
+    r = subprocess.run([exe, "slots=64", "reps=1"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rows = {x["mode"]: x for x in map(json.loads, (l for l in r.stdout.splitlines() if l.startswith("{")))}
+    assert set(rows) == {"stream", "graph", "graph_fixed"}, r.stdout
+    for m, x in rows.items():
+        assert x["crc_mismatches"] == 0 and x["gbps"] > 0.1, x

@@ -64,3 +64,20 @@ def test_resumable_chunk_with_overlap_is_deduplicated(native, server):
     assert r.status == 200
     c = native.Client({"protocol": "http", "endpoint": server.url})
     assert c.read_bytes(B, "ovl") == data
+
+
+def test_write_crc_worker_on_its_own_cpus(native):
+    """ServerConfig::crc_cpus (bench --write-split): the WriteObject CRC
+    worker pinned apart from the connection thread still checks every
+    message and the object lands exact."""
+    cpus = sorted(os.sched_getaffinity(0))
+    srv = native.Server({"port": 0, "cpus": cpus[:1], "crc_cpus": cpus[-1:], "send_cpus": cpus[-1:]})
+    srv.start()
+    try:
+        data = os.urandom(6 * (1 << 20) + 3)
+        c = native.Client({"protocol": "grpc", "endpoint": srv.url})
+        m = c.write_bytes(B, "split/obj", data, True, 2 << 20)
+        assert m["size"] == len(data) and m["crc32c"] == native.crc32c(data)
+        assert c.read_bytes(B, "split/obj") == data
+    finally:
+        srv.stop()

@@ -7,6 +7,7 @@
 // ReadObject stream over ONE HTTP/2 connection when the pool size is 1
 // (reference main.go:30,111; SURVEY.md §3.3 "the key contention point").
 #pragma once
+#include <algorithm>
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
@@ -72,6 +73,27 @@ struct SendPiece {
   bool splice = false;
 };
 
+// Append-only small-byte store for zero-copy sends: a byte vmsplice()d into
+// a pipe is referenced, not copied, until the peer has read it, so it must
+// never change.  put() copies into an mmap()ed chunk and never reuses a
+// byte; a full chunk is munmap()ed (pages still referenced by a pipe or the
+// socket stay alive, unchanged, until the kernel drops them) and a fresh one
+// mapped.  Frame headers and the gRPC / protobuf framing around spliced
+// payload pages go through it.
+class StableBytes {
+ public:
+  StableBytes() = default;
+  ~StableBytes();
+  StableBytes(const StableBytes&) = delete;
+  StableBytes& operator=(const StableBytes&) = delete;
+  const uint8_t* put(const void* p, size_t n);
+  static constexpr size_t kChunk = 1u << 20;
+
+ private:
+  uint8_t* base_ = nullptr;
+  size_t used_ = 0;
+};
+
 // Mutual exclusion granted in arrival order, one wake per hand-off.  The
 // frame writes of a connection's streams go through it: a std::mutex lets
 // the thread that just wrote a frame take the lock straight back, so with 48
@@ -128,6 +150,19 @@ class H2Writer {
   void write_frame_pieces(uint8_t type, uint8_t flags, uint32_t stream, const std::vector<SendPiece>& pieces,
                           size_t total,
                           const std::string* lead_headers = nullptr, const std::string* trailers = nullptr);
+  // A train of DATA frames of one stream in ONE write: `total` payload bytes
+  // (send window already reserved, e.g. try_reserve_train) cut into frames
+  // of at most the peer's SETTINGS_MAX_FRAME_SIZE, `last_flags` on the last
+  // one; lead_headers / trailers as in write_frame_pieces.  With a `splice`
+  // piece every byte goes by vmsplice (headers and small pieces through
+  // StableBytes): two system calls per pipe-full (~40 frames of 16 KiB)
+  // instead of three per frame; without one a single writev.  `fd` pieces
+  // (sendfile) fall back to a write_frame_pieces per frame.  At the RFC
+  // default of 16 KiB frames -- what a client that does not advertise a
+  // larger SETTINGS_MAX_FRAME_SIZE, grpc-go's, receives -- the endpoint
+  // would otherwise be the bound of every gRPC read.
+  void write_data_train(uint32_t stream, const std::vector<SendPiece>& pieces, size_t total, uint8_t last_flags,
+                        const std::string* lead_headers = nullptr, const std::string* trailers = nullptr);
   // Header block (HEADERS + CONTINUATION as needed).
   void write_headers(uint32_t stream, const std::string& block, bool end_stream);
   // HEADERS + one DATA frame (END_STREAM) in a single writev: a unary or
@@ -158,6 +193,12 @@ class H2Writer {
   // reserve() that never blocks: 0 if the windows allow nothing now; *gone
   // set (and 0 returned) if the stream or the connection is dead.
   size_t try_reserve(uint32_t stream, size_t want, bool* gone);
+  // reserve() / try_reserve() for a frame train: up to `want` bytes, bounded
+  // by the send windows only (write_data_train cuts the frames).  Less than
+  // want (window-limited) is rounded down to whole max-size frames when at
+  // least one fits, so a message's frames stay full-size up to its last.
+  size_t reserve_train(uint32_t stream, size_t want);
+  size_t try_reserve_train(uint32_t stream, size_t want, bool* gone);
   // Waits up to timeout_ms for a window update (or kill / settings change).
   void wait_window(int timeout_ms);
   void register_stream(uint32_t stream);
@@ -171,6 +212,7 @@ class H2Writer {
 
  private:
   void note_data_frame();
+  size_t train_grant_locked(int64_t avail, size_t want) const;
   // Holds wmu_ for one frame write; on release sends the control frames
   // queued meanwhile (write_control), then unlocks.
   class WriteLock {
@@ -189,6 +231,7 @@ class H2Writer {
   std::mutex ctl_mu_;        // guards ctl_pending_; taken before wmu_'s own mutex
   std::string ctl_pending_;  // encoded control frames waiting for the writer
   size_t quantum_ = 0;
+  StableBytes stable_;  // under wmu_
   H2SendStats sstats_;
   H2SendStats* sink_ = nullptr;
   std::mutex fmu_;  // flow control
@@ -203,10 +246,14 @@ class H2Writer {
 };
 
 // Receive-side window replenishment: credits consumed bytes back to the peer
-// in large batches (we advertise 2^31-1 windows, so this never throttles).
+// once `threshold` of them are pending (a quarter of the advertised window,
+// as grpc-go's inFlow [lib]; at most 16 / 64 MiB for the 2^31-1 windows).
 class RecvWindow {
  public:
   explicit RecvWindow(int64_t threshold = 64 << 20) : threshold_(threshold) {}
+  void set_threshold(int64_t t) { threshold_ = t; }
+  // the threshold for an advertised window of w bytes
+  static int64_t threshold_for(uint32_t w, int64_t cap) { return std::max<int64_t>(1, std::min<int64_t>(w / 4, cap)); }
   // returns increment to send now (0 = nothing yet)
   uint32_t consume(uint32_t n) {
     pending_ += n;

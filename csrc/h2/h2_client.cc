@@ -14,7 +14,9 @@ namespace gcsb {
 
 namespace {
 std::atomic<uint64_t> g_frames{0}, g_data_frames{0}, g_header_blocks{0}, g_data_bytes{0}, g_wait_ns{0},
-    g_data_ns{0}, g_headers_ns{0}, g_other_ns{0}, g_long_waits{0}, g_long_wait_ns{0}, g_readers{0};
+    g_data_ns{0}, g_headers_ns{0}, g_other_ns{0}, g_long_waits{0}, g_long_wait_ns{0}, g_readers{0},
+    g_spanned_frames{0}, g_span_reads{0}, g_span_spills{0};
+constexpr int kMaxSpanFrames = 64;  // frames one read_spanning plan covers (1 MiB of 16 KiB frames)
 constexpr int64_t kLongWaitNs = 5000000;
 }  // namespace
 
@@ -31,7 +33,117 @@ H2ReaderStats h2_reader_stats() {
   s.long_waits = g_long_waits.load();
   s.long_wait_ns = g_long_wait_ns.load();
   s.readers_alive = g_readers.load();
+  s.spanned_frames = g_spanned_frames.load();
+  s.span_reads = g_span_reads.load();
+  s.span_spills = g_span_spills.load();
   return s;
+}
+
+// --- H2DataCursor ------------------------------------------------------------
+
+void H2DataCursor::read_exact(void* dst, size_t n) {
+  if (n > left_) throw StorageError("http2: read past the end of a DATA frame", false);
+  bc_->read_exact(dst, n);
+  left_ -= static_cast<uint32_t>(n);
+}
+
+uint8_t H2DataCursor::read_byte() {
+  if (left_ == 0) throw StorageError("http2: read past the end of a DATA frame", false);
+  --left_;
+  return bc_->read_byte();
+}
+
+void H2DataCursor::skip(size_t n) {
+  if (n > left_) throw StorageError("http2: skip past the end of a DATA frame", false);
+  bc_->skip(n);
+  left_ -= static_cast<uint32_t>(n);
+}
+
+size_t H2DataCursor::read_some(void* dst, size_t n) {
+  n = std::min<size_t>(n, left_);
+  if (n == 0) throw StorageError("http2: read past the end of a DATA frame", false);
+  const size_t m = bc_->read_some(dst, n);
+  if (m == 0) throw StorageError("connection closed inside a DATA frame", true);
+  left_ -= static_cast<uint32_t>(m);
+  return m;
+}
+
+size_t H2DataCursor::take_inplace(size_t n, const uint8_t** p) {
+  n = std::min<size_t>(n, left_);
+  const size_t m = bc_->take_inplace(n, p);
+  left_ -= static_cast<uint32_t>(m);
+  return m;
+}
+
+void H2DataCursor::spill(const struct iovec* iov, int cnt, size_t i, size_t off, size_t n) {
+  g_span_spills.fetch_add(1, std::memory_order_relaxed);
+  std::vector<uint8_t> v;
+  v.reserve(n);
+  for (; n > 0 && static_cast<int>(i) < cnt; ++i, off = 0) {
+    const size_t k = std::min(n, iov[i].iov_len - off);
+    const auto* p = static_cast<const uint8_t*>(iov[i].iov_base) + off;
+    v.insert(v.end(), p, p + k);
+    n -= k;
+  }
+  bc_->unread(v.data(), v.size());
+}
+
+size_t H2DataCursor::read_spanning(uint8_t* dst, size_t want) {
+  if (want <= left_ || !can_span_ || end_ || left_ == 0 || bc_->buffered() > 0 || bc_->inplace())
+    return read_some(dst, want);
+  // the plan: [rest of this frame -> dst] then per frame [header -> hdr[j]]
+  // [payload -> right after the previous payload in dst]
+  uint8_t hdr[kMaxSpanFrames][9];
+  iovec iov[2 * kMaxSpanFrames + 1];
+  uint32_t plen[kMaxSpanFrames];
+  int cnt = 0, nf = 0;
+  iov[cnt++] = {dst, left_};
+  size_t placed = left_;
+  while (placed < want && nf < kMaxSpanFrames) {
+    iov[cnt++] = {hdr[nf], 9};
+    plen[nf] = static_cast<uint32_t>(std::min<size_t>(max_frame_, want - placed));
+    iov[cnt++] = {dst + placed, plen[nf]};
+    placed += plen[nf];
+    ++nf;
+  }
+  g_span_reads.fetch_add(1, std::memory_order_relaxed);
+  const size_t r = bc_->recv_scatter(iov, cnt);
+  if (r <= left_) {
+    left_ -= static_cast<uint32_t>(r);
+    return r;
+  }
+  size_t got = left_, rem = r - left_;
+  left_ = 0;
+  for (int j = 0; j < nf; ++j) {
+    const size_t hi = 1 + 2 * static_cast<size_t>(j);  // iov index of frame j's header
+    if (rem < 9) {  // the header is still on its way: the reader loop reads it
+      if (rem) spill(iov, cnt, hi, 0, rem);
+      return got;
+    }
+    const uint8_t* b = hdr[j];
+    const uint32_t len = (uint32_t(b[0]) << 16) | (uint32_t(b[1]) << 8) | b[2];
+    const uint32_t sid = be32(b + 5) & 0x7FFFFFFF;
+    if (b[3] != h2::kData || sid != stream_ || b[4] != 0 || len > max_frame_) {
+      // not a plain DATA frame of this stream: the reader loop dispatches it
+      spill(iov, cnt, hi, 0, rem);
+      return got;
+    }
+    rem -= 9;
+    ++spanned_frames_;
+    spanned_wire_ += len;
+    const size_t take = std::min<size_t>({rem, plen[j], len});
+    got += take;
+    rem -= take;
+    left_ = len - static_cast<uint32_t>(take);
+    if (rem == 0) return got;  // what is left of frame j is still on the socket
+    if (take < plen[j]) {
+      // frame j was shorter than planned: what follows it is not where the
+      // plan put it
+      spill(iov, cnt, hi + 1, take, rem);
+      return got;
+    }
+  }
+  return got;  // every planned frame came whole (bytes past the plan are buffered)
 }
 
 std::shared_ptr<H2ClientConn> H2ClientConn::dial(const Endpoint& ep, const H2ClientOptions& opt) {
@@ -44,11 +156,15 @@ std::shared_ptr<H2ClientConn> H2ClientConn::dial(const Endpoint& ep, const H2Cli
   c->dec_ = HpackDecoder(opt.header_table_size);
   // connection preface + our SETTINGS + open the connection window wide
   c->bc_->conn().write_all(h2::kPreface, 24);
-  c->w_->write_settings(encode_settings({{h2::kSettingsEnablePush, 0},
-                                          {h2::kSettingsInitialWindowSize, opt.initial_window},
-                                          {h2::kSettingsMaxFrameSize, opt.max_frame_size},
-                                          {h2::kSettingsHeaderTableSize, opt.header_table_size}}));
-  c->w_->write_window_update(0, static_cast<uint32_t>(h2::kMaxWindow - h2::kDefaultWindow));
+  std::vector<std::pair<uint16_t, uint32_t>> settings = {{h2::kSettingsEnablePush, 0},
+                                                         {h2::kSettingsInitialWindowSize, opt.initial_window},
+                                                         {h2::kSettingsHeaderTableSize, opt.header_table_size}};
+  // max_frame_size 0: not advertised, the peer keeps the RFC default (16 KiB)
+  if (opt.max_frame_size) settings.push_back({h2::kSettingsMaxFrameSize, opt.max_frame_size});
+  c->w_->write_settings(encode_settings(settings));
+  // the connection window opens to the stream window's size
+  if (opt.initial_window > h2::kDefaultWindow) c->w_->write_window_update(0, opt.initial_window - h2::kDefaultWindow);
+  c->conn_recv_.set_threshold(RecvWindow::threshold_for(std::max(opt.initial_window, h2::kDefaultWindow), 64 << 20));
   c->reader_ = std::thread([raw = c.get()] {
     pin_current_thread(raw->opt_.cpus);
     name_current_thread("gcsb-h2-reader");
@@ -133,6 +249,7 @@ void H2ClientConn::start_stream(const std::shared_ptr<H2ClientStream>& s, const 
   }
   s->id_ = next_id_;
   s->conn_frames_ = &frames_;
+  s->recv_window_.set_threshold(RecvWindow::threshold_for(opt_.initial_window, 16 << 20));
   next_id_ += 2;
   {
     std::lock_guard<std::mutex> lk(mu_);
@@ -160,6 +277,7 @@ void H2ClientConn::start_stream_with_body(const std::shared_ptr<H2ClientStream>&
     }
     s->id_ = next_id_;
     s->conn_frames_ = &frames_;
+    s->recv_window_.set_threshold(RecvWindow::threshold_for(opt_.initial_window, 16 << 20));
     next_id_ += 2;
     {
       std::lock_guard<std::mutex> lk(mu_);
@@ -310,7 +428,7 @@ void H2ClientConn::reader_loop() {
               .fetch_add(d, std::memory_order_relaxed);
         }
       } account{fh.type, t_frame};
-      if (fh.length > opt_.max_frame_size) throw StorageError("http2: frame exceeds max_frame_size", true);
+      if (fh.length > accept_max_frame()) throw StorageError("http2: frame exceeds max_frame_size", true);
       switch (fh.type) {
         case h2::kData: {
           uint32_t n = fh.length;
@@ -324,21 +442,33 @@ void H2ClientConn::reader_loop() {
           }
           auto s = acquire(fh.stream);
           bool end = fh.flags & h2::kFlagEndStream;
-          g_data_frames.fetch_add(1, std::memory_order_relaxed);
-          g_data_bytes.fetch_add(n, std::memory_order_relaxed);
+          const uint32_t amax = accept_max_frame();
+          H2DataCursor cur(*bc_, fh.stream, n, end,
+                           pad == 0 && opt_.span_max_frame > 0 && amax <= opt_.span_max_frame, amax);
           if (s) {
             s->progress_.fetch_add(1, std::memory_order_relaxed);
-            s->on_data(*bc_, n, end);
+            s->on_data(cur);
             s->progress_.fetch_add(1, std::memory_order_relaxed);
             release(*s);
-          } else {
-            bc_->skip(n);
           }
+          if (cur.left()) bc_->skip(cur.left());  // an unknown stream, or one that left bytes
           if (pad) bc_->skip(pad);
+          end = cur.end_stream();
+          const uint64_t extra = cur.spanned_frames_;
+          const uint64_t wire = fh.length + cur.spanned_wire_;
+          g_data_frames.fetch_add(1 + extra, std::memory_order_relaxed);
+          g_data_bytes.fetch_add(wire - (fh.length - n), std::memory_order_relaxed);
+          if (extra) {
+            g_frames.fetch_add(extra, std::memory_order_relaxed);
+            g_spanned_frames.fetch_add(extra, std::memory_order_relaxed);
+            frames_.fetch_add(extra, std::memory_order_relaxed);
+            last_frame_ns_.store(now_ns(), std::memory_order_relaxed);
+          }
           // replenish flow-control credit (connection + stream)
-          if (uint32_t inc = conn_recv_.consume(fh.length)) w_->write_window_update(0, inc);
+          if (uint32_t inc = conn_recv_.consume(static_cast<uint32_t>(wire))) w_->write_window_update(0, inc);
           if (s && !end)
-            if (uint32_t inc = s->recv_window_.consume(fh.length)) w_->write_window_update(fh.stream, inc);
+            if (uint32_t inc = s->recv_window_.consume(static_cast<uint32_t>(wire)))
+              w_->write_window_update(fh.stream, inc);
           break;
         }
         case h2::kHeaders:

@@ -18,13 +18,66 @@
 
 namespace gcsb {
 
+class H2ClientConn;
+
+// The DATA frame being dispatched to a stream (H2ClientStream::on_data), on
+// the connection's reader thread.  Reads stay inside the frame's payload
+// (padding already stripped), except read_spanning(), which may run on into
+// the frames that follow.
+//
+// Why: the reference's grpc-go client (reference go.mod:20, main.go:106-117)
+// does not advertise SETTINGS_MAX_FRAME_SIZE, so its peer sends DATA frames
+// of at most the RFC 7540 default of 16,384 bytes [lib, parity-unpinned].
+// A recv() per 16 KiB frame would bound a 25 GB/s read at its syscall rate,
+// so read_spanning() posts ONE recvmsg() whose iovecs predict the wire: the
+// rest of this frame's payload, then for each following frame a 9-byte header
+// slot and its payload straight after the previous one in dst.  After the
+// call every header that arrived is checked (DATA, this stream, no flags,
+// the predicted length); the first that is not what the plan assumed ends
+// the run and every byte from it on goes back to the parser
+// (BufferedConn::unread).  The payload lands contiguously with one kernel
+// copy, as with one 2 MiB frame.
+class H2DataCursor {
+ public:
+  uint32_t left() const { return left_; }        // payload bytes of the current frame not read yet
+  bool end_stream() const { return end_; }       // END_STREAM on the current frame
+  uint32_t stream() const { return stream_; }
+  void read_exact(void* dst, size_t n);          // n <= left()
+  uint8_t read_byte();
+  void skip(size_t n);                           // n <= left()
+  size_t read_some(void* dst, size_t n);         // 1..min(n, left()) bytes
+  bool inplace() const { return bc_->inplace(); }
+  size_t take_inplace(size_t n, const uint8_t** p);  // n <= left()
+  // 1..want payload bytes of this stream into dst, contiguous; may consume
+  // following DATA frames of the stream when want > left() (see above).
+  size_t read_spanning(uint8_t* dst, size_t want);
+  // frames and payload bytes the spanning reads took past the first frame
+  uint64_t spanned_frames() const { return spanned_frames_; }
+
+ private:
+  friend class H2ClientConn;
+  H2DataCursor(BufferedConn& bc, uint32_t stream, uint32_t len, bool end, bool can_span, uint32_t max_frame)
+      : bc_(&bc), stream_(stream), left_(len), end_(end), can_span_(can_span), max_frame_(max_frame) {}
+  void spill(const struct iovec* iov, int cnt, size_t from_iov, size_t from_off, size_t n);
+  BufferedConn* bc_;
+  uint32_t stream_;
+  uint32_t left_;
+  bool end_;
+  bool can_span_;
+  uint32_t max_frame_;
+  uint64_t spanned_frames_ = 0;
+  uint64_t spanned_wire_ = 0;  // their frame lengths (flow control)
+};
+
 class H2ClientStream {
  public:
   virtual ~H2ClientStream() = default;
   // Response headers or trailers (end_stream set on trailers / trailers-only).
   virtual void on_headers(const HeaderList& h, bool end_stream) = 0;
-  // Must consume exactly n bytes from bc (already stripped of padding).
-  virtual void on_data(BufferedConn& bc, uint32_t n, bool end_stream) = 0;
+  // Must consume the whole current frame (c.left() == 0 on return); the
+  // frame's END_STREAM is c.end_stream() after the reads (a spanning read
+  // moves the cursor to a later frame).
+  virtual void on_data(H2DataCursor& c) = 0;
   virtual void on_reset(uint32_t code) = 0;
   virtual void on_conn_error(const std::string& msg) = 0;
   uint32_t id() const { return id_; }
@@ -82,13 +135,24 @@ class H2ClientStream {
   // connection's stream-map lock, so none starts once the stream is erased)
   std::atomic<int> busy_{0};
   bool cancelled_ = false;  // cancel_stream() ran (owner thread only)
-  RecvWindow recv_window_{16 << 20};
+  RecvWindow recv_window_{16 << 20};  // threshold set by start_stream from the options
 };
 
 struct H2ClientOptions {
   SocketOptions sock;
-  uint32_t initial_window = 0x7FFFFFFF;    // per-stream receive window we advertise
-  uint32_t max_frame_size = (1u << 24) - 1;  // largest DATA frame we accept
+  // Receive flow control we advertise: the per-stream initial window, and
+  // the connection window opened to the same size at dial.  Consumed bytes
+  // are credited back (WINDOW_UPDATE) once a quarter of the window is
+  // pending, as grpc-go's inFlow does [lib].  grpc-go's BDP estimator grows
+  // both windows to at most 16 MiB (its maxWindowSize) [lib, parity-unpinned].
+  uint32_t initial_window = 0x7FFFFFFF;
+  // Largest DATA frame we accept (SETTINGS_MAX_FRAME_SIZE).  0 = do not
+  // advertise: the RFC 7540 default of 16,384 bytes, which is what grpc-go's
+  // client leaves its peer with [lib].
+  uint32_t max_frame_size = (1u << 24) - 1;
+  // DATA frames up to this size are read with H2DataCursor::read_spanning's
+  // multi-frame recvmsg(); 0 = never (A/B)
+  uint32_t span_max_frame = 256u << 10;
   uint32_t header_table_size = 4096;
   std::vector<int> cpus;  // pin the connection's reader thread
   // receive into this arena (net/buffered.h): the GPU sink's connection ring
@@ -106,6 +170,10 @@ struct H2ReaderStats {
   uint64_t data_ns = 0;         // DATA frames: stream dispatch incl. recv() into the sink
   uint64_t headers_ns = 0;      // HEADERS/CONTINUATION: read + HPACK decode + stream dispatch
   uint64_t other_ns = 0;        // every other frame type
+  // DATA frames taken by read_spanning past the dispatched one (no header
+  // parse of their own on the reader loop), spill = plans whose guess of a
+  // frame boundary was wrong
+  uint64_t spanned_frames = 0, span_reads = 0, span_spills = 0;
   // waits over 5 ms for the next frame (an idle connection's first frame
   // after a pause, e.g. a pooled connection reused by a later block): count
   // and their time, so a block's split can leave them out
@@ -148,6 +216,7 @@ class H2ClientConn {
 
  private:
   H2ClientConn(Endpoint ep, H2ClientOptions opt) : ep_(std::move(ep)), opt_(opt) {}
+  uint32_t accept_max_frame() const { return opt_.max_frame_size ? opt_.max_frame_size : h2::kDefaultMaxFrame; }
   void reader_loop();
   void fail_all(const std::string& msg);
   // the stream with this id, marked busy (release() after the dispatch)
@@ -167,7 +236,7 @@ class H2ClientConn {
   uint32_t next_id_ = 1;
   std::mutex open_mu_;  // id allocation + HEADERS ordering
   H2Settings peer_;
-  RecvWindow conn_recv_{64 << 20};
+  RecvWindow conn_recv_{64 << 20};  // threshold reset in dial() from the options
   std::atomic<bool> dead_{false}, goaway_{false};
   std::atomic<int64_t> last_frame_ns_{0};  // steady clock of the last frame header read
   std::atomic<uint64_t> frames_{0};         // frames read (starvation vs stall, H2ClientStream::wait_progress)

@@ -114,6 +114,16 @@ class BufferedConn {
     }
     return conn_->read_some(dst, n);
   }
+  // Scatter receive for the HTTP/2 reader's frame spanning
+  // (h2/h2_client.h H2DataCursor::read_spanning): ONE recvmsg() into
+  // iov[0..cnt) and then this buffer (whatever follows the plan, e.g. the
+  // next frame's header).  Needs an empty buffer; returns the bytes that
+  // landed in iov (any past them are buffered now).  TLS: iov[0] alone.
+  size_t recv_scatter(struct iovec* iov, int cnt);
+  // Puts n bytes back in front of the buffered ones: a scatter plan that
+  // guessed a frame boundary wrong hands the bytes after it back to the
+  // parser (the buffer grows if they do not fit).
+  void unread(const uint8_t* p, size_t n);
   void skip(size_t n) {
     uint8_t tmp[4096];
     while (n) {
@@ -138,12 +148,12 @@ class BufferedConn {
   static constexpr size_t kRefillMin = 64u << 10;
   void fill() {
     if (pos_ == end_) pos_ = end_ = 0;
-    if (end_ == kCap) {
+    if (end_ == cap_) {
       std::memmove(buf_.get(), buf_.get() + pos_, end_ - pos_);
       end_ -= pos_;
       pos_ = 0;
     }
-    const size_t room = kCap - end_;
+    const size_t room = cap_ - end_;
     size_t r = conn_->read_some(buf_.get() + end_, room < fill_cap() ? room : fill_cap());
     if (r == 0) throw StorageError("unexpected EOF", true);
     end_ += r;
@@ -166,6 +176,7 @@ class BufferedConn {
   std::unique_ptr<uint8_t[]> buf_;
   RecvArena* arena_ = nullptr;
   uint8_t* abuf_ = nullptr;  // arena mode: start of the current window
+  size_t cap_ = kCap;        // buf_'s size (unread() may grow it)
   size_t pos_ = 0, end_ = 0;
 };
 

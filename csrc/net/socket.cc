@@ -448,6 +448,26 @@ size_t Conn::read_some2(void* a, size_t na, void* b, size_t nb) {
   }
 }
 
+size_t Conn::read_somev(struct iovec* iov, int cnt) {
+  if (ssl_ || cnt == 1) return read_some(iov[0].iov_base, iov[0].iov_len);
+  if (fd_ < 0) throw StorageError("read on closed connection", true);
+  for (;;) {
+    msghdr m{};
+    m.msg_iov = iov;
+    m.msg_iovlen = static_cast<size_t>(cnt);
+    const ssize_t r = ::recvmsg(fd_, &m, 0);
+    if (r >= 0) {
+      bytes_read_ += static_cast<uint64_t>(r);
+      g_recv_calls.fetch_add(1, std::memory_order_relaxed);
+      g_recv_bytes.fetch_add(static_cast<uint64_t>(r), std::memory_order_relaxed);
+      return static_cast<size_t>(r);
+    }
+    if (errno == EINTR) continue;
+    if (errno == EAGAIN || errno == EWOULDBLOCK) throw StorageError("read timeout", true);
+    throw StorageError(std::string("recv: ") + std::strerror(errno), true);
+  }
+}
+
 void Conn::read_exact(void* buf, size_t n) {
   auto* p = static_cast<uint8_t*>(buf);
   while (n > 0) {
@@ -513,16 +533,39 @@ void Conn::writev_all(struct iovec* iov, int cnt, bool more) {
   }
 }
 
+void Conn::ensure_pipe() {
+  if (pipe_[0] >= 0) return;
+  if (::pipe2(pipe_, O_CLOEXEC) != 0) throw StorageError(std::string("pipe2: ") + std::strerror(errno), false);
+  // a 1 MiB pipe (fs.pipe-max-size default): 2 syscalls per MiB
+  (void)::fcntl(pipe_[1], F_SETPIPE_SZ, 1 << 20);
+  const int c = ::fcntl(pipe_[1], F_GETPIPE_SZ);
+  pipe_cap_ = c > 0 ? static_cast<size_t>(c) : 65536;
+}
+
+void Conn::splice_out(size_t left, bool more) {
+  while (left > 0) {
+    const unsigned fl = SPLICE_F_MOVE | (more ? SPLICE_F_MORE : 0u);
+    ssize_t w = ::splice(pipe_[0], nullptr, fd_, nullptr, left, fl);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      const int e = errno;
+      // the pipe may still hold page references: drop it with the connection
+      for (int& q : pipe_) {
+        ::close(q);
+        q = -1;
+      }
+      throw StorageError(std::string("splice: ") + std::strerror(e), true);
+    }
+    if (w == 0) throw StorageError("splice: connection closed", true);
+    bytes_written_ += static_cast<uint64_t>(w);
+    left -= static_cast<size_t>(w);
+  }
+}
+
 void Conn::splice_user_all(const void* data, size_t n, bool more) {
   if (fd_ < 0) throw StorageError("write on closed connection", true);
   if (ssl_) return write_all(data, n);
-  if (pipe_[0] < 0) {
-    if (::pipe2(pipe_, O_CLOEXEC) != 0) throw StorageError(std::string("pipe2: ") + std::strerror(errno), false);
-    // a 1 MiB pipe (fs.pipe-max-size default): 2 syscalls per MiB
-    (void)::fcntl(pipe_[1], F_SETPIPE_SZ, 1 << 20);
-    const int c = ::fcntl(pipe_[1], F_GETPIPE_SZ);
-    pipe_cap_ = c > 0 ? static_cast<size_t>(c) : 65536;
-  }
+  ensure_pipe();
   auto* p = static_cast<const uint8_t*>(data);
   while (n > 0) {
     iovec iov{const_cast<uint8_t*>(p), std::min(n, pipe_cap_)};
@@ -533,24 +576,33 @@ void Conn::splice_user_all(const void* data, size_t n, bool more) {
     }
     p += k;
     n -= static_cast<size_t>(k);
-    size_t left = static_cast<size_t>(k);
-    while (left > 0) {
-      const unsigned fl = SPLICE_F_MOVE | ((more || n > 0) ? SPLICE_F_MORE : 0u);
-      ssize_t w = ::splice(pipe_[0], nullptr, fd_, nullptr, left, fl);
-      if (w < 0) {
-        if (errno == EINTR) continue;
-        const int e = errno;
-        // the pipe may still hold page references: drop it with the connection
-        for (int& q : pipe_) {
-          ::close(q);
-          q = -1;
-        }
-        throw StorageError(std::string("splice: ") + std::strerror(e), true);
-      }
-      if (w == 0) throw StorageError("splice: connection closed", true);
-      bytes_written_ += static_cast<uint64_t>(w);
-      left -= static_cast<size_t>(w);
+    splice_out(static_cast<size_t>(k), more || n > 0);
+  }
+}
+
+void Conn::splice_iov_all(const struct iovec* iov_in, int cnt, bool more) {
+  if (fd_ < 0) throw StorageError("write on closed connection", true);
+  std::vector<iovec> v(iov_in, iov_in + cnt);
+  if (ssl_) return writev_all(v.data(), cnt, more);
+  ensure_pipe();
+  size_t i = 0;
+  while (i < v.size()) {
+    const int m = static_cast<int>(std::min<size_t>(v.size() - i, 1024));
+    ssize_t k = ::vmsplice(pipe_[1], &v[i], static_cast<unsigned long>(m), 0);
+    if (k < 0) {
+      if (errno == EINTR) continue;
+      throw StorageError(std::string("vmsplice: ") + std::strerror(errno), true);
     }
+    size_t left = static_cast<size_t>(k);
+    while (i < v.size() && left >= v[i].iov_len) {
+      left -= v[i].iov_len;
+      ++i;
+    }
+    if (left) {
+      v[i].iov_base = static_cast<uint8_t*>(v[i].iov_base) + left;
+      v[i].iov_len -= left;
+    }
+    splice_out(static_cast<size_t>(k), more || i < v.size());
   }
 }
 

@@ -111,6 +111,8 @@ class Conn {
   // payload read that also picks up what follows it (the next frame's
   // header) saves the header its own system call.  TLS: a alone.
   size_t read_some2(void* a, size_t na, void* b, size_t nb);
+  // One recvmsg() into iov[0..cnt) in order (plain TCP; TLS: iov[0] alone).
+  size_t read_somev(struct iovec* iov, int cnt);
   // Reads exactly n bytes or throws (EOF mid-way is a retryable error).
   void read_exact(void* buf, size_t n);
   void write_all(const void* buf, size_t n);
@@ -122,6 +124,9 @@ class Conn {
   // the caller must leave them unchanged until the peer has read the bytes
   // (for an upload: until its final response).  TLS falls back to a copy.
   void splice_user_all(const void* p, size_t n, bool more = false);
+  // Same for an iovec list, in order (vmsplice takes many segments per call;
+  // every segment's memory must stay unchanged until the peer read it).
+  void splice_iov_all(const struct iovec* iov, int cnt, bool more = false);
   void shutdown_write();
   void close();
   int fd() const { return fd_; }
@@ -148,6 +153,8 @@ class Conn {
   size_t fill_bytes_ = 16384;
   uint64_t bytes_read_ = 0;
   uint64_t bytes_written_ = 0;
+  void ensure_pipe();
+  void splice_out(size_t n, bool more);  // the pipe's first n bytes to the socket
   int pipe_[2] = {-1, -1};  // splice_user_all's page pipe (lazily created)
   size_t pipe_cap_ = 0;
 };

@@ -63,6 +63,13 @@ ClientConfig client_from(const py::dict& d) {
   c.max_idle_conns_per_host = get_or<int>(d, "max_idle_conns_per_host", 100);
   c.grpc_conn_pool_size = get_or<int>(d, "grpc_conn_pool_size", 1);
   c.read_chunk = get_or<size_t>(d, "read_chunk", 2u << 20);
+  c.h2_max_frame_size = get_or<uint32_t>(d, "h2_max_frame_size", c.h2_max_frame_size);
+  c.h2_window = get_or<uint32_t>(d, "h2_window", c.h2_window);
+  c.h2_span_max_frame = get_or<uint32_t>(d, "h2_span_max_frame", c.h2_span_max_frame);
+  if (c.h2_max_frame_size && (c.h2_max_frame_size < 16384 || c.h2_max_frame_size > (1u << 24) - 1))
+    throw std::invalid_argument("h2_max_frame_size: 0 (RFC default) or 16384 .. 16777215");
+  if (c.h2_window < 65535 || c.h2_window > 0x7FFFFFFFu)
+    throw std::invalid_argument("h2_window: 65535 .. 2147483647");
   c.retry = retry_from(d);
   // 0 = kernel TCP autotuning; an explicit size is capped at rmem_max (the
   // bench's one-stream read asks for 64 MiB: profiles/r2_rcvbuf)
@@ -1010,6 +1017,9 @@ PYBIND11_MODULE(_native, m) {
     d["other_ns"] = s.other_ns;
     d["long_waits"] = s.long_waits;
     d["long_wait_ns"] = s.long_wait_ns;
+    d["spanned_frames"] = s.spanned_frames;
+    d["span_reads"] = s.span_reads;
+    d["span_spills"] = s.span_spills;
     d["readers_alive"] = s.readers_alive;
     return d;
   });

@@ -578,7 +578,9 @@ class H2ServerConn {
     size_t want = j.left;
     if (active > 1 && srv_.config().h2_quantum > 0) want = std::min(want, srv_.config().h2_quantum);
     bool gone = false;
-    const size_t n = w_.try_reserve(s.id, want, &gone);
+    // a train of frames (each <= the client's SETTINGS_MAX_FRAME_SIZE) in
+    // one write: H2Writer::write_data_train
+    const size_t n = w_.try_reserve_train(s.id, want, &gone);
     if (gone) throw Cancelled{};
     if (n == 0) {
       if (!j.headers_sent) {  // no window yet: the response HEADERS go now
@@ -609,11 +611,12 @@ class H2ServerConn {
         j.poff = 0;
       }
     }
-    w_.write_frame_pieces(h2::kData, 0, s.id, frame, n, lead ? &ok_headers_ : nullptr, last ? &ok_trailers_ : nullptr);
-    if (lead) {
-      srv_.stats().note_ttfb(now_ns() - s.request_done_ns);
-      j.headers_sent = true;
-    }
+    // time to first byte: the response HEADERS are about to go, in the same
+    // write as the first DATA (recorded before the write, which may move a
+    // whole message)
+    if (lead) srv_.stats().note_ttfb(now_ns() - s.request_done_ns);
+    w_.write_data_train(s.id, frame, n, 0, lead ? &ok_headers_ : nullptr, last ? &ok_trailers_ : nullptr);
+    if (lead) j.headers_sent = true;
     j.left -= n;
     if (j.left > 0) return 0;
     j.msg_open = false;
@@ -907,7 +910,7 @@ class H2ServerConn {
           continue;
         }
       }
-      const size_t n = w_.reserve(s.id, want);
+      const size_t n = w_.reserve_train(s.id, want);
       if (n == 0) throw Cancelled{};
       if (disc >= 0 && static_cast<int64_t>(off + n) > disc && static_cast<int64_t>(off) <= disc) {
         disc = -1;
@@ -946,7 +949,7 @@ class H2ServerConn {
       } else {
         pieces.push_back(mem(p, n));
       }
-      w_.write_frame_pieces(h2::kData, sent + n == len ? h2::kFlagEndStream : 0, s.id, pieces, n);
+      w_.write_data_train(s.id, pieces, n, sent + n == len ? h2::kFlagEndStream : 0);
       sent += n;
       if (bps > 0) {
         int64_t due = t0 + static_cast<int64_t>(sent * 1e9 / static_cast<double>(bps));

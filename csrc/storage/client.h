@@ -34,6 +34,16 @@ struct ClientConfig {
   int max_idle_conns_per_host = 100;  // reference main.go:32
   int grpc_conn_pool_size = 1;        // reference main.go:30
   size_t read_chunk = 2 << 20;        // bytes per recv into the sink (reference intent, main.go:123-125)
+  // HTTP/2 receive settings we advertise (gRPC and -client-protocol http2),
+  // h2/h2_client.h H2ClientOptions: the largest DATA frame we accept (0 =
+  // not advertised, the RFC 7540 default of 16,384 bytes grpc-go's client
+  // leaves its peer with [lib]) and the stream / connection window (grpc-go's
+  // BDP estimator stops at 16 MiB [lib]).
+  uint32_t h2_max_frame_size = (1u << 24) - 1;
+  uint32_t h2_window = 0x7FFFFFFF;
+  // DATA frames up to this size are received many per recvmsg()
+  // (H2DataCursor::read_spanning); 0 = one frame per receive (A/B)
+  uint32_t h2_span_max_frame = 256u << 10;
   RetryPolicy retry;
   SocketOptions sock;
   std::shared_ptr<TokenSource> token;  // null = no Authorization header

@@ -72,8 +72,10 @@ class MessageHandler {
  public:
   virtual ~MessageHandler() = default;
   virtual void begin(uint32_t len) = 0;
-  // Consume exactly n bytes of the current message from bc.
-  virtual void bytes(BufferedConn& bc, uint32_t n) = 0;
+  // Consume 1..msg_left bytes of the current message from the DATA cursor
+  // (c.left() >= 1); returns how many.  Only a spanning read
+  // (H2DataCursor::read_spanning) may consume more than c.left().
+  virtual uint64_t bytes(H2DataCursor& c, uint64_t msg_left) = 0;
   virtual void end() = 0;
 };
 
@@ -83,10 +85,12 @@ class BufferingHandler : public MessageHandler {
     cur_.clear();
     cur_.reserve(len);
   }
-  void bytes(BufferedConn& bc, uint32_t n) override {
+  uint64_t bytes(H2DataCursor& c, uint64_t msg_left) override {
+    const size_t n = static_cast<size_t>(std::min<uint64_t>(c.left(), msg_left));
     size_t old = cur_.size();
     cur_.resize(old + n);
-    bc.read_exact(&cur_[old], n);
+    c.read_exact(&cur_[old], n);
+    return n;
   }
   void end() override { msgs_.push_back(std::move(cur_)); }
   std::vector<std::string>& messages() { return msgs_; }
@@ -135,17 +139,16 @@ class GrpcCall : public H2ClientStream {
     }
   }
 
-  void on_data(BufferedConn& bc, uint32_t n, bool end_stream) override {
-    while (n > 0) {
+  void on_data(H2DataCursor& c) override {
+    while (c.left() > 0) {
       if (failed_handler_) {
-        bc.skip(n);
+        c.skip(c.left());
         break;
       }
       if (have_ < 5) {
-        uint32_t k = std::min<uint32_t>(n, 5 - have_);
-        bc.read_exact(prefix_ + have_, k);
+        uint32_t k = std::min<uint32_t>(c.left(), 5 - have_);
+        c.read_exact(prefix_ + have_, k);
         have_ += k;
-        n -= k;
         if (have_ == 5) {
           if (prefix_[0] & 1) {
             handler_error("compressed gRPC message without negotiated encoding");
@@ -160,17 +163,15 @@ class GrpcCall : public H2ClientStream {
         }
         continue;
       }
-      uint32_t k = std::min(n, msg_left_);
       // socket errors propagate (connection level); sink errors are per call
-      handler_->bytes(bc, k);
-      msg_left_ -= k;
-      n -= k;
+      const uint64_t k = handler_->bytes(c, msg_left_);
+      msg_left_ -= static_cast<uint32_t>(k);
       if (msg_left_ == 0) {
         guarded([&] { handler_->end(); });
         have_ = 0;
       }
     }
-    if (end_stream) {
+    if (c.end_stream()) {
       {
         std::lock_guard<std::mutex> lk(mu_);
         if (grpc_status_ < 0) {
@@ -297,17 +298,22 @@ class ReadObjectHandler : public MessageHandler {
     vshift_ = 0;
   }
 
-  void bytes(BufferedConn& bc, uint32_t n) override {
-    while (n > 0) {
+  uint64_t bytes(H2DataCursor& c, uint64_t msg_left) override {
+    uint64_t used = 0;
+    while (c.left() > 0 && used < msg_left) {
       if (st_ == kContent) {
-        uint64_t k = std::min<uint64_t>(n, content_left_);
-        if (*delivered_ + k > cap_) throw StorageError("ReadObject: server sent more than read_limit bytes", false);
-        if (bc.inplace() && (sink_failed_ || sink_.accepts_inplace())) {
+        // content may run on past this frame (a spanning read takes the
+        // frames that follow); never past the message
+        uint64_t k = std::min<uint64_t>(content_left_, msg_left - used);
+        if (*delivered_ + std::min<uint64_t>(k, c.left()) > cap_)
+          throw StorageError("ReadObject: server sent more than read_limit bytes", false);
+        if (c.inplace() && (sink_failed_ || sink_.accepts_inplace())) {
           // the content already lies in the sink's arena: hand it over where
           // it is (one recv() may have brought several frames' worth)
+          k = std::min<uint64_t>(k, c.left());
           while (k > 0) {
             const uint8_t* p = nullptr;
-            const size_t m = bc.take_inplace(static_cast<size_t>(k), &p);
+            const size_t m = c.take_inplace(static_cast<size_t>(k), &p);
             if (!rr_->first_byte_ns) rr_->first_byte_ns = now_ns();
             if (!sink_failed_) {
               try {
@@ -318,55 +324,57 @@ class ReadObjectHandler : public MessageHandler {
             }
             *delivered_ += m;
             consume(static_cast<uint32_t>(m));
-            n -= static_cast<uint32_t>(m);
+            used += m;
             content_left_ -= m;
             k -= m;
           }
           if (content_left_ == 0) after_cd_field();
           continue;
         }
-        while (k > 0) {
-          Window w;
-          if (!sink_failed_) {
-            try {
-              w = sink_.acquire(static_cast<size_t>(k));
-            } catch (const std::exception& e) {
-              fail_sink(e.what());
-            }
-          }
-          if (sink_failed_) {
-            bc.skip(static_cast<size_t>(k));
-            consume(static_cast<uint32_t>(k));
-            n -= static_cast<uint32_t>(k);
-            content_left_ -= k;
-            k = 0;
-            break;
-          }
-          // commit whatever the socket has now (not the whole frame), so the
-          // sink's CRC / slot hand-off overlaps the rest of the frame arriving
-          size_t m = bc.read_some(w.ptr, std::min<uint64_t>(k, w.cap));
-          if (m == 0) throw StorageError("connection closed inside a DATA frame", true);
-          if (!rr_->first_byte_ns) rr_->first_byte_ns = now_ns();
+        Window w;
+        if (!sink_failed_) {
           try {
-            sink_.commit(m);
+            w = sink_.acquire(static_cast<size_t>(k));
           } catch (const std::exception& e) {
             fail_sink(e.what());
           }
-          *delivered_ += m;
-          consume(static_cast<uint32_t>(m));
-          n -= static_cast<uint32_t>(m);
-          content_left_ -= m;
-          k -= m;
         }
+        if (sink_failed_) {
+          const size_t m = static_cast<size_t>(std::min<uint64_t>(k, c.left()));
+          c.skip(m);
+          consume(static_cast<uint32_t>(m));
+          used += m;
+          content_left_ -= m;
+          if (content_left_ == 0) after_cd_field();
+          continue;
+        }
+        // commit whatever the socket has now (not the whole frame), so the
+        // sink's CRC / slot hand-off overlaps the rest arriving; a read past
+        // the frame's end lands the following frames' payload contiguously
+        uint64_t room = std::min<uint64_t>(k, w.cap);
+        if (*delivered_ + room > cap_) room = std::min<uint64_t>(room, c.left());  // checked frame by frame
+        const size_t m = c.read_spanning(w.ptr, static_cast<size_t>(room));
+        if (*delivered_ + m > cap_) throw StorageError("ReadObject: server sent more than read_limit bytes", false);
+        if (!rr_->first_byte_ns) rr_->first_byte_ns = now_ns();
+        try {
+          sink_.commit(m);
+        } catch (const std::exception& e) {
+          fail_sink(e.what());
+        }
+        *delivered_ += m;
+        consume(static_cast<uint32_t>(m));
+        used += m;
+        content_left_ -= m;
         if (content_left_ == 0) after_cd_field();
         continue;
       }
       // token bytes (tags, lengths, fixed32, small fields): byte at a time
-      uint8_t b = bc.read_byte();
+      uint8_t b = c.read_byte();
       consume(1);
-      --n;
+      ++used;
       step(b);
     }
+    return used;
   }
 
   void end() override {
@@ -580,6 +588,9 @@ class GrpcStorageClient : public StorageClient {
     idle_ms_ = cfg.sock.io_timeout_ms;
     opt_.sock.io_timeout_ms = 0;
     opt_.cpus = cfg.reader_cpus.empty() ? cfg.cpus : cfg.reader_cpus;
+    opt_.max_frame_size = cfg.h2_max_frame_size;
+    opt_.initial_window = cfg.h2_window;
+    opt_.span_max_frame = cfg.h2_span_max_frame;
     // one arena, one reader: only a pool of one connection receives into it
     if (cfg.grpc_conn_pool_size == 1) opt_.recv_arena = cfg.recv_arena;
     // DirectPath (reference main.go:106-117: GOOGLE_CLOUD_ENABLE_DIRECT_PATH_XDS

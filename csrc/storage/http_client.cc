@@ -98,6 +98,8 @@ class H2MediaGet : public H2ClientStream {
           // server ignored Range: skip what we already have, as the HTTP/1.1
           // path does (an error here would retry forever against that server)
           if (status_ == 200 && offset_ > 0) skip_left_ = static_cast<uint64_t>(offset_);
+          // body bytes bound for the sink (spanning reads stay within them)
+          if (clen >= 0) body_left_ = std::max<int64_t>(0, clen - static_cast<int64_t>(skip_left_));
           const bool full = offset_ == 0 && limit_ < 0 && status_ == 200;
           if (first_) {
             ObjectInfo bi = info;
@@ -114,40 +116,43 @@ class H2MediaGet : public H2ClientStream {
     if (end_stream) done();
   }
 
-  void on_data(BufferedConn& bc, uint32_t n, bool end_stream) override {
+  void on_data(H2DataCursor& c) override {
     if (status_ != 200 && status_ != 206) {
       // error body (JSON / XML), kept for the message
-      while (n > 0) {
+      while (c.left() > 0) {
         char tmp[4096];
-        size_t k = std::min<size_t>(n, sizeof(tmp));
-        bc.read_exact(tmp, k);
+        size_t k = std::min<size_t>(c.left(), sizeof(tmp));
+        c.read_exact(tmp, k);
         if (err_body_.size() < 4096) err_body_.append(tmp, k);
-        n -= static_cast<uint32_t>(k);
       }
     } else {
-      while (n > 0) {
+      while (c.left() > 0) {
         if (skip_left_ > 0) {
-          const uint32_t k = static_cast<uint32_t>(std::min<uint64_t>(n, skip_left_));
-          bc.skip(k);
+          const uint32_t k = static_cast<uint32_t>(std::min<uint64_t>(c.left(), skip_left_));
+          c.skip(k);
           skip_left_ -= k;
-          n -= k;
           continue;
         }
         if (failed_.load() || *delivered_ >= cap_total_) {
           if (!failed_.load()) fail("http2 GET: server sent more than the requested range", false);
-          bc.skip(n);
+          c.skip(c.left());
           break;
         }
+        // the body may run on past this frame: a spanning read takes the
+        // frames that follow (H2DataCursor::read_spanning), up to the range
+        // still expected (content-length / the requested range)
+        const uint64_t expect = body_left_ > 0 ? static_cast<uint64_t>(body_left_) : c.left();
+        const uint64_t want = std::max<uint64_t>(c.left(), std::min<uint64_t>(expect, cap_total_ - *delivered_));
         Window w;
         try {
-          w = sink_.acquire(n);
+          w = sink_.acquire(static_cast<size_t>(want));
         } catch (const std::exception& e) {
           fail(std::string("sink: ") + e.what(), false);
           continue;
         }
-        size_t cap = std::min<uint64_t>({static_cast<uint64_t>(n), w.cap, cap_total_ - *delivered_});
-        size_t m = bc.read_some(w.ptr, cap);
-        if (m == 0) throw StorageError("connection closed inside a DATA frame", true);
+        size_t cap = static_cast<size_t>(std::min<uint64_t>({want, w.cap, cap_total_ - *delivered_}));
+        size_t m = c.read_spanning(w.ptr, cap);
+        if (body_left_ > 0) body_left_ -= static_cast<int64_t>(std::min<uint64_t>(m, body_left_));
         if (!rr_->first_byte_ns) rr_->first_byte_ns = now_ns();
         try {
           sink_.commit(m);
@@ -155,7 +160,6 @@ class H2MediaGet : public H2ClientStream {
           fail(std::string("sink: ") + e.what(), false);
         }
         *delivered_ += m;
-        n -= static_cast<uint32_t>(m);
         // deferred sink (host CRC on the waiting worker): wake it every
         // 2 MiB so its replay overlaps the rest of the body arriving
         if (sink_.deferred() && (unpoked_ += m) >= (2u << 20)) {
@@ -164,7 +168,7 @@ class H2MediaGet : public H2ClientStream {
         }
       }
     }
-    if (end_stream) done();
+    if (c.end_stream()) done();
   }
 
   void on_reset(uint32_t code) override {
@@ -232,6 +236,7 @@ class H2MediaGet : public H2ClientStream {
   bool got_head_ = false;
   int status_ = 0;
   uint64_t skip_left_ = 0;  // 200 to a ranged GET: body bytes before the offset
+  int64_t body_left_ = 0;   // body bytes still due for the sink (0: unknown / done)
   std::string err_body_;
   std::atomic<bool> failed_{false};
   std::mutex mu_;
@@ -566,6 +571,9 @@ class HttpStorageClient : public StorageClient {
     o.sock = with_alpn(cfg_.sock, "h2");
     o.sock.io_timeout_ms = 0;  // -read-timeout is per stream on the shared connection
     o.cpus = cfg_.reader_cpus.empty() ? cfg_.cpus : cfg_.reader_cpus;
+    o.max_frame_size = cfg_.h2_max_frame_size;
+    o.initial_window = cfg_.h2_window;
+    o.span_max_frame = cfg_.h2_span_max_frame;
     return o;
   }();
   std::mutex h2_mu_;

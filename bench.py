@@ -15,10 +15,17 @@ Timed region: W untimed warm-up reads, then K reads bracketed by an RCCL
 barrier + torch.cuda.synchronize() on both sides; `value` = all ranks' bytes /
 the slowest rank's elapsed time (MiB/s for the whole job).
 
-At N = 1 the K timed reads run in 4 chunks interleaved with chunks of the
-reference-semantics baseline and of a never-DMA-read twin (--paired; the
-headline's value counts only its own chunks): vs_baseline_paired and
-headline_vs_nodma are the medians of the per-chunk ratios.
+The K timed reads run in 4 chunks interleaved with chunks of the
+reference-semantics baseline and of a never-DMA-read twin (--paired, at every
+N: each rank runs the same arm order between barriers; the headline's value
+counts only its own chunks): vs_baseline_paired and headline_vs_nodma are the
+medians of the per-chunk ratios.
+
+gRPC runs at the reference's HTTP/2 receive settings (--h2-framing ref):
+grpc-go advertises no SETTINGS_MAX_FRAME_SIZE, so the endpoint sends 16 KiB
+DATA frames, and its windows stop at 16 MiB (/root/reference/go.mod:20,
+main.go:106-117).  The client receives many frames per recvmsg()
+(csrc/h2/h2_client.h H2DataCursor).
 
 Output: rank 0 prints ONE JSON line (<= 8 KiB, the driver keys first, side
 blocks as scalars: custom_go_client_benchmark_amd/benchmark/report.py); the
@@ -227,6 +234,17 @@ def build_parser() -> argparse.ArgumentParser:
                          "object); vs_baseline_paired / headline_vs_nodma = medians of the per-chunk ratios. "
                          "auto: on at N = 1")
     ap.add_argument("--paired-chunks", type=int, default=4)
+    ap.add_argument("--paired-rewarm", type=int, default=1,
+                    help="untimed reads of each paired arm right before its chunk (outside the barriers): the "
+                         "reference reads back to back, so a chunk's first read should not pay for the connection "
+                         "and copy engines idling through the other arms (0 = off)")
+    ap.add_argument("--h2-framing", default="ref", choices=["ref", "large"],
+                    help="HTTP/2 receive settings of every gRPC client: ref = the reference's grpc-go (no "
+                         "SETTINGS_MAX_FRAME_SIZE advertised -> 16 KiB DATA frames, 16 MiB stream/connection "
+                         "windows); large = 16 MiB frames and 2 GiB windows (one frame per 2 MiB message)")
+    ap.add_argument("--framing-twin", default="on", choices=["on", "off"],
+                    help="side blocks at the OTHER framing: the headline paired chunk by chunk with its "
+                         "reference-semantics baseline, list_read_grpc and ref_default_grpc")
     ap.add_argument("--ref-effective", default="on", choices=["on", "off"],
                     help="ref_effective_grpc block: 48 x 100 MiB over one gRPC connection with the reference's "
                          "effective read path (whole <= 2 MiB messages decoded, CRC per message, copied out in "

@@ -10,6 +10,7 @@
 #include <cmath>
 #include <cstdio>
 #include <random>
+#include <stdexcept>
 
 #include "core/affinity.h"
 #include "core/hugebuf.h"
@@ -114,6 +115,13 @@ Runner::Runner(RunnerConfig cfg) : cfg_(std::move(cfg)) {
 Runner::~Runner() {
   stop();
   wait();
+  {
+    std::lock_guard<std::mutex> lk(ctl_mu_);
+    shutdown_ = true;
+  }
+  run_cv_.notify_all();
+  for (auto& t : threads_)
+    if (t.joinable()) t.join();
 }
 
 std::string Runner::object_for(int worker, int64_t seq) const {
@@ -163,6 +171,7 @@ void Runner::reset_stats() {
   steady_ms_.clear();
   pending_.clear();
   t_first_ = t_last_ = 0;
+  start_delay_max_ms_ = 0;
   for (auto& s : sliced_)
     if (s) s->reset_skew();
   // the sinks live across phases: their counters restart with the timed reads
@@ -185,29 +194,67 @@ void Runner::start() {
     sliced_.resize(cfg_.workers);
     landing_.resize(cfg_.workers);
   }
-  for (int w = 0; w < cfg_.workers; ++w)
-    threads_.emplace_back([this, w] {
-      worker_main(w);
-      // the thread ends here: keep its CPU time for the per-thread split
-      rusage ru{};
-      getrusage(RUSAGE_THREAD, &ru);
-      const double cpu = ru.ru_utime.tv_sec + ru.ru_utime.tv_usec * 1e-6 + ru.ru_stime.tv_sec + ru.ru_stime.tv_usec * 1e-6;
-      std::lock_guard<std::mutex> lk(mu_);
-      worker_cpu_s_ += cpu;
-    });
+  {
+    std::lock_guard<std::mutex> lk(ctl_mu_);
+    if (busy_ > 0) throw std::logic_error("Runner::start while a run is in progress");
+    start_ns_ = now_ns();
+    busy_ = cfg_.workers;
+    ++gen_;
+    if (threads_.empty())
+      for (int w = 0; w < cfg_.workers; ++w) threads_.emplace_back([this, w] { worker_loop(w); });
+  }
+  run_cv_.notify_all();
 }
 
 void Runner::wait() {
-  for (auto& t : threads_)
-    if (t.joinable()) t.join();
-  threads_.clear();
+  std::unique_lock<std::mutex> lk(ctl_mu_);
+  done_cv_.wait(lk, [&] { return busy_ == 0; });
   running_ = false;
+}
+
+namespace {
+double thread_cpu_s() {
+  rusage ru{};
+  getrusage(RUSAGE_THREAD, &ru);
+  return ru.ru_utime.tv_sec + ru.ru_utime.tv_usec * 1e-6 + ru.ru_stime.tv_sec + ru.ru_stime.tv_usec * 1e-6;
+}
+}  // namespace
+
+void Runner::worker_loop(int w) {
+  // pin before the sink allocates its pinned ring: NUMA-local first touch
+  pin_current_thread(cfg_.client.cpus);
+  name_current_thread("gcsb-worker");
+  uint64_t seen = 0;
+  for (;;) {
+    {
+      std::unique_lock<std::mutex> lk(ctl_mu_);
+      run_cv_.wait(lk, [&] { return shutdown_ || gen_ != seen; });
+      if (shutdown_) return;
+      seen = gen_;
+    }
+    const double c0 = thread_cpu_s();
+    worker_main(w);
+    const double c1 = thread_cpu_s();
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      worker_cpu_s_ += c1 - c0;  // this run's share of the thread's CPU
+    }
+    std::lock_guard<std::mutex> lk(ctl_mu_);
+    if (--busy_ == 0) done_cv_.notify_all();
+  }
 }
 
 void Runner::stop() { stop_flag_ = true; }
 
 void Runner::record(ReadRecord&& r, double ms, double host_ms) {
   std::lock_guard<std::mutex> lk(mu_);
+  if (!recording_.load(std::memory_order_relaxed)) {
+    if (!r.ok) {
+      ++acc_.errors;
+      if (acc_.first_error.empty()) acc_.first_error = "untimed read of object " + r.object + ": " + r.error;
+    }
+    return;
+  }
   ++acc_.reads;
   if (!r.ok) {
     ++acc_.errors;
@@ -236,9 +283,6 @@ void Runner::record(ReadRecord&& r, double ms, double host_ms) {
 }
 
 void Runner::worker_main(int w) {
-  // pin before the sink allocates its pinned ring: NUMA-local first touch
-  pin_current_thread(cfg_.client.cpus);
-  name_current_thread("gcsb-worker");
   try {
     if (cfg_.slices > 1 && !sliced_[w]) {
       SlicedReadConfig sc;
@@ -308,6 +352,16 @@ void Runner::worker_main(int w) {
   const int64_t t_begin = now_ns();
   std::vector<int> diag_avoid = cfg_.diag_avoid_cpus;
   diag_avoid.insert(diag_avoid.end(), cfg_.client.cpus.begin(), cfg_.client.cpus.end());
+  {
+    int64_t st;
+    {
+      std::lock_guard<std::mutex> lk(ctl_mu_);
+      st = start_ns_;
+    }
+    const double d = (now_ns() - st) / 1e6;
+    std::lock_guard<std::mutex> lk(mu_);
+    if (recording_.load(std::memory_order_relaxed)) start_delay_max_ms_ = std::max(start_delay_max_ms_, d);
+  }
   for (int64_t i = 0; i < cfg_.reads_per_worker; ++i) {
     if (stop_flag_) break;
     if (cfg_.duration_s > 0 && (now_ns() - t_begin) / 1e9 >= cfg_.duration_s) break;
@@ -406,6 +460,7 @@ RunSummary Runner::summary(bool percentiles) const {
   std::lock_guard<std::mutex> lk(mu_);
   RunSummary s = acc_;
   s.worker_cpu_s = worker_cpu_s_;
+  s.start_delay_max_ms = start_delay_max_ms_;
   s.elapsed_s = t_last_ > t_first_ ? (t_last_ - t_first_) / 1e9 : 0;
   s.mb_per_s = s.elapsed_s > 0 ? s.bytes / 1048576.0 / s.elapsed_s : 0;
   if (!lat_ms_.empty()) s.avg_ms = lat_ms_.sum() / lat_ms_.size();

@@ -18,6 +18,7 @@
 #include <atomic>
 #include <cstdint>
 #include <memory>
+#include <condition_variable>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -124,7 +125,10 @@ struct RunSummary {
   // reads are the p99.  Split out so the steady-state tail is visible.
   double first_read_p50_ms = 0, first_read_max_ms = 0, steady_p50_ms = 0, steady_p99_ms = 0;
   double slice_skew_ms = 0;  // sliced reads: mean spread of the slices' host-landed times
-  double worker_cpu_s = 0;   // CPU time of the worker threads (RUSAGE_THREAD at their exit)
+  double worker_cpu_s = 0;   // CPU time of the worker threads in the runs since reset_stats (RUSAGE_THREAD)
+  // start() -> the first read's start, slowest worker (the workers are
+  // parked between runs; a cold hand-off shows here, not in a read)
+  double start_delay_max_ms = 0;
   uint64_t oc_buckets[kOcBuckets] = {0};
   // the 3 slowest reads: {index in completion order, ms, host-landed ms, TTFB ms}
   std::vector<std::vector<double>> slowest;
@@ -184,6 +188,10 @@ class Runner {
   // Phased runs (bench warmup -> timed): sinks (pinned ring, HBM landing
   // buffers) and connections survive between start()/wait() cycles.
   void set_reads_per_worker(int64_t n) { cfg_.reads_per_worker = n; }
+  // false: the next runs' reads are untimed (a bench arm's re-warm read
+  // between chunks): they count nowhere but a failure still counts as an
+  // error of the run.  Set between runs only.
+  void set_recording(bool on) { recording_ = on; }
   void reset_stats();
   StorageClient& client() { return *client_; }
   // HBM address worker w's last object landed at (GPU sink, object landing;
@@ -198,6 +206,7 @@ class Runner {
   double ring_thp_fraction(int w) const;
 
  private:
+  void worker_loop(int w);
   void worker_main(int w);
   void record(ReadRecord&& r, double ms, double host_ms);
   RunnerConfig cfg_;
@@ -205,8 +214,19 @@ class Runner {
   // fill it) and after the sinks whose segments it holds
   std::unique_ptr<ConnRing> conn_ring_;
   std::unique_ptr<StorageClient> client_;
+  // The workers live as long as the Runner: created by the first start(),
+  // parked between runs (a bench's chunks, warm-up -> timed), woken by the
+  // next start().  A run ends when every worker finished its reads.
   std::vector<std::thread> threads_;
+  std::mutex ctl_mu_;
+  std::condition_variable run_cv_, done_cv_;
+  uint64_t gen_ = 0;       // runs started (ctl_mu_)
+  int busy_ = 0;           // workers still in the current run (ctl_mu_)
+  bool shutdown_ = false;  // ctl_mu_
+  int64_t start_ns_ = 0;   // the current run's start() (ctl_mu_)
+  double start_delay_max_ms_ = 0;  // mu_
   std::atomic<bool> running_{false};
+  std::atomic<bool> recording_{true};
   volatile bool stop_flag_ = false;
   mutable std::mutex mu_;
   std::vector<ReadRecord> pending_;

@@ -574,6 +574,7 @@ class PyRunner {
     for (const ReadSchedDiag& x : s.slowest_diag) sd.append(sched_diag_dict(x));
     d["slowest_diag"] = sd;
     d["worker_cpu_s"] = s.worker_cpu_s;
+    d["start_delay_max_ms"] = s.start_delay_max_ms;
     py::list b;
     for (int i = 0; i < kOcBuckets; ++i) b.append(s.oc_buckets[i]);
     d["oc_buckets"] = b;
@@ -604,6 +605,7 @@ class PyRunner {
   }
   std::string transport_path() { return runner_->client().transport_path(); }
   void set_reads_per_worker(int64_t n) { runner_->set_reads_per_worker(n); }
+  void set_recording(bool on) { runner_->set_recording(on); }
   void reset_stats() { runner_->reset_stats(); }
 
  private:
@@ -1231,6 +1233,8 @@ PYBIND11_MODULE(_native, m) {
            "counters of the multiplexed connection's shared receive ring (None without one)")
       .def("transport_path", &PyRunner::transport_path)
       .def("set_reads_per_worker", &PyRunner::set_reads_per_worker)
+      .def("set_recording", &PyRunner::set_recording,
+           "False: the next runs' reads are untimed (counted nowhere; a failure still counts as an error)")
       .def("reset_stats", &PyRunner::reset_stats);
 
   py::class_<PyServer>(m, "Server")

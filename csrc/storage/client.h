@@ -38,9 +38,9 @@ struct ClientConfig {
   // h2/h2_client.h H2ClientOptions: the largest DATA frame we accept (0 =
   // not advertised, the RFC 7540 default of 16,384 bytes grpc-go's client
   // leaves its peer with [lib]) and the stream / connection window (grpc-go's
-  // BDP estimator stops at 16 MiB [lib]).
-  uint32_t h2_max_frame_size = (1u << 24) - 1;
-  uint32_t h2_window = 0x7FFFFFFF;
+  // BDP estimator stops at 16 MiB [lib]).  Defaults: the reference's.
+  uint32_t h2_max_frame_size = 0;
+  uint32_t h2_window = 16u << 20;
   // DATA frames up to this size are received many per recvmsg()
   // (H2DataCursor::read_spanning); 0 = one frame per receive (A/B)
   uint32_t h2_span_max_frame = 256u << 10;

@@ -17,20 +17,35 @@ class SideBlocks:
 
     # ------------------------------------------------------ paired headline
     def paired_headline(self, head_over: dict, base_over: dict, nodma_over: dict | None, steps: int,
-                        warmup: int, chunks: int) -> tuple[dict, dict]:
+                        warmup: int, chunks: int, probe_tcp: bool = True, what: str = "paired") -> tuple[dict, dict]:
         """The headline's `steps` timed reads in `chunks` chunks, each chunk
         followed -- in a rotating order -- by a chunk of the same size of the
         reference-semantics baseline and of the never-DMA-read twin.  Only
         the headline's chunks count toward its value and ms_per_step.
+
+        Every arm's chunk is preceded by --paired-rewarm untimed reads of
+        that arm (outside the barriers): the reference reads back to back
+        (/root/reference/main.go:127-153), and a chunk's first read otherwise
+        paid for the connection, ring and copy engines having idled through
+        the other arms' chunks (round 5: the slowest timed reads were the
+        chunk-first ones).  Each head / base chunk window
+        carries its first read's latency, TTFB and host-landed time and the
+        workers' hand-off delay, so that cost stays visible.
         Returns (headline block stats, paired summary + per-chunk windows)."""
         from ..utils import sysdiag
 
         arms = {"head": head_over, "base": base_over}
         if nodma_over is not None:
             arms["nodma"] = nodma_over
+        rewarm = max(0, int(getattr(self.args, "paired_rewarm", 1)))
         runners, errs = {}, {}
         for a, over in arms.items():
-            runners[a], errs[a] = self.open_runner(over, warmup if a == "head" else self.side_warm)
+            # per-read records of the chunk arms (a few dozen reads): each
+            # chunk's first read is reported on its window
+            runners[a], errs[a] = self.open_runner({**over, "keep_records": True},
+                                                   warmup if a == "head" else self.side_warm)
+            if runners[a] is not None:
+                runners[a].drain()
         meters = {a: Meter() for a in arms}
         ep_stats = self.srv.stats
         before = self._counters(ep_stats)
@@ -47,22 +62,29 @@ class SideBlocks:
         # same chunks, so the headline's fraction of it is paired too (the
         # ceiling block's single probe after the side blocks drifted above
         # the headline in 2 of 3 runs, profiles/r5_window)
-        probe_tcp = self.use_gpu and self.placement.get("client")
+        probe_tcp = probe_tcp and self.use_gpu and self.placement.get("client")
         for ci, k in enumerate(sizes):
             row = {}
             for a in rp.arm_order(list(arms) + (["tcp"] if probe_tcp else []), ci):
                 if a == "tcp":
+                    t, terr = None, ""
                     try:
                         t = self.n.loopback_ceiling({"mode": "tcp", "object_bytes": self.size, "reads": k,
                                                      "ring_bytes": self.args.slots * parse_size(self.args.slot_bytes),
                                                      "rcvbuf": parse_size(self.args.rcvbuf),
                                                      "recv_cpus": self.placement["client"],
                                                      "send_cpus": self.placement["server"], "ring_pages": 1})
-                        row["tcp"] = t["gbps"] * 1e9 / (1 << 20)
+                    except Exception as e:  # noqa: BLE001 - the probe is a side measurement
+                        terr = str(e)[:200]
+                    # whole-job like the arms' rates: every rank probes its own link
+                    mine = t["gbps"] * 1e9 / (1 << 20) if t else 0.0
+                    red = self.gdist.reduce_stats(self.ctx, tcp=mine, ok=0.0 if terr else 1.0)
+                    if red["ok_min"] >= 1.0:
+                        row["tcp"] = red["tcp_sum"]
                         windows.append({"chunk": ci, "arm": "tcp", "reads": k, "mib_s": round(row["tcp"], 1),
                                         "recv_cpu_s_per_gib": round(t["recv_cpu_s_per_gib"], 4)})
-                    except Exception as e:  # noqa: BLE001 - the probe is a side measurement
-                        windows.append({"chunk": ci, "arm": "tcp", "error": str(e)[:200]})
+                    else:
+                        windows.append({"chunk": ci, "arm": "tcp", "error": terr or "a peer's probe failed"})
                     continue
                 # light window: the receiving core's clock, host vmstat and
                 # the receiving thread's schedstat, outside the CPU bracket
@@ -70,8 +92,10 @@ class SideBlocks:
                 vm0, sch0 = vmstat(), sysdiag.thread_sched()
                 m = meters[a]
                 m.last = {}
+                if rewarm and not errs[a]:
+                    self.untimed_reads(runners[a], rewarm)
                 c0 = self._counters(ep_stats, reset_hip=False) if a == "head" else None
-                e = self.timed_segment(runners[a], k, f"paired {a} chunk {ci}", errs[a], m)
+                e = self.timed_segment(runners[a], k, f"{what} {a} chunk {ci}", errs[a], m)
                 sch1, vm1 = sysdiag.thread_sched(), vmstat()
                 if c0 is not None:
                     c1 = self._counters(ep_stats, reset_hip=False)
@@ -99,6 +123,15 @@ class SideBlocks:
                 w = {"chunk": ci, "arm": a, "reads": k, "mib_s": round(row.get(a, 0.0), 1),
                      "recv_cpu_s_per_gib": round(recv / gib, 4) if recv else None,
                      "run_delay_ms": round(rd / 1e6, 3)}
+                if runners[a] is not None and not errs[a]:
+                    recs = sorted(runners[a].drain(), key=lambda x: x["start_ns"])
+                    if recs:
+                        f0 = recs[0]
+                        w["first_read"] = rp.read_times(f0)
+                        w["reads_ms"] = [round((x["end_ns"] - x["start_ns"]) / 1e6, 3) for x in recs]
+                        if self.last_start_ns:
+                            # start() -> the first read's start (the parked workers' wake-up)
+                            w["start_delay_ms"] = round((f0["start_ns"] - self.last_start_ns) / 1e6, 3)
                 if mhz:
                     w["clock_mhz"] = round(sum(v["mean"] for v in mhz.values()) / len(mhz))
                     w["clock_mhz_min"] = min(v["min"] for v in mhz.values())
@@ -116,6 +149,8 @@ class SideBlocks:
         head = self.finish_block(runners.pop("head"), errs["head"], head_over, steps, elapsed["head"],
                                  meters["head"], before, ep_stats, None, None)
         out = rp.paired_summary(rates)
+        out["rewarm_reads"] = rewarm
+        out["chunk_first"] = rp.chunk_first_summary(windows)
         out["windows"] = windows
         out["slow_windows"] = rp.attribute_windows(windows)
         for a in list(runners):
@@ -136,6 +171,18 @@ class SideBlocks:
                 out[f"{a}_error"] = errs[a][:200]
             del r
         return head, out
+
+    def untimed_reads(self, r1, reads: int) -> None:
+        """`reads` reads per worker of an open runner that count nowhere (a
+        failure still fails the block)."""
+        r1.set_recording(False)
+        try:
+            r1.set_reads_per_worker(reads)
+            r1.start()
+            r1.wait()
+        finally:
+            r1.set_recording(True)
+        r1.drain()
 
     # ------------------------------------------------------------ endpoints
     def share_endpoint(self):
@@ -190,10 +237,10 @@ class SideBlocks:
             if sh["client"]:
                 os.sched_setaffinity(0, sh["client"])
             client = n.Client({"protocol": self.protocol, "endpoint": ep.url, "retry_initial_s": 0.05,
-                               "tcp_congestion": args.client_cc, "loopback_rto_min": True})
+                               "tcp_congestion": args.client_cc, "loopback_rto_min": True, **self.framing})
             if parts > 1:
                 client = n.SlicedWriter({"protocol": self.protocol, "endpoint": ep.url, "retry_initial_s": 0.05,
-                                         "tcp_congestion": args.client_cc, "loopback_rto_min": True,
+                                         "tcp_congestion": args.client_cc, "loopback_rto_min": True, **self.framing,
                                          "slices": parts, "slice_min_bytes": 1 << 20, "cpus": sh["client"]})
             buf = torch.empty(wsize, dtype=torch.uint8, device=f"cuda:{gpu}")
             n.gpu_fill_pattern(gpu, buf.data_ptr(), wsize, f"upload/rank{rank}", 0)
@@ -265,7 +312,7 @@ class SideBlocks:
             want = self.srv.object_info(self.bucket, name)["crc32c"]
             client = n.Client({"protocol": self.protocol, "endpoint": self.srv.url, "retry_initial_s": 0.05,
                                "tcp_congestion": args.client_cc, "loopback_rto_min": True,
-                               "cpus": self.placement["client"], "rcvbuf": parse_size(args.rcvbuf)})
+                               "cpus": self.placement["client"], "rcvbuf": parse_size(args.rcvbuf), **self.framing})
             full = torch.empty(size, dtype=torch.uint8, device=f"cuda:{gpu}" if self.use_gpu else "cpu")
             # this rank's slice lands in place: the all-gather's input is the
             # slice of its output at rank * part_n (in-place all-gather)
@@ -323,7 +370,7 @@ class SideBlocks:
         return st
 
     # ------------------------------------------------------------ list-read
-    def list_read_block(self, proto: str, warmup_passes: int) -> dict:
+    def list_read_block(self, proto: str, warmup_passes: int, extra: dict | None = None) -> dict:
         """Config 3 (BASELINE.json): list `--list-objects` 1 MiB objects, then
         `--list-workers` readers read every listed object once into HBM, GPU
         CRC32C on every read (reference list_operation + read_operation).
@@ -345,7 +392,7 @@ class SideBlocks:
                            "retain_uploads": False})
             ep.start()
             ep.add_synthetic(self.bucket, f"c3_rank{rank}/file_", "", 0, nobj, 1 << 20)
-            lister = n.Client({"protocol": proto, "endpoint": ep.url, "retry_initial_s": 0.05})
+            lister = n.Client({"protocol": proto, "endpoint": ep.url, "retry_initial_s": 0.05, **self.framing})
             t0 = time.perf_counter()
             names = [o["name"] for o in lister.list_all(self.bucket, f"c3_rank{rank}/file_", 1000)]
             list_ms = (time.perf_counter() - t0) * 1e3
@@ -360,6 +407,8 @@ class SideBlocks:
                 "object_names": names or [f"c3_rank{rank}/file_0"], "cpus": sh["client"], "worker_id_offset": 0,
                 "rcvbuf": parse_size(args.list_rcvbuf), "ring_slots": int(lslots), "ring_slot_bytes": parse_size(lbytes),
                 "ring_wc": args.list_ring_wc == "on", "reader_cpus": sh.get("reader_cpus")}
+        if extra:
+            over.update(extra)
         st = self.read_block(over, per_pass, per_pass * warmup_passes, f"{proto} list-read", endpoint=ep)
         if err:
             st["error"] = err
@@ -426,12 +475,14 @@ class SideBlocks:
         out = {"ok": st["ok_min"] >= 1.0}
         for k in r:  # the slowest rank's bound (each rank measures its own)
             out[k] = round(st[k + "_min"], 3)
+        # (the headline's fraction of the run's ONE ceiling -- the best of
+        # these probes and the paired chunks' -- is on the line:
+        # report.unified_ceiling)
         head_gbps = head_mib_s_per_rank * (1 << 20) / 1e9
         bounds = [b for b in (out["tcp_gbps"], out["h2d_gbps"] if self.use_gpu else 0.0) if b > 0]
         if bounds:
             out["bound_gbps"] = round(min(bounds), 3)
             out["headline_gbps_per_gpu"] = round(head_gbps, 3)
-            out["headline_frac_of_ceiling"] = round(head_gbps / min(bounds), 3)
         if err:
             out["error"] = err[:300]
         return out

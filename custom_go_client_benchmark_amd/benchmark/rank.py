@@ -36,6 +36,16 @@ METRIC = "p50/p99 read latency (ms) + MB/s per GPU; HTTP vs gRPC at 1/2/4/8 MI35
 # side blocks a multi-GPU run does by default (the rest with --blocks all)
 SCALE_BLOCKS = ("cpu_baseline", "compare", "write", "fanout")
 
+# HTTP/2 receive settings of the gRPC clients (--h2-framing).  ref: what the
+# reference's grpc-go client (go.mod:20, built with library defaults at
+# main.go:106-117) leaves its peer with -- no SETTINGS_MAX_FRAME_SIZE, so
+# 16,384-byte DATA frames, and windows its BDP estimator grows to at most
+# 16 MiB [lib, parity-unpinned].  large: 16 MiB - 1 frames, 2 GiB - 1 windows
+# (one DATA frame per <= 2 MiB gRPC message; rounds 2-5).
+FRAMING = {"ref": {"h2_max_frame_size": 0, "h2_window": 16 << 20},
+           "large": {"h2_max_frame_size": (1 << 24) - 1, "h2_window": 0x7FFFFFFF}}
+FRAME_LABEL = {"ref": "16KiB", "large": "16MiB"}
+
 
 class RankBench(SideBlocks):
     """One rank's benchmark: its endpoint, placement and blocks."""
@@ -58,6 +68,7 @@ class RankBench(SideBlocks):
         self.use_gpu = args.sink == "gpu"
         self.rehearsal = os.environ.get("GCSB_DIST_BACKEND") == "gloo"
         self.diag: dict = {}  # the sidecar (rank 0 writes it)
+        self.last_start_ns = 0  # steady clock of the last timed_segment's start() (CLOCK_MONOTONIC, as now_ns())
 
     # ------------------------------------------------------------------ setup
     def setup(self) -> int:
@@ -148,6 +159,9 @@ class RankBench(SideBlocks):
             "recv_refill": bool(args.recv_refill),
             "fill_bytes": parse_size(getattr(args, "fill_bytes", "16KiB")),
         }
+        self.framing_name = getattr(args, "h2_framing", "ref")
+        self.framing = dict(FRAMING[self.framing_name])
+        self.cfg.update(self.framing)
         return 0
 
     def sync(self) -> None:
@@ -197,6 +211,7 @@ class RankBench(SideBlocks):
         if meter is not None and not err:
             meter.begin()
         t1 = time.perf_counter()
+        self.last_start_ns = time.monotonic_ns()
         if not err:
             r1.start()
             r1.wait()
@@ -366,8 +381,10 @@ class RankBench(SideBlocks):
         explicit = only - {"all"}
         base_on = args.baseline == "on" and (not explicit or "cpu_baseline" in explicit) and side_steps > 0
         bracket = args.baseline_bracket == "on" or (args.baseline_bracket == "auto" and world == 1)
-        paired = args.workload == "read" and base_on and args.steps >= 2 and (
-            args.paired == "on" or (args.paired == "auto" and world == 1))
+        # paired at every N: every rank runs the same arm
+        # order between the same barriers, so the scaling run is credited on
+        # the same estimator as the 1-GPU bench
+        paired = args.workload == "read" and base_on and args.steps >= 2 and args.paired in ("on", "auto")
         self.base_before = None
         self.paired = None
         if args.workload == "read" and use_gpu and bracket and base_on:
@@ -433,6 +450,21 @@ class RankBench(SideBlocks):
                                    {"protocol": p, "sink": "discard", "_conns": 1, "_place": "pair",
                                     "note": "reference semantics: io.Discard + host CRC32C; client + submitter cores"})
             self.stash_headline()
+            alt = "large" if self.framing_name == "ref" else "ref"
+            twin_on = protocol == "grpc" and getattr(args, "framing_twin", "on") == "on"
+            if twin_on and base_on and want("framing_twin"):
+                # the headline config at the OTHER framing, paired chunk by
+                # chunk with its reference-semantics baseline at that framing
+                fo = FRAMING[alt]
+                st_t, pr_t = self.paired_headline(dict(fo), {**self.baseline_over(), **fo}, None, side_steps,
+                                                  side_warm, args.paired_chunks, probe_tcp=False,
+                                                  what=f"{alt} framing")
+                blocks[f"{alt}_framing"] = (st_t, {"protocol": protocol, "sink": args.sink, "_conns": 1,
+                                                   "_place": "pair", "h2_frames": FRAME_LABEL[alt],
+                                                   "vs_baseline_paired": pr_t.get("vs_baseline_paired"),
+                                                   "base_mib_s": pr_t.get("base_mib_s"),
+                                                   "note": "headline config at the other HTTP/2 framing, paired "
+                                                           "with its reference-semantics baseline"})
             if (world == 1 and protocol == "grpc" and args.ref_effective == "on" and want("ref_effective")):
                 # the reference's EFFECTIVE read on the headline config: the
                 # baseline (same endpoint, cores, object and steps) whose
@@ -474,7 +506,15 @@ class RankBench(SideBlocks):
                                                    "object_bytes": parse_size(args.ref_object_size),
                                                    "reads_per_worker": args.ref_reads,
                                                    "_conns": 1 if p == "grpc" else args.ref_workers, "_place": "same",
+                                                   "h2_frames": FRAME_LABEL[self.framing_name] if p == "grpc" else None,
                                                    "note": "reference default experiment (execute_pb.sh)"})
+                if "grpc" in protos and twin_on:
+                    blocks[f"ref_default_grpc_{alt}"] = (
+                        self.ref_default_block("grpc", extra=dict(FRAMING[alt])),
+                        {"protocol": "grpc", "workers": args.ref_workers, "sink": "discard",
+                         "object_bytes": parse_size(args.ref_object_size), "reads_per_worker": args.ref_reads,
+                         "_conns": 1, "_place": "same", "h2_frames": FRAME_LABEL[alt],
+                         "note": "ref_default_grpc at the other HTTP/2 framing"})
             if args.ref_workers > 0 and args.ref_effective == "on" and "grpc" in protos and want("ref_effective"):
                 # the reference's EFFECTIVE read path: io.Discard.ReadFrom ignores
                 # the 2 MiB buffer and pulls 8 KiB reads out of each decoded
@@ -514,7 +554,15 @@ class RankBench(SideBlocks):
                                                  "workers": args.list_workers, "ring": args.list_ring,
                                                  "sink": self.args.sink,
                                                  "_conns": 1 if p == "grpc" else args.list_workers, "_place": "same",
+                                                 "h2_frames": FRAME_LABEL[self.framing_name] if p == "grpc" else None,
                                                  "config": "BASELINE config 3"})
+                if "grpc" in protos and twin_on:
+                    blocks[f"list_read_grpc_{alt}"] = (
+                        self.list_read_block("grpc", 1, extra=dict(FRAMING[alt])),
+                        {"protocol": "grpc", "objects": args.list_objects, "object_bytes": 1 << 20,
+                         "workers": args.list_workers, "ring": args.list_ring, "sink": self.args.sink, "_conns": 1,
+                         "_place": "same", "h2_frames": FRAME_LABEL[alt],
+                         "note": "list_read_grpc at the other HTTP/2 framing"})
             if use_gpu and want("write"):
                 blocks["write"] = (self.write_block(side_steps, side_warm),
                                    {"protocol": protocol, "object_bytes": parse_size(args.write_size),
@@ -669,13 +717,18 @@ class RankBench(SideBlocks):
             ceil = self.blocks["ceiling"][0]
         if self.paired:
             pr = self.paired
-            for k in ("vs_baseline_paired", "headline_vs_nodma", "headline_frac_of_ceiling"):
+            for k in ("vs_baseline_paired", "headline_vs_nodma", "headline_vs_tcp_paired"):
                 if k in pr:
                     out[k] = pr[k]
             diag["paired"] = pr
-        if "headline_frac_of_ceiling" not in out and ceil and ceil.get("headline_frac_of_ceiling") is not None:
-            # unpaired runs (N > 1): the ceiling block's probe after the side blocks
-            out["headline_frac_of_ceiling"] = ceil["headline_frac_of_ceiling"]
+        # ONE ceiling: the best of every TCP probe of the run (paired chunks +
+        # the ceiling block) and the H2D copy rate (report.unified_ceiling)
+        uc = rp.unified_ceiling(value / max(1, self.n_gpus), (self.paired or {}).get("tcp_mib_s"), ceil, world,
+                                self.use_gpu)
+        if uc:
+            out["headline_frac_of_ceiling"] = uc["headline_frac_of_ceiling"]
+            diag["ceiling"] = uc
+        out["h2_frames"] = FRAME_LABEL[self.framing_name] if self.protocol == "grpc" else None
         if args.workload == "read":
             out["ttfb_p50_ms"] = round(head["ttfb_p50_max"], 3)
             out["host_landed_p50_ms"] = round(head["host_p50_max"], 3)
@@ -689,7 +742,10 @@ class RankBench(SideBlocks):
         if self.paired:
             pr = self.paired
             out["paired"] = {k: pr[k] for k in ("chunks", "pair_ratios", "nodma_ratios", "tcp_ratios", "head_mib_s",
-                                                "base_mib_s", "nodma_mib_s", "tcp_mib_s") if k in pr}
+                                                "base_mib_s", "nodma_mib_s", "tcp_mib_s", "rewarm_reads") if k in pr}
+            cf = (pr.get("chunk_first") or {}).get("head")
+            if cf:
+                out["paired"]["head_first_vs_median"] = cf["first_vs_median"]
             if pr.get("slow_windows"):
                 out["paired"]["slow_windows"] = [[w["chunk"], w["cause"][:120]] for w in pr["slow_windows"][:2]]
         # host-memory placement of the object's page cache and the pinned ring
@@ -739,16 +795,29 @@ class RankBench(SideBlocks):
                                      "same run" + (", run right before and right after the headline, pooled"
                                                    if len(runs) == 2 else ", run right after the headline"))
         full = {}
+        tcp_best_gbps = (uc["tcp_best_mib_s"] / rp.MIB_PER_GBPS) if uc else 0.0
         for key, (st, extra) in self.blocks.items():
             if extra is None:  # already a JSON block (ceiling)
                 full[key] = dict(st)
                 continue
             b = self.full_block(key, st, extra)
             if ceil and ceil.get("ok"):
-                tcp = ceil.get("tcp_gbps_same" if extra.get("_place") == "same" else "tcp_gbps", 0.0) or 0.0
-                b.update(rp.frac_of_bound(b["mib_s"], ceil.get("h2d_gbps", 0.0) or 0.0, tcp, extra.get("_conns"),
-                                          extra.get("sink") == "gpu" and self.use_gpu))
+                # the headline's placement: the run's best probe; one L3 domain: its own probe
+                tcp = (ceil.get("tcp_gbps_same", 0.0) if extra.get("_place") == "same"
+                       else max(tcp_best_gbps, ceil.get("tcp_gbps", 0.0))) or 0.0
+                b.update(rp.frac_of_bound(b["mib_s"] / max(1, world), ceil.get("h2d_gbps", 0.0) or 0.0, tcp,
+                                          extra.get("_conns"), extra.get("sink") == "gpu" and self.use_gpu))
+                if "bound_mib_s" in b:  # per GPU: each rank's bound is its own link / copy engines
+                    b["bound_mib_s"] = round(b["bound_mib_s"] * max(1, world), 1)
             full[key] = b
+        head_bound = (value, "tcp_1conn", uc["tcp_best_mib_s"] * max(1, world)) if uc else None
+        raised = rp.observed_bounds(full, head_bound)
+        if raised:
+            diag["bounds_raised_to_observed"] = raised
+            hb = raised.get(f"tcp_1conn@{round(uc['tcp_best_mib_s'] * max(1, world), 1)}") if uc else None
+            if hb and uc.get("ceiling_bound") == "tcp_1conn":
+                # a block of the headline's own bound beat every probe: that rate is the ceiling
+                out["headline_frac_of_ceiling"] = round(value / hb, 3)
         for key, b in full.items():
             if key.startswith("ref_default_100m_") and key.endswith("_gpu"):
                 twin = full.get(key[:-len("_gpu")] + "_discard")

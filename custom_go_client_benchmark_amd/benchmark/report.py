@@ -26,7 +26,7 @@ BLOCK_KEYS = ("ok", "mib_s", "p50_ms", "p99_ms", "protocol", "workers", "sink", 
               "frac_of_bound", "bound", "vs_discard_twin", "vs_ref_effective", "recv_cpu_s_per_gib",
               "py_cpu_s_per_gib", "first_read_p50_ms", "steady_p99_ms", "list_ms", "per_gpu_mib_s",
               "crc_verified_ranks", "tcp_gbps", "tcp_gbps_same", "memcpy_gbps", "h2d_gbps", "bound_gbps", "headline_frac_of_ceiling",
-              "partial", "error")
+              "h2_frames", "vs_baseline_paired", "partial", "error")
 
 # receiving threads, in order of preference: the HTTP/2 connection reader
 # (gRPC) or the worker that recv()s its own HTTP/1.1 stream
@@ -82,14 +82,50 @@ def paired_summary(chunks: list[dict]) -> dict:
         out["nodma_ratios"] = [round(x, 3) for x in rn]
     rt = ratios("tcp")
     if rt:
-        # the headline against the raw one-stream TCP ceiling probed between
-        # the same chunks (no GPU, no framing): a paired frac_of_ceiling
-        out["headline_frac_of_ceiling"] = round(median(rt), 3)
+        # the headline against the raw one-stream TCP probe run between the
+        # same chunks (no GPU, no framing), chunk by chunk; the ceiling itself
+        # is the best of every probe (unified_ceiling)
+        out["headline_vs_tcp_paired"] = round(median(rt), 3)
         out["tcp_ratios"] = [round(x, 3) for x in rt]
     for arm in ("head", "base", "nodma", "tcp"):
         v = [c[arm] for c in chunks if c.get(arm)]
         if v:
             out[f"{arm}_mib_s"] = [round(x, 1) for x in v]
+    return out
+
+
+def read_times(rec: dict) -> list[float]:
+    """[ms, TTFB ms, host-landed ms] of one Runner record (drain())."""
+    st = rec["start_ns"]
+    ms = (rec["end_ns"] - st) / 1e6
+    ttfb = (rec["ttfb_ns"] - st) / 1e6 if rec.get("ttfb_ns", 0) > st else 0.0
+    host = (rec["host_done_ns"] - st) / 1e6 if rec.get("host_done_ns", 0) > st else ms
+    return [round(ms, 3), round(ttfb, 3), round(host, 3)]
+
+
+def chunk_first_summary(windows: list[dict]) -> dict:
+    """Per arm: each chunk's first read against the chunk's median read
+    (ms ratios), the first reads' TTFB and host-landed times, and how many
+    chunks had their first read as their slowest.  Whether a chunk restart
+    costs anything, and where (connection / TTFB, receive / host-landed, or
+    the GPU's copy + CRC after the last host byte)."""
+    out = {}
+    for arm in ("head", "base"):
+        ws = [w for w in windows if w.get("arm") == arm and w.get("reads_ms")]
+        if not ws:
+            continue
+        ratios, slowest_first = [], 0
+        for w in ws:
+            r = w["reads_ms"]
+            med = median(r)
+            if med:
+                ratios.append(round(w["first_read"][0] / med, 3))
+            if len(r) > 1 and w["first_read"][0] >= max(r):
+                slowest_first += 1
+        out[arm] = {"first_vs_median": ratios, "first_is_slowest": slowest_first, "chunks": len(ws),
+                    "first_ttfb_ms": [w["first_read"][1] for w in ws],
+                    "first_host_ms": [w["first_read"][2] for w in ws],
+                    "start_delay_ms": [w.get("start_delay_ms") for w in ws]}
     return out
 
 
@@ -112,6 +148,65 @@ def frac_of_bound(block_mib_s: float, h2d_gbps: float, tcp_gbps: float, connecti
     bound_mib_s = gbps * 1e9 / (1 << 20)
     return {"bound": name, "bound_mib_s": round(bound_mib_s, 1),
             "frac_of_bound": round(block_mib_s / max(bound_mib_s, 1e-9), 3)}
+
+
+MIB_PER_GBPS = 1e9 / (1 << 20)
+
+
+def unified_ceiling(head_mib_s_per_gpu: float, paired_tcp_mib_s: list[float] | None, ceiling: dict | None,
+                    world: int, gpu_sink: bool) -> dict:
+    """ONE one-stream TCP ceiling per run: the best of
+    every loopback TCP probe the process made in the headline's placement --
+    the paired chunks' probes (whole-job rates, so / world) and the ceiling
+    block's best of three -- and the pinned -> HBM copy rate for a GPU sink.
+    headline_frac_of_ceiling = headline per GPU / the lower of the two."""
+    probes = [x / max(1, world) for x in (paired_tcp_mib_s or []) if x]
+    if ceiling and ceiling.get("ok") and ceiling.get("tcp_gbps"):
+        probes.append(ceiling["tcp_gbps"] * MIB_PER_GBPS)
+    if not probes:
+        return {}
+    tcp = max(probes)
+    bounds = [("tcp_1conn", tcp)]
+    if gpu_sink and ceiling and ceiling.get("ok") and ceiling.get("h2d_gbps"):
+        bounds.append(("h2d", ceiling["h2d_gbps"] * MIB_PER_GBPS))
+    name, b = min(bounds, key=lambda x: x[1])
+    out = {"tcp_best_mib_s": round(tcp, 1), "tcp_probes": len(probes), "ceiling_bound": name,
+           "ceiling_mib_s": round(b, 1)}
+    if head_mib_s_per_gpu > b:
+        # the headline did what the probe said one stream cannot: the probe
+        # was no ceiling; the observed rate is
+        out["ceiling_observed"] = "headline"
+        b = head_mib_s_per_gpu
+    out["headline_frac_of_ceiling"] = round(head_mib_s_per_gpu / max(b, 1e-9), 3)
+    return out
+
+
+def observed_bounds(blocks: dict[str, dict], head: tuple[float, str, float] | None = None) -> dict:
+    """A bound no measured rate may beat: per bound (name, rate), if any block
+    -- or the headline, head = (MiB/s per GPU, bound name, bound MiB/s) --
+    ran faster than the probe, that rate is what one connection / the copy
+    engines did in this process, so the bound becomes it and every block of
+    that bound is re-divided (`bound_observed` names the block that set it).
+    Mutates the blocks' frac_of_bound / bound_mib_s; returns {bound key:
+    observed MiB/s} for the raised ones."""
+    groups: dict[tuple, list] = {}
+    for k, b in blocks.items():
+        if b.get("bound") and b.get("bound_mib_s") and b.get("mib_s") is not None:
+            groups.setdefault((b["bound"], b["bound_mib_s"]), []).append(k)
+    raised = {}
+    for (name, bmib), keys in groups.items():
+        best_k = max(keys, key=lambda k: blocks[k]["mib_s"])
+        best = blocks[best_k]["mib_s"]
+        if head and head[1] == name and abs(head[2] - bmib) < 0.5 and head[0] > best:
+            best, best_k = head[0], "headline"
+        if best <= bmib:
+            continue
+        raised[f"{name}@{bmib}"] = round(best, 1)
+        for k in keys:
+            blocks[k]["bound_mib_s"] = round(best, 1)
+            blocks[k]["frac_of_bound"] = round(blocks[k]["mib_s"] / best, 3)
+            blocks[k]["bound_observed"] = best_k
+    return raised
 
 
 def recv_cost(cpu: dict) -> float | None:
@@ -228,7 +323,7 @@ def fit_line(out: dict, blocks: dict[str, dict], target: int = LINE_TARGET, limi
     if _size(line) <= target:
         return line
     core = ("ok", "mib_s", "p50_ms", "p99_ms", "frac_of_bound", "vs_discard_twin", "vs_ref_effective",
-            "recv_cpu_s_per_gib", "headline_frac_of_ceiling", "error")
+            "recv_cpu_s_per_gib", "headline_frac_of_ceiling", "vs_baseline_paired", "h2_frames", "error")
     for k in comp:  # 2: side blocks down to their core scalars
         comp[k] = {f: v for f, v in comp[k].items() if f in core}
     line.update(comp)

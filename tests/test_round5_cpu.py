@@ -17,7 +17,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ALL_BLOCKS = ("cpu_baseline", "cpu_baseline_http", "compare", "cpu_baseline_before", "sliced", "ceiling",
               "ref_default_http", "ref_default_grpc", "ref_effective_grpc", "ref_default_100m_http_discard",
               "ref_default_100m_http_gpu", "ref_default_100m_grpc_discard", "ref_default_100m_grpc_gpu",
-              "c1_http_cpu", "list_read_grpc", "list_read_http", "write", "write_composite", "fanout")
+              "c1_http_cpu", "list_read_grpc", "list_read_http", "write", "write_composite", "fanout",
+              "large_framing", "ref_default_grpc_large", "list_read_grpc_large", "ref_effective_head")
 
 
 def _worst_block(i: int) -> dict:
@@ -99,7 +100,7 @@ def test_paired_summary_median_resists_one_slow_window():
     # the TCP arm: a paired fraction of the raw one-stream ceiling
     s3 = rp.paired_summary([{"head": 27000, "tcp": 30000}, {"head": 26000, "tcp": 29000},
                             {"head": 25000, "tcp": 24000}])
-    assert s3["headline_frac_of_ceiling"] == 0.9 and len(s3["tcp_ratios"]) == 3  # median of 0.897, 0.9, 1.042
+    assert s3["headline_vs_tcp_paired"] == 0.9 and len(s3["tcp_ratios"]) == 3  # median of 0.897, 0.9, 1.042
 
 
 def test_frac_of_bound_is_a_ceiling():
@@ -116,6 +117,36 @@ def test_frac_of_bound_is_a_ceiling():
     assert rp.frac_of_bound(20000.0, 0.0, 30.0, 1, False)["bound"] == "tcp_1conn"
     # h2d below TCP: h2d is the bound
     assert rp.frac_of_bound(20000.0, 25.0, 30.0, 1, True)["bound"] == "h2d"
+
+
+def test_unified_ceiling_is_the_best_probe():
+    # the paired probes are whole-job rates: per GPU they are / world
+    u = rp.unified_ceiling(25000.0, [2 * 27000.0, 2 * 29000.0], {"ok": True, "tcp_gbps": 29.0e9 / (1 << 20) / 1e3
+                                                                  * 1e3 * (1 << 20) / 1e9 * 1.0, "h2d_gbps": 50.0},
+                           2, True)
+    assert u["tcp_probes"] == 3 and u["tcp_best_mib_s"] == 29000.0 and u["ceiling_bound"] == "tcp_1conn"
+    assert u["headline_frac_of_ceiling"] == round(25000.0 / 29000.0, 3)
+    # h2d below TCP: h2d is the ceiling
+    u = rp.unified_ceiling(20000.0, [30000.0], {"ok": True, "tcp_gbps": 0.0, "h2d_gbps": 22.0}, 1, True)
+    assert u["ceiling_bound"] == "h2d" and u["headline_frac_of_ceiling"] == round(20000.0 / (22.0 * rp.MIB_PER_GBPS), 3)
+    # a headline faster than every probe: the probe was no ceiling
+    u = rp.unified_ceiling(31000.0, [30000.0], None, 1, False)
+    assert u["headline_frac_of_ceiling"] == 1.0 and u["ceiling_observed"] == "headline"
+    assert rp.unified_ceiling(1.0, None, None, 1, True) == {}
+
+
+def test_observed_bounds_never_beaten():
+    blocks = {"a": {"mib_s": 31000.0, "bound": "tcp_1conn", "bound_mib_s": 30000.0, "frac_of_bound": 1.033},
+              "b": {"mib_s": 24000.0, "bound": "tcp_1conn", "bound_mib_s": 30000.0, "frac_of_bound": 0.8},
+              "c": {"mib_s": 40000.0, "bound": "h2d", "bound_mib_s": 48000.0, "frac_of_bound": 0.833},
+              "d": {"mib_s": 20000.0, "bound": "tcp_1conn", "bound_mib_s": 22000.0, "frac_of_bound": 0.909}}
+    raised = rp.observed_bounds(blocks, (32000.0, "tcp_1conn", 30000.0))
+    # the headline beat both the probe and block a: its rate is the bound of the group
+    assert raised == {"tcp_1conn@30000.0": 32000.0}
+    assert blocks["a"]["frac_of_bound"] == round(31000 / 32000, 3) and blocks["a"]["bound_observed"] == "headline"
+    assert blocks["b"]["frac_of_bound"] == 0.75 and blocks["c"]["frac_of_bound"] == 0.833
+    assert blocks["d"]["frac_of_bound"] == 0.909  # another bound group, untouched
+    assert all(b["frac_of_bound"] <= 1.0 for b in blocks.values())
 
 
 def test_attribute_windows_names_the_cause():
@@ -163,16 +194,26 @@ def test_bench_line_fits_the_driver_tail(gpus, tmp_path):
     # the sidecar holds the verbose views and the same line
     d = json.loads(diag.read_text())
     assert d["line"] == line and "blocks" in d and "placement" in d
+    # the paired headline at every N (each rank the same arm order between barriers)
+    assert line["paired"]["chunks"] == 4 and 0.2 < line["vs_baseline_paired"] < 5.0
+    assert len(d["paired"]["windows"]) == 8  # 4 chunks x (head, base): no nodma without a GPU
+    # each chunk's first read is reported, after the arm's untimed re-warm read
+    assert line["paired"]["rewarm_reads"] == 1 and len(line["paired"]["head_first_vs_median"]) == 4
+    assert all(len(w["first_read"]) == 3 for w in d["paired"]["windows"])
+    # the headline config at the other framing, paired with its baseline
+    assert line["large_framing"]["ok"] and line["large_framing"]["h2_frames"] == "16MiB"
+    assert line["large_framing"]["vs_baseline_paired"] > 0 and line["h2_frames"] == "16KiB"
+    # one ceiling: no block beats its bound
+    for k, b in line.items():
+        if isinstance(b, dict) and "frac_of_bound" in b:
+            assert b["frac_of_bound"] <= 1.0, (k, b)
     if gpus == 1:
-        # N = 1: the paired headline and its per-chunk windows
-        assert line["paired"]["chunks"] == 4 and 0.3 < line["vs_baseline_paired"] < 3.0
-        assert len(d["paired"]["windows"]) == 8  # 4 chunks x (head, base): no nodma without a GPU
         assert line["ref_effective_grpc"]["ok"] and line["ref_default_100m_grpc_discard"]["vs_ref_effective"] > 0
         # the effective-path twin of the headline config, next to vs_baseline
         assert line["ref_effective_head"]["ok"] and line["headline_vs_ref_effective"] > 0
         assert "host" in d["blocks"]["compare"]
     else:
-        assert "paired" not in line and len(line["per_rank_mib_s"]) == 8
+        assert len(line["per_rank_mib_s"]) == 8
 
 
 def test_native_stdout_noise_goes_to_stderr():

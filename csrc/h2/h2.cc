@@ -1,6 +1,5 @@
 #include "h2/h2.h"
 
-#include <sys/mman.h>
 #include <sys/uio.h>
 
 #include <chrono>
@@ -70,28 +69,6 @@ bool apply_settings_payload(const uint8_t* p, size_t n, H2Settings* s) {
     }
   }
   return true;
-}
-
-StableBytes::~StableBytes() {
-  if (base_) ::munmap(base_, kChunk);
-}
-
-const uint8_t* StableBytes::put(const void* p, size_t n) {
-  if (n > kChunk) throw std::logic_error("StableBytes::put: piece larger than a chunk");
-  if (!base_ || used_ + n > kChunk) {
-    if (base_) ::munmap(base_, kChunk);  // referenced pages outlive the mapping, unchanged
-    void* m = ::mmap(nullptr, kChunk, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
-    if (m == MAP_FAILED) {
-      base_ = nullptr;
-      throw StorageError("StableBytes: mmap failed", true);
-    }
-    base_ = static_cast<uint8_t*>(m);
-    used_ = 0;
-  }
-  uint8_t* d = base_ + used_;
-  std::memcpy(d, p, n);
-  used_ += n;
-  return d;
 }
 
 namespace {
@@ -243,13 +220,10 @@ void H2Writer::write_frame_pieces(uint8_t type, uint8_t flags, uint32_t stream, 
 void H2Writer::write_data_train(uint32_t stream, const std::vector<SendPiece>& pieces, size_t total,
                                 uint8_t last_flags, const std::string* lead_headers, const std::string* trailers) {
   const size_t fmax = std::max<size_t>(1, peer_max_frame_.load());
-  bool any_splice = false, any_fd = false;
-  for (const SendPiece& p : pieces) {
-    any_splice |= p.splice && p.n > 0;
-    any_fd |= p.fd >= 0 && p.n > 0;
-  }
-  if (any_fd || total <= fmax) {
-    // one frame, or sendfile pieces: frame by frame (write_frame_pieces)
+  bool any_fd = false;
+  for (const SendPiece& p : pieces) any_fd |= p.fd >= 0 && p.n > 0;
+  if (any_fd || total <= fmax || fmax >= kTrainCopyMaxFrame) {
+    // one frame, large frames or sendfile pieces: frame by frame (zero copy)
     size_t idx = 0, off = 0, left = total;
     bool first = true;
     std::vector<SendPiece> frame;
@@ -281,35 +255,28 @@ void H2Writer::write_data_train(uint32_t stream, const std::vector<SendPiece>& p
   const size_t nframes = (total + fmax - 1) / fmax;
   std::vector<iovec> iov;
   iov.reserve(pieces.size() + 3 * nframes + 4);
-  std::vector<uint8_t> hdrs(9 * (nframes + 2));  // writev path: headers live here until the write
+  std::vector<uint8_t> hdrs(9 * (nframes + 2));  // the headers live here until the write
   size_t hpos = 0;
-  WriteLock lk(*this);
-  auto small = [&](const void* p, size_t n) {
-    if (n) iov.push_back({const_cast<uint8_t*>(any_splice ? stable_.put(p, n) : static_cast<const uint8_t*>(p)), n});
-  };
   auto header = [&](uint32_t len, uint8_t type, uint8_t flags) {
     uint8_t* h = &hdrs[hpos];
     hpos += 9;
     encode_frame_header(h, len, type, flags, stream);
-    small(h, 9);
+    iov.push_back({h, 9});
   };
   if (lead_headers) {
     header(static_cast<uint32_t>(lead_headers->size()), h2::kHeaders, h2::kFlagEndHeaders);
-    small(lead_headers->data(), lead_headers->size());
+    if (!lead_headers->empty()) iov.push_back({const_cast<char*>(lead_headers->data()), lead_headers->size()});
   }
-  size_t idx = 0, off = 0, left = total;
+  size_t idx = 0, off = 0, left = total, frames = 0;
   while (left > 0) {
     const size_t n = std::min(left, fmax);
     left -= n;
     header(static_cast<uint32_t>(n), h2::kData, left == 0 ? last_flags : 0);
-    note_data_frame();
+    ++frames;
     for (size_t need = n; need > 0;) {
       const SendPiece& src = pieces[idx];
       const size_t k = std::min(need, src.n - off);
-      if (k) {
-        if (src.splice) iov.push_back({const_cast<uint8_t*>(src.p + off), k});
-        else small(src.p + off, k);
-      }
+      if (k) iov.push_back({const_cast<uint8_t*>(src.p + off), k});
       need -= k;
       off += k;
       if (off == src.n) {
@@ -320,12 +287,11 @@ void H2Writer::write_data_train(uint32_t stream, const std::vector<SendPiece>& p
   }
   if (trailers) {
     header(static_cast<uint32_t>(trailers->size()), h2::kHeaders, h2::kFlagEndHeaders | h2::kFlagEndStream);
-    small(trailers->data(), trailers->size());
+    if (!trailers->empty()) iov.push_back({const_cast<char*>(trailers->data()), trailers->size()});
   }
-  if (any_splice)
-    conn_.splice_iov_all(iov.data(), static_cast<int>(iov.size()));
-  else
-    conn_.writev_all(iov.data(), static_cast<int>(iov.size()));
+  WriteLock lk(*this);
+  for (size_t i = 0; i < frames; ++i) note_data_frame();
+  conn_.writev_all(iov.data(), static_cast<int>(iov.size()));
 }
 
 void H2Writer::write_headers(uint32_t stream, const std::string& block, bool end_stream) {

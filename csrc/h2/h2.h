@@ -73,27 +73,6 @@ struct SendPiece {
   bool splice = false;
 };
 
-// Append-only small-byte store for zero-copy sends: a byte vmsplice()d into
-// a pipe is referenced, not copied, until the peer has read it, so it must
-// never change.  put() copies into an mmap()ed chunk and never reuses a
-// byte; a full chunk is munmap()ed (pages still referenced by a pipe or the
-// socket stay alive, unchanged, until the kernel drops them) and a fresh one
-// mapped.  Frame headers and the gRPC / protobuf framing around spliced
-// payload pages go through it.
-class StableBytes {
- public:
-  StableBytes() = default;
-  ~StableBytes();
-  StableBytes(const StableBytes&) = delete;
-  StableBytes& operator=(const StableBytes&) = delete;
-  const uint8_t* put(const void* p, size_t n);
-  static constexpr size_t kChunk = 1u << 20;
-
- private:
-  uint8_t* base_ = nullptr;
-  size_t used_ = 0;
-};
-
 // Mutual exclusion granted in arrival order, one wake per hand-off.  The
 // frame writes of a connection's streams go through it: a std::mutex lets
 // the thread that just wrote a frame take the lock straight back, so with 48
@@ -153,14 +132,16 @@ class H2Writer {
   // A train of DATA frames of one stream in ONE write: `total` payload bytes
   // (send window already reserved, e.g. try_reserve_train) cut into frames
   // of at most the peer's SETTINGS_MAX_FRAME_SIZE, `last_flags` on the last
-  // one; lead_headers / trailers as in write_frame_pieces.  With a `splice`
-  // piece every byte goes by vmsplice (headers and small pieces through
-  // StableBytes): two system calls per pipe-full (~40 frames of 16 KiB)
-  // instead of three per frame; without one a single writev.  `fd` pieces
-  // (sendfile) fall back to a write_frame_pieces per frame.  At the RFC
-  // default of 16 KiB frames -- what a client that does not advertise a
-  // larger SETTINGS_MAX_FRAME_SIZE, grpc-go's, receives -- the endpoint
-  // would otherwise be the bound of every gRPC read.
+  // one; lead_headers / trailers as in write_frame_pieces.  Frames below
+  // kTrainCopyMaxFrame go as ONE writev of every header and payload piece
+  // (the kernel copies the payload; a `splice` piece is read as memory):
+  // at the RFC default of 16 KiB -- what a client that advertises no larger
+  // SETTINGS_MAX_FRAME_SIZE, grpc-go's, receives -- vmsplice()ing a 9-byte
+  // header and 4 pages per frame stalled reads for up to 1.2 s on loopback
+  // (5 of 8 reads > 90 ms), one write per 1 MiB of frames did not.  Larger
+  // frames keep write_frame_pieces (vmsplice / sendfile per frame), as do
+  // `fd` pieces.
+  static constexpr size_t kTrainCopyMaxFrame = 256u << 10;
   void write_data_train(uint32_t stream, const std::vector<SendPiece>& pieces, size_t total, uint8_t last_flags,
                         const std::string* lead_headers = nullptr, const std::string* trailers = nullptr);
   // Header block (HEADERS + CONTINUATION as needed).
@@ -231,7 +212,6 @@ class H2Writer {
   std::mutex ctl_mu_;        // guards ctl_pending_; taken before wmu_'s own mutex
   std::string ctl_pending_;  // encoded control frames waiting for the writer
   size_t quantum_ = 0;
-  StableBytes stable_;  // under wmu_
   H2SendStats sstats_;
   H2SendStats* sink_ = nullptr;
   std::mutex fmu_;  // flow control

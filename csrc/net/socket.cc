@@ -580,32 +580,6 @@ void Conn::splice_user_all(const void* data, size_t n, bool more) {
   }
 }
 
-void Conn::splice_iov_all(const struct iovec* iov_in, int cnt, bool more) {
-  if (fd_ < 0) throw StorageError("write on closed connection", true);
-  std::vector<iovec> v(iov_in, iov_in + cnt);
-  if (ssl_) return writev_all(v.data(), cnt, more);
-  ensure_pipe();
-  size_t i = 0;
-  while (i < v.size()) {
-    const int m = static_cast<int>(std::min<size_t>(v.size() - i, 1024));
-    ssize_t k = ::vmsplice(pipe_[1], &v[i], static_cast<unsigned long>(m), 0);
-    if (k < 0) {
-      if (errno == EINTR) continue;
-      throw StorageError(std::string("vmsplice: ") + std::strerror(errno), true);
-    }
-    size_t left = static_cast<size_t>(k);
-    while (i < v.size() && left >= v[i].iov_len) {
-      left -= v[i].iov_len;
-      ++i;
-    }
-    if (left) {
-      v[i].iov_base = static_cast<uint8_t*>(v[i].iov_base) + left;
-      v[i].iov_len -= left;
-    }
-    splice_out(static_cast<size_t>(k), more || i < v.size());
-  }
-}
-
 void Conn::sendfile_all(int in_fd, uint64_t off, size_t n, bool more) {
   if (fd_ < 0) throw StorageError("write on closed connection", true);
   if (ssl_) {  // no kernel TLS here: fall back to pread + SSL_write

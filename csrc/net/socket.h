@@ -124,9 +124,6 @@ class Conn {
   // the caller must leave them unchanged until the peer has read the bytes
   // (for an upload: until its final response).  TLS falls back to a copy.
   void splice_user_all(const void* p, size_t n, bool more = false);
-  // Same for an iovec list, in order (vmsplice takes many segments per call;
-  // every segment's memory must stay unchanged until the peer read it).
-  void splice_iov_all(const struct iovec* iov, int cnt, bool more = false);
   void shutdown_write();
   void close();
   int fd() const { return fd_; }

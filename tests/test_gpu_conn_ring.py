@@ -21,17 +21,26 @@ def _runner(native, server, workers, reads, slot_bytes, slots, proto="grpc", **k
     return native.Runner(cfg)
 
 
+FRAMES = {"ref": {"h2_max_frame_size": 0, "h2_window": 16 << 20},
+          "ref_nospan": {"h2_max_frame_size": 0, "h2_window": 16 << 20, "h2_span_max_frame": 0},
+          "large": {"h2_max_frame_size": (1 << 24) - 1, "h2_window": 0x7FFFFFFF}}
+
+
+@pytest.mark.parametrize("frames", ["ref", "ref_nospan", "large"])
 @pytest.mark.parametrize("proto,slot_bytes,slots,inplace", [("grpc", 1 << 20, 4, False), ("grpc", 1 << 20, 2, False),
                                                             ("grpc", 64 << 10, 3, False), ("grpc", 1 << 20, 4, True),
                                                             ("grpc", 64 << 10, 3, True), ("http2", 1 << 20, 4, False)])
-def test_conn_ring_many_streams_byte_exact(native, server, gpu_available, proto, slot_bytes, slots, inplace):
+def test_conn_ring_many_streams_byte_exact(native, server, gpu_available, proto, slot_bytes, slots, inplace, frames):
     """12 streams on one connection; inplace: the arena (the reader recv()s
-    into the ring itself, the sinks take their runs in place)."""
+    into the ring itself, the sinks take their runs in place); frames: the
+    HTTP/2 receive settings (the reference's 16 KiB frames with and without
+    the multi-frame spanning receive, or 16 MiB frames)."""
     workers = 12
     sizes = [(3 << 20) + 4099 * i + 77 for i in range(workers)]
     for i, n in enumerate(sizes):
         server.add_synthetic(B, P, "", i, 1, n)
-    r = _runner(native, server, workers, 3, slot_bytes, slots, proto=proto, conn_ring_inplace=inplace)
+    r = _runner(native, server, workers, 3, slot_bytes, slots, proto=proto, conn_ring_inplace=inplace,
+                **FRAMES[frames])
     r.start()
     r.wait()
     s = r.summary()

@@ -48,11 +48,12 @@ def read_response_msg(native, content):
 
 
 class RawPeer:
-    """Accepts one connection, answers the first request stream with `plan`
-    (a function of the gRPC byte stream returning the frames to send)."""
+    """Accepts one connection, waits for `nreq` request streams and answers
+    them with build(stream ids) (the frames to send)."""
 
-    def __init__(self, build):
+    def __init__(self, build, nreq=1):
         self.build = build
+        self.nreq = nreq
         self.ls = socket.socket()
         self.ls.bind(("127.0.0.1", 0))
         self.ls.listen(1)
@@ -83,14 +84,14 @@ class RawPeer:
             while len(got) < 24:
                 got += c.recv(24 - len(got))
             c.sendall(frame(4, 0, 0, b""))  # our SETTINGS (all defaults)
-            sid = None
-            while sid is None:
+            sids = []
+            while len(sids) < self.nreq:
                 t, fl, s, p = self.recv_frame(c)
                 if t == 4 and not (fl & 1):
                     c.sendall(frame(4, 1, 0, b""))
                 if t == 0 and (fl & 1):
-                    sid = s
-            c.sendall(b"".join(self.build(sid)))
+                    sids.append(s)
+            c.sendall(b"".join(self.build(sids[0] if self.nreq == 1 else sids)))
             while True:
                 self.recv_frame(c)
         except (EOFError, OSError):
@@ -215,3 +216,41 @@ def test_end_stream_on_last_data(native, contents):
     c = native.Client({"protocol": "grpc", "endpoint": peer.url, "h2_max_frame_size": 0, "retry_max_attempts": 1})
     with pytest.raises(Exception, match="without trailers|grpc-status|code"):
         c.read_bytes("b", "o")
+
+
+def test_two_streams_interleaved_frame_by_frame(native, contents):
+    """Two reads multiplexed on one connection (gRPC pool 1), their DATA
+    frames alternating in runs of 1..3: every spanning plan meets the other
+    stream's frame.  Both land byte-exact (discard sink, host CRC32C)."""
+    other = [make_content(200001, 9), make_content(16384 * 2 + 5, 10)]
+
+    def build(sids):
+        a = split(stream_of(native, contents), [16384])
+        b = split(stream_of(native, other), [16384])
+        out = [resp_headers(sids[0]), resp_headers(sids[1])]
+        i = j = k = 0
+        while i < len(a) or j < len(b):
+            for _ in range(1 + k % 3):
+                if i < len(a):
+                    out.append(frame(0, 0, sids[0], a[i]))
+                    i += 1
+            for _ in range(1 + (k + 1) % 3):
+                if j < len(b):
+                    out.append(frame(0, 0, sids[1], b[j]))
+                    j += 1
+            k += 1
+        return out + [trailers(sids[0]), trailers(sids[1])]
+
+    peer = RawPeer(build, nreq=2)
+    s0 = native.h2_reader_stats()
+    r = native.Runner({"protocol": "grpc", "endpoint": peer.url, "bucket": "b", "object_names": ["o"], "workers": 2,
+                       "reads_per_worker": 1, "sink": "discard", "grpc_conn_pool_size": 1, "keep_records": True,
+                       "retry_max_attempts": 1, "h2_max_frame_size": 0})
+    r.start()
+    r.wait()
+    s = r.summary()
+    d = native.h2_reader_stats()
+    assert s["errors"] == 0 and s["verified"] == 2, s["first_error"]
+    got = sorted(x["bytes"] for x in r.drain())
+    assert got == sorted([sum(map(len, contents)), sum(map(len, other))])
+    assert d["span_spills"] > s0["span_spills"]

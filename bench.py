@@ -21,10 +21,14 @@ N: each rank runs the same arm order between barriers; the headline's value
 counts only its own chunks): vs_baseline_paired and headline_vs_nodma are the
 medians of the per-chunk ratios.
 
-gRPC runs at the reference's HTTP/2 receive settings (--h2-framing ref):
-grpc-go advertises no SETTINGS_MAX_FRAME_SIZE, so the endpoint sends 16 KiB
-DATA frames, and its windows stop at 16 MiB (/root/reference/go.mod:20,
-main.go:106-117).  The client receives many frames per recvmsg()
+HTTP/2 framing: the reference's grpc-go client advertises no
+SETTINGS_MAX_FRAME_SIZE, so its peer sends 16 KiB DATA frames, and its windows
+stop at 16 MiB (/root/reference/go.mod:20, main.go:106-117).  The headline
+runs 16 MiB frames (--h2-framing large, one frame per 2 MiB message, as in
+rounds 2-5); the ref_framing side block runs the headline config at the
+reference's settings, paired chunk by chunk with its reference-semantics
+baseline at the same settings, and so do list_read_grpc_ref and
+ref_default_grpc_ref.  The client receives many 16 KiB frames per recvmsg()
 (csrc/h2/h2_client.h H2DataCursor).
 
 Output: rank 0 prints ONE JSON line (<= 8 KiB, the driver keys first, side
@@ -238,10 +242,14 @@ def build_parser() -> argparse.ArgumentParser:
                     help="untimed reads of each paired arm right before its chunk (outside the barriers): the "
                          "reference reads back to back, so a chunk's first read should not pay for the connection "
                          "and copy engines idling through the other arms (0 = off)")
-    ap.add_argument("--h2-framing", default="ref", choices=["ref", "large"],
-                    help="HTTP/2 receive settings of every gRPC client: ref = the reference's grpc-go (no "
+    ap.add_argument("--h2-framing", default="large", choices=["ref", "large"],
+                    help="HTTP/2 receive settings of the gRPC clients: ref = the reference's grpc-go (no "
                          "SETTINGS_MAX_FRAME_SIZE advertised -> 16 KiB DATA frames, 16 MiB stream/connection "
-                         "windows); large = 16 MiB frames and 2 GiB windows (one frame per 2 MiB message)")
+                         "windows); large = 16 MiB frames and 2 GiB windows (one frame per 2 MiB message).  The "
+                         "headline keeps large: at 16 KiB frames the synthetic endpoint's one send thread per "
+                         "connection is the bound (~12 GB/s copying frame trains, README), so a ref headline would "
+                         "measure the endpoint; the ref_framing block pairs the headline config at 16 KiB frames "
+                         "with its reference-semantics baseline")
     ap.add_argument("--framing-twin", default="on", choices=["on", "off"],
                     help="side blocks at the OTHER framing: the headline paired chunk by chunk with its "
                          "reference-semantics baseline, list_read_grpc and ref_default_grpc")

@@ -249,6 +249,10 @@ class GpuSink : public Sink {
   bool ring_waiting_ = false;
   int ring_open_slot_ = -1;  // ring slot / segment index of this sink's open segment (-1: none)
   size_t ring_open_seg_ = 0;
+  uint64_t ring_open_gen_ = 0;  // ... and that slot's fill generation (RSlot::gen)
+  // this sink's open segment is the last of the reader's current slot, in
+  // the same fill of it, and not submitted yet: more bytes may extend it
+  bool ring_extends(const ConnRing& R) const;
   struct ChunkMark {
     uint64_t start = 0, end = 0;
     bool closed = false, has_crc = false, broken = false;
@@ -305,6 +309,11 @@ class ConnRing : public RecvArena {
     size_t submitted = 0;  // segs handed to the submitter
     size_t collected = 0;  // segs whose results were copied out
     bool filling = false;  // the reader's current slot
+    // fills of this slot so far: a sink's remembered (slot, segment) from an
+    // earlier fill must never extend another sink's segment that now sits at
+    // the same index (with 16 KiB frames of 12 streams a slot wraps between
+    // two frames of one stream)
+    uint64_t gen = 0;
     hipStream_t st = nullptr;
     int st_idx = -1;
     uint32_t* tiles = nullptr;

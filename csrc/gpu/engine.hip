@@ -1333,9 +1333,17 @@ ConnRing::RSlot& ConnRing::take_slot_locked(std::unique_lock<std::mutex>& lk) {
   r.used = 0;
   r.submitted = r.collected = 0;
   r.filling = true;
+  ++r.gen;
   cur_ = next_;
   next_ = (next_ + 1) % static_cast<int>(slots_.size());
   return r;
+}
+
+bool GpuSink::ring_extends(const ConnRing& R) const {
+  if (R.cur_ < 0 || ring_open_slot_ != R.cur_) return false;
+  const ConnRing::RSlot& r = R.slots_[R.cur_];
+  return ring_open_gen_ == r.gen && ring_open_seg_ + 1 == r.segs.size() && ring_open_seg_ >= r.submitted &&
+         r.segs[ring_open_seg_].owner == this;
 }
 
 Window GpuSink::ring_acquire() {
@@ -1350,13 +1358,12 @@ Window GpuSink::ring_acquire() {
   R.window_open_ = false;  // a window the reader never committed (its recv failed) is dropped
   R.window_owner_ = nullptr;
   ConnRing::RSlot* r = R.cur_ >= 0 ? &R.slots_[R.cur_] : nullptr;
-  const bool mine = r && ring_open_slot_ == R.cur_ && ring_open_seg_ + 1 == r->segs.size() &&
-                    ring_open_seg_ >= r->submitted;
+  const bool mine = r && ring_extends(R);
   if (!r || r->used == R.slot_bytes_ || (!mine && r->segs.size() >= static_cast<size_t>(kMaxSeg))) {
     r = &R.take_slot_locked(lk);
     ring_open_slot_ = -1;
   }
-  if (!(ring_open_slot_ == R.cur_ && ring_open_seg_ + 1 == r->segs.size() && ring_open_seg_ >= r->submitted)) {
+  if (!ring_extends(R)) {
     ConnRing::Seg g;
     g.owner = this;
     g.seq = ring_res_.size();
@@ -1368,6 +1375,7 @@ Window GpuSink::ring_acquire() {
     r->segs.push_back(g);
     ring_open_slot_ = R.cur_;
     ring_open_seg_ = r->segs.size() - 1;
+    ring_open_gen_ = r->gen;
   }
   size_t cap = R.slot_bytes_ - r->used;
   if (obj_cap_ - delivered_ < cap) cap = obj_cap_ - delivered_;
@@ -1407,7 +1415,7 @@ void GpuSink::commit_inplace(const uint8_t* p, size_t n) {
   if (p < r.host || p + n > r.host + r.used)
     throw std::logic_error("GpuSink::commit_inplace: bytes outside the arena's current slot");
   const uint32_t off = static_cast<uint32_t>(p - r.host);
-  bool extend = ring_open_slot_ == R.cur_ && ring_open_seg_ + 1 == r.segs.size() && ring_open_seg_ >= r.submitted;
+  bool extend = ring_extends(R);
   if (extend) {
     const ConnRing::Seg& g = r.segs.back();
     extend = g.owner == this && g.slot_off + g.len == off;
@@ -1431,6 +1439,7 @@ void GpuSink::commit_inplace(const uint8_t* p, size_t n) {
     r.segs.push_back(g);
     ring_open_slot_ = R.cur_;
     ring_open_seg_ = r.segs.size() - 1;
+    ring_open_gen_ = r.gen;
   }
   delivered_ += n;
 }

@@ -25,7 +25,7 @@ step() {  # step <name> <timeout> <cmd...>
 step import 300 python -c "import custom_go_client_benchmark_amd as p; print(p._native.__file__)" || exit 1
 step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step bench 600 python bench.py --steps ${BENCH_STEPS:-20} --warmup 3 --json-out $OUT/bench.json
+step bench 600 python -X faulthandler bench.py --steps ${BENCH_STEPS:-20} --warmup 3 --json-out $OUT/bench.json
 if [ "${PROFILE:-1}" = "1" ]; then
   step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- \
     python bench.py --steps 10 --warmup 2

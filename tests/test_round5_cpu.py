@@ -18,7 +18,7 @@ ALL_BLOCKS = ("cpu_baseline", "cpu_baseline_http", "compare", "cpu_baseline_befo
               "ref_default_http", "ref_default_grpc", "ref_effective_grpc", "ref_default_100m_http_discard",
               "ref_default_100m_http_gpu", "ref_default_100m_grpc_discard", "ref_default_100m_grpc_gpu",
               "c1_http_cpu", "list_read_grpc", "list_read_http", "write", "write_composite", "fanout",
-              "large_framing", "ref_default_grpc_large", "list_read_grpc_large", "ref_effective_head")
+              "ref_framing", "ref_default_grpc_ref", "list_read_grpc_ref", "ref_effective_head")
 
 
 def _worst_block(i: int) -> dict:
@@ -201,8 +201,9 @@ def test_bench_line_fits_the_driver_tail(gpus, tmp_path):
     assert line["paired"]["rewarm_reads"] == 1 and len(line["paired"]["head_first_vs_median"]) == 4
     assert all(len(w["first_read"]) == 3 for w in d["paired"]["windows"])
     # the headline config at the other framing, paired with its baseline
-    assert line["large_framing"]["ok"] and line["large_framing"]["h2_frames"] == "16MiB"
-    assert line["large_framing"]["vs_baseline_paired"] > 0 and line["h2_frames"] == "16KiB"
+    assert line["ref_framing"]["ok"] and line["ref_framing"]["h2_frames"] == "16KiB"
+    assert line["ref_framing"]["vs_baseline_paired"] > 0 and line["h2_frames"] == "16MiB"
+    assert line["list_read_grpc_ref"]["ok"] and line["ref_default_grpc_ref"]["h2_frames"] == "16KiB"
     # one ceiling: no block beats its bound
     for k, b in line.items():
         if isinstance(b, dict) and "frac_of_bound" in b:

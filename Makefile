@@ -23,7 +23,7 @@ CORE_SRCS := csrc/core/crc32c.cc csrc/core/affinity.cc csrc/core/ceiling.cc csrc
              csrc/net/socket.cc csrc/net/tcp_chrono.cc csrc/net/buffered.cc \
              csrc/http1/http1.cc csrc/h2/hpack.cc csrc/h2/h2.cc csrc/h2/h2_client.cc csrc/proto/storage_v2.cc \
              csrc/storage/sink.cc csrc/storage/sliced.cc csrc/storage/auth.cc csrc/storage/client.cc csrc/storage/http_client.cc \
-             csrc/storage/grpc_client.cc csrc/storage/host_arena.cc \
+             csrc/storage/grpc_client.cc \
              csrc/server/store.cc csrc/server/media.cc csrc/server/fakegcs.cc csrc/server/server_http1.cc csrc/server/server_grpc.cc \
              csrc/gpu/crc_host.cc
 GPU_SRCS  := csrc/gpu/crc32c_kernels.hip csrc/gpu/engine.hip csrc/gpu/copy_engines.hip
@@ -36,15 +36,11 @@ PY_OBJS   := $(patsubst csrc/%.cc,$(BUILD)/%.o,$(PY_SRCS))
 EXT := $(PKG)/_native$(EXT_SUFFIX)
 TOOLS := fakegcs read_operation ssd_test write_operations list_operation open_file small_poc loopback_ceiling
 TOOL_BINS := $(addprefix $(PKG)/bin/,$(TOOLS))
-# experiment probes (not part of the default build): make probes
-PROBES := splice_probe zc_probe
-PROBE_BINS := $(addprefix $(PKG)/bin/,$(PROBES)) $(PKG)/bin/ring_dma_probe $(PKG)/bin/graph_probe
 
-.PHONY: all clean ext tools probes asan tsan stress
+.PHONY: all clean ext tools asan tsan stress
 all: ext tools
 ext: $(EXT)
 tools: $(TOOL_BINS)
-probes: $(PROBE_BINS)
 
 $(BUILD)/%.o: csrc/%.cc
 	@mkdir -p $(dir $@)
@@ -61,18 +57,6 @@ $(BUILD)/libgcsbcore.a: $(CORE_OBJS)
 $(EXT): $(PY_OBJS) $(GPU_OBJS) $(BUILD)/libgcsbcore.a
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(PY_OBJS) $(GPU_OBJS) $(BUILD)/libgcsbcore.a \
 	  -L/opt/rocm/lib -lamdhip64 -lhsa-runtime64 -lrocprofiler-sdk-roctx $(LDLIBS) -Wl,-rpath,/opt/rocm/lib
-
-$(PKG)/bin/ring_dma_probe: csrc/tools/ring_dma_probe.hip
-	@mkdir -p $(PKG)/bin
-	$(HIPCC) --offload-arch=$(ARCH) -O2 -std=c++17 -o $@ $< -L/opt/rocm/lib -lamdhip64 -pthread -Wl,-rpath,/opt/rocm/lib
-
-$(BUILD)/tools/graph_probe.o: csrc/tools/graph_probe.hip
-	@mkdir -p $(dir $@)
-	$(HIPCC) $(HIPFLAGS) -MMD -MP -c $< -o $@
-
-$(PKG)/bin/graph_probe: $(BUILD)/tools/graph_probe.o $(BUILD)/gpu/crc32c_kernels.o $(BUILD)/libgcsbcore.a
-	@mkdir -p $(PKG)/bin
-	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^ -L/opt/rocm/lib -lamdhip64 $(LDLIBS) -Wl,-rpath,/opt/rocm/lib
 
 $(PKG)/bin/%: csrc/tools/%.cc $(BUILD)/libgcsbcore.a
 	@mkdir -p $(PKG)/bin $(BUILD)/tools
@@ -110,6 +94,6 @@ stress: $(BUILD)/plain/stress
   $(patsubst csrc/%.cc,$(BUILD)/plain/%.d,$(SAN_SRCS))
 
 clean:
-	rm -rf $(BUILD) $(EXT) $(TOOL_BINS) $(PROBE_BINS)
+	rm -rf $(BUILD) $(EXT) $(TOOL_BINS)
 
 -include $(CORE_OBJS:.o=.d) $(GPU_OBJS:.o=.d) $(PY_OBJS:.o=.d) $(wildcard $(BUILD)/tools/*.d)

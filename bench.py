@@ -80,59 +80,16 @@ def build_parser() -> argparse.ArgumentParser:
                          "still in the receiving CCD's L3; against 8 x 2 MiB the receive copy went 0.046 -> 0.036 "
                          "CPU-s/GiB, 22.0k -> 27.5k MiB/s interleaved (profiles/r4_main8, profiles/r4_recvcost)")
     ap.add_argument("--slots", type=int, default=4)
-    ap.add_argument("--ring-wc", default="off", choices=["on", "off"],
-                    help="the headline sink's ring in write-combined pinned memory (the receive copy's stores skip "
-                         "the CPU caches); A/B against the cached ring")
-    ap.add_argument("--conn-ring", default="4x1MiB",
-                    help="GPU sink on one multiplexed gRPC connection (list_read_grpc, ref_default_100m_grpc_gpu): "
-                         "every worker's stream through one connection ring of SLOTSxBYTES instead of a ring per "
-                         "worker (profiles/r4_bigring, r4_connring); off: a ring per worker")
-    ap.add_argument("--conn-ring-inplace", default="off", choices=["on", "off"],
-                    help="connection ring on gRPC pool 1: the reader recv()s straight into the ring, a slot's worth "
-                         "per recv() across frame boundaries, and the sinks take payload in place (off: a window "
-                         "per DATA-frame payload)")
-    ap.add_argument("--crc-slice8", default="on", choices=["on", "off"],
-                    help="slot CRC kernel stages slice-by-8 tables (8 KiB) instead of slice-by-16 "
-                         "(profiles/r4_crc8)")
-    ap.add_argument("--crc-slot-waves", type=int, default=0, choices=[0, 1, 2, 4, 8],
-                    help="slot CRC kernel waves per workgroup (0: by slot size); A/B of the kernel's table staging")
-    ap.add_argument("--async-submit", type=int, default=1, choices=[0, 1],
-                    help="slot hand-off (H2D copy + CRC launches) on a per-device submitter thread instead of the "
-                         "receiving thread: one stream per read is bound by its receiving core, so taking the HIP "
-                         "calls off it gave +15-35%% (profiles/r2_single_stream)")
-    ap.add_argument("--submit-cpus", default="aux", choices=["aux", "inherit"],
-                    help="aux: the per-device submitter thread gets a core of its own from the placement plan; "
-                         "inherit: it keeps the first posting transport thread's CPU set")
-    ap.add_argument("--rcvbuf", default="64MiB",
-                    help="client SO_RCVBUF of the headline read (0 = kernel autotuning). An explicit 64 MiB request "
-                         "(capped at net.core.rmem_max = 32 MiB on the GPU boxes, doubled by the kernel) won 5 of 8 "
-                         "interleaved pairs against autotuning, medians 16.8k/14.0k vs 13.3k/13.4k MiB/s over two "
-                         "boxes (profiles/r2_rcvbuf); the box's limits are reported in the JSON line")
     ap.add_argument("--grpc-pool", type=int, default=1)
     ap.add_argument("--slices", type=int, default=1,
                     help="streams per object read in the HEADLINE run (1 = the reference's sequential read)")
     ap.add_argument("--sliced-streams", type=int, default=8,
                     help="streams per read in the `sliced` extension block (0 = skip the block)")
-    ap.add_argument("--sliced-slot-bytes", default="2MiB",
-                    help="sliced block: ring slot per sink (2 MiB x 8 won 2 of 2 interleaved reps against 4 x 4 MiB, "
-                         "8 MiB x 2, 4/16 pool streams and async hand-off: profiles/r2_sliced)")
-    ap.add_argument("--sliced-slots", type=int, default=2,
-                    help="sliced block: ring slots per sink. With the THP endpoint the receive copies are the "
-                         "bound and each stream's 2 sinks x ring is its destination footprint: 2 x 2 MiB ran "
-                         "46.3-49.9k MiB/s against 41.5-45.0k with 8 x 2 MiB (profiles/r3_ring_thp/sliced)")
-    ap.add_argument("--sliced-async-submit", type=int, default=0, choices=[0, 1],
-                    help="sliced block: slot hand-off on the device submitter thread (default inline)")
-    ap.add_argument("--piece-bytes", default="8MiB",
-                    help="sliced reads: streams pull pieces of this size from a shared cursor (0 = fixed shares)")
-    ap.add_argument("--piece-min-bytes", default="0",
-                    help="sliced reads: taper the piece size toward the end of the object down to this")
     ap.add_argument("--affinity", default="auto",
                     help="CPU placement of client/endpoint threads: auto|pair|share|same|split|numa|none "
                          "(parallel/affinity.py). auto: pair for one stream per read (won 3 of 3 interleaved "
                          "reps, profiles/r2_placement), share for sliced reads; the sliced block always runs "
                          "on its own share-placed endpoint")
-    ap.add_argument("--event-wait", default="block", choices=["spin", "block"],
-                    help="how GPU sinks wait on slot events: block (interrupt) or spin")
     ap.add_argument("--side-steps", type=int, default=-1,
                     help="timed reads/uploads per side block (compare / sliced / write); -1: = --steps, 0: skip all")
     ap.add_argument("--fanout", default="on", choices=["on", "off"],
@@ -145,12 +102,6 @@ def build_parser() -> argparse.ArgumentParser:
                     help="config 3 side block: pinned ring per reader, SLOTSxSLOT_BYTES (1 MiB objects). 2 x 1 MiB "
                          "keeps the 8 readers' receive destinations at 16 MiB: gRPC 18.6-18.8k MiB/s at p50 "
                          "0.42 ms against 15.5-17.0k at 0.46-0.49 with 8 x 2 MiB (profiles/r3_mux_thp/listring)")
-    ap.add_argument("--list-placement", default="same", choices=["same", "split", "share"],
-                    help="list_read_*: one L3 domain for the readers and the endpoint (same), two (split), or the "
-                         "rank's whole share of the node's L3 domains (share)")
-    ap.add_argument("--list-ring-wc", default="on", choices=["on", "off"],
-                    help="config 3 side block: the readers' rings in write-combined pinned memory (p50 0.346-0.379 "
-                         "ms against 0.412-0.519 with cached THP rings, profiles/r3_ring_thp/wc)")
     ap.add_argument("--write-size", default="64MiB", help="config 5 object size")
     ap.add_argument("--write-chunk", default="16MiB", help="resumable upload chunk (HTTP) / message batch")
     ap.add_argument("--baseline", default="on", choices=["on", "off"],
@@ -163,22 +114,11 @@ def build_parser() -> argparse.ArgumentParser:
                          "host drifting between blocks cancels (the same baseline swung 12%% between two benches on "
                          "one box, profiles/r4_main9).  auto: on at N = 1; off at N > 1, where nothing may run "
                          "before the headline")
-    ap.add_argument("--ceiling", default="on", choices=["on", "off"],
-                    help="ceiling side block: one loopback TCP stream (sendfile -> recv into a THP ring, no GPU, "
-                         "no framing) and pinned -> HBM copies, in the headline's placement")
     ap.add_argument("--ref-workers", type=int, default=48,
                     help="ref_default_* side blocks: the reference's default experiment, -worker 48 on 1 MiB "
                          "objects, gRPC pool 1 vs HTTP keep-alive, discard sink + host CRC (0 = off)")
     ap.add_argument("--ref-reads", type=int, default=50, help="ref_default_*: timed reads per worker")
-    ap.add_argument("--ref-grpc-placement", default="same", choices=["share_quota", "same", "share", "pair"],
-                    help="ref_default_grpc: CPU placement of the 48 workers, the endpoint and the one connection's "
-                         "reader. One L3 domain (same): 16.0-19.5k MiB/s at p50 2.1-2.4 ms against 8.4-8.8k at "
-                         "4.5-5.0 ms spread over the quota's cores (profiles/r3_mux_thp/refplace). HTTP keeps "
-                         "share_quota: its 48 receiving workers need the cores")
     ap.add_argument("--ref-object-size", default="1MiB", help="ref_default_*: object size")
-    ap.add_argument("--ref-http-placement", default="share_quota", choices=["share_quota", "split_quota"],
-                    help="ref_default_http*: client workers and endpoint handlers over the rank's quota cores "
-                         "together (share_quota) or on separate cores, a quarter for the endpoint (split_quota)")
     ap.add_argument("--ref100-reads", type=int, default=3,
                     help="ref_default_100m_* blocks: the reference's real operating point, 48 workers x 100 MiB "
                          "objects (princer_100M_files), HTTP vs gRPC pool 1, discard + host CRC vs HBM + GPU CRC; "
@@ -186,45 +126,10 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--ref100-object-size", default="100MiB",
                     help="ref_default_100m_* / ref_effective_grpc object size (the reference's princer_100M_files; "
                          "smaller only for CPU rehearsals)")
-    ap.add_argument("--ref-gpu-ring", default="2x2MiB",
-                    help="ref_default_100m_*_gpu: pinned ring per worker, SLOTSxSLOT_BYTES")
-    ap.add_argument("--write-placement", default="pair", choices=["share", "pair"],
-                    help="config-5 upload block: pair (uploader on one quiet core, endpoint receive + CRC on two "
-                         "more of the same L3 domain; 18.0-21.6k MiB/s in 6 runs) or share (uploader and endpoint "
-                         "threads over the rank's share of L3 domains; 7.7-19.7k, profiles/r3_write/placement)")
-    ap.add_argument("--list-rcvbuf", default="64MiB",
-                    help="config-3 list-read blocks: client SO_RCVBUF (0 = kernel autotuning; 64 MiB as the headline, "
-                         "profiles/r3_w48_tail)")
-    ap.add_argument("--ref-grpc-rcvbuf", default="0",
-                    help="ref_default_grpc / ref_default_100m_grpc_* / ref_effective_grpc: the one connection's "
-                         "SO_RCVBUF (0 = kernel autotuning)")
-    ap.add_argument("--write-split", default="off", choices=["on", "off"],
-                    help="write block (pair placement): the endpoint's receiving thread and its CRC worker each "
-                         "pinned to a core of their own (on) or floating over both (off)")
-    ap.add_argument("--fill-bytes", default="16KiB",
-                    help="most bytes one fill of a reader's 16 KiB small-read buffer takes from the socket "
-                         "(SocketOptions::fill_bytes): what a frame-header fill takes of the payload behind it "
-                         "is copied twice")
-    ap.add_argument("--mux-send", default="isolate", choices=["shared", "isolate"],
-                    help="multiplexed gRPC blocks: the endpoint's send thread on a physical core of its own "
-                         "(isolate; ServerConfig::send_cpus) or on the shared set. With --mux-reader isolate: "
-                         "ref_default_grpc 21.1k -> 24.2k MiB/s, list_read_grpc 21.6k -> 22.6k, h2 reader "
-                         "0.046 -> 0.039 CPU-s/GiB, medians of 5 interleaved pairs (profiles/r5_muxiso)")
-    ap.add_argument("--mux-reader", default="isolate", choices=["shared", "isolate"],
-                    help="multiplexed blocks (list_read_grpc, ref_default_grpc): isolate gives the connection's "
-                         "reader thread a physical core the workers and endpoint do not use (affinity.isolate_reader); "
-                         "alone it did not help (profiles/r4_muxiso), with --mux-send isolate it does (r5_muxiso)")
     ap.add_argument("--blocks", default="",
                     help="comma list of side blocks to run (A/B sessions): cpu_baseline, compare, sliced, ceiling, "
                          "ref_default, c1_http_cpu, list_read, write, write_composite, fanout; 'all' = every block; empty = "
                          "all at N = 1, cpu_baseline,compare,write,fanout at N > 1")
-    ap.add_argument("--client-cc", default="cubic",
-                    help="client sockets' TCP congestion control, set before connect (\"\" = the host default, BBR "
-                         "on the GPU boxes, whose internal pacing arms an hrtimer per 64 KiB skb of an upload on a "
-                         "loopback link: profiles/r4_recvcost). Every block uses it, baselines included")
-    ap.add_argument("--recv-refill", type=int, default=0, choices=[0, 1],
-                    help="client sockets: a payload recv() also reads what follows it (the next HTTP/2 frame "
-                         "header) in the same recvmsg (SocketOptions::recv_refill)")
     ap.add_argument("--read-diag", action="store_true",
                     help="per-read stall attribution (Runner read_diag): scheduler and softirq deltas of the "
                          "receiving / sending threads around every timed read; the slowest reads carry them and a "

@@ -103,12 +103,9 @@ Runner::Runner(RunnerConfig cfg) : cfg_(std::move(cfg)) {
   // HTTP/2 media GETs (always one connection)
   const bool one_conn = (cfg_.client.protocol == "grpc" && cfg_.client.grpc_conn_pool_size == 1) ||
                         cfg_.client.protocol == "http2";
-  const bool arena = cfg_.conn_ring_inplace && cfg_.client.protocol == "grpc";
-  if (cfg_.conn_ring && cfg_.sink == "gpu" && one_conn && (cfg_.workers > 1 || (cfg_.conn_ring_single && arena)) &&
-      cfg_.slices <= 1 && g.verify && g.landing == Landing::kObject && g.stage == GpuSinkConfig::Stage::kH2D) {
-    conn_ring_ = std::make_unique<ConnRing>(g.device, cfg_.conn_ring_slot_bytes, cfg_.conn_ring_slots, arena);
-    if (arena) cfg_.client.recv_arena = conn_ring_.get();
-  }
+  if (cfg_.conn_ring && cfg_.sink == "gpu" && one_conn && cfg_.workers > 1 && cfg_.slices <= 1 && g.verify &&
+      g.landing == Landing::kObject && g.stage == GpuSinkConfig::Stage::kH2D)
+    conn_ring_ = std::make_unique<ConnRing>(g.device, cfg_.conn_ring_slot_bytes, cfg_.conn_ring_slots);
   client_ = make_client(cfg_.client);
 }
 

@@ -82,16 +82,6 @@ struct RunnerConfig {
   // 16.8k / 18.0k with 8 x 1 MiB, 15.4k / 14.1k with 16 x 1 MiB and 13.9k /
   // 15.5k with a ring per worker (profiles/r4_ringgeom).
   bool conn_ring = true;
-  // gRPC pool 1: the connection's reader recv()s straight into the ring
-  // (net/buffered.h RecvArena), as much as a slot holds per recv(), across
-  // frame and message boundaries; payload is taken where it lies.  false:
-  // each sink acquires a window per DATA-frame payload.  Off by default:
-  // 510-560 instead of 320-355 KiB per recv() on list_read_grpc, the same
-  // rate and reader CPU (3 interleaved pairs, profiles/r5_arena).
-  bool conn_ring_inplace = false;
-  // the connection ring (arena) for a ONE-worker gRPC read too, instead of
-  // the sink's own ring (measured: no faster, profiles/r5_arena)
-  bool conn_ring_single = false;
   size_t conn_ring_slot_bytes = size_t(1) << 20;
   int conn_ring_slots = 4;
   // CPUs the read_diag sampler must not run on (the placement's; the client

@@ -42,21 +42,16 @@ uint32_t* crc_scratch_alloc(uint64_t tiles);
 // Kernel variant selection for launch_crc32c_batch, process-wide.  The
 // defaults are the measured winners; the others stay reachable for kernel
 // A/Bs and their tests (scripts/crc_kernel_bench.py, tests/test_gpu_crc32c.py):
-//   slot_kernel   slot-sized batches (<= kCrcFusedMaxTiles 4 KiB tiles) on
-//                 crc32c_slot_kernel; false = the round-2 fused tile kernel
 //   slot_waves    waves per slot-kernel workgroup (1, 2, 4, 8; 0 = by size)
 //   xor_arrival   slot kernel: 64-bit XOR arrival words per counter group
 //                 (false = per-tile stores + done counters for every batch)
-//   nibble_tables slot kernel: 16-entry nibble tables (fewer LDS bank
-//                 conflicts, more lookups); false = byte tables
-//   mfma          bulk 4 KiB-tile batches on the int8-MFMA tile kernel
-//                 (correct, slower than the table kernel: profiles/r2_crc_mfma)
+// Measured and dropped (round 5, removed in round 6; git history and
+// profiles/ keep them): an int8-MFMA tile kernel (2.9 TB/s against the table
+// kernels' 3.9, profiles/r2_crc_mfma, r5_kernels), bank-replicated nibble
+// tables (3.2 TB/s), the round-2 fused tile kernel for slot batches.
 struct CrcLaunchOptions {
-  bool slot_kernel = true;
   int slot_waves = 0;
   bool xor_arrival = true;
-  bool nibble_tables = false;
-  bool mfma = false;
   // slot kernel: stage slice-by-8 tables (8 KiB, T0..T7) instead of
   // slice-by-16 (16 KiB): the L2-cold stage in the read pipeline.  8.58-8.62
   // against 8.78-8.79 us per 1 MiB slot, min 6.5 against 7.0-7.3

@@ -88,18 +88,6 @@ __device__ __forceinline__ uint32_t update16_s8(const uint32_t* __restrict__ sl,
   return c;
 }
 
-// The same 16-byte update from the bank-replicated nibble tables (CrcTables::nib):
-// nb = nib + (lane & 31); table t of nibble n at nb[t * 512 + n * 32].
-__device__ __forceinline__ uint32_t update16_nib(const uint32_t* __restrict__ nb, uint32_t state, uint4 v) {
-  const uint32_t w[4] = {state ^ v.x, v.y, v.z, v.w};
-  uint32_t c = 0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int k = 0; k < 8; ++k) c ^= nb[(q * 8 + k) * 512 + ((w[q] >> (4 * k)) & 15u) * 32];
-  return c;
-}
-
 __device__ __forceinline__ uint32_t mask_low_bytes(uint32_t w, int keep_from) {
   // zero bytes [0, keep_from) of a little-endian word (keep_from in 0..4)
   if (keep_from <= 0) return w;
@@ -143,7 +131,7 @@ __device__ __forceinline__ void load_tile(const CrcBatch& b, uint32_t s, uint32_
 }
 
 // The lane's CRC register over its chunks of the tile.
-template <int R, bool kNib = false, bool kS8 = false>
+template <int R, bool kS8 = false>
 __device__ __forceinline__ uint32_t lane_chain(const uint4 (&v)[R * kCrcChunkPieces], const uint32_t* sl,
                                                const uint32_t* lane_shift, int lane) {
   uint32_t state = 0;
@@ -152,9 +140,7 @@ __device__ __forceinline__ uint32_t lane_chain(const uint4 (&v)[R * kCrcChunkPie
     if (k) state = shift4(lane_shift + 6 * 1024, state);  // over the 4032-byte gap to this lane's next chunk
 #pragma unroll
     for (int j = 0; j < kCrcChunkPieces; ++j) {
-      if constexpr (kNib)
-        state = update16_nib(sl + (lane & 31), state, v[k * kCrcChunkPieces + j]);
-      else if constexpr (kS8)
+      if constexpr (kS8)
         state = update16_s8(sl, state, v[k * kCrcChunkPieces + j]);
       else
         state = update16(sl, state, v[k * kCrcChunkPieces + j]);
@@ -167,7 +153,7 @@ __device__ __forceinline__ uint32_t lane_chain(const uint4 (&v)[R * kCrcChunkPie
 // start read as zeros (free for a raw CRC); the piece straddling it is masked.
 // Tiles are right-aligned to the segment end, so only the first tile of a
 // segment has such a head.
-template <int R, bool kNib = false>
+template <int R>
 __device__ __forceinline__ uint32_t lane_state(const CrcBatch& b, uint32_t s, uint32_t gt, const uint32_t* sl,
                                                const uint32_t* lane_shift, int lane) {
   uint4 v[R * kCrcChunkPieces];
@@ -175,7 +161,7 @@ __device__ __forceinline__ uint32_t lane_state(const CrcBatch& b, uint32_t s, ui
   // keep all the tile's loads in flight before the first lookup (the
   // scheduler otherwise sinks them into the lookup chain)
   __builtin_amdgcn_sched_barrier(0);
-  return lane_chain<R, kNib>(v, sl, lane_shift, lane);
+  return lane_chain<R>(v, sl, lane_shift, lane);
 }
 
 // wave tree: lane l's last chunk ends 64 (63 - l) bytes before the tile end
@@ -232,7 +218,6 @@ __device__ __forceinline__ uint32_t tail_byte(const CrcSeg& sg, int lane, int* r
 }
 
 // ... folded into `raw` (slice-by-r, one independent lookup per lane)
-template <bool kNib>
 __device__ __forceinline__ uint32_t fold_tail(uint32_t byte, int r, uint32_t raw, const uint32_t* tab, int lane) {
   if (r == 0) return raw;
   uint32_t x = 0;
@@ -240,13 +225,7 @@ __device__ __forceinline__ uint32_t fold_tail(uint32_t byte, int r, uint32_t raw
     const uint32_t sb = lane < 4 ? (raw >> (8 * lane)) & 0xff : 0u;
     const uint32_t bv = (byte ^ sb) & 0xff;
     const int m = r - 1 - lane;  // slice16 table index
-    if constexpr (kNib) {
-      const uint32_t* nb = tab + (lane & 31);
-      const int t = 2 * (15 - m);
-      x = nb[t * 512 + (bv & 15u) * 32] ^ nb[(t + 1) * 512 + (bv >> 4) * 32];
-    } else {
-      x = tab[m * 256 + bv];
-    }
+    x = tab[m * 256 + bv];
   }
 #pragma unroll
   for (int o = 8; o > 0; o >>= 1) x ^= __shfl_xor(x, o, 64);
@@ -402,10 +381,16 @@ __global__ __launch_bounds__(kBpThreads) void crc32c_tiles_bp_kernel(const CrcBa
   constexpr int kShWords = 6 * 1024 + (R > 1 ? 1024 : 0);
   __shared__ __attribute__((aligned(16))) uint32_t s_bp[kBpWords];
   __shared__ __attribute__((aligned(16))) uint32_t s_sh[kShWords];
+  // latency probes of the kernel bench (CrcBatch::probe), as the other tile
+  // kernels: 2 = exit at entry, 1 = after the table staging; 4 (after the
+  // tiles) is where this kernel ends anyway
+  const uint32_t probe = b.probe & 0xffu;
+  if (probe == 2) return;
   // word i = T_(i / (256 kRep))[(i / kRep) & 255], bank i % kRep
   for (int i = threadIdx.x; i < kBpWords; i += blockDim.x) s_bp[i] = tabs->slice16[i / (256 * kRep)][(i / kRep) & 255];
   stage(s_sh, &tabs->lane_shift[0][0][0], kShWords);
   __syncthreads();
+  if (probe == 1) return;
   const uint32_t* sh = s_sh;
   const int lane = threadIdx.x & 63;
   const uint32_t* bp = s_bp + (lane & (kRep - 1));
@@ -465,11 +450,11 @@ __device__ __forceinline__ uint32_t xor_over_lanes(uint32_t x, int width) {
 // lane, a 6-level lookup chain), 1.0 us on the done counter, 2.5 us in the
 // last workgroup's Horner + tree fold.  W (waves per workgroup) is picked so
 // the grid puts a tile on every CU.
-template <int W, bool kNib, bool kS8 = false>
+template <int W, bool kS8 = false>
 __global__ __launch_bounds__(64 * W) void crc32c_slot_kernel(const CrcBatch b, const CrcTables* __restrict__ tabs,
                                                             uint32_t* __restrict__ scratch,
                                                             CrcSegResult* __restrict__ out) {
-  constexpr int kTabWords = kNib ? 32 * 16 * 32 : kS8 ? 8 * 256 : kSliceWords;
+  constexpr int kTabWords = kS8 ? 8 * 256 : kSliceWords;
   // the tail fold looks up T0..T15: from L2 when only T0..T7 were staged
   const uint32_t* tail_tab = kS8 ? &tabs->slice16[0][0] : nullptr;
   __shared__ __attribute__((aligned(16))) uint32_t s_sl[kTabWords];
@@ -503,10 +488,7 @@ __global__ __launch_bounds__(64 * W) void crc32c_slot_kernel(const CrcBatch b, c
       kl[4 * j + 3] = q.w;
     }
   }
-  if constexpr (kNib)
-    stage(s_sl, &tabs->nib[0][0][0], kTabWords);
-  else
-    stage(s_sl, &tabs->slice16[0][0], kTabWords);
+  stage(s_sl, &tabs->slice16[0][0], kTabWords);
   __syncthreads();
   if (probe == 1) return;
   uint32_t* tiles = scratch + kCrcScratchHeader;
@@ -528,7 +510,7 @@ __global__ __launch_bounds__(64 * W) void crc32c_slot_kernel(const CrcBatch b, c
       load_tile<1>(b, s, gt, lane, v);
       __builtin_amdgcn_sched_barrier(0);
     }
-    const uint32_t state = lane_chain<1, kNib, kS8>(v, s_sl, nullptr, lane);
+    const uint32_t state = lane_chain<1, kS8>(v, s_sl, nullptr, lane);
     uint32_t c = 0;
 #pragma unroll
     for (int i = 0; i < 32; ++i) c ^= kl[i] & (0u - ((state >> i) & 1u));
@@ -579,7 +561,7 @@ __global__ __launch_bounds__(64 * W) void crc32c_slot_kernel(const CrcBatch b, c
     }
     __syncthreads();
     if (!s_last || probe == 3 || wave != 0) return;
-    const uint32_t raw = fold_tail<kNib>(tail_b, tail_r, s_raw, kS8 ? tail_tab : s_sl, lane);
+    const uint32_t raw = fold_tail(tail_b, tail_r, s_raw, kS8 ? tail_tab : s_sl, lane);
     if (lane == 0) store_result(out + 0, seg_result(b.seg[0], raw));
     return;
   }
@@ -623,143 +605,8 @@ __global__ __launch_bounds__(64 * W) void crc32c_slot_kernel(const CrcBatch b, c
 #pragma unroll
     for (int k = 0; k < static_cast<int>(kCrcFusedMaxTiles / 64); ++k) acc ^= v[k];
     uint32_t raw = xor_over_lanes(acc, 64);
-    raw = fold_tail<kNib>(tb, r, raw, kS8 ? tail_tab : s_sl, lane);
+    raw = fold_tail(tb, r, raw, kS8 ? tail_tab : s_sl, lane);
     if (lane == 0) store_result(out + g, seg_result(sg, raw));
-  }
-}
-
-// --- int8-MFMA tile CRC ---------------------------------------------------------
-// 4 KiB tiles as for tile_crc<1>, one wave per tile, but the GF(2) algebra runs
-// on the matrix cores instead of LDS lookups (CrcTables::mfma, crc_types.h):
-// lane l reads 16 bytes of interleaved chunk l & 31 per piece (each load
-// instruction covers 1 KiB contiguous), and for each of the
-// 8 bit planes feeds them shifted right by k as the B operand of one
-// v_mfma_i32_32x32x32_i8 against a constant 0/1 A fragment held in VGPRs
-// (32 fragments, 128 VGPRs, loaded once per wave).  The low bit of each int32
-// accumulator is one bit of one chunk's raw CRC; 16 per-lane shift columns and
-// an XOR over the lanes give the tile's raw CRC.  No LDS at all.  The next
-// tile's loads are issued before the current tile's MFMAs.
-typedef int gcsb_v4i __attribute__((ext_vector_type(4)));
-typedef int gcsb_v16i __attribute__((ext_vector_type(16)));
-
-// The lane's 4 x 16 bytes of tile gt (global_load_dwordx4 through an
-// address-space-1 pointer: flat loads would also count against lgkmcnt).  The
-// head mask (bytes before the segment start, first tile only) is returned in
-// *zb (5 bits per piece: leading bytes to zero, 16 = the whole piece) and
-// applied by the consumer, so a prefetch never waits for its own data.
-__device__ __forceinline__ void load_mfma_tile(const CrcBatch& b, uint32_t s, uint32_t gt, int lane, uint4 (&x)[4],
-                                               uint32_t* zb) {
-  typedef unsigned int u4v __attribute__((ext_vector_type(4)));
-  typedef const u4v __attribute__((address_space(1)))* gptr;
-  const uintptr_t addr = reinterpret_cast<uintptr_t>(b.seg[s].addr);
-  const uint32_t len = b.seg[s].len;
-  const uint32_t t = gt - b.seg[s].tile_base;
-  const uintptr_t a16 = addr & ~uintptr_t(15);
-  const uint64_t full = (addr + len - a16 + 15) / 16 - 1;
-  const intptr_t vend = static_cast<intptr_t>(a16 + 16 * full);
-  const intptr_t tstart = vend - static_cast<intptr_t>(kCrcRoundBytes) * static_cast<intptr_t>(b.seg[s].ntiles - t);
-  uint32_t z = 0;
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const intptr_t q = tstart + 16 * (lane & 31) + 1024 * p + 512 * (lane >> 5);
-    const intptr_t lead = static_cast<intptr_t>(addr) - q;  // bytes of this piece before the segment
-    x[p] = make_uint4(0, 0, 0, 0);
-    if (lead < 16) {
-      const u4v v = *reinterpret_cast<gptr>(q);
-      x[p] = make_uint4(v.x, v.y, v.z, v.w);
-    }
-    const uint32_t zp = lead <= 0 ? 0u : (lead >= 16 ? 16u : static_cast<uint32_t>(lead));
-    z |= zp << (5 * p);
-  }
-  *zb = z;
-}
-
-__device__ __forceinline__ uint4 apply_head_mask(uint4 v, uint32_t zp) {
-  if (zp == 0) return v;
-  const int h = static_cast<int>(zp);
-  v.x = mask_low_bytes(v.x, h);
-  v.y = mask_low_bytes(v.y, h - 4);
-  v.z = mask_low_bytes(v.z, h - 8);
-  v.w = mask_low_bytes(v.w, h - 12);
-  return v;
-}
-
-// One tile through the 32 MFMAs; returns its raw CRC (every lane).
-__device__ __forceinline__ uint32_t mfma_tile_crc(const uint4 (&xr)[4], uint32_t zb, const gcsb_v4i* __restrict__ a,
-                                                  const uint32_t (&kc)[16]) {
-  // the A fragments are loop-invariant LDS data: without this the compiler
-  // hoists all 32 reads out of the tile loop into 128 VGPRs again
-  __asm__ __volatile__("" ::: "memory");
-  gcsb_v16i acc = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    // at most one piece's 8 A fragments live at a time
-    if (p) __asm__ __volatile__("" ::: "memory");
-    const uint4 xp = apply_head_mask(xr[p], (zb >> (5 * p)) & 31u);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const gcsb_v4i bv = {static_cast<int>(xp.x >> k), static_cast<int>(xp.y >> k),
-                           static_cast<int>(xp.z >> k), static_cast<int>(xp.w >> k)};
-      acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[(8 * p + k) * 64], bv, acc, 0, 0, 0);
-    }
-  }
-  uint32_t c = 0;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) c ^= kc[r] & (0u - (static_cast<uint32_t>(acc[r]) & 1u));
-  return xor_over_lanes(c, 64);
-}
-
-__global__ __launch_bounds__(256) void crc32c_mfma_tiles_kernel(const CrcBatch b, const CrcTables* __restrict__ tabs,
-                                                                uint32_t* __restrict__ scratch) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
-  const uint32_t g0 = blockIdx.x * (blockDim.x >> 6) + wave;
-  const uint32_t T = b.total_tiles;
-  // three tile buffers in rotation, indexed statically (the loop is unrolled
-  // by 3): two tiles' loads stay in flight while one runs through the MFMAs.
-  // Rotating one buffer array by register moves made the compiler wait for
-  // every outstanding load at the top of each tile.
-  uint4 x0[4], x1[4], x2[4];
-  uint32_t s = 0, z0 = 0, z1 = 0, z2 = 0;
-  auto fetch = [&](uint32_t g, uint4 (&x)[4], uint32_t& z) {
-    while (s + 1 < b.nseg && b.seg[s + 1].tile_base <= g) ++s;
-    load_mfma_tile(b, s, g, lane, x, &z);
-  };
-  if (g0 < T) fetch(g0, x0, z0);
-  if (g0 + nw < T) fetch(g0 + nw, x1, z1);
-  // the 32 A fragments (32 KiB) in LDS, one ds_read_b128 per lane per MFMA
-  // (contiguous across lanes: conflict-free); in VGPRs they held occupancy at
-  // 2 waves per SIMD and the memory waits at 36 % of wave cycles
-  __shared__ __attribute__((aligned(16))) gcsb_v4i s_a[32 * 64];
-  {
-    const gcsb_v4i* src = reinterpret_cast<const gcsb_v4i*>(&tabs->mfma.a[0][0][0]);
-    for (int i = threadIdx.x; i < 32 * 64; i += blockDim.x) s_a[i] = src[i];
-  }
-  __syncthreads();
-  const gcsb_v4i* a = s_a + lane;
-  uint32_t kc[16];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) kc[r] = tabs->mfma.kc[lane][r];
-  uint32_t* tiles = scratch + kCrcScratchHeader;
-  for (uint32_t g = g0; g < T; g += 3 * nw) {
-    if (g + 2 * nw < T) fetch(g + 2 * nw, x2, z2);
-    {
-      const uint32_t c = mfma_tile_crc(x0, z0, a, kc);
-      if (lane == 0) tiles[g] = c;
-    }
-    if (g + nw >= T) break;
-    if (g + 3 * nw < T) fetch(g + 3 * nw, x0, z0);
-    {
-      const uint32_t c = mfma_tile_crc(x1, z1, a, kc);
-      if (lane == 0) tiles[g + nw] = c;
-    }
-    if (g + 2 * nw >= T) break;
-    if (g + 4 * nw < T) fetch(g + 4 * nw, x1, z1);
-    {
-      const uint32_t c = mfma_tile_crc(x2, z2, a, kc);
-      if (lane == 0) tiles[g + 2 * nw] = c;
-    }
   }
 }
 
@@ -911,7 +758,7 @@ void launch_crc32c_batch(const CrcBatch& b, const CrcTables* d_tables, uint32_t*
   const bool fused = b.max_seg_tiles <= kCrcFusedMaxTiles;
   const bool small = b.tile_log2 == static_cast<uint32_t>(kCrcMinTileLog2);
   const CrcLaunchOptions o = crc_launch_options();
-  if (fused && small && o.slot_kernel) {
+  if (fused && small) {
     // waves per workgroup: enough workgroups to put a tile on every CU first,
     // but two waves from 1 MiB up (each workgroup stages the 16 KiB tables,
     // L2-cold between slots: 1 MiB slots in the read pipeline averaged 9.23 /
@@ -928,21 +775,10 @@ void launch_crc32c_batch(const CrcBatch& b, const CrcTables* d_tables, uint32_t*
       bx.probe |= 0x100u;
     }
     if (g == 0) g = 1;
-    const bool nib = o.nibble_tables;
-#define GCSB_SLOT(WV, NB) \
-  hipLaunchKernelGGL((crc32c_slot_kernel<WV, NB>), dim3(g), dim3(64 * WV), 0, stream, no_xor ? bx : b, d_tables, \
+#define GCSB_SLOT(WV, S8) \
+  hipLaunchKernelGGL((crc32c_slot_kernel<WV, S8>), dim3(g), dim3(64 * WV), 0, stream, no_xor ? bx : b, d_tables, \
                      d_scratch, d_results)
-#define GCSB_SLOT8(WV) \
-  hipLaunchKernelGGL((crc32c_slot_kernel<WV, false, true>), dim3(g), dim3(64 * WV), 0, stream, no_xor ? bx : b, \
-                     d_tables, d_scratch, d_results)
-    if (!nib && o.slice8) {
-      switch (w) {
-        case 1: GCSB_SLOT8(1); break;
-        case 2: GCSB_SLOT8(2); break;
-        case 4: GCSB_SLOT8(4); break;
-        default: GCSB_SLOT8(8); break;
-      }
-    } else if (nib) {
+    if (o.slice8) {
       switch (w) {
         case 1: GCSB_SLOT(1, true); break;
         case 2: GCSB_SLOT(2, true); break;
@@ -958,26 +794,16 @@ void launch_crc32c_batch(const CrcBatch& b, const CrcTables* d_tables, uint32_t*
       }
     }
 #undef GCSB_SLOT
-#undef GCSB_SLOT8
     hip_check(hipGetLastError(), "crc32c_slot_kernel");
     return;
   }
-  if (fused) {
-    if (small)
-      hipLaunchKernelGGL((crc32c_tiles_kernel<1, true>), dim3(blocks), dim3(kThreads), 0, stream, b, d_tables,
-                         d_scratch, d_results);
-    else
-      hipLaunchKernelGGL((crc32c_tiles_kernel<4, true>), dim3(blocks), dim3(kThreads), 0, stream, b, d_tables,
-                         d_scratch, d_results);
+  if (fused) {  // 16 KiB tiles (batches over 4 MiB whose segments fold in one pass)
+    hipLaunchKernelGGL((crc32c_tiles_kernel<4, true>), dim3(blocks), dim3(kThreads), 0, stream, b, d_tables,
+                       d_scratch, d_results);
     hip_check(hipGetLastError(), "crc32c_tiles_kernel(fused)");
     return;
   }
-  const bool mfma = o.mfma;
-  if (small && mfma) {
-    uint32_t g = (b.total_tiles + 3) / 4;
-    if (g > 2048) g = 2048;
-    hipLaunchKernelGGL(crc32c_mfma_tiles_kernel, dim3(g), dim3(256), 0, stream, b, d_tables, d_scratch);
-  } else if (o.bank_private) {
+  if (o.bank_private) {
     // a persistent grid: one workgroup per CU (128 KiB of tables each)
     static std::atomic<int> cu_count[64];  // per device, 0 = not asked yet
     int dev = 0, cus = 256;

@@ -11,7 +11,6 @@ namespace gcsb {
 
 void build_crc_tables(CrcTables* t) {
   crc32c_build_slice16(t->slice16);
-  build_mfma_crc_tables(&t->mfma);
   for (int lv = 0; lv < 6; ++lv) crc32c_build_shift_table(static_cast<uint64_t>(kCrcChunkBytes) << lv, t->lane_shift[lv]);
   crc32c_build_shift_table(kCrcLaneGap, t->lane_shift[6]);
   for (int lv = 0; lv < kCrcTileShiftLevels; ++lv)
@@ -19,58 +18,11 @@ void build_crc_tables(CrcTables* t) {
   for (int l = 0; l < 64; ++l)
     for (int i = 0; i < 32; ++i)
       t->lane_k[l][i] = crc32c_shift(1u << i, static_cast<uint64_t>(kCrcChunkBytes) * (63 - l));
-  for (int j = 0; j < 16; ++j)
-    for (int h = 0; h < 2; ++h)
-      for (int n = 0; n < 16; ++n)
-        for (int r = 0; r < 32; ++r) t->nib[2 * j + h][n][r] = t->slice16[15 - j][n << (4 * h)];
   for (uint32_t d = 0; d < kCrcFusedMaxTiles; ++d) {
     // column i of shift by d tiles = shift of column i by one tile, d times
     for (int i = 0; i < 32; ++i)
       t->tile_k[d][i] = d == 0 ? (1u << i) : crc32c_shift(t->tile_k[d - 1][i], kCrcMinTile);
   }
-}
-
-void build_mfma_crc_tables(MfmaCrcTables* t) {
-  uint32_t slice[16][256];
-  crc32c_build_slice16(slice);
-  for (int p = 0; p < 4; ++p)
-    for (int k = 0; k < 8; ++k)
-      for (int lane = 0; lane < 64; ++lane)
-        for (int j = 0; j < 16; ++j) {
-          // lane (n, h) of MFMA piece p holds tile bytes 16 n + 1024 p + 512 h + j:
-          // the shift to the tile end splits into this n-independent part and
-          // 16 (31 - n) bytes applied by kc
-          const int pos = 1024 * p + 512 * (lane >> 5) + j;
-          const uint32_t e = crc32c_shift(slice[0][1u << k], static_cast<uint64_t>(4095 - 16 * 31 - pos));
-          t->a[8 * p + k][lane][j] = static_cast<int8_t>((e >> (lane & 31)) & 1u);
-        }
-  for (int lane = 0; lane < 64; ++lane)
-    for (int reg = 0; reg < 16; ++reg) {
-      const int row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
-      t->kc[lane][reg] = crc32c_shift(1u << row, static_cast<uint64_t>(16) * (31 - (lane & 31)));
-    }
-}
-
-uint32_t emulate_mfma_tile_crc(const uint8_t* tile, const MfmaCrcTables& t) {
-  // C[row][n] = sum_m sum_(h,j) A_m[row][(h,j)] * B_m[(h,j)][n], as the MFMA
-  // pairs fragment element j of lane half h of A and B
-  uint32_t out = 0;
-  for (int lane = 0; lane < 64; ++lane) {
-    const int n = lane & 31;
-    for (int reg = 0; reg < 16; ++reg) {
-      const int row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
-      int64_t acc = 0;
-      for (int p = 0; p < 4; ++p)
-        for (int k = 0; k < 8; ++k)
-          for (int h = 0; h < 2; ++h)
-            for (int j = 0; j < 16; ++j) {
-              const int8_t b = static_cast<int8_t>(tile[16 * n + 1024 * p + 512 * h + j] >> k);
-              acc += static_cast<int64_t>(t.a[8 * p + k][32 * h + row][j]) * b;
-            }
-      if (acc & 1) out ^= t.kc[lane][reg];
-    }
-  }
-  return out;
 }
 
 namespace {

@@ -73,23 +73,6 @@ struct CrcSegResult {
 // (GpuSink: slot reuse without a HIP call on the receiving thread).
 constexpr uint32_t kCrcStatusPending = 0xFFFFFFFFu;
 
-// Int8-MFMA tile CRC (crc32c_mfma_tiles_kernel): CRC over GF(2) is linear, so
-// the raw CRCs of 32 interleaved "chunks" of a 4 KiB tile (chunk n = the 16-byte
-// pieces at tile offsets 16 n + 512 q, q = 0..7) are one int8 GEMM
-// C[32 bits][32 chunks] = sum over 4 pieces x 8 bit planes of
-// A[p][k] (32 x 32, 0/1) . B (32 bytes x 32 chunks, data >> k), taken mod 2:
-// only the low bit of each B byte reaches the parity, so a bit plane is the
-// data shifted right by k, no unpacking.  One v_mfma_i32_32x32x32_i8 per
-// (piece, plane); each of the 4 loads of a tile reads 1 KiB contiguous.
-// a[m][lane][j]: lane `lane`'s A fragment of MFMA m = 8 p + k, bit (lane & 31)
-// of the shift to the tile end (less 16 (31 - n)) of bit k of tile byte
-// 1024 p + 512 (lane >> 5) + j.  kc[lane][reg]: the C element in accumulator
-// register reg of lane `lane` (chunk n = lane & 31, CRC bit
-// (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)) shifted by the remaining 16 (31 - n).
-struct MfmaCrcTables {
-  int8_t a[32][64][16];
-  uint32_t kc[64][16];
-};
 struct CrcTables {
   uint32_t slice16[16][256];
   uint32_t lane_shift[7][4][256];  // [0..5]: shift by kCrcChunkBytes * 2^lv (wave tree); [6]: kCrcLaneGap
@@ -102,13 +85,6 @@ struct CrcTables {
   //              16-byte boundary (d < kCrcFusedMaxTiles).
   uint32_t lane_k[64][32];
   uint32_t tile_k[kCrcFusedMaxTiles][32];
-  // slice-by-16 split into nibbles and replicated per LDS bank:
-  // nib[2j + h][n][r] = slice16[15 - j][n << 4h] for every replica r < 32,
-  // so lane l reads replica l & 31 and a ds_read_b32 never conflicts
-  // (banks = (addr / 4) mod 32 per 32-lane group).  Twice the lookups of the
-  // byte tables, none of their ~4-way conflicts.
-  uint32_t nib[32][16][32];
-  MfmaCrcTables mfma;
 };
 
 // Number of tiles (of 2^tile_log2 bytes) covering a segment's 16-byte pieces
@@ -124,11 +100,6 @@ inline void crc_segment_geometry(uintptr_t addr, uint32_t len, uint32_t tile_log
   const uint64_t per_tile = (uint64_t(1) << tile_log2) / 16;
   *ntiles = static_cast<uint32_t>((full + per_tile - 1) / per_tile);
 }
-
-void build_mfma_crc_tables(MfmaCrcTables* t);
-// Host model of the MFMA tile CRC (same tables and decomposition): raw CRC
-// of one 4 KiB tile.
-uint32_t emulate_mfma_tile_crc(const uint8_t* tile, const MfmaCrcTables& t);
 
 void build_crc_tables(CrcTables* t);
 // Fills seg.tile_base/ntiles/fixup, batch.total_tiles/max_seg_tiles and picks

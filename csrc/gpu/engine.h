@@ -140,8 +140,6 @@ class GpuSink : public Sink {
   void update_info(const ObjectInfo& info) override;
   Window acquire(size_t want) override;
   void commit(size_t n) override;
-  bool accepts_inplace() const override;
-  void commit_inplace(const uint8_t* p, size_t n) override;
   void chunk_begin(size_t len) override;
   void chunk_end(bool has_crc, uint32_t crc) override;
   void resume_at(int64_t offset) override;
@@ -270,18 +268,10 @@ class GpuSink : public Sink {
 // reader is not writing into (a slot may go in several parts) and collects
 // its segments' results as the kernel publishes them (no HIP call).  The
 // reader reuses a slot once every segment's result was collected.
-class ConnRing : public RecvArena {
+class ConnRing {
  public:
-  // arena: the connection's reader recv()s into the ring itself
-  // (net/buffered.h RecvArena) and the sinks take their payload in place
-  // (GpuSink::commit_inplace); otherwise each sink acquires windows.
-  ConnRing(int device, size_t slot_bytes, int slots, bool arena = false);
-  ~ConnRing() override;
-  bool arena() const { return arena_; }
-  std::pair<uint8_t*, size_t> recv_window() override;
-  void received(size_t n) override;
-  uint64_t arena_recvs() const { return arena_recvs_.load(std::memory_order_relaxed); }
-  uint64_t arena_bytes() const { return arena_bytes_.load(std::memory_order_relaxed); }
+  ConnRing(int device, size_t slot_bytes, int slots);
+  ~ConnRing();
   ConnRing(const ConnRing&) = delete;
   ConnRing& operator=(const ConnRing&) = delete;
   struct Stats {
@@ -331,13 +321,8 @@ class ConnRing : public RecvArena {
   // waiting sink (one at a time: 48 pollers on mu_ starved the reader)
   void hand_off_poller_locked();
 
-  std::atomic<uint64_t> arena_recvs_{0}, arena_bytes_{0};
   int device_;
-  bool arena_ = false;
-  // result entries per slot: kMaxSeg for window mode (a sink takes a new
-  // slot when they run out); in arena mode a slot holds whatever one recv()
-  // brought, every content run separated by >= 9 bytes of frame header, so
-  // slot_bytes / 9 + 2 entries can never run out
+  // result entries per slot (a sink takes a new slot when they run out)
   size_t res_cap_ = 0;
   bool poller_ = false;
   std::vector<GpuSink*> waiters_;

@@ -1118,10 +1118,10 @@ namespace {
 constexpr int64_t kRingWaitLimitNs = 60LL * 1000 * 1000 * 1000;
 }  // namespace
 
-ConnRing::ConnRing(int device, size_t slot_bytes, int slots, bool arena) : device_(device), arena_(arena) {
+ConnRing::ConnRing(int device, size_t slot_bytes, int slots) : device_(device) {
   slot_bytes_ = std::max<size_t>((slot_bytes + 4095) / 4096 * 4096, 65536);
   if (slots < 2) slots = 2;
-  res_cap_ = arena_ ? slot_bytes_ / 9 + 2 : static_cast<size_t>(kMaxSeg);
+  res_cap_ = static_cast<size_t>(kMaxSeg);
   ensure_device(device_);
   DeviceStreamPool& pool = DeviceStreamPool::get(device_);
   d_tables_ = device_crc_tables(device_);
@@ -1189,9 +1189,8 @@ void ConnRing::submit_locked(int slot, size_t upto) {
   };
   std::vector<Copy> copies;
   copies.reserve(upto - a);
-  // one CRC launch per kMaxSeg segments (an arena slot can hold more runs
-  // than one batch); the batches run in order on the slot's stream and
-  // share its tile scratch
+  // one CRC launch per kMaxSeg segments; the batches run in order on the
+  // slot's stream and share its tile scratch
   std::vector<CrcBatch> batches((upto - a + kMaxSeg - 1) / kMaxSeg);
   for (CrcBatch& b : batches) std::memset(&b, 0, sizeof(b));
   for (size_t i = a; i < upto; ++i) {
@@ -1277,24 +1276,6 @@ void ConnRing::collect_all_locked() {
   for (RSlot& r : slots_) collect_locked(r);
 }
 
-// Arena mode (net/buffered.h RecvArena): the reader's next recv() goes to
-// the rest of the current slot, or to the next slot once this one is full
-// (its segments go to the GPU then; take_slot_locked waits until the next
-// slot's previous contents were copied and checked).
-std::pair<uint8_t*, size_t> ConnRing::recv_window() {
-  std::unique_lock<std::mutex> lk(mu_);
-  RSlot* r = cur_ >= 0 ? &slots_[cur_] : nullptr;
-  if (!r || r->used == slot_bytes_) r = &take_slot_locked(lk);
-  return {r->host + r->used, slot_bytes_ - r->used};
-}
-
-void ConnRing::received(size_t n) {
-  std::lock_guard<std::mutex> lk(mu_);
-  slots_[cur_].used += n;
-  arena_recvs_.fetch_add(1, std::memory_order_relaxed);
-  arena_bytes_.fetch_add(n, std::memory_order_relaxed);
-}
-
 // Everything the reader is not receiving into goes to the GPU now.
 void ConnRing::flush_locked() {
   if (cur_ < 0) return;
@@ -1348,9 +1329,6 @@ bool GpuSink::ring_extends(const ConnRing& R) const {
 
 Window GpuSink::ring_acquire() {
   ConnRing& R = *cfg_.conn_ring;
-  // an arena's slots are filled by the connection's recv() alone: a window
-  // handed out here would overlap it
-  if (R.arena_) throw std::logic_error("GpuSink::acquire on an arena connection ring (use commit_inplace)");
   if (delivered_ >= obj_cap_)
     // size unknown so far (or larger than announced): grow, keeping landed bytes
     grow_object_buffer(std::max<uint64_t>(2 * obj_cap_, delivered_ + R.slot_bytes_));
@@ -1395,52 +1373,6 @@ void GpuSink::ring_commit(size_t n) {
   g.len += static_cast<uint32_t>(n);
   r.used += n;
   ring_res_[g.seq].len += static_cast<uint32_t>(n);
-  delivered_ += n;
-}
-
-bool GpuSink::accepts_inplace() const { return cfg_.conn_ring && cfg_.conn_ring->arena(); }
-
-// Arena mode: n payload bytes of this sink's object already lie at p in the
-// connection ring's current slot (the reader recv()'d them there): they
-// extend this sink's last segment when contiguous with it, else open one.
-void GpuSink::commit_inplace(const uint8_t* p, size_t n) {
-  if (n == 0) return;
-  ConnRing& R = *cfg_.conn_ring;
-  if (delivered_ + n > obj_cap_)
-    // size unknown so far (or larger than announced): grow, keeping landed bytes
-    grow_object_buffer(std::max<uint64_t>(2 * obj_cap_, delivered_ + n));
-  std::lock_guard<std::mutex> lk(R.mu_);
-  if (R.cur_ < 0) throw std::logic_error("GpuSink::commit_inplace before the arena's first window");
-  ConnRing::RSlot& r = R.slots_[R.cur_];
-  if (p < r.host || p + n > r.host + r.used)
-    throw std::logic_error("GpuSink::commit_inplace: bytes outside the arena's current slot");
-  const uint32_t off = static_cast<uint32_t>(p - r.host);
-  bool extend = ring_extends(R);
-  if (extend) {
-    const ConnRing::Seg& g = r.segs.back();
-    extend = g.owner == this && g.slot_off + g.len == off;
-  }
-  if (extend) {
-    ConnRing::Seg& g = r.segs.back();
-    g.len += static_cast<uint32_t>(n);
-    ring_res_[g.seq].len += static_cast<uint32_t>(n);
-  } else {
-    if (r.segs.size() >= R.res_cap_) throw std::logic_error("ConnRing: a slot's result entries ran out");
-    ConnRing::Seg g;
-    g.owner = this;
-    g.seq = ring_res_.size();
-    g.slot_off = off;
-    g.len = static_cast<uint32_t>(n);
-    g.dst = obj_dst_ + delivered_;
-    RingRes rr;
-    rr.obj_off = delivered_;
-    rr.len = static_cast<uint32_t>(n);
-    ring_res_.push_back(rr);
-    r.segs.push_back(g);
-    ring_open_slot_ = R.cur_;
-    ring_open_seg_ = r.segs.size() - 1;
-    ring_open_gen_ = r.gen;
-  }
   delivered_ += n;
 }
 

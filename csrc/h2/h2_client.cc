@@ -68,13 +68,6 @@ size_t H2DataCursor::read_some(void* dst, size_t n) {
   return m;
 }
 
-size_t H2DataCursor::take_inplace(size_t n, const uint8_t** p) {
-  n = std::min<size_t>(n, left_);
-  const size_t m = bc_->take_inplace(n, p);
-  left_ -= static_cast<uint32_t>(m);
-  return m;
-}
-
 void H2DataCursor::spill(const struct iovec* iov, int cnt, size_t i, size_t off, size_t n) {
   g_span_spills.fetch_add(1, std::memory_order_relaxed);
   std::vector<uint8_t> v;
@@ -89,7 +82,7 @@ void H2DataCursor::spill(const struct iovec* iov, int cnt, size_t i, size_t off,
 }
 
 size_t H2DataCursor::read_spanning(uint8_t* dst, size_t want) {
-  if (want <= left_ || !can_span_ || end_ || left_ == 0 || bc_->buffered() > 0 || bc_->inplace())
+  if (want <= left_ || !can_span_ || end_ || left_ == 0 || bc_->buffered() > 0)
     return read_some(dst, want);
   // the plan: [rest of this frame -> dst] then per frame [header -> hdr[j]]
   // [payload -> right after the previous payload in dst]
@@ -151,7 +144,7 @@ std::shared_ptr<H2ClientConn> H2ClientConn::dial(const Endpoint& ep, const H2Cli
   auto conn = Conn::dial(ep, opt.sock);
   if (conn->tls() && conn->alpn() != "h2")
     throw StorageError("TLS peer " + ep.host + " did not negotiate h2 (ALPN '" + conn->alpn() + "')", false);
-  c->bc_ = std::make_unique<BufferedConn>(std::move(conn), opt.recv_arena);
+  c->bc_ = std::make_unique<BufferedConn>(std::move(conn));
   c->w_ = std::make_unique<H2Writer>(c->bc_->conn());
   c->dec_ = HpackDecoder(opt.header_table_size);
   // connection preface + our SETTINGS + open the connection window wide

@@ -46,8 +46,6 @@ class H2DataCursor {
   uint8_t read_byte();
   void skip(size_t n);                           // n <= left()
   size_t read_some(void* dst, size_t n);         // 1..min(n, left()) bytes
-  bool inplace() const { return bc_->inplace(); }
-  size_t take_inplace(size_t n, const uint8_t** p);  // n <= left()
   // 1..want payload bytes of this stream into dst, contiguous; may consume
   // following DATA frames of the stream when want > left() (see above).
   size_t read_spanning(uint8_t* dst, size_t want);
@@ -155,8 +153,6 @@ struct H2ClientOptions {
   uint32_t span_max_frame = 256u << 10;
   uint32_t header_table_size = 4096;
   std::vector<int> cpus;  // pin the connection's reader thread
-  // receive into this arena (net/buffered.h): the GPU sink's connection ring
-  RecvArena* recv_arena = nullptr;
 };
 
 // Where the connection reader threads' time goes (process totals): waiting

@@ -10,7 +10,6 @@
 namespace gcsb {
 
 std::string BufferedConn::read_line(size_t max) {
-  if (arena_) throw std::logic_error("BufferedConn::read_line in arena mode (HTTP/1.1 never uses an arena)");
   std::string line;
   for (;;) {
     if (!buffered()) fill();
@@ -31,7 +30,7 @@ std::string BufferedConn::read_line(size_t max) {
 }
 
 size_t BufferedConn::recv_scatter(struct iovec* iov, int cnt) {
-  if (arena_ || buffered()) throw std::logic_error("BufferedConn::recv_scatter needs an empty, non-arena buffer");
+  if (buffered()) throw std::logic_error("BufferedConn::recv_scatter needs an empty buffer");
   pos_ = end_ = 0;
   if (conn_->tls()) {
     const size_t r = conn_->read_some(iov[0].iov_base, iov[0].iov_len);
@@ -52,7 +51,6 @@ size_t BufferedConn::recv_scatter(struct iovec* iov, int cnt) {
 }
 
 void BufferedConn::unread(const uint8_t* p, size_t n) {
-  if (arena_) throw std::logic_error("BufferedConn::unread in arena mode");
   if (n == 0) return;
   const size_t have = buffered();
   if (n + have > cap_) {

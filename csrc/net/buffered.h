@@ -2,7 +2,8 @@
 // headers, protobuf tags) are served from a 16 KiB buffer, large payload reads
 // bypass it and recv() straight into the caller's memory (the pinned ring slot
 // when the GPU sink is active), so object bytes are copied exactly once by the
-// kernel from socket buffers to their landing memory.
+// kernel from socket buffers to their landing memory.  An HTTP/2 spanning
+// receive (recv_scatter) lands many frames' payload in one recvmsg().
 #pragma once
 #include <cstdlib>
 #include <cstring>
@@ -17,57 +18,15 @@
 
 namespace gcsb {
 
-// Receive memory owned by someone else (the GPU sink's connection ring,
-// gpu/engine.h ConnRing): a BufferedConn in arena mode recv()s straight into
-// it, as much as the window holds, and parses protocol bytes in place;
-// payload is handed to the sink where it already lies (take_inplace), so one
-// recv() crosses frame and message boundaries and no byte goes through a
-// bounce buffer.  Only the connection's reader thread calls these.
-class RecvArena {
- public:
-  virtual ~RecvArena() = default;
-  // Writable memory for the next recv() (blocks until the arena has room).
-  // Called only when every byte of the previous windows was consumed.
-  virtual std::pair<uint8_t*, size_t> recv_window() = 0;
-  // n bytes were received at the start of the last window.
-  virtual void received(size_t n) = 0;
-};
-
 class BufferedConn {
  public:
-  explicit BufferedConn(std::unique_ptr<Conn> c, RecvArena* arena = nullptr)
-      : conn_(std::move(c)), buf_(arena ? nullptr : new uint8_t[kCap]), arena_(arena) {}
+  explicit BufferedConn(std::unique_ptr<Conn> c) : conn_(std::move(c)), buf_(new uint8_t[kCap]) {}
   Conn& conn() { return *conn_; }
   bool is_open() const { return conn_ && conn_->is_open(); }
   size_t buffered() const { return end_ - pos_; }
-  // arena mode: payload can be taken in place (take_inplace)
-  bool inplace() const { return arena_ != nullptr; }
-
-  // Up to n payload bytes where they lie in the arena (arena mode only): a
-  // recv() happens only when nothing is buffered, and it fills the whole
-  // window.  Returns the count (>= 1) and sets *p.
-  size_t take_inplace(size_t n, const uint8_t** p) {
-    if (!buffered()) afill();
-    const size_t b = buffered() < n ? buffered() : n;
-    *p = abuf_ + pos_;
-    pos_ += b;
-    return b;
-  }
 
   // Read exactly n bytes (n small or large).
   void read_exact(void* dst, size_t n) {
-    if (arena_) {
-      auto* d = static_cast<uint8_t*>(dst);
-      while (n) {
-        if (!buffered()) afill();
-        const size_t b = buffered() < n ? buffered() : n;
-        std::memcpy(d, abuf_ + pos_, b);
-        pos_ += b;
-        d += b;
-        n -= b;
-      }
-      return;
-    }
     auto* d = static_cast<uint8_t*>(dst);
     size_t b = buffered() < n ? buffered() : n;
     if (b) {
@@ -86,31 +45,12 @@ class BufferedConn {
     }
   }
   // Read 1..n bytes directly (large-payload path). Returns 0 only on EOF.
-  // SocketOptions::recv_refill: a large read also refills this buffer in the
-  // same recvmsg(), so whatever follows the payload (the next frame header)
-  // is parsed without a system call of its own.  Round 3 saw half the
-  // receive calls and no rate change under the pacing-timer noise
-  // (profiles/r3_refill); HTTP bodies pay a 16 KiB bounce per read.
   size_t read_some(void* dst, size_t n) {
-    if (arena_) {  // a sink that cannot take bytes in place: copy them out
-      if (!buffered()) afill();
-      const size_t b = buffered() < n ? buffered() : n;
-      std::memcpy(dst, abuf_ + pos_, b);
-      pos_ += b;
-      return b;
-    }
     if (buffered()) {
       size_t b = buffered() < n ? buffered() : n;
       std::memcpy(dst, buf_.get() + pos_, b);
       pos_ += b;
       return b;
-    }
-    if (n >= kRefillMin && conn_->recv_refill()) {
-      pos_ = end_ = 0;
-      const size_t r = conn_->read_some2(dst, n, buf_.get(), fill_cap());
-      if (r <= n) return r;
-      end_ = r - n;
-      return n;
     }
     return conn_->read_some(dst, n);
   }
@@ -133,10 +73,6 @@ class BufferedConn {
     }
   }
   uint8_t read_byte() {
-    if (arena_) {
-      if (!buffered()) afill();
-      return abuf_[pos_++];
-    }
     if (!buffered()) fill();
     return buf_[pos_++];
   }
@@ -145,7 +81,6 @@ class BufferedConn {
 
  private:
   static constexpr size_t kCap = 16384;
-  static constexpr size_t kRefillMin = 64u << 10;
   void fill() {
     if (pos_ == end_) pos_ = end_ = 0;
     if (end_ == cap_) {
@@ -162,21 +97,9 @@ class BufferedConn {
     const size_t f = conn_->fill_bytes();
     return f < 64 ? 64 : (f > kCap ? kCap : f);
   }
-  // arena mode: the next window, filled by one recv()
-  void afill() {
-    auto w = arena_->recv_window();
-    const size_t r = conn_->read_some(w.first, w.second);
-    if (r == 0) throw StorageError("unexpected EOF", true);
-    arena_->received(r);
-    abuf_ = w.first;
-    pos_ = 0;
-    end_ = r;
-  }
   std::unique_ptr<Conn> conn_;
   std::unique_ptr<uint8_t[]> buf_;
-  RecvArena* arena_ = nullptr;
-  uint8_t* abuf_ = nullptr;  // arena mode: start of the current window
-  size_t cap_ = kCap;        // buf_'s size (unread() may grow it)
+  size_t cap_ = kCap;  // buf_'s size (unread() may grow it)
   size_t pos_ = 0, end_ = 0;
 };
 

@@ -241,7 +241,6 @@ std::unique_ptr<Conn> Conn::dial(const Endpoint& ep, const SocketOptions& opt) {
   if (fd < 0) throw StorageError("connect " + ep.host + ":" + port + ": " + last_err, true);
   auto conn = std::make_unique<Conn>();
   conn->fd_ = fd;
-  conn->recv_refill_ = opt.recv_refill;
   conn->fill_bytes_ = opt.fill_bytes;
   if (ep.scheme == "https") {
     SSL* ssl = SSL_new(client_ssl_ctx(opt.tls_verify, opt.tls_ca_file));
@@ -257,8 +256,7 @@ std::unique_ptr<Conn> Conn::dial(const Endpoint& ep, const SocketOptions& opt) {
       std::string why = vr != X509_V_OK ? std::string(": certificate ") + X509_verify_cert_error_string(vr) : "";
       SSL_free(ssl);
       conn->fd_ = fd;  // closed by ~Conn
-      conn->recv_refill_ = opt.recv_refill;
-  conn->fill_bytes_ = opt.fill_bytes;
+      conn->fill_bytes_ = opt.fill_bytes;
       // a certificate failure will not fix itself: not retryable
       throw StorageError("TLS handshake with " + ep.host + " failed" + why, vr == X509_V_OK);
     }
@@ -327,7 +325,6 @@ std::unique_ptr<Conn> Conn::adopt(int fd, const SocketOptions& opt) {
   apply_socket_options(fd, opt);
   auto conn = std::make_unique<Conn>();
   conn->fd_ = fd;
-  conn->recv_refill_ = opt.recv_refill;
   conn->fill_bytes_ = opt.fill_bytes;
   return conn;
 }
@@ -398,44 +395,6 @@ size_t Conn::read_some(void* buf, size_t n) {
       r = ::recv(fd_, buf, n, 0);
       if (t0) g_diag_ns.fetch_add(static_cast<uint64_t>(now_ns() - t0), std::memory_order_relaxed);
     }
-    if (r >= 0) {
-      bytes_read_ += static_cast<uint64_t>(r);
-      g_recv_calls.fetch_add(1, std::memory_order_relaxed);
-      g_recv_bytes.fetch_add(static_cast<uint64_t>(r), std::memory_order_relaxed);
-      return static_cast<size_t>(r);
-    }
-    if (errno == EINTR) continue;
-    if (errno == EAGAIN || errno == EWOULDBLOCK) throw StorageError("read timeout", true);
-    throw StorageError(std::string("recv: ") + std::strerror(errno), true);
-  }
-}
-
-size_t Conn::read_some2(void* a, size_t na, void* b, size_t nb) {
-  if (ssl_ || nb == 0) return read_some(a, na);
-  if (fd_ < 0) throw StorageError("read on closed connection", true);
-  static const bool diag = [] {
-    const char* e = std::getenv("GCSB_RECV_DIAG");
-    return e && e[0] == '1';
-  }();
-  for (;;) {
-    int64_t t0 = 0;
-    if (diag && na >= (64u << 10)) {
-      int inq = 0;
-      if (::ioctl(fd_, SIOCINQ, &inq) == 0) {
-        g_diag_calls.fetch_add(1, std::memory_order_relaxed);
-        g_diag_want.fetch_add(na, std::memory_order_relaxed);
-        g_diag_inq.fetch_add(static_cast<uint64_t>(inq), std::memory_order_relaxed);
-        if (inq == 0) g_diag_empty.fetch_add(1, std::memory_order_relaxed);
-        else if (static_cast<size_t>(inq) < na) g_diag_short.fetch_add(1, std::memory_order_relaxed);
-        t0 = now_ns();
-      }
-    }
-    iovec iov[2] = {{a, na}, {b, nb}};
-    msghdr m{};
-    m.msg_iov = iov;
-    m.msg_iovlen = 2;
-    const ssize_t r = ::recvmsg(fd_, &m, 0);
-    if (t0) g_diag_ns.fetch_add(static_cast<uint64_t>(now_ns() - t0), std::memory_order_relaxed);
     if (r >= 0) {
       bytes_read_ += static_cast<uint64_t>(r);
       g_recv_calls.fetch_add(1, std::memory_order_relaxed);

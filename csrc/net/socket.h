@@ -51,10 +51,6 @@ struct SocketOptions {
   // Loopback endpoints only: minimum RTO kLoopbackRtoMinUs instead of 200 ms
   // (set_loopback_rto_min); never for a real network path.
   bool loopback_rto_min = false;
-  // A payload recv() also refills the reader's 16 KiB buffer (one recvmsg,
-  // two iovecs), so the bytes after the payload -- the next HTTP/2 frame's
-  // header -- need no system call of their own (BufferedConn::read_some).
-  bool recv_refill = false;
   // Most bytes one fill (or refill) of the reader's small-read buffer takes
   // from the socket (<= its 16 KiB).  A fill for a 9-byte frame header also
   // takes the payload behind it, which then costs a second copy out of the
@@ -107,10 +103,6 @@ class Conn {
 
   // Returns bytes read (0 = orderly EOF); throws StorageError(retryable) on reset.
   size_t read_some(void* buf, size_t n);
-  // One recvmsg() into a then b (plain TCP): bytes past na land in b.  A
-  // payload read that also picks up what follows it (the next frame's
-  // header) saves the header its own system call.  TLS: a alone.
-  size_t read_some2(void* a, size_t na, void* b, size_t nb);
   // One recvmsg() into iov[0..cnt) in order (plain TCP; TLS: iov[0] alone).
   size_t read_somev(struct iovec* iov, int cnt);
   // Reads exactly n bytes or throws (EOF mid-way is a retryable error).
@@ -130,7 +122,6 @@ class Conn {
   bool is_open() const { return fd_ >= 0; }
   bool tls() const { return ssl_ != nullptr; }
   uint64_t bytes_read() const { return bytes_read_; }
-  bool recv_refill() const { return recv_refill_; }
   size_t fill_bytes() const { return fill_bytes_; }
   uint64_t bytes_written() const { return bytes_written_; }
 
@@ -146,7 +137,6 @@ class Conn {
   SSL* ssl_ = nullptr;
   std::mutex ssl_mu_;
   int io_timeout_ms_ = 0;
-  bool recv_refill_ = false;
   size_t fill_bytes_ = 16384;
   uint64_t bytes_read_ = 0;
   uint64_t bytes_written_ = 0;

@@ -27,7 +27,6 @@
 #include "server/fakegcs.h"
 #include "storage/auth.h"
 #include "storage/client.h"
-#include "storage/host_arena.h"
 #include "storage/sliced.h"
 
 namespace py = pybind11;
@@ -78,7 +77,6 @@ ClientConfig client_from(const py::dict& d) {
   c.sock.io_timeout_ms = get_or<int>(d, "io_timeout_ms", 0);
   c.sock.congestion = get_or<std::string>(d, "tcp_congestion", "");
   c.sock.loopback_rto_min = get_or<bool>(d, "loopback_rto_min", false);
-  c.sock.recv_refill = get_or<bool>(d, "recv_refill", false);
   c.sock.fill_bytes = get_or<size_t>(d, "fill_bytes", c.sock.fill_bytes);
   c.sock.tls_verify = get_or<bool>(d, "tls_verify", true);
   c.sock.tls_ca_file = get_or<std::string>(d, "tls_ca_file", "");
@@ -494,8 +492,6 @@ class PyRunner {
     c.keep_records = get_or<bool>(d, "keep_records", true);
     c.read_diag = get_or<bool>(d, "read_diag", false);
     c.conn_ring = get_or<bool>(d, "conn_ring", c.conn_ring);
-    c.conn_ring_inplace = get_or<bool>(d, "conn_ring_inplace", c.conn_ring_inplace);
-    c.conn_ring_single = get_or<bool>(d, "conn_ring_single", c.conn_ring_single);
     c.conn_ring_slot_bytes = get_or<size_t>(d, "conn_ring_slot_bytes", c.conn_ring_slot_bytes);
     c.conn_ring_slots = get_or<int>(d, "conn_ring_slots", c.conn_ring_slots);
     if (d.contains("diag_avoid_cpus") && !d["diag_avoid_cpus"].is_none())
@@ -598,9 +594,6 @@ class PyRunner {
     d["reader_wait_s"] = s.reader_wait_s;
     d["finish_polls"] = s.finish_polls;
     d["finish_sleeps"] = s.finish_sleeps;
-    d["arena"] = r->arena();
-    d["arena_recvs"] = r->arena_recvs();
-    d["arena_bytes"] = r->arena_bytes();
     return d;
   }
   std::string transport_path() { return runner_->client().transport_path(); }
@@ -747,6 +740,8 @@ namespace {
 // process in std::terminate.  Under pytest, stderr is captured at the fd
 // level, so the runtime's own message is lost with the process: write the
 // exception, the thread and a backtrace straight to the terminal's stderr.
+std::terminate_handler g_prev_terminate = nullptr;
+
 [[noreturn]] void terminate_with_report() {
   char name[32] = "?";
   pthread_getname_np(pthread_self(), name, sizeof(name));
@@ -760,14 +755,12 @@ namespace {
       what = "(non-std exception)";
     }
   }
-  int fd = ::open("/dev/tty", O_WRONLY | O_CLOEXEC);
-  if (fd < 0) fd = 2;
   const std::string head = "gcsb: std::terminate in thread '" + std::string(name) + "': " + what + "\n";
-  (void)!::write(fd, head.data(), head.size());
   void* frames[64];
   const int nf = backtrace(frames, 64);
-  backtrace_symbols_fd(frames, nf, fd);
-  if (const char* path = std::getenv("GCSB_TERMINATE_LOG")) {
+  (void)!::write(2, head.data(), head.size());
+  backtrace_symbols_fd(frames, nf, 2);
+  if (const char* path = std::getenv("GCSB_TERMINATE_LOG"); path && *path) {
     const int lf = ::open(path, O_WRONLY | O_CREAT | O_APPEND | O_CLOEXEC, 0644);
     if (lf >= 0) {
       (void)!::write(lf, head.data(), head.size());
@@ -775,44 +768,18 @@ namespace {
       ::close(lf);
     }
   }
+  if (g_prev_terminate) g_prev_terminate();  // whatever handler was installed before ours
   std::abort();
 }
 }  // namespace
 
 PYBIND11_MODULE(_native, m) {
   m.doc() = "MI355X-native object-storage benchmark core (C++/HIP)";
-  std::set_terminate(terminate_with_report);
+  // opt-in (GCSB_TERMINATE_LOG=<file>): a process-wide terminate handler is
+  // no side effect an import should have; it reports to fd 2 and
+  // the file, then chains to the handler it replaced
+  if (const char* e = std::getenv("GCSB_TERMINATE_LOG"); e && *e) g_prev_terminate = std::set_terminate(terminate_with_report);
   py::register_exception<StorageError>(m, "StorageError");
-
-  // The arena parse path on the CPU (storage/host_arena.h): a gRPC read whose
-  // connection recv()s into a host arena, payload taken in place.
-  m.def(
-      "arena_read",
-      [](const py::dict& cfg, const std::string& bucket, const std::string& name, size_t slot_bytes, int slots,
-         bool want_data) {
-        HostArena arena(slot_bytes, slots);
-        InplaceHostSink sink(&arena);
-        ReadResult rr;
-        {
-          ClientConfig cc = client_from(cfg);
-          cc.protocol = "grpc";
-          cc.grpc_conn_pool_size = 1;
-          cc.recv_arena = &arena;
-          py::gil_scoped_release nogil;
-          auto client = make_client(cc);  // destroyed (reader joined) before the arena
-          rr = client->read_object(bucket, name, sink);
-        }
-        py::dict d = sink_result_dict(rr);
-        d["arena_recvs"] = arena.recvs();
-        d["arena_bytes"] = arena.bytes();
-        d["inplace_commits"] = sink.inplace_commits();
-        d["chunks_checked"] = sink.chunks_checked();
-        if (want_data)
-          d["data"] = py::bytes(reinterpret_cast<const char*>(sink.data().data()), sink.data().size());
-        return d;
-      },
-      py::arg("cfg"), py::arg("bucket"), py::arg("name"), py::arg("slot_bytes") = 1 << 20, py::arg("slots") = 4,
-      py::arg("want_data") = false);
 
   m.def("set_deferred_wake_blocks", [](int n) { DiscardSink::wake_blocks().store(n); },
         "A/B: a deferred discard sink wakes its worker once this many blocks are queued (0: every message)");
@@ -851,16 +818,6 @@ PYBIND11_MODULE(_native, m) {
       },
       py::arg("data"), py::arg("misalign") = 0, py::arg("expected") = 0, py::arg("check") = false,
       py::arg("tile_log2") = kCrcMaxTileLog2, py::arg("fold_waves") = 8);
-  m.def("emulate_mfma_tile_crc", [](const py::bytes& b) {
-    static MfmaCrcTables* t = [] {
-      auto* x = new MfmaCrcTables();
-      build_mfma_crc_tables(x);
-      return x;
-    }();
-    std::string s = b;
-    if (s.size() != 4096) throw std::invalid_argument("a tile is 4096 bytes");
-    return emulate_mfma_tile_crc(reinterpret_cast<const uint8_t*>(s.data()), *t);
-  });
   m.def("object_rotation", &object_rotation);
   m.def("object_bytes", [](const std::string& name, uint64_t off, uint64_t n) {
     std::string out(n, '\0');
@@ -1115,22 +1072,16 @@ PYBIND11_MODULE(_native, m) {
   // kernel A/Bs and tests; returns the options now in force
   m.def("set_crc_options", [](const py::dict& d) {
     CrcLaunchOptions o = crc_launch_options();
-    o.slot_kernel = get_or<bool>(d, "slot_kernel", o.slot_kernel);
     o.slot_waves = get_or<int>(d, "slot_waves", o.slot_waves);
     o.xor_arrival = get_or<bool>(d, "xor_arrival", o.xor_arrival);
-    o.nibble_tables = get_or<bool>(d, "nibble_tables", o.nibble_tables);
-    o.mfma = get_or<bool>(d, "mfma", o.mfma);
     o.slice8 = get_or<bool>(d, "slice8", o.slice8);
     o.bank_private = get_or<bool>(d, "bank_private", o.bank_private);
     set_crc_launch_options(o);
     py::dict r;
     r["bank_private"] = o.bank_private;
-    r["slot_kernel"] = o.slot_kernel;
     r["slot_waves"] = o.slot_waves;
     r["xor_arrival"] = o.xor_arrival;
-    r["nibble_tables"] = o.nibble_tables;
     r["slice8"] = o.slice8;
-    r["mfma"] = o.mfma;
     return r;
   }, py::arg("options") = py::dict());
   m.def("gpu_read_bytes",[](int dev, uintptr_t ptr, size_t n) {

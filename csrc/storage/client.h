@@ -23,7 +23,6 @@
 
 namespace gcsb {
 
-class RecvArena;  // net/buffered.h
 
 struct ClientConfig {
   std::string protocol = "http";  // http | http2 | grpc
@@ -53,9 +52,6 @@ struct ClientConfig {
   // multiplexed connection's one reader receives every stream's bytes, so it
   // gets a physical core the workers do not share (affinity.isolate_reader)
   std::vector<int> reader_cpus;
-  // gRPC, pool size 1: the connection's reader recv()s into this arena and
-  // hands payload to the sinks in place (gpu/engine.h ConnRing); not owned
-  RecvArena* recv_arena = nullptr;
 };
 
 struct ObjectMeta {

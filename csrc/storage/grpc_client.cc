@@ -307,30 +307,6 @@ class ReadObjectHandler : public MessageHandler {
         uint64_t k = std::min<uint64_t>(content_left_, msg_left - used);
         if (*delivered_ + std::min<uint64_t>(k, c.left()) > cap_)
           throw StorageError("ReadObject: server sent more than read_limit bytes", false);
-        if (c.inplace() && (sink_failed_ || sink_.accepts_inplace())) {
-          // the content already lies in the sink's arena: hand it over where
-          // it is (one recv() may have brought several frames' worth)
-          k = std::min<uint64_t>(k, c.left());
-          while (k > 0) {
-            const uint8_t* p = nullptr;
-            const size_t m = c.take_inplace(static_cast<size_t>(k), &p);
-            if (!rr_->first_byte_ns) rr_->first_byte_ns = now_ns();
-            if (!sink_failed_) {
-              try {
-                sink_.commit_inplace(p, m);
-              } catch (const std::exception& e) {
-                fail_sink(e.what());
-              }
-            }
-            *delivered_ += m;
-            consume(static_cast<uint32_t>(m));
-            used += m;
-            content_left_ -= m;
-            k -= m;
-          }
-          if (content_left_ == 0) after_cd_field();
-          continue;
-        }
         Window w;
         if (!sink_failed_) {
           try {
@@ -591,8 +567,6 @@ class GrpcStorageClient : public StorageClient {
     opt_.max_frame_size = cfg.h2_max_frame_size;
     opt_.initial_window = cfg.h2_window;
     opt_.span_max_frame = cfg.h2_span_max_frame;
-    // one arena, one reader: only a pool of one connection receives into it
-    if (cfg.grpc_conn_pool_size == 1) opt_.recv_arena = cfg.recv_arena;
     // DirectPath (reference main.go:106-117: GOOGLE_CLOUD_ENABLE_DIRECT_PATH_XDS
     // is set only around NewGRPCClient, with the google-c2p xDS resolver and
     // the RLS balancer linked in).  DirectPath needs the GCE metadata server,

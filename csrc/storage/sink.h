@@ -53,11 +53,6 @@ class Sink {
   virtual Window acquire(size_t want) = 0;
   // `n` bytes were written at the start of the last acquired window.
   virtual void commit(size_t n) = 0;
-  // In-place delivery: the transport received into the connection's arena
-  // (net/buffered.h RecvArena) and `n` payload bytes already lie at `p`.
-  // Only a sink that owns that arena accepts them (GpuSink on a ConnRing).
-  virtual bool accepts_inplace() const { return false; }
-  virtual void commit_inplace(const uint8_t* p, size_t n) { (void)p; (void)n; }
   // gRPC ChecksummedData framing: a chunk of `len` content bytes follows...
   virtual void chunk_begin(size_t len) { (void)len; }
   // ...and ended; its crc32c if the message carried one.

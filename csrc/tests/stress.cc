@@ -20,7 +20,6 @@
 #include "core/crc32c.h"
 #include "server/fakegcs.h"
 #include "storage/client.h"
-#include "storage/host_arena.h"
 #include "storage/sink.h"
 #include "storage/sliced.h"
 
@@ -45,10 +44,6 @@ ClientConfig client_cfg(const std::string& proto, const std::string& url) {
   c.retry.max_s = 0.01;
   c.retry.max_attempts = 8;
   c.read_chunk = 256 << 10;
-  // the optional receive path (SocketOptions::recv_refill) for the
-  // sanitizer runs that ask for it
-  const char* e = std::getenv("STRESS_RECV_REFILL");
-  c.sock.recv_refill = e && *e == '1';
   return c;
 }
 
@@ -107,37 +102,20 @@ int main(int argc, char** argv) {
     srv2.stop();
   }
 
-  // arena receive (net/buffered.h RecvArena): the gRPC connection's reader
-  // recv()s into one host arena and hands every stream's payload to its sink
-  // in place; three workers' streams share it, then a mid-stream disconnect
-  {
-    HostArena arena(64 << 10, 4);
-    ClientConfig ac = client_cfg("grpc", srv.url());
-    ac.recv_arena = &arena;
-    auto cli = make_client(ac);
-    for (int round = 0; round < 2; ++round) {
-      if (round == 1) {
-        srv.faults().disconnect_at = (1 << 20) + 11;
-        srv.faults().disconnect_count = 1;
-      }
-      std::vector<std::thread> th;
-      for (int t = 0; t < 3; ++t)
-        th.emplace_back([&, t] {
-          InplaceHostSink sink(&arena);
-          for (int i = 0; i < 2 * scale; ++i) {
-            const std::string name = "obj_" + std::to_string((t + i) % nobj);
-            try {
-              ReadResult rr = cli->read_object(bucket, name, sink);
-              check(rr.sink.verified && !rr.sink.crc_mismatch, "arena read " + name + ": " + rr.sink.detail);
-            } catch (const std::exception& e) {
-              check(false, "arena read " + name + ": " + e.what());
-            }
-          }
-        });
-      for (auto& x : th) x.join();
-      srv.faults().disconnect_count = 0;
-    }
-    check(arena.recvs() > 0, "arena used");
+  // the reference's HTTP/2 receive settings (16 KiB DATA frames, 16 MiB
+  // windows): six workers' streams multiplexed on one connection land through
+  // the spanning receive (h2/h2_client.h H2DataCursor), whose plans meet the
+  // other streams' frames and hand bytes back; then a mid-stream disconnect
+  for (const char* proto : {"grpc", "http2"}) {
+    ClientConfig fc = client_cfg(proto, srv.url());
+    fc.h2_max_frame_size = 0;
+    fc.h2_window = 16u << 20;
+    auto cli = make_client(fc);
+    readers(*cli, bucket, nobj, 6, 2 * scale);
+    srv.faults().disconnect_at = (1 << 20) + 16384 * 3 + 11;
+    srv.faults().disconnect_count = 1;
+    readers(*cli, bucket, nobj, 3, 2);
+    srv.faults().disconnect_count = 0;
   }
 
   // one stream goes silent MID-BODY past the read timeout while the others on
@@ -145,16 +123,18 @@ int main(int argc, char** argv) {
   // the reader may be inside its dispatch), resumes at its delivered offset
   // on the same connection, and the endpoint's stalled handler wakes later
   // into a cancelled stream (tests/test_gpu_conn_ring.py stalled case, host
-  // sinks); then the same with the arena
-  for (const char* proto : {"http2", "grpc", "grpc-arena"}) {
-    const bool use_arena = std::strcmp(proto, "grpc-arena") == 0;
-    HostArena arena(1 << 20, 4);
-    ClientConfig tc = client_cfg(use_arena ? "grpc" : proto, srv.url());
+  // sinks); then the same at 16 KiB frames
+  for (const char* proto : {"http2", "grpc", "grpc-16k"}) {
+    const bool small = std::strcmp(proto, "grpc-16k") == 0;
+    ClientConfig tc = client_cfg(small ? "grpc" : proto, srv.url());
+    if (small) {
+      tc.h2_max_frame_size = 0;
+      tc.h2_window = 16u << 20;
+    }
     // the stall outlasts the starvation allowance (h2_client.h
     // kStarvedWindows) even when the other streams are slow (TSan)
     tc.sock.io_timeout_ms = 150;
     tc.retry.max_attempts = 6;
-    if (use_arena) tc.recv_arena = &arena;
     auto tcli = make_client(tc);
     for (int round = 0; round < 2 * scale; ++round) {
       srv.faults().stall_at = (1 << 20) + 77 * round;
@@ -163,11 +143,7 @@ int main(int argc, char** argv) {
       std::vector<std::thread> th;
       for (int t = 0; t < 6; ++t)
         th.emplace_back([&, t] {
-          std::unique_ptr<Sink> sink;
-          if (use_arena)
-            sink = std::make_unique<InplaceHostSink>(&arena);
-          else
-            sink = std::make_unique<DiscardSink>(tc.read_chunk, true, true);
+          auto sink = std::make_unique<DiscardSink>(tc.read_chunk, true, true);
           for (int i = 0; i < 2; ++i) {
             const std::string name = "obj_" + std::to_string((t + i) % nobj);
             try {

@@ -222,10 +222,6 @@ class SideBlocks:
                 # the other two (profiles/r3_write/placement)
                 pl = self.affinity.plan(gpu, "pair", self.slot)
                 sh = {"client": pl["client"], "server": sorted(pl["server"] + pl.get("aux", []))}
-                if getattr(args, "write_split", "off") == "on" and pl.get("aux"):
-                    # the endpoint's receiving connection thread on one core,
-                    # its CRC worker on the other
-                    sh = {"client": pl["client"], "server": pl["server"], "crc_cpus": pl["aux"]}
                 ep = n.Server({"port": 0, "md5": False, "cpus": sh["server"], "send_cpus": sh.get("send_cpus"),
                                "crc_cpus": sh.get("crc_cpus"),
                                "retain_uploads": False})

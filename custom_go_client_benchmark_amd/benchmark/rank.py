@@ -46,6 +46,33 @@ FRAMING = {"ref": {"h2_max_frame_size": 0, "h2_window": 16 << 20},
            "large": {"h2_max_frame_size": (1 << 24) - 1, "h2_window": 0x7FFFFFFF}}
 FRAME_LABEL = {"ref": "16KiB", "large": "16MiB"}
 
+# Settings fixed by measurement in rounds 2-5 (no longer flags; the profiles/
+# that chose each are cited where it is used).
+FIXED = {
+    "conn_ring": "4x1MiB",        # multiplexed gRPC -> HBM: one 4 x 1 MiB ring per connection (r4_ringgeom)
+    "async_submit": 1,            # slot hand-off on the device submitter thread (r2_single_stream)
+    "submit_cpus": "aux",         # ... on a core of its own from the placement plan
+    "rcvbuf": "64MiB",            # one-stream reads' SO_RCVBUF request (r2_rcvbuf)
+    "sliced_slot_bytes": "2MiB",  # sliced block: 2 x 2 MiB ring per sink (r2_sliced, r3_ring_thp/sliced)
+    "sliced_slots": 2,
+    "sliced_async_submit": 0,
+    "piece_bytes": "8MiB",        # sliced reads pull 8 MiB pieces from a shared cursor
+    "piece_min_bytes": "0",
+    "event_wait": "block",        # GPU sinks wait on slot events by blocking (the CPU quota)
+    "list_placement": "same",     # config 3: readers and endpoint in one L3 domain (r2_check_s4b)
+    "list_ring_wc": "on",         # config 3: write-combined rings (r3_ring_thp/wc)
+    "list_rcvbuf": "64MiB",
+    "ceiling": "on",              # the ceiling block (--blocks selects it away)
+    "ref_grpc_placement": "same",        # 48 workers on one connection in one L3 domain (r3_mux_thp/refplace)
+    "ref_http_placement": "share_quota",  # 48 HTTP receivers over the quota's cores
+    "ref_gpu_ring": "2x2MiB",
+    "ref_grpc_rcvbuf": "0",
+    "write_placement": "pair",    # config 5: uploader + endpoint on three quiet cores (r3_write/placement)
+    "mux_send": "isolate",        # multiplexed blocks: the endpoint send thread and the
+    "mux_reader": "isolate",      # connection reader on physical cores of their own (r5_muxiso)
+    "client_cc": "cubic",         # client sockets' congestion control, set before connect (r4_recvcost)
+}
+
 
 class RankBench(SideBlocks):
     """One rank's benchmark: its endpoint, placement and blocks."""
@@ -64,6 +91,9 @@ class RankBench(SideBlocks):
         self.affinity = affinity
         self.gdist = gdist
         self.n = pkg._native
+        for k, v in FIXED.items():
+            if not hasattr(args, k):
+                setattr(args, k, v)
         self.rank, self.world, self.local_rank = gdist.env_rank()
         self.use_gpu = args.sink == "gpu"
         self.rehearsal = os.environ.get("GCSB_DIST_BACKEND") == "gloo"
@@ -118,8 +148,6 @@ class RankBench(SideBlocks):
         self.placement = affinity.plan(self.gpu, aff, self.slot) if self.use_gpu else {"client": [], "server": []}
         if self.use_gpu and args.submit_cpus == "aux" and self.placement.get("aux"):
             n.set_submitter_cpus(self.placement["aux"])
-        if self.use_gpu and (args.crc_slot_waves or args.crc_slice8 == "off"):
-            n.set_crc_options({"slot_waves": args.crc_slot_waves, "slice8": args.crc_slice8 == "on"})
         self.srv = n.Server({"port": 0, "md5": False, "cpus": self.placement["server"], "retain_uploads": False})
         self.srv.start()
         self.bucket = "princer-working-dirs"
@@ -138,9 +166,7 @@ class RankBench(SideBlocks):
             "device": self.gpu if self.use_gpu else 0,
             "ring_slot_bytes": parse_size(args.slot_bytes),
             "ring_slots": args.slots,
-            "ring_wc": getattr(args, "ring_wc", "off") == "on",
             "conn_ring": args.conn_ring != "off",
-            "conn_ring_inplace": args.conn_ring_inplace == "on",
             "conn_ring_slots": int(args.conn_ring.partition("x")[0]) if "x" in args.conn_ring else 4,
             "conn_ring_slot_bytes": parse_size(args.conn_ring.partition("x")[2]) if "x" in args.conn_ring else 1 << 20,
             "landing": "object",
@@ -156,10 +182,8 @@ class RankBench(SideBlocks):
             "rcvbuf": parse_size(args.rcvbuf),
             "tcp_congestion": args.client_cc,
             "loopback_rto_min": True,
-            "recv_refill": bool(args.recv_refill),
-            "fill_bytes": parse_size(getattr(args, "fill_bytes", "16KiB")),
         }
-        self.framing_name = getattr(args, "h2_framing", "ref")
+        self.framing_name = getattr(args, "h2_framing", "large")
         self.framing = dict(FRAMING[self.framing_name])
         self.cfg.update(self.framing)
         return 0

@@ -219,21 +219,3 @@ def test_fs_suite_drivers(tmp_path):
     assert len(phases) == 11 and all(p["rc"] == 0 for p in d["phases"])
     ssd = [p for p in d["phases"] if p["phase"].startswith("ssd_test")]
     assert all("P50" in p["stdout"] or "p99" in p["stdout"] for p in ssd)
-
-
-@pytest.mark.parametrize("mode,send", [("recv", "sendfile"), ("zc_map", "sendfile"), ("zc_workers", "msg_zerocopy")])
-def test_zc_probe_moves_every_byte(mode, send):
-    """csrc/tools/zc_probe.cc (profiles/r5_zc): every mode receives the whole
-    stream and reports one JSON line; how much is mapped depends on the
-    kernel, so only its range is checked."""
-    exe = f"{BIN}/zc_probe"
-    if not os.path.exists(exe):
-        pytest.skip("probes not built (make probes)")
-    r = run([exe, "-mode", mode, "-send", send, "-workers", "2", "-total", str(64 << 20), "-object", str(16 << 20)],
-            timeout=60)
-    if r.returncode != 0 and "TCP_ZEROCOPY_RECEIVE" in r.stderr + r.stdout and mode != "recv":
-        pytest.skip("kernel without TCP zero-copy receive")
-    assert r.returncode == 0, r.stderr[-2000:]
-    d = json.loads(r.stdout.strip().splitlines()[-1])
-    assert d["mode"] == mode and abs(d["payload_gib"] - 64 / 1024) < 0.006  # printed with 2 decimals
-    assert 0.0 <= d["mapped_frac"] <= 1.0 and d["gbps"] > 0

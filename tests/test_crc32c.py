@@ -89,15 +89,3 @@ def test_goog_hash_parsing(native):
     has, crc, md5 = native.parse_goog_hash("crc32c=4waSgw==,md5=XUFAKrxLKna5cZ2REBfFkg==")
     assert has and crc == 0xE3069283
     assert len(md5) == 16
-
-
-def test_mfma_tile_crc_model(native):
-    """The int8-MFMA tile CRC decomposition (4 pieces x 8 bit planes of
-    32 x 32 GF(2) matrices per 128-byte chunk, parity of int32 sums, chunk ->
-    tile-end shift columns) reproduces the raw CRC of a 4 KiB tile."""
-    for _ in range(4):
-        d = os.urandom(4096)
-        assert native.emulate_mfma_tile_crc(d) == native.crc32c_raw(d)
-    assert native.emulate_mfma_tile_crc(bytes(4096)) == 0
-    d = bytes([0xFF]) * 4096
-    assert native.emulate_mfma_tile_crc(d) == native.crc32c_raw(d)

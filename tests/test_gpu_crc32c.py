@@ -54,7 +54,6 @@ def test_fill_and_verify_pattern(native, gpu_available):
 
 
 @pytest.mark.parametrize("opts", [{"slot_waves": 1}, {"xor_arrival": False}, {"slot_waves": 8},
-                                  {"nibble_tables": True}, {"slot_kernel": False}, {"mfma": True},
                                   {"slice8": False}, {"slice8": False, "slot_waves": 1},
                                   {"slice8": False, "xor_arrival": False}, {"slice8": True},
                                   {"bank_private": False}, {"bank_private": True}])

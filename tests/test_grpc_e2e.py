@@ -48,12 +48,12 @@ def test_send_threads_on_their_own_cpus(native):
 
 
 @pytest.mark.parametrize("fill", [64, 512, 16384])
-@pytest.mark.parametrize("refill", [False, True])
-def test_small_buffer_fills_stay_exact(native, server, fill, refill):
+@pytest.mark.parametrize("frame", [0, (1 << 24) - 1])
+def test_small_buffer_fills_stay_exact(native, server, fill, frame):
     """SocketOptions::fill_bytes caps what a frame-header fill takes of the
-    payload behind it (with and without the payload recv's refill)."""
+    payload behind it (16 KiB frames with the spanning receive, 16 MiB frames)."""
     server.add_synthetic(B, "fill/file_", "", 0, 3, 5 * (1 << 20) + 7)
-    c = _c(native, server, fill_bytes=fill, recv_refill=refill)
+    c = _c(native, server, fill_bytes=fill, h2_max_frame_size=frame)
     for i in range(3):
         assert c.read_bytes(B, f"fill/file_{i}") == native.object_bytes(f"fill/file_{i}", 0, 5 * (1 << 20) + 7)
         assert c.read(B, f"fill/file_{i}")["verified"]

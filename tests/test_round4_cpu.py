@@ -1,6 +1,6 @@
 """Round-4 host-side features on CPU: the endpoint's listener congestion
 control (no inherited BBR pacing), FIFO HTTP/2 frame writes with a quantum,
-per-read stall attribution (Runner read_diag), recv_refill, client-side
+per-read stall attribution (Runner read_diag), client-side
 congestion control, and the sysdiag host view."""
 import os
 import threading
@@ -148,15 +148,6 @@ def test_attribute_names_run_queue_delay_and_timer_storms():
     assert "receive copy itself" in sysdiag.attribute(d, 14.0, 10.0)
     d["tcp"] = {"RetransSegs": 12, "TCPTimeouts": 1, "TCPLossProbes": 0}
     assert "12 TCP retransmits (1 RTOs" in sysdiag.attribute(d, 14.0, 10.0)
-
-
-@pytest.mark.parametrize("proto", ["grpc", "http2", "http"])
-def test_recv_refill_byte_exact(native, server, proto):
-    size = (9 << 20) + 4321
-    server.add_synthetic(B, P, "", 0, 1, size)
-    c = native.Client({"protocol": proto, "endpoint": server.url, "recv_refill": True})
-    assert c.read_bytes(B, P + "0") == native.object_bytes(P + "0", 0, size)
-    assert c.read(B, P + "0")["verified"]
 
 
 def test_client_congestion_control_option(native, server):

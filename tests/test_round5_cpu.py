@@ -235,48 +235,6 @@ def test_native_stdout_noise_goes_to_stderr():
     assert "RCCL version" in r.stderr and "python noise" in r.stderr
 
 
-# ---------------------------------------------------------------- arena path
-@pytest.mark.parametrize("chunk", [2 << 20, 99991, 4096 + 7])
-@pytest.mark.parametrize("slot_bytes,slots", [(1 << 20, 4), (64 << 10, 3), (4096, 2)])
-def test_arena_read_byte_exact(native, chunk, slot_bytes, slots):
-    """The connection's recv() lands in the arena a slot's worth at a time,
-    across HTTP/2 frame and gRPC message boundaries; the gRPC parser reads
-    headers in place and hands every content run to the sink where it lies
-    (net/buffered.h RecvArena, storage/host_arena.h).  Frame headers, message
-    prefixes and protobuf tags fall anywhere in a slot, or across two."""
-    srv = native.Server({"port": 0, "grpc_chunk": chunk})
-    srv.start()
-    try:
-        size = (3 << 20) + 12345
-        srv.add_synthetic("b", "a/f_", "", 0, 1, size)
-        r = native.arena_read({"endpoint": srv.url}, "b", "a/f_0", slot_bytes, slots, True)
-        assert r["bytes"] == size and r["verified"] and not r["crc_mismatch"], r["detail"]
-        assert r["data"] == native.object_bytes("a/f_0", 0, size)
-        assert r["chunks_checked"] == (size + chunk - 1) // chunk
-        assert r["inplace_commits"] >= r["chunks_checked"]
-        # every byte came through the arena: payload plus the protocol bytes around it
-        assert r["arena_bytes"] > size and r["arena_recvs"] >= 1
-    finally:
-        srv.stop()
-
-
-def test_arena_read_detects_corruption_and_resumes(native):
-    srv = native.Server({"port": 0, "grpc_chunk": 99991})
-    srv.start()
-    try:
-        size = (2 << 20) + 5
-        srv.add_synthetic("b", "a/f_", "", 0, 1, size)
-        srv.set_faults({"corrupt_at": (1 << 20) + 3, "corrupt_count": 1})
-        r = native.arena_read({"endpoint": srv.url}, "b", "a/f_0", 64 << 10, 4, False)
-        assert r["crc_mismatch"] and "mismatch" in r["detail"]
-        srv.set_faults({"disconnect_at": (1 << 20) + 17, "disconnect_count": 1})
-        r = native.arena_read({"endpoint": srv.url, "retry_initial_s": 0.01}, "b", "a/f_0", 64 << 10, 4, True)
-        assert r["attempts"] >= 2 and r["bytes"] == size and not r["crc_mismatch"], r
-        assert r["data"] == native.object_bytes("a/f_0", 0, size)
-    finally:
-        srv.stop()
-
-
 def test_fit_line_never_exceeds_the_limit():
     """Even a pathological headline (huge config strings) yields a line within
     the limit with the driver keys, never an exception."""

@@ -67,7 +67,7 @@ def test_resumable_chunk_with_overlap_is_deduplicated(native, server):
 
 
 def test_write_crc_worker_on_its_own_cpus(native):
-    """ServerConfig::crc_cpus (bench --write-split): the WriteObject CRC
+    """ServerConfig::crc_cpus: the WriteObject CRC
     worker pinned apart from the connection thread still checks every
     message and the object lands exact."""
     cpus = sorted(os.sched_getaffinity(0))

@@ -344,7 +344,13 @@ class ConnRing {
 
 // Upload source for the write path (config 5): HBM -> pinned ring via
 // hipMemcpyAsync D2H on a side stream, `slots` copies kept in flight ahead of
-// the transport; the object CRC32C is computed on the GPU from HBM.
+// the transport.  CRC32C on the GPU from HBM, per staged slot: each slot's
+// copy is followed on its stream by one CRC launch over the slot's range
+// (a segment per chunk of the message grid), results in host-mapped memory,
+// so a message's CRC is ready when its slot's event is; the object CRC is the
+// host combine of the chunk CRCs, known once every slot was staged.  Round 5
+// ran one synchronous whole-object gpu_crc32c in the constructor instead: a
+// launch + sync before the first D2H of every upload.
 class GpuByteSource : public ByteSource {
  public:
   GpuByteSource(int device, const void* dptr, uint64_t n, size_t slot_bytes, int slots, bool gpu_crc = true);
@@ -353,7 +359,8 @@ class GpuByteSource : public ByteSource {
   std::pair<const uint8_t*, size_t> next(size_t max) override;
   void seek(uint64_t off) override;
   bool has_crc32c() const override { return has_crc_; }
-  uint32_t crc32c() const override { return crc_; }
+  uint32_t crc32c() const override;
+  bool crc32c_ready() const override;
   // Ranges on the chunk grid (start on a grid multiple, end on one or at the
   // object end) are answered from the GPU-computed chunk CRCs.
   bool range_crc32c(uint64_t off, size_t len, uint32_t* crc) override;
@@ -375,6 +382,7 @@ class GpuByteSource : public ByteSource {
   void restart(uint64_t off);
   void issue(int slot, uint64_t off);
   void wait_all();
+  void harvest(int slot) const;  // slot's event done: its chunk CRCs into chunk_crc_
   int device_;
   const uint8_t* src_;
   uint64_t n_;
@@ -391,10 +399,23 @@ class GpuByteSource : public ByteSource {
   uint64_t next_issue_ = 0; // next object offset to prefetch
   int cur_ = 0;
   bool has_crc_ = false;
-  uint32_t crc_ = 0;
+  mutable bool crc_done_ = false;
+  mutable uint32_t crc_ = 0;
   uint64_t copies_ = 0;
-  uint64_t grid_ = 0;                // chunk grid of chunk_crc_ (0 = none)
-  std::vector<uint32_t> chunk_crc_;  // CRC32C of [i*grid_, min((i+1)*grid_, n_))
+  uint64_t grid_ = 0;                // message grid of range_crc32c (0 = none)
+  uint64_t chunk_ = 0;               // CRC chunk: grid_, or the slot when there is no grid
+  mutable std::vector<uint32_t> chunk_crc_;  // CRC32C of [i*chunk_, min((i+1)*chunk_, n_))
+  mutable std::vector<char> chunk_known_;
+  mutable size_t chunks_known_ = 0;
+  struct SlotCrc {
+    uint32_t* tiles = nullptr;  // tile scratch (pooled per device)
+    size_t tiles_cap = 0;
+    CrcSegResult* res = nullptr;  // host-mapped results, kMaxSeg entries
+    CrcSegResult* d_res = nullptr;
+  };
+  std::vector<SlotCrc> scr_;
+  mutable std::vector<char> slot_harvested_;
+  const CrcTables* d_tables_ = nullptr;
   uint64_t range_hits_ = 0;
 };
 

@@ -1478,6 +1478,53 @@ void GpuSink::ring_fold() {
 // ---------------------------------------------------------------------------
 // write path: HBM -> pinned ring (D2H) -> transport
 
+namespace {
+// Per-device pool of CRC tile scratch + host-mapped result blocks for the
+// upload sources (one per staging slot): a source lives for one upload, and
+// hipMalloc / hipHostMalloc per upload would cost more than its CRCs.
+struct CrcScratchBlock {
+  uint32_t* tiles = nullptr;
+  size_t tiles_cap = 0;
+  CrcSegResult* res = nullptr;
+  CrcSegResult* d_res = nullptr;
+};
+std::mutex g_crc_pool_mu;
+std::map<int, std::vector<CrcScratchBlock>> g_crc_pool;
+
+CrcScratchBlock crc_block_get(int device, size_t tiles_cap) {
+  {
+    std::lock_guard<std::mutex> lk(g_crc_pool_mu);
+    auto& v = g_crc_pool[device];
+    for (size_t i = 0; i < v.size(); ++i)
+      if (v[i].tiles_cap >= tiles_cap) {
+        CrcScratchBlock b = v[i];
+        v.erase(v.begin() + static_cast<long>(i));
+        return b;
+      }
+  }
+  CrcScratchBlock b;
+  b.tiles_cap = tiles_cap;
+  b.tiles = crc_scratch_alloc(tiles_cap);
+  hip_check(hipHostMalloc(reinterpret_cast<void**>(&b.res), sizeof(CrcSegResult) * kMaxSeg,
+                          hipHostMallocMapped | hipHostMallocCoherent),
+            "hipHostMalloc(upload CRC results)");
+  std::memset(b.res, 0, sizeof(CrcSegResult) * kMaxSeg);
+  hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&b.d_res), b.res, 0), "hipHostGetDevicePointer");
+  return b;
+}
+
+void crc_block_put(int device, const CrcScratchBlock& b) {
+  std::lock_guard<std::mutex> lk(g_crc_pool_mu);
+  auto& v = g_crc_pool[device];
+  if (v.size() < 64) {
+    v.push_back(b);
+    return;
+  }
+  (void)hipFree(b.tiles);
+  (void)hipHostFree(b.res);
+}
+}  // namespace
+
 GpuByteSource::GpuByteSource(int device, const void* dptr, uint64_t n, size_t slot_bytes, int slots, bool gpu_crc)
     : device_(device),
       src_(static_cast<const uint8_t*>(dptr)),
@@ -1523,10 +1570,24 @@ GpuByteSource::GpuByteSource(int device, const void* dptr, uint64_t n, size_t sl
     // messages are <= 2 MiB (gRPC MAX_WRITE_CHUNK_BYTES) and never cross a
     // staging slot, so with slot-aligned slots gcd(slot, 2 MiB) tiles them.
     const uint64_t g = std::gcd<uint64_t>(slot_bytes_, uint64_t(2) << 20);
-    if (g >= 65536) grid_ = g;
-    crc_ = gpu_crc32c(device_, src_, n_, grid_, grid_ ? &chunk_crc_ : nullptr);
+    grid_ = g >= 65536 ? g : 0;
+    chunk_ = grid_ ? grid_ : slot_bytes_;
+    if ((slot_bytes_ + chunk_ - 1) / chunk_ > static_cast<uint64_t>(kMaxSeg)) {  // one launch per slot
+      grid_ = 0;
+      chunk_ = slot_bytes_;
+    }
+    const size_t nchunks = static_cast<size_t>((n_ + chunk_ - 1) / chunk_);
+    chunk_crc_.assign(nchunks, 0);
+    chunk_known_.assign(nchunks, 0);
+    d_tables_ = device_crc_tables(device_);
+    scr_.resize(nslots_);
+    for (int i = 0; i < nslots_; ++i) {
+      CrcScratchBlock b = crc_block_get(device_, slot_bytes_ / kCrcMinTile + 2 * kMaxSeg + 8);
+      scr_[i] = {b.tiles, b.tiles_cap, b.res, b.d_res};
+    }
     has_crc_ = true;
   }
+  slot_harvested_.assign(nslots_, 1);
   restart(0);
 }
 
@@ -1536,11 +1597,58 @@ bool GpuByteSource::range_crc32c(uint64_t off, size_t len, uint32_t* crc) {
   if (end > n_ || (end % grid_ != 0 && end != n_)) return false;
   const size_t i = off / grid_, j = (end + grid_ - 1) / grid_;
   if (j > chunk_crc_.size()) return false;
+  for (size_t k = i; k < j; ++k)
+    if (!chunk_known_[k]) return false;  // not staged yet: the caller checksums the bytes
   uint32_t c = chunk_crc_[i];
   for (size_t k = i + 1; k < j; ++k) c = crc32c_combine(c, chunk_crc_[k], std::min<uint64_t>(grid_, n_ - k * grid_));
   *crc = c;
   ++range_hits_;
   return true;
+}
+
+void GpuByteSource::harvest(int slot) const {
+  if (slot_harvested_[slot] || !has_crc_ || slot_off_[slot] == ~0ull) return;
+  slot_harvested_[slot] = 1;
+  const uint64_t off = slot_off_[slot];
+  const size_t nseg = static_cast<size_t>((slot_len_[slot] + chunk_ - 1) / chunk_);
+  for (size_t k = 0; k < nseg; ++k) {
+    const CrcSegResult& r = scr_[slot].res[k];
+    if (__atomic_load_n(&r.status, __ATOMIC_ACQUIRE) == kCrcStatusPending)
+      throw std::logic_error("GpuByteSource: a staged slot's CRC result is missing");
+    const size_t c = static_cast<size_t>(off / chunk_) + k;
+    if (!chunk_known_[c]) {
+      chunk_known_[c] = 1;
+      ++chunks_known_;
+    }
+    chunk_crc_[c] = r.crc;
+  }
+}
+
+bool GpuByteSource::crc32c_ready() const { return has_crc_ && (crc_done_ || chunks_known_ == chunk_crc_.size()); }
+
+uint32_t GpuByteSource::crc32c() const {
+  if (!has_crc_) return 0;
+  if (crc_done_) return crc_;
+  if (chunks_known_ < chunk_crc_.size()) {
+    // asked before the upload staged every slot: collect what is in flight
+    for (int i = 0; i < nslots_; ++i)
+      if (!slot_harvested_[i] && slot_off_[i] != ~0ull) {
+        hip_check(hipEventSynchronize(ev_[i]), "hipEventSynchronize");
+        harvest(i);
+      }
+  }
+  if (chunks_known_ == chunk_crc_.size()) {
+    uint32_t c = 0;
+    for (size_t k = 0; k < chunk_crc_.size(); ++k)
+      c = k ? crc32c_combine(c, chunk_crc_[k], std::min<uint64_t>(chunk_, n_ - k * chunk_)) : chunk_crc_[0];
+    crc_ = n_ ? c : 0;
+  } else {
+    // an object larger than the staging ring, asked for up front: one
+    // whole-object pass now
+    crc_ = gpu_crc32c(device_, src_, n_);
+  }
+  crc_done_ = true;
+  return crc_;
 }
 
 GpuByteSource::~GpuByteSource() {
@@ -1552,6 +1660,7 @@ GpuByteSource::~GpuByteSource() {
     PinnedPool::put(host_[i], slot_bytes_);
     EventPool::put(device_, ev_[i]);
   }
+  for (const SlotCrc& c : scr_) crc_block_put(device_, {c.tiles, c.tiles_cap, c.res, c.d_res});
   if (own_stream_) (void)hipStreamDestroy(own_stream_);
 }
 
@@ -1559,7 +1668,10 @@ GpuByteSource::~GpuByteSource() {
 void GpuByteSource::wait_all() {
   hip_check(hipSetDevice(device_), "hipSetDevice");
   for (int i = 0; i < nslots_; ++i)
-    if (slot_off_[i] != ~0ull) hip_check(hipEventSynchronize(ev_[i]), "hipEventSynchronize");
+    if (slot_off_[i] != ~0ull) {
+      hip_check(hipEventSynchronize(ev_[i]), "hipEventSynchronize");
+      harvest(i);
+    }
 }
 
 void GpuByteSource::issue(int slot, uint64_t off) {
@@ -1570,8 +1682,27 @@ void GpuByteSource::issue(int slot, uint64_t off) {
   hip_check(hipMemcpyAsync(host_[slot], src_ + off, len, hipMemcpyDeviceToHost, st_[slot]), "hipMemcpyAsync(D2H)");
   const int64_t t1 = now_ns();
   note_hip_call("hipMemcpyAsync(D2H)", st_idx_[slot], t0, t1);
+  if (has_crc_) {
+    // the slot's chunk CRCs from HBM, on the copy's stream (both only read
+    // the object): ready with the slot's event
+    CrcBatch b;
+    std::memset(&b, 0, sizeof(b));
+    for (uint64_t o = off; o < off + len; o += chunk_) {
+      CrcSeg& c = b.seg[b.nseg++];
+      c.addr = src_ + o;
+      c.len = static_cast<uint32_t>(std::min<uint64_t>(chunk_, off + len - o));
+      c.flags = 0;
+    }
+    finalize_crc_batch(&b);
+    if (b.total_tiles > scr_[slot].tiles_cap) throw std::logic_error("GpuByteSource: CRC tile scratch too small");
+    for (uint32_t k = 0; k < b.nseg; ++k) __atomic_store_n(&scr_[slot].res[k].status, kCrcStatusPending, __ATOMIC_RELAXED);
+    launch_crc32c_batch(b, d_tables_, scr_[slot].tiles, scr_[slot].d_res, st_[slot]);
+    slot_harvested_[slot] = 0;
+    note_hip_call("crc launch(upload)", st_idx_[slot], t1, now_ns());
+  }
+  const int64_t t2 = now_ns();
   hip_check(hipEventRecord(ev_[slot], st_[slot]), "hipEventRecord");
-  note_hip_call("hipEventRecord(D2H)", st_idx_[slot], t1, now_ns());
+  note_hip_call("hipEventRecord(D2H)", st_idx_[slot], t2, now_ns());
   ++copies_;
 }
 
@@ -1606,6 +1737,7 @@ std::pair<const uint8_t*, size_t> GpuByteSource::next(size_t max) {
   }
   hip_check(hipSetDevice(device_), "hipSetDevice");
   hip_check(hipEventSynchronize(ev_[cur_]), "hipEventSynchronize");
+  harvest(cur_);
   const uint64_t so = slot_off_[cur_];
   if (so == ~0ull || pos_ < so || pos_ >= so + slot_len_[cur_])
     throw std::logic_error("GpuByteSource: staging ring out of step");

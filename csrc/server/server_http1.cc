@@ -603,6 +603,18 @@ class Http1Handler {
         persisted = static_cast<int64_t>(s->received);
       }
       if (total >= 0 && persisted == total) {
+        // the object's CRC32C may come with the final request instead of the
+        // session's metadata (x-goog-hash: crc32c=...)
+        if (const auto* gh = r.header("x-goog-hash")) {
+          bool has = false;
+          uint32_t crc = 0;
+          std::string md5;
+          parse_goog_hash(*gh, &has, &crc, &md5);
+          if (has) {
+            s->has_crc = true;
+            s->crc = crc;
+          }
+        }
         std::string err;
         auto o = srv_.store().finalize_upload(*s, &err);
         if (!o) return respond(c_, 400, {}, json_error(400, err, "invalid"));

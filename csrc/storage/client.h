@@ -96,7 +96,13 @@ class ByteSource {
   // Restart at `offset` (resumable upload recovery).
   virtual void seek(uint64_t offset) = 0;
   virtual bool has_crc32c() const { return false; }
+  // The object's CRC32C (has_crc32c()); a source that checksums as it stages
+  // (GpuByteSource) may have to finish that first when asked early.
   virtual uint32_t crc32c() const { return 0; }
+  // crc32c() is known now, without waiting: a transport asks for it at the
+  // start of an upload (StartResumableWrite / the session's metadata) only
+  // then, and otherwise sends it with the last message / chunk.
+  virtual bool crc32c_ready() const { return has_crc32c(); }
   // CRC32C of [off, off+len) when the source already holds it (the GPU
   // source checksums the object in HBM up front, chunk by chunk); false = the
   // caller computes it from the bytes.

@@ -735,9 +735,11 @@ class GrpcStorageClient : public StorageClient {
     return r;
   }
 
-  // Streams [from, total) of src as WriteObjectRequest messages on one call.
+  // Streams [from, total) of src as WriteObjectRequest messages on one call;
+  // the last one carries the object's checksums, asked of the source only
+  // then (a GPU source knows them once every slot was staged).
   ObjectMeta write_stream(const std::string& bucket_res, const std::string& upload_id, const std::string* spec,
-                          ByteSource& src, uint64_t from, const std::string& object_checksums) {
+                          ByteSource& src, uint64_t from) {
     const uint64_t total = src.size();
     const size_t kMsg = 2u << 20;  // ServiceConstants MAX_WRITE_CHUNK_BYTES [lib]
     BufferingHandler h;
@@ -759,6 +761,8 @@ class GrpcStorageClient : public StorageClient {
         // sources (no host pass over the bytes), else SSE4.2 on the host
         uint32_t crc = 0;
         if (k && !src.range_crc32c(off, k, &crc)) crc = crc32c(p, k);
+        const std::string object_checksums = last ? v2::encode_checksums(src.has_crc32c(), src.crc32c(), "")
+                                                  : std::string();
         v2::WriteRequestParts parts = v2::encode_write_request(first ? upload_id : std::string(),
                                                                first ? spec : nullptr, static_cast<int64_t>(off), k,
                                                                k > 0, crc, last ? &object_checksums : nullptr, last);
@@ -826,15 +830,20 @@ class GrpcStorageClient : public StorageClient {
     spec.resource.bucket = bres;
     spec.resource.content_type = opt.content_type;
     spec.object_size = static_cast<int64_t>(src.size());
-    const std::string checksums = v2::encode_checksums(src.has_crc32c(), src.crc32c(), "");
     if (!opt.resumable) {
       const std::string sp = v2::encode_write_spec(spec);
-      return with_retry([&] { return write_stream(bres, "", &sp, src, 0, checksums); });
+      return with_retry([&] { return write_stream(bres, "", &sp, src, 0); });
     }
     std::string upload_id;
     {
-      std::string resp =
-          with_retry([&] { return unary("StartResumableWrite", bres, v2::encode_start_resumable(spec, &checksums)); });
+      // the object's checksums up front only when the source already has
+      // them; else they ride in the last WriteObjectRequest (finish_write)
+      const std::string checksums =
+          src.crc32c_ready() ? v2::encode_checksums(src.has_crc32c(), src.crc32c(), "") : std::string();
+      std::string resp = with_retry([&] {
+        return unary("StartResumableWrite", bres,
+                     v2::encode_start_resumable(spec, checksums.empty() ? nullptr : &checksums));
+      });
       if (!v2::decode_upload_id(resp, &upload_id) || upload_id.empty())
         throw StorageError("StartResumableWrite: no upload_id", false);
     }
@@ -843,7 +852,7 @@ class GrpcStorageClient : public StorageClient {
     uint64_t from = 0;
     for (int attempt = 1;; ++attempt) {
       try {
-        return write_stream(bres, upload_id, nullptr, src, from, checksums);
+        return write_stream(bres, upload_id, nullptr, src, from);
       } catch (const StorageError& e) {
         if (!should_retry(cfg_.retry, e, attempt, t0)) throw;
         ++stats_.retries;

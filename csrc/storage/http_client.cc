@@ -450,7 +450,10 @@ class HttpStorageClient : public StorageClient {
     Json md = Json::object();
     md.set("name", Json::str(object));
     md.set("contentType", Json::str(opt.content_type));
-    if (src.has_crc32c()) md.set("crc32c", Json::str(crc32c_b64(src.crc32c())));
+    // the object's CRC32C in the session's metadata when the source already
+    // has it; else (a GPU source still staging) with the final chunk
+    const bool crc_up_front = src.crc32c_ready();
+    if (crc_up_front) md.set("crc32c", Json::str(crc32c_b64(src.crc32c())));
     auto stream_body = [&](Conn& c, uint64_t n) {
       while (n > 0) {
         auto [p, k] = src.next(n < (8u << 20) ? static_cast<size_t>(n) : (8u << 20));
@@ -513,6 +516,7 @@ class HttpStorageClient : public StorageClient {
                                           (last ? std::to_string(total) : "*");
         Http1Exchange ex(pool_, decorators_);
         Headers h{{"Content-Range", cr}};
+        if (last && !crc_up_front && src.has_crc32c()) h.emplace_back("x-goog-hash", "crc32c=" + crc32c_b64(src.crc32c()));
         src.seek(off);
         ex.send_stream("PUT", session, h, n, [&](Conn& c) { stream_body(c, n); });
         std::string body = ex.read_body_string();

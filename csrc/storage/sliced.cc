@@ -364,9 +364,10 @@ ObjectMeta SlicedWriter::write(const std::string& bucket, const std::string& obj
     names[i] = object + ".gcsb-part-" + tag + "-" + std::to_string(i);
     jobs_[i].fn = [&, i] {
       auto src = make_source(i, parts[i].first, parts[i].second);
+      metas[i] = clients_[i]->write_object(bucket, names[i], *src, opt);
+      // after the upload: a GPU source has every chunk CRC by then
       has_crc[i] = src->has_crc32c();
       crcs[i] = src->crc32c();
-      metas[i] = clients_[i]->write_object(bucket, names[i], *src, opt);
     };
   }
   run_all(n);

@@ -213,6 +213,7 @@ class SideBlocks:
         chunk = parse_size(args.write_chunk)
         client = buf = None
         ep = None
+        sh: dict = {}
         saved_aff = os.sched_getaffinity(0)
         gpu, rank = self.gpu, self.rank
         try:
@@ -271,6 +272,20 @@ class SideBlocks:
         by_name = {k: v - th0.get(k, 0.0) for k, v in cpuacct.thread_cpu().items()}
         cpu_split = {k: round(v / max(nbytes, 1) * (1 << 30), 4) for k, v in sorted(by_name.items())
                      if v > 0.0005 and nbytes}
+        # the upload's own bound, outside the timed region: ONE loopback TCP
+        # stream in the upload's direction and placement -- the uploader's
+        # core sending pages by reference (as the transport splices the
+        # staging ring), the endpoint's cores receiving into a 2 x 2 MiB THP
+        # buffer (as its WriteObject receive does); best of 3 probes
+        up_tcp = 0.0
+        if not err and parts == 1 and sh.get("client") and sh.get("server"):
+            try:
+                runs = [n.loopback_ceiling({"mode": "tcp", "object_bytes": wsize, "reads": max(3, min(8, steps)),
+                                            "ring_bytes": 4 << 20, "recv_cpus": sh["server"],
+                                            "send_cpus": sh["client"], "ring_pages": 1}) for _ in range(3)]
+                up_tcp = max(r["gbps"] for r in runs) * 1e9 / (1 << 20)
+            except Exception as e:  # noqa: BLE001 - the probe is a side measurement
+                cpu_split["upload_probe_error"] = str(e)[:160]
         s = sorted(lat)
         p50 = s[len(s) * 50 // 100] if s else 0.0
         p99 = s[min(len(s) - 1, len(s) * 99 // 100)] if s else 0.0
@@ -278,7 +293,8 @@ class SideBlocks:
             del client
             ep.stop()
         os.sched_setaffinity(0, saved_aff)
-        st = gdist.reduce_stats(self.ctx, elapsed=e1, nbytes=float(nbytes), p50=p50, p99=p99, ok=0.0 if err else 1.0)
+        st = gdist.reduce_stats(self.ctx, elapsed=e1, nbytes=float(nbytes), p50=p50, p99=p99, ok=0.0 if err else 1.0,
+                                upload_tcp=up_tcp)
         st["error"] = err
         st["slowest"] = [[i, round(v, 2)] for i, v in sorted(enumerate(lat), key=lambda x: -x[1])[:3]]
         st["slow_hip"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in n.slow_hip_calls().items()}

@@ -825,6 +825,14 @@ class RankBench(SideBlocks):
                 full[key] = dict(st)
                 continue
             b = self.full_block(key, st, extra)
+            if key == "write" and st.get("upload_tcp_min", 0.0) > 0:
+                # config 5's bound: one loopback TCP stream in the upload's
+                # direction and placement (write_block), per GPU
+                bmib = st["upload_tcp_min"] * max(1, world)
+                b.update({"bound": "tcp_upload", "bound_mib_s": round(bmib, 1),
+                          "frac_of_bound": round(b["mib_s"] / bmib, 3)})
+                full[key] = b
+                continue
             if ceil and ceil.get("ok"):
                 # the headline's placement: the run's best probe; one L3 domain: its own probe
                 tcp = (ceil.get("tcp_gbps_same", 0.0) if extra.get("_place") == "same"

@@ -429,6 +429,13 @@ class PyClient {
       whole = src.stable_until_done();
     }
     py::dict d = meta_dict(m);
+    const UploadPhases& ph = client_->last_upload();
+    py::dict p;
+    p["start_rpc_ms"] = ph.start_rpc_ns / 1e6;
+    p["first_send_ms"] = ph.first_send_ns / 1e6;
+    p["last_send_ms"] = ph.last_send_ns / 1e6;
+    p["response_ms"] = ph.response_ns / 1e6;
+    d["phases"] = p;
     d["gpu_crc32c"] = crc;
     d["staged_whole"] = whole;  // the whole object staged at once (zero-copy sends)
     d["gpu_message_crcs"] = range_crcs;  // upload messages whose CRC came from the GPU

@@ -362,10 +362,14 @@ class H2ServerConn {
         if (s.wmsg_len == 0) post_write_message(sp);
         continue;
       }
-      const uint32_t k = std::min(n, s.wmsg_len - s.wmsg_have);
-      bc_.read_exact(s.wmsg.get() + s.wmsg_have, k);
-      s.wmsg_have += k;
-      n -= k;
+      // whatever the socket holds now, not the whole frame (recv without
+      // MSG_WAITALL, as the client's readers): the thread copies as the bytes
+      // arrive instead of sleeping until a whole message is queued
+      const uint32_t want = std::min(n, s.wmsg_len - s.wmsg_have);
+      const size_t k = bc_.read_some(s.wmsg.get() + s.wmsg_have, want);
+      if (k == 0) throw StorageError("connection closed inside a WriteObject message", true);
+      s.wmsg_have += static_cast<uint32_t>(k);
+      n -= static_cast<uint32_t>(k);
       if (s.wmsg_have == s.wmsg_len) post_write_message(sp);
     }
   }

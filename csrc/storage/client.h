@@ -145,6 +145,14 @@ struct CallStats {
   std::atomic<uint64_t> requests{0}, retries{0}, bytes_in{0}, bytes_out{0}, dials{0};
 };
 
+// Where the last upload of a client went (steady-clock ns from its start;
+// 0 = not reached): the session's start RPC answered, the first and the last
+// content byte handed to the socket, the final response.  One uploading
+// thread per client (the bench's write block).
+struct UploadPhases {
+  int64_t start_rpc_ns = 0, first_send_ns = 0, last_send_ns = 0, response_ns = 0;
+};
+
 class StorageClient {
  public:
   virtual ~StorageClient() = default;
@@ -166,11 +174,13 @@ class StorageClient {
                           const WriteOptions& opt = {});
   const ClientConfig& config() const { return cfg_; }
   CallStats& stats() { return stats_; }
+  const UploadPhases& last_upload() const { return upload_; }
   virtual std::string transport_name() const = 0;
   // Network path actually used (gRPC: DirectPath vs CloudPath, see grpc_client.cc).
   virtual std::string transport_path() const { return "cloudpath"; }
 
  protected:
+  UploadPhases upload_;  // set by write_impl (gRPC)
   explicit StorageClient(ClientConfig cfg) : cfg_(std::move(cfg)) {}
   // One attempt; throws StorageError. `delivered` is incremented as bytes
   // are committed to the sink so the retry loop can resume.

@@ -750,6 +750,7 @@ class GrpcStorageClient : public StorageClient {
     const bool splice = src.stable_until_done();
     constexpr size_t kMinSplice = 64 << 10;  // below this a copy is cheaper than 2 syscalls
     c->start_stream(call, headers("WriteObject", bucket_res), false);
+    const int64_t t_base = upload_t0_;
     try {
       src.seek(from);
       uint64_t off = from;
@@ -790,6 +791,8 @@ class GrpcStorageClient : public StorageClient {
                           {parts.tail.data(), parts.tail.size()}};
           c->send_data_iov(*call, iov, 4, last);
         }
+        if (first && t_base) upload_.first_send_ns = now_ns() - t_base;
+        if (last && t_base) upload_.last_send_ns = now_ns() - t_base;
         off += k;
         first = false;
         if (last) break;
@@ -815,6 +818,7 @@ class GrpcStorageClient : public StorageClient {
       throw;
     }
     c->end_stream(*call, false);
+    if (t_base) upload_.response_ns = now_ns() - t_base;
     if (h.messages().empty()) throw StorageError("WriteObject: no response", true);
     v2::WriteStatus st;
     if (!v2::decode_write_status(h.messages().front(), &st) || !st.has_resource)
@@ -825,6 +829,8 @@ class GrpcStorageClient : public StorageClient {
   ObjectMeta write_impl(const std::string& bucket, const std::string& object, ByteSource& src,
                         const WriteOptions& opt) override {
     const std::string bres = v2::bucket_resource(bucket);
+    upload_ = UploadPhases();
+    upload_t0_ = now_ns();
     v2::WriteObjectSpec spec;
     spec.resource.name = object;
     spec.resource.bucket = bres;
@@ -846,6 +852,7 @@ class GrpcStorageClient : public StorageClient {
       });
       if (!v2::decode_upload_id(resp, &upload_id) || upload_id.empty())
         throw StorageError("StartResumableWrite: no upload_id", false);
+      upload_.start_rpc_ns = now_ns() - upload_t0_;
     }
     Backoff bo(cfg_.retry);
     int64_t t0 = now_ns();
@@ -872,6 +879,7 @@ class GrpcStorageClient : public StorageClient {
  private:
   H2ClientOptions opt_;
   int idle_ms_ = 0;
+  int64_t upload_t0_ = 0;  // steady clock of the current upload's start (UploadPhases)
   std::mutex mu_;
   std::vector<std::shared_ptr<H2ClientConn>> conns_;
   std::atomic<uint64_t> rr_{0};

@@ -209,6 +209,7 @@ class SideBlocks:
         args, n, torch, gdist = self.args, self.n, self.torch, self.gdist
         err = ""
         lat = []
+        phases = []  # per upload: where its time went (the client's UploadPhases)
         wsize = parse_size(args.write_size)
         chunk = parse_size(args.write_chunk)
         client = buf = None
@@ -259,6 +260,8 @@ class SideBlocks:
                     m = client.write_from_device(self.bucket, f"upload/rank{rank}_{i}", buf.data_ptr(), wsize, gpu,
                                                  True, chunk, parse_size(args.slot_bytes), args.slots)
                     lat.append((time.perf_counter() - t0) * 1e3)
+                    if m.get("phases"):
+                        phases.append(m["phases"])
                     # (SlicedWriter checks the composed CRC32C itself)
                     if m["size"] != wsize or (parts == 1 and m["crc32c"] != m["gpu_crc32c"]):
                         err = f"upload {i} not confirmed: {m}"
@@ -299,6 +302,10 @@ class SideBlocks:
         st["slowest"] = [[i, round(v, 2)] for i, v in sorted(enumerate(lat), key=lambda x: -x[1])[:3]]
         st["slow_hip"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in n.slow_hip_calls().items()}
         st["cpu_s_per_gib_by_thread"] = cpu_split
+        if phases:
+            # medians over the timed uploads: the start RPC, the first and
+            # last content byte sent, the final response (ms from the start)
+            st["phases_ms"] = {k: round(sorted(p[k] for p in phases)[len(phases) // 2], 3) for k in phases[0]}
         return st
 
     # --------------------------------------------------------------- fanout

@@ -411,22 +411,26 @@ class PyClient {
     uint64_t copies = 0, range_crcs = 0;
     uint32_t crc = 0;
     bool whole = false;
+    double done_ms = 0;
     {
       py::gil_scoped_release nogil;
       int64_t t0 = now_ns();
-      GpuByteSource src(device, reinterpret_cast<const void*>(dptr), n, slot_bytes, slots, true);
+      auto src = std::make_unique<GpuByteSource>(device, reinterpret_cast<const void*>(dptr), n, slot_bytes, slots,
+                                                 true);
       int64_t t1 = now_ns();
       WriteOptions o;
       o.resumable = resumable;
       o.chunk_bytes = chunk_bytes;
-      m = client_->write_object(bucket, name, src, o);
+      m = client_->write_object(bucket, name, *src, o);
       int64_t t2 = now_ns();
       crc_ms = (t1 - t0) / 1e6;
       upload_ms = (t2 - t1) / 1e6;
-      copies = src.copies();
-      range_crcs = src.gpu_range_crcs();
-      crc = src.crc32c();
-      whole = src.stable_until_done();
+      copies = src->copies();
+      range_crcs = src->gpu_range_crcs();
+      crc = src->crc32c();
+      whole = src->stable_until_done();
+      src.reset();  // staging drained and returned to the pool
+      done_ms = (now_ns() - t0) / 1e6;
     }
     py::dict d = meta_dict(m);
     const UploadPhases& ph = client_->last_upload();
@@ -435,6 +439,11 @@ class PyClient {
     p["first_send_ms"] = ph.first_send_ns / 1e6;
     p["last_send_ms"] = ph.last_send_ns / 1e6;
     p["response_ms"] = ph.response_ns / 1e6;
+    // around write_object: the source's setup before it (D2H staging
+    // started, buffers taken) and the whole call including the source's
+    // teardown after the response
+    p["setup_ms"] = crc_ms;
+    p["done_ms"] = done_ms;
     d["phases"] = p;
     d["gpu_crc32c"] = crc;
     d["staged_whole"] = whole;  // the whole object staged at once (zero-copy sends)

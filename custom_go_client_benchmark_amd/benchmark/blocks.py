@@ -281,12 +281,17 @@ class SideBlocks:
         # staging ring), the endpoint's cores receiving into a 2 x 2 MiB THP
         # buffer (as its WriteObject receive does); best of 3 probes
         up_tcp = 0.0
+        up_probe = {}
         if not err and parts == 1 and sh.get("client") and sh.get("server"):
             try:
                 runs = [n.loopback_ceiling({"mode": "tcp", "object_bytes": wsize, "reads": max(3, min(8, steps)),
                                             "ring_bytes": 4 << 20, "recv_cpus": sh["server"],
                                             "send_cpus": sh["client"], "ring_pages": 1}) for _ in range(3)]
-                up_tcp = max(r["gbps"] for r in runs) * 1e9 / (1 << 20)
+                best = max(runs, key=lambda r: r["gbps"])
+                up_tcp = best["gbps"] * 1e9 / (1 << 20)
+                # the probe's receiver against the endpoint's gcsb-srv-conn
+                up_probe = {"recv_cpu_s_per_gib": round(best["recv_cpu_s_per_gib"], 4),
+                            "send_cpu_s_per_gib": round(best["send_cpu_s_per_gib"], 4)}
             except Exception as e:  # noqa: BLE001 - the probe is a side measurement
                 cpu_split["upload_probe_error"] = str(e)[:160]
         s = sorted(lat)
@@ -302,6 +307,8 @@ class SideBlocks:
         st["slowest"] = [[i, round(v, 2)] for i, v in sorted(enumerate(lat), key=lambda x: -x[1])[:3]]
         st["slow_hip"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in n.slow_hip_calls().items()}
         st["cpu_s_per_gib_by_thread"] = cpu_split
+        if up_probe:
+            st["upload_probe"] = up_probe
         if phases:
             # medians over the timed uploads: the start RPC, the first and
             # last content byte sent, the final response (ms from the start)

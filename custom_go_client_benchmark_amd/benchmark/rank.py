@@ -685,8 +685,14 @@ class RankBench(SideBlocks):
             b["cpu_s_per_gib_by_thread"] = st["cpu_s_per_gib_by_thread"]
         if key.startswith("list_read_"):
             b["list_ms"] = round(st["list_ms_max"], 3)
+            if "host_p50_max" in st:
+                # the read's last byte on the host (the reference's stop
+                # point); p50_ms - this = the GPU tail (last H2D copy + CRC)
+                b["host_landed_p50_ms"] = round(st["host_p50_max"], 3)
         if st.get("phases_ms"):
             b["phases_ms"] = st["phases_ms"]
+        if st.get("upload_probe"):
+            b["upload_probe"] = st["upload_probe"]
         if key == "sliced":
             b["host_landed_p50_ms"] = round(st["host_p50_max"], 3)
             b["slice_skew_ms"] = round(st["skew_max"], 3)

@@ -106,6 +106,7 @@ Runner::Runner(RunnerConfig cfg) : cfg_(std::move(cfg)) {
   if (cfg_.conn_ring && cfg_.sink == "gpu" && one_conn && cfg_.workers > 1 && cfg_.slices <= 1 && g.verify &&
       g.landing == Landing::kObject && g.stage == GpuSinkConfig::Stage::kH2D)
     conn_ring_ = std::make_unique<ConnRing>(g.device, cfg_.conn_ring_slot_bytes, cfg_.conn_ring_slots);
+  overlap_ = cfg_.overlap_finish && cfg_.sink == "gpu" && cfg_.slices <= 1 && !conn_ring_ && !cfg_.read_diag;
   client_ = make_client(cfg_.client);
 }
 
@@ -119,6 +120,80 @@ Runner::~Runner() {
   run_cv_.notify_all();
   for (auto& t : threads_)
     if (t.joinable()) t.join();
+  for (auto& f : fin_) {
+    if (!f) continue;
+    {
+      std::lock_guard<std::mutex> lk(f->mu);
+      f->stop = true;
+    }
+    f->cv.notify_all();
+    if (f->th.joinable()) f->th.join();
+  }
+}
+
+namespace {
+void add_gpu_stats(GpuSinkStats& t, const GpuSinkStats& g) {
+  t.slots_submitted += g.slots_submitted;
+  t.segments += g.segments;
+  t.chunks_verified_gpu += g.chunks_verified_gpu;
+  t.chunks_verified_host += g.chunks_verified_host;
+  t.objects_verified += g.objects_verified;
+  t.slot_waits += g.slot_waits;
+  t.slot_wait_s += g.slot_wait_s;
+  t.flag_reuses += g.flag_reuses;
+  t.handoff_s += g.handoff_s;
+}
+}  // namespace
+
+void Runner::finisher_loop(int w) {
+  pin_current_thread(cfg_.client.cpus);
+  name_current_thread("gcsb-worker");  // accounted with the workers
+  Finisher& f = *fin_[w];
+  std::unique_lock<std::mutex> lk(f.mu);
+  for (;;) {
+    f.cv.wait(lk, [&] { return f.stop || f.has; });
+    if (!f.has) return;
+    GpuSink* s = f.sink;
+    ReadRecord r = std::move(f.r);
+    ReadResult rr = std::move(f.rr);
+    lk.unlock();
+    bool ok = true;
+    try {
+      rr.sink = s->finish();
+    } catch (const std::exception& e) {
+      r.error = e.what();
+      ok = false;
+    }
+    r.end_ns = now_ns();
+    const bool good = conclude(std::move(r), rr, ok);
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      last_landed_[w] = s;
+    }
+    if (!good && cfg_.stop_on_error) stop_flag_ = true;
+    lk.lock();
+    f.has = false;
+    f.cv.notify_all();
+  }
+}
+
+void Runner::finisher_post(int w, GpuSink* sink, ReadRecord&& r, ReadResult&& rr) {
+  Finisher& f = *fin_[w];
+  std::unique_lock<std::mutex> lk(f.mu);
+  // at most one read waits on its GPU tail: the one on the other sink
+  f.cv.wait(lk, [&] { return !f.has; });
+  f.sink = sink;
+  f.r = std::move(r);
+  f.rr = std::move(rr);
+  f.has = true;
+  lk.unlock();
+  f.cv.notify_all();
+}
+
+void Runner::finisher_drain(int w) {
+  Finisher& f = *fin_[w];
+  std::unique_lock<std::mutex> lk(f.mu);
+  f.cv.wait(lk, [&] { return !f.has; });
 }
 
 std::string Runner::object_for(int worker, int64_t seq) const {
@@ -133,6 +208,11 @@ std::string Runner::object_for(int worker, int64_t seq) const {
 uintptr_t Runner::landing_ptr(int w) const {
   if (w < 0 || w >= static_cast<int>(sinks_.size())) return 0;
   if (landing_[w]) return reinterpret_cast<uintptr_t>(landing_[w]->data());
+  if (overlap_) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (w < static_cast<int>(last_landed_.size()) && last_landed_[w])
+      return reinterpret_cast<uintptr_t>(last_landed_[w]->object_device_ptr());
+  }
   if (gpu_sinks_[w]) return reinterpret_cast<uintptr_t>(gpu_sinks_[w]->object_device_ptr());
   return 0;
 }
@@ -174,6 +254,8 @@ void Runner::reset_stats() {
   // the sinks live across phases: their counters restart with the timed reads
   for (GpuSink* g : gpu_sinks_)
     if (g) g->reset_stats();
+  for (auto& g : sinks_b_)
+    if (g) g->reset_stats();
   if (cfg_.sink == "gpu")
     for (auto& sr : sliced_)
       if (sr)
@@ -190,6 +272,11 @@ void Runner::start() {
     gpu_stats_.assign(cfg_.workers, GpuSinkStats{});
     sliced_.resize(cfg_.workers);
     landing_.resize(cfg_.workers);
+    if (overlap_) {
+      sinks_b_.resize(cfg_.workers);
+      fin_.resize(cfg_.workers);
+      last_landed_.assign(cfg_.workers, nullptr);
+    }
   }
   {
     std::lock_guard<std::mutex> lk(ctl_mu_);
@@ -323,6 +410,11 @@ void Runner::worker_main(int w) {
         auto g = std::make_unique<GpuSink>(gc);
         gpu_sinks_[w] = g.get();
         sinks_[w] = std::move(g);
+        if (overlap_) {
+          sinks_b_[w] = std::make_unique<GpuSink>(gc);
+          fin_[w] = std::make_unique<Finisher>();
+          fin_[w]->th = std::thread([this, w] { finisher_loop(w); });
+        }
       } else {
         // multiplexed gRPC: host CRC on the worker thread, not the connection's reader
         sinks_[w] = std::make_unique<DiscardSink>(cfg_.client.read_chunk, cfg_.host_crc, defer_host_crc(cfg_.client),
@@ -379,71 +471,77 @@ void Runner::worker_main(int w) {
     SchedSample diag0;
     if (cfg_.read_diag) diag0 = sched_sample_offcore(kDiagThreads, diag_avoid);
     RoctxRange rg(sliced ? "gcsb.read_object(sliced)" : "gcsb.read_object");
+    // overlap_finish: this read's sink (the two alternate); its GPU tail is
+    // the finisher's, and the loop goes on to the next read
+    GpuSink* osink = overlap_ && gsink ? ((i & 1) ? sinks_b_[w].get() : gsink) : nullptr;
     r.start_wall_ns = wall_ns();
     r.start_ns = now_ns();
-    double ms = 0, host_ms = 0;
+    ReadResult rr;
+    bool ok = true;
     try {
-      ReadResult rr = sliced ? sliced->read(cfg_.bucket, r.object, &stop_flag_)
-                             : client_->read_object(cfg_.bucket, r.object, *sink, cfg_.range_offset,
-                                                    cfg_.range_limit, &stop_flag_);
-      r.end_ns = now_ns();
-      r.ttfb_ns = rr.first_byte_ns;
-      r.host_done_ns = rr.host_done_ns;
-      r.bytes = rr.bytes;
-      r.attempts = rr.attempts;
-      r.verified = rr.sink.verified;
-      r.ok = !rr.sink.crc_mismatch;
-      if (!r.ok) r.error = "while reading and discarding content: " + rr.sink.detail;
-      if (r.ok && rr.info.size >= 0 && cfg_.range_limit < 0 && cfg_.range_offset == 0 &&
-          rr.bytes != static_cast<uint64_t>(rr.info.size)) {
-        r.ok = false;
-        r.error = "short read: " + std::to_string(rr.bytes) + " of " + std::to_string(rr.info.size) + " bytes";
-      }
+      rr = sliced ? sliced->read(cfg_.bucket, r.object, &stop_flag_)
+                  : client_->read_object(cfg_.bucket, r.object, osink ? *osink : *sink, cfg_.range_offset,
+                                         cfg_.range_limit, &stop_flag_, 0, /*defer_finish=*/osink != nullptr);
     } catch (const StorageError& e) {
-      r.end_ns = now_ns();
       r.error = std::string("while creating reader object: ") + e.what();
+      ok = false;
     } catch (const std::exception& e) {
-      r.end_ns = now_ns();
       r.error = e.what();
+      ok = false;
     }
+    if (osink && ok) {
+      finisher_post(w, osink, std::move(r), std::move(rr));
+      continue;
+    }
+    r.end_ns = now_ns();
     if (cfg_.read_diag)
       r.diag = std::make_shared<ReadSchedDiag>(sched_delta(diag0, sched_sample_offcore(kDiagThreads, diag_avoid)));
-    ms = (r.end_ns - r.start_ns) / 1e6;
-    host_ms = r.host_done_ns ? (r.host_done_ns - r.start_ns) / 1e6 : ms;
-    if (r.ok && cfg_.latency_fd >= 0) {
-      char line[64];
-      int n = std::snprintf(line, sizeof(line), "%.3fms\n", ms);
-      std::lock_guard<std::mutex> lk(out_mu_);
-      ssize_t wr = ::write(cfg_.latency_fd, line, static_cast<size_t>(n));
-      (void)wr;
-    }
-    bool ok = r.ok;
-    record(std::move(r), ms, host_ms);
-    if (!ok && cfg_.stop_on_error) {
+    if (!conclude(std::move(r), rr, ok) && cfg_.stop_on_error) {
       stop_flag_ = true;
       break;
     }
   }
+  if (overlap_ && gsink) finisher_drain(w);
   if (gsink) {
+    GpuSinkStats t = gsink->stats();
+    if (overlap_ && sinks_b_[w]) add_gpu_stats(t, sinks_b_[w]->stats());
     std::lock_guard<std::mutex> lk(mu_);
-    gpu_stats_[w] = gsink->stats();
+    gpu_stats_[w] = t;
   } else if (sliced && cfg_.sink == "gpu") {
     GpuSinkStats t;
-    for (int i = 0; i < sliced->num_sinks(); ++i) {
-      const GpuSinkStats& g = static_cast<GpuSink&>(sliced->sink(i)).stats();
-      t.slots_submitted += g.slots_submitted;
-      t.segments += g.segments;
-      t.chunks_verified_gpu += g.chunks_verified_gpu;
-      t.chunks_verified_host += g.chunks_verified_host;
-      t.objects_verified += g.objects_verified;
-      t.slot_waits += g.slot_waits;
-      t.slot_wait_s += g.slot_wait_s;
-      t.flag_reuses += g.flag_reuses;
-      t.handoff_s += g.handoff_s;
-    }
+    for (int i = 0; i < sliced->num_sinks(); ++i) add_gpu_stats(t, static_cast<GpuSink&>(sliced->sink(i)).stats());
     std::lock_guard<std::mutex> lk(mu_);
     gpu_stats_[w] = t;
   }
+}
+
+bool Runner::conclude(ReadRecord&& r, const ReadResult& rr, bool ok_so_far) {
+  if (ok_so_far) {
+    r.ttfb_ns = rr.first_byte_ns;
+    r.host_done_ns = rr.host_done_ns;
+    r.bytes = rr.bytes;
+    r.attempts = rr.attempts;
+    r.verified = rr.sink.verified;
+    r.ok = !rr.sink.crc_mismatch;
+    if (!r.ok) r.error = "while reading and discarding content: " + rr.sink.detail;
+    if (r.ok && rr.info.size >= 0 && cfg_.range_limit < 0 && cfg_.range_offset == 0 &&
+        rr.bytes != static_cast<uint64_t>(rr.info.size)) {
+      r.ok = false;
+      r.error = "short read: " + std::to_string(rr.bytes) + " of " + std::to_string(rr.info.size) + " bytes";
+    }
+  }
+  const double ms = (r.end_ns - r.start_ns) / 1e6;
+  const double host_ms = r.host_done_ns ? (r.host_done_ns - r.start_ns) / 1e6 : ms;
+  if (r.ok && cfg_.latency_fd >= 0) {
+    char line[64];
+    int n = std::snprintf(line, sizeof(line), "%.3fms\n", ms);
+    std::lock_guard<std::mutex> lk(out_mu_);
+    ssize_t wr = ::write(cfg_.latency_fd, line, static_cast<size_t>(n));
+    (void)wr;
+  }
+  const bool ok = r.ok;
+  record(std::move(r), ms, host_ms);
+  return ok;
 }
 
 std::vector<ReadRecord> Runner::drain() {

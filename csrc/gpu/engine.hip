@@ -1525,13 +1525,15 @@ void crc_block_put(int device, const CrcScratchBlock& b) {
 }
 }  // namespace
 
-GpuByteSource::GpuByteSource(int device, const void* dptr, uint64_t n, size_t slot_bytes, int slots, bool gpu_crc)
+GpuByteSource::GpuByteSource(int device, const void* dptr, uint64_t n, size_t slot_bytes, int slots, bool gpu_crc,
+                             bool async_stage)
     : device_(device),
       src_(static_cast<const uint8_t*>(dptr)),
       n_(n),
       // a ring slot never larger than the (part of the) object it stages
       slot_bytes_(std::max<size_t>(std::min<uint64_t>(slot_bytes, (n + 65535) / 65536 * 65536), 65536)),
       nslots_(std::max(2, slots)) {
+  async_stage_ = async_stage;
   if (n_ <= kWholeRingMax)
     nslots_ = std::max<int>(nslots_, static_cast<int>((n_ + slot_bytes_ - 1) / slot_bytes_));
   hip_check(hipSetDevice(device_), "hipSetDevice");
@@ -1630,6 +1632,7 @@ uint32_t GpuByteSource::crc32c() const {
   if (!has_crc_) return 0;
   if (crc_done_) return crc_;
   if (chunks_known_ < chunk_crc_.size()) {
+    await_async();
     // asked before the upload staged every slot: collect what is in flight
     for (int i = 0; i < nslots_; ++i)
       if (!slot_harvested_[i] && slot_off_[i] != ~0ull) {
@@ -1664,8 +1667,21 @@ GpuByteSource::~GpuByteSource() {
   if (own_stream_) (void)hipStreamDestroy(own_stream_);
 }
 
+void GpuByteSource::await_async() const {
+  std::unique_lock<std::mutex> lk(amu_);
+  acv_.wait(lk, [&] { return !async_busy_; });
+}
+
+void GpuByteSource::await_issued(int slot) const {
+  if (issued_.load(std::memory_order_acquire) > slot) return;
+  std::unique_lock<std::mutex> lk(amu_);
+  acv_.wait(lk, [&] { return issued_.load(std::memory_order_acquire) > slot || !async_busy_; });
+  if (!async_err_.empty()) throw std::runtime_error("GpuByteSource: staging on the submitter: " + async_err_);
+}
+
 // This source's queued copies (its slot events; the pool streams are shared).
 void GpuByteSource::wait_all() {
+  await_async();
   hip_check(hipSetDevice(device_), "hipSetDevice");
   for (int i = 0; i < nslots_; ++i)
     if (slot_off_[i] != ~0ull) {
@@ -1703,7 +1719,7 @@ void GpuByteSource::issue(int slot, uint64_t off) {
   const int64_t t2 = now_ns();
   hip_check(hipEventRecord(ev_[slot], st_[slot]), "hipEventRecord");
   note_hip_call("hipEventRecord(D2H)", st_idx_[slot], t2, now_ns());
-  ++copies_;
+  copies_.fetch_add(1, std::memory_order_relaxed);
 }
 
 void GpuByteSource::restart(uint64_t off) {
@@ -1713,10 +1729,47 @@ void GpuByteSource::restart(uint64_t off) {
   next_issue_ = base;
   cur_ = 0;
   slot_off_.assign(nslots_, ~0ull);
-  for (int i = 0; i < nslots_ && next_issue_ < n_; ++i) {
+  async_err_.clear();
+  // the whole object in one ring, staged from its start: no slot is ever
+  // refilled, so the submitter can issue every slot past the first few
+  // while this thread already sends (next() waits per slot on issued_)
+  const bool whole = async_stage_ && base == 0 && stable_until_done() && nslots_ > kSyncSlots;
+  int i = 0;
+  for (; i < nslots_ && next_issue_ < n_ && (!whole || i < kSyncSlots); ++i) {
     issue(i, next_issue_);
     next_issue_ += slot_bytes_;
   }
+  if (!whole || next_issue_ >= n_) {
+    issued_.store(nslots_, std::memory_order_release);
+    return;
+  }
+  issued_.store(i, std::memory_order_release);
+  {
+    std::lock_guard<std::mutex> lk(amu_);
+    async_busy_ = true;
+  }
+  const int first = i;
+  const uint64_t from = next_issue_;
+  next_issue_ = n_;  // every slot is (being) issued
+  DeviceSubmitter::get(device_).post([this, first, from] {
+    std::string err;
+    try {
+      uint64_t o = from;
+      for (int s = first; s < nslots_ && o < n_; ++s, o += slot_bytes_) {
+        issue(s, o);
+        issued_.store(s + 1, std::memory_order_release);
+        { std::lock_guard<std::mutex> lk(amu_); }  // a waiter between its check and its wait sees this
+        acv_.notify_all();
+      }
+    } catch (const std::exception& e) {
+      err = e.what();
+    }
+    std::lock_guard<std::mutex> lk(amu_);
+    async_err_ = err;
+    async_busy_ = false;
+    issued_.store(err.empty() ? nslots_ : issued_.load(), std::memory_order_release);
+    acv_.notify_all();
+  });
 }
 
 void GpuByteSource::seek(uint64_t off) {
@@ -1726,6 +1779,7 @@ void GpuByteSource::seek(uint64_t off) {
 
 std::pair<const uint8_t*, size_t> GpuByteSource::next(size_t max) {
   if (pos_ >= n_ || max == 0) return {nullptr, 0};
+  await_issued(cur_);
   // slot cur_ holds [slot_off_, slot_off_ + len) and pos_ lies inside it
   if (slot_off_[cur_] == ~0ull || pos_ >= slot_off_[cur_] + slot_len_[cur_]) {
     // the consumer moved past this slot: refill it far ahead, advance
@@ -1734,6 +1788,7 @@ std::pair<const uint8_t*, size_t> GpuByteSource::next(size_t max) {
       next_issue_ += slot_bytes_;
     }
     cur_ = (cur_ + 1) % nslots_;
+    await_issued(cur_);
   }
   hip_check(hipSetDevice(device_), "hipSetDevice");
   hip_check(hipEventSynchronize(ev_[cur_]), "hipEventSynchronize");

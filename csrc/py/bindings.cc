@@ -221,7 +221,8 @@ struct PySlicedWriter {
     return meta_dict(m);
   }
   py::dict write_from_device(const std::string& bucket, const std::string& name, uintptr_t dptr, uint64_t n,
-                             int device, bool resumable, size_t chunk_bytes, size_t slot_bytes, int slots) {
+                             int device, bool resumable, size_t chunk_bytes, size_t slot_bytes, int slots,
+                             bool async_stage) {
     ObjectMeta m;
     double ms = 0;
     {
@@ -233,7 +234,8 @@ struct PySlicedWriter {
       const int64_t t0 = now_ns();
       m = writer->write(bucket, name, n,
                         [=](int, uint64_t off, uint64_t len) -> std::unique_ptr<ByteSource> {
-                          return std::make_unique<GpuByteSource>(device, base + off, len, slot_bytes, slots, true);
+                          return std::make_unique<GpuByteSource>(device, base + off, len, slot_bytes, slots, true,
+                                                                 async_stage);
                         },
                         o);
       ms = (now_ns() - t0) / 1e6;
@@ -405,7 +407,8 @@ class PyClient {
 
   // Write path (config 5): object bytes in HBM -> pinned ring (D2H) -> upload.
   py::dict write_from_device(const std::string& bucket, const std::string& name, uintptr_t dptr, uint64_t n,
-                             int device, bool resumable, size_t chunk_bytes, size_t slot_bytes, int slots) {
+                             int device, bool resumable, size_t chunk_bytes, size_t slot_bytes, int slots,
+                             bool async_stage) {
     ObjectMeta m;
     double crc_ms = 0, upload_ms = 0;
     uint64_t copies = 0, range_crcs = 0;
@@ -416,7 +419,7 @@ class PyClient {
       py::gil_scoped_release nogil;
       int64_t t0 = now_ns();
       auto src = std::make_unique<GpuByteSource>(device, reinterpret_cast<const void*>(dptr), n, slot_bytes, slots,
-                                                 true);
+                                                 true, async_stage);
       int64_t t1 = now_ns();
       WriteOptions o;
       o.resumable = resumable;
@@ -433,7 +436,7 @@ class PyClient {
       done_ms = (now_ns() - t0) / 1e6;
     }
     py::dict d = meta_dict(m);
-    const UploadPhases& ph = client_->last_upload();
+    const UploadPhases ph = client_->last_upload();
     py::dict p;
     p["start_rpc_ms"] = ph.start_rpc_ns / 1e6;
     p["first_send_ms"] = ph.first_send_ns / 1e6;
@@ -510,6 +513,7 @@ class PyRunner {
     c.conn_ring = get_or<bool>(d, "conn_ring", c.conn_ring);
     c.conn_ring_slot_bytes = get_or<size_t>(d, "conn_ring_slot_bytes", c.conn_ring_slot_bytes);
     c.conn_ring_slots = get_or<int>(d, "conn_ring_slots", c.conn_ring_slots);
+    c.overlap_finish = get_or<bool>(d, "overlap_finish", c.overlap_finish);
     if (d.contains("diag_avoid_cpus") && !d["diag_avoid_cpus"].is_none())
       c.diag_avoid_cpus = d["diag_avoid_cpus"].cast<std::vector<int>>();
     c.stop_on_error = get_or<bool>(d, "stop_on_error", true);
@@ -1124,7 +1128,8 @@ PYBIND11_MODULE(_native, m) {
            py::arg("resumable") = true, py::arg("chunk_bytes") = 16u << 20)
       .def("write_from_device", &PySlicedWriter::write_from_device, py::arg("bucket"), py::arg("name"),
            py::arg("dptr"), py::arg("n"), py::arg("device") = 0, py::arg("resumable") = true,
-           py::arg("chunk_bytes") = 16u << 20, py::arg("slot_bytes") = 8u << 20, py::arg("slots") = 4);
+           py::arg("chunk_bytes") = 16u << 20, py::arg("slot_bytes") = 8u << 20, py::arg("slots") = 4,
+           py::arg("async_stage") = true);
 
   py::class_<PySlicedGpuReader>(m, "SlicedGpuReader")
       .def(py::init<const py::dict&>())
@@ -1165,7 +1170,7 @@ PYBIND11_MODULE(_native, m) {
            py::arg("resumable") = true, py::arg("chunk_bytes") = 16u << 20)
       .def("write_from_device", &PyClient::write_from_device, py::arg("bucket"), py::arg("name"), py::arg("dptr"),
            py::arg("n"), py::arg("device") = 0, py::arg("resumable") = true, py::arg("chunk_bytes") = 16u << 20,
-           py::arg("slot_bytes") = 8u << 20, py::arg("slots") = 4)
+           py::arg("slot_bytes") = 8u << 20, py::arg("slots") = 4, py::arg("async_stage") = true)
       .def("compose", &PyClient::compose, py::arg("bucket"), py::arg("dest"), py::arg("sources"),
            py::arg("content_type") = "")
       .def("delete", &PyClient::remove)

@@ -12,6 +12,7 @@
 #include <cstdint>
 #include <functional>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -145,10 +146,11 @@ struct CallStats {
   std::atomic<uint64_t> requests{0}, retries{0}, bytes_in{0}, bytes_out{0}, dials{0};
 };
 
-// Where the last upload of a client went (steady-clock ns from its start;
-// 0 = not reached): the session's start RPC answered, the first and the last
-// content byte handed to the socket, the final response.  One uploading
-// thread per client (the bench's write block).
+// Where an upload's time went (steady-clock ns from its start; 0 = not
+// reached): the session's start RPC answered, the first and the last content
+// byte handed to the socket, the final response.  Each upload fills its own
+// and publishes it when it returns (StorageClient::last_upload): a client
+// shared by uploading threads reports the last one to finish.
 struct UploadPhases {
   int64_t start_rpc_ns = 0, first_send_ns = 0, last_send_ns = 0, response_ns = 0;
 };
@@ -174,13 +176,19 @@ class StorageClient {
                           const WriteOptions& opt = {});
   const ClientConfig& config() const { return cfg_; }
   CallStats& stats() { return stats_; }
-  const UploadPhases& last_upload() const { return upload_; }
+  UploadPhases last_upload() const {
+    std::lock_guard<std::mutex> lk(upload_mu_);
+    return upload_;
+  }
   virtual std::string transport_name() const = 0;
   // Network path actually used (gRPC: DirectPath vs CloudPath, see grpc_client.cc).
   virtual std::string transport_path() const { return "cloudpath"; }
 
  protected:
-  UploadPhases upload_;  // set by write_impl (gRPC)
+  void set_last_upload(const UploadPhases& p) {
+    std::lock_guard<std::mutex> lk(upload_mu_);
+    upload_ = p;
+  }
   explicit StorageClient(ClientConfig cfg) : cfg_(std::move(cfg)) {}
   // One attempt; throws StorageError. `delivered` is incremented as bytes
   // are committed to the sink so the retry loop can resume.
@@ -198,6 +206,10 @@ class StorageClient {
   auto with_retry(F&& f, const volatile bool* cancel = nullptr) -> decltype(f());
   ClientConfig cfg_;
   CallStats stats_;
+
+ private:
+  mutable std::mutex upload_mu_;
+  UploadPhases upload_;  // the last finished upload's (gRPC write_impl)
 };
 
 bool should_retry(const RetryPolicy& p, const StorageError& e, int attempt, int64_t t0);

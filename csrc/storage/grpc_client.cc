@@ -739,7 +739,7 @@ class GrpcStorageClient : public StorageClient {
   // the last one carries the object's checksums, asked of the source only
   // then (a GPU source knows them once every slot was staged).
   ObjectMeta write_stream(const std::string& bucket_res, const std::string& upload_id, const std::string* spec,
-                          ByteSource& src, uint64_t from) {
+                          ByteSource& src, uint64_t from, UploadPhases* ph = nullptr, int64_t t_base = 0) {
     const uint64_t total = src.size();
     const size_t kMsg = 2u << 20;  // ServiceConstants MAX_WRITE_CHUNK_BYTES [lib]
     BufferingHandler h;
@@ -750,7 +750,6 @@ class GrpcStorageClient : public StorageClient {
     const bool splice = src.stable_until_done();
     constexpr size_t kMinSplice = 64 << 10;  // below this a copy is cheaper than 2 syscalls
     c->start_stream(call, headers("WriteObject", bucket_res), false);
-    const int64_t t_base = upload_t0_;
     try {
       src.seek(from);
       uint64_t off = from;
@@ -791,8 +790,8 @@ class GrpcStorageClient : public StorageClient {
                           {parts.tail.data(), parts.tail.size()}};
           c->send_data_iov(*call, iov, 4, last);
         }
-        if (first && t_base) upload_.first_send_ns = now_ns() - t_base;
-        if (last && t_base) upload_.last_send_ns = now_ns() - t_base;
+        if (first && ph) ph->first_send_ns = now_ns() - t_base;
+        if (last && ph) ph->last_send_ns = now_ns() - t_base;
         off += k;
         first = false;
         if (last) break;
@@ -818,7 +817,7 @@ class GrpcStorageClient : public StorageClient {
       throw;
     }
     c->end_stream(*call, false);
-    if (t_base) upload_.response_ns = now_ns() - t_base;
+    if (ph) ph->response_ns = now_ns() - t_base;
     if (h.messages().empty()) throw StorageError("WriteObject: no response", true);
     v2::WriteStatus st;
     if (!v2::decode_write_status(h.messages().front(), &st) || !st.has_resource)
@@ -829,8 +828,13 @@ class GrpcStorageClient : public StorageClient {
   ObjectMeta write_impl(const std::string& bucket, const std::string& object, ByteSource& src,
                         const WriteOptions& opt) override {
     const std::string bres = v2::bucket_resource(bucket);
-    upload_ = UploadPhases();
-    upload_t0_ = now_ns();
+    // this upload's phases, published however it returns
+    struct Phases {
+      GrpcStorageClient* self;
+      UploadPhases ph;
+      const int64_t t0 = now_ns();
+      ~Phases() { self->set_last_upload(ph); }
+    } up{this, {}};
     v2::WriteObjectSpec spec;
     spec.resource.name = object;
     spec.resource.bucket = bres;
@@ -838,7 +842,7 @@ class GrpcStorageClient : public StorageClient {
     spec.object_size = static_cast<int64_t>(src.size());
     if (!opt.resumable) {
       const std::string sp = v2::encode_write_spec(spec);
-      return with_retry([&] { return write_stream(bres, "", &sp, src, 0); });
+      return with_retry([&] { return write_stream(bres, "", &sp, src, 0, &up.ph, up.t0); });
     }
     std::string upload_id;
     {
@@ -852,14 +856,14 @@ class GrpcStorageClient : public StorageClient {
       });
       if (!v2::decode_upload_id(resp, &upload_id) || upload_id.empty())
         throw StorageError("StartResumableWrite: no upload_id", false);
-      upload_.start_rpc_ns = now_ns() - upload_t0_;
+      up.ph.start_rpc_ns = now_ns() - up.t0;
     }
     Backoff bo(cfg_.retry);
     int64_t t0 = now_ns();
     uint64_t from = 0;
     for (int attempt = 1;; ++attempt) {
       try {
-        return write_stream(bres, upload_id, nullptr, src, from);
+        return write_stream(bres, upload_id, nullptr, src, from, &up.ph, up.t0);
       } catch (const StorageError& e) {
         if (!should_retry(cfg_.retry, e, attempt, t0)) throw;
         ++stats_.retries;
@@ -879,7 +883,6 @@ class GrpcStorageClient : public StorageClient {
  private:
   H2ClientOptions opt_;
   int idle_ms_ = 0;
-  int64_t upload_t0_ = 0;  // steady clock of the current upload's start (UploadPhases)
   std::mutex mu_;
   std::vector<std::shared_ptr<H2ClientConn>> conns_;
   std::atomic<uint64_t> rr_{0};

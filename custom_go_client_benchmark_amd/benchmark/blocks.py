@@ -211,6 +211,7 @@ class SideBlocks:
         lat = []
         phases = []  # per upload: where its time went (the client's UploadPhases)
         wsize = parse_size(args.write_size)
+        astage = getattr(args, "write_async_stage", "on") == "on"
         chunk = parse_size(args.write_chunk)
         client = buf = None
         ep = None
@@ -244,7 +245,7 @@ class SideBlocks:
             n.gpu_fill_pattern(gpu, buf.data_ptr(), wsize, f"upload/rank{rank}", 0)
             for i in range(warmup):
                 client.write_from_device(self.bucket, f"upload/warmup_{rank}_{i}", buf.data_ptr(), wsize, gpu, True,
-                                         chunk, parse_size(args.slot_bytes), args.slots)
+                                         chunk, parse_size(args.slot_bytes), args.slots, astage)
         except Exception as e:  # noqa: BLE001
             err = f"{type(e).__name__}: {e}"
         gdist.barrier(self.ctx, "R1 write start barrier")
@@ -258,7 +259,7 @@ class SideBlocks:
                 for i in range(steps):
                     t0 = time.perf_counter()
                     m = client.write_from_device(self.bucket, f"upload/rank{rank}_{i}", buf.data_ptr(), wsize, gpu,
-                                                 True, chunk, parse_size(args.slot_bytes), args.slots)
+                                                 True, chunk, parse_size(args.slot_bytes), args.slots, astage)
                     lat.append((time.perf_counter() - t0) * 1e3)
                     if m.get("phases"):
                         phases.append(m["phases"])
@@ -432,7 +433,8 @@ class SideBlocks:
         over = {"protocol": proto, "endpoint": ep.url if ep is not None else "", "workers": workers,
                 "object_names": names or [f"c3_rank{rank}/file_0"], "cpus": sh["client"], "worker_id_offset": 0,
                 "rcvbuf": parse_size(args.list_rcvbuf), "ring_slots": int(lslots), "ring_slot_bytes": parse_size(lbytes),
-                "ring_wc": args.list_ring_wc == "on", "reader_cpus": sh.get("reader_cpus")}
+                "ring_wc": args.list_ring_wc == "on", "reader_cpus": sh.get("reader_cpus"),
+                "overlap_finish": args.list_overlap == "on"}
         if extra:
             over.update(extra)
         st = self.read_block(over, per_pass, per_pass * warmup_passes, f"{proto} list-read", endpoint=ep)

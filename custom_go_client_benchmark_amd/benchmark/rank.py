@@ -71,7 +71,24 @@ FIXED = {
     "mux_send": "isolate",        # multiplexed blocks: the endpoint send thread and the
     "mux_reader": "isolate",      # connection reader on physical cores of their own (r5_muxiso)
     "client_cc": "cubic",         # client sockets' congestion control, set before connect (r4_recvcost)
+    "list_overlap": "on",         # config 3 over HTTP: next read starts at host landing (RunnerConfig::overlap_finish)
+    "write_async_stage": "on",    # config 5: staging past the first slots issued on the submitter (r6_e)
 }
+
+
+def fixed_overrides(env: str | None) -> dict:
+    """GCSB_FIXED="key=value,key=value": experiments override FIXED values
+    (A/B sessions) without a bench flag each; unknown keys are an error."""
+    out = {}
+    for item in (env or "").split(","):
+        if not item.strip():
+            continue
+        k, sep, v = item.partition("=")
+        k = k.strip()
+        if not sep or k not in FIXED:
+            raise SystemExit(f"GCSB_FIXED: unknown or malformed item {item!r} (keys: {', '.join(FIXED)})")
+        out[k] = type(FIXED[k])(v.strip())
+    return out
 
 
 class RankBench(SideBlocks):
@@ -91,7 +108,8 @@ class RankBench(SideBlocks):
         self.affinity = affinity
         self.gdist = gdist
         self.n = pkg._native
-        for k, v in FIXED.items():
+        fixed = {**FIXED, **fixed_overrides(os.environ.get("GCSB_FIXED"))}
+        for k, v in fixed.items():
             if not hasattr(args, k):
                 setattr(args, k, v)
         self.rank, self.world, self.local_rank = gdist.env_rank()

@@ -54,12 +54,15 @@ def test_copy_ceiling(native, gpu_available, direction):
     assert 10.0 < r["gbps"] < 100.0, r
 
 
+@pytest.mark.parametrize("async_stage", [True, False])
+@pytest.mark.parametrize("slot", [(1 << 20), (2 << 20)])
 @pytest.mark.parametrize("size", [(64 << 20), (5 << 20) + 4321])
-def test_spliced_upload_from_hbm_is_byte_exact(native, server, gpu_available, size):
+def test_spliced_upload_from_hbm_is_byte_exact(native, server, gpu_available, size, slot, async_stage):
     """Uploads from HBM stage the whole object (no slot refilled mid-upload)
     and hand the staged pages to the socket by reference (vmsplice +
     splice); the endpoint's CRC32C of what it received must equal the GPU's,
-    and a read-back must match the HBM bytes."""
+    and a read-back must match the HBM bytes.  async_stage: slots past the
+    first two are issued on the device submitter while the upload sends."""
     import torch
 
     srv = native.Server({"port": 0, "retain_uploads": True})
@@ -71,8 +74,9 @@ def test_spliced_upload_from_hbm_is_byte_exact(native, server, gpu_available, si
             c = native.Client({"protocol": proto, "endpoint": srv.url})
             for i in range(3):  # the pinned staging ring is recycled between uploads
                 name = f"splice/{size}_{i}"
-                m = c.write_from_device(B, name, t.data_ptr(), size, 0, True, 16 << 20, 2 << 20, 8)
+                m = c.write_from_device(B, name, t.data_ptr(), size, 0, True, 16 << 20, slot, 8, async_stage)
                 assert m["size"] == size and m["crc32c"] == m["gpu_crc32c"], m
+                assert m["staged_whole"] and m["d2h_copies"] == -(-size // slot), m
                 back = c.read_bytes(B, name)
                 assert native.crc32c(back) == m["crc32c"]
                 assert back == native.gpu_read_bytes(0, t.data_ptr(), size)

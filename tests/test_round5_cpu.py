@@ -272,3 +272,18 @@ def test_rocprof_db_summary_reads_the_sqlite_views(tmp_path):
     md = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "rocprof_db_summary.py"), str(tmp_path), "--md"],
                         capture_output=True, text=True, timeout=60)
     assert md.returncode == 0 and "| `crc32c_slot_kernel` | 2 |" in md.stdout
+
+
+def test_fixed_overrides_parse_and_reject():
+    """GCSB_FIXED overrides FIXED settings for A/B sessions; an unknown key or
+    an item without '=' ends the run instead of being ignored."""
+    from custom_go_client_benchmark_amd.benchmark import rank
+
+    assert rank.fixed_overrides(None) == {}
+    assert rank.fixed_overrides("list_overlap=off, write_async_stage=off") == {
+        "list_overlap": "off", "write_async_stage": "off"}
+    assert rank.fixed_overrides("sliced_slots=3") == {"sliced_slots": 3}
+    with pytest.raises(SystemExit):
+        rank.fixed_overrides("no_such_key=1")
+    with pytest.raises(SystemExit):
+        rank.fixed_overrides("list_overlap")

@@ -106,7 +106,6 @@ Runner::Runner(RunnerConfig cfg) : cfg_(std::move(cfg)) {
   if (cfg_.conn_ring && cfg_.sink == "gpu" && one_conn && cfg_.workers > 1 && cfg_.slices <= 1 && g.verify &&
       g.landing == Landing::kObject && g.stage == GpuSinkConfig::Stage::kH2D)
     conn_ring_ = std::make_unique<ConnRing>(g.device, cfg_.conn_ring_slot_bytes, cfg_.conn_ring_slots);
-  overlap_ = cfg_.overlap_finish && cfg_.sink == "gpu" && cfg_.slices <= 1 && !conn_ring_ && !cfg_.read_diag;
   client_ = make_client(cfg_.client);
 }
 
@@ -120,15 +119,6 @@ Runner::~Runner() {
   run_cv_.notify_all();
   for (auto& t : threads_)
     if (t.joinable()) t.join();
-  for (auto& f : fin_) {
-    if (!f) continue;
-    {
-      std::lock_guard<std::mutex> lk(f->mu);
-      f->stop = true;
-    }
-    f->cv.notify_all();
-    if (f->th.joinable()) f->th.join();
-  }
 }
 
 namespace {
@@ -145,56 +135,6 @@ void add_gpu_stats(GpuSinkStats& t, const GpuSinkStats& g) {
 }
 }  // namespace
 
-void Runner::finisher_loop(int w) {
-  pin_current_thread(cfg_.client.cpus);
-  name_current_thread("gcsb-worker");  // accounted with the workers
-  Finisher& f = *fin_[w];
-  std::unique_lock<std::mutex> lk(f.mu);
-  for (;;) {
-    f.cv.wait(lk, [&] { return f.stop || f.has; });
-    if (!f.has) return;
-    GpuSink* s = f.sink;
-    ReadRecord r = std::move(f.r);
-    ReadResult rr = std::move(f.rr);
-    lk.unlock();
-    bool ok = true;
-    try {
-      rr.sink = s->finish();
-    } catch (const std::exception& e) {
-      r.error = e.what();
-      ok = false;
-    }
-    r.end_ns = now_ns();
-    const bool good = conclude(std::move(r), rr, ok);
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      last_landed_[w] = s;
-    }
-    if (!good && cfg_.stop_on_error) stop_flag_ = true;
-    lk.lock();
-    f.has = false;
-    f.cv.notify_all();
-  }
-}
-
-void Runner::finisher_post(int w, GpuSink* sink, ReadRecord&& r, ReadResult&& rr) {
-  Finisher& f = *fin_[w];
-  std::unique_lock<std::mutex> lk(f.mu);
-  // at most one read waits on its GPU tail: the one on the other sink
-  f.cv.wait(lk, [&] { return !f.has; });
-  f.sink = sink;
-  f.r = std::move(r);
-  f.rr = std::move(rr);
-  f.has = true;
-  lk.unlock();
-  f.cv.notify_all();
-}
-
-void Runner::finisher_drain(int w) {
-  Finisher& f = *fin_[w];
-  std::unique_lock<std::mutex> lk(f.mu);
-  f.cv.wait(lk, [&] { return !f.has; });
-}
 
 std::string Runner::object_for(int worker, int64_t seq) const {
   if (!cfg_.object_names.empty()) {
@@ -208,11 +148,6 @@ std::string Runner::object_for(int worker, int64_t seq) const {
 uintptr_t Runner::landing_ptr(int w) const {
   if (w < 0 || w >= static_cast<int>(sinks_.size())) return 0;
   if (landing_[w]) return reinterpret_cast<uintptr_t>(landing_[w]->data());
-  if (overlap_) {
-    std::lock_guard<std::mutex> lk(mu_);
-    if (w < static_cast<int>(last_landed_.size()) && last_landed_[w])
-      return reinterpret_cast<uintptr_t>(last_landed_[w]->object_device_ptr());
-  }
   if (gpu_sinks_[w]) return reinterpret_cast<uintptr_t>(gpu_sinks_[w]->object_device_ptr());
   return 0;
 }
@@ -254,8 +189,6 @@ void Runner::reset_stats() {
   // the sinks live across phases: their counters restart with the timed reads
   for (GpuSink* g : gpu_sinks_)
     if (g) g->reset_stats();
-  for (auto& g : sinks_b_)
-    if (g) g->reset_stats();
   if (cfg_.sink == "gpu")
     for (auto& sr : sliced_)
       if (sr)
@@ -272,11 +205,6 @@ void Runner::start() {
     gpu_stats_.assign(cfg_.workers, GpuSinkStats{});
     sliced_.resize(cfg_.workers);
     landing_.resize(cfg_.workers);
-    if (overlap_) {
-      sinks_b_.resize(cfg_.workers);
-      fin_.resize(cfg_.workers);
-      last_landed_.assign(cfg_.workers, nullptr);
-    }
   }
   {
     std::lock_guard<std::mutex> lk(ctl_mu_);
@@ -410,11 +338,6 @@ void Runner::worker_main(int w) {
         auto g = std::make_unique<GpuSink>(gc);
         gpu_sinks_[w] = g.get();
         sinks_[w] = std::move(g);
-        if (overlap_) {
-          sinks_b_[w] = std::make_unique<GpuSink>(gc);
-          fin_[w] = std::make_unique<Finisher>();
-          fin_[w]->th = std::thread([this, w] { finisher_loop(w); });
-        }
       } else {
         // multiplexed gRPC: host CRC on the worker thread, not the connection's reader
         sinks_[w] = std::make_unique<DiscardSink>(cfg_.client.read_chunk, cfg_.host_crc, defer_host_crc(cfg_.client),
@@ -471,27 +394,20 @@ void Runner::worker_main(int w) {
     SchedSample diag0;
     if (cfg_.read_diag) diag0 = sched_sample_offcore(kDiagThreads, diag_avoid);
     RoctxRange rg(sliced ? "gcsb.read_object(sliced)" : "gcsb.read_object");
-    // overlap_finish: this read's sink (the two alternate); its GPU tail is
-    // the finisher's, and the loop goes on to the next read
-    GpuSink* osink = overlap_ && gsink ? ((i & 1) ? sinks_b_[w].get() : gsink) : nullptr;
     r.start_wall_ns = wall_ns();
     r.start_ns = now_ns();
     ReadResult rr;
     bool ok = true;
     try {
       rr = sliced ? sliced->read(cfg_.bucket, r.object, &stop_flag_)
-                  : client_->read_object(cfg_.bucket, r.object, osink ? *osink : *sink, cfg_.range_offset,
-                                         cfg_.range_limit, &stop_flag_, 0, /*defer_finish=*/osink != nullptr);
+                  : client_->read_object(cfg_.bucket, r.object, *sink, cfg_.range_offset, cfg_.range_limit,
+                                         &stop_flag_);
     } catch (const StorageError& e) {
       r.error = std::string("while creating reader object: ") + e.what();
       ok = false;
     } catch (const std::exception& e) {
       r.error = e.what();
       ok = false;
-    }
-    if (osink && ok) {
-      finisher_post(w, osink, std::move(r), std::move(rr));
-      continue;
     }
     r.end_ns = now_ns();
     if (cfg_.read_diag)
@@ -501,12 +417,9 @@ void Runner::worker_main(int w) {
       break;
     }
   }
-  if (overlap_ && gsink) finisher_drain(w);
   if (gsink) {
-    GpuSinkStats t = gsink->stats();
-    if (overlap_ && sinks_b_[w]) add_gpu_stats(t, sinks_b_[w]->stats());
     std::lock_guard<std::mutex> lk(mu_);
-    gpu_stats_[w] = t;
+    gpu_stats_[w] = gsink->stats();
   } else if (sliced && cfg_.sink == "gpu") {
     GpuSinkStats t;
     for (int i = 0; i < sliced->num_sinks(); ++i) add_gpu_stats(t, static_cast<GpuSink&>(sliced->sink(i)).stats());

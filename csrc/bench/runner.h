@@ -84,15 +84,6 @@ struct RunnerConfig {
   bool conn_ring = true;
   size_t conn_ring_slot_bytes = size_t(1) << 20;
   int conn_ring_slots = 4;
-  // GPU sink with a ring per worker (HTTP, or gRPC with a connection per
-  // worker): each worker alternates two sinks and starts its next read once
-  // the previous one's last byte is on the host; a finisher thread per
-  // worker waits out that read's last H2D copy + CRC (GpuSink::finish) and
-  // stamps its end.  A read's latency still runs until every byte is in HBM
-  // and verified; the worker just does not idle through the GPU tail (as the
-  // reference's next NewReader follows io.Copy's return).  Ignored with
-  // slices > 1, a connection ring, or read_diag.
-  bool overlap_finish = false;
   // CPUs the read_diag sampler must not run on (the placement's; the client
   // CPUs are always added): sched_sample_offcore
   std::vector<int> diag_avoid_cpus;
@@ -211,24 +202,6 @@ class Runner {
   // r.end_ns stamped by the caller: fill the record from rr, write the
   // latency line, record it; false = the read failed
   bool conclude(ReadRecord&& r, const ReadResult& rr, bool ok_so_far);
-  // RunnerConfig::overlap_finish: worker w's finisher thread and its one
-  // outstanding read (the worker's other sink holds the next one)
-  struct Finisher {
-    std::mutex mu;
-    std::condition_variable cv;
-    bool has = false, stop = false;
-    GpuSink* sink = nullptr;
-    ReadRecord r;
-    ReadResult rr;
-    std::thread th;
-  };
-  void finisher_loop(int w);
-  void finisher_post(int w, GpuSink* sink, ReadRecord&& r, ReadResult&& rr);
-  void finisher_drain(int w);
-  bool overlap_ = false;
-  std::vector<std::unique_ptr<Finisher>> fin_;
-  std::vector<std::unique_ptr<GpuSink>> sinks_b_;  // each worker's second sink
-  std::vector<GpuSink*> last_landed_;              // mu_: the sink of w's last finished read
   RunnerConfig cfg_;
   // before client_: destroyed after the connections (their reader threads
   // fill it) and after the sinks whose segments it holds

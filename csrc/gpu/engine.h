@@ -368,6 +368,9 @@ class GpuByteSource : public ByteSource {
   bool range_crc32c(uint64_t off, size_t len, uint32_t* crc) override;
   uint64_t copies() const { return copies_.load(std::memory_order_relaxed); }
   uint64_t gpu_range_crcs() const { return range_hits_; }
+  // time next() waited for staged bytes (a slot's issue on the submitter,
+  // its D2H copy + CRC): the upload's sender stalled on the staging
+  int64_t stage_wait_ns() const { return stage_wait_ns_; }
   // Whole-object staging issues its first kSyncSlots slots on the calling
   // thread and hands the rest (a D2H copy, a CRC launch and an event each)
   // to the device's submitter thread, so the upload's first byte does not
@@ -435,6 +438,7 @@ class GpuByteSource : public ByteSource {
   mutable std::vector<char> slot_harvested_;
   const CrcTables* d_tables_ = nullptr;
   uint64_t range_hits_ = 0;
+  int64_t stage_wait_ns_ = 0;
 };
 
 // Grow-only HBM buffer (e.g. the landing zone a sliced read's slice sinks

@@ -1779,6 +1779,7 @@ void GpuByteSource::seek(uint64_t off) {
 
 std::pair<const uint8_t*, size_t> GpuByteSource::next(size_t max) {
   if (pos_ >= n_ || max == 0) return {nullptr, 0};
+  const int64_t w0 = now_ns();
   await_issued(cur_);
   // slot cur_ holds [slot_off_, slot_off_ + len) and pos_ lies inside it
   if (slot_off_[cur_] == ~0ull || pos_ >= slot_off_[cur_] + slot_len_[cur_]) {
@@ -1792,6 +1793,7 @@ std::pair<const uint8_t*, size_t> GpuByteSource::next(size_t max) {
   }
   hip_check(hipSetDevice(device_), "hipSetDevice");
   hip_check(hipEventSynchronize(ev_[cur_]), "hipEventSynchronize");
+  stage_wait_ns_ += now_ns() - w0;
   harvest(cur_);
   const uint64_t so = slot_off_[cur_];
   if (so == ~0ull || pos_ < so || pos_ >= so + slot_len_[cur_])

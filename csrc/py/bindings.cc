@@ -414,7 +414,7 @@ class PyClient {
     uint64_t copies = 0, range_crcs = 0;
     uint32_t crc = 0;
     bool whole = false;
-    double done_ms = 0;
+    double done_ms = 0, stage_wait_ms = 0;
     {
       py::gil_scoped_release nogil;
       int64_t t0 = now_ns();
@@ -432,6 +432,7 @@ class PyClient {
       range_crcs = src->gpu_range_crcs();
       crc = src->crc32c();
       whole = src->stable_until_done();
+      stage_wait_ms = src->stage_wait_ns() / 1e6;
       src.reset();  // staging drained and returned to the pool
       done_ms = (now_ns() - t0) / 1e6;
     }
@@ -447,6 +448,7 @@ class PyClient {
     // teardown after the response
     p["setup_ms"] = crc_ms;
     p["done_ms"] = done_ms;
+    p["stage_wait_ms"] = stage_wait_ms;  // the sender waiting for staged bytes
     d["phases"] = p;
     d["gpu_crc32c"] = crc;
     d["staged_whole"] = whole;  // the whole object staged at once (zero-copy sends)
@@ -513,7 +515,6 @@ class PyRunner {
     c.conn_ring = get_or<bool>(d, "conn_ring", c.conn_ring);
     c.conn_ring_slot_bytes = get_or<size_t>(d, "conn_ring_slot_bytes", c.conn_ring_slot_bytes);
     c.conn_ring_slots = get_or<int>(d, "conn_ring_slots", c.conn_ring_slots);
-    c.overlap_finish = get_or<bool>(d, "overlap_finish", c.overlap_finish);
     if (d.contains("diag_avoid_cpus") && !d["diag_avoid_cpus"].is_none())
       c.diag_avoid_cpus = d["diag_avoid_cpus"].cast<std::vector<int>>();
     c.stop_on_error = get_or<bool>(d, "stop_on_error", true);

@@ -71,7 +71,6 @@ FIXED = {
     "mux_send": "isolate",        # multiplexed blocks: the endpoint send thread and the
     "mux_reader": "isolate",      # connection reader on physical cores of their own (r5_muxiso)
     "client_cc": "cubic",         # client sockets' congestion control, set before connect (r4_recvcost)
-    "list_overlap": "on",         # config 3 over HTTP: next read starts at host landing (RunnerConfig::overlap_finish)
     "write_async_stage": "on",    # config 5: staging past the first slots issued on the submitter (r6_e)
 }
 

@@ -301,41 +301,3 @@ def test_write_combined_ring_byte_exact(native, server, gpu_available):
     sink = native.GpuSink({"device": 0, "ring_slot_bytes": 1 << 20, "ring_slots": 2, "ring_wc": True})
     r = c.read_gpu(B, P + "0", sink)
     assert r["crc_mismatch"] and not r["verified"]
-
-
-@pytest.mark.parametrize("overlap", [False, True])
-def test_runner_overlap_finish(native, server, gpu_available, overlap):
-    """overlap_finish (config 3 over HTTP): each worker alternates two sinks
-    and starts its next read at the previous one's host landing, a finisher
-    thread waits out that read's GPU tail.  Every read is still verified,
-    counted once and timed to its end in HBM; the last landed object is
-    byte-exact; a corrupted object still fails its read."""
-    size, workers, reads = (1 << 20) + 777, 4, 5
-    names = [f"ovl{int(overlap)}/file_{i}" for i in range(workers * reads)]
-    server.add_synthetic(B, f"ovl{int(overlap)}/file_", "", 0, len(names), size)
-    run = native.Runner({"protocol": "http", "endpoint": server.url, "bucket": B, "workers": workers,
-                         "object_names": names, "reads_per_worker": reads, "sink": "gpu",
-                         "ring_slot_bytes": 1 << 20, "ring_slots": 2, "overlap_finish": overlap})
-    run.start()
-    run.wait()
-    s = run.summary()
-    assert s["reads"] == workers * reads and s["errors"] == 0 and s["verified"] == workers * reads, s
-    assert s["gpu"]["objects_verified"] == workers * reads, s["gpu"]
-    recs = run.drain()
-    assert len(recs) == workers * reads
-    for r in recs:
-        # the timer runs to the GPU's end: never before the host landed
-        assert r["ok"] and r["end_ns"] >= r["host_done_ns"] > r["start_ns"], r
-    last = names[(0 + (reads - 1) * workers) % len(names)]
-    bad, first = native.gpu_verify_pattern(0, run.landing_ptr(0), size, last, 0)
-    assert bad == 0, first
-    server.set_faults({"corrupt_at": 4099, "corrupt_count": 1})
-    run2 = native.Runner({"protocol": "http", "endpoint": server.url, "bucket": B, "workers": 1,
-                          "object_names": names[:3], "reads_per_worker": 3, "sink": "gpu",
-                          "ring_slot_bytes": 1 << 20, "ring_slots": 2, "overlap_finish": overlap,
-                          "stop_on_error": False})
-    run2.start()
-    run2.wait()
-    s2 = run2.summary()
-    assert s2["reads"] == 3 and s2["errors"] == 1, s2
-    assert "crc" in s2["first_error"].lower(), s2["first_error"]

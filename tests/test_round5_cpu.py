@@ -280,10 +280,10 @@ def test_fixed_overrides_parse_and_reject():
     from custom_go_client_benchmark_amd.benchmark import rank
 
     assert rank.fixed_overrides(None) == {}
-    assert rank.fixed_overrides("list_overlap=off, write_async_stage=off") == {
-        "list_overlap": "off", "write_async_stage": "off"}
+    assert rank.fixed_overrides("list_ring_wc=off, write_async_stage=off") == {
+        "list_ring_wc": "off", "write_async_stage": "off"}
     assert rank.fixed_overrides("sliced_slots=3") == {"sliced_slots": 3}
     with pytest.raises(SystemExit):
         rank.fixed_overrides("no_such_key=1")
     with pytest.raises(SystemExit):
-        rank.fixed_overrides("list_overlap")
+        rank.fixed_overrides("list_ring_wc")

@@ -225,14 +225,8 @@ class SideBlocks:
                 # the other two (profiles/r3_write/placement)
                 pl = self.affinity.plan(gpu, "pair", self.slot)
                 sh = {"client": pl["client"], "server": sorted(pl["server"] + pl.get("aux", []))}
-                srv_cpus, crc_cpus = sh["server"], None
-                if getattr(args, "write_crc", "shared") == "sibling" and len(pl["server"]) > 1:
-                    # the CRC worker on the receiving core's SMT sibling: it
-                    # reads each message out of the L2 the receive wrote,
-                    # instead of pulling the lines to another core
-                    srv_cpus, crc_cpus = pl["server"][:1], pl["server"][1:]
-                ep = n.Server({"port": 0, "md5": False, "cpus": srv_cpus, "send_cpus": sh.get("send_cpus"),
-                               "crc_cpus": crc_cpus, "retain_uploads": False})
+                ep = n.Server({"port": 0, "md5": False, "cpus": sh["server"], "send_cpus": sh.get("send_cpus"),
+                               "retain_uploads": False})
                 ep.start()
             else:
                 ep, sh = self.share_endpoint()
@@ -462,7 +456,7 @@ class SideBlocks:
         args, n = self.args, self.n
         err = ""
         r = {"tcp_gbps": 0.0, "tcp_gbps_same": 0.0, "tcp_recv_cpu_s_per_gib": 0.0, "tcp_send_cpu_s_per_gib": 0.0,
-             "memcpy_gbps": 0.0, "h2d_gbps": 0.0, "h2d_1mib_gbps": 0.0}
+             "memcpy_gbps": 0.0, "h2d_gbps": 0.0}
         try:
             ring = args.slots * parse_size(args.slot_bytes)
             reads = max(3, min(10, self.side_steps))
@@ -499,10 +493,6 @@ class SideBlocks:
                 pats = [(parse_size(args.slot_bytes), args.slots, args.slots), (2 << 20, 8, 8), (8 << 20, 8, 8)]
                 r["h2d_gbps"] = max(n.copy_ceiling(self.gpu, "h2d", self.size, c, sl, st, 5)["gbps"]
                                     for c, sl, st in pats)
-                # config 3's copies: one 1 MiB object per copy, 8 readers'
-                # rings on the 8 pool streams (the list-read blocks' own
-                # copy pattern; diagnostic next to the best-pattern bound)
-                r["h2d_1mib_gbps"] = n.copy_ceiling(self.gpu, "h2d", 64 << 20, 1 << 20, 16, 8, 5)["gbps"]
             else:
                 r["tcp_gbps_same"] = t["gbps"]
         except Exception as e:  # noqa: BLE001 - reported in the block, collectives still run

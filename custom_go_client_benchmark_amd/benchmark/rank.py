@@ -72,7 +72,6 @@ FIXED = {
     "mux_reader": "isolate",      # connection reader on physical cores of their own (r5_muxiso)
     "client_cc": "cubic",         # client sockets' congestion control, set before connect (r4_recvcost)
     "write_async_stage": "on",    # config 5: staging past the first slots issued on the submitter (r6_f, r6_g)
-    "write_crc": "shared",        # config 5: the endpoint's CRC worker on the endpoint's cores | sibling (SMT)
 }
 
 
@@ -867,10 +866,6 @@ class RankBench(SideBlocks):
                                           extra.get("_conns"), extra.get("sink") == "gpu" and self.use_gpu))
                 if "bound_mib_s" in b:  # per GPU: each rank's bound is its own link / copy engines
                     b["bound_mib_s"] = round(b["bound_mib_s"] * max(1, world), 1)
-                if key.startswith("list_read_") and extra.get("sink") == "gpu" and ceil.get("h2d_1mib_gbps"):
-                    # against its own copy pattern: one 1 MiB copy per object
-                    c1 = ceil["h2d_1mib_gbps"] * rp.MIB_PER_GBPS
-                    b["frac_of_copy_1mib"] = round(b["mib_s"] / max(1, world) / c1, 3)
             full[key] = b
         head_bound = (value, "tcp_1conn", uc["tcp_best_mib_s"] * max(1, world)) if uc else None
         raised = rp.observed_bounds(full, head_bound)

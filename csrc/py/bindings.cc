@@ -646,6 +646,7 @@ class PyServer {
     if (d.contains("crc_cpus") && !d["crc_cpus"].is_none()) c.crc_cpus = d["crc_cpus"].cast<std::vector<int>>();
     store_ = std::make_shared<ObjectStore>(get_or<bool>(d, "md5", true));
     store_->set_retain_uploads(get_or<bool>(d, "retain_uploads", true));
+    c.write_verify = get_or<bool>(d, "write_verify", true);
     srv_ = std::make_unique<FakeGcsServer>(c, store_);
   }
   void start() { srv_->start(); }
@@ -723,6 +724,8 @@ class PyServer {
     d["bytes_sent"] = s.bytes_sent.load();
     d["bytes_received"] = s.bytes_received.load();
     d["faults_injected"] = s.faults_injected.load();
+    d["write_recvs"] = s.write_recvs.load();
+    d["write_recv_bytes"] = s.write_recv_bytes.load();
     d["auth_failures"] = s.auth_failures.load();
     d["body_sends"] = s.body_sends.load();
     d["body_wall_us"] = s.body_wall_us.load();

@@ -64,6 +64,10 @@ struct ServerConfig {
   // connection's bytes in flight in the socket buffers, not the endpoint's
   // queue (profiles/r4_main7 mux; endpoint request -> HEADERS 10-30 us).
   size_t h2_quantum = 0;
+  // Attribution A/B only: false = WriteObject messages are not CRC-checked
+  // (the endpoint trusts the client's per-message crc32c), so nothing but
+  // the receive reads the uploaded bytes.  Default true.
+  bool write_verify = true;
   // https / gRPC over TLS (ALPN h2 or http/1.1) when both are set (PEM files)
   std::string tls_cert_file, tls_key_file;
 };
@@ -71,6 +75,9 @@ struct ServerConfig {
 struct ServerStats {
   std::atomic<uint64_t> connections{0}, http_requests{0}, grpc_calls{0}, bytes_sent{0}, bytes_received{0},
       faults_injected{0}, auth_failures{0};
+  // WriteObject content receives on the connection thread (recv calls and
+  // bytes): the upload's receive granularity
+  std::atomic<uint64_t> write_recvs{0}, write_recv_bytes{0};
   // object-body sends (HTTP GET bodies, gRPC ReadObject streams): the
   // kernel's send chronographs over each (TCP_INFO deltas, us) and the
   // congestion window at its end -- what bounded the endpoint's sending

@@ -368,6 +368,8 @@ class H2ServerConn {
       const uint32_t want = std::min(n, s.wmsg_len - s.wmsg_have);
       const size_t k = bc_.read_some(s.wmsg.get() + s.wmsg_have, want);
       if (k == 0) throw StorageError("connection closed inside a WriteObject message", true);
+      srv_.stats().write_recvs.fetch_add(1, std::memory_order_relaxed);
+      srv_.stats().write_recv_bytes.fetch_add(k, std::memory_order_relaxed);
       s.wmsg_have += static_cast<uint32_t>(k);
       n -= static_cast<uint32_t>(k);
       if (s.wmsg_have == s.wmsg_len) post_write_message(sp);
@@ -1214,7 +1216,9 @@ class H2ServerConn {
                                              std::to_string(persisted));
     } else if (w.has_data) {
       // one CRC pass: checks the message and extends the object CRC
-      const uint32_t c = crc32c(w.content.data(), w.content.size());
+      const uint32_t c = srv_.config().write_verify || !w.has_content_crc
+                             ? crc32c(w.content.data(), w.content.size())
+                             : w.content_crc;
       if (w.has_content_crc && c != w.content_crc) return fail(kDataLoss, "ChecksummedData crc32c mismatch");
       u.append_with_crc(w.content.data(), w.content.size(), c);
     }

@@ -226,7 +226,8 @@ class SideBlocks:
                 pl = self.affinity.plan(gpu, "pair", self.slot)
                 sh = {"client": pl["client"], "server": sorted(pl["server"] + pl.get("aux", []))}
                 ep = n.Server({"port": 0, "md5": False, "cpus": sh["server"], "send_cpus": sh.get("send_cpus"),
-                               "retain_uploads": False})
+                               "retain_uploads": False,
+                               "write_verify": getattr(args, "write_verify", "on") == "on"})
                 ep.start()
             else:
                 ep, sh = self.share_endpoint()
@@ -250,6 +251,7 @@ class SideBlocks:
         gdist.barrier(self.ctx, "R1 write start barrier")
         self.sync()
         n.reset_slow_hip_calls()
+        es0 = ep.stats() if ep is not None and parts == 1 else None
         th0 = cpuacct.thread_cpu()
         t1 = time.perf_counter()
         nbytes = 0
@@ -272,6 +274,7 @@ class SideBlocks:
         self.sync()
         gdist.barrier(self.ctx, "R2 write stop barrier")
         e1 = time.perf_counter() - t1
+        es1 = ep.stats() if es0 is not None else None
         by_name = {k: v - th0.get(k, 0.0) for k, v in cpuacct.thread_cpu().items()}
         cpu_split = {k: round(v / max(nbytes, 1) * (1 << 30), 4) for k, v in sorted(by_name.items())
                      if v > 0.0005 and nbytes}
@@ -309,6 +312,11 @@ class SideBlocks:
         st["cpu_s_per_gib_by_thread"] = cpu_split
         if up_probe:
             st["upload_probe"] = up_probe
+        if es1 is not None and es1.get("write_recvs", 0) > es0.get("write_recvs", 0):
+            # the endpoint's WriteObject receive granularity over the timed uploads
+            nrecv = es1["write_recvs"] - es0["write_recvs"]
+            st.setdefault("upload_probe", {})["endpoint_recv_avg_kib"] = round(
+                (es1["write_recv_bytes"] - es0["write_recv_bytes"]) / nrecv / 1024, 1)
         if phases:
             # medians over the timed uploads: the start RPC, the first and
             # last content byte sent, the final response (ms from the start)

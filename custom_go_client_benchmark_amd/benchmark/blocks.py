@@ -212,6 +212,9 @@ class SideBlocks:
         phases = []  # per upload: where its time went (the client's UploadPhases)
         wsize = parse_size(args.write_size)
         astage = getattr(args, "write_async_stage", "on") == "on"
+        # staging slot = the largest upload message the transport sends from
+        # it (messages never cross a slot; gRPC caps them at 2 MiB)
+        wslot = parse_size(getattr(args, "write_slot_bytes", args.slot_bytes))
         chunk = parse_size(args.write_chunk)
         client = buf = None
         ep = None
@@ -245,7 +248,7 @@ class SideBlocks:
             n.gpu_fill_pattern(gpu, buf.data_ptr(), wsize, f"upload/rank{rank}", 0)
             for i in range(warmup):
                 client.write_from_device(self.bucket, f"upload/warmup_{rank}_{i}", buf.data_ptr(), wsize, gpu, True,
-                                         chunk, parse_size(args.slot_bytes), args.slots, astage)
+                                         chunk, wslot, args.slots, astage)
         except Exception as e:  # noqa: BLE001
             err = f"{type(e).__name__}: {e}"
         gdist.barrier(self.ctx, "R1 write start barrier")
@@ -260,7 +263,7 @@ class SideBlocks:
                 for i in range(steps):
                     t0 = time.perf_counter()
                     m = client.write_from_device(self.bucket, f"upload/rank{rank}_{i}", buf.data_ptr(), wsize, gpu,
-                                                 True, chunk, parse_size(args.slot_bytes), args.slots, astage)
+                                                 True, chunk, wslot, args.slots, astage)
                     lat.append((time.perf_counter() - t0) * 1e3)
                     if m.get("phases"):
                         phases.append(m["phases"])

@@ -647,7 +647,6 @@ class PyServer {
     store_ = std::make_shared<ObjectStore>(get_or<bool>(d, "md5", true));
     store_->set_retain_uploads(get_or<bool>(d, "retain_uploads", true));
     c.write_verify = get_or<bool>(d, "write_verify", true);
-    c.write_scatter = get_or<bool>(d, "write_scatter", true);
     srv_ = std::make_unique<FakeGcsServer>(c, store_);
   }
   void start() { srv_->start(); }

@@ -68,9 +68,6 @@ struct ServerConfig {
   // (the endpoint trusts the client's per-message crc32c), so nothing but
   // the receive reads the uploaded bytes.  Default true.
   bool write_verify = true;
-  // WriteObject receive: the rest of a frame plus what follows it in one
-  // recvmsg() (H2ServerConn::recv_write_data); false = a receive per piece
-  bool write_scatter = true;
   // https / gRPC over TLS (ALPN h2 or http/1.1) when both are set (PEM files)
   std::string tls_cert_file, tls_key_file;
 };

@@ -366,17 +366,7 @@ class H2ServerConn {
       // MSG_WAITALL, as the client's readers): the thread copies as the bytes
       // arrive instead of sleeping until a whole message is queued
       const uint32_t want = std::min(n, s.wmsg_len - s.wmsg_have);
-      size_t k;
-      if (srv_.config().write_scatter && !bc_.buffered() && want >= (64u << 10)) {
-        // the rest of the frame into the message and whatever follows it
-        // (the next frame's header, the next message's prefix) into the
-        // frame parser's buffer, in ONE recvmsg(): no separate fill
-        // receive per frame
-        iovec iov{s.wmsg.get() + s.wmsg_have, want};
-        k = bc_.recv_scatter(&iov, 1);
-      } else {
-        k = bc_.read_some(s.wmsg.get() + s.wmsg_have, want);
-      }
+      const size_t k = bc_.read_some(s.wmsg.get() + s.wmsg_have, want);
       if (k == 0) throw StorageError("connection closed inside a WriteObject message", true);
       srv_.stats().write_recvs.fetch_add(1, std::memory_order_relaxed);
       srv_.stats().write_recv_bytes.fetch_add(k, std::memory_order_relaxed);

@@ -230,8 +230,7 @@ class SideBlocks:
                 sh = {"client": pl["client"], "server": sorted(pl["server"] + pl.get("aux", []))}
                 ep = n.Server({"port": 0, "md5": False, "cpus": sh["server"], "send_cpus": sh.get("send_cpus"),
                                "retain_uploads": False,
-                               "write_verify": getattr(args, "write_verify", "on") == "on",
-                               "write_scatter": getattr(args, "write_scatter", "on") == "on"})
+                               "write_verify": getattr(args, "write_verify", "on") == "on"})
                 ep.start()
             else:
                 ep, sh = self.share_endpoint()

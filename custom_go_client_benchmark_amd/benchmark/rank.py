@@ -73,8 +73,7 @@ FIXED = {
     "client_cc": "cubic",         # client sockets' congestion control, set before connect (r4_recvcost)
     "write_async_stage": "on",    # config 5: staging past the first slots issued on the submitter (r6_f, r6_g)
     "write_verify": "on",         # config 5: the endpoint CRC-checks every message (off: attribution A/B only)
-    "write_slot_bytes": "1MiB",   # config 5: upload staging slot (and so WriteObject message) size
-    "write_scatter": "on",        # config 5: endpoint receives a frame's rest + the next header in one recvmsg
+    "write_slot_bytes": "2MiB",   # config 5: upload staging slot = one 2 MiB WriteObject message (r6_j)
 }
 
 

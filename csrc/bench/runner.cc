@@ -132,7 +132,6 @@ void add_gpu_stats(GpuSinkStats& t, const GpuSinkStats& g) {
   t.slot_wait_s += g.slot_wait_s;
   t.flag_reuses += g.flag_reuses;
   t.handoff_s += g.handoff_s;
-  t.slots_pulled += g.slots_pulled;
 }
 }  // namespace
 
@@ -508,7 +507,17 @@ RunSummary Runner::summary(bool percentiles) const {
       ++nsliced;
     }
   if (nsliced) s.slice_skew_ms /= nsliced;
-  for (const auto& g : gpu_stats_) add_gpu_stats(s.gpu, g);
+  for (const auto& g : gpu_stats_) {
+    s.gpu.slots_submitted += g.slots_submitted;
+    s.gpu.segments += g.segments;
+    s.gpu.chunks_verified_gpu += g.chunks_verified_gpu;
+    s.gpu.chunks_verified_host += g.chunks_verified_host;
+    s.gpu.objects_verified += g.objects_verified;
+    s.gpu.slot_waits += g.slot_waits;
+    s.gpu.slot_wait_s += g.slot_wait_s;
+    s.gpu.flag_reuses += g.flag_reuses;
+    s.gpu.handoff_s += g.handoff_s;
+  }
   return s;
 }
 

@@ -232,51 +232,6 @@ __device__ __forceinline__ uint32_t fold_tail(uint32_t byte, int r, uint32_t raw
   return x ^ (r < 4 ? raw >> (8 * r) : 0u);
 }
 
-// Fused pull (CrcSeg::dst): a tile's bytes, as load_tile<1> brought them
-// into registers from the pinned host slot, also go to the segment's HBM
-// destination.  The result's status still says only that the slot was read
-// and checked (every workgroup arrived after its loads): the HBM stores are
-// complete at the kernel's end, i.e. at the slot's event, which the sink
-// waits for before a read counts as landed (GpuSink::finish).
-// The H2D copy rides along with the CRC instead of running as
-// a separate SDMA copy before it.  Pieces before the segment's start were
-// loaded as zeros and are skipped; the first piece may begin inside the
-// segment (byte stores for its bytes from the start on).  dst - addr is a
-// multiple of 16, so every other piece is one aligned 16-byte store.
-__device__ __forceinline__ void store_tile(const CrcBatch& b, uint32_t s, uint32_t gt, int lane,
-                                           const uint4 (&v)[kCrcChunkPieces]) {
-  const intptr_t addr = static_cast<intptr_t>(reinterpret_cast<uintptr_t>(b.seg[s].addr));
-  uint8_t* const dst = b.seg[s].dst;
-  const uint32_t len = b.seg[s].len;
-  const uint32_t t = gt - b.seg[s].tile_base;
-  const intptr_t a16 = addr & ~intptr_t(15);
-  const int64_t full = (addr + len - a16 + 15) / 16 - 1;
-  const intptr_t vend = a16 + 16 * full;
-  const intptr_t tstart = vend - static_cast<intptr_t>(kCrcRoundBytes) * static_cast<intptr_t>(b.seg[s].ntiles - t);
-#pragma unroll
-  for (int j = 0; j < kCrcChunkPieces; ++j) {
-    const intptr_t p = tstart + kCrcChunkBytes * lane + 16 * j;
-    if (p >= addr) {
-      *reinterpret_cast<uint4*>(dst + (p - addr)) = v[j];
-    } else if (p + 16 > addr) {
-      const uint32_t w[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
-      for (int i = static_cast<int>(addr - p); i < 16; ++i)
-        dst[p + i - addr] = static_cast<uint8_t>(w[i >> 2] >> (8 * (i & 3)));
-    }
-  }
-}
-
-// ... and the segment's 1..16-byte tail (tail_byte's bytes, one per lane).
-__device__ __forceinline__ void store_tail(const CrcSeg& sg, int lane, uint32_t byte, int r) {
-  if (lane >= r) return;
-  const uintptr_t addr = reinterpret_cast<uintptr_t>(sg.addr);
-  const uintptr_t a16 = addr & ~uintptr_t(15);
-  const uintptr_t e = addr + sg.len;
-  const uintptr_t vend = a16 + 16 * ((e - a16 + 15) / 16 - 1);
-  const uintptr_t p0 = vend > addr ? vend : addr;
-  sg.dst[p0 + lane - addr] = static_cast<uint8_t>(byte);
-}
-
 // Result store for (host-mapped) result slots: raw / crc first, then, after
 // a system-scope fence, the status word the host polls (kCrcStatusPending).
 __device__ __forceinline__ void store_result(CrcSegResult* o, const CrcSegResult& r) {
@@ -495,7 +450,7 @@ __device__ __forceinline__ uint32_t xor_over_lanes(uint32_t x, int width) {
 // lane, a 6-level lookup chain), 1.0 us on the done counter, 2.5 us in the
 // last workgroup's Horner + tree fold.  W (waves per workgroup) is picked so
 // the grid puts a tile on every CU.
-template <int W, bool kS8 = false, bool kPull = false>
+template <int W, bool kS8 = false>
 __global__ __launch_bounds__(64 * W) void crc32c_slot_kernel(const CrcBatch b, const CrcTables* __restrict__ tabs,
                                                             uint32_t* __restrict__ scratch,
                                                             CrcSegResult* __restrict__ out) {
@@ -519,7 +474,6 @@ __global__ __launch_bounds__(64 * W) void crc32c_slot_kernel(const CrcBatch b, c
     while (s + 1 < b.nseg && b.seg[s + 1].tile_base <= gt0) ++s;
     kt = tabs->tile_k[b.seg[s].ntiles - 1 - (gt0 - b.seg[s].tile_base)][lane & 31];
     load_tile<1>(b, s, gt0, lane, v);
-    if constexpr (kPull) store_tile(b, s, gt0, lane, v);
   }
   // this lane's chunk -> tile end: 32 matrix columns, in registers
   uint32_t kl[32];
@@ -548,15 +502,12 @@ __global__ __launch_bounds__(64 * W) void crc32c_slot_kernel(const CrcBatch b, c
   const bool xor_path = b.nseg == 1 && gridDim.x <= 32u * groups && !(b.probe & 0x100u);
   int tail_r = 0;
   const uint32_t tail_b = xor_path && wave == 0 ? tail_byte(b.seg[0], lane, &tail_r) : 0u;
-  if constexpr (kPull)
-    if (xor_path && wave == 0 && blockIdx.x == 0) store_tail(b.seg[0], lane, tail_b, tail_r);
   uint32_t wsum = 0;
   for (uint32_t gt = gt0; gt < b.total_tiles; gt += gridDim.x * W) {
     if (gt != gt0) {
       while (s + 1 < b.nseg && b.seg[s + 1].tile_base <= gt) ++s;
       kt = tabs->tile_k[b.seg[s].ntiles - 1 - (gt - b.seg[s].tile_base)][lane & 31];
       load_tile<1>(b, s, gt, lane, v);
-      if constexpr (kPull) store_tile(b, s, gt, lane, v);
       __builtin_amdgcn_sched_barrier(0);
     }
     const uint32_t state = lane_chain<1, kS8>(v, s_sl, nullptr, lane);
@@ -644,7 +595,6 @@ __global__ __launch_bounds__(64 * W) void crc32c_slot_kernel(const CrcBatch b, c
     // per step (3.1 us for 8 steps)
     int r = 0;
     const uint32_t tb = tail_byte(sg, lane, &r);
-    if constexpr (kPull) store_tail(sg, lane, tb, r);
     uint32_t v[kCrcFusedMaxTiles / 64];
 #pragma unroll
     for (int k = 0; k < static_cast<int>(kCrcFusedMaxTiles / 64); ++k) {
@@ -808,17 +758,6 @@ void launch_crc32c_batch(const CrcBatch& b, const CrcTables* d_tables, uint32_t*
   const bool fused = b.max_seg_tiles <= kCrcFusedMaxTiles;
   const bool small = b.tile_log2 == static_cast<uint32_t>(kCrcMinTileLog2);
   const CrcLaunchOptions o = crc_launch_options();
-  // fused pull batches (CrcSeg::dst) run on the slot kernel only, every
-  // segment pulled
-  const bool pull = b.seg[0].dst != nullptr;
-  for (uint32_t i = 1; i < b.nseg; ++i)
-    if ((b.seg[i].dst != nullptr) != pull) throw std::logic_error("CRC batch mixes pulled and in-HBM segments");
-  if (pull) {
-    if (!(fused && small)) throw std::logic_error("fused pull needs a slot-sized CRC batch");
-    for (uint32_t i = 0; i < b.nseg; ++i)
-      if ((reinterpret_cast<uintptr_t>(b.seg[i].dst) - reinterpret_cast<uintptr_t>(b.seg[i].addr)) & 15u)
-        throw std::logic_error("fused pull: destination and source not congruent mod 16");
-  }
   if (fused && small) {
     // waves per workgroup: enough workgroups to put a tile on every CU first,
     // but two waves from 1 MiB up (each workgroup stages the 16 KiB tables,
@@ -836,15 +775,9 @@ void launch_crc32c_batch(const CrcBatch& b, const CrcTables* d_tables, uint32_t*
       bx.probe |= 0x100u;
     }
     if (g == 0) g = 1;
-#define GCSB_SLOT(WV, S8)                                                                                      \
-  do {                                                                                                         \
-    if (pull)                                                                                                  \
-      hipLaunchKernelGGL((crc32c_slot_kernel<WV, S8, true>), dim3(g), dim3(64 * WV), 0, stream,               \
-                         no_xor ? bx : b, d_tables, d_scratch, d_results);                                    \
-    else                                                                                                       \
-      hipLaunchKernelGGL((crc32c_slot_kernel<WV, S8, false>), dim3(g), dim3(64 * WV), 0, stream,              \
-                         no_xor ? bx : b, d_tables, d_scratch, d_results);                                    \
-  } while (0)
+#define GCSB_SLOT(WV, S8) \
+  hipLaunchKernelGGL((crc32c_slot_kernel<WV, S8>), dim3(g), dim3(64 * WV), 0, stream, no_xor ? bx : b, d_tables, \
+                     d_scratch, d_results)
     if (o.slice8) {
       switch (w) {
         case 1: GCSB_SLOT(1, true); break;

@@ -48,11 +48,6 @@ struct CrcSeg {
   uint32_t expected;
   uint32_t fixup;      // crc32c(d) = raw(d) ^ fixup(|d|)
   uint32_t flags;      // bit0: compare against expected
-  // Fused pull (slot kernel only): addr is a pinned host slot's device
-  // alias, and the kernel also stores the segment's bytes here (HBM) from
-  // the registers it CRCs them in -- no separate H2D copy.  dst - addr must
-  // be a multiple of 16.  nullptr: CRC only (addr is already in HBM).
-  uint8_t* dst;
 };
 
 struct CrcBatch {

@@ -99,12 +99,6 @@ struct GpuSinkConfig {
   // runs on into the next slot when it is free (GpuSink::acquire); false:
   // every window stops at its slot's end (A/B).
   bool ring_span = true;
-  // Fused pull: a slot's CRC kernel reads the pinned slot itself (its
-  // device alias) and stores the bytes to HBM as it CRCs them -- one launch
-  // per slot, no SDMA copy (crc32c_kernels.hip store_tile).  Per-slot
-  // fallback to copy + CRC when the slot's HBM destination is not 16-byte
-  // congruent with it (a resume at an odd offset).  Needs verify.
-  bool pull = false;
 };
 
 struct GpuSinkStats {
@@ -117,7 +111,6 @@ struct GpuSinkStats {
   double slot_wait_s = 0;
   uint64_t flag_reuses = 0;           // slots reused on the kernel's host-visible status (no HIP call)
   double handoff_s = 0;               // receiving thread inside the slot hand-off (submit + take, waits included)
-  uint64_t slots_pulled = 0;          // slots landed by the fused pull kernel (GpuSinkConfig::pull), no SDMA copy
 };
 
 class GpuSink : public Sink {
@@ -182,7 +175,6 @@ class GpuSink : public Sink {
     uint64_t posted = 0, issued = 0;
     CrcSegResult* res = nullptr;  // host-mapped, kMaxSeg entries
     CrcSegResult* d_res = nullptr;  // device alias of res
-    const uint8_t* host_dev = nullptr;  // device alias of host (GpuSinkConfig::pull)
   };
   void enqueue_slot(Slot& s, uint8_t* dst, const CrcBatch* batch);
   void ensure_object_capacity(int64_t size);
@@ -229,7 +221,6 @@ class GpuSink : public Sink {
   uint64_t obj_len_ = 0;
   bool mismatch_ = false;
   bool any_checked_ = false;
-  bool pulled_ = false;  // a slot of the current object went through the fused pull
   std::string detail_;
   // cached x^(8n) operators for the host fold
   uint64_t op_len_[4] = {~0ull, ~0ull, ~0ull, ~0ull};

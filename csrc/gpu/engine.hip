@@ -579,11 +579,6 @@ GpuSink::GpuSink(const GpuSinkConfig& cfg) : cfg_(cfg) {
     s.tiles = d_tiles_ + crc_scratch_words(tiles_cap_) * static_cast<size_t>(i);
     s.res = res_host_ + static_cast<size_t>(i) * kMaxSeg;
     hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&s.d_res), s.res, 0), "hipHostGetDevicePointer");
-    if (cfg_.pull && cfg_.verify) {
-      void* d = nullptr;
-      if (hipHostGetDevicePointer(&d, s.host, 0) == hipSuccess) s.host_dev = static_cast<const uint8_t*>(d);
-      else (void)hipGetLastError();  // not mapped: this slot copies
-    }
   }
 }
 
@@ -908,18 +903,13 @@ void GpuSink::submit_current() {
   uint8_t* dst = cfg_.landing == Landing::kObject ? obj_dst_ + s.obj_off : s.dev_ring;
   CrcBatch b;
   const bool crc = cfg_.verify && !s.segs.empty();
-  // fused pull: the kernel reads the slot and lands it; every byte of the
-  // slot is in a segment (each commit opens or extends one)
-  const bool pull = crc && s.host_dev && s.used <= (size_t(4) << 20) &&  // the slot kernel's batches
-                    ((reinterpret_cast<uintptr_t>(dst) - reinterpret_cast<uintptr_t>(s.host_dev)) & 15u) == 0;
   if (crc) {
     std::memset(&b, 0, sizeof(b));
     b.nseg = static_cast<uint32_t>(s.segs.size());
     for (size_t i = 0; i < s.segs.size(); ++i) {
       const SegInfo& g = s.segs[i];
       CrcSeg& c = b.seg[i];
-      c.addr = pull ? s.host_dev + g.slot_off : dst + g.slot_off;
-      c.dst = pull ? dst + g.slot_off : nullptr;
+      c.addr = dst + g.slot_off;
       c.len = g.len;
       c.expected = g.expected;
       c.flags = (g.chunk_start && g.chunk_end && g.has_expected && !g.broken_chunk) ? 1u : 0u;
@@ -931,10 +921,6 @@ void GpuSink::submit_current() {
   }
   s.inflight = true;
   ++stats_.slots_submitted;
-  if (pull) {
-    pulled_ = true;
-    ++stats_.slots_pulled;
-  }
   enqueue_slot(s, dst, crc ? &b : nullptr);
 }
 
@@ -948,14 +934,11 @@ void GpuSink::enqueue_slot(Slot& s, uint8_t* dst, const CrcBatch* batch) {
     }
     if (cfg_.stage == GpuSinkConfig::Stage::kNone) return;
     ensure_device(cfg_.device);
-    // copy, CRC and completion event in one stream's order: no cross-stream
-    // wait (a fused-pull batch lands the slot itself: no copy)
+    // copy, CRC and completion event in one stream's order: no cross-stream wait
     const int64_t t0 = now_ns();
-    if (!(b && b->seg[0].dst)) {
-      hip_check(hipMemcpyAsync(dst, s.host, s.used, hipMemcpyHostToDevice, s.st), "hipMemcpyAsync(H2D)");
-      note_hip_call("hipMemcpyAsync(H2D)", s.st_idx, t0, now_ns());
-    }
+    hip_check(hipMemcpyAsync(dst, s.host, s.used, hipMemcpyHostToDevice, s.st), "hipMemcpyAsync(H2D)");
     const int64_t t1 = now_ns();
+    note_hip_call("hipMemcpyAsync(H2D)", s.st_idx, t0, t1);
     if (b) {
       launch_crc32c_batch(*b, d_tables_, s.tiles, s.d_res, s.st);
       note_hip_call("crc launch", s.st_idx, t1, now_ns());
@@ -1077,20 +1060,6 @@ SinkResult GpuSink::finish() {
   } else {
     submit_current();
     for (int k = 0; k < cfg_.slots; ++k) wait_slot(slots_[(next_ + k) % cfg_.slots]);
-    if (pulled_) {
-      // fused pull: a slot reused on its result flags may still have had
-      // HBM stores in flight; every slot's last hand-off issued and its
-      // event done = every byte of this object landed
-      set_device();
-      for (Slot& s : slots_) {
-        if (cfg_.async_submit) {
-          std::unique_lock<std::mutex> lk(sub_mu_);
-          sub_cv_.wait(lk, [&] { return s.issued == s.posted; });
-        }
-        wait_event(s.ev);
-      }
-      pulled_ = false;
-    }
   }
   SinkResult r;
   r.bytes = delivered_;

@@ -106,7 +106,6 @@ GpuSinkConfig gpu_from(const py::dict& d) {
   g.wait_poll_us = get_or<int>(d, "wait_poll_us", g.wait_poll_us);
   g.ring_wc = get_or<bool>(d, "ring_wc", g.ring_wc);
   g.ring_span = get_or<bool>(d, "ring_span", g.ring_span);
-  g.pull = get_or<bool>(d, "gpu_pull", g.pull);
   const std::string stage = get_or<std::string>(d, "gpu_stage", "h2d");
   if (stage == "none") g.stage = GpuSinkConfig::Stage::kNone;
   else if (stage == "host_read") g.stage = GpuSinkConfig::Stage::kHostRead;
@@ -185,7 +184,6 @@ py::dict gpu_stats_dict(const GpuSinkStats& g) {
   r["slot_wait_s"] = g.slot_wait_s;
   r["flag_reuses"] = g.flag_reuses;
   r["handoff_s"] = g.handoff_s;
-  r["slots_pulled"] = g.slots_pulled;
   return r;
 }
 

@@ -62,7 +62,6 @@ FIXED = {
     "list_placement": "same",     # config 3: readers and endpoint in one L3 domain (r2_check_s4b)
     "list_ring_wc": "on",         # config 3: write-combined rings (r3_ring_thp/wc)
     "list_rcvbuf": "64MiB",
-    "list_pull": "off",           # config 3: the CRC kernel pulls each ring slot into HBM (no SDMA copy)
     "ceiling": "on",              # the ceiling block (--blocks selects it away)
     "ref_grpc_placement": "same",        # 48 workers on one connection in one L3 domain (r3_mux_thp/refplace)
     "ref_http_placement": "share_quota",  # 48 HTTP receivers over the quota's cores

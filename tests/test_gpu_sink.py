@@ -301,69 +301,3 @@ def test_write_combined_ring_byte_exact(native, server, gpu_available):
     sink = native.GpuSink({"device": 0, "ring_slot_bytes": 1 << 20, "ring_slots": 2, "ring_wc": True})
     r = c.read_gpu(B, P + "0", sink)
     assert r["crc_mismatch"] and not r["verified"]
-
-
-@pytest.mark.parametrize("chunk", [2 << 20, 300001])
-@pytest.mark.parametrize("size", [3, (1 << 20) + 777, (5 << 20) + 4099])
-@pytest.mark.parametrize("proto", ["http", "grpc"])
-def test_fused_pull_lands_byte_exact(native, gpu_available, proto, size, chunk):
-    """gpu_pull: each slot's CRC kernel reads the pinned slot itself and
-    stores the bytes to HBM (no SDMA copy).  Odd gRPC message sizes put
-    segment boundaries at odd slot offsets (the kernel's partial head piece
-    and 1..16-byte tails); every byte must land, every CRC must check, and
-    the pull path must be the one that ran."""
-    import torch
-
-    if proto == "http" and chunk != 2 << 20:
-        pytest.skip("the message size is a gRPC setting")
-    srv = native.Server({"port": 0, "grpc_chunk": chunk})
-    srv.start()
-    try:
-        srv.add_synthetic(B, "pull/file_", "", 0, 1, size)
-        c = native.Client({"protocol": proto, "endpoint": srv.url})
-        t = torch.empty(size + 4096, dtype=torch.uint8, device="cuda:0")
-        t.fill_(0xA5)
-        sink = native.GpuSink({"device": 0, "ring_slot_bytes": 1 << 20, "ring_slots": 2, "gpu_pull": True})
-        sink.set_external_destination(t.data_ptr(), t.numel())
-        for _ in range(2):  # the ring's slots are reused on the second read
-            r = c.read_gpu(B, "pull/file_0", sink)
-            assert r["verified"] and not r["crc_mismatch"] and r["bytes"] == size, r
-            torch.cuda.synchronize()
-            bad, first = native.gpu_verify_pattern(0, t.data_ptr(), size, "pull/file_0", 0)
-            assert bad == 0, (proto, size, chunk, first)
-            # nothing past the object was written
-            assert int((t[size:] != 0xA5).sum()) == 0
-        assert sink.stats()["slots_pulled"] >= 2, sink.stats()
-    finally:
-        srv.stop()
-
-
-def test_fused_pull_detects_corruption(native, server, gpu_available):
-    server.add_synthetic(B, P, "", 0, 1, 6 << 20)
-    server.set_faults({"corrupt_at": (3 << 20) + 5, "corrupt_count": 1})
-    c = native.Client({"protocol": "grpc", "endpoint": server.url})
-    sink = native.GpuSink({"device": 0, "ring_slot_bytes": 1 << 20, "ring_slots": 2, "gpu_pull": True})
-    r = c.read_gpu(B, P + "0", sink)
-    assert r["crc_mismatch"] and not r["verified"], r
-    assert sink.stats()["slots_pulled"] > 0
-
-
-def test_runner_fused_pull_list_read(native, server, gpu_available):
-    """The config-3 list-read shape with gpu_pull: 8 workers, 1 MiB objects,
-    one HTTP connection each; every read verified, the last objects
-    byte-exact in HBM, no slot copied by SDMA."""
-    size, workers, reads = 1 << 20, 8, 4
-    names = [f"pl/file_{i}" for i in range(workers * reads)]
-    server.add_synthetic(B, "pl/file_", "", 0, len(names), size)
-    run = native.Runner({"protocol": "http", "endpoint": server.url, "bucket": B, "workers": workers,
-                         "object_names": names, "reads_per_worker": reads, "sink": "gpu",
-                         "ring_slot_bytes": 1 << 20, "ring_slots": 2, "ring_wc": True, "gpu_pull": True})
-    run.start()
-    run.wait()
-    s = run.summary()
-    assert s["reads"] == workers * reads and s["errors"] == 0 and s["verified"] == workers * reads, s
-    assert s["gpu"]["slots_pulled"] == s["gpu"]["slots_submitted"] > 0, s["gpu"]
-    for w in range(workers):
-        last = names[(w + (reads - 1) * workers) % len(names)]
-        bad, first = native.gpu_verify_pattern(0, run.landing_ptr(w), size, last, 0)
-        assert bad == 0, (w, first)

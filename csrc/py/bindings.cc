@@ -1177,6 +1177,17 @@ PYBIND11_MODULE(_native, m) {
            py::arg("slot_bytes") = 8u << 20, py::arg("slots") = 4, py::arg("async_stage") = true)
       .def("compose", &PyClient::compose, py::arg("bucket"), py::arg("dest"), py::arg("sources"),
            py::arg("content_type") = "")
+      .def("last_upload",
+           [](PyClient& c) {
+             const UploadPhases ph = c.client().last_upload();
+             py::dict p;
+             p["start_rpc_ms"] = ph.start_rpc_ns / 1e6;
+             p["first_send_ms"] = ph.first_send_ns / 1e6;
+             p["last_send_ms"] = ph.last_send_ns / 1e6;
+             p["response_ms"] = ph.response_ns / 1e6;
+             return p;
+           },
+           "the last finished upload's phases, ms from its start (gRPC; 0 = not reached)")
       .def("delete", &PyClient::remove)
       .def("stats", &PyClient::stats);
 

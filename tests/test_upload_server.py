@@ -81,3 +81,15 @@ def test_write_crc_worker_on_its_own_cpus(native):
         assert c.read_bytes(B, "split/obj") == data
     finally:
         srv.stop()
+
+
+def test_upload_phases_are_ordered(native, server):
+    """UploadPhases (the write block's phases_ms): a resumable gRPC upload's
+    start RPC answers before the first content byte is sent, the last byte
+    after the first, and the final response after the last byte."""
+    c = native.Client({"protocol": "grpc", "endpoint": server.url})
+    data = bytes(range(256)) * ((6 << 20) // 256)
+    m = c.write_bytes(B, "phases/obj", data, True, 16 << 20)
+    assert m["size"] == len(data)
+    p = c.last_upload()
+    assert 0 < p["start_rpc_ms"] <= p["first_send_ms"] <= p["last_send_ms"] <= p["response_ms"], p

@@ -856,6 +856,10 @@ class RankBench(SideBlocks):
                 # config 5's bound: one loopback TCP stream in the upload's
                 # direction and placement (write_block), per GPU
                 bmib = st["upload_tcp_min"] * max(1, world)
+                if b["mib_s"] > bmib:
+                    # the upload beat its probe: the rate it reached is the bound
+                    diag.setdefault("bounds_raised_to_observed", {})[f"tcp_upload@{round(bmib, 1)}"] = b["mib_s"]
+                    bmib = b["mib_s"]
                 b.update({"bound": "tcp_upload", "bound_mib_s": round(bmib, 1),
                           "frac_of_bound": round(b["mib_s"] / bmib, 3)})
                 full[key] = b
@@ -872,7 +876,7 @@ class RankBench(SideBlocks):
         head_bound = (value, "tcp_1conn", uc["tcp_best_mib_s"] * max(1, world)) if uc else None
         raised = rp.observed_bounds(full, head_bound)
         if raised:
-            diag["bounds_raised_to_observed"] = raised
+            diag.setdefault("bounds_raised_to_observed", {}).update(raised)
             hb = raised.get(f"tcp_1conn@{round(uc['tcp_best_mib_s'] * max(1, world), 1)}") if uc else None
             if hb and uc.get("ceiling_bound") == "tcp_1conn":
                 # a block of the headline's own bound beat every probe: that rate is the ceiling

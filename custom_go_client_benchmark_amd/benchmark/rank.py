@@ -6,9 +6,10 @@ the pinned ring + hipMemcpyAsync, every CRC32C verified by the CDNA4
 kernels.  Rank r reads file_<r> (weak scaling; the reference's worker
 fan-out main.go:200-210 spread over GPUs).
 
-Paired headline (`--paired`, on at N = 1): the K timed headline reads run in
-4 chunks; between them, untimed for the headline, chunks of the same size of
-two twins on the same endpoint, placement and object:
+Paired headline (`--paired`, on at every N): the K timed headline reads run
+in 4 chunks; between them, untimed for the headline, chunks of the same size
+of two twins on the same endpoint, placement and object (and a raw TCP
+probe):
   base   reference semantics -- discard sink + host CRC32C (main.go:140,
          the Go library's reader), on the headline's two cores;
   nodma  the headline's own ring and receive path, the ring never DMA-read
@@ -46,8 +47,9 @@ FRAMING = {"ref": {"h2_max_frame_size": 0, "h2_window": 16 << 20},
            "large": {"h2_max_frame_size": (1 << 24) - 1, "h2_window": 0x7FFFFFFF}}
 FRAME_LABEL = {"ref": "16KiB", "large": "16MiB"}
 
-# Settings fixed by measurement in rounds 2-5 (no longer flags; the profiles/
-# that chose each are cited where it is used).
+# Settings fixed by measurement in rounds 2-6 (no longer flags; the profiles/
+# that chose each are cited where it is used).  GCSB_FIXED overrides them for
+# an A/B session (fixed_overrides).
 FIXED = {
     "conn_ring": "4x1MiB",        # multiplexed gRPC -> HBM: one 4 x 1 MiB ring per connection (r4_ringgeom)
     "async_submit": 1,            # slot hand-off on the device submitter thread (r2_single_stream)

@@ -141,7 +141,7 @@ def build_parser() -> argparse.ArgumentParser:
                     help="interleave the headline's timed reads in --paired-chunks chunks with chunks of the "
                          "reference-semantics baseline and of the never-DMA-read twin (same endpoint, cores, "
                          "object); vs_baseline_paired / headline_vs_nodma = medians of the per-chunk ratios. "
-                         "auto: on at N = 1")
+                         "auto: on (at every N; at N > 1 each chunk's arm rate is summed over the ranks)")
     ap.add_argument("--paired-chunks", type=int, default=4)
     ap.add_argument("--paired-rewarm", type=int, default=1,
                     help="untimed reads of each paired arm right before its chunk (outside the barriers): the "

@@ -89,14 +89,14 @@ class SideBlocks:
                 # light window: the receiving core's clock, host vmstat and
                 # the receiving thread's schedstat, outside the CPU bracket
                 clock = sysdiag.ClockSampler(recv_cpus[:4]) if recv_cpus and not errs[a] else None
-                vm0, sch0 = vmstat(), sysdiag.thread_sched()
+                vm0, sch0, tcp0 = vmstat(), sysdiag.thread_sched(), sysdiag.tcp_snapshot()
                 m = meters[a]
                 m.last = {}
                 if rewarm and not errs[a]:
                     self.untimed_reads(runners[a], rewarm)
                 c0 = self._counters(ep_stats, reset_hip=False) if a == "head" else None
                 e = self.timed_segment(runners[a], k, f"{what} {a} chunk {ci}", errs[a], m)
-                sch1, vm1 = sysdiag.thread_sched(), vmstat()
+                sch1, vm1, tcp1 = sysdiag.thread_sched(), vmstat(), sysdiag.tcp_snapshot()
                 if c0 is not None:
                     c1 = self._counters(ep_stats, reset_hip=False)
                     acc["rv"] = [acc["rv"][i] + c1["rv"][i] - c0["rv"][i] for i in range(2)]
@@ -122,7 +122,10 @@ class SideBlocks:
                 rd = _d("run_delay_ns", ("gcsb-h2-reader", "gcsb-worker"))
                 w = {"chunk": ci, "arm": a, "reads": k, "mib_s": round(row.get(a, 0.0), 1),
                      "recv_cpu_s_per_gib": round(recv / gib, 4) if recv else None,
-                     "run_delay_ms": round(rd / 1e6, 3)}
+                     "run_delay_ms": round(rd / 1e6, 3),
+                     # namespace TCP retransmits in the chunk (loopback: spurious
+                     # fast retransmits after reordering, README "Known limits")
+                     "tcp_retrans": tcp1.get("RetransSegs", 0) - tcp0.get("RetransSegs", 0)}
                 if runners[a] is not None and not errs[a]:
                     recs = sorted(runners[a].drain(), key=lambda x: x["start_ns"])
                     if recs:

@@ -254,7 +254,8 @@ def receiver_interference(head_cpu: dict, base_cpus: list[dict]) -> dict:
 def window_cause(w: dict, typical_recv: float | None) -> str:
     """Names what made one paired chunk slow from its window fields (the
     receiving thread's CPU-s/GiB against the run's median, its core's clock,
-    NUMA page migrations and compaction stalls during the chunk)."""
+    NUMA page migrations, compaction stalls and TCP retransmits during the
+    chunk)."""
     causes = []
     mhz, mhz_ref = w.get("clock_mhz"), w.get("clock_mhz_ref")
     if mhz and mhz_ref and mhz < 0.9 * mhz_ref:
@@ -269,6 +270,8 @@ def window_cause(w: dict, typical_recv: float | None) -> str:
                       f"or co-tenant)")
     if w.get("run_delay_ms", 0) > 1.0:
         causes.append(f"receiving thread waited {w['run_delay_ms']:.1f} ms for a CPU")
+    if w.get("tcp_retrans", 0) > 0:
+        causes.append(f"{w['tcp_retrans']} TCP retransmits (loopback reordering)")
     return "; ".join(causes) or "none named"
 
 

@@ -153,12 +153,13 @@ def test_attribute_windows_names_the_cause():
     w = [{"chunk": i, "arm": "head", "mib_s": 27000.0, "recv_cpu_s_per_gib": 0.036, "clock_mhz": 5000}
          for i in range(4)]
     w[2] = {"chunk": 2, "arm": "head", "mib_s": 15000.0, "recv_cpu_s_per_gib": 0.07, "clock_mhz": 3000,
-            "numa_pages_migrated": 512, "compact_stall": 0}
+            "numa_pages_migrated": 512, "compact_stall": 0, "tcp_retrans": 37}
     w.append({"chunk": 2, "arm": "base", "mib_s": 15000.0})
     slow = rp.attribute_windows(w)
     assert len(slow) == 1 and slow[0]["chunk"] == 2
     c = slow[0]["cause"]
     assert "clock 3000" in c and "512 NUMA page migrations" in c and "receive copy" in c
+    assert "37 TCP retransmits" in c
     assert rp.attribute_windows(w[:2]) == []
 
 

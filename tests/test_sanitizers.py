@@ -29,9 +29,6 @@ def _build(target):
 @pytest.mark.parametrize("kind,env", [
     ("asan", {"ASAN_OPTIONS": "detect_leaks=1", "UBSAN_OPTIONS": "halt_on_error=1"}),
     ("tsan", {"TSAN_OPTIONS": "halt_on_error=1 second_deadlock_stack=1"}),
-    # the optional receive paths and the endpoint's old send path
-    ("asan", {"ASAN_OPTIONS": "detect_leaks=1", "UBSAN_OPTIONS": "halt_on_error=1", "STRESS_RECV_REFILL": "1"}),
-    ("tsan", {"TSAN_OPTIONS": "halt_on_error=1 second_deadlock_stack=1", "STRESS_RECV_REFILL": "1"}),
 ])
 def test_stress_under_sanitizer(kind, env):
     _build(f"build/{kind}/stress")

@@ -122,12 +122,13 @@ CeilingResult memcpy_ceiling(const CeilingConfig& c) {
 CeilingResult tcp_ceiling(const CeilingConfig& c) {
   ::signal(SIGPIPE, SIG_IGN);  // a sender outliving a failed receiver must not kill the process
   const size_t obj = c.object_bytes;
-  Fd mfd(memfd_create("ceiling-object", 0));
-  if (mfd.fd < 0) fail("memfd_create");
-  if (ftruncate(mfd.fd, static_cast<off_t>(obj)) != 0) fail("ftruncate");
-  const bool thp = c.zerocopy_send && c.thp_source;
+  CeilingSource* const ext = c.source;
+  Fd mfd(ext ? -1 : memfd_create("ceiling-object", 0));
+  if (!ext && mfd.fd < 0) fail("memfd_create");
+  if (!ext && ftruncate(mfd.fd, static_cast<off_t>(obj)) != 0) fail("ftruncate");
+  const bool thp = !ext && c.zerocopy_send && c.thp_source;
   uint8_t* src = nullptr;  // thp: the object in THP anonymous memory
-  {
+  if (!ext) {
     // the object's pages on the sender's NUMA node, as the endpoint's source
     // (server/fakegcs.cc): the receiver's copy reads these pages, and pages
     // on the far socket cost it up to 2x per byte (profiles/r2_numa)
@@ -172,6 +173,7 @@ CeilingResult tcp_ceiling(const CeilingConfig& c) {
   std::atomic<int> go{0};
   std::atomic<bool> quit{false};
   std::atomic<int> conn_fd{-1};
+  std::atomic<int> received{0};  // reads the receiver completed (ext: when end() may run)
   double send_cpu_total = 0;
   std::exception_ptr send_err, recv_err;
   std::thread sender([&] {
@@ -187,31 +189,52 @@ CeilingResult tcp_ceiling(const CeilingConfig& c) {
       if (!c.zerocopy_send) copybuf.resize(2u << 20);
       Fd sp[2];
       const double c0 = thread_cpu_s();
+      auto splice_pages = [&](const uint8_t* p, size_t k) {
+        if (sp[0].fd < 0) {
+          int q[2];
+          if (pipe2(q, O_CLOEXEC) != 0) fail("pipe2");
+          sp[0].fd = q[0];
+          sp[1].fd = q[1];
+          (void)fcntl(q[1], F_SETPIPE_SZ, 1 << 20);
+        }
+        for (size_t done = 0; done < k;) {
+          iovec iov{const_cast<uint8_t*>(p + done), k - done};
+          const ssize_t v = vmsplice(sp[1].fd, &iov, 1, 0);
+          if (v <= 0) fail("vmsplice");
+          for (ssize_t left = v; left > 0;) {
+            const ssize_t w = splice(sp[0].fd, nullptr, s.fd, nullptr, static_cast<size_t>(left),
+                                     SPLICE_F_MOVE | SPLICE_F_MORE);
+            if (w <= 0) fail("splice");
+            left -= w;
+          }
+          done += static_cast<size_t>(v);
+        }
+      };
       for (int r = 0; r < c.reads; ++r) {
         while (go.load() <= r && !quit.load()) std::this_thread::yield();
         if (quit.load()) break;
+        if (ext) {
+          // one upload's worth: the source stages the object, the pages go
+          // out by reference as the transport sends them (grpc_client.cc
+          // write_stream), and stay put until the receiver has them all
+          ext->begin();
+          for (size_t off = 0; off < obj;) {
+            auto [p, k] = ext->next(std::min<size_t>(obj - off, 2u << 20));
+            if (k == 0) throw std::runtime_error("ceiling: upload source ended early");
+            splice_pages(p, k);
+            off += k;
+          }
+          while (received.load() <= r && !quit.load()) std::this_thread::yield();
+          ext->end();
+          continue;
+        }
         off_t off = 0;
         while (static_cast<size_t>(off) < obj) {
           const size_t k = std::min<size_t>(obj - off, 2u << 20);
           if (thp) {
             // vmsplice the pages into a pipe, splice the pipe into the socket
-            if (sp[0].fd < 0) {
-              int q[2];
-              if (pipe2(q, O_CLOEXEC) != 0) fail("pipe2");
-              sp[0].fd = q[0];
-              sp[1].fd = q[1];
-              (void)fcntl(q[1], F_SETPIPE_SZ, 1 << 20);
-            }
-            iovec iov{src + off, k};
-            const ssize_t v = vmsplice(sp[1].fd, &iov, 1, 0);
-            if (v <= 0) fail("vmsplice");
-            for (ssize_t left = v; left > 0;) {
-              const ssize_t w = splice(sp[0].fd, nullptr, s.fd, nullptr, static_cast<size_t>(left),
-                                       SPLICE_F_MOVE | SPLICE_F_MORE);
-              if (w <= 0) fail("splice");
-              left -= w;
-            }
-            off += static_cast<off_t>(v);
+            splice_pages(src + off, k);
+            off += static_cast<off_t>(k);
           } else if (c.zerocopy_send) {
             if (sendfile(s.fd, mfd.fd, &off, k) <= 0) fail("sendfile");
           } else {
@@ -262,6 +285,7 @@ CeilingResult tcp_ceiling(const CeilingConfig& c) {
           roff += static_cast<size_t>(n);
         }
         lat.push_back((now_s() - st) * 1e3);
+        received.store(r + 1);
       }
       const double el = now_s() - t0, cpu = thread_cpu_s() - c0;
       res.gbps = static_cast<double>(obj) * c.reads / el / 1e9;

@@ -11,6 +11,8 @@
 // copy_to_user rate bounds the read.
 #pragma once
 #include <cstddef>
+#include <cstdint>
+#include <utility>
 #include <vector>
 
 namespace gcsb {
@@ -20,6 +22,19 @@ struct CeilingResult {
   double p50_ms = 0;               // per object
   double recv_cpu_s_per_gib = 0;   // receiving (or copying) thread
   double send_cpu_s_per_gib = 0;   // sending thread (tcp)
+};
+
+// The sender's bytes for tcp_ceiling's upload bound: one object per read,
+// sent by reference (vmsplice + splice) and left unchanged until end(), which
+// runs once the receiver holds every byte.  bindings.cc wraps the uploader's
+// own GpuByteSource (HBM staged into pinned slots by D2H copies), so the probe
+// sends the pages a timed upload sends, written the way it writes them.
+class CeilingSource {
+ public:
+  virtual ~CeilingSource() = default;
+  virtual void begin() = 0;
+  virtual std::pair<const uint8_t*, size_t> next(size_t max) = 0;
+  virtual void end() = 0;
 };
 
 struct CeilingConfig {
@@ -34,6 +49,7 @@ struct CeilingConfig {
   // the endpoint's default) or a memfd by sendfile
   bool thp_source = true;
   int ring_pages = 1;                     // 0 default, 1 MADV_HUGEPAGE (the THP ring), 2 small pages
+  CeilingSource* source = nullptr;        // tcp: the sender's bytes (default: the object above)
 };
 
 // One thread memcpy()s a DRAM-resident object into the ring (recv_cpus).

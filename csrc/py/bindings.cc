@@ -1031,6 +1031,22 @@ PYBIND11_MODULE(_native, m) {
   }, py::arg("device"), py::arg("dir") = "h2d", py::arg("total") = size_t(256) << 20, py::arg("chunk") = size_t(2) << 20,
      py::arg("slots") = 8, py::arg("streams") = 8, py::arg("iters") = 5);
   m.def("loopback_ceiling", [](const py::dict& d) {
+    // upload bound (blocks.py write block): the sender sends a GpuByteSource's
+    // staging pages -- HBM copied D2H into pinned slots, as a timed upload --
+    // instead of the endpoint's THP object
+    struct GpuStaged : CeilingSource {
+      int dev;
+      const void* p;
+      uint64_t n;
+      size_t slot;
+      int slots;
+      std::unique_ptr<GpuByteSource> src;
+      GpuStaged(int d, const void* ptr, uint64_t bytes, size_t sb, int ns)
+          : dev(d), p(ptr), n(bytes), slot(sb), slots(ns) {}
+      void begin() override { src = std::make_unique<GpuByteSource>(dev, p, n, slot, slots, true, true); }
+      std::pair<const uint8_t*, size_t> next(size_t max) override { return src->next(max); }
+      void end() override { src.reset(); }
+    };
     CeilingConfig c;
     c.object_bytes = get_or<size_t>(d, "object_bytes", c.object_bytes);
     c.reads = get_or<int>(d, "reads", c.reads);
@@ -1043,6 +1059,14 @@ PYBIND11_MODULE(_native, m) {
     if (d.contains("send_cpus")) c.send_cpus = d["send_cpus"].cast<std::vector<int>>();
     if (d.contains("recv_cpus")) c.recv_cpus = d["recv_cpus"].cast<std::vector<int>>();
     const std::string mode = get_or<std::string>(d, "mode", "tcp");
+    std::unique_ptr<GpuStaged> staged;
+    if (d.contains("gpu_source_ptr")) {
+      staged = std::make_unique<GpuStaged>(get_or<int>(d, "gpu_source_device", 0),
+                                           reinterpret_cast<const void*>(d["gpu_source_ptr"].cast<uintptr_t>()),
+                                           c.object_bytes, get_or<size_t>(d, "gpu_source_slot_bytes", size_t(2) << 20),
+                                           get_or<int>(d, "gpu_source_slots", 4));
+      c.source = staged.get();
+    }
     CeilingResult r;
     {
       py::gil_scoped_release nogil;

@@ -228,11 +228,18 @@ class SideBlocks:
             if parts == 1 and self.use_gpu and args.write_placement == "pair":
                 # three quiet cores of one L3 domain: the uploader (this
                 # thread) on one, the endpoint's receive and CRC threads on
-                # the other two (profiles/r3_write/placement)
+                # the other two (profiles/r3_write/placement).  Each of the
+                # two on a physical core of its own: left to the scheduler
+                # over both cores' four hardware threads, the receive thread
+                # -- the upload's bound -- often shared its core with the CRC
+                # worker, and its cost per GiB swung 0.040 - 0.057 between
+                # runs while the raw probe's receiver stayed at 0.037 (r6_t)
                 pl = self.affinity.plan(gpu, "pair", self.slot)
-                sh = {"client": pl["client"], "server": sorted(pl["server"] + pl.get("aux", []))}
+                own = getattr(args, "write_crc_core", "own") == "own" and pl.get("aux")
+                sh = {"client": pl["client"],
+                      "server": pl["server"] if own else sorted(pl["server"] + pl.get("aux", []))}
                 ep = n.Server({"port": 0, "md5": False, "cpus": sh["server"], "send_cpus": sh.get("send_cpus"),
-                               "retain_uploads": False,
+                               "crc_cpus": pl["aux"] if own else None, "retain_uploads": False,
                                "write_verify": getattr(args, "write_verify", "on") == "on"})
                 ep.start()
             else:
@@ -286,21 +293,33 @@ class SideBlocks:
                      if v > 0.0005 and nbytes}
         # the upload's own bound, outside the timed region: ONE loopback TCP
         # stream in the upload's direction and placement -- the uploader's
-        # core sending pages by reference (as the transport splices the
-        # staging ring), the endpoint's cores receiving into a 2 x 2 MiB THP
-        # buffer (as its WriteObject receive does); best of 3 probes
+        # core sending the upload's own staging pages by reference (a
+        # GpuByteSource: this HBM buffer copied D2H into pinned slots, as the
+        # transport splices them), the endpoint's cores receiving into a
+        # 2 x 2 MiB THP buffer (as its WriteObject receive does); best of 3
+        # probes.  The same probe sending the endpoint's THP object (pages no
+        # DMA engine wrote) is reported beside it.
         up_tcp = 0.0
         up_probe = {}
         if not err and parts == 1 and sh.get("client") and sh.get("server"):
             try:
-                runs = [n.loopback_ceiling({"mode": "tcp", "object_bytes": wsize, "reads": max(3, min(8, steps)),
-                                            "ring_bytes": 4 << 20, "recv_cpus": sh["server"],
-                                            "send_cpus": sh["client"], "ring_pages": 1}) for _ in range(3)]
+                base = {"mode": "tcp", "object_bytes": wsize, "reads": max(3, min(8, steps)),
+                        "ring_bytes": 4 << 20, "recv_cpus": sh["server"], "send_cpus": sh["client"], "ring_pages": 1}
+                staged = {**base, "gpu_source_ptr": buf.data_ptr(), "gpu_source_device": gpu,
+                          "gpu_source_slot_bytes": wslot, "gpu_source_slots": args.slots}
+                runs, thp = [], []
+                for _ in range(3):
+                    runs.append(n.loopback_ceiling(staged))
+                    thp.append(n.loopback_ceiling(base))
                 best = max(runs, key=lambda r: r["gbps"])
+                bthp = max(thp, key=lambda r: r["gbps"])
                 up_tcp = best["gbps"] * 1e9 / (1 << 20)
                 # the probe's receiver against the endpoint's gcsb-srv-conn
-                up_probe = {"recv_cpu_s_per_gib": round(best["recv_cpu_s_per_gib"], 4),
-                            "send_cpu_s_per_gib": round(best["send_cpu_s_per_gib"], 4)}
+                up_probe = {"source": "gpu_staged",
+                            "recv_cpu_s_per_gib": round(best["recv_cpu_s_per_gib"], 4),
+                            "send_cpu_s_per_gib": round(best["send_cpu_s_per_gib"], 4),
+                            "thp_source_mib_s": round(bthp["gbps"] * 1e9 / (1 << 20), 1),
+                            "thp_recv_cpu_s_per_gib": round(bthp["recv_cpu_s_per_gib"], 4)}
             except Exception as e:  # noqa: BLE001 - the probe is a side measurement
                 cpu_split["upload_probe_error"] = str(e)[:160]
         s = sorted(lat)

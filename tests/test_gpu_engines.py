@@ -84,6 +84,23 @@ def test_spliced_upload_from_hbm_is_byte_exact(native, server, gpu_available, si
         srv.stop()
 
 
+def test_upload_ceiling_sends_gpu_staged_pages(native, gpu_available):
+    """The write block's bound: the probe's sender sends a GpuByteSource's
+    staging pages (HBM copied D2H into pinned slots) by reference, one
+    object per read, and releases them only after the receiver has them."""
+    import torch
+
+    size = 64 << 20
+    t = torch.empty(size, dtype=torch.uint8, device="cuda:0")
+    native.gpu_fill_pattern(0, t.data_ptr(), size, "ceil/src", 0)
+    base = {"mode": "tcp", "object_bytes": size, "reads": 4, "ring_bytes": 4 << 20}
+    staged = native.loopback_ceiling({**base, "gpu_source_ptr": t.data_ptr(), "gpu_source_device": 0,
+                                      "gpu_source_slot_bytes": 2 << 20, "gpu_source_slots": 4})
+    thp = native.loopback_ceiling(base)
+    assert staged["gbps"] > 1.0 and thp["gbps"] > 1.0, (staged, thp)
+    assert staged["recv_cpu_s_per_gib"] > 0 and staged["send_cpu_s_per_gib"] > 0, staged
+
+
 @pytest.mark.parametrize("poll_us", [0, 10])
 def test_end_of_read_wait_modes(native, server, gpu_available, poll_us):
     """Both slot-event waits land and verify every byte: the runtime's

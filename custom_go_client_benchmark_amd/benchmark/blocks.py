@@ -465,7 +465,9 @@ class SideBlocks:
         over = {"protocol": proto, "endpoint": ep.url if ep is not None else "", "workers": workers,
                 "object_names": names or [f"c3_rank{rank}/file_0"], "cpus": sh["client"], "worker_id_offset": 0,
                 "rcvbuf": parse_size(args.list_rcvbuf), "ring_slots": int(lslots), "ring_slot_bytes": parse_size(lbytes),
-                "ring_wc": args.list_ring_wc == "on", "reader_cpus": sh.get("reader_cpus")}
+                "ring_wc": args.list_ring_wc == "on", "reader_cpus": sh.get("reader_cpus"),
+                "async_submit": bool(getattr(args, "list_async_submit", 1)),
+                "wait_poll_us": int(getattr(args, "list_wait_poll_us", 10))}
         if extra:
             over.update(extra)
         st = self.read_block(over, per_pass, per_pass * warmup_passes, f"{proto} list-read", endpoint=ep)

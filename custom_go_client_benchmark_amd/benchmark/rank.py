@@ -64,6 +64,9 @@ FIXED = {
     "list_placement": "same",     # config 3: readers and endpoint in one L3 domain (r2_check_s4b)
     "list_ring_wc": "on",         # config 3: write-combined rings (r3_ring_thp/wc)
     "list_rcvbuf": "64MiB",
+    "list_async_submit": 0,       # config 3: each reader issues its own copy + CRC launch; the shared
+                                  # submitter thread, ~2/3 busy, queued the 8 readers' hand-offs (r6_w)
+    "list_wait_poll_us": 10,      # config 3: end-of-read event poll period (0: hipEventSynchronize; 5 ~ 10, r6_w)
     "ceiling": "on",              # the ceiling block (--blocks selects it away)
     "ref_grpc_placement": "same",        # 48 workers on one connection in one L3 domain (r3_mux_thp/refplace)
     "ref_http_placement": "share_quota",  # 48 HTTP receivers over the quota's cores

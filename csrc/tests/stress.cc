@@ -7,6 +7,7 @@
 #include <execinfo.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -16,6 +17,7 @@
 #include <thread>
 #include <vector>
 
+#include "core/ceiling.h"
 #include "core/content.h"
 #include "core/crc32c.h"
 #include "server/fakegcs.h"
@@ -255,6 +257,43 @@ int main(int argc, char** argv) {
     }
   }
   srv.stop();
+  // 7) the ceiling probe's sender and receiver threads: the THP-object
+  //    sender, and an external source staged per read (as the upload bound's
+  //    GpuByteSource, here a host copy into two slots) whose pages must stay
+  //    put until the receiver has every byte
+  {
+    CeilingConfig cc;
+    cc.object_bytes = 6u << 20;
+    cc.reads = 3;
+    cc.ring_bytes = 2u << 20;
+    cc.recv_chunk = 256u << 10;
+    CeilingResult r = tcp_ceiling(cc);
+    check(r.gbps > 0, "ceiling probe (THP source)");
+    struct Staged : CeilingSource {
+      std::vector<uint8_t> obj, stage;
+      size_t pos = 0;
+      int begins = 0, ends = 0;
+      void begin() override {
+        ++begins;
+        stage.assign(obj.begin(), obj.end());  // "D2H": a fresh copy per read
+        pos = 0;
+      }
+      std::pair<const uint8_t*, size_t> next(size_t max) override {
+        const size_t k = std::min(max, stage.size() - pos);
+        pos += k;
+        return {stage.data() + pos - k, k};
+      }
+      void end() override {
+        ++ends;
+        stage.assign(stage.size(), 0);  // reused at once: the receiver must have had every byte
+      }
+    } src;
+    src.obj.resize(cc.object_bytes);
+    for (size_t i = 0; i < src.obj.size(); ++i) src.obj[i] = static_cast<uint8_t>(i * 7 + 1);
+    cc.source = &src;
+    r = tcp_ceiling(cc);
+    check(r.gbps > 0 && src.begins == cc.reads && src.ends == cc.reads, "ceiling probe (staged source)");
+  }
   if (g_fail) {
     std::fprintf(stderr, "stress: %d failures\n", g_fail.load());
     return 1;

@@ -242,6 +242,11 @@ class SideBlocks:
                                "crc_cpus": pl["aux"] if own else None, "retain_uploads": False,
                                "write_verify": getattr(args, "write_verify", "on") == "on"})
                 ep.start()
+            elif parts > 1 and self.use_gpu and getattr(args, "write_composite_placement", "share") != "share":
+                sh = self.affinity.plan(gpu, args.write_composite_placement, self.slot)
+                ep = n.Server({"port": 0, "md5": False, "cpus": sh["server"], "retain_uploads": False,
+                               "write_verify": getattr(args, "write_verify", "on") == "on"})
+                ep.start()
             else:
                 ep, sh = self.share_endpoint()
             # the upload runs on this (Python main) thread: keep it, its

@@ -79,8 +79,10 @@ FIXED = {
     "write_async_stage": "on",    # config 5: staging past the first slots issued on the submitter (r6_f, r6_g)
     "write_verify": "on",         # config 5: the endpoint CRC-checks every message (off: attribution A/B only)
     "write_slot_bytes": "2MiB",   # config 5: upload staging slot = one 2 MiB WriteObject message (r6_j)
+    "write_composite_placement": "split",  # the 8-part upload: writers and endpoint on two L3 domains
+                                           # (median 31.2k against 23.0k MiB/s spread over the share, r6_ad)
     "write_crc_core": "own",      # config 5: the endpoint's receive thread and its CRC worker pinned to
-                                  # different physical cores ("shared": both over both, r6_t)
+                                  # different physical cores ("shared": both over both, r6_u)
 }
 
 

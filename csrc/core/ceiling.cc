@@ -189,6 +189,13 @@ CeilingResult tcp_ceiling(const CeilingConfig& c) {
       if (!c.zerocopy_send) copybuf.resize(2u << 20);
       Fd sp[2];
       const double c0 = thread_cpu_s();
+      double idle_cpu = 0;  // spent spinning for the receiver: not the sender's per-byte cost
+      auto wait_for = [&](const std::atomic<int>& a, int past) {
+        if (a.load() > past || quit.load()) return;
+        const double w0 = thread_cpu_s();
+        while (a.load() <= past && !quit.load()) std::this_thread::yield();
+        idle_cpu += thread_cpu_s() - w0;
+      };
       auto splice_pages = [&](const uint8_t* p, size_t k) {
         if (sp[0].fd < 0) {
           int q[2];
@@ -211,7 +218,7 @@ CeilingResult tcp_ceiling(const CeilingConfig& c) {
         }
       };
       for (int r = 0; r < c.reads; ++r) {
-        while (go.load() <= r && !quit.load()) std::this_thread::yield();
+        wait_for(go, r);
         if (quit.load()) break;
         if (ext) {
           // one upload's worth: the source stages the object, the pages go
@@ -224,7 +231,7 @@ CeilingResult tcp_ceiling(const CeilingConfig& c) {
             splice_pages(p, k);
             off += k;
           }
-          while (received.load() <= r && !quit.load()) std::this_thread::yield();
+          wait_for(received, r);
           ext->end();
           continue;
         }
@@ -249,7 +256,7 @@ CeilingResult tcp_ceiling(const CeilingConfig& c) {
           }
         }
       }
-      send_cpu_total = thread_cpu_s() - c0;
+      send_cpu_total = thread_cpu_s() - c0 - idle_cpu;
     } catch (...) {
       send_err = std::current_exception();
       quit.store(true);

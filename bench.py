@@ -25,7 +25,7 @@ HTTP/2 framing: the reference's grpc-go client advertises no
 SETTINGS_MAX_FRAME_SIZE, so its peer sends 16 KiB DATA frames, and its windows
 stop at 16 MiB (/root/reference/go.mod:20, main.go:106-117).  The headline
 runs 16 MiB frames (--h2-framing large, one frame per 2 MiB message, as in
-rounds 2-5); the ref_framing side block runs the headline config at the
+rounds 2-5) with the reference's 16 MiB windows; the ref_framing side block runs the headline config at the
 reference's settings, paired chunk by chunk with its reference-semantics
 baseline at the same settings, and so do list_read_grpc_ref and
 ref_default_grpc_ref.  The client receives many 16 KiB frames per recvmsg()
@@ -150,7 +150,7 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--h2-framing", default="large", choices=["ref", "large"],
                     help="HTTP/2 receive settings of the gRPC clients: ref = the reference's grpc-go (no "
                          "SETTINGS_MAX_FRAME_SIZE advertised -> 16 KiB DATA frames, 16 MiB stream/connection "
-                         "windows); large = 16 MiB frames and 2 GiB windows (one frame per 2 MiB message).  The "
+                         "windows); large = 16 MiB frames and 16 MiB windows (one frame per 2 MiB message).  The "
                          "headline keeps large: at 16 KiB frames the synthetic endpoint's one send thread per "
                          "connection is the bound (~12 GB/s copying frame trains, README), so a ref headline would "
                          "measure the endpoint; the ref_framing block pairs the headline config at 16 KiB frames "

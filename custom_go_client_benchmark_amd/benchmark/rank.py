@@ -793,6 +793,8 @@ class RankBench(SideBlocks):
             out["headline_frac_of_ceiling"] = uc["headline_frac_of_ceiling"]
             diag["ceiling"] = uc
         out["h2_frames"] = FRAME_LABEL[self.framing_name] if self.protocol == "grpc" else None
+        # the HTTP/2 windows the client advertised (MiB): the reference's 16
+        out["h2_window_mib"] = (self.framing["h2_window"] >> 20) if self.protocol == "grpc" else None
         if args.workload == "read":
             out["ttfb_p50_ms"] = round(head["ttfb_p50_max"], 3)
             out["host_landed_p50_ms"] = round(head["host_p50_max"], 3)

@@ -204,6 +204,7 @@ def test_bench_line_fits_the_driver_tail(gpus, tmp_path):
     # the headline config at the other framing, paired with its baseline
     assert line["ref_framing"]["ok"] and line["ref_framing"]["h2_frames"] == "16KiB"
     assert line["ref_framing"]["vs_baseline_paired"] > 0 and line["h2_frames"] == "16MiB"
+    assert line["h2_window_mib"] == 16  # the reference's window at both framings
     assert line["list_read_grpc_ref"]["ok"] and line["ref_default_grpc_ref"]["h2_frames"] == "16KiB"
     # one ceiling: no block beats its bound
     for k, b in line.items():
